@@ -1,0 +1,98 @@
+"""Single-GPU micro-benchmark of the worker training step.
+
+Compares (a) the psx HIP engine (eager launches), (b) the same step replayed from a HIP graph,
+and (c) a PyTorch-ROCm reference step (channels_last, bf16 autocast, MIOpen convs, autograd,
+SGD) on the same ResNet-18 / batch — the library baseline our kernels must beat.
+
+    python bench/engine_step.py --batch 128 --iters 50
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+import psx  # noqa: E402,F401
+from psx.models.engine import HipResNetEngine  # noqa: E402
+from psx.models.layout import ParamLayout  # noqa: E402
+from psx.models.resnet import ResNet18  # noqa: E402
+from psx.ops import kernels as K  # noqa: E402
+
+
+def timeit(fn, iters, warm=5):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--no-torch", action="store_true")
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    B = a.batch
+    torch.manual_seed(0)
+    model = ResNet18(100)
+    layout = ParamLayout.from_module(model)
+    arena, _ = layout.pack(model)
+    arena = arena.cuda()
+    eng = HipResNetEngine(model, layout, B)
+    n = 50000
+    imgs = torch.empty(n, 32, 32, 3, dtype=torch.uint8, device="cuda")
+    labs = torch.empty(n, dtype=torch.int32, device="cuda")
+    K.synth_gen(imgs, labs, n, 32, 32, 100, 1)
+    eng.index.copy_(torch.randperm(n, device="cuda")[:B].to(torch.int32))
+    res = {"batch": B}
+
+    def step():
+        eng.train_step(arena, imgs, labs)
+        K.sgd_apply(arena, eng.grads, 0.0, n=layout.param_numel)  # lr 0: keep weights fixed
+
+    if a.only in ("", "eager"):
+        t = timeit(step, a.iters)
+        res["hip_eager_ms"] = t * 1e3
+        res["hip_eager_img_s"] = B / t
+    if a.only in ("", "graph"):
+        eng.capture(arena, imgs, labs)
+
+        def gstep():
+            eng.step_graph()
+            K.sgd_apply(arena, eng.grads, 0.0, n=layout.param_numel)
+
+        t = timeit(gstep, a.iters)
+        res["hip_graph_ms"] = t * 1e3
+        res["hip_graph_img_s"] = B / t
+    if not a.no_torch and a.only in ("", "torch"):
+        m = ResNet18(100).cuda().to(memory_format=torch.channels_last)
+        opt = torch.optim.SGD(m.parameters(), lr=0.1)
+        x = torch.randn(B, 3, 32, 32, device="cuda").to(memory_format=torch.channels_last)
+        y = torch.randint(0, 100, (B,), device="cuda")
+
+        def tstep():
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = F.cross_entropy(m(x), y)
+            loss.backward()
+            opt.step()
+
+        t = timeit(tstep, a.iters)
+        res["torch_bf16_ms"] = t * 1e3
+        res["torch_bf16_img_s"] = B / t
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

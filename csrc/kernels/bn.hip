@@ -1,0 +1,364 @@
+// Training-mode BatchNorm2d (+ReLU, +residual) on NHWC bf16 activations.
+//
+// Replaces nn.BatchNorm2d / torch.relu / `out += shortcut` of the reference BasicBlock
+// (reference: src/parameter_server/server.py:21-41, identical copies in worker.py:20-76).
+// Semantics follow torch: batch statistics over (N,H,W), biased variance for normalisation,
+// running_var updated with the unbiased variance, momentum 0.1, eps 1e-5.
+//
+// Forward statistics come from the conv epilogue as per-tile partial (sum, sumsq) slabs
+// ([T][2][C]); bn_finalize reduces them (fp64, fixed order => deterministic), produces the
+// per-channel affine (scale, shift) and updates the running stats. Every elementwise pass is
+// vectorised at 16 B per lane (8 channels).
+#include "common.hpp"
+
+namespace psx {
+
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ part, int T, int C, float count,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps, float momentum,
+                                                          float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                          float* __restrict__ scale, float* __restrict__ shift,
+                                                          float* __restrict__ save_mean,
+                                                          float* __restrict__ save_invstd) {
+  __shared__ double red[2][4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lane4 = threadIdx.x >> 6;
+  double s = 0.0, ss = 0.0;
+  if (c < C) {
+    for (int t = lane4; t < T; t += 4) {
+      s += part[((size_t)t * 2 + 0) * C + c];
+      ss += part[((size_t)t * 2 + 1) * C + c];
+    }
+  }
+  red[0][lane4][threadIdx.x & 63] = s;
+  red[1][lane4][threadIdx.x & 63] = ss;
+  __syncthreads();
+  if (lane4 == 0 && c < C) {
+    s = red[0][0][threadIdx.x] + red[0][1][threadIdx.x] + red[0][2][threadIdx.x] + red[0][3][threadIdx.x];
+    ss = red[1][0][threadIdx.x] + red[1][1][threadIdx.x] + red[1][2][threadIdx.x] + red[1][3][threadIdx.x];
+    const double mean = s / count;
+    double var = ss / count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = gamma[c] * invstd;
+    scale[c] = sc;
+    shift[c] = beta[c] - (float)mean * sc;
+    save_mean[c] = (float)mean;
+    save_invstd[c] = invstd;
+    if (run_mean) {
+      const double unb = count > 1.f ? var * count / (count - 1.0) : var;
+      run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+      run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+    }
+  }
+}
+
+// Eval-mode affine from running statistics.
+__global__ void bn_eval_affine_kernel(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
+                                      float eps, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) {
+    const float sc = gamma[c] * rsqrtf(rv[c] + eps);
+    scale[c] = sc;
+    shift[c] = beta[c] - rm[c] * sc;
+  }
+}
+
+// out = act( y*scale + shift  [+ res]  [+ res2*scale2 + shift2] )
+// MODE 0: no residual, 1: identity residual, 2: BN'd residual.
+template <int MODE, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const uint16_t* __restrict__ res,
+                                                       const float* __restrict__ scale2,
+                                                       const float* __restrict__ shift2, uint16_t* __restrict__ out,
+                                                       size_t nvec, int C) {
+  const int cvec = C >> 3;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cvec) << 3;
+    const u32x4 v = reinterpret_cast<const u32x4*>(y)[i];
+    u32x4 rv = {0u, 0u, 0u, 0u};
+    if (MODE != 0) rv = reinterpret_cast<const u32x4*>(res)[i];
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + 2 * j;
+      float a0 = lo_bf(v[j]) * scale[c] + shift[c];
+      float a1 = hi_bf(v[j]) * scale[c + 1] + shift[c + 1];
+      if (MODE == 1) {
+        a0 += lo_bf(rv[j]);
+        a1 += hi_bf(rv[j]);
+      } else if (MODE == 2) {
+        a0 += lo_bf(rv[j]) * scale2[c] + shift2[c];
+        a1 += hi_bf(rv[j]) * scale2[c + 1] + shift2[c + 1];
+      }
+      if (RELU) {
+        a0 = fmaxf(a0, 0.f);
+        a1 = fmaxf(a1, 0.f);
+      }
+      o[j] = pack_bf2(a0, a1);
+    }
+    reinterpret_cast<u32x4*>(out)[i] = o;
+  }
+}
+
+// Backward pass 1: per-channel partials of sum(dz), sum(dz*xhat1) [, sum(dz*xhat2)], with
+// dz = g * (o > 0) (ReLU mask from the stored activation) or dz = g.
+// part layout: [gridDim.x][NS][C], NS = 2 or 3.
+template <bool MASK, bool TWO>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g,
+                                                            const uint16_t* __restrict__ o,
+                                                            const uint16_t* __restrict__ y1,
+                                                            const float* __restrict__ mean1,
+                                                            const float* __restrict__ invstd1,
+                                                            const uint16_t* __restrict__ y2,
+                                                            const float* __restrict__ mean2,
+                                                            const float* __restrict__ invstd2, float* __restrict__ part,
+                                                            int npix, int C, int pix_per_block) {
+  constexpr int NS = TWO ? 3 : 2;
+  extern __shared__ __attribute__((aligned(16))) float sred[];  // [256][NS*8]
+  const int cvec = C >> 3;
+  const int tpp = 256 / cvec;  // threads per pixel row set (pixels processed per iteration)
+  const int cg = threadIdx.x % cvec, pr = threadIdx.x / cvec;
+  const int c0 = cg * 8;
+  float m1[8], i1[8], m2[8], i2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m1[j] = mean1[c0 + j];
+    i1[j] = invstd1[c0 + j];
+    if (TWO) {
+      m2[j] = mean2[c0 + j];
+      i2[j] = invstd2[c0 + j];
+    }
+  }
+  float sdz[8], sx1[8], sx2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sdz[j] = sx1[j] = sx2[j] = 0.f;
+  const int pbeg = blockIdx.x * pix_per_block;
+  const int pend = min(npix, pbeg + pix_per_block);
+  for (int p = pbeg + pr; p < pend; p += tpp) {
+    const size_t vi = (size_t)p * cvec + cg;
+    const u32x4 gv = reinterpret_cast<const u32x4*>(g)[vi];
+    u32x4 ov = {0u, 0u, 0u, 0u};
+    if (MASK) ov = reinterpret_cast<const u32x4*>(o)[vi];
+    const u32x4 yv = reinterpret_cast<const u32x4*>(y1)[vi];
+    u32x4 y2v = {0u, 0u, 0u, 0u};
+    if (TWO) y2v = reinterpret_cast<const u32x4*>(y2)[vi];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float d0 = lo_bf(gv[j]), d1 = hi_bf(gv[j]);
+      if (MASK) {
+        if (!(lo_bf(ov[j]) > 0.f)) d0 = 0.f;
+        if (!(hi_bf(ov[j]) > 0.f)) d1 = 0.f;
+      }
+      sdz[2 * j] += d0;
+      sdz[2 * j + 1] += d1;
+      sx1[2 * j] += d0 * (lo_bf(yv[j]) - m1[2 * j]) * i1[2 * j];
+      sx1[2 * j + 1] += d1 * (hi_bf(yv[j]) - m1[2 * j + 1]) * i1[2 * j + 1];
+      if (TWO) {
+        sx2[2 * j] += d0 * (lo_bf(y2v[j]) - m2[2 * j]) * i2[2 * j];
+        sx2[2 * j + 1] += d1 * (hi_bf(y2v[j]) - m2[2 * j + 1]) * i2[2 * j + 1];
+      }
+    }
+  }
+  float* mine = sred + threadIdx.x * (NS * 8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mine[j] = sdz[j];
+    mine[8 + j] = sx1[j];
+    if (TWO) mine[16 + j] = sx2[j];
+  }
+  __syncthreads();
+  // reduce over pr (threads with the same cg): thread t < cvec*NS*8 sums one (cg, stat, j)
+  for (int t = threadIdx.x; t < cvec * NS * 8; t += 256) {
+    const int cgi = t / (NS * 8), sj = t - cgi * (NS * 8);
+    float acc = 0.f;
+    for (int q = 0; q < tpp; ++q) acc += sred[(q * cvec + cgi) * (NS * 8) + sj];
+    const int stat = sj >> 3, j = sj & 7;
+    part[((size_t)blockIdx.x * NS + stat) * C + cgi * 8 + j] = acc;
+  }
+}
+
+// Backward finalize: dgamma = sum(dz*xhat), dbeta = sum(dz); dx = k1*dz + k2*y + k3.
+// Writes dgamma/dbeta (scaled) into the gradient sink (fp16 wire codec or fp32).
+template <typename GT>
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int T, int NS, int which, int C, float count,
+                                       const float* __restrict__ gamma, const float* __restrict__ mean,
+                                       const float* __restrict__ invstd, float* __restrict__ coef,
+                                       GT* __restrict__ dgamma, GT* __restrict__ dbeta, float gscale) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sdz = 0.0, sxh = 0.0;
+  for (int t = 0; t < T; ++t) {
+    sdz += part[((size_t)t * NS + 0) * C + c];
+    sxh += part[((size_t)t * NS + which) * C + c];
+  }
+  const float mdz = (float)(sdz / count), mxh = (float)(sxh / count);
+  const float is = invstd[c], gm = gamma[c];
+  const float k1 = gm * is;
+  const float k2 = -gm * is * is * mxh;
+  const float k3 = -gm * is * mdz + gm * is * is * mean[c] * mxh;
+  coef[c] = k1;
+  coef[C + c] = k2;
+  coef[2 * C + c] = k3;
+  const float dg = (float)sxh * gscale, db = (float)sdz * gscale;
+  if constexpr (sizeof(GT) == 2) {
+    dgamma[c] = __builtin_bit_cast(uint16_t, (_Float16)dg);
+    dbeta[c] = __builtin_bit_cast(uint16_t, (_Float16)db);
+  } else {
+    dgamma[c] = dg;
+    dbeta[c] = db;
+  }
+}
+
+// dx1 = k1*dz + k2*y1 + k3 [, dx2 = k1'*dz + k2'*y2 + k3'] [, dzout = dz]
+template <bool MASK, bool TWO, bool DZOUT>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __restrict__ g,
+                                                           const uint16_t* __restrict__ o,
+                                                           const uint16_t* __restrict__ y1,
+                                                           const float* __restrict__ coef1,
+                                                           uint16_t* __restrict__ dx1,
+                                                           const uint16_t* __restrict__ y2,
+                                                           const float* __restrict__ coef2,
+                                                           uint16_t* __restrict__ dx2, uint16_t* __restrict__ dzout,
+                                                           size_t nvec, int C) {
+  const int cvec = C >> 3;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cvec) << 3;
+    const u32x4 gv = reinterpret_cast<const u32x4*>(g)[i];
+    u32x4 ov = {0u, 0u, 0u, 0u};
+    if (MASK) ov = reinterpret_cast<const u32x4*>(o)[i];
+    const u32x4 yv = reinterpret_cast<const u32x4*>(y1)[i];
+    u32x4 y2v = {0u, 0u, 0u, 0u};
+    if (TWO) y2v = reinterpret_cast<const u32x4*>(y2)[i];
+    u32x4 r1, r2, rz;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + 2 * j;
+      float d0 = lo_bf(gv[j]), d1 = hi_bf(gv[j]);
+      if (MASK) {
+        if (!(lo_bf(ov[j]) > 0.f)) d0 = 0.f;
+        if (!(hi_bf(ov[j]) > 0.f)) d1 = 0.f;
+      }
+      r1[j] = pack_bf2(coef1[c] * d0 + coef1[C + c] * lo_bf(yv[j]) + coef1[2 * C + c],
+                       coef1[c + 1] * d1 + coef1[C + c + 1] * hi_bf(yv[j]) + coef1[2 * C + c + 1]);
+      if (TWO)
+        r2[j] = pack_bf2(coef2[c] * d0 + coef2[C + c] * lo_bf(y2v[j]) + coef2[2 * C + c],
+                         coef2[c + 1] * d1 + coef2[C + c + 1] * hi_bf(y2v[j]) + coef2[2 * C + c + 1]);
+      if (DZOUT) rz[j] = pack_bf2(d0, d1);
+    }
+    reinterpret_cast<u32x4*>(dx1)[i] = r1;
+    if (TWO) reinterpret_cast<u32x4*>(dx2)[i] = r2;
+    if (DZOUT) reinterpret_cast<u32x4*>(dzout)[i] = rz;
+  }
+}
+
+}  // namespace psx
+
+using namespace psx;
+
+static int ew_grid(size_t nvec) {
+  size_t g = (nvec + 255) / 256;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+extern "C" {
+
+int psx_bn_finalize(const float* part, int T, int C, float count, const float* gamma, const float* beta, float eps,
+                    float momentum, float* run_mean, float* run_var, float* scale, float* shift, float* save_mean,
+                    float* save_invstd, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, part, T, C, count, gamma, beta, eps,
+                     momentum, run_mean, run_var, scale, shift, save_mean, save_invstd);
+  return (int)hipGetLastError();
+}
+
+int psx_bn_eval_affine(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
+                       float* scale, float* shift, hipStream_t st) {
+  hipLaunchKernelGGL(bn_eval_affine_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma, beta, rm, rv, eps,
+                     scale, shift);
+  return (int)hipGetLastError();
+}
+
+// mode: 0 plain, 1 +identity residual, 2 +BN'd residual
+int psx_bn_apply(const void* y, const float* scale, const float* shift, const void* res, const float* scale2,
+                 const float* shift2, void* out, long nelem, int C, int mode, int relu, hipStream_t st) {
+  if (C % 8 || nelem % 8) return -2;
+  const size_t nvec = (size_t)nelem / 8;
+  const int grid = ew_grid(nvec);
+#define PSX_BNA(M, R)                                                                                         \
+  hipLaunchKernelGGL((bn_apply_kernel<M, R>), dim3(grid), dim3(256), 0, st, (const uint16_t*)y, scale, shift, \
+                     (const uint16_t*)res, scale2, shift2, (uint16_t*)out, nvec, C)
+  if (mode == 0 && relu) PSX_BNA(0, true);
+  else if (mode == 0) PSX_BNA(0, false);
+  else if (mode == 1 && relu) PSX_BNA(1, true);
+  else if (mode == 1) PSX_BNA(1, false);
+  else if (mode == 2 && relu) PSX_BNA(2, true);
+  else if (mode == 2) PSX_BNA(2, false);
+  else return -3;
+#undef PSX_BNA
+  return (int)hipGetLastError();
+}
+
+// Returns the number of partial rows T (query with part == nullptr).
+int psx_bn_bwd_reduce(const void* g, const void* o, const void* y1, const float* mean1, const float* invstd1,
+                      const void* y2, const float* mean2, const float* invstd2, float* part, int npix, int C,
+                      hipStream_t st) {
+  if (C % 8 || 256 % (C / 8)) return -2;
+  // ~512 blocks, at least 64 pixels each
+  int ppb = (npix + 511) / 512;
+  if (ppb < 64) ppb = 64;
+  const int T = (npix + ppb - 1) / ppb;
+  if (!part) return T;
+  const bool mask = o != nullptr, two = y2 != nullptr;
+  const size_t lds = 256 * (two ? 3 : 2) * 8 * sizeof(float);
+#define PSX_BBR(M, TW)                                                                                          \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<M, TW>), dim3(T), dim3(256), lds, st, (const uint16_t*)g,           \
+                     (const uint16_t*)o, (const uint16_t*)y1, mean1, invstd1, (const uint16_t*)y2, mean2, invstd2, \
+                     part, npix, C, ppb)
+  if (mask && two) PSX_BBR(true, true);
+  else if (mask) PSX_BBR(true, false);
+  else if (two) PSX_BBR(false, true);
+  else PSX_BBR(false, false);
+#undef PSX_BBR
+  const int e = (int)hipGetLastError();
+  return e ? -e : T;
+}
+
+int psx_bn_bwd_finalize(const float* part, int T, int NS, int which, int C, float count, const float* gamma,
+                        const float* mean, const float* invstd, float* coef, void* dgamma, void* dbeta, float gscale,
+                        int grad_fp16, hipStream_t st) {
+  const dim3 grid((C + 255) / 256);
+  if (grad_fp16)
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<uint16_t>, grid, dim3(256), 0, st, part, T, NS, which, C, count, gamma,
+                       mean, invstd, coef, (uint16_t*)dgamma, (uint16_t*)dbeta, gscale);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, grid, dim3(256), 0, st, part, T, NS, which, C, count, gamma,
+                       mean, invstd, coef, (float*)dgamma, (float*)dbeta, gscale);
+  return (int)hipGetLastError();
+}
+
+int psx_bn_bwd_apply(const void* g, const void* o, const void* y1, const float* coef1, void* dx1, const void* y2,
+                     const float* coef2, void* dx2, void* dzout, long nelem, int C, hipStream_t st) {
+  if (C % 8 || nelem % 8) return -2;
+  const size_t nvec = (size_t)nelem / 8;
+  const int grid = ew_grid(nvec);
+  const bool mask = o != nullptr, two = y2 != nullptr, dz = dzout != nullptr;
+#define PSX_BBA(M, TW, DZ)                                                                                        \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<M, TW, DZ>), dim3(grid), dim3(256), 0, st, (const uint16_t*)g,         \
+                     (const uint16_t*)o, (const uint16_t*)y1, coef1, (uint16_t*)dx1, (const uint16_t*)y2, coef2, \
+                     (uint16_t*)dx2, (uint16_t*)dzout, nvec, C)
+  if (mask && two && dz) PSX_BBA(true, true, true);
+  else if (mask && two) PSX_BBA(true, true, false);
+  else if (mask && dz) PSX_BBA(true, false, true);
+  else if (mask) PSX_BBA(true, false, false);
+  else if (two && dz) PSX_BBA(false, true, true);
+  else if (two) PSX_BBA(false, true, false);
+  else if (dz) PSX_BBA(false, false, true);
+  else PSX_BBA(false, false, false);
+#undef PSX_BBA
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

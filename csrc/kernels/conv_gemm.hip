@@ -1,0 +1,550 @@
+// Implicit-GEMM convolution on CDNA4 MFMA (v_mfma_f32_16x16x32_bf16), NHWC bf16.
+//
+// Replaces the nn.Conv2d forward/backward of the reference ResNet-18
+// (reference: src/parameter_server/server.py:24,26,32,48 and the autograd of
+// src/workers/worker.py:345) with three hand-written kernels:
+//
+//   conv_fwd   : Y[pix][oc]   = sum_k im2col(X)[pix][k] * Wf[oc][k]        k = (r,s,c)
+//   conv_dgrad : dX[pix][c]   = sum_k im2col'(dY)[pix][k] * Wd[c][k]       k = (r,s,oc)
+//   conv_wgrad : dW[oc][k]    = sum_pix dY[pix][oc] * im2col(X)[pix][k]    (split-K over pix)
+//
+// fwd and dgrad share one kernel body (both GEMM operands K-contiguous, LDS tiles read with
+// ds_read_b128); wgrad reduces over the pixel dimension, which is the strided dimension of
+// both operands, so its LDS tiles are pixel-major and its MFMA fragments are fetched with the
+// gfx950 transposing LDS read ds_read_b64_tr_b16.
+//
+// MFMA orientation: A = weights (rows = output channels), B = im2col pixels, so the
+// accumulator of one lane holds 4 consecutive output channels of one pixel -> each lane
+// stores 8 contiguous bytes of the NHWC output.
+#include "common.hpp"
+
+namespace psx {
+
+struct ConvArgs {
+  const uint16_t* in;   // gathered activation, NHWC [Nb][IH][IW][IC]
+  const uint16_t* w;    // weights [OC][Kg]  (bf16, K-contiguous, zero padded to Kg)
+  uint16_t* out;        // NHWC [Nb][OH][OW][OC]
+  const uint16_t* res;  // optional residual added in the epilogue (same shape as out)
+  float* stats;         // optional BN partials [gridPix][2][OC]
+  int Nb, IH, IW, IC;   // IC: power of two, multiple of 8
+  int OH, OW, OC;
+  int R, S, pad, stride;
+  int Kg;               // padded GEMM-K (multiple of 64)
+  int log2_icc;         // log2(IC / 8)
+  int npix;             // Nb*OH*OW
+  int n_oc_tiles, n_pix_tiles;
+};
+
+// LDS byte offset of 16-byte chunk c (0..7) of row r in a K-major tile with 128-byte rows.
+// Conflict-free for the ds_read_b128 fragment reads below (lane groups of MI355X_MICROARCH §LDS).
+PSX_DEV int kmaj_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+template <int MODE>  // 0 = forward conv gather, 1 = data-grad gather (stride 1), 2 = dgrad stride 2
+PSX_DEV u32x4 gather_chunk(const ConvArgs& a, int nbase, int hb, int wb, bool pvalid, int gk) {
+  u32x4 v = {0u, 0u, 0u, 0u};
+  const int tap = gk >> a.log2_icc;
+  const int c0 = (gk & ((1 << a.log2_icc) - 1)) << 3;
+  if (!pvalid || tap >= a.R * a.S) return v;
+  const int r = tap / a.S;
+  const int s = tap - r * a.S;
+  int ih, iw;
+  if (MODE == 0) {
+    ih = hb + r;
+    iw = wb + s;
+  } else {
+    const int th = hb - r, tw = wb - s;
+    if (MODE == 2) {
+      if ((th | tw) & 1) return v;
+      ih = th >> 1;
+      iw = tw >> 1;
+    } else {
+      ih = th;
+      iw = tw;
+    }
+  }
+  if ((unsigned)ih >= (unsigned)a.IH || (unsigned)iw >= (unsigned)a.IW) return v;
+  const uint16_t* p = a.in + ((size_t)(nbase + ih * a.IW + iw) * a.IC + c0);
+  return *reinterpret_cast<const u32x4*>(p);
+}
+
+// BM: output-channel tile (MFMA rows); BN: pixel tile (MFMA cols). 4 waves in 2x2.
+template <int BM, int BN, int MODE, bool HAS_RES>
+__global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
+  constexpr int BK = 64;
+  constexpr int MT = BM / 32, NT = BN / 32;      // 16x16 MFMA tiles per wave
+  constexpr int LA = BM / 32, LB = BN / 32;      // 16-byte chunks per thread per k-step
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* sA = smem;                       // [2][BM][128B]
+  unsigned char* sB = smem + 2 * BM * 128;        // [2][BN][128B]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nwg = a.n_oc_tiles * a.n_pix_tiles;
+  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int oc_t = tile % a.n_oc_tiles, pix_t = tile / a.n_oc_tiles;
+  const int oc0 = oc_t * BM, pix0 = pix_t * BN;
+
+  const int kc = tid & 7;  // this thread's chunk column in every row it loads
+  // Per-row gather state for the B (pixel) operand.
+  int nbase[LB], hb[LB], wb[LB];
+  bool pv[LB];
+#pragma unroll
+  for (int i = 0; i < LB; ++i) {
+    const int pix = pix0 + (tid >> 3) + 32 * i;
+    pv[i] = pix < a.npix;
+    const int pp = pv[i] ? pix : 0;
+    const int ohw = a.OH * a.OW;
+    const int n = pp / ohw, rem = pp - n * ohw;
+    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+    nbase[i] = n * a.IH * a.IW;
+    if (MODE == 0) {
+      hb[i] = oh * a.stride - a.pad;
+      wb[i] = ow * a.stride - a.pad;
+    } else {
+      hb[i] = oh + a.pad;
+      wb[i] = ow + a.pad;
+    }
+  }
+
+  const uint16_t* wrow = a.w + (size_t)(oc0 + (tid >> 3)) * a.Kg + kc * 8;
+  const int nk = a.Kg / BK;
+
+  u32x4 ra[LA], rb[LB];
+  auto gload = [&](int ks) {
+#pragma unroll
+    for (int i = 0; i < LA; ++i)
+      ra[i] = *reinterpret_cast<const u32x4*>(wrow + (size_t)32 * i * a.Kg + ks * BK);
+#pragma unroll
+    for (int i = 0; i < LB; ++i) rb[i] = gather_chunk<MODE>(a, nbase[i], hb[i], wb[i], pv[i], ks * 8 + kc);
+  };
+  auto lstore = [&](int stage) {
+    unsigned char* A = sA + stage * BM * 128;
+    unsigned char* B = sB + stage * BN * 128;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) *reinterpret_cast<u32x4*>(A + kmaj_off((tid >> 3) + 32 * i, kc)) = ra[i];
+#pragma unroll
+    for (int i = 0; i < LB; ++i) *reinterpret_cast<u32x4*>(B + kmaj_off((tid >> 3) + 32 * i, kc)) = rb[i];
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+
+  const int frow = lane & 15, fchunk = lane >> 4;
+  for (int ks = 0; ks < nk; ++ks) {
+    const int cur = ks & 1;
+    if (ks + 1 < nk) gload(ks + 1);
+    const unsigned char* A = sA + cur * BM * 128;
+    const unsigned char* B = sB + cur * BN * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[MT], fb[NT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        fa[m] = *reinterpret_cast<const bf16x8*>(A + kmaj_off(wm * (BM / 2) + m * 16 + frow, kk * 4 + fchunk));
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+        fb[n] = *reinterpret_cast<const bf16x8*>(B + kmaj_off(wn * (BN / 2) + n * 16 + frow, kk * 4 + fchunk));
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
+    }
+    if (ks + 1 < nk) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: bf16 NHWC store (+residual), optional BN partial statistics ----
+  float s1[MT][4], s2[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s1[m][i] = s2[m][i] = 0.f;
+
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int pix = pix0 + wn * (BN / 2) + n * 16 + (lane & 15);
+    const bool ok = pix < a.npix;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int oc = oc0 + wm * (BM / 2) + m * 16 + 4 * (lane >> 4);
+      float v0 = acc[m][n][0], v1 = acc[m][n][1], v2 = acc[m][n][2], v3 = acc[m][n][3];
+      if (ok) {
+        const size_t off = (size_t)pix * a.OC + oc;
+        if (HAS_RES) {
+          const u32x2 rr = *reinterpret_cast<const u32x2*>(a.res + off);
+          v0 += lo_bf(rr[0]); v1 += hi_bf(rr[0]); v2 += lo_bf(rr[1]); v3 += hi_bf(rr[1]);
+        }
+        u32x2 o;
+        o[0] = pack_bf2(v0, v1);
+        o[1] = pack_bf2(v2, v3);
+        *reinterpret_cast<u32x2*>(a.out + off) = o;
+        if (a.stats) {  // statistics of the stored (bf16-rounded) values
+          const float q0 = lo_bf(o[0]), q1 = hi_bf(o[0]), q2 = lo_bf(o[1]), q3 = hi_bf(o[1]);
+          s1[m][0] += q0; s2[m][0] += q0 * q0;
+          s1[m][1] += q1; s2[m][1] += q1 * q1;
+          s1[m][2] += q2; s2[m][2] += q2 * q2;
+          s1[m][3] += q3; s2[m][3] += q3 * q3;
+        }
+      }
+    }
+  }
+  if (a.stats) {
+    // reduce over the 16 pixel lanes that share (lane>>4)
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s1[m][i] += __shfl_xor(s1[m][i], o, 64);
+          s2[m][i] += __shfl_xor(s2[m][i], o, 64);
+        }
+      }
+    __syncthreads();  // LDS reuse
+    float* red = reinterpret_cast<float*>(smem);  // [2 wn][2][BM]
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = wm * (BM / 2) + m * 16 + 4 * (lane >> 4) + i;
+          red[(wn * 2 + 0) * BM + row] = s1[m][i];
+          red[(wn * 2 + 1) * BM + row] = s2[m][i];
+        }
+    }
+    __syncthreads();
+    for (int j = tid; j < 2 * BM; j += 256) {
+      const int which = j / BM, row = j - which * BM;
+      const float v = red[(0 * 2 + which) * BM + row] + red[(1 * 2 + which) * BM + row];
+      a.stats[((size_t)pix_t * 2 + which) * a.OC + oc0 + row] = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Weight gradient: dW[oc][k] = sum_pix dY[pix][oc] * im2col(X)[pix][k]
+// MFMA rows = k (im2col column), cols = oc. Both LDS tiles are pixel-major [64 pix][64 col]
+// and the K=pixel fragments are read with ds_read_b64_tr_b16.
+// ------------------------------------------------------------------------------------
+struct WgradArgs {
+  const uint16_t* x;   // NHWC [Nb][IH][IW][IC]
+  const uint16_t* dy;  // NHWC [Nb][OH][OW][OC]
+  float* part;         // [splits][OC][Kg] fp32 partial sums
+  int Nb, IH, IW, IC, OH, OW, OC, R, S, pad, stride;
+  int Kg, log2_icc, npix;
+  int n_k_tiles, n_oc_tiles, splits, pix_per_split;  // pix_per_split multiple of 64
+};
+
+// Pixel-major tile, 128-byte rows: swizzle chosen so that the 8 rows one 32-lane half of a
+// ds_read_b64_tr_b16 touches (rows 8a..8a+7) and their 32-byte column pairs are bank-disjoint.
+PSX_DEV int pmaj_off(int r, int c) { return r * 128 + ((c ^ (((r >> 1) & 3) << 1)) << 4); }
+
+PSX_DEV s16x4 tr_read(const unsigned char* base, int byte_off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + byte_off));
+}
+
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
+  constexpr int BR = 64, BC = 64, BKP = 64;  // k rows, oc cols, pixels per step
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* sX = smem;               // [2][64 pix][128B]
+  unsigned char* sD = smem + 2 * 64 * 128;  // [2][64 pix][128B]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntile = a.n_k_tiles * a.n_oc_tiles;
+  const int nwg = ntile * a.splits;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int split = bid / ntile, t = bid - split * ntile;
+  const int oc_t = t % a.n_oc_tiles, k_t = t / a.n_oc_tiles;
+  const int k0 = k_t * BR, oc0 = oc_t * BC;
+  const int pbeg = split * a.pix_per_split;
+  const int pend = min(a.npix, pbeg + a.pix_per_split);
+
+  const int kc = tid & 7;
+  const int prow = tid >> 3;  // rows prow and prow+32
+  const int gk = (k0 >> 3) + kc;
+  const int tap = gk >> a.log2_icc;
+  const int c0 = (gk & ((1 << a.log2_icc) - 1)) << 3;
+  const bool tap_ok = tap < a.R * a.S;
+  const int r = tap_ok ? tap / a.S : 0, s = tap_ok ? tap - r * a.S : 0;
+  const int ohw = a.OH * a.OW;
+
+  u32x4 rx[2], rd[2];
+  auto gload = [&](int p0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int pix = p0 + prow + 32 * i;
+      u32x4 vx = {0u, 0u, 0u, 0u}, vd = {0u, 0u, 0u, 0u};
+      if (pix < pend) {
+        vd = *reinterpret_cast<const u32x4*>(a.dy + (size_t)pix * a.OC + oc0 + kc * 8);
+        if (tap_ok) {
+          const int n = pix / ohw, rem = pix - n * ohw;
+          const int oh = rem / a.OW, ow = rem - oh * a.OW;
+          const int ih = oh * a.stride - a.pad + r, iw = ow * a.stride - a.pad + s;
+          if ((unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW)
+            vx = *reinterpret_cast<const u32x4*>(a.x + ((size_t)(n * a.IH + ih) * a.IW + iw) * a.IC + c0);
+        }
+      }
+      rx[i] = vx;
+      rd[i] = vd;
+    }
+  };
+  auto lstore = [&](int stage) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      *reinterpret_cast<u32x4*>(sX + stage * 8192 + pmaj_off(prow + 32 * i, kc)) = rx[i];
+      *reinterpret_cast<u32x4*>(sD + stage * 8192 + pmaj_off(prow + 32 * i, kc)) = rd[i];
+    }
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = (pend - pbeg + BKP - 1) / BKP;
+  if (nsteps > 0) {
+    gload(pbeg);
+    lstore(0);
+  }
+  __syncthreads();
+
+  // tr-read addressing: lane l, group g = l>>4, i = l&15, q = i>>2, p = i&3.
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  for (int st = 0; st < nsteps; ++st) {
+    const int cur = st & 1;
+    if (st + 1 < nsteps) gload(pbeg + (st + 1) * BKP);
+    const unsigned char* X = sX + cur * 8192;
+    const unsigned char* D = sD + cur * 8192;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = kk * 32 + h * 16 + 4 * g + q;  // pixel row supplying elements 4h..4h+3
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const int col = wm * 32 + m * 16 + 4 * p;  // bf16 column within the 64-col tile
+          const s16x4 v = tr_read(X, pmaj_off(row, col >> 3) + ((col & 7) << 1));
+          fa[m][4 * h + 0] = __builtin_bit_cast(__bf16, v[0]);
+          fa[m][4 * h + 1] = __builtin_bit_cast(__bf16, v[1]);
+          fa[m][4 * h + 2] = __builtin_bit_cast(__bf16, v[2]);
+          fa[m][4 * h + 3] = __builtin_bit_cast(__bf16, v[3]);
+        }
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          const int col = wn * 32 + n * 16 + 4 * p;
+          const s16x4 v = tr_read(D, pmaj_off(row, col >> 3) + ((col & 7) << 1));
+          fb[n][4 * h + 0] = __builtin_bit_cast(__bf16, v[0]);
+          fb[n][4 * h + 1] = __builtin_bit_cast(__bf16, v[1]);
+          fb[n][4 * h + 2] = __builtin_bit_cast(__bf16, v[2]);
+          fb[n][4 * h + 3] = __builtin_bit_cast(__bf16, v[3]);
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
+    }
+    if (st + 1 < nsteps) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // D[row = k][col = oc]: lane holds k = 4(l>>4)+i for oc = l&15 -> 16-byte fp32 store
+  float* part = a.part + (size_t)split * a.OC * a.Kg;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int k = k0 + wm * 32 + m * 16 + 4 * (lane >> 4);
+      const int oc = oc0 + wn * 32 + n * 16 + (lane & 15);
+      *reinterpret_cast<f32x4*>(part + (size_t)oc * a.Kg + k) = acc[m][n];
+    }
+}
+
+// Sum the split-K partials, permute (oc, r, s, c) -> reference OIHW (oc, c, r, s), drop the
+// channel padding and emit the gradient straight into the wire buffer (fp16 codec or fp32).
+template <typename OutT>
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int OC,
+                                                           int Kg, int Cin, int IC, int R, int S, float scale,
+                                                           OutT* __restrict__ out) {
+  const int total = OC * Cin * R * S;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    // idx enumerates the OIHW destination
+    const int s_ = idx % S;
+    int t = idx / S;
+    const int r_ = t % R;
+    t /= R;
+    const int c = t % Cin;
+    const int oc = t / Cin;
+    const int k = (r_ * S + s_) * IC + c;
+    float v = 0.f;
+    const float* p = part + (size_t)oc * Kg + k;
+    for (int sp = 0; sp < splits; ++sp) v += p[(size_t)sp * OC * Kg];
+    v *= scale;
+    if constexpr (sizeof(OutT) == 2) {
+      out[idx] = __builtin_bit_cast(uint16_t, (_Float16)v);
+    } else {
+      out[idx] = v;
+    }
+  }
+}
+
+}  // namespace psx
+
+// ------------------------------------------------------------------------------------
+// C ABI launchers
+// ------------------------------------------------------------------------------------
+using namespace psx;
+
+template <int BM, int BN, int MODE, bool RES>
+static int launch_conv(const ConvArgs& a, hipStream_t st) {
+  ConvArgs b = a;
+  b.n_oc_tiles = a.OC / BM;
+  b.n_pix_tiles = (a.npix + BN - 1) / BN;
+  const size_t lds = (size_t)2 * (BM + BN) * 128;
+  const int grid = b.n_oc_tiles * b.n_pix_tiles;
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, RES>), dim3(grid), dim3(256), lds, st, b);
+  return (int)hipGetLastError();
+}
+
+template <int MODE, bool RES>
+static int dispatch_tile(int tile_cfg, const ConvArgs& a, hipStream_t st) {
+  switch (tile_cfg) {
+    case 0: return launch_conv<64, 128, MODE, RES>(a, st);
+    case 1: return launch_conv<128, 128, MODE, RES>(a, st);
+    case 2: return launch_conv<64, 64, MODE, RES>(a, st);
+    case 3: return launch_conv<128, 64, MODE, RES>(a, st);
+    default: return -1;
+  }
+}
+
+static int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+
+// Tile selection: output-channel tile (BM) must divide OC; prefer >= 512 workgroups.
+static int pick_tile(int OC, int npix) {
+  if (OC % 128 == 0 && (long)(OC / 128) * ((npix + 127) / 128) >= 512) return 1;
+  if ((long)(OC / 64) * ((npix + 127) / 128) >= 256) return 0;
+  if (OC % 128 == 0 && (long)(OC / 128) * ((npix + 63) / 64) >= 256) return 3;
+  return 2;
+}
+
+extern "C" {
+
+// Forward conv. x: NHWC [Nb][H][W][IC]; wf: [OC][Kg]; y: NHWC [Nb][P][Q][OC].
+// stats (nullable): BN partial sums [n_pix_tiles][2][OC]; returns n_pix_tiles via *ntiles.
+int psx_conv_fwd(const void* x, const void* wf, void* y, float* stats, int Nb, int H, int W, int IC, int OC, int R,
+                 int S, int stride, int pad, int Kg, int tile_cfg, int* ntiles, hipStream_t st) {
+  ConvArgs a{};
+  a.in = (const uint16_t*)x;
+  a.w = (const uint16_t*)wf;
+  a.out = (uint16_t*)y;
+  a.res = nullptr;
+  a.stats = stats;
+  a.Nb = Nb; a.IH = H; a.IW = W; a.IC = IC;
+  a.OH = (H + 2 * pad - R) / stride + 1;
+  a.OW = (W + 2 * pad - S) / stride + 1;
+  a.OC = OC; a.R = R; a.S = S; a.pad = pad; a.stride = stride;
+  a.Kg = Kg;
+  a.log2_icc = ilog2(IC / 8);
+  a.npix = Nb * a.OH * a.OW;
+  if (OC % 64 || Kg % 64 || IC % 8 || (IC & (IC - 1))) return -2;
+  if (tile_cfg < 0) tile_cfg = pick_tile(OC, a.npix);
+  if ((tile_cfg == 1 || tile_cfg == 3) && OC % 128) tile_cfg = (tile_cfg == 1) ? 0 : 2;
+  const int BN = (tile_cfg == 0 || tile_cfg == 1) ? 128 : 64;
+  if (ntiles) *ntiles = (a.npix + BN - 1) / BN;
+  return dispatch_tile<0, false>(tile_cfg, a, st);
+}
+
+// Data gradient. dy: NHWC [Nb][P][Q][OC_fwd]; wd: [IC_fwd][Kg'] with Kg' >= R*S*OC_fwd;
+// dx: NHWC [Nb][H][W][IC_fwd]; res (nullable) is added to dx.
+int psx_conv_dgrad(const void* dy, const void* wd, void* dx, const void* res, int Nb, int H, int W, int IC_fwd,
+                   int OC_fwd, int R, int S, int stride, int pad, int Kg, int tile_cfg, hipStream_t st) {
+  ConvArgs a{};
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  a.in = (const uint16_t*)dy;
+  a.w = (const uint16_t*)wd;
+  a.out = (uint16_t*)dx;
+  a.res = (const uint16_t*)res;
+  a.stats = nullptr;
+  a.Nb = Nb; a.IH = P; a.IW = Q; a.IC = OC_fwd;
+  a.OH = H; a.OW = W; a.OC = IC_fwd;
+  a.R = R; a.S = S; a.pad = pad; a.stride = stride;
+  a.Kg = Kg;
+  a.log2_icc = ilog2(OC_fwd / 8);
+  a.npix = Nb * H * W;
+  if (IC_fwd % 64 || Kg % 64 || (OC_fwd & (OC_fwd - 1))) return -2;
+  if (tile_cfg < 0) tile_cfg = pick_tile(IC_fwd, a.npix);
+  if ((tile_cfg == 1 || tile_cfg == 3) && IC_fwd % 128) tile_cfg = (tile_cfg == 1) ? 0 : 2;
+  if (stride == 1) return res ? dispatch_tile<1, true>(tile_cfg, a, st) : dispatch_tile<1, false>(tile_cfg, a, st);
+  if (stride == 2) return res ? dispatch_tile<2, true>(tile_cfg, a, st) : dispatch_tile<2, false>(tile_cfg, a, st);
+  return -4;
+}
+
+// Weight-gradient partials; returns the number of splits used (partials buffer must hold
+// splits*OC*Kg floats; query with part == nullptr).
+int psx_conv_wgrad(const void* x, const void* dy, float* part, int Nb, int H, int W, int IC, int OC, int R, int S,
+                   int stride, int pad, int Kg, int splits, hipStream_t st) {
+  WgradArgs a{};
+  a.x = (const uint16_t*)x;
+  a.dy = (const uint16_t*)dy;
+  a.part = part;
+  a.Nb = Nb; a.IH = H; a.IW = W; a.IC = IC;
+  a.OH = (H + 2 * pad - R) / stride + 1;
+  a.OW = (W + 2 * pad - S) / stride + 1;
+  a.OC = OC; a.R = R; a.S = S; a.pad = pad; a.stride = stride;
+  a.Kg = Kg;
+  a.log2_icc = ilog2(IC / 8);
+  a.npix = Nb * a.OH * a.OW;
+  a.n_k_tiles = Kg / 64;
+  a.n_oc_tiles = OC / 64;
+  if (OC % 64 || Kg % 64) return -2;
+  const int tiles = a.n_k_tiles * a.n_oc_tiles;
+  if (splits <= 0) {
+    // aim for ~1024 workgroups, at least 8 pixel-steps (512 pixels) per split
+    const int max_splits = (a.npix + 511) / 512;
+    splits = (1024 + tiles - 1) / tiles;
+    if (splits > max_splits) splits = max_splits;
+    if (splits < 1) splits = 1;
+  }
+  int pps = (a.npix + splits - 1) / splits;
+  pps = (pps + 63) / 64 * 64;
+  splits = (a.npix + pps - 1) / pps;
+  a.splits = splits;
+  a.pix_per_split = pps;
+  if (!part) return splits;
+  const size_t lds = 2 * 2 * 64 * 128;
+  hipLaunchKernelGGL(conv_wgrad_kernel, dim3(tiles * splits), dim3(256), lds, st, a);
+  const int e = (int)hipGetLastError();
+  return e ? -e : splits;
+}
+
+int psx_wgrad_reduce(const float* part, int splits, int OC, int Kg, int Cin, int IC, int R, int S, float scale,
+                     void* out, int out_fp16, hipStream_t st) {
+  const int total = OC * Cin * R * S;
+  int grid = (total + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  if (out_fp16)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<uint16_t>, dim3(grid), dim3(256), 0, st, part, splits, OC, Kg, Cin, IC,
+                       R, S, scale, (uint16_t*)out);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<float>, dim3(grid), dim3(256), 0, st, part, splits, OC, Kg, Cin, IC, R,
+                       S, scale, (float*)out);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,198 @@
+// Parameter-server numerics on HBM-resident flat arenas:
+//   * sgd_apply     : the server update p <- p - lr * w * g  (reference server.py:126-143,
+//                     apply_gradients; w = 1/W for sync averaging server.py:166-167 or the
+//                     async staleness weight server.py:178), optionally with momentum and
+//                     weight decay (baseline optimizer, baseline_training.py:223),
+//                     reading fp16 wire gradients directly (codec unpack fused).
+//   * grad_aggregate: N-input gradient sum (reference aggregate_gradients_sync, server.py:145-169)
+//   * fp16 codec    : pack/unpack (reference compress_gradients worker.py:264-268 /
+//                     decompress_gradients server.py:232-237)
+//   * param_unpack  : fp32 OIHW master weights -> bf16 implicit-GEMM operands (KRSC for the
+//                     forward conv, transposed CRSK for the data-gradient conv); one launch for
+//                     every conv of the model, table-driven.
+#include "common.hpp"
+
+namespace psx {
+
+PSX_DEV float ld_grad(const uint16_t* g, size_t i) { return (float)__builtin_bit_cast(_Float16, g[i]); }
+PSX_DEV float ld_grad(const float* g, size_t i) { return g[i]; }
+
+template <typename GT, bool MOM>
+__global__ __launch_bounds__(256) void sgd_apply_kernel(float* __restrict__ p, const GT* __restrict__ g,
+                                                        float* __restrict__ buf, size_t n, float lr, float gscale,
+                                                        float momentum, float wd, int first) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float d = ld_grad(g, i) * gscale;
+    const float pv = p[i];
+    if (wd != 0.f) d += wd * pv;
+    if (MOM) {
+      const float v = first ? d : momentum * buf[i] + d;
+      buf[i] = v;
+      d = v;
+    }
+    p[i] = pv - lr * d;
+  }
+}
+
+// vectorised fp16-gradient fast path (no momentum): 8 elements per lane
+__global__ __launch_bounds__(256) void sgd_apply_h8_kernel(float* __restrict__ p, const uint16_t* __restrict__ g,
+                                                           size_t n8, float step, float wd_step) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
+    const u32x4 gv = reinterpret_cast<const u32x4*>(g)[i];
+    f32x4 p0 = reinterpret_cast<f32x4*>(p)[2 * i];
+    f32x4 p1 = reinterpret_cast<f32x4*>(p)[2 * i + 1];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t w0 = gv[j], w1 = gv[2 + j];
+      const float a = (float)__builtin_bit_cast(_Float16, (uint16_t)(w0 & 0xffff));
+      const float b = (float)__builtin_bit_cast(_Float16, (uint16_t)(w0 >> 16));
+      const float c = (float)__builtin_bit_cast(_Float16, (uint16_t)(w1 & 0xffff));
+      const float d = (float)__builtin_bit_cast(_Float16, (uint16_t)(w1 >> 16));
+      p0[2 * j] -= step * a + wd_step * p0[2 * j];
+      p0[2 * j + 1] -= step * b + wd_step * p0[2 * j + 1];
+      p1[2 * j] -= step * c + wd_step * p1[2 * j];
+      p1[2 * j + 1] -= step * d + wd_step * p1[2 * j + 1];
+    }
+    reinterpret_cast<f32x4*>(p)[2 * i] = p0;
+    reinterpret_cast<f32x4*>(p)[2 * i + 1] = p1;
+  }
+}
+
+// dst = sum_i src_i * scale  (fp16 or fp32 sources; fp32 or fp16 destination)
+template <typename ST, typename DT>
+__global__ __launch_bounds__(256) void aggregate_kernel(const ST* const* __restrict__ srcs, int nsrc,
+                                                        DT* __restrict__ dst, size_t n, float scale, int accumulate) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < nsrc; ++k) s += ld_grad(srcs[k], i);
+    s *= scale;
+    if constexpr (sizeof(DT) == 2) {
+      if (accumulate) s += ld_grad(dst, i);
+      dst[i] = __builtin_bit_cast(uint16_t, (_Float16)s);
+    } else {
+      if (accumulate) s += dst[i];
+      dst[i] = s;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void fp16_pack_kernel(const float* __restrict__ src, uint16_t* __restrict__ dst,
+                                                        size_t n, float scale) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = __builtin_bit_cast(uint16_t, (_Float16)(src[i] * scale));
+}
+__global__ __launch_bounds__(256) void fp16_unpack_kernel(const uint16_t* __restrict__ src, float* __restrict__ dst,
+                                                          size_t n, float scale) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = (float)__builtin_bit_cast(_Float16, src[i]) * scale;
+}
+
+struct UnpackDesc {
+  long src_off;  // element offset of the OIHW fp32 weight in the arena
+  long wf_off;   // element offset of the bf16 [OC][Kg] forward operand
+  long wd_off;   // element offset of the bf16 [Cp][Kgd] dgrad operand, -1 if none
+  int OC, Cin, R, S, Cp, Kg, Kgd, pad_;
+};
+
+__global__ __launch_bounds__(256) void param_unpack_kernel(const float* __restrict__ arena,
+                                                           const UnpackDesc* __restrict__ descs,
+                                                           uint16_t* __restrict__ wbuf) {
+  const UnpackDesc d = descs[blockIdx.y];
+  const float* src = arena + d.src_off;
+  const long nf = (long)d.OC * d.Kg;
+  const long nd = d.wd_off >= 0 ? (long)d.Cp * d.Kgd : 0;
+  const int RS = d.R * d.S;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nf + nd; i += (long)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (i < nf) {
+      const int oc = (int)(i / d.Kg), k = (int)(i - (long)oc * d.Kg);
+      const int tap = k / d.Cp, c = k - tap * d.Cp;
+      if (tap < RS && c < d.Cin) v = src[((size_t)oc * d.Cin + c) * RS + tap];
+      wbuf[d.wf_off + i] = f2bf(v);
+    } else {
+      const long j = i - nf;
+      const int c = (int)(j / d.Kgd), k = (int)(j - (long)c * d.Kgd);
+      const int tap = k / d.OC, oc = k - tap * d.OC;
+      if (tap < RS && c < d.Cin) v = src[((size_t)oc * d.Cin + c) * RS + tap];
+      wbuf[d.wd_off + j] = f2bf(v);
+    }
+  }
+}
+
+}  // namespace psx
+
+using namespace psx;
+
+static int grid_for(size_t n) {
+  size_t g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+extern "C" {
+
+// p -= lr * (gscale*g + wd*p) [with momentum buffer]; grads fp16 (wire) or fp32.
+int psx_sgd_apply(float* p, const void* g, float* buf, long n, float lr, float gscale, float momentum, float wd,
+                  int first, int grad_fp16, hipStream_t st) {
+  const bool mom = buf != nullptr && momentum != 0.f;
+  if (!mom && grad_fp16 && n % 8 == 0 && ((uintptr_t)p % 32 == 0) && ((uintptr_t)g % 16 == 0)) {
+    hipLaunchKernelGGL(sgd_apply_h8_kernel, dim3(grid_for(n / 8)), dim3(256), 0, st, p, (const uint16_t*)g,
+                       (size_t)n / 8, lr * gscale, lr * wd);
+    return (int)hipGetLastError();
+  }
+  const int grid = grid_for(n);
+  if (grad_fp16) {
+    if (mom)
+      hipLaunchKernelGGL((sgd_apply_kernel<uint16_t, true>), dim3(grid), dim3(256), 0, st, p, (const uint16_t*)g, buf,
+                         (size_t)n, lr, gscale, momentum, wd, first);
+    else
+      hipLaunchKernelGGL((sgd_apply_kernel<uint16_t, false>), dim3(grid), dim3(256), 0, st, p, (const uint16_t*)g,
+                         buf, (size_t)n, lr, gscale, momentum, wd, first);
+  } else {
+    if (mom)
+      hipLaunchKernelGGL((sgd_apply_kernel<float, true>), dim3(grid), dim3(256), 0, st, p, (const float*)g, buf,
+                         (size_t)n, lr, gscale, momentum, wd, first);
+    else
+      hipLaunchKernelGGL((sgd_apply_kernel<float, false>), dim3(grid), dim3(256), 0, st, p, (const float*)g, buf,
+                         (size_t)n, lr, gscale, momentum, wd, first);
+  }
+  return (int)hipGetLastError();
+}
+
+// srcs: device array of nsrc device pointers.
+int psx_grad_aggregate(const void* const* srcs, int nsrc, int src_fp16, void* dst, int dst_fp16, long n, float scale,
+                       int accumulate, hipStream_t st) {
+  const int grid = grid_for(n);
+#define PSX_AGG(S, D)                                                                                      \
+  hipLaunchKernelGGL((aggregate_kernel<S, D>), dim3(grid), dim3(256), 0, st, (const S* const*)srcs, nsrc, \
+                     (D*)dst, (size_t)n, scale, accumulate)
+  if (src_fp16 && dst_fp16) PSX_AGG(uint16_t, uint16_t);
+  else if (src_fp16) PSX_AGG(uint16_t, float);
+  else if (dst_fp16) PSX_AGG(float, uint16_t);
+  else PSX_AGG(float, float);
+#undef PSX_AGG
+  return (int)hipGetLastError();
+}
+
+int psx_fp16_pack(const float* src, void* dst, long n, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(fp16_pack_kernel, dim3(grid_for(n)), dim3(256), 0, st, src, (uint16_t*)dst, (size_t)n, scale);
+  return (int)hipGetLastError();
+}
+
+int psx_fp16_unpack(const void* src, float* dst, long n, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(fp16_unpack_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const uint16_t*)src, dst, (size_t)n,
+                     scale);
+  return (int)hipGetLastError();
+}
+
+// descs: device array of ndesc UnpackDesc (see struct layout above: 3 int64 + 8 int32)
+int psx_param_unpack(const float* arena, const void* descs, int ndesc, void* wbuf, hipStream_t st) {
+  hipLaunchKernelGGL(param_unpack_kernel, dim3(256, ndesc), dim3(256), 0, st, arena, (const UnpackDesc*)descs,
+                     (uint16_t*)wbuf);
+  return (int)hipGetLastError();
+}
+
+int psx_unpack_desc_size() { return (int)sizeof(UnpackDesc); }
+
+}  // extern "C"

@@ -1,0 +1,464 @@
+"""HIP training engine: ResNet forward/backward on hand-written CDNA4 kernels.
+
+This is the MI355X replacement for the worker's ``train_local_batch`` (reference:
+src/workers/worker.py:333-348 — zero_grad, forward, CrossEntropyLoss, backward) and for
+``evaluate_model`` (worker.py:313-331). Instead of autograd over ``nn.Module``s it runs an
+explicit, statically-scheduled forward + backward over pre-allocated HBM buffers:
+
+* activations NHWC bf16; conv = MFMA implicit GEMM (fwd / dgrad / split-K wgrad), BN batch
+  statistics produced by the conv epilogue, BN+ReLU(+residual) fused elementwise passes,
+  fused pool+FC+softmax-xent head;
+* gradients are written straight into one flat wire buffer (fp16 codec by default) laid out
+  like the trainable-parameter prefix of the parameter arena (models/layout.py), so a push is
+  a single RCCL reduce/send of one buffer and the server update one fused kernel;
+* parameters are read from a worker-local fp32 arena (the fetched server state) and unpacked
+  to bf16 implicit-GEMM operands by one table-driven kernel per fetch;
+* no allocation, host sync or data-dependent host control flow inside a step, so the whole
+  step (unpack + augment + fwd + bwd) is captured once into a HIP graph and replayed.
+
+The network is described by a generic block list so ResNet-18 (CIFAR stem) and ResNet-50
+(ImageNet stem with max-pool) share one engine.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..ops import kernels as K
+from .layout import ParamLayout
+from .resnet import Bottleneck, BasicBlock
+
+CIFAR_MEAN = (0.5071, 0.4867, 0.4408)  # reference worker.py:149-150
+CIFAR_STD = (0.2675, 0.2565, 0.2761)
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def _pow2_ceil(v: int) -> int:
+    p = 8
+    while p < v:
+        p *= 2
+    return p
+
+
+@dataclass
+class ConvSpec:
+    name: str
+    cin: int
+    cout: int
+    k: int
+    stride: int
+    pad: int
+    h: int = 0  # input spatial
+    w: int = 0
+    need_dgrad: bool = True
+    cp: int = 0
+    kg: int = 0
+    kgd: int = 0
+    wf_off: int = 0
+    wd_off: int = -1
+
+    def finalize(self):
+        self.cp = _pow2_ceil(self.cin)
+        self.kg = -(-(self.k * self.k * self.cp) // 64) * 64
+        self.kgd = self.k * self.k * self.cout  # cout % 64 == 0 for every ResNet conv
+        assert self.kgd % 64 == 0 and self.cout % 64 == 0, self.name
+
+    @property
+    def out_hw(self):
+        return K.conv_out_hw(self.h, self.w, self.k, self.stride, self.pad)
+
+
+@dataclass
+class BNSpec:
+    name: str
+    c: int
+
+
+@dataclass
+class BlockSpec:
+    convs: list
+    bns: list
+    down: tuple | None = None  # (ConvSpec, BNSpec)
+
+
+@dataclass
+class NetSpec:
+    stem_conv: ConvSpec
+    stem_bn: BNSpec
+    maxpool: bool
+    blocks: list = field(default_factory=list)
+    fc: str = "fc"
+    fc_in: int = 512
+    classes: int = 100
+    in_hw: tuple = (32, 32)
+
+
+def netspec_from_module(model: torch.nn.Module, in_hw) -> NetSpec:
+    def conv_of(m, name, h, w):
+        return ConvSpec(name, m.in_channels, m.out_channels, m.kernel_size[0], m.stride[0], m.padding[0], h, w)
+
+    h, w = in_hw
+    stem = conv_of(model.conv1, "conv1", h, w)
+    stem.need_dgrad = False
+    h, w = stem.out_hw
+    maxpool = hasattr(model, "maxpool")
+    if maxpool:
+        h, w = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1
+    spec = NetSpec(stem, BNSpec("bn1", model.bn1.num_features), maxpool)
+    for li in range(1, 5):
+        layer = getattr(model, f"layer{li}")
+        for bi, blk in enumerate(layer):
+            pre = f"layer{li}.{bi}"
+            if isinstance(blk, BasicBlock):
+                names = ["conv1", "conv2"]
+                down_mod = blk.shortcut if len(blk.shortcut) else None
+                down_names = (f"{pre}.shortcut.0", f"{pre}.shortcut.1")
+            elif isinstance(blk, Bottleneck):
+                names = ["conv1", "conv2", "conv3"]
+                down_mod = blk.downsample
+                down_names = (f"{pre}.downsample.0", f"{pre}.downsample.1")
+            else:
+                raise TypeError(type(blk))
+            convs, bns = [], []
+            ch, cw = h, w
+            for i, n in enumerate(names):
+                m = getattr(blk, n)
+                cs = conv_of(m, f"{pre}.{n}", ch, cw)
+                convs.append(cs)
+                bns.append(BNSpec(f"{pre}.bn{i + 1}", getattr(blk, f"bn{i + 1}").num_features))
+                ch, cw = cs.out_hw
+            down = None
+            if down_mod is not None:
+                ds = conv_of(down_mod[0], down_names[0], h, w)
+                down = (ds, BNSpec(down_names[1], down_mod[1].num_features))
+            spec.blocks.append(BlockSpec(convs, bns, down))
+            h, w = ch, cw
+    spec.fc_in = model.fc.in_features
+    spec.classes = model.fc.out_features
+    spec.in_hw = tuple(in_hw)
+    return spec
+
+
+def all_convs(spec: NetSpec):
+    yield spec.stem_conv
+    for b in spec.blocks:
+        yield from b.convs
+        if b.down:
+            yield b.down[0]
+
+
+class HipResNetEngine:
+    """Pre-allocated, graph-capturable ResNet training step on psx HIP kernels."""
+
+    def __init__(self, model: torch.nn.Module, layout: ParamLayout, batch: int, device="cuda",
+                 grad_dtype=torch.float16, in_hw=(32, 32), mean=CIFAR_MEAN, std=CIFAR_STD, bn_eps=1e-5,
+                 bn_momentum=0.1, seed=1234):
+        if not torch.cuda.is_available():
+            raise RuntimeError("HipResNetEngine needs an MI355X (torch.cuda / HIP device)")
+        K.unpack_desc_size()  # fail loudly right here if the native library is missing
+        self.dev = torch.device(device)
+        self.layout = layout
+        self.B = batch
+        self.spec = netspec_from_module(model, in_hw)
+        self.grad_dtype = grad_dtype
+        self.grad_fp16 = grad_dtype == torch.float16
+        self.mean, self.std = mean, std
+        self.eps, self.mom = bn_eps, bn_momentum
+        self.seed = seed
+        self.graph = None
+        self._build()
+
+    # ------------------------------------------------------------------ allocation
+    def _bf(self, *shape):
+        return torch.empty(*shape, dtype=torch.bfloat16, device=self.dev)
+
+    def _f32(self, *shape):
+        return torch.zeros(*shape, dtype=torch.float32, device=self.dev)
+
+    def _build(self):
+        sp, B = self.spec, self.B
+        # weights: one bf16 buffer holding every conv's fwd (and dgrad) operand
+        off = 0
+        descs = []
+        for cs in all_convs(sp):
+            cs.finalize()
+            cs.wf_off = off
+            off += cs.cout * cs.kg
+            if cs.need_dgrad:
+                cs.wd_off = off
+                off += cs.cp * cs.kgd
+            else:
+                cs.wd_off = -1
+            descs.append((self.layout.offset(f"{cs.name}.weight"), cs.wf_off, cs.wd_off, cs.cout, cs.cin, cs.k, cs.k,
+                          cs.cp, cs.kg, cs.kgd, 0))
+        self.wbuf = torch.zeros(off, dtype=torch.bfloat16, device=self.dev)
+        dsz = K.unpack_desc_size()
+        assert dsz == 3 * 8 + 8 * 4, dsz
+        raw = np.zeros(len(descs), dtype=np.dtype([("o", "<i8", 3), ("i", "<i4", 8)]))
+        for j, d in enumerate(descs):
+            raw[j]["o"] = d[:3]
+            raw[j]["i"] = d[3:]
+        self.descs = torch.from_numpy(raw.view(np.uint8).copy()).to(self.dev)
+        self.ndesc = len(descs)
+
+        H, W = sp.in_hw
+        self.x0 = self._bf(B, H, W, sp.stem_conv.cp)
+        self.labels = torch.zeros(B, dtype=torch.int32, device=self.dev)
+        self.index = torch.zeros(B, dtype=torch.int32, device=self.dev)
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=self.dev)
+
+        # per-BN persistent state: affine [2,C] (scale, shift), saved [2,C] (mean, invstd), coef [3,C]
+        self.bn = {}
+
+        def bn_state(bs: BNSpec):
+            self.bn[bs.name] = dict(affine=self._f32(2, bs.c), saved=self._f32(2, bs.c), coef=self._f32(3, bs.c),
+                                    c=bs.c)
+
+        # activation / gradient buffers
+        st = sp.stem_conv
+        p, q = st.out_hw
+        self.y0 = self._bf(B, p, q, st.cout)
+        self.a0 = self._bf(B, p, q, st.cout)
+        self.g0 = self._bf(B, p, q, st.cout)   # grad wrt a0 (or wrt maxpool input)
+        self.dy0 = self._bf(B, p, q, st.cout)
+        bn_state(sp.stem_bn)
+        max_stats = 2 * st.cout * K.conv_fwd_ntiles(st.cout, B * p * q, K.pick_tile(st.cout, B * p * q))
+        max_bnp = 0
+        max_wg = 0
+
+        def track(cs: ConvSpec):
+            nonlocal max_stats, max_wg, max_bnp
+            oh, ow = cs.out_hw
+            npix = B * oh * ow
+            cfg = K.pick_tile(cs.cout, npix)
+            max_stats = max(max_stats, 2 * cs.cout * K.conv_fwd_ntiles(cs.cout, npix, cfg))
+            s = K.conv_wgrad_splits(B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
+            cs.splits = s
+            max_wg = max(max_wg, s * cs.cout * cs.kg)
+            max_bnp = max(max_bnp, 3 * cs.cout * K.bn_bwd_reduce_T(npix, cs.cout))
+
+        track(st)
+        if sp.maxpool:
+            raise NotImplementedError("max-pool stem (ResNet-50) kernels land with the ResNet-50 engine")
+        self.blk = []
+        h_in = self.a0
+        for b in sp.blocks:
+            d = dict(inp=h_in)
+            d["y"] = [self._bf(B, *cs.out_hw, cs.cout) for cs in b.convs]
+            d["a"] = [self._bf(B, *cs.out_hw, cs.cout) for cs in b.convs[:-1]]
+            d["dy"] = [self._bf(B, *cs.out_hw, cs.cout) for cs in b.convs]
+            d["da"] = [self._bf(B, *cs.out_hw, cs.cout) for cs in b.convs[:-1]]
+            last = b.convs[-1]
+            d["out"] = self._bf(B, *last.out_hw, last.cout)
+            d["gin"] = torch.empty_like(h_in)  # grad wrt block input
+            for cs in b.convs:
+                track(cs)
+            for bs in b.bns:
+                bn_state(bs)
+            if b.down:
+                ds, dbn = b.down
+                track(ds)
+                bn_state(dbn)
+                d["ys"] = self._bf(B, *ds.out_hw, ds.cout)
+                d["dys"] = self._bf(B, *ds.out_hw, ds.cout)
+                d["dxs"] = torch.empty_like(h_in)
+            else:
+                d["dz"] = self._bf(B, *last.out_hw, last.cout)
+            self.blk.append(d)
+            h_in = d["out"]
+        self.final = h_in
+        self.stats = self._f32(max_stats)
+        self.wpart = self._f32(max_wg)
+        self.bnpart = self._f32(max(max_bnp, 1))
+        # head
+        fh, fw = self.final.shape[1], self.final.shape[2]
+        self.head_hw = fh * fw
+        self.pooled = self._f32(B, sp.fc_in)
+        self.dlogits = self._f32(B, sp.classes)
+        self.loss = self._f32(B)
+        self.correct = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.dfinal = torch.empty_like(self.final)
+        # gradient wire buffer (trainable-parameter prefix of the arena)
+        self.grads = torch.zeros(self.layout.param_numel, dtype=self.grad_dtype, device=self.dev)
+
+    # ------------------------------------------------------------------ helpers
+    def _gptr(self, name: str) -> int:
+        return self.grads.data_ptr() + self.grads.element_size() * self.layout.offset(name)
+
+    def _aview(self, arena, name):
+        return self.layout.view(arena, name)
+
+    def _conv_fwd(self, cs: ConvSpec, x, y, stats=True):
+        oh, ow = cs.out_hw
+        npix = self.B * oh * ow
+        cfg = K.pick_tile(cs.cout, npix)
+        wf = self.wbuf[cs.wf_off:cs.wf_off + cs.cout * cs.kg]
+        K.conv_fwd(x, wf, y, self.stats if stats else None, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride,
+                   cs.pad, cs.kg, cfg)
+        return K.conv_fwd_ntiles(cs.cout, npix, cfg), npix
+
+    def _bn_train(self, bs: BNSpec, arena, T, count):
+        st = self.bn[bs.name]
+        K.bn_finalize(self.stats, T, bs.c, count, self._aview(arena, f"{bs.name}.weight"),
+                      self._aview(arena, f"{bs.name}.bias"), self.eps, self.mom,
+                      self._aview(arena, f"{bs.name}.running_mean"), self._aview(arena, f"{bs.name}.running_var"),
+                      st["affine"], st["saved"])
+
+    def _bn_eval(self, bs: BNSpec, arena):
+        st = self.bn[bs.name]
+        K.bn_eval_affine(bs.c, self._aview(arena, f"{bs.name}.weight"), self._aview(arena, f"{bs.name}.bias"),
+                         self._aview(arena, f"{bs.name}.running_mean"), self._aview(arena, f"{bs.name}.running_var"),
+                         self.eps, st["affine"])
+
+    def _wgrad(self, cs: ConvSpec, x, dy):
+        K.conv_wgrad(x, dy, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg, cs.splits)
+        K.wgrad_reduce(self.wpart, cs.splits, cs.cout, cs.kg, cs.cin, cs.cp, cs.k, 1.0, self._gptr(f"{cs.name}.weight"),
+                       self.grad_fp16)
+
+    def _dgrad(self, cs: ConvSpec, dy, dx, res=None):
+        wd = self.wbuf[cs.wd_off:cs.wd_off + cs.cp * cs.kgd]
+        K.conv_dgrad(dy, wd, dx, res, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kgd)
+
+    def _bn_bwd(self, bs: BNSpec, arena, g, o, y, dx, npix, two=None, dzout=None):
+        """BN (+ReLU mask from o) backward; two = (bs2, y2, dx2) for a shared-dz second BN."""
+        st = self.bn[bs.name]
+        if two is None:
+            T = K.bn_bwd_reduce(g, o, y, st["saved"], self.bnpart, npix, bs.c)
+            K.bn_bwd_finalize(self.bnpart, T, 2, 1, bs.c, npix, self._aview(arena, f"{bs.name}.weight"),
+                              st["saved"], st["coef"], self._gptr(f"{bs.name}.weight"),
+                              self._gptr(f"{bs.name}.bias"), 1.0, self.grad_fp16)
+            K.bn_bwd_apply(g, o, y, st["coef"], dx, bs.c, dzout=dzout)
+        else:
+            bs2, y2, dx2 = two
+            st2 = self.bn[bs2.name]
+            T = K.bn_bwd_reduce(g, o, y, st["saved"], self.bnpart, npix, bs.c, y2=y2, saved2=st2["saved"])
+            K.bn_bwd_finalize(self.bnpart, T, 3, 1, bs.c, npix, self._aview(arena, f"{bs.name}.weight"),
+                              st["saved"], st["coef"], self._gptr(f"{bs.name}.weight"),
+                              self._gptr(f"{bs.name}.bias"), 1.0, self.grad_fp16)
+            K.bn_bwd_finalize(self.bnpart, T, 3, 2, bs2.c, npix, self._aview(arena, f"{bs2.name}.weight"),
+                              st2["saved"], st2["coef"], self._gptr(f"{bs2.name}.weight"),
+                              self._gptr(f"{bs2.name}.bias"), 1.0, self.grad_fp16)
+            K.bn_bwd_apply(g, o, y, st["coef"], dx, bs.c, y2=y2, coef2=st2["coef"], dx2=dx2, dzout=dzout)
+
+    # ------------------------------------------------------------------ public API
+    def unpack(self, arena: torch.Tensor):
+        """fp32 OIHW master weights (fetched arena) -> bf16 implicit-GEMM operands."""
+        K.param_unpack(arena, self.descs, self.ndesc, self.wbuf)
+
+    def load_batch(self, images_u8, labels_all, train=True):
+        """Gather self.index rows of the HBM-resident dataset + fused crop/flip/normalize."""
+        H, W = self.spec.in_hw
+        K.augment(images_u8, labels_all, self.index, self.x0, self.labels, self.B, H, W, 4, self.seed, self.step_dev,
+                  train, self.mean, self.std)
+
+    def forward(self, arena: torch.Tensor, train: bool = True):
+        sp, B = self.spec, self.B
+        st = sp.stem_conv
+        T, npix = self._conv_fwd(st, self.x0, self.y0, stats=train)
+        if train:
+            self._bn_train(sp.stem_bn, arena, T, npix)
+        else:
+            self._bn_eval(sp.stem_bn, arena)
+        K.bn_apply(self.y0, self.bn["bn1"]["affine"], self.a0, st.cout, relu=True)
+        for b, d in zip(sp.blocks, self.blk):
+            src = d["inp"]
+            L = len(b.convs)
+            for i, cs in enumerate(b.convs):
+                T, npix = self._conv_fwd(cs, src, d["y"][i], stats=train)
+                (self._bn_train(b.bns[i], arena, T, npix) if train else self._bn_eval(b.bns[i], arena))
+                if i < L - 1:
+                    K.bn_apply(d["y"][i], self.bn[b.bns[i].name]["affine"], d["a"][i], cs.cout, relu=True)
+                    src = d["a"][i]
+            last = b.convs[-1]
+            aff = self.bn[b.bns[-1].name]["affine"]
+            if b.down:
+                ds, dbn = b.down
+                T, npix = self._conv_fwd(ds, d["inp"], d["ys"], stats=train)
+                (self._bn_train(dbn, arena, T, npix) if train else self._bn_eval(dbn, arena))
+                K.bn_apply(d["y"][-1], aff, d["out"], last.cout, relu=True, res=d["ys"],
+                           affine2=self.bn[dbn.name]["affine"])
+            else:
+                K.bn_apply(d["y"][-1], aff, d["out"], last.cout, relu=True, res=d["inp"])
+        return self.final
+
+    def head(self, arena: torch.Tensor, backward: bool = True):
+        sp = self.spec
+        self.correct.zero_()
+        K.head_fwd_bwd(self.final, self.B, self.head_hw, sp.fc_in, self._aview(arena, f"{sp.fc}.weight"),
+                       self._aview(arena, f"{sp.fc}.bias"), sp.classes, self.labels, self.pooled, self.dlogits,
+                       self.dfinal if backward else None, self.loss, self.correct)
+
+    def backward(self, arena: torch.Tensor):
+        sp, B = self.spec, self.B
+        K.head_wgrad(self.dlogits, self.pooled, B, sp.classes, sp.fc_in, self._gptr(f"{sp.fc}.weight"),
+                     self._gptr(f"{sp.fc}.bias"), 1.0, self.grad_fp16)
+        g = self.dfinal
+        for b, d in zip(reversed(sp.blocks), reversed(self.blk)):
+            L = len(b.convs)
+            last = b.convs[-1]
+            oh, ow = last.out_hw
+            npix = B * oh * ow
+            if b.down:
+                ds, dbn = b.down
+                self._bn_bwd(b.bns[-1], arena, g, d["out"], d["y"][-1], d["dy"][-1], npix,
+                             two=(dbn, d["ys"], d["dys"]))
+            else:
+                self._bn_bwd(b.bns[-1], arena, g, d["out"], d["y"][-1], d["dy"][-1], npix, dzout=d["dz"])
+            for i in range(L - 1, -1, -1):
+                cs = b.convs[i]
+                x_in = d["inp"] if i == 0 else d["a"][i - 1]
+                self._wgrad(cs, x_in, d["dy"][i])
+                if i > 0:
+                    self._dgrad(cs, d["dy"][i], d["da"][i - 1])
+                    ph, pw = cs.h, cs.w
+                    self._bn_bwd(b.bns[i - 1], arena, d["da"][i - 1], d["a"][i - 1], d["y"][i - 1], d["dy"][i - 1],
+                                 B * ph * pw)
+                else:
+                    if b.down:
+                        ds, dbn = b.down
+                        self._wgrad(ds, d["inp"], d["dys"])
+                        self._dgrad(ds, d["dys"], d["dxs"])
+                        self._dgrad(cs, d["dy"][0], d["gin"], res=d["dxs"])
+                    else:
+                        self._dgrad(cs, d["dy"][0], d["gin"], res=d["dz"])
+            g = d["gin"]
+        st = sp.stem_conv
+        p, q = st.out_hw
+        self._bn_bwd(sp.stem_bn, arena, g, self.a0, self.y0, self.dy0, B * p * q)
+        self._wgrad(st, self.x0, self.dy0)
+
+    def train_step(self, arena: torch.Tensor, images_u8=None, labels_all=None, unpack=True):
+        """unpack (optional) + batch load + forward + loss + backward -> self.grads."""
+        if unpack:
+            self.unpack(arena)
+        if images_u8 is not None:
+            self.load_batch(images_u8, labels_all, train=True)
+        self.forward(arena, train=True)
+        self.head(arena, backward=True)
+        self.backward(arena)
+
+    # ------------------------------------------------------------------ graphs
+    def capture(self, arena, images_u8, labels_all, unpack=True, warmup=2):
+        """Capture the full step into a HIP graph; replay with ``step_graph()``."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.train_step(arena, images_u8, labels_all, unpack)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.train_step(arena, images_u8, labels_all, unpack)
+        self.graph = g
+        return g
+
+    def step_graph(self):
+        self.graph.replay()
+
+    def evaluate_batch(self, arena, images_u8, labels_all):
+        self.load_batch(images_u8, labels_all, train=False)
+        self.forward(arena, train=False)
+        self.head(arena, backward=False)

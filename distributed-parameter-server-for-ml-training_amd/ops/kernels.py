@@ -1,0 +1,176 @@
+"""Thin, allocation-free Python wrappers over the HIP kernel library.
+
+Every function takes pre-allocated torch tensors (device memory), launches on the current
+torch stream (so it composes with torch ops and is captured by ``torch.cuda.CUDAGraph``) and
+raises on a launch error. Layout conventions: NHWC bf16 activations with channels padded to a
+multiple of 8; conv weights as bf16 ``[OC][Kg]`` implicit-GEMM rows (see models/engine.py);
+fp32 parameter arenas; fp16 (wire codec) or fp32 gradient sinks.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from ._lib import check, kernels, ptr, stream_ptr
+
+# conv tile configurations (must match csrc/kernels/conv_gemm.hip dispatch_tile)
+TILE_CFGS = {0: (64, 128), 1: (128, 128), 2: (64, 64), 3: (128, 64)}
+
+
+def pick_tile(oc: int, npix: int) -> int:
+    """Output-channel x pixel tile for conv fwd/dgrad: fill >= 256 CUs with >= 1-2 waves of tiles."""
+    if oc % 128 == 0 and (oc // 128) * -(-npix // 128) >= 512:
+        return 1
+    if (oc // 64) * -(-npix // 128) >= 256:
+        return 0
+    if oc % 128 == 0 and (oc // 128) * -(-npix // 64) >= 256:
+        return 3
+    return 2
+
+
+def conv_out_hw(h: int, w: int, k: int, stride: int, pad: int):
+    return (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+
+
+def conv_fwd_ntiles(oc: int, npix: int, cfg: int) -> int:
+    return -(-npix // TILE_CFGS[cfg][1])
+
+
+def conv_fwd(x, wf, y, stats, nb, h, w, ic, oc, k, stride, pad, kg, cfg=None):
+    p, q = conv_out_hw(h, w, k, stride, pad)
+    if cfg is None:
+        cfg = pick_tile(oc, nb * p * q)
+    nt = C.c_int(0)
+    check(kernels().psx_conv_fwd(ptr(x), ptr(wf), ptr(y), ptr(stats), nb, h, w, ic, oc, k, k, stride, pad, kg, cfg,
+                                 C.byref(nt), stream_ptr()), "conv_fwd")
+    return nt.value
+
+
+def conv_dgrad(dy, wd, dx, res, nb, h, w, ic_fwd, oc_fwd, k, stride, pad, kgd, cfg=None):
+    if cfg is None:
+        cfg = pick_tile(ic_fwd, nb * h * w)
+    check(kernels().psx_conv_dgrad(ptr(dy), ptr(wd), ptr(dx), ptr(res), nb, h, w, ic_fwd, oc_fwd, k, k, stride, pad,
+                                   kgd, cfg, stream_ptr()), "conv_dgrad")
+
+
+def conv_wgrad_splits(nb, h, w, ic, oc, k, stride, pad, kg, splits=0) -> int:
+    n = kernels().psx_conv_wgrad(None, None, None, nb, h, w, ic, oc, k, k, stride, pad, kg, splits, None)
+    if n <= 0:
+        raise RuntimeError(f"conv_wgrad split query failed ({n})")
+    return n
+
+
+def conv_wgrad(x, dy, part, nb, h, w, ic, oc, k, stride, pad, kg, splits) -> int:
+    n = kernels().psx_conv_wgrad(ptr(x), ptr(dy), ptr(part), nb, h, w, ic, oc, k, k, stride, pad, kg, splits,
+                                 stream_ptr())
+    if n <= 0:
+        raise RuntimeError(f"conv_wgrad failed ({n})")
+    return n
+
+
+def wgrad_reduce(part, splits, oc, kg, cin, ic, k, scale, out_ptr: int, out_fp16: bool):
+    check(kernels().psx_wgrad_reduce(ptr(part), splits, oc, kg, cin, ic, k, k, float(scale), out_ptr, int(out_fp16),
+                                     stream_ptr()), "wgrad_reduce")
+
+
+def bn_finalize(part, T, c, count, gamma, beta, eps, momentum, run_mean, run_var, affine, saved):
+    """affine: [2, C] (scale, shift); saved: [2, C] (mean, invstd)."""
+    check(kernels().psx_bn_finalize(ptr(part), T, c, float(count), ptr(gamma), ptr(beta), float(eps),
+                                    float(momentum), ptr(run_mean), ptr(run_var), ptr(affine), ptr(affine) + 4 * c,
+                                    ptr(saved), ptr(saved) + 4 * c, stream_ptr()), "bn_finalize")
+
+
+def bn_eval_affine(c, gamma, beta, rm, rv, eps, affine):
+    check(kernels().psx_bn_eval_affine(c, ptr(gamma), ptr(beta), ptr(rm), ptr(rv), float(eps), ptr(affine),
+                                       ptr(affine) + 4 * c, stream_ptr()), "bn_eval_affine")
+
+
+def bn_apply(y, affine, out, c, relu=True, res=None, affine2=None):
+    mode = 0 if res is None else (1 if affine2 is None else 2)
+    a2 = ptr(affine2)
+    check(kernels().psx_bn_apply(ptr(y), ptr(affine), ptr(affine) + 4 * c, ptr(res), a2,
+                                 (a2 + 4 * c) if a2 else None, ptr(out), y.numel(), c, mode, int(relu),
+                                 stream_ptr()), "bn_apply")
+
+
+def bn_bwd_reduce_T(npix: int, c: int) -> int:
+    return kernels().psx_bn_bwd_reduce(None, None, None, None, None, None, None, None, None, npix, c, None)
+
+
+def bn_bwd_reduce(g, o, y1, saved1, part, npix, c, y2=None, saved2=None) -> int:
+    s2 = ptr(saved2)
+    T = kernels().psx_bn_bwd_reduce(ptr(g), ptr(o), ptr(y1), ptr(saved1), ptr(saved1) + 4 * c, ptr(y2), s2,
+                                    (s2 + 4 * c) if s2 else None, ptr(part), npix, c, stream_ptr())
+    if T <= 0:
+        raise RuntimeError(f"bn_bwd_reduce failed ({T})")
+    return T
+
+
+def bn_bwd_finalize(part, T, ns, which, c, count, gamma, saved, coef, dgamma_ptr, dbeta_ptr, gscale, grad_fp16):
+    check(kernels().psx_bn_bwd_finalize(ptr(part), T, ns, which, c, float(count), ptr(gamma), ptr(saved),
+                                        ptr(saved) + 4 * c, ptr(coef), dgamma_ptr, dbeta_ptr, float(gscale),
+                                        int(grad_fp16), stream_ptr()), "bn_bwd_finalize")
+
+
+def bn_bwd_apply(g, o, y1, coef1, dx1, c, y2=None, coef2=None, dx2=None, dzout=None):
+    check(kernels().psx_bn_bwd_apply(ptr(g), ptr(o), ptr(y1), ptr(coef1), ptr(dx1), ptr(y2), ptr(coef2), ptr(dx2),
+                                     ptr(dzout), g.numel(), c, stream_ptr()), "bn_bwd_apply")
+
+
+def head_fwd_bwd(act, b, hw, c, fcw, fcb, k, labels, pooled, dlogits, dact, loss, correct):
+    check(kernels().psx_head_fwd_bwd(ptr(act), b, hw, c, ptr(fcw), ptr(fcb), k, ptr(labels), ptr(pooled),
+                                     ptr(dlogits), ptr(dact), ptr(loss), ptr(correct), stream_ptr()), "head_fwd_bwd")
+
+
+def head_wgrad(dlogits, pooled, b, k, c, dw_ptr, db_ptr, gscale, grad_fp16):
+    check(kernels().psx_head_wgrad(ptr(dlogits), ptr(pooled), b, k, c, dw_ptr, db_ptr, float(gscale),
+                                   int(grad_fp16), stream_ptr()), "head_wgrad")
+
+
+def sgd_apply(p, g, lr, gscale=1.0, momentum=0.0, wd=0.0, buf=None, first=False, n=None):
+    n = p.numel() if n is None else n
+    fp16 = g.dtype == torch.float16
+    check(kernels().psx_sgd_apply(ptr(p), ptr(g), ptr(buf), n, float(lr), float(gscale), float(momentum), float(wd),
+                                  int(first), int(fp16), stream_ptr()), "sgd_apply")
+
+
+def grad_aggregate(srcs_dev_ptrs, nsrc, src_fp16, dst, n, scale=1.0, accumulate=False):
+    """srcs_dev_ptrs: int64 device tensor holding nsrc device pointers."""
+    check(kernels().psx_grad_aggregate(ptr(srcs_dev_ptrs), nsrc, int(src_fp16), ptr(dst),
+                                       int(dst.dtype == torch.float16), n, float(scale), int(accumulate),
+                                       stream_ptr()), "grad_aggregate")
+
+
+def fp16_pack(src, dst, scale=1.0):
+    check(kernels().psx_fp16_pack(ptr(src), ptr(dst), src.numel(), float(scale), stream_ptr()), "fp16_pack")
+
+
+def fp16_unpack(src, dst, scale=1.0):
+    check(kernels().psx_fp16_unpack(ptr(src), ptr(dst), src.numel(), float(scale), stream_ptr()), "fp16_unpack")
+
+
+def param_unpack(arena, descs_dev, ndesc, wbuf):
+    check(kernels().psx_param_unpack(ptr(arena), ptr(descs_dev), ndesc, ptr(wbuf), stream_ptr()), "param_unpack")
+
+
+def unpack_desc_size() -> int:
+    return kernels().psx_unpack_desc_size()
+
+
+def synth_gen(img, labels, n, h, w, classes, seed):
+    check(kernels().psx_synth_gen(ptr(img), ptr(labels), n, h, w, classes, seed & 0xFFFFFFFF, stream_ptr()),
+          "synth_gen")
+
+
+_F3 = C.c_float * 3
+
+
+def augment(img, labels, index, out, out_labels, b, h, w, pad, seed, step_dev, train, mean, std):
+    check(kernels().psx_augment(ptr(img), ptr(labels), ptr(index), ptr(out), ptr(out_labels), b, h, w, pad,
+                                seed & 0xFFFFFFFF, ptr(step_dev), int(train), _F3(*mean), _F3(*std), stream_ptr()),
+          "augment")
+
+
+def nchw_to_nhwc(x, y, n, c, h, w, cp):
+    check(kernels().psx_nchw_to_nhwc(ptr(x), ptr(y), n, c, h, w, cp, stream_ptr()), "nchw_to_nhwc")

@@ -1,0 +1,100 @@
+"""Whole-network check: one ResNet-18 training step on the HIP engine vs torch fp32 autograd."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from psx.models.engine import HipResNetEngine  # noqa: E402
+from psx.models.layout import ParamLayout  # noqa: E402
+from psx.models.resnet import ResNet18  # noqa: E402
+from psx.ops import kernels as K  # noqa: E402
+
+DEV = "cuda"
+
+
+def _bf16_round_(model):
+    with torch.no_grad():
+        for m in model.modules():
+            if isinstance(m, torch.nn.Conv2d):
+                m.weight.copy_(m.weight.to(torch.bfloat16).float())
+
+
+def _cos(a, b):
+    a, b = a.flatten().double(), b.flatten().double()
+    return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
+
+
+@pytest.fixture(scope="module")
+def setup():
+    torch.manual_seed(0)
+    B = 32
+    model = ResNet18(100)
+    _bf16_round_(model)
+    layout = ParamLayout.from_module(model)
+    arena, _ = layout.pack(model)
+    model = model.to(DEV)
+    eng = HipResNetEngine(model, layout, B, grad_dtype=torch.float32)
+    x = torch.randn(B, 3, 32, 32, device=DEV).to(torch.bfloat16).float()
+    y = torch.randint(0, 100, (B,), device=DEV)
+    return model, layout, arena.to(DEV), eng, x, y
+
+
+def test_train_step_matches_torch(setup):
+    model, layout, arena, eng, x, y = setup
+    arena_k = arena.clone()
+    eng.unpack(arena_k)
+    K.nchw_to_nhwc(x, eng.x0, x.shape[0], 3, 32, 32, 8)
+    eng.labels.copy_(y.to(torch.int32))
+    eng.forward(arena_k, train=True)
+    eng.head(arena_k, backward=True)
+    eng.backward(arena_k)
+    torch.cuda.synchronize()
+
+    model.train()
+    model.zero_grad()
+    out = model(x)
+    loss = F.cross_entropy(out, y)
+    loss.backward()
+    assert abs(eng.loss.mean().item() - loss.item()) < 0.02 * max(1.0, loss.item())
+    worst = 1.0
+    for name, p in model.named_parameters():
+        g = layout.grad_view(eng.grads, name)
+        c = _cos(g, p.grad)
+        worst = min(worst, c)
+        assert c > 0.97, (name, c)
+    # running statistics were updated in the worker-local arena exactly like torch's
+    sd = model.state_dict()
+    for name in ("bn1.running_mean", "layer2.0.bn1.running_var", "layer4.1.bn2.running_mean"):
+        got = layout.view(arena_k, name)
+        assert torch.allclose(got, sd[name], rtol=2e-2, atol=2e-3), name
+
+
+def test_graph_replay_matches_eager(setup):
+    model, layout, arena, eng, x, y = setup
+    n = 256
+    imgs = torch.randint(0, 256, (n, 32, 32, 3), dtype=torch.uint8, device=DEV)
+    labs = torch.randint(0, 100, (n,), dtype=torch.int32, device=DEV)
+    eng.index.copy_(torch.arange(eng.B, dtype=torch.int32, device=DEV))
+    a1 = arena.clone()
+    eng.train_step(a1, imgs, labs)
+    torch.cuda.synchronize()
+    eager = eng.grads.clone()
+    a2 = arena.clone()
+    eng.capture(a2, imgs, labs, warmup=1)
+    a2.copy_(arena)
+    eng.step_graph()
+    torch.cuda.synchronize()
+    assert torch.equal(eng.grads, eager)
+
+
+def test_eval_counts_correct(setup):
+    model, layout, arena, eng, x, y = setup
+    n = 64
+    imgs = torch.randint(0, 256, (n, 32, 32, 3), dtype=torch.uint8, device=DEV)
+    labs = torch.randint(0, 100, (n,), dtype=torch.int32, device=DEV)
+    eng.index.copy_(torch.arange(eng.B, dtype=torch.int32, device=DEV))
+    eng.unpack(arena)
+    eng.evaluate_batch(arena, imgs, labs)
+    torch.cuda.synchronize()
+    assert 0 <= eng.correct.item() <= eng.B

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
 
 // Backward pass 1: per-channel partials of sum(dz), sum(dz*xhat1) [, sum(dz*xhat2)], with
 // dz = g * (o > 0) (ReLU mask from the stored activation) or dz = g.
-// part layout: [gridDim.x][NS][C], NS = 2 or 3.
+// part layout: [PSX_STAT_SLOTS][NS][C] (pre-zeroed, fp32 atomics), NS = 2 or 3.
 template <bool MASK, bool TWO>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g,
                                                             const uint16_t* __restrict__ o,
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
     float acc = 0.f;
     for (int q = 0; q < tpp; ++q) acc += sred[(q * cvec + cgi) * (NS * 8) + sj];
     const int stat = sj >> 3, j = sj & 7;
-    part[((size_t)blockIdx.x * NS + stat) * C + cgi * 8 + j] = acc;
+    atomicAdd(part + ((size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * NS + stat) * C + cgi * 8 + j, acc);
   }
 }
 
@@ -310,7 +310,7 @@ int psx_bn_bwd_reduce(const void* g, const void* o, const void* y1, const float*
   int ppb = (npix + 511) / 512;
   if (ppb < 64) ppb = 64;
   const int T = (npix + ppb - 1) / ppb;
-  if (!part) return T;
+  if (!part) return PSX_STAT_SLOTS;
   const bool mask = o != nullptr, two = y2 != nullptr;
   const size_t lds = 256 * (two ? 3 : 2) * 8 * sizeof(float);
 #define PSX_BBR(M, TW)                                                                                          \
@@ -323,7 +323,7 @@ int psx_bn_bwd_reduce(const void* g, const void* o, const void* y1, const float*
   else PSX_BBR(false, false);
 #undef PSX_BBR
   const int e = (int)hipGetLastError();
-  return e ? -e : T;
+  return e ? -e : PSX_STAT_SLOTS;
 }
 
 int psx_bn_bwd_finalize(const float* part, int T, int NS, int which, int C, float count, const float* gamma,

@@ -13,6 +13,10 @@
 
 #define PSX_DEV __device__ __forceinline__
 
+// Cross-workgroup per-channel reductions (BN statistics, BN backward sums) are accumulated with
+// fp32 atomics into this many slot rows; consumers sum the slots in a fixed order.
+#define PSX_STAT_SLOTS 32
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));

@@ -25,7 +25,7 @@ struct ConvArgs {
   const uint16_t* w;    // weights [OC][Kg]  (bf16, K-contiguous, zero padded to Kg)
   uint16_t* out;        // NHWC [Nb][OH][OW][OC]
   const uint16_t* res;  // optional residual added in the epilogue (same shape as out)
-  float* stats;         // optional BN partials [gridPix][2][OC]
+  float* stats;         // optional BN partial sums [PSX_STAT_SLOTS][2][OC], pre-zeroed
   int Nb, IH, IW, IC;   // IC: power of two, multiple of 8
   int OH, OW, OC;
   int R, S, pad, stride;
@@ -221,10 +221,13 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
         }
     }
     __syncthreads();
+    // fire-and-forget fp32 atomics into one of PSX_STAT_SLOTS slot rows (zeroed once per step);
+    // spreading blocks over slots keeps per-address contention low.
+    float* dst = a.stats + (size_t)(pix_t & (PSX_STAT_SLOTS - 1)) * 2 * a.OC;
     for (int j = tid; j < 2 * BM; j += 256) {
       const int which = j / BM, row = j - which * BM;
       const float v = red[(0 * 2 + which) * BM + row] + red[(1 * 2 + which) * BM + row];
-      a.stats[((size_t)pix_t * 2 + which) * a.OC + oc0 + row] = v;
+      atomicAdd(dst + which * a.OC + oc0 + row, v);
     }
   }
 }
@@ -327,28 +330,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
     const unsigned char* D = sD + cur * 8192;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
+      // element j = 4h+e of lane (g, i) <-> pixel row kk*32 + 16h + 4g + e (same for A and B)
+      const int row0 = kk * 32 + 4 * g + q, row1 = row0 + 16;
       bf16x8 fa[2], fb[2];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int row = kk * 32 + h * 16 + 4 * g + q;  // pixel row supplying elements 4h..4h+3
+      for (int m = 0; m < 2; ++m) {
+        const int col = wm * 32 + m * 16 + 4 * p;  // bf16 column within the 64-col tile
+        const s16x4 lo = tr_read(X, pmaj_off(row0, col >> 3) + ((col & 7) << 1));
+        const s16x4 hi = tr_read(X, pmaj_off(row1, col >> 3) + ((col & 7) << 1));
+        fa[m] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
 #pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          const int col = wm * 32 + m * 16 + 4 * p;  // bf16 column within the 64-col tile
-          const s16x4 v = tr_read(X, pmaj_off(row, col >> 3) + ((col & 7) << 1));
-          fa[m][4 * h + 0] = __builtin_bit_cast(__bf16, v[0]);
-          fa[m][4 * h + 1] = __builtin_bit_cast(__bf16, v[1]);
-          fa[m][4 * h + 2] = __builtin_bit_cast(__bf16, v[2]);
-          fa[m][4 * h + 3] = __builtin_bit_cast(__bf16, v[3]);
-        }
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-          const int col = wn * 32 + n * 16 + 4 * p;
-          const s16x4 v = tr_read(D, pmaj_off(row, col >> 3) + ((col & 7) << 1));
-          fb[n][4 * h + 0] = __builtin_bit_cast(__bf16, v[0]);
-          fb[n][4 * h + 1] = __builtin_bit_cast(__bf16, v[1]);
-          fb[n][4 * h + 2] = __builtin_bit_cast(__bf16, v[2]);
-          fb[n][4 * h + 3] = __builtin_bit_cast(__bf16, v[3]);
-        }
+      for (int n = 0; n < 2; ++n) {
+        const int col = wn * 32 + n * 16 + 4 * p;
+        const s16x4 lo = tr_read(D, pmaj_off(row0, col >> 3) + ((col & 7) << 1));
+        const s16x4 hi = tr_read(D, pmaj_off(row1, col >> 3) + ((col & 7) << 1));
+        fb[n] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
       for (int m = 0; m < 2; ++m)
@@ -374,28 +371,40 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 
 // Sum the split-K partials, permute (oc, r, s, c) -> reference OIHW (oc, c, r, s), drop the
 // channel padding and emit the gradient straight into the wire buffer (fp16 codec or fp32).
+// Block = 4 waves; each lane owns 4 consecutive partial columns (16-byte loads), the waves split
+// the split-K slabs 4 ways (fixed order => deterministic) and combine through LDS.
 template <typename OutT>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int OC,
                                                            int Kg, int Cin, int IC, int R, int S, float scale,
                                                            OutT* __restrict__ out) {
-  const int total = OC * Cin * R * S;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
-    // idx enumerates the OIHW destination
-    const int s_ = idx % S;
-    int t = idx / S;
-    const int r_ = t % R;
-    t /= R;
-    const int c = t % Cin;
-    const int oc = t / Cin;
-    const int k = (r_ * S + s_) * IC + c;
-    float v = 0.f;
-    const float* p = part + (size_t)oc * Kg + k;
-    for (int sp = 0; sp < splits; ++sp) v += p[(size_t)sp * OC * Kg];
-    v *= scale;
+  __shared__ f32x4 red[4][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const size_t slab = (size_t)OC * Kg;
+  const size_t base = (size_t)blockIdx.x * 256 + lane * 4;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  int sp = g;
+  for (; sp + 4 < splits; sp += 8) {
+    acc0 += *reinterpret_cast<const f32x4*>(part + sp * slab + base);
+    acc1 += *reinterpret_cast<const f32x4*>(part + (sp + 4) * slab + base);
+  }
+  if (sp < splits) acc0 += *reinterpret_cast<const f32x4*>(part + sp * slab + base);
+  red[g][lane] = acc0 + acc1;
+  __syncthreads();
+  if (g != 0) return;
+  const f32x4 v = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+  const int RS = R * S;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const size_t idx = base + e;
+    const int oc = (int)(idx / Kg), k = (int)(idx - (size_t)oc * Kg);
+    const int tap = k / IC, c = k - tap * IC;
+    if (tap >= RS || c >= Cin) continue;
+    const float val = v[e] * scale;
+    const size_t o = ((size_t)oc * Cin + c) * RS + tap;
     if constexpr (sizeof(OutT) == 2) {
-      out[idx] = __builtin_bit_cast(uint16_t, (_Float16)v);
+      out[o] = __builtin_bit_cast(uint16_t, (_Float16)val);
     } else {
-      out[idx] = v;
+      out[o] = val;
     }
   }
 }
@@ -446,7 +455,7 @@ static int pick_tile(int OC, int npix) {
 extern "C" {
 
 // Forward conv. x: NHWC [Nb][H][W][IC]; wf: [OC][Kg]; y: NHWC [Nb][P][Q][OC].
-// stats (nullable): BN partial sums [n_pix_tiles][2][OC]; returns n_pix_tiles via *ntiles.
+// stats (nullable, pre-zeroed): BN partial sums [PSX_STAT_SLOTS][2][OC]; *ntiles = PSX_STAT_SLOTS.
 int psx_conv_fwd(const void* x, const void* wf, void* y, float* stats, int Nb, int H, int W, int IC, int OC, int R,
                  int S, int stride, int pad, int Kg, int tile_cfg, int* ntiles, hipStream_t st) {
   ConvArgs a{};
@@ -466,7 +475,8 @@ int psx_conv_fwd(const void* x, const void* wf, void* y, float* stats, int Nb, i
   if (tile_cfg < 0) tile_cfg = pick_tile(OC, a.npix);
   if ((tile_cfg == 1 || tile_cfg == 3) && OC % 128) tile_cfg = (tile_cfg == 1) ? 0 : 2;
   const int BN = (tile_cfg == 0 || tile_cfg == 1) ? 128 : 64;
-  if (ntiles) *ntiles = (a.npix + BN - 1) / BN;
+  if (ntiles) *ntiles = PSX_STAT_SLOTS;
+  (void)BN;
   return dispatch_tile<0, false>(tile_cfg, a, st);
 }
 
@@ -515,9 +525,9 @@ int psx_conv_wgrad(const void* x, const void* dy, float* part, int Nb, int H, in
   if (OC % 64 || Kg % 64) return -2;
   const int tiles = a.n_k_tiles * a.n_oc_tiles;
   if (splits <= 0) {
-    // aim for ~1024 workgroups, at least 8 pixel-steps (512 pixels) per split
-    const int max_splits = (a.npix + 511) / 512;
-    splits = (1024 + tiles - 1) / tiles;
+    // aim for ~512 workgroups (2 per CU), at least 16 pixel-steps (1024 pixels) per split
+    const int max_splits = (a.npix + 1023) / 1024;
+    splits = (512 + tiles - 1) / tiles;
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
   }
@@ -535,9 +545,8 @@ int psx_conv_wgrad(const void* x, const void* dy, float* part, int Nb, int H, in
 
 int psx_wgrad_reduce(const float* part, int splits, int OC, int Kg, int Cin, int IC, int R, int S, float scale,
                      void* out, int out_fp16, hipStream_t st) {
-  const int total = OC * Cin * R * S;
-  int grid = (total + 255) / 256;
-  if (grid > 4096) grid = 4096;
+  if (((long)OC * Kg) % 256) return -2;
+  const int grid = (int)(((long)OC * Kg) / 256);
   if (out_fp16)
     hipLaunchKernelGGL(wgrad_reduce_kernel<uint16_t>, dim3(grid), dim3(256), 0, st, part, splits, OC, Kg, Cin, IC,
                        R, S, scale, (uint16_t*)out);

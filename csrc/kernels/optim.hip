@@ -94,27 +94,45 @@ struct UnpackDesc {
   int OC, Cin, R, S, Cp, Kg, Kgd, pad_;
 };
 
+// One workgroup per (32 oc x 32 c) tile of one conv (blockIdx.y = conv). For every tap the
+// tile goes through LDS so both destination layouts are written with contiguous runs:
+// wf[oc][tap*Cp + c] (c fastest) and wd[c][tap*OC + oc] (oc fastest). Channels c >= Cin of the
+// forward operand are written as zeros; the Kg tail beyond R*S*Cp is zeroed once at allocation.
 __global__ __launch_bounds__(256) void param_unpack_kernel(const float* __restrict__ arena,
                                                            const UnpackDesc* __restrict__ descs,
                                                            uint16_t* __restrict__ wbuf) {
+  __shared__ float tile[32][33];
   const UnpackDesc d = descs[blockIdx.y];
   const float* src = arena + d.src_off;
-  const long nf = (long)d.OC * d.Kg;
-  const long nd = d.wd_off >= 0 ? (long)d.Cp * d.Kgd : 0;
   const int RS = d.R * d.S;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nf + nd; i += (long)gridDim.x * blockDim.x) {
-    float v = 0.f;
-    if (i < nf) {
-      const int oc = (int)(i / d.Kg), k = (int)(i - (long)oc * d.Kg);
-      const int tap = k / d.Cp, c = k - tap * d.Cp;
-      if (tap < RS && c < d.Cin) v = src[((size_t)oc * d.Cin + c) * RS + tap];
-      wbuf[d.wf_off + i] = f2bf(v);
-    } else {
-      const long j = i - nf;
-      const int c = (int)(j / d.Kgd), k = (int)(j - (long)c * d.Kgd);
-      const int tap = k / d.OC, oc = k - tap * d.OC;
-      if (tap < RS && c < d.Cin) v = src[((size_t)oc * d.Cin + c) * RS + tap];
-      wbuf[d.wd_off + j] = f2bf(v);
+  const int n_oc = (d.OC + 31) / 32, n_c = (d.Cp + 31) / 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int t = blockIdx.x; t < n_oc * n_c; t += gridDim.x) {
+    const int oc0 = (t / n_c) * 32, c0 = (t % n_c) * 32;
+    for (int tap = 0; tap < RS; ++tap) {
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // tile[oc][c] = W[oc0+oc][c0+c][tap]
+        const int oc = ty + 8 * j, c = tx;
+        float v = 0.f;
+        if (oc0 + oc < d.OC && c0 + c < d.Cin) v = src[((size_t)(oc0 + oc) * d.Cin + (c0 + c)) * RS + tap];
+        tile[oc][c] = v;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int oc = ty + 8 * j, c = tx;  // wf: c contiguous
+        if (oc0 + oc < d.OC && c0 + c < d.Cp)
+          wbuf[d.wf_off + (size_t)(oc0 + oc) * d.Kg + tap * d.Cp + c0 + c] = f2bf(tile[oc][c]);
+      }
+      if (d.wd_off >= 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = ty + 8 * j, oc = tx;  // wd: oc contiguous
+          if (oc0 + oc < d.OC && c0 + c < d.Cp)
+            wbuf[d.wd_off + (size_t)(c0 + c) * d.Kgd + tap * d.OC + oc0 + oc] = f2bf(tile[oc][c]);
+        }
+      }
     }
   }
 }
@@ -188,7 +206,7 @@ int psx_fp16_unpack(const void* src, float* dst, long n, float scale, hipStream_
 
 // descs: device array of ndesc UnpackDesc (see struct layout above: 3 int64 + 8 int32)
 int psx_param_unpack(const float* arena, const void* descs, int ndesc, void* wbuf, hipStream_t st) {
-  hipLaunchKernelGGL(param_unpack_kernel, dim3(256, ndesc), dim3(256), 0, st, arena, (const UnpackDesc*)descs,
+  hipLaunchKernelGGL(param_unpack_kernel, dim3(64, ndesc), dim3(256), 0, st, arena, (const UnpackDesc*)descs,
                      (uint16_t*)wbuf);
   return (int)hipGetLastError();
 }

@@ -213,9 +213,18 @@ class HipResNetEngine:
         # per-BN persistent state: affine [2,C] (scale, shift), saved [2,C] (mean, invstd), coef [3,C]
         self.bn = {}
 
+        # Cross-workgroup reductions (BN fwd statistics from the conv epilogue, BN bwd sums) use
+        # fp32 atomics into PSX_STAT_SLOTS slot rows per BN layer; all slot rows live in one
+        # buffer that is zeroed once at the start of every step (one memset node in the graph).
+        self.nslots = K.bn_bwd_reduce_T(1, 64)
+        red_off = [0]
+
         def bn_state(bs: BNSpec):
+            fwd = red_off[0]
+            bwd = fwd + self.nslots * 2 * bs.c
+            red_off[0] = bwd + self.nslots * 3 * bs.c
             self.bn[bs.name] = dict(affine=self._f32(2, bs.c), saved=self._f32(2, bs.c), coef=self._f32(3, bs.c),
-                                    c=bs.c)
+                                    c=bs.c, fwd=(fwd, self.nslots * 2 * bs.c), bwd=(bwd, self.nslots * 3 * bs.c))
 
         # activation / gradient buffers
         st = sp.stem_conv
@@ -225,20 +234,13 @@ class HipResNetEngine:
         self.g0 = self._bf(B, p, q, st.cout)   # grad wrt a0 (or wrt maxpool input)
         self.dy0 = self._bf(B, p, q, st.cout)
         bn_state(sp.stem_bn)
-        max_stats = 2 * st.cout * K.conv_fwd_ntiles(st.cout, B * p * q, K.pick_tile(st.cout, B * p * q))
-        max_bnp = 0
         max_wg = 0
 
         def track(cs: ConvSpec):
-            nonlocal max_stats, max_wg, max_bnp
-            oh, ow = cs.out_hw
-            npix = B * oh * ow
-            cfg = K.pick_tile(cs.cout, npix)
-            max_stats = max(max_stats, 2 * cs.cout * K.conv_fwd_ntiles(cs.cout, npix, cfg))
+            nonlocal max_wg
             s = K.conv_wgrad_splits(B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
             cs.splits = s
             max_wg = max(max_wg, s * cs.cout * cs.kg)
-            max_bnp = max(max_bnp, 3 * cs.cout * K.bn_bwd_reduce_T(npix, cs.cout))
 
         track(st)
         if sp.maxpool:
@@ -270,9 +272,8 @@ class HipResNetEngine:
             self.blk.append(d)
             h_in = d["out"]
         self.final = h_in
-        self.stats = self._f32(max_stats)
+        self.red = self._f32(red_off[0])
         self.wpart = self._f32(max_wg)
-        self.bnpart = self._f32(max(max_bnp, 1))
         # head
         fh, fw = self.final.shape[1], self.final.shape[2]
         self.head_hw = fh * fw
@@ -291,18 +292,22 @@ class HipResNetEngine:
     def _aview(self, arena, name):
         return self.layout.view(arena, name)
 
-    def _conv_fwd(self, cs: ConvSpec, x, y, stats=True):
+    def _red(self, bs: BNSpec, which: str):
+        off, n = self.bn[bs.name][which]
+        return self.red[off:off + n]
+
+    def _conv_fwd(self, cs: ConvSpec, x, y, bs: BNSpec | None):
         oh, ow = cs.out_hw
         npix = self.B * oh * ow
         cfg = K.pick_tile(cs.cout, npix)
         wf = self.wbuf[cs.wf_off:cs.wf_off + cs.cout * cs.kg]
-        K.conv_fwd(x, wf, y, self.stats if stats else None, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride,
-                   cs.pad, cs.kg, cfg)
-        return K.conv_fwd_ntiles(cs.cout, npix, cfg), npix
+        K.conv_fwd(x, wf, y, self._red(bs, "fwd") if bs is not None else None, self.B, cs.h, cs.w, cs.cp, cs.cout,
+                   cs.k, cs.stride, cs.pad, cs.kg, cfg)
+        return self.nslots, npix
 
     def _bn_train(self, bs: BNSpec, arena, T, count):
         st = self.bn[bs.name]
-        K.bn_finalize(self.stats, T, bs.c, count, self._aview(arena, f"{bs.name}.weight"),
+        K.bn_finalize(self._red(bs, "fwd"), T, bs.c, count, self._aview(arena, f"{bs.name}.weight"),
                       self._aview(arena, f"{bs.name}.bias"), self.eps, self.mom,
                       self._aview(arena, f"{bs.name}.running_mean"), self._aview(arena, f"{bs.name}.running_var"),
                       st["affine"], st["saved"])
@@ -325,20 +330,21 @@ class HipResNetEngine:
     def _bn_bwd(self, bs: BNSpec, arena, g, o, y, dx, npix, two=None, dzout=None):
         """BN (+ReLU mask from o) backward; two = (bs2, y2, dx2) for a shared-dz second BN."""
         st = self.bn[bs.name]
+        part = self._red(bs, "bwd")
         if two is None:
-            T = K.bn_bwd_reduce(g, o, y, st["saved"], self.bnpart, npix, bs.c)
-            K.bn_bwd_finalize(self.bnpart, T, 2, 1, bs.c, npix, self._aview(arena, f"{bs.name}.weight"),
+            T = K.bn_bwd_reduce(g, o, y, st["saved"], part, npix, bs.c)
+            K.bn_bwd_finalize(part, T, 2, 1, bs.c, npix, self._aview(arena, f"{bs.name}.weight"),
                               st["saved"], st["coef"], self._gptr(f"{bs.name}.weight"),
                               self._gptr(f"{bs.name}.bias"), 1.0, self.grad_fp16)
             K.bn_bwd_apply(g, o, y, st["coef"], dx, bs.c, dzout=dzout)
         else:
             bs2, y2, dx2 = two
             st2 = self.bn[bs2.name]
-            T = K.bn_bwd_reduce(g, o, y, st["saved"], self.bnpart, npix, bs.c, y2=y2, saved2=st2["saved"])
-            K.bn_bwd_finalize(self.bnpart, T, 3, 1, bs.c, npix, self._aview(arena, f"{bs.name}.weight"),
+            T = K.bn_bwd_reduce(g, o, y, st["saved"], part, npix, bs.c, y2=y2, saved2=st2["saved"])
+            K.bn_bwd_finalize(part, T, 3, 1, bs.c, npix, self._aview(arena, f"{bs.name}.weight"),
                               st["saved"], st["coef"], self._gptr(f"{bs.name}.weight"),
                               self._gptr(f"{bs.name}.bias"), 1.0, self.grad_fp16)
-            K.bn_bwd_finalize(self.bnpart, T, 3, 2, bs2.c, npix, self._aview(arena, f"{bs2.name}.weight"),
+            K.bn_bwd_finalize(part, T, 3, 2, bs2.c, npix, self._aview(arena, f"{bs2.name}.weight"),
                               st2["saved"], st2["coef"], self._gptr(f"{bs2.name}.weight"),
                               self._gptr(f"{bs2.name}.bias"), 1.0, self.grad_fp16)
             K.bn_bwd_apply(g, o, y, st["coef"], dx, bs.c, y2=y2, coef2=st2["coef"], dx2=dx2, dzout=dzout)
@@ -357,7 +363,9 @@ class HipResNetEngine:
     def forward(self, arena: torch.Tensor, train: bool = True):
         sp, B = self.spec, self.B
         st = sp.stem_conv
-        T, npix = self._conv_fwd(st, self.x0, self.y0, stats=train)
+        if train:
+            self.red.zero_()
+        T, npix = self._conv_fwd(st, self.x0, self.y0, sp.stem_bn if train else None)
         if train:
             self._bn_train(sp.stem_bn, arena, T, npix)
         else:
@@ -367,7 +375,7 @@ class HipResNetEngine:
             src = d["inp"]
             L = len(b.convs)
             for i, cs in enumerate(b.convs):
-                T, npix = self._conv_fwd(cs, src, d["y"][i], stats=train)
+                T, npix = self._conv_fwd(cs, src, d["y"][i], b.bns[i] if train else None)
                 (self._bn_train(b.bns[i], arena, T, npix) if train else self._bn_eval(b.bns[i], arena))
                 if i < L - 1:
                     K.bn_apply(d["y"][i], self.bn[b.bns[i].name]["affine"], d["a"][i], cs.cout, relu=True)
@@ -376,7 +384,7 @@ class HipResNetEngine:
             aff = self.bn[b.bns[-1].name]["affine"]
             if b.down:
                 ds, dbn = b.down
-                T, npix = self._conv_fwd(ds, d["inp"], d["ys"], stats=train)
+                T, npix = self._conv_fwd(ds, d["inp"], d["ys"], dbn if train else None)
                 (self._bn_train(dbn, arena, T, npix) if train else self._bn_eval(dbn, arena))
                 K.bn_apply(d["y"][-1], aff, d["out"], last.cout, relu=True, res=d["ys"],
                            affine2=self.bn[dbn.name]["affine"])

@@ -33,8 +33,12 @@ def conv_out_hw(h: int, w: int, k: int, stride: int, pad: int):
     return (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
 
 
+STAT_SLOTS = 32  # PSX_STAT_SLOTS in csrc/kernels/common.hpp
+
+
 def conv_fwd_ntiles(oc: int, npix: int, cfg: int) -> int:
-    return -(-npix // TILE_CFGS[cfg][1])
+    """Rows of the BN-statistics slab the conv epilogue accumulates into (pre-zeroed)."""
+    return STAT_SLOTS
 
 
 def conv_fwd(x, wf, y, stats, nb, h, w, ic, oc, k, stride, pad, kg, cfg=None):

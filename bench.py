@@ -1,0 +1,162 @@
+#!/usr/bin/env python3
+"""Headline benchmark: images/sec (whole node) of ResNet-18 / CIFAR-100-shaped data in the
+synchronous parameter-server mode on 1..8 MI355X (BASELINE.json metric).
+
+  python bench.py                                   # N=1: server + worker co-located, loopback
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \\
+      --master-port 29500 bench.py --gpus 8 --steps 50 --warmup 10
+
+One step = fetch (RCCL broadcast of the fp32 parameter arena from rank 0) -> batch gather +
+augment -> forward/backward on the HIP engine (hand-written CDNA4 kernels, one HIP graph) ->
+push (RCCL reduce of the fp16 wire gradients to rank 0) -> fused SGD apply of the average on
+rank 0. Batch 128 per worker, lr 0.1, sync period 1 (the reference's CLI defaults). Weak
+scaling: every rank is a worker (rank 0 also hosts the parameter server, ``--topology
+colocated``); ``--topology dedicated`` reproduces the reference's 1 server + (N-1) workers.
+W warmup steps are untimed; exactly K steps are timed between barrier+synchronize pairs and
+the max over ranks is reported. Data is synthetic CIFAR-100-shaped (no network access), weights
+random-init.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import psx  # noqa: E402,F401
+from psx.parallel.compute import HipCompute  # noqa: E402
+from psx.parallel.runner import build_state, make_datasets  # noqa: E402
+from psx.parallel.server import ParameterServer  # noqa: E402
+from psx.parallel.transport import DistTransport, env_world  # noqa: E402
+from psx.parallel.worker import InProcessChannel, SyncCollectiveChannel, Worker  # noqa: E402
+from psx.utils.config import PSConfig  # noqa: E402
+
+BASELINE_SYNC_IMG_S = 82.7  # sync PS, 4 workers, measured (experiment_results/sync_4workers.json)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--topology", choices=["colocated", "dedicated"], default="colocated")
+    ap.add_argument("--codec", choices=["fp16", "none"], default="fp16")
+    ap.add_argument("--no-graph", action="store_true")
+    a = ap.parse_args()
+
+    rank, world, local = env_world()
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs MI355X GPUs")
+    torch.cuda.set_device(local % torch.cuda.device_count())
+    device = torch.device("cuda", torch.cuda.current_device())
+    cfg = PSConfig(mode="sync", model="resnet18", batch_size=a.batch, lr=0.1, sync_steps=1, epochs=1,
+                   eval_every=0, verbose=0, codec=a.codec, use_graph=not a.no_graph).validate()
+    model, layout, arena, counters = build_state(cfg)
+    wire = torch.float16 if a.codec == "fp16" else torch.float32
+
+    t = None
+    force_dist = os.environ.get("PSX_FORCE_DIST", "0") == "1"  # exercise the RCCL path even at N=1
+    if world > 1 or force_dist:
+        t = DistTransport(device=device)
+    dedicated = a.topology == "dedicated" and world > 1
+    worker_ranks = list(range(1, world)) if dedicated else list(range(world))
+    W = len(worker_ranks)
+    cfg.workers = W
+    is_worker = rank in worker_ranks
+    server = None
+    if rank == 0:
+        server = ParameterServer(cfg, layout, arena, counters, device=device, total_workers=W, log=lambda *x: None)
+        for i in range(W):
+            server.register_worker(f"worker-{i}", i)
+    train, _ = make_datasets(cfg, device, model.fc.out_features)
+    chan = InProcessChannel(server) if t is None else SyncCollectiveChannel(t, server, members=list(range(W)))
+    wk = None
+    zeros = None
+    if is_worker:
+        comp = HipCompute(model, layout, a.batch, device, "resnet18", wire, seed=rank, use_graph=cfg.use_graph)
+        wid = worker_ranks.index(rank)
+        wk = Worker(cfg, comp, chan, train, None, worker_name=f"worker-{wid}", rank=rank, log=lambda *x: None,
+                    requested_id=wid)
+        wk.connect_to_server()
+        wk.setup_data()
+        batches = wk.sampler.epoch_indices(0)
+    else:
+        zeros = torch.zeros(layout.param_numel, dtype=wire, device=device)
+
+    def step(i):
+        if wk is not None:
+            wk.fetch_parameters()
+            wk.train_local_batch(batches[i % len(batches)])
+            wk.push_gradients()
+        else:  # dedicated server rank
+            chan.fetch(None, None)
+            zeros.zero_()
+            chan.push(None, zeros, server.core.global_step)
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        if t is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(a.warmup):
+        step(i)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(a.warmup + i)
+    barrier_sync()
+    dt = time.perf_counter() - t0
+    if t is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    imgs = a.steps * a.batch * W
+    value = imgs / dt
+    loss = wk.compute.last_loss() if wk is not None else None
+    if rank == 0:
+        rec = {
+            "metric": "images/sec (whole node) ResNet-18 sync-PS at 1/2/4/8 MI355X; async staleness",
+            "value": round(value, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1e3 * dt / a.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_SYNC_IMG_S, 2),
+            "dtype": "bf16",
+            "data": "synthetic CIFAR-100-shaped (50000x32x32x3 uint8 in HBM, on-device crop/flip/normalize), "
+                    "random-init weights",
+            "config": {
+                "model": "resnet18-cifar (11,220,132 params, reference ResNet18(num_classes=100))",
+                "global_batch": a.batch * W,
+                "per_worker_batch": a.batch,
+                "seq_len": None,
+                "parallelism": (f"sync-PS: rank0 = parameter server{' only' if dedicated else ' + worker 0'}, "
+                                f"{W} data-parallel worker(s); RCCL reduce(fp16 grads)+broadcast(fp32 arena) "
+                                f"over xGMI" if world > 1 else "sync-PS: server + 1 worker co-located on 1 GPU"),
+                "lr": 0.1,
+                "sync_steps": 1,
+                "codec": a.codec,
+                "topology": "dedicated" if dedicated else ("colocated" if world > 1 else "loopback"),
+                "hip_graph": cfg.use_graph,
+            },
+            "global_steps": server.core.global_step,
+            "last_loss": round(loss, 4) if loss is not None else None,
+            "baseline_img_s": BASELINE_SYNC_IMG_S,
+        }
+        print(json.dumps(rec), flush=True)
+    if t is not None:
+        t.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -21,15 +21,17 @@ PSX_DEV uint32_t hash32(uint32_t x) {
 PSX_DEV uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) { return hash32(a ^ hash32(b ^ hash32(c + 0x9e3779b9u))); }
 
 // images: [N][H][W][3] uint8, labels: [N] int32. Class prototypes are low-frequency colour
-// patterns; each sample = prototype + per-pixel noise, so the task is learnable.
+// patterns fixed by `seed`; each sample = prototype + per-pixel noise, so the task is learnable.
+// `offset` selects a disjoint sample range (train set offset 0, test set a large offset) over
+// the same class prototypes.
 __global__ void synth_gen_kernel(uint8_t* __restrict__ img, int* __restrict__ labels, int N, int H, int W,
-                                 int classes, uint32_t seed) {
+                                 int classes, uint32_t seed, uint32_t offset) {
   const long total = (long)N * H * W;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int n = (int)(i / (H * W));
     const int hw = (int)(i - (long)n * H * W);
     const int h = hw / W, w = hw - (hw / W) * W;
-    const int y = (int)(hash3(seed, (uint32_t)n, 77u) % (uint32_t)classes);
+    const int y = (int)(hash3(seed, (uint32_t)n + offset, 77u) % (uint32_t)classes);
     if (hw == 0) labels[n] = y;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
@@ -38,7 +40,7 @@ __global__ void synth_gen_kernel(uint8_t* __restrict__ img, int* __restrict__ la
       const int fx = 1 + (hp & 3), fy = 1 + ((hp >> 2) & 3), ph = (hp >> 4) & 31;
       const int tri_x = ((h * fx + ph) & 31), tri_y = ((w * fy + (ph >> 1)) & 31);
       const int proto = ((tri_x < 16 ? tri_x : 31 - tri_x) + (tri_y < 16 ? tri_y : 31 - tri_y)) * 8;  // 0..240
-      const int noise = (int)(hash3(seed, (uint32_t)i, (uint32_t)c) & 63) - 32;
+      const int noise = (int)(hash3(seed + offset, (uint32_t)i, (uint32_t)c) & 63) - 32;
       int v = proto + noise;
       v = v < 0 ? 0 : (v > 255 ? 255 : v);
       img[i * 3 + c] = (uint8_t)v;
@@ -115,12 +117,13 @@ using namespace psx;
 
 extern "C" {
 
-int psx_synth_gen(void* img, int* labels, int N, int H, int W, int classes, unsigned seed, hipStream_t st) {
+int psx_synth_gen(void* img, int* labels, int N, int H, int W, int classes, unsigned seed, unsigned offset,
+                  hipStream_t st) {
   long total = (long)N * H * W;
   long g = (total + 255) / 256;
   if (g > 8192) g = 8192;
   hipLaunchKernelGGL(synth_gen_kernel, dim3((unsigned)g), dim3(256), 0, st, (uint8_t*)img, labels, N, H, W, classes,
-                     (uint32_t)seed);
+                     (uint32_t)seed, (uint32_t)offset);
   return (int)hipGetLastError();
 }
 

@@ -115,10 +115,26 @@ class ResNet50(nn.Module):
         return self.fc(torch.flatten(self.avgpool(x), 1))
 
 
-MODELS = {"resnet18": ResNet18, "resnet50": ResNet50}
+class TinyResNet(ResNet18):
+    """Same module names/structure family as ResNet18 (one BasicBlock per stage, widths
+    8/16/32/64) — a seconds-per-step model for the CPU test-suite only."""
+
+    def __init__(self, num_classes: int = 10):
+        nn.Module.__init__(self)
+        self.conv1 = nn.Conv2d(3, 8, 3, 1, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(8)
+        cin = 8
+        for i, (w, s) in enumerate(zip((8, 16, 32, 64), (1, 2, 2, 2))):
+            setattr(self, f"layer{i + 1}", nn.Sequential(BasicBlock(cin, w, s)))
+            cin = w
+        self.avg_pool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(64, num_classes)
+
+
+MODELS = {"resnet18": ResNet18, "resnet50": ResNet50, "resnet_tiny": TinyResNet}
 
 # input geometry per model: (channels, height, width), default classes
-MODEL_INPUT = {"resnet18": ((3, 32, 32), 100), "resnet50": ((3, 224, 224), 1000)}
+MODEL_INPUT = {"resnet18": ((3, 32, 32), 100), "resnet50": ((3, 224, 224), 1000), "resnet_tiny": ((3, 32, 32), 10)}
 
 
 def build_model(name: str, num_classes: int | None = None, seed: int | None = 0) -> nn.Module:

@@ -162,9 +162,9 @@ def unpack_desc_size() -> int:
     return kernels().psx_unpack_desc_size()
 
 
-def synth_gen(img, labels, n, h, w, classes, seed):
-    check(kernels().psx_synth_gen(ptr(img), ptr(labels), n, h, w, classes, seed & 0xFFFFFFFF, stream_ptr()),
-          "synth_gen")
+def synth_gen(img, labels, n, h, w, classes, seed, offset=0):
+    check(kernels().psx_synth_gen(ptr(img), ptr(labels), n, h, w, classes, seed & 0xFFFFFFFF, offset & 0xFFFFFFFF,
+                                  stream_ptr()), "synth_gen")
 
 
 _F3 = C.c_float * 3

@@ -1,0 +1,181 @@
+"""Worker compute backends: produce the flat wire gradient of one local batch.
+
+* ``HipCompute``   — the MI355X path: models/engine.py (hand-written CDNA4 kernels), whole step
+                     captured in a HIP graph; parameters come from the worker-local fp32 arena.
+* ``TorchCompute`` — the CPU reference path (torch nn.Module + autograd), used by the CPU
+                     test-suite and for numerics checks. It is never selected on a GPU device.
+
+Both expose the same surface: ``local_arena`` (fetched server state, fp32), ``grads`` (wire
+buffer over the trainable-parameter prefix, fp16 codec or fp32), ``train_step(indices)``,
+``evaluate(dataset)`` and ``last_loss()``. This replaces the reference's
+setup_model/train_local_batch/evaluate_model (src/workers/worker.py:128-138,313-348).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ..models.layout import ParamLayout
+from ..models.resnet import MODEL_INPUT
+
+
+class TorchCompute:
+    def __init__(self, model: torch.nn.Module, layout: ParamLayout, batch: int, grad_dtype=torch.float16,
+                 mean=(0.5071, 0.4867, 0.4408), std=(0.2675, 0.2565, 0.2761), seed: int = 0):
+        self.model = model.cpu()
+        self.layout = layout
+        self.B = batch
+        self.device = torch.device("cpu")
+        self.local_arena = torch.zeros(layout.arena_numel, dtype=torch.float32)
+        self.grads = torch.zeros(layout.param_numel, dtype=grad_dtype)
+        self.mean = torch.tensor(mean).view(1, 3, 1, 1)
+        self.std = torch.tensor(std).view(1, 3, 1, 1)
+        self._loss = 0.0
+        self._step = 0
+        self.seed = seed
+
+    # arena <-> module
+    def _load_module(self):
+        with torch.no_grad():
+            sd = self.model.state_dict()
+            for name, e in self.layout.entries.items():
+                if e.region == "counter":
+                    continue
+                sd[name].copy_(self.local_arena[e.offset:e.offset + e.numel].view(e.shape))
+
+    def _store_buffers(self):
+        with torch.no_grad():
+            sd = self.model.state_dict()
+            for name, e in self.layout.entries.items():
+                if e.region == "buffer":
+                    self.local_arena[e.offset:e.offset + e.numel] = sd[name].reshape(-1)
+
+    def _batch(self, dataset, idx, train=True):
+        x = dataset.images[torch.as_tensor(idx, dtype=torch.long)].permute(0, 3, 1, 2).float() / 255.0
+        if train:
+            rng = np.random.default_rng([self.seed, self._step])
+            xp = F.pad(x, (4, 4, 4, 4))
+            out = torch.empty_like(x)
+            for i in range(x.shape[0]):
+                dy, dx = rng.integers(0, 9, size=2)
+                crop = xp[i, :, dy:dy + x.shape[2], dx:dx + x.shape[3]]
+                out[i] = crop.flip(2) if rng.integers(0, 2) else crop
+            x = out
+        x = (x - self.mean) / self.std
+        y = dataset.labels[torch.as_tensor(idx, dtype=torch.long)].long()
+        return x, y
+
+    def train_step(self, dataset, idx):
+        self._load_module()
+        self.model.train()
+        self.model.zero_grad(set_to_none=False)
+        x, y = self._batch(dataset, idx, train=True)
+        loss = F.cross_entropy(self.model(x), y)
+        loss.backward()
+        self._loss = loss.item()
+        with torch.no_grad():
+            for name, p in self.model.named_parameters():
+                e = self.layout.entries[name]
+                self.grads[e.offset:e.offset + e.numel] = p.grad.reshape(-1).to(self.grads.dtype)
+        self._store_buffers()
+        self._step += 1
+
+    def last_loss(self) -> float:
+        return self._loss
+
+    @torch.no_grad()
+    def evaluate(self, dataset, batch=None) -> float:
+        self._load_module()
+        self.model.eval()
+        b = batch or self.B
+        correct = 0
+        n = len(dataset)
+        for s in range(0, n, b):
+            idx = np.arange(s, min(n, s + b))
+            x, y = self._batch(dataset, idx, train=False)
+            correct += int((self.model(x).argmax(1) == y).sum())
+        return 100.0 * correct / max(1, n)
+
+
+class HipCompute:
+    def __init__(self, model: torch.nn.Module, layout: ParamLayout, batch: int, device, model_name="resnet18",
+                 grad_dtype=torch.float16, seed: int = 0, use_graph: bool = True):
+        from ..models.engine import CIFAR_MEAN, CIFAR_STD, IMAGENET_MEAN, IMAGENET_STD, HipResNetEngine
+
+        (c, h, w), _ = MODEL_INPUT.get(model_name, ((3, 32, 32), 100))
+        mean, std = (CIFAR_MEAN, CIFAR_STD) if h == 32 else (IMAGENET_MEAN, IMAGENET_STD)
+        self.device = torch.device(device)
+        self.layout = layout
+        self.B = batch
+        self.engine = HipResNetEngine(model, layout, batch, device=self.device, grad_dtype=grad_dtype, in_hw=(h, w),
+                                      mean=mean, std=std, seed=1234 + seed)
+        self.local_arena = torch.zeros(layout.arena_numel, dtype=torch.float32, device=self.device)
+        self.grads = self.engine.grads
+        self.use_graph = use_graph
+        self._dataset = None
+        self._step = 0
+        self._idx_host = torch.zeros(batch, dtype=torch.int32).pin_memory()
+
+    def _set_batch(self, idx):
+        self._idx_host.copy_(torch.as_tensor(idx, dtype=torch.int32))
+        self.engine.index.copy_(self._idx_host, non_blocking=True)
+        self.engine.step_dev.fill_(self._step)
+
+    def train_step(self, dataset, idx):
+        self._set_batch(idx)
+        if self.use_graph:
+            if self.engine.graph is None or self._dataset is not dataset:
+                # One-time capture of unpack + augment + fwd + bwd over the fixed local arena
+                # (fetches land in it in place). Warm-up/capture side effects on the BN running
+                # statistics are undone so the first replay starts from the fetched state.
+                self._dataset = dataset
+                backup = self.local_arena.clone()
+                self.engine.capture(self.local_arena, dataset.images, dataset.labels, unpack=True, warmup=1)
+                self.local_arena.copy_(backup)
+                del backup
+            self.engine.step_graph()
+        else:
+            self.engine.train_step(self.local_arena, dataset.images, dataset.labels, unpack=True)
+        self._step += 1
+
+    def last_loss(self) -> float:
+        return float(self.engine.loss.mean())
+
+    @torch.no_grad()
+    def evaluate(self, dataset, batch=None) -> float:
+        n = len(dataset)
+        B = self.B
+        correct = 0
+        self.engine.unpack(self.local_arena)
+        for s in range(0, n, B):
+            idx = np.arange(s, s + B) % n
+            self._set_batch(idx)
+            self.engine.evaluate_batch(self.local_arena, dataset.images, dataset.labels)
+            valid = min(B, n - s)
+            if valid == B:
+                correct += int(self.engine.correct.item())
+            else:  # partial last batch: recount only the valid rows
+                logits_ok = self._count_prefix(valid)
+                correct += logits_ok
+        return 100.0 * correct / max(1, n)
+
+    def _count_prefix(self, valid: int) -> int:
+        # re-run the head on the first `valid` samples only
+        from ..ops import kernels as K
+
+        sp = self.engine.spec
+        self.engine.correct.zero_()
+        K.head_fwd_bwd(self.engine.final, valid, self.engine.head_hw, sp.fc_in,
+                       self.layout.view(self.local_arena, f"{sp.fc}.weight"),
+                       self.layout.view(self.local_arena, f"{sp.fc}.bias"), sp.classes, self.engine.labels,
+                       self.engine.pooled, self.engine.dlogits, None, self.engine.loss, self.engine.correct)
+        return int(self.engine.correct.item())
+
+
+def make_compute(model, layout, batch, device, model_name="resnet18", grad_dtype=torch.float16, seed=0,
+                 use_graph=True):
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        return HipCompute(model, layout, batch, dev, model_name, grad_dtype, seed, use_graph)
+    return TorchCompute(model, layout, batch, grad_dtype, seed=seed)

@@ -1,0 +1,274 @@
+"""Job orchestration: one process per GPU (torchrun-style env) or a single loopback process.
+
+Replaces the reference's deployment (one gRPC server container + N worker containers,
+reference: terraform/main.tf:387-435, server.py:370-433, worker.py:455-506) with a single-node
+layout on MI355X:
+
+* ``world_size == 1``: the parameter server and ``--workers`` simulated workers share one
+  GPU in one process (loopback): sync rounds aggregate in HBM, async pushes interleave
+  round-robin so staleness reaches W-1 like W concurrent workers;
+* ``world_size > 1``: RCCL over xGMI. Topology ``colocated`` (default): rank 0 hosts the PS
+  state *and* worker 0, ranks 1..N-1 are workers (W = N); ``dedicated``: rank 0 is only the
+  PS (W = N-1), the reference's server/worker split.
+  - sync:  every step is fetch (RCCL broadcast) -> fwd/bwd -> push (RCCL reduce to rank 0 ->
+    fused SGD apply of the average);
+  - async: workers talk to the rank-0 server event loop (shared-memory mailbox for control,
+    RCCL send/recv for tensors); the co-located worker of rank 0 runs next to the server loop.
+"""
+from __future__ import annotations
+
+import os
+import queue
+import threading
+import time
+import uuid
+
+import torch
+
+from ..models.layout import ParamLayout
+from ..models.resnet import MODEL_INPUT, build_model
+from ..utils import metrics as M
+from ..utils.data import DeviceDataset, shard_range, steps_per_epoch
+from . import control as CP
+from .compute import make_compute
+from .server import ParameterServer
+from .transport import DistTransport, LocalTransport, env_world
+from .worker import (AsyncChannel, InProcessChannel, LocalAsyncChannel, SyncCollectiveChannel, Worker)
+
+
+def _device_for(local_rank: int):
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_rank % torch.cuda.device_count())
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def _wire_dtype(cfg):
+    return torch.float32 if cfg.codec == "none" else torch.float16
+
+
+def build_state(cfg):
+    model = build_model(cfg.model, cfg.num_classes, seed=cfg.seed)
+    layout = ParamLayout.from_module(model)
+    arena, counters = layout.pack(model)
+    return model, layout, arena, counters
+
+
+def make_datasets(cfg, device, classes):
+    (_, h, _), _ = MODEL_INPUT[cfg.model]
+    if cfg.data_dir:
+        tr = os.path.join(cfg.data_dir, "train.bin")
+        te = os.path.join(cfg.data_dir, "test.bin")
+        train = DeviceDataset.cifar_binary(tr, max_records=cfg.train_samples, device=device)
+        test = DeviceDataset.cifar_binary(te, max_records=cfg.test_samples, device=device) if os.path.exists(te) else None
+        return train, test
+    train = DeviceDataset.synthetic(cfg.train_samples, h, classes, seed=cfg.seed, device=device)
+    test = None
+    if cfg.eval_every and cfg.test_samples:
+        test = DeviceDataset.synthetic(cfg.test_samples, h, classes, seed=cfg.seed, device=device, offset=10_000_000)
+    return train, test
+
+
+def _common_steps(cfg, W, n):
+    return max(steps_per_epoch(e - s, cfg.batch_size) for s, e in (shard_range(w, W, n) for w in range(W)))
+
+
+# ---------------------------------------------------------------------------- loopback
+def run_local(cfg, log=print) -> dict:
+    device = _device_for(0)
+    W = cfg.workers
+    model, layout, arena, counters = build_state(cfg)
+    classes = model.fc.out_features
+    server = ParameterServer(cfg, layout, arena, counters, device=device, total_workers=W, log=log)
+    train, test = make_datasets(cfg, device, classes)
+    workers = []
+    for w in range(W):
+        m = model if w == 0 else build_model(cfg.model, cfg.num_classes, seed=cfg.seed)
+        comp = make_compute(m, layout, cfg.batch_size, device, cfg.model, _wire_dtype(cfg), seed=cfg.seed + w,
+                            use_graph=cfg.use_graph)
+        wk = Worker(cfg, comp, InProcessChannel(server), train, test, worker_name=f"{cfg.worker_name}-{w}", rank=0,
+                    log=log, requested_id=w, steps_per_epoch=_common_steps(cfg, W, len(train)))
+        wk.connect_to_server()
+        wk.setup_data()
+        workers.append(wk)
+    t0 = time.time()
+    if W == 1:
+        workers[0].run_training()
+    else:
+        _interleave(cfg, workers, server, log)
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    wall = time.time() - t0
+    imgs = sum(w.images for w in workers)
+    extra = {"images_per_second": round(imgs / wall, 2) if wall > 0 else 0.0, "gpus": 1, "topology": "loopback"}
+    sm = server.final_metrics(emit=True, extra=extra)
+    return {"server": sm, "workers": [getattr(w, "final_metrics", None) for w in workers]}
+
+
+def _interleave(cfg, workers, server, log):
+    """W simulated workers on one device. Sync: every worker fetches the same version, the last
+    push of a round triggers the averaged update. Async: pipelined round-robin (each worker
+    pushes gradients computed W-1 updates ago, then fetches), i.e. W equal-speed concurrent
+    workers."""
+    K = max(1, cfg.sync_steps)
+    for wk in workers:
+        wk.training_start_time = time.time()
+    steps = len(workers[0].sampler)
+    for epoch in range(cfg.epochs):
+        t_ep = time.time()
+        batches = [wk.sampler.epoch_indices(epoch) for wk in workers]
+        if cfg.mode == "async":
+            for wk in workers:
+                wk.fetch_parameters()
+        for b in range(steps):
+            for wk, bt in zip(workers, batches):
+                if cfg.mode == "sync" and b % K == 0:
+                    wk.fetch_parameters()
+                wk.train_local_batch(bt[b])
+                if b % K == 0:
+                    wk.push_gradients()
+                if cfg.mode == "async":
+                    wk.fetch_parameters()
+            if cfg.verbose and b % 50 == 0:
+                log(f"  epoch {epoch + 1} batch {b}/{steps} loss(w0) {workers[0].compute.last_loss():.4f} "
+                    f"global_step {server.core.global_step}")
+            if cfg.max_steps and workers[0].local_step_counter >= cfg.max_steps:
+                break
+        if server.device.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.time() - t_ep
+        for wk in workers:
+            wk.epoch_times.append(dt)
+            if cfg.eval_every and (epoch + 1) % cfg.eval_every == 0:
+                wk.evaluate_model()
+        if cfg.max_steps and workers[0].local_step_counter >= cfg.max_steps:
+            break
+    for wk in workers:
+        wk.cleanup()
+        wk.print_worker_statistics()
+
+
+# ---------------------------------------------------------------------------- distributed
+def run_distributed(cfg, log=print) -> dict:
+    rank, world, local = env_world()
+    device = _device_for(local)
+    t = DistTransport(device=device)
+    dedicated = cfg.topology == "dedicated" and world > 1
+    worker_ranks = list(range(1, world)) if dedicated else list(range(world))
+    W = len(worker_ranks)
+    wid_of_rank = {r: i for i, r in enumerate(worker_ranks)}
+    rank_of_wid = {i: r for r, i in wid_of_rank.items()}
+    if cfg.workers != W:
+        if rank == 0 and cfg.verbose:
+            log(f"[psx] {world} ranks, topology {cfg.topology}: total workers = {W} (overrides --workers {cfg.workers})")
+        cfg.workers = W
+    lg = log if rank == 0 else (lambda *a, **k: None)
+    model, layout, arena, counters = build_state(cfg)
+    classes = model.fc.out_features
+    names = t.all_gather_object(f"{cfg.worker_name}-r{rank}")
+    server = None
+    if rank == 0:
+        server = ParameterServer(cfg, layout, arena, counters, device=device, total_workers=W, log=log)
+    is_worker = rank in wid_of_rank
+    train, test = make_datasets(cfg, device, classes) if is_worker else (None, None)
+    n_train = max(t.all_gather_object(len(train) if train is not None else 0))
+    steps = _common_steps(cfg, W, n_train)
+    wk = None
+    if is_worker:
+        comp = make_compute(model, layout, cfg.batch_size, device, cfg.model, _wire_dtype(cfg),
+                            seed=cfg.seed + wid_of_rank[rank], use_graph=cfg.use_graph)
+    t0 = time.time()
+    if cfg.mode == "sync":
+        if rank == 0:
+            for r in worker_ranks:
+                server.register_worker(names[r], wid_of_rank[r])
+        chan = SyncCollectiveChannel(t, server, members=list(range(W)))
+        if is_worker:
+            wk = Worker(cfg, comp, chan, train, test, worker_name=names[rank], rank=rank, log=lg,
+                        requested_id=wid_of_rank[rank], steps_per_epoch=steps)
+            wk.connect_to_server()
+            wk.run_training()
+        else:
+            _dedicated_sync_server(cfg, server, chan, steps, device)
+    else:
+        mbox_name = t.broadcast_object(f"/psx_{uuid.uuid4().hex[:12]}" if rank == 0 else None)
+        mbox = CP.ShmMailbox(mbox_name, nreply=world, owner=(rank == 0)) if rank == 0 else None
+        t.barrier()
+        if rank != 0:
+            mbox = CP.ShmMailbox(mbox_name, nreply=world, owner=False)
+        remote = {w: r for w, r in rank_of_wid.items() if r != 0}
+        if rank == 0:
+            q = queue.Queue() if is_worker else None
+            srv = threading.Thread(target=server.serve_async, args=(t, mbox, remote),
+                                   kwargs={"local_queue": q, "expected": W}, daemon=True)
+            if is_worker:
+                srv.start()
+                wk = Worker(cfg, comp, LocalAsyncChannel(server, q), train, test, worker_name=names[0], rank=0,
+                            log=lg, requested_id=wid_of_rank[0])
+                wk.connect_to_server()
+                wk.run_training()
+                srv.join()
+            else:
+                server.serve_async(t, mbox, remote, local_queue=None, expected=W)
+        else:
+            hb = None
+            chan = AsyncChannel(t, mbox, rank)
+            wk = Worker(cfg, comp, chan, train, test, worker_name=names[rank], rank=rank, log=lg,
+                        requested_id=wid_of_rank[rank])
+            wk.connect_to_server()
+            hb = CP.Heartbeat(mbox, wk.worker_id, rank, period=max(1.0, cfg.heartbeat_timeout / 6))
+            hb.start()
+            try:
+                wk.run_training()
+            finally:
+                hb.stop()
+        t.barrier()
+        mbox.close()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    wall = time.time() - t0
+    imgs = t.all_gather_object(wk.images if wk is not None else 0)
+    result = {"worker": getattr(wk, "final_metrics", None)}
+    if rank == 0:
+        extra = {"images_per_second": round(sum(imgs) / wall, 2) if wall > 0 else 0.0, "gpus": world,
+                 "topology": "dedicated" if dedicated else "colocated"}
+        server.images_processed = sum(imgs)
+        result["server"] = server.final_metrics(emit=True, extra=extra)
+    t.close()
+    return result
+
+
+def _dedicated_sync_server(cfg, server, chan, steps, device):
+    """Rank 0 of the dedicated topology: takes part in every round's collectives with a zero
+    gradient contribution and applies the averaged update."""
+    K = max(1, cfg.sync_steps)
+    zeros = torch.zeros(server.n, dtype=_wire_dtype(cfg), device=device)
+    done = 0
+    for epoch in range(cfg.epochs):
+        for b in range(steps):
+            if b % K == 0:
+                chan.fetch(None, None)
+                zeros.zero_()
+                chan.push(None, zeros, server.core.global_step)
+            done += 1
+            if cfg.max_steps and done >= cfg.max_steps:
+                return
+
+
+def run(cfg, log=print) -> dict:
+    _, world, _ = env_world()
+    if world <= 1:
+        return run_local(cfg, log=log)
+    return run_distributed(cfg, log=log)
+
+
+def main(argv=None):
+    from ..utils.config import parse
+
+    cfg = parse(argv, description="psx MI355X parameter-server training (rank per GPU)")
+    res = run(cfg)
+    return 0 if res is not None else 1
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

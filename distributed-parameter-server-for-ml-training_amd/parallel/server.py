@@ -1,0 +1,303 @@
+"""The parameter server role (rank 0).
+
+MI355X-native counterpart of the reference ParameterServerServicer
+(reference: src/parameter_server/server.py:81-368):
+
+* state lives in HBM: one fp32 arena holding the full state_dict (models/layout.py), an
+  optional momentum buffer, a staging/aggregation buffer — no pickle, no param_lock: every
+  update is one fused kernel (csrc/kernels/optim.hip) ordered on the server's HIP stream;
+* decisions (registration ids, sync barrier, async staleness reject/weight, statistics) are
+  made by the native core (csrc/runtime/ps_core.cpp, parallel/core.py);
+* the reference RPC surface is kept for in-process use and naming parity:
+  ``RegisterWorker``/``register_worker``, ``FetchParameters``/``fetch_parameters``,
+  ``PushGradrients`` (sic, ps.proto:12) / ``PushGradients`` / ``push_gradients``,
+  ``JobFinished``/``job_finished``;
+* ``serve_async`` is the server event loop of the multi-process async mode: control
+  requests arrive on the shared-memory mailbox, bulk tensors over RCCL point-to-point, and every
+  fetch is served from a per-worker snapshot of the arena so in-flight sends never race the
+  next update (the double-buffered arena of SURVEY.md §5.2).
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import torch
+
+from ..utils import checkpoint as ckpt
+from ..utils import metrics as M
+from . import control as CP
+from .core import APPLY, WAIT, ServerCore
+
+_TRACE = os.environ.get("PSX_TRACE", "0") == "1"
+
+
+class ParameterServer:
+    def __init__(self, cfg, layout, init_arena: torch.Tensor, counters: torch.Tensor | None = None, device="cpu",
+                 total_workers: int | None = None, log=print):
+        self.cfg = cfg
+        self.layout = layout
+        self.device = torch.device(device)
+        self.total_workers = total_workers if total_workers is not None else cfg.workers
+        self.lr = cfg.lr
+        self.log = log if cfg.verbose else (lambda *a, **k: None)
+        self.arena = init_arena.to(self.device, dtype=torch.float32).contiguous()
+        self.counters = counters if counters is not None else torch.zeros(max(1, layout.num_counters), dtype=torch.int64)
+        self.n = layout.param_numel
+        self.params = self.arena[: self.n]
+        self.momentum_buf = torch.zeros_like(self.params) if cfg.momentum else None
+        self._mom_first = True
+        self.agg = None  # fp32 aggregation buffer for in-process sync rounds
+        self._pending = {}
+        self.core = ServerCore(cfg.mode, self.total_workers, cfg.lr, cfg.staleness_bound, cfg.sync_semantics)
+        self.start_time = time.time()
+        self.bytes_pushed = 0
+        self.bytes_fetched = 0
+        self.images_processed = 0
+        self.log(f"Initializing Parameter Server in {cfg.mode.upper()} mode on {self.device} "
+                 f"({len(layout.entries)} state_dict tensors, {self.n:,} trainable params)")
+        if cfg.resume:
+            self.resume(cfg.resume)
+
+    # ------------------------------------------------------------------ numerics
+    def apply(self, grads: torch.Tensor, weight: float):
+        """p <- p - lr * (weight * g [+ wd p]) [momentum]; grads are fp16 wire or fp32."""
+        t0 = time.perf_counter()
+        g = grads[: self.n]
+        if self.device.type == "cuda":
+            from ..ops import kernels as K
+
+            K.sgd_apply(self.params, g, self.lr, gscale=weight, momentum=self.cfg.momentum,
+                        wd=self.cfg.weight_decay, buf=self.momentum_buf, first=self._mom_first, n=self.n)
+        else:
+            d = g.to(torch.float32) * weight
+            if self.cfg.weight_decay:
+                d = d + self.cfg.weight_decay * self.params
+            if self.momentum_buf is not None:
+                if self._mom_first:
+                    self.momentum_buf.copy_(d)
+                else:
+                    self.momentum_buf.mul_(self.cfg.momentum).add_(d)
+                d = self.momentum_buf
+            self.params.sub_(self.lr * d)
+        self._mom_first = False
+        dt = time.perf_counter() - t0  # host-side issue time (device work is stream-ordered)
+        self.core.on_applied(dt)
+        return dt
+
+    def _accumulate(self, grads: torch.Tensor, first: bool):
+        if self.agg is None:
+            self.agg = torch.zeros(self.n, dtype=torch.float32, device=self.device)
+        if first:
+            self.agg.copy_(grads[: self.n])
+        else:
+            self.agg.add_(grads[: self.n].to(torch.float32))
+
+    # ------------------------------------------------------------------ RPC surface
+    def register_worker(self, worker_name: str = "worker-node", requested_id: int = -1):
+        wid = self.core.register(worker_name, requested_id)
+        self.log(f"[RegisterWorker] Worker {wid} from {worker_name} registered")
+        self.log(f"Active workers: {self.core.num_active()}/{self.total_workers}")
+        return wid, self.total_workers
+
+    def fetch_parameters(self, worker_id: int):
+        gs = self.core.on_fetch(worker_id)
+        self.bytes_fetched += self.arena.numel() * 4
+        return self.arena, gs
+
+    def push_gradients(self, worker_id: int, grads: torch.Tensor, local_step: int) -> bool:
+        """In-process push (single-process loopback runs). Sync: aggregate until the barrier
+        completes, then apply the average. Async: staleness check + weighted apply."""
+        self.bytes_pushed += grads[: self.n].numel() * grads.element_size()
+        res = self.core.on_push(worker_id, local_step)
+        self.last_push = res
+        if self.cfg.mode == "sync":
+            if self.cfg.sync_semantics == "reference":
+                # reference: pending[worker_id] = grads (overwrites), average over the dict
+                # entries when the push counter reaches total_workers (server.py:264-288)
+                if res.decision in (WAIT, APPLY):
+                    self._pending[worker_id] = grads[: self.n].to(torch.float32).clone()
+                if res.apply:
+                    self._accumulate(sum(self._pending.values()), True)
+                    self._pending.clear()
+                    self.apply(self.agg, res.weight)
+                return True  # the reference always answers received=True in sync mode
+            if res.decision in (WAIT, APPLY):
+                self._accumulate(grads, self._round_count == 0)
+                self._round_count += 1
+            if res.apply:
+                self.apply(self.agg, res.weight)
+                self._round_count = 0
+            return res.accepted
+        if res.apply:
+            self.apply(grads, res.weight)
+        return res.accepted
+
+    _round_count = 0
+    _pending: dict = {}
+    last_push = None
+
+    def job_finished(self, worker_id: int, emit: bool = True) -> str:
+        """Reference server.py:306-318: when the last active worker finishes, print the final
+        statistics (runners that append job-level fields pass emit=False and emit once)."""
+        self.log(f"[JobFinished] Worker {worker_id} completed")
+        if self.core.job_finished(worker_id) and emit:
+            self.final_metrics(emit=True)
+        return "Acknowledged"
+
+    # reference RPC names (ps.proto:4-19, including the PushGradrients typo)
+    RegisterWorker = register_worker
+    FetchParameters = fetch_parameters
+    PushGradients = push_gradients
+    PushGradrients = push_gradients
+    JobFinished = job_finished
+
+    # ------------------------------------------------------------------ sync (collective) path
+    def apply_reduced(self, summed: torch.Tensor, members: list[int], local_steps: list[int]) -> bool:
+        """Bookkeeping + update for one sync round whose gradient sum arrived by RCCL reduce."""
+        res = None
+        for wid, ls in zip(members, local_steps):
+            res = self.core.on_push(wid, ls)
+        self.bytes_pushed += len(members) * self.n * summed.element_size()
+        if res is not None and res.apply:
+            self.apply(summed, res.weight)
+            return True
+        return False
+
+    # ------------------------------------------------------------------ checkpoint
+    def checkpoint(self, path: str | None = None) -> str:
+        step = self.core.global_step
+        path = path or ckpt.path_for(self.cfg.ckpt_dir, step)
+        ckpt.save(path, self.layout, self.arena, self.counters, step, self.cfg.mode, self.total_workers, self.lr,
+                  self.momentum_buf, self.cfg.to_json())
+        self.log(f"[Checkpoint] global step {step} -> {path}")
+        return path
+
+    def maybe_checkpoint(self):
+        if self.cfg.ckpt_every and self.core.global_step % self.cfg.ckpt_every == 0 and self.core.global_step:
+            return self.checkpoint()
+        return None
+
+    def resume(self, path: str):
+        if path == "latest":
+            path = ckpt.latest(self.cfg.ckpt_dir)
+            if path is None:
+                self.log("[Resume] no checkpoint found; starting fresh")
+                return
+        arena, counters, step, mom, _ = ckpt.restore(path, self.layout)
+        self.arena.copy_(arena.to(self.device))
+        self.counters = counters
+        self.core.global_step = step
+        if mom is not None and self.momentum_buf is not None:
+            self.momentum_buf.copy_(mom.to(self.device))
+            self._mom_first = False
+        self.log(f"[Resume] restored global step {step} from {path}")
+
+    # ------------------------------------------------------------------ metrics
+    def final_metrics(self, emit: bool = False, extra: dict | None = None) -> dict:
+        m = self.core.metrics()
+        m["bytes_pushed"] = int(self.bytes_pushed)
+        m["bytes_fetched"] = int(self.bytes_fetched)
+        if self.images_processed:
+            m["images_processed"] = int(self.images_processed)
+        if extra:
+            m.update(extra)
+        if emit:
+            self.log(f"\n{'=' * 50}\nPARAMETER SERVER FINAL STATISTICS\n{'=' * 50}")
+            self.log(f"Mode: {m['mode'].upper()}  workers: {m['total_workers']}  global steps: "
+                     f"{m['global_steps_completed']}  updates/s: {m['updates_per_second']}")
+            M.emit(m, self.cfg.log_dir, rank=0)
+            self.log("--- End Server Metrics ---")
+        return m
+
+    # ------------------------------------------------------------------ async event loop
+    def serve_async(self, transport, mbox, rank_of: dict, stop_when_done: bool = True, local_queue=None,
+                    poll: float = 0.0005, expected: int | None = None):
+        """Multi-process async server loop (runs on rank 0, in its own thread when rank 0 also
+        trains). rank_of: worker_id -> transport rank of the *remote* workers. ``local_queue``
+        (optional) delivers requests of the co-located worker as (kind, worker_id, grads,
+        local_step, event, box). The loop ends once ``expected`` workers finished or died."""
+        expected = expected if expected is not None else len(rank_of) + (1 if local_queue is not None else 0)
+        finished = set()
+        n = self.n
+        wire_dtype = torch.float16 if self.cfg.codec == "fp16" else torch.float32
+        slots = {w: torch.empty(n, dtype=wire_dtype, device=self.device) for w in rank_of}
+        snaps = {w: torch.empty_like(self.arena) for w in rank_of}
+        pending_recv = []   # (wid, local_step, work)
+        pending_send = {}   # wid -> work
+        done = set()
+        last_to = time.monotonic()
+        while True:
+            msg = mbox.recv(timeout=poll)
+            if msg is not None and _TRACE:
+                print(f"[psx-server] {msg} pending_recv={[p[0] for p in pending_recv]}", flush=True)
+            if msg is not None:
+                t, wid = msg.type, msg.a
+                if t == CP.HELLO:
+                    got, total = self.register_worker(f"rank{msg.src}", msg.a)
+                    mbox.reply(msg.src, CP.Msg(CP.R_REGISTERED, 0, got, total))
+                elif t == CP.FETCH:
+                    gs = self.core.on_fetch(wid)
+                    prev = pending_send.pop(wid, None)
+                    if prev is not None:
+                        prev.wait()
+                    snaps[wid].copy_(self.arena)
+                    pending_send[wid] = transport.isend(snaps[wid], rank_of[wid])
+                    self.bytes_fetched += self.arena.numel() * 4
+                    mbox.reply(rank_of[wid], CP.Msg(CP.R_FETCHED, 0, wid, 0, gs))
+                elif t == CP.PUSH:
+                    pending_recv.append((wid, msg.c, transport.irecv(slots[wid], rank_of[wid])))
+                elif t == CP.DONE:
+                    finished.add(wid)
+                    self.core.job_finished(wid)
+                    mbox.reply(rank_of[wid], CP.Msg(CP.R_ACK, 0, wid))
+                    self.log(f"[JobFinished] Worker {wid} completed")
+                elif t == CP.HEARTBEAT:
+                    self.core.heartbeat(wid)
+                elif t == CP.STOP:
+                    break
+            # complete arrived pushes in arrival order
+            keep = []
+            for wid, ls, work in pending_recv:
+                if transport.completed(work):  # each work is waited exactly once (gloo!)
+                    res = self.core.on_push(wid, ls)
+                    self.bytes_pushed += n * slots[wid].element_size()
+                    if res.apply:
+                        self.apply(slots[wid], res.weight)
+                        self.maybe_checkpoint()
+                    mbox.reply(rank_of[wid], CP.Msg(CP.R_PUSHED, 0, wid, int(res.accepted), self.core.global_step,
+                                                    res.staleness))
+                else:
+                    keep.append((wid, ls, work))
+            pending_recv = keep
+            stop = False
+            if local_queue is not None:
+                while True:
+                    try:
+                        kind, wid, grads, ls, ev, box = local_queue.get_nowait()
+                    except Exception:
+                        break
+                    if kind == "push":
+                        res = self.core.on_push(wid, ls)
+                        self.bytes_pushed += n * grads.element_size()
+                        if res.apply:
+                            self.apply(grads, res.weight)
+                            self.maybe_checkpoint()
+                        box["res"] = res
+                        box["global_step"] = self.core.global_step
+                    else:  # "done"
+                        self.log(f"[JobFinished] Worker {wid} completed")
+                        self.core.job_finished(wid)
+                        finished.add(wid)
+                    ev.set()
+            now = time.monotonic()
+            if self.cfg.heartbeat_timeout and now - last_to > 1.0:
+                last_to = now
+                for w in self.core.check_timeouts(self.cfg.heartbeat_timeout):
+                    self.log(f"[Failure] worker {w} missed heartbeats for {self.cfg.heartbeat_timeout}s; marked dead")
+                    finished.add(w)
+            if stop_when_done and len(finished) >= expected and not pending_recv:
+                break
+        for w in pending_send.values():
+            w.wait()
+

@@ -1,0 +1,135 @@
+"""Data plane: bulk tensor movement between the parameter server (rank 0) and the workers.
+
+Replaces the reference's gRPC + pickle transport (reference: src/communication/ps_pb2_grpc.py:28-121,
+src/parameter_server/server.py:370-393, src/workers/worker.py:199-311):
+
+  reference RPC               payload                          here (one process per GPU)
+  PushGradrients  (sync)      pickled fp16 dict, 22.4 MB       RCCL reduce(sum) of the flat fp16
+                                                               wire buffer to rank 0
+  FetchParameters (sync)      pickled fp32 state_dict, 44.9 MB RCCL broadcast of the flat fp32 arena
+  PushGradrients  (async)     same                             RCCL send(worker -> 0) into a
+                                                               per-worker staging slot
+  FetchParameters (async)     same                             RCCL send(0 -> worker) of a
+                                                               per-worker snapshot of the arena
+
+``DistTransport`` is torch.distributed with backend "nccl" (= RCCL over xGMI on ROCm) for
+device tensors, or "gloo" for the CPU test path — the same code drives both. A gloo side group
+carries small host-side collectives (registration names, metrics gathering).
+``LocalTransport`` is the single-process (1 GPU, server + workers co-located) loopback.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class LocalTransport:
+    rank = 0
+    world_size = 1
+    is_distributed = False
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+
+    def reduce_sum_to_server(self, t):
+        return t
+
+    def broadcast_from_server(self, t):
+        return t
+
+    def isend(self, t, dst):
+        raise RuntimeError("LocalTransport has no peers")
+
+    irecv = isend
+
+    def barrier(self):
+        pass
+
+    def all_gather_object(self, obj):
+        return [obj]
+
+    def broadcast_object(self, obj):
+        return obj
+
+    def close(self):
+        pass
+
+
+class DistTransport:
+    is_distributed = True
+
+    def __init__(self, backend: str | None = None, device=None, timeout_s: float = 600.0):
+        if not dist.is_initialized():
+            if backend is None:
+                backend = "nccl" if torch.cuda.is_available() else "gloo"
+            kw = {}
+            if backend == "nccl" and device is not None:
+                kw["device_id"] = torch.device(device)
+            dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        self.backend = dist.get_backend()
+        self.rank = dist.get_rank()
+        self.world_size = dist.get_world_size()
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        # host-side control collectives always go through gloo
+        self.ctrl = dist.new_group(backend="gloo") if self.backend != "gloo" else dist.group.WORLD
+
+    # ---- sync mode collectives (bulk, device tensors)
+    def reduce_sum_to_server(self, t):
+        dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
+        return t
+
+    def broadcast_from_server(self, t):
+        dist.broadcast(t, src=0)
+        return t
+
+    # ---- async mode point-to-point (bulk)
+    def isend(self, t, dst: int):
+        return dist.isend(t, dst=dst)
+
+    def irecv(self, t, src: int):
+        return dist.irecv(t, src=src)
+
+    def completed(self, work) -> bool:
+        """Non-blocking completion test of a p2p work. RCCL works are polled through their HIP
+        event; gloo works only complete inside wait(), so they are waited for (the payload is
+        already in flight when the server polls, see ParameterServer.serve_async)."""
+        if self.backend == "gloo":
+            work.wait()
+            return True
+        if work.is_completed():
+            work.wait()  # orders the caller's stream after the RCCL stream (no host block)
+            return True
+        return False
+
+    # ---- host control
+    def barrier(self):
+        dist.barrier(group=self.ctrl)
+
+    def all_gather_object(self, obj):
+        out = [None] * self.world_size
+        dist.all_gather_object(out, obj, group=self.ctrl)
+        return out
+
+    def broadcast_object(self, obj):
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=0, group=self.ctrl)
+        return lst[0]
+
+    def close(self):
+        if dist.is_initialized():
+            try:
+                dist.barrier(group=self.ctrl)
+            except Exception:
+                pass
+            dist.destroy_process_group()
+
+
+def env_world() -> tuple[int, int, int]:
+    """(rank, world_size, local_rank) from torchrun-style environment (defaults: single process)."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local

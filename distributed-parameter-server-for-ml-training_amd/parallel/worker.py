@@ -1,0 +1,313 @@
+"""The data-parallel worker role.
+
+MI355X-native counterpart of the reference DistributedWorker (reference:
+src/workers/worker.py:78-453). The method names and the training-loop contract are kept:
+``connect_to_server`` (register), ``setup_data`` (contiguous shard), ``fetch_parameters``,
+``train_local_batch``, ``push_gradients``, ``evaluate_model``, ``run_training``,
+``print_worker_statistics`` (WORKER_FINAL_METRICS), ``cleanup`` (JobFinished).
+
+The protocol side is a *channel*:
+
+* ``InProcessChannel``  — direct calls into a ParameterServer object (1-process loopback; the
+  server may host several simulated workers on one GPU);
+* ``SyncCollectiveChannel`` — sync mode over RCCL: push = reduce(sum) of the wire buffer to rank 0,
+  where the server applies the averaged update, fetch = broadcast of the arena (all ranks step
+  together, so the wait-for-N barrier is the collective itself);
+* ``AsyncChannel``      — async mode: control request on the shared-memory mailbox, bulk tensor by
+  RCCL send/recv, reply (received flag, global step) on the worker's reply slot;
+* ``LocalAsyncChannel`` — the worker co-located with the async server on rank 0 (pushes go to
+  the server thread through a queue, fetches are device copies).
+"""
+from __future__ import annotations
+
+import queue
+import threading
+import time
+
+import numpy as np
+import torch
+
+from ..utils import metrics as M
+from ..utils.data import EpochSampler, shard_range
+from . import control as CP
+
+
+class InProcessChannel:
+    def __init__(self, server, emit_on_last: bool = False):
+        self.server = server
+        self.emit_on_last = emit_on_last
+
+    def register(self, name, requested_id=-1):
+        return self.server.register_worker(name, requested_id)
+
+    def fetch(self, worker_id, local_arena):
+        arena, gs = self.server.fetch_parameters(worker_id)
+        local_arena.copy_(arena)
+        return gs
+
+    def push(self, worker_id, grads, local_step):
+        return self.server.push_gradients(worker_id, grads, local_step)
+
+    def finished(self, worker_id):
+        self.server.job_finished(worker_id, emit=self.emit_on_last)
+
+
+class SyncCollectiveChannel:
+    """All ranks call push/fetch in lockstep. Rank 0 may or may not train (topology)."""
+
+    def __init__(self, transport, server=None, members=None):
+        self.t = transport
+        self.server = server
+        self.members = members or []
+        self._registered = None
+
+    def register(self, name, requested_id=-1):
+        if self.server is not None:
+            pass  # registrations are done for every rank by the runner (gathered names)
+        return requested_id, len(self.members)
+
+    def fetch(self, worker_id, local_arena):
+        if self.server is not None:
+            for w in self.members:
+                self.server.core.on_fetch(w)
+            self.t.broadcast_from_server(self.server.arena)
+            self.server.bytes_fetched += self.server.arena.numel() * 4 * max(0, len(self.members) - 1)
+            if local_arena is not None and local_arena.data_ptr() != self.server.arena.data_ptr():
+                local_arena.copy_(self.server.arena)
+            return self.server.core.global_step
+        self.t.broadcast_from_server(local_arena)
+        return self._gs_after_fetch()
+
+    def _gs_after_fetch(self):
+        # global step advances by exactly one per sync round; workers track it locally
+        self._gs = getattr(self, "_gs", 0)
+        return self._gs
+
+    def push(self, worker_id, grads, local_step):
+        self.t.reduce_sum_to_server(grads)
+        if self.server is not None:
+            self.server.apply_reduced(grads, self.members, [local_step] * len(self.members))
+            self.server.maybe_checkpoint()
+        else:
+            self._gs = getattr(self, "_gs", 0) + 1
+        return True
+
+    def finished(self, worker_id):
+        pass
+
+
+class AsyncChannel:
+    def __init__(self, transport, mbox, rank):
+        self.t, self.mbox, self.rank = transport, mbox, rank
+
+    def register(self, name, requested_id=-1):
+        self.mbox.send(CP.Msg(CP.HELLO, self.rank, requested_id))
+        r = self.mbox.wait_reply(self.rank)
+        return r.a, r.b
+
+    def fetch(self, worker_id, local_arena):
+        self.mbox.send(CP.Msg(CP.FETCH, self.rank, worker_id))
+        work = self.t.irecv(local_arena, 0)
+        r = self.mbox.wait_reply(self.rank)
+        work.wait()
+        return r.c
+
+    def push(self, worker_id, grads, local_step):
+        self.mbox.send(CP.Msg(CP.PUSH, self.rank, worker_id, 0, local_step))
+        self.t.isend(grads, 0).wait()
+        r = self.mbox.wait_reply(self.rank)
+        self.last_staleness = r.d
+        return bool(r.b)
+
+    def finished(self, worker_id):
+        self.mbox.send(CP.Msg(CP.DONE, self.rank, worker_id))
+        self.mbox.wait_reply(self.rank)
+
+
+class LocalAsyncChannel:
+    def __init__(self, server, q: "queue.Queue"):
+        self.server, self.q = server, q
+
+    def register(self, name, requested_id=-1):
+        return self.server.register_worker(name, requested_id)
+
+    def fetch(self, worker_id, local_arena):
+        gs = self.server.core.on_fetch(worker_id)
+        local_arena.copy_(self.server.arena)
+        return gs
+
+    def push(self, worker_id, grads, local_step):
+        ev, box = threading.Event(), {}
+        self.q.put(("push", worker_id, grads, local_step, ev, box))
+        ev.wait()
+        return box["res"].accepted
+
+    def finished(self, worker_id):
+        ev, box = threading.Event(), {}
+        self.q.put(("done", worker_id, None, 0, ev, box))
+        ev.wait()
+
+
+class Worker:
+    def __init__(self, cfg, compute, channel, train_set, test_set=None, worker_name=None, rank=0, log=print,
+                 steps_per_epoch=None, requested_id=-1):
+        self.cfg = cfg
+        self.compute = compute
+        self.channel = channel
+        self.train_set, self.test_set = train_set, test_set
+        self.worker_name = worker_name or cfg.worker_name
+        self.rank = rank
+        self.log = log if cfg.verbose else (lambda *a, **k: None)
+        self.batch_size = cfg.batch_size
+        self.learning_rate = cfg.lr
+        self.num_epochs = cfg.epochs
+        self.local_steps_per_sync = max(1, cfg.sync_steps)
+        self.worker_id = None
+        self.total_workers = None
+        self.requested_id = requested_id
+        self._forced_steps = steps_per_epoch
+        self.local_step_counter = 0
+        self.global_step_cache = 0
+        self.training_start_time = None
+        self.epoch_times = []
+        self.accuracies = []
+        self.losses = []
+        self.pushes_rejected = 0
+        self.images = 0
+        self.timer = M.PhaseTimer(device=getattr(compute, "device", None))
+        self.sampler = None
+
+    # ---------------------------------------------------------------- reference API
+    def connect_to_server(self):
+        self.worker_id, self.total_workers = self.channel.register(self.worker_name, self.requested_id)
+        self.log(f"Registered as Worker {self.worker_id} (Total workers: {self.total_workers})")
+
+    def setup_data(self):
+        start, end = shard_range(self.worker_id, self.total_workers, len(self.train_set))
+        self.sampler = EpochSampler(start, end, self.batch_size, seed=self.cfg.seed + 17 * self.worker_id,
+                                    steps=self._forced_steps)
+        self.log(f"Worker {self.worker_id} assigned {end - start} training samples (indices {start}-{end - 1}); "
+                 f"{len(self.sampler)} batches per epoch")
+
+    def fetch_parameters(self):
+        self.global_step_cache = self.channel.fetch(self.worker_id, self.compute.local_arena)
+        return self.global_step_cache
+
+    def push_gradients(self):
+        ok = self.channel.push(self.worker_id, self.compute.grads, self.global_step_cache)
+        if not ok:
+            self.pushes_rejected += 1
+        return ok
+
+    def train_local_batch(self, idx):
+        self.compute.train_step(self.train_set, idx)
+        self.local_step_counter += 1
+        self.images += len(idx)
+
+    def evaluate_model(self):
+        if self.test_set is None:
+            return None
+        acc = self.compute.evaluate(self.test_set)
+        self.log(f"  > Worker {self.worker_id} test accuracy: {acc:.2f}%")
+        self.accuracies.append(acc)
+        return acc
+
+    def _sync(self):
+        if torch.cuda.is_available() and getattr(self.compute, "device", torch.device("cpu")).type == "cuda":
+            torch.cuda.synchronize()
+
+    def run_training(self):
+        if self.sampler is None:
+            self.setup_data()
+        self.log(f"\n--- Starting distributed training for {self.num_epochs} epochs ---")
+        self.training_start_time = time.time()
+        K = self.local_steps_per_sync
+        fi_worker, fi_step = _parse_fault(self.cfg.fault_inject)
+        try:
+            for epoch in range(self.num_epochs):
+                self._sync()
+                t_ep = time.time()
+                batches = self.sampler.epoch_indices(epoch)
+                for batch_idx, idx in enumerate(batches):
+                    if fi_worker == self.worker_id and self.local_step_counter == fi_step:
+                        raise _InjectedFault(f"fault injected: worker {self.worker_id} at step {fi_step}")
+                    if batch_idx % K == 0:
+                        with self.timer.span("fetch"):
+                            self.fetch_parameters()
+                    with self.timer.span("compute_issue"):
+                        self.train_local_batch(idx)
+                    if batch_idx % K == 0:
+                        with self.timer.span("push"):
+                            self.push_gradients()
+                    if self.cfg.verbose and batch_idx % 50 == 0:
+                        loss = self.compute.last_loss()
+                        self.losses.append(loss)
+                        self.log(f"  Worker {self.worker_id} epoch {epoch + 1} batch {batch_idx}/{len(batches)} "
+                                 f"loss {loss:.4f} elapsed {time.time() - t_ep:.1f}s")
+                    if self.cfg.max_steps and self.local_step_counter >= self.cfg.max_steps:
+                        break
+                self._sync()
+                self.epoch_times.append(time.time() - t_ep)
+                self.log(f"Epoch {epoch + 1} completed in {self.epoch_times[-1]:.2f}s")
+                if self.cfg.eval_every and (epoch + 1) % self.cfg.eval_every == 0:
+                    self.evaluate_model()
+                if self.cfg.max_steps and self.local_step_counter >= self.cfg.max_steps:
+                    break
+        finally:
+            self._sync()
+            self.cleanup()
+            self.print_worker_statistics()
+
+    def print_worker_statistics(self):
+        if self.training_start_time is None:
+            return None
+        total = time.time() - self.training_start_time
+        avg_ep = float(np.mean(self.epoch_times)) if self.epoch_times else 0.0
+        final_acc = self.accuracies[-1] if self.accuracies else 0.0
+        rec = {
+            "type": "WORKER_FINAL_METRICS",
+            "worker_id": self.worker_id,
+            "total_workers": self.total_workers,
+            "total_training_time_seconds": round(total, 2),
+            "average_epoch_time_seconds": round(avg_ep, 2),
+            "epoch_times_seconds": [round(t, 2) for t in self.epoch_times],
+            "final_test_accuracy_percent": round(final_acc, 2),
+            "all_accuracies_percent": [round(a, 2) for a in self.accuracies],
+            "local_steps_completed": self.local_step_counter,
+            "batch_size": self.batch_size,
+            "learning_rate": self.learning_rate,
+            "num_epochs": self.num_epochs,
+            # psx extensions
+            "images_per_second": round(self.images / total, 2) if total > 0 else 0.0,
+            "rejected_pushes": self.pushes_rejected,
+            "phase_ms": self.timer.summary_ms(),
+            "last_loss": round(self.losses[-1], 4) if self.losses else None,
+            "rank": self.rank,
+        }
+        self.log(f"\n--- Worker {self.worker_id} Statistics ---\nTotal training time: {total:.1f} seconds\n"
+                 f"Local steps completed: {self.local_step_counter}\n--- End Statistics ---")
+        M.emit(rec, self.cfg.log_dir, rank=self.rank)
+        self.final_metrics = rec
+        return rec
+
+    def cleanup(self):
+        try:
+            self.channel.finished(self.worker_id)
+        except Exception as e:  # reference swallows errors here (worker.py:444-450)
+            self.log(f"cleanup: {e}")
+
+    # reference method names
+    train_local = train_local_batch
+
+
+class _InjectedFault(RuntimeError):
+    pass
+
+
+def _parse_fault(spec: str):
+    """'kill_worker:K@S' -> (K, S); anything else -> (None, None)."""
+    if not spec or not spec.startswith("kill_worker:"):
+        return None, None
+    body = spec.split(":", 1)[1]
+    k, s = body.split("@")
+    return int(k), int(s)

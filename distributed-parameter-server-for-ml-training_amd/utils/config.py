@@ -1,0 +1,161 @@
+"""Configuration: CLI flags + environment defaults + optional JSON file.
+
+Keeps every flag and environment variable of the reference with the same defaults
+(reference: src/parameter_server/server.py:405-433 and src/workers/worker.py:455-482):
+
+  server  --mode {sync,async}  env SERVER_MODE             default sync
+          --workers N (1..32)  env TOTAL_WORKERS_EXPECTED  default 4
+          --lr 0.1, --port (env SERVER_PORT, 8000), --staleness-bound 5 (now actually wired)
+  worker  --server (env PARAMETER_SERVER_ADDRESS, localhost:8000), --worker-name,
+          --epochs 3, --batch-size 128, --lr 0.1, --sync-steps 1
+
+and adds the MI355X-native knobs: --gpus/--nproc, --codec, --topk-ratio,
+--dtype, --momentum/--weight-decay (server optimizer, default 0 = reference parity), --model,
+--synthetic, --ckpt-every/--resume, --sync-semantics {barrier,reference}, --topology.
+Precedence: explicit CLI flag > JSON config file (--config) > environment > default.
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import json
+import os
+from dataclasses import dataclass, field
+
+
+def _env(name, default, cast=str):
+    v = os.environ.get(name)
+    return cast(v) if v not in (None, "") else default
+
+
+@dataclass
+class PSConfig:
+    # --- reference server flags
+    mode: str = "sync"
+    workers: int = 4
+    lr: float = 0.1
+    port: int = 8000
+    staleness_bound: int = 5
+    # --- reference worker flags
+    server: str = "localhost:8000"
+    worker_name: str = "worker-node"
+    epochs: int = 3
+    batch_size: int = 128
+    sync_steps: int = 1
+    # --- MI355X-native extensions
+    model: str = "resnet18"
+    num_classes: int | None = None
+    gpus: int = 1                  # processes / GPUs on this node (1 = server+worker co-located)
+    topology: str = "colocated"    # colocated: rank 0 = PS + worker 0; dedicated: rank 0 = PS only
+    codec: str = "fp16"            # none (fp32 wire) | fp16 (reference) | topk
+    topk_ratio: float = 0.01
+    dtype: str = "bf16"            # compute dtype of the HIP engine
+    momentum: float = 0.0          # server optimizer (0 = reference plain SGD, server.py:133)
+    weight_decay: float = 0.0
+    sync_semantics: str = "barrier"  # barrier (wait-for-N) | reference (count-triggered)
+    synthetic: bool = True
+    data_dir: str = ""
+    train_samples: int = 50000
+    test_samples: int = 10000
+    eval_every: int = 1            # epochs between evaluations (0 = never)
+    max_steps: int = 0             # stop after this many local steps (0 = full epochs)
+    ckpt_every: int = 0
+    ckpt_dir: str = "checkpoints"
+    resume: str = ""
+    seed: int = 0
+    heartbeat_timeout: float = 60.0
+    log_dir: str = ""
+    use_graph: bool = True
+    fault_inject: str = ""         # e.g. "kill_worker:2@5" (worker 2 exits at its step 5)
+    verbose: int = 1
+    extra: dict = field(default_factory=dict)
+
+    def validate(self):
+        if self.mode not in ("sync", "async"):
+            raise ValueError(f"--mode must be sync or async, got {self.mode!r}")
+        if not (1 <= self.workers <= 32):  # reference server.py:424-426
+            raise ValueError("Number of workers must be between 1 and 32")
+        if self.codec not in ("none", "fp16", "topk"):
+            raise ValueError(f"--codec must be none, fp16 or topk, got {self.codec!r}")
+        if self.topology not in ("colocated", "dedicated"):
+            raise ValueError(f"--topology must be colocated or dedicated, got {self.topology!r}")
+        if self.sync_semantics not in ("barrier", "reference"):
+            raise ValueError("--sync-semantics must be barrier or reference")
+        if self.staleness_bound < 0:
+            raise ValueError("--staleness-bound must be >= 0")
+        if not (0.0 < self.topk_ratio <= 1.0):
+            raise ValueError("--topk-ratio must be in (0, 1]")
+        return self
+
+    def to_json(self) -> str:
+        return json.dumps(dataclasses.asdict(self), sort_keys=True)
+
+
+def add_arguments(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
+    d = PSConfig()
+    A = ap.add_argument
+    A("--config", default="", help="JSON file with PSConfig fields")
+    A("--mode", choices=["sync", "async"], default=None, help="Training mode (env SERVER_MODE)")
+    A("--workers", type=int, default=None, help="Expected number of workers, 1-32 (env TOTAL_WORKERS_EXPECTED)")
+    A("--lr", type=float, default=None, help="Learning rate (server SGD)")
+    A("--port", type=int, default=None, help="Rendezvous port (env SERVER_PORT)")
+    A("--staleness-bound", type=int, default=None, help="Maximum staleness accepted in async mode")
+    A("--server", default=None, help="Server address host:port (env PARAMETER_SERVER_ADDRESS)")
+    A("--worker-name", default=None, help="Worker name for identification")
+    A("--epochs", type=int, default=None)
+    A("--batch-size", type=int, default=None)
+    A("--sync-steps", type=int, default=None, help="Local steps between push/fetch (reference semantics)")
+    A("--model", choices=["resnet18", "resnet50", "resnet_tiny"], default=None)
+    A("--num-classes", type=int, default=None)
+    A("--gpus", "--nproc", dest="gpus", type=int, default=None)
+    A("--topology", choices=["colocated", "dedicated"], default=None)
+    A("--codec", choices=["none", "fp16", "topk"], default=None)
+    A("--topk-ratio", type=float, default=None)
+    A("--dtype", choices=["bf16"], default=None)
+    A("--momentum", type=float, default=None)
+    A("--weight-decay", type=float, default=None)
+    A("--sync-semantics", choices=["barrier", "reference"], default=None)
+    A("--synthetic", action="store_true", default=None)
+    A("--data-dir", default=None, help="directory with cifar-100-binary/{train,test}.bin")
+    A("--train-samples", type=int, default=None)
+    A("--test-samples", type=int, default=None)
+    A("--eval-every", type=int, default=None)
+    A("--max-steps", type=int, default=None)
+    A("--ckpt-every", type=int, default=None)
+    A("--ckpt-dir", default=None)
+    A("--resume", default=None)
+    A("--seed", type=int, default=None)
+    A("--heartbeat-timeout", type=float, default=None)
+    A("--log-dir", default=None)
+    A("--no-graph", dest="use_graph", action="store_false", default=None)
+    A("--fault-inject", default=None)
+    A("--verbose", type=int, default=None)
+    return ap
+
+
+def from_args(ns: argparse.Namespace) -> PSConfig:
+    cfg = PSConfig()
+    # environment defaults (reference env vars)
+    cfg.mode = _env("SERVER_MODE", cfg.mode)
+    cfg.workers = _env("TOTAL_WORKERS_EXPECTED", cfg.workers, int)
+    cfg.port = _env("SERVER_PORT", cfg.port, int)
+    cfg.server = _env("PARAMETER_SERVER_ADDRESS", cfg.server)
+    # JSON config file
+    if getattr(ns, "config", ""):
+        with open(ns.config) as f:
+            data = json.load(f)
+        for k, v in data.items():
+            if not hasattr(cfg, k):
+                raise ValueError(f"unknown config key {k!r} in {ns.config}")
+            setattr(cfg, k, v)
+    # explicit CLI flags
+    for f in dataclasses.fields(PSConfig):
+        v = getattr(ns, f.name, None)
+        if v is not None:
+            setattr(cfg, f.name, v)
+    return cfg.validate()
+
+
+def parse(argv=None, description="psx parameter server") -> PSConfig:
+    ap = add_arguments(argparse.ArgumentParser(description=description))
+    return from_args(ap.parse_args(argv))

@@ -1,0 +1,147 @@
+"""End-to-end parameter-server runs on CPU: loopback (1 process) and multi-process over gloo.
+
+The multi-process tests launch real ranks (torch.distributed gloo, 127.0.0.1) through the same
+runner the GPU job uses (RCCL there); the model is the CPU-sized TinyResNet.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from psx.models.layout import ParamLayout
+from psx.models.resnet import TinyResNet
+from psx.parallel.compute import TorchCompute
+from psx.parallel.runner import run_local
+from psx.parallel.server import ParameterServer
+from psx.utils import metrics as M
+from psx.utils.config import PSConfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def tiny_cfg(**kw):
+    base = dict(model="resnet_tiny", batch_size=8, epochs=1, train_samples=96, test_samples=32, eval_every=1,
+                verbose=0, use_graph=False, lr=0.05)
+    base.update(kw)
+    return PSConfig(**base).validate()
+
+
+def test_inprocess_sync_matches_manual_average():
+    torch.manual_seed(0)
+    cfg = tiny_cfg(mode="sync", workers=2)
+    m = TinyResNet(10)
+    lay = ParamLayout.from_module(m)
+    arena, counters = lay.pack(m)
+    srv = ParameterServer(cfg, lay, arena.clone(), counters, total_workers=2, log=lambda *a: None)
+    for w in range(2):
+        assert srv.RegisterWorker(f"w{w}", w) == (w, 2)
+    g0 = torch.randn(lay.param_numel).half()
+    g1 = torch.randn(lay.param_numel).half()
+    before = srv.arena.clone()
+    assert srv.PushGradrients(0, g0, 0) is True  # reference RPC name (typo kept)
+    assert torch.equal(srv.arena, before)  # barrier not complete yet
+    assert srv.push_gradients(1, g1, 0) is True
+    expect = before[: lay.param_numel] - 0.05 * (g0.float() + g1.float()) / 2
+    assert torch.allclose(srv.arena[: lay.param_numel], expect, atol=1e-6)
+    _, gs = srv.FetchParameters(0)
+    assert gs == 1
+
+
+def test_inprocess_async_staleness_weights():
+    cfg = tiny_cfg(mode="async", workers=2, staleness_bound=1)
+    m = TinyResNet(10)
+    lay = ParamLayout.from_module(m)
+    arena, counters = lay.pack(m)
+    srv = ParameterServer(cfg, lay, arena.clone(), counters, total_workers=2, log=lambda *a: None)
+    srv.register_worker("a", 0)
+    srv.register_worker("b", 1)
+    g = torch.ones(lay.param_numel, dtype=torch.float16)
+    p0 = srv.arena[0].item()
+    assert srv.push_gradients(0, g, 0)  # staleness 0, weight 1
+    assert srv.arena[0].item() == pytest.approx(p0 - 0.05, abs=1e-6)
+    assert srv.push_gradients(1, g, 0)  # staleness 1, weight 1/1.1
+    assert srv.arena[0].item() == pytest.approx(p0 - 0.05 - 0.05 / 1.1, abs=1e-6)
+    assert not srv.push_gradients(0, g, 0)  # staleness 2 > bound 1 -> rejected, no update
+    assert srv.arena[0].item() == pytest.approx(p0 - 0.05 - 0.05 / 1.1, abs=1e-6)
+
+
+def test_torch_compute_grads_match_autograd():
+    torch.manual_seed(0)
+    m = TinyResNet(10)
+    lay = ParamLayout.from_module(m)
+    arena, _ = lay.pack(m)
+    from psx.utils.data import DeviceDataset
+
+    ds = DeviceDataset.synthetic(16, 32, 10, seed=0, device="cpu")
+    comp = TorchCompute(TinyResNet(10), lay, 8, grad_dtype=torch.float32)
+    comp.local_arena.copy_(arena)
+    comp.train_step(ds, list(range(8)))
+    assert comp.last_loss() > 0
+    assert torch.isfinite(comp.grads).all()
+    assert comp.grads.abs().sum() > 0
+
+
+@pytest.mark.parametrize("mode,workers", [("sync", 1), ("sync", 3), ("async", 3)])
+def test_run_local(mode, workers, capsys):
+    cfg = tiny_cfg(mode=mode, workers=workers)
+    res = run_local(cfg, log=lambda *a, **k: None)
+    srv = res["server"]
+    out = capsys.readouterr().out
+    recs = M.parse_lines(out.splitlines())
+    types = [r["type"] for r in recs]
+    assert types.count("WORKER_FINAL_METRICS") == workers
+    assert types.count("SERVER_FINAL_METRICS") == 1
+    steps = -(-(96 // workers) // 8)  # ceil(shard / batch)
+    assert srv["gradients_processed"] == workers * steps
+    if mode == "sync":
+        assert srv["global_steps_completed"] == steps
+    else:
+        assert srv["global_steps_completed"] == workers * steps
+        assert srv["max_staleness_observed"] == workers - 1
+        assert srv["staleness_histogram"][workers - 1] > 0
+    w = [r for r in recs if r["type"] == "WORKER_FINAL_METRICS"][0]
+    assert w["local_steps_completed"] == steps and len(w["all_accuracies_percent"]) == 1
+
+
+def _spawn(nproc, args, timeout=240):
+    port = 29500 + (os.getpid() % 2000)
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    env.pop("CUDA_VISIBLE_DEVICES", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "scripts", "psx_train.py"),
+           "--cpu"] + args
+    r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-4000:]
+    return M.parse_lines(r.stdout.splitlines()), r.stdout
+
+
+TINY = ["--model", "resnet_tiny", "--batch-size", "8", "--epochs", "1", "--train-samples", "96",
+        "--test-samples", "16", "--eval-every", "1", "--verbose", "0", "--no-graph", "--lr", "0.05"]
+
+
+@pytest.mark.parametrize("topology", ["colocated", "dedicated"])
+def test_dist_sync_gloo(topology):
+    recs, out = _spawn(3, ["--mode", "sync", "--topology", topology] + TINY)
+    W = 3 if topology == "colocated" else 2
+    srv = [r for r in recs if r["type"] == "SERVER_FINAL_METRICS"]
+    wks = [r for r in recs if r["type"] == "WORKER_FINAL_METRICS"]
+    assert len(srv) == 1 and len(wks) == W
+    steps = -(-(96 // W + 96 % W) // 8)
+    assert srv[0]["global_steps_completed"] == steps
+    assert srv[0]["gradients_processed"] == W * steps
+    assert sorted(w["worker_id"] for w in wks) == list(range(W))
+    assert srv[0]["topology"] == topology and srv[0]["gpus"] == 3
+
+
+def test_dist_async_gloo():
+    recs, out = _spawn(3, ["--mode", "async", "--staleness-bound", "50"] + TINY)
+    srv = [r for r in recs if r["type"] == "SERVER_FINAL_METRICS"][0]
+    wks = [r for r in recs if r["type"] == "WORKER_FINAL_METRICS"]
+    assert len(wks) == 3
+    total = sum(w["local_steps_completed"] for w in wks)
+    assert srv["gradients_processed"] == total
+    assert srv["global_steps_completed"] == srv["async_updates"] == total - srv["rejected_pushes"]
+    assert sum(srv["staleness_histogram"]) == srv["async_updates"]

@@ -243,13 +243,16 @@ def _dedicated_sync_server(cfg, server, chan, steps, device):
     gradient contribution and applies the averaged update."""
     K = max(1, cfg.sync_steps)
     zeros = torch.zeros(server.n, dtype=_wire_dtype(cfg), device=device)
+    zbuf = torch.zeros(server.layout.buffer_numel, dtype=torch.float32, device=device) if cfg.bn_sync else None
     done = 0
     for epoch in range(cfg.epochs):
         for b in range(steps):
             if b % K == 0:
                 chan.fetch(None, None)
                 zeros.zero_()
-                chan.push(None, zeros, server.core.global_step)
+                if zbuf is not None:
+                    zbuf.zero_()
+                chan.push(None, zeros, server.core.global_step, buffers=zbuf)
             done += 1
             if cfg.max_steps and done >= cfg.max_steps:
                 return

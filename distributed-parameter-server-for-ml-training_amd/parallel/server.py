@@ -121,12 +121,14 @@ class ParameterServer:
                     self._accumulate(sum(self._pending.values()), True)
                     self._pending.clear()
                     self.apply(self.agg, res.weight)
+                    self._commit_buffers()
                 return True  # the reference always answers received=True in sync mode
             if res.decision in (WAIT, APPLY):
                 self._accumulate(grads, self._round_count == 0)
                 self._round_count += 1
             if res.apply:
                 self.apply(self.agg, res.weight)
+                self._commit_buffers()
                 self._round_count = 0
             return res.accepted
         if res.apply:
@@ -136,6 +138,33 @@ class ParameterServer:
     _round_count = 0
     _pending: dict = {}
     last_push = None
+    _buf_acc = None
+    _buf_n = 0
+
+    # ------------------------------------------------------------------ BN running stats (--bn-sync)
+    def push_buffers(self, worker_id: int, bufs: torch.Tensor):
+        """Worker BN running statistics (float buffer region of its local arena). Sync: averaged
+        over the round (committed with the round's update); async: blended with weight 1/W."""
+        if self.layout.buffer_numel == 0:
+            return
+        region = self.arena[self.n:]
+        if self.cfg.mode == "sync":
+            if self._buf_acc is None:
+                self._buf_acc = torch.zeros_like(region)
+            self._buf_acc.add_(bufs.to(region.device))
+            self._buf_n += 1
+        else:
+            w = 1.0 / max(1, self.total_workers)
+            region.mul_(1.0 - w).add_(bufs.to(region.device), alpha=w)
+
+    def _commit_buffers(self):
+        if self._buf_n:
+            self.arena[self.n:].copy_(self._buf_acc / self._buf_n)
+            self._buf_acc.zero_()
+            self._buf_n = 0
+
+    def set_buffers_from_sum(self, summed: torch.Tensor, count: int):
+        self.arena[self.n:].copy_(summed / max(1, count))
 
     def job_finished(self, worker_id: int, emit: bool = True) -> str:
         """Reference server.py:306-318: when the last active worker finishes, print the final
@@ -153,7 +182,8 @@ class ParameterServer:
     JobFinished = job_finished
 
     # ------------------------------------------------------------------ sync (collective) path
-    def apply_reduced(self, summed: torch.Tensor, members: list[int], local_steps: list[int]) -> bool:
+    def apply_reduced(self, summed: torch.Tensor, members: list[int], local_steps: list[int],
+                      buffers_sum: torch.Tensor | None = None) -> bool:
         """Bookkeeping + update for one sync round whose gradient sum arrived by RCCL reduce."""
         res = None
         for wid, ls in zip(members, local_steps):
@@ -161,6 +191,8 @@ class ParameterServer:
         self.bytes_pushed += len(members) * self.n * summed.element_size()
         if res is not None and res.apply:
             self.apply(summed, res.weight)
+            if buffers_sum is not None:
+                self.set_buffers_from_sum(buffers_sum, len(members))
             return True
         return False
 
@@ -223,6 +255,7 @@ class ParameterServer:
         wire_dtype = torch.float16 if self.cfg.codec == "fp16" else torch.float32
         slots = {w: torch.empty(n, dtype=wire_dtype, device=self.device) for w in rank_of}
         snaps = {w: torch.empty_like(self.arena) for w in rank_of}
+        bufslots = {}
         pending_recv = []   # (wid, local_step, work)
         pending_send = {}   # wid -> work
         done = set()
@@ -246,7 +279,14 @@ class ParameterServer:
                     self.bytes_fetched += self.arena.numel() * 4
                     mbox.reply(rank_of[wid], CP.Msg(CP.R_FETCHED, 0, wid, 0, gs))
                 elif t == CP.PUSH:
-                    pending_recv.append((wid, msg.c, transport.irecv(slots[wid], rank_of[wid])))
+                    work = transport.irecv(slots[wid], rank_of[wid])
+                    bwork = None
+                    if msg.b:  # BN running statistics follow the gradients (--bn-sync)
+                        if wid not in bufslots:
+                            bufslots[wid] = torch.empty(self.layout.buffer_numel, dtype=torch.float32,
+                                                        device=self.device)
+                        bwork = transport.irecv(bufslots[wid], rank_of[wid])
+                    pending_recv.append((wid, msg.c, work, bwork))
                 elif t == CP.DONE:
                     finished.add(wid)
                     self.core.job_finished(wid)
@@ -258,17 +298,21 @@ class ParameterServer:
                     break
             # complete arrived pushes in arrival order
             keep = []
-            for wid, ls, work in pending_recv:
+            for wid, ls, work, bwork in pending_recv:
                 if transport.completed(work):  # each work is waited exactly once (gloo!)
+                    if bwork is not None:
+                        transport.completed(bwork) or bwork.wait()
                     res = self.core.on_push(wid, ls)
                     self.bytes_pushed += n * slots[wid].element_size()
                     if res.apply:
                         self.apply(slots[wid], res.weight)
+                        if bwork is not None:
+                            self.push_buffers(wid, bufslots[wid])
                         self.maybe_checkpoint()
                     mbox.reply(rank_of[wid], CP.Msg(CP.R_PUSHED, 0, wid, int(res.accepted), self.core.global_step,
                                                     res.staleness))
                 else:
-                    keep.append((wid, ls, work))
+                    keep.append((wid, ls, work, bwork))
             pending_recv = keep
             stop = False
             if local_queue is not None:
@@ -282,6 +326,8 @@ class ParameterServer:
                         self.bytes_pushed += n * grads.element_size()
                         if res.apply:
                             self.apply(grads, res.weight)
+                            if box.get("bufs") is not None:
+                                self.push_buffers(wid, box["bufs"])
                             self.maybe_checkpoint()
                         box["res"] = res
                         box["global_step"] = self.core.global_step

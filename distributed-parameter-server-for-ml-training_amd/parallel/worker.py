@@ -45,7 +45,9 @@ class InProcessChannel:
         local_arena.copy_(arena)
         return gs
 
-    def push(self, worker_id, grads, local_step):
+    def push(self, worker_id, grads, local_step, buffers=None):
+        if buffers is not None:
+            self.server.push_buffers(worker_id, buffers)
         return self.server.push_gradients(worker_id, grads, local_step)
 
     def finished(self, worker_id):
@@ -83,10 +85,12 @@ class SyncCollectiveChannel:
         self._gs = getattr(self, "_gs", 0)
         return self._gs
 
-    def push(self, worker_id, grads, local_step):
+    def push(self, worker_id, grads, local_step, buffers=None):
         self.t.reduce_sum_to_server(grads)
+        if buffers is not None:
+            self.t.reduce_sum_to_server(buffers)
         if self.server is not None:
-            self.server.apply_reduced(grads, self.members, [local_step] * len(self.members))
+            self.server.apply_reduced(grads, self.members, [local_step] * len(self.members), buffers_sum=buffers)
             self.server.maybe_checkpoint()
         else:
             self._gs = getattr(self, "_gs", 0) + 1
@@ -112,9 +116,12 @@ class AsyncChannel:
         work.wait()
         return r.c
 
-    def push(self, worker_id, grads, local_step):
-        self.mbox.send(CP.Msg(CP.PUSH, self.rank, worker_id, 0, local_step))
-        self.t.isend(grads, 0).wait()
+    def push(self, worker_id, grads, local_step, buffers=None):
+        self.mbox.send(CP.Msg(CP.PUSH, self.rank, worker_id, int(buffers is not None), local_step))
+        w = self.t.isend(grads, 0)
+        if buffers is not None:
+            self.t.isend(buffers, 0).wait()
+        w.wait()
         r = self.mbox.wait_reply(self.rank)
         self.last_staleness = r.d
         return bool(r.b)
@@ -136,8 +143,8 @@ class LocalAsyncChannel:
         local_arena.copy_(self.server.arena)
         return gs
 
-    def push(self, worker_id, grads, local_step):
-        ev, box = threading.Event(), {}
+    def push(self, worker_id, grads, local_step, buffers=None):
+        ev, box = threading.Event(), {"bufs": buffers}
         self.q.put(("push", worker_id, grads, local_step, ev, box))
         ev.wait()
         return box["res"].accepted
@@ -194,7 +201,10 @@ class Worker:
         return self.global_step_cache
 
     def push_gradients(self):
-        ok = self.channel.push(self.worker_id, self.compute.grads, self.global_step_cache)
+        bufs = None
+        if self.cfg.bn_sync:
+            bufs = self.compute.local_arena[self.compute.layout.param_numel:]
+        ok = self.channel.push(self.worker_id, self.compute.grads, self.global_step_cache, buffers=bufs)
         if not ok:
             self.pushes_rejected += 1
         return ok

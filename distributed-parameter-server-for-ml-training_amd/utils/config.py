@@ -53,6 +53,11 @@ class PSConfig:
     momentum: float = 0.0          # server optimizer (0 = reference plain SGD, server.py:133)
     weight_decay: float = 0.0
     sync_semantics: str = "barrier"  # barrier (wait-for-N) | reference (count-triggered)
+    # The reference server never updates BN running statistics and every fetch overwrites the
+    # workers' copies (server.py:96,131-133 + worker.py:252), so evaluation runs on near-initial
+    # statistics. bn_sync=True makes workers push their running stats with each gradient push;
+    # the server averages them (sync) or blends them 1/W (async). Default off = reference parity.
+    bn_sync: bool = False
     synthetic: bool = True
     data_dir: str = ""
     train_samples: int = 50000
@@ -115,6 +120,7 @@ def add_arguments(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     A("--momentum", type=float, default=None)
     A("--weight-decay", type=float, default=None)
     A("--sync-semantics", choices=["barrier", "reference"], default=None)
+    A("--bn-sync", action="store_true", default=None, help="workers push BN running stats; server averages")
     A("--synthetic", action="store_true", default=None)
     A("--data-dir", default=None, help="directory with cifar-100-binary/{train,test}.bin")
     A("--train-samples", type=int, default=None)

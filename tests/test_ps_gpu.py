@@ -23,7 +23,7 @@ def cfg(**kw):
 
 
 def test_sync_single_worker_loss_decreases(capsys):
-    c = cfg(mode="sync", workers=1, epochs=3, train_samples=6400, eval_every=3)
+    c = cfg(mode="sync", workers=1, epochs=3, train_samples=6400, eval_every=3, bn_sync=True)
     res = run_local(c, log=lambda *a, **k: None)
     recs = M.parse_lines(capsys.readouterr().out.splitlines())
     w = [r for r in recs if r["type"] == "WORKER_FINAL_METRICS"][0]

@@ -20,22 +20,27 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
                                                           float* __restrict__ scale, float* __restrict__ shift,
                                                           float* __restrict__ save_mean,
                                                           float* __restrict__ save_invstd) {
-  __shared__ double red[2][4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int lane4 = threadIdx.x >> 6;
-  double s = 0.0, ss = 0.0;
+  // 8 slot groups x 32 channels per block (T slot rows read with 8-way parallelism)
+  __shared__ double red[2][8][32];
+  const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  float fs = 0.f, fss = 0.f;
   if (c < C) {
-    for (int t = lane4; t < T; t += 4) {
-      s += part[((size_t)t * 2 + 0) * C + c];
-      ss += part[((size_t)t * 2 + 1) * C + c];
+    for (int t = grp; t < T; t += 8) {
+      fs += part[((size_t)t * 2 + 0) * C + c];
+      fss += part[((size_t)t * 2 + 1) * C + c];
     }
   }
-  red[0][lane4][threadIdx.x & 63] = s;
-  red[1][lane4][threadIdx.x & 63] = ss;
+  red[0][grp][cl] = fs;
+  red[1][grp][cl] = fss;
   __syncthreads();
-  if (lane4 == 0 && c < C) {
-    s = red[0][0][threadIdx.x] + red[0][1][threadIdx.x] + red[0][2][threadIdx.x] + red[0][3][threadIdx.x];
-    ss = red[1][0][threadIdx.x] + red[1][1][threadIdx.x] + red[1][2][threadIdx.x] + red[1][3][threadIdx.x];
+  if (grp == 0 && c < C) {
+    double s = 0.0, ss = 0.0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      s += red[0][g][cl];
+      ss += red[1][g][cl];
+    }
     const double mean = s / count;
     double var = ss / count - mean * mean;
     if (var < 0.0) var = 0.0;
@@ -186,12 +191,26 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int T, in
                                        const float* __restrict__ gamma, const float* __restrict__ mean,
                                        const float* __restrict__ invstd, float* __restrict__ coef,
                                        GT* __restrict__ dgamma, GT* __restrict__ dbeta, float gscale) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  // 8 slot groups x 32 channels per block: the T slot rows are read with 8-way parallelism
+  __shared__ float red[2][8][32];
+  const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+    for (int t = grp; t < T; t += 8) {
+      a += part[((size_t)t * NS + 0) * C + c];
+      b += part[((size_t)t * NS + which) * C + c];
+    }
+  }
+  red[0][grp][cl] = a;
+  red[1][grp][cl] = b;
+  __syncthreads();
+  if (grp != 0 || c >= C) return;
   double sdz = 0.0, sxh = 0.0;
-  for (int t = 0; t < T; ++t) {
-    sdz += part[((size_t)t * NS + 0) * C + c];
-    sxh += part[((size_t)t * NS + which) * C + c];
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    sdz += red[0][g][cl];
+    sxh += red[1][g][cl];
   }
   const float mdz = (float)(sdz / count), mxh = (float)(sxh / count);
   const float is = invstd[c], gm = gamma[c];
@@ -269,7 +288,7 @@ extern "C" {
 int psx_bn_finalize(const float* part, int T, int C, float count, const float* gamma, const float* beta, float eps,
                     float momentum, float* run_mean, float* run_var, float* scale, float* shift, float* save_mean,
                     float* save_invstd, hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, part, T, C, count, gamma, beta, eps,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, st, part, T, C, count, gamma, beta, eps,
                      momentum, run_mean, run_var, scale, shift, save_mean, save_invstd);
   return (int)hipGetLastError();
 }
@@ -329,7 +348,7 @@ int psx_bn_bwd_reduce(const void* g, const void* o, const void* y1, const float*
 int psx_bn_bwd_finalize(const float* part, int T, int NS, int which, int C, float count, const float* gamma,
                         const float* mean, const float* invstd, float* coef, void* dgamma, void* dbeta, float gscale,
                         int grad_fp16, hipStream_t st) {
-  const dim3 grid((C + 255) / 256);
+  const dim3 grid((C + 31) / 32);
   if (grad_fp16)
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<uint16_t>, grid, dim3(256), 0, st, part, T, NS, which, C, count, gamma,
                        mean, invstd, coef, (uint16_t*)dgamma, (uint16_t*)dbeta, gscale);

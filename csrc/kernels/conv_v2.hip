@@ -1,0 +1,464 @@
+// Implicit-GEMM convolution v2: LDS-DMA (global_load_lds) operand staging, 3-stage LDS ring
+// with counted vmcnt waits, optional split-K. Forward conv and data-gradient conv.
+//
+// Same math as conv_gemm.hip (v1) — see there for the GEMM formulation and the MFMA
+// orientation — but the mainloop is built for CDNA4 latency hiding:
+//   * operands go HBM/L2 -> LDS with `global_load_lds_dwordx4` (no VGPR staging). The im2col
+//     gather is expressed through the per-lane *source* address (any pixel / tap / channel
+//     chunk, zero padding = a pointer to a 16-byte zero page), while the LDS destination stays
+//     lane-linear (cdna_hip_programming.md §5 'Async global->LDS copy', rule 21): the XOR swizzle
+//     of the K-major tile is applied on the source side and undone on the fragment read.
+//   * 3 LDS stages: k-step t+2 is in flight while t is consumed; one raw s_barrier per k-step,
+//     preceded by a counted `s_waitcnt vmcnt(N)` that retires only the stage about to be read.
+//   * split-K over the GEMM-K dimension (blockIdx.y) for the small-M layers (ResNet stages 3-4),
+//     writing fp32 slabs that conv_splitk_epilogue reduces (+ bf16 store, residual, BN stats).
+// Kernel selection lives in psx_conv_fwd2 / psx_conv_dgrad2 (shape-driven).
+#include "common.hpp"
+
+namespace psx {
+
+struct Conv2Args {
+  const uint16_t* in;    // NHWC [Nb][IH][IW][IC] gathered operand
+  const uint16_t* w;     // [OC][Kg] bf16 (K-contiguous, zero padded)
+  uint16_t* out;         // NHWC [Nb][OH][OW][OC]
+  const uint16_t* res;   // optional residual (same shape as out)
+  float* stats;          // optional BN partial sums [PSX_STAT_SLOTS][2][OC]
+  float* part;           // split-K fp32 slabs [splits][npix][OC]
+  const uint16_t* zero;  // 16-byte zero page (DMA source for padding)
+  int Nb, IH, IW, IC, OH, OW, OC, R, S, pad, stride;
+  int Kg, log2_icc, npix;
+  int n_oc_tiles, n_pix_tiles, splits, kps;  // kps: k-steps per split
+};
+
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+PSX_DEV void glds16(const void* g, unsigned char* lds) {
+  __builtin_amdgcn_global_load_lds((gptr_t)g, (lptr_t)lds, 16, 0, 0);
+}
+
+template <int N>
+PSX_DEV void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+PSX_DEV int kmaj2(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+template <int MODE>
+PSX_DEV const uint16_t* gather_src(const Conv2Args& a, int nbase, int hb, int wb, bool pv, int gk) {
+  const int tap = gk >> a.log2_icc;
+  const int c0 = (gk & ((1 << a.log2_icc) - 1)) << 3;
+  if (!pv || tap >= a.R * a.S) return a.zero;
+  const int r = tap / a.S, s = tap - r * a.S;
+  int ih, iw;
+  if (MODE == 0) {
+    ih = hb + r;
+    iw = wb + s;
+  } else {
+    const int th = hb - r, tw = wb - s;
+    if (MODE == 2) {
+      if ((th | tw) & 1) return a.zero;
+      ih = th >> 1;
+      iw = tw >> 1;
+    } else {
+      ih = th;
+      iw = tw;
+    }
+  }
+  if ((unsigned)ih >= (unsigned)a.IH || (unsigned)iw >= (unsigned)a.IW) return a.zero;
+  return a.in + ((size_t)(nbase + ih * a.IW + iw) * a.IC + c0);
+}
+
+template <int BM, int BN, int MODE, bool HAS_RES, bool SPLIT>
+__global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
+  constexpr int NSTAGE = 3;
+  constexpr int MT = BM / 32, NT = BN / 32;   // 16x16 MFMA tiles per wave (2x2 waves)
+  constexpr int LA = BM / 32, LB = BN / 32;   // DMA instructions per wave per stage
+  constexpr int STAGE = (BM + BN) * 128;      // bytes per stage
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nwg = a.n_oc_tiles * a.n_pix_tiles;
+  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int oc_t = tile % a.n_oc_tiles, pix_t = tile / a.n_oc_tiles;
+  const int oc0 = oc_t * BM, pix0 = pix_t * BN;
+  const int split = SPLIT ? blockIdx.y : 0;
+  const int ks0 = split * a.kps;
+  const int nk = SPLIT ? min(a.kps, a.Kg / 64 - ks0) : a.Kg / 64;
+
+  // ---- per-lane DMA source state (fixed across k-steps) ----
+  const int lrow = lane >> 3, lpos = lane & 7;
+  const uint16_t* wsrc[LA];
+#pragma unroll
+  for (int i = 0; i < LA; ++i) {
+    const int row = (i * 4 + wid) * 8 + lrow;
+    const int c = lpos ^ ((row >> 1) & 7);
+    wsrc[i] = a.w + (size_t)(oc0 + row) * a.Kg + c * 8;
+  }
+  int nbase[LB], hb[LB], wb[LB], bc[LB];
+  bool pv[LB];
+#pragma unroll
+  for (int i = 0; i < LB; ++i) {
+    const int row = (i * 4 + wid) * 8 + lrow;
+    bc[i] = lpos ^ ((row >> 1) & 7);
+    const int pix = pix0 + row;
+    pv[i] = pix < a.npix;
+    const int pp = pv[i] ? pix : 0;
+    const int ohw = a.OH * a.OW;
+    const int n = pp / ohw, rem = pp - n * ohw;
+    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+    nbase[i] = n * a.IH * a.IW;
+    if (MODE == 0) {
+      hb[i] = oh * a.stride - a.pad;
+      wb[i] = ow * a.stride - a.pad;
+    } else {
+      hb[i] = oh + a.pad;
+      wb[i] = ow + a.pad;
+    }
+  }
+
+  auto issue = [&](int ks, int stage) {
+    unsigned char* base = smem + stage * STAGE;
+    const int kglob = ks0 + ks;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) glds16(wsrc[i] + kglob * 64, base + (i * 4 + wid) * 1024);
+#pragma unroll
+    for (int i = 0; i < LB; ++i)
+      glds16(gather_src<MODE>(a, nbase[i], hb[i], wb[i], pv[i], kglob * 8 + bc[i]),
+             base + BM * 128 + (i * 4 + wid) * 1024);
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  const int frow = lane & 15, fch = lane >> 4;
+  int stage = 0;
+  for (int ks = 0; ks < nk; ++ks) {
+    if (ks + 1 < nk)
+      wait_vmcnt<LA + LB>();
+    else
+      wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (ks + 2 < nk) issue(ks + 2, stage == 0 ? 2 : stage - 1);
+    const unsigned char* A = smem + stage * STAGE;
+    const unsigned char* B = A + BM * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[MT], fb[NT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        fa[m] = *reinterpret_cast<const bf16x8*>(A + kmaj2(wm * (BM / 2) + m * 16 + frow, kk * 4 + fch));
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+        fb[n] = *reinterpret_cast<const bf16x8*>(B + kmaj2(wn * (BN / 2) + n * 16 + frow, kk * 4 + fch));
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
+    }
+    stage = stage == 2 ? 0 : stage + 1;
+  }
+
+  if constexpr (SPLIT) {
+    float* dst = a.part + (size_t)split * a.npix * a.OC;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const int pix = pix0 + wn * (BN / 2) + n * 16 + (lane & 15);
+      if (pix >= a.npix) continue;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int oc = oc0 + wm * (BM / 2) + m * 16 + 4 * (lane >> 4);
+        *reinterpret_cast<f32x4*>(dst + (size_t)pix * a.OC + oc) = acc[m][n];
+      }
+    }
+    return;
+  }
+
+  // ---- epilogue: bf16 NHWC store (+residual), BN partial statistics ----
+  float s1[MT][4], s2[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s1[m][i] = s2[m][i] = 0.f;
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int pix = pix0 + wn * (BN / 2) + n * 16 + (lane & 15);
+    const bool ok = pix < a.npix;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int oc = oc0 + wm * (BM / 2) + m * 16 + 4 * (lane >> 4);
+      float v0 = acc[m][n][0], v1 = acc[m][n][1], v2 = acc[m][n][2], v3 = acc[m][n][3];
+      if (ok) {
+        const size_t off = (size_t)pix * a.OC + oc;
+        if (HAS_RES) {
+          const u32x2 rr = *reinterpret_cast<const u32x2*>(a.res + off);
+          v0 += lo_bf(rr[0]); v1 += hi_bf(rr[0]); v2 += lo_bf(rr[1]); v3 += hi_bf(rr[1]);
+        }
+        u32x2 o;
+        o[0] = pack_bf2(v0, v1);
+        o[1] = pack_bf2(v2, v3);
+        *reinterpret_cast<u32x2*>(a.out + off) = o;
+        if (a.stats) {
+          const float q0 = lo_bf(o[0]), q1 = hi_bf(o[0]), q2 = lo_bf(o[1]), q3 = hi_bf(o[1]);
+          s1[m][0] += q0; s2[m][0] += q0 * q0;
+          s1[m][1] += q1; s2[m][1] += q1 * q1;
+          s1[m][2] += q2; s2[m][2] += q2 * q2;
+          s1[m][3] += q3; s2[m][3] += q3 * q3;
+        }
+      }
+    }
+  }
+  if (a.stats) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s1[m][i] += __shfl_xor(s1[m][i], o, 64);
+          s2[m][i] += __shfl_xor(s2[m][i], o, 64);
+        }
+      }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [2 wn][2][BM]
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = wm * (BM / 2) + m * 16 + 4 * (lane >> 4) + i;
+          red[(wn * 2 + 0) * BM + row] = s1[m][i];
+          red[(wn * 2 + 1) * BM + row] = s2[m][i];
+        }
+    }
+    __syncthreads();
+    float* dst = a.stats + (size_t)(pix_t & (PSX_STAT_SLOTS - 1)) * 2 * a.OC;
+    for (int j = tid; j < 2 * BM; j += 256) {
+      const int which = j / BM, row = j - which * BM;
+      atomicAdd(dst + which * a.OC + oc0 + row, red[which * BM + row] + red[(2 + which) * BM + row]);
+    }
+  }
+}
+
+// Split-K epilogue: out = bf16(sum_s part[s] (+res)); BN partial statistics into slot rows.
+// Block = 256 threads; thread owns 8 channels of a pixel; blocks stride over pixel ranges.
+template <bool HAS_RES>
+__global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restrict__ part, int splits, int npix,
+                                                            int OC, uint16_t* __restrict__ out,
+                                                            const uint16_t* __restrict__ res,
+                                                            float* __restrict__ stats, int pix_per_block) {
+  extern __shared__ __attribute__((aligned(16))) float sred[];  // [256][16]
+  const int cvec = OC >> 3, tpp = 256 / cvec;
+  const int cg = threadIdx.x % cvec, pr = threadIdx.x / cvec;
+  const size_t slab = (size_t)npix * OC;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  const int pbeg = blockIdx.x * pix_per_block, pend = min(npix, pbeg + pix_per_block);
+  for (int p = pbeg + pr; p < pend; p += tpp) {
+    const size_t off = (size_t)p * OC + cg * 8;
+    f32x4 x0 = *reinterpret_cast<const f32x4*>(part + off);
+    f32x4 x1 = *reinterpret_cast<const f32x4*>(part + off + 4);
+    for (int s = 1; s < splits; ++s) {
+      x0 += *reinterpret_cast<const f32x4*>(part + s * slab + off);
+      x1 += *reinterpret_cast<const f32x4*>(part + s * slab + off + 4);
+    }
+    float v[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    if (HAS_RES) {
+      const u32x4 r = *reinterpret_cast<const u32x4*>(res + off);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[2 * j] += lo_bf(r[j]);
+        v[2 * j + 1] += hi_bf(r[j]);
+      }
+    }
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = pack_bf2(v[2 * j], v[2 * j + 1]);
+    *reinterpret_cast<u32x4*>(out + off) = o;
+    if (stats) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float q0 = lo_bf(o[j]), q1 = hi_bf(o[j]);
+        s1[2 * j] += q0; s2[2 * j] += q0 * q0;
+        s1[2 * j + 1] += q1; s2[2 * j + 1] += q1 * q1;
+      }
+    }
+  }
+  if (!stats) return;
+  float* mine = sred + threadIdx.x * 16;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mine[j] = s1[j];
+    mine[8 + j] = s2[j];
+  }
+  __syncthreads();
+  float* dst = stats + (size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * 2 * OC;
+  for (int t = threadIdx.x; t < cvec * 16; t += 256) {
+    const int cgi = t / 16, sj = t - cgi * 16;
+    float acc = 0.f;
+    for (int q = 0; q < tpp; ++q) acc += sred[(q * cvec + cgi) * 16 + sj];
+    const int which = sj >> 3, j = sj & 7;
+    atomicAdd(dst + which * OC + cgi * 8 + j, acc);
+  }
+}
+
+}  // namespace psx
+
+using namespace psx;
+
+namespace {
+
+int ilog2i(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+
+struct Plan {
+  int BM, BN, splits;
+};
+
+// Tile / split-K plan: prefer >= 2 workgroups per CU; split-K only while each split keeps
+// >= 8 k-steps.
+Plan plan_for(int OC, int npix, int ksteps) {
+  Plan p{64, 128, 1};
+  if (OC % 128 == 0 && (long)(OC / 128) * ((npix + 127) / 128) >= 512) {
+    p.BM = 128;
+    p.BN = 128;
+  } else if ((long)(OC / 64) * ((npix + 127) / 128) >= 512) {
+    p.BM = 64;
+    p.BN = 128;
+  } else {
+    p.BM = 64;
+    p.BN = 64;
+  }
+  const long tiles = (long)(OC / p.BM) * ((npix + p.BN - 1) / p.BN);
+  while (p.splits < 8 && tiles * p.splits < 512 && ksteps / (p.splits * 2) >= 8) p.splits *= 2;
+  return p;
+}
+
+template <int BM, int BN, int MODE, bool RES, bool SPLIT>
+int launch2(const Conv2Args& a, hipStream_t st) {
+  const size_t lds = (size_t)3 * (BM + BN) * 128;
+  dim3 grid(a.n_oc_tiles * a.n_pix_tiles, SPLIT ? a.splits : 1);
+  hipLaunchKernelGGL((conv2_kernel<BM, BN, MODE, RES, SPLIT>), grid, dim3(256), lds, st, a);
+  return (int)hipGetLastError();
+}
+
+template <int MODE, bool RES>
+int dispatch2(const Plan& p, const Conv2Args& a, hipStream_t st) {
+  const bool sp = p.splits > 1;
+#define PSX_L2(BM_, BN_)                                                                       \
+  if (p.BM == BM_ && p.BN == BN_)                                                              \
+    return sp ? launch2<BM_, BN_, MODE, false, true>(a, st) : launch2<BM_, BN_, MODE, RES, false>(a, st);
+  PSX_L2(128, 128)
+  PSX_L2(64, 128)
+  PSX_L2(64, 64)
+#undef PSX_L2
+  return -7;
+}
+
+int finish_split(const Conv2Args& a, hipStream_t st) {
+  const int cvec = a.OC / 8;
+  if (256 % cvec) return -8;
+  int ppb = (a.npix + 511) / 512;
+  if (ppb < 8) ppb = 8;
+  const int grid = (a.npix + ppb - 1) / ppb;
+  const size_t lds = 256 * 16 * sizeof(float);
+  if (a.res)
+    hipLaunchKernelGGL(conv_splitk_epilogue<true>, dim3(grid), dim3(256), lds, st, a.part, a.splits, a.npix, a.OC,
+                       a.out, a.res, a.stats, ppb);
+  else
+    hipLaunchKernelGGL(conv_splitk_epilogue<false>, dim3(grid), dim3(256), lds, st, a.part, a.splits, a.npix, a.OC,
+                       a.out, (const uint16_t*)nullptr, a.stats, ppb);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+// Bytes of fp32 split-K workspace the v2 conv needs for this problem (0 = no split).
+long psx_conv2_workspace(int Nb, int OH, int OW, int OC, int Kg) {
+  const int npix = Nb * OH * OW;
+  const Plan p = plan_for(OC, npix, Kg / 64);
+  return p.splits > 1 ? (long)p.splits * npix * OC * 4 : 0;
+}
+
+// Forward conv (v2). Same operands as psx_conv_fwd plus a 16-byte zero page and a split-K
+// workspace (>= psx_conv2_workspace bytes, may be null when that is 0).
+int psx_conv_fwd2(const void* x, const void* wf, void* y, float* stats, const void* zero, float* ws, int Nb, int H,
+                  int W, int IC, int OC, int R, int S, int stride, int pad, int Kg, hipStream_t st) {
+  Conv2Args a{};
+  a.in = (const uint16_t*)x;
+  a.w = (const uint16_t*)wf;
+  a.out = (uint16_t*)y;
+  a.res = nullptr;
+  a.stats = stats;
+  a.part = ws;
+  a.zero = (const uint16_t*)zero;
+  a.Nb = Nb; a.IH = H; a.IW = W; a.IC = IC;
+  a.OH = (H + 2 * pad - R) / stride + 1;
+  a.OW = (W + 2 * pad - S) / stride + 1;
+  a.OC = OC; a.R = R; a.S = S; a.pad = pad; a.stride = stride;
+  a.Kg = Kg;
+  a.log2_icc = ilog2i(IC / 8);
+  a.npix = Nb * a.OH * a.OW;
+  if (OC % 64 || Kg % 64 || IC % 8 || (IC & (IC - 1))) return -2;
+  const Plan p = plan_for(OC, a.npix, Kg / 64);
+  a.n_oc_tiles = OC / p.BM;
+  a.n_pix_tiles = (a.npix + p.BN - 1) / p.BN;
+  a.splits = p.splits;
+  a.kps = (Kg / 64 + p.splits - 1) / p.splits;
+  if (p.splits > 1 && !ws) return -9;
+  int e = dispatch2<0, false>(p, a, st);
+  if (e || p.splits == 1) return e;
+  return finish_split(a, st);
+}
+
+int psx_conv_dgrad2(const void* dy, const void* wd, void* dx, const void* res, const void* zero, float* ws, int Nb,
+                    int H, int W, int IC_fwd, int OC_fwd, int R, int S, int stride, int pad, int Kg, hipStream_t st) {
+  Conv2Args a{};
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  a.in = (const uint16_t*)dy;
+  a.w = (const uint16_t*)wd;
+  a.out = (uint16_t*)dx;
+  a.res = (const uint16_t*)res;
+  a.stats = nullptr;
+  a.part = ws;
+  a.zero = (const uint16_t*)zero;
+  a.Nb = Nb; a.IH = P; a.IW = Q; a.IC = OC_fwd;
+  a.OH = H; a.OW = W; a.OC = IC_fwd;
+  a.R = R; a.S = S; a.pad = pad; a.stride = stride;
+  a.Kg = Kg;
+  a.log2_icc = ilog2i(OC_fwd / 8);
+  a.npix = Nb * H * W;
+  if (IC_fwd % 64 || Kg % 64 || (OC_fwd & (OC_fwd - 1))) return -2;
+  const Plan p = plan_for(IC_fwd, a.npix, Kg / 64);
+  a.n_oc_tiles = IC_fwd / p.BM;
+  a.n_pix_tiles = (a.npix + p.BN - 1) / p.BN;
+  a.splits = p.splits;
+  a.kps = (Kg / 64 + p.splits - 1) / p.splits;
+  if (p.splits > 1 && !ws) return -9;
+  int e;
+  if (stride == 1)
+    e = res ? dispatch2<1, true>(p, a, st) : dispatch2<1, false>(p, a, st);
+  else if (stride == 2)
+    e = res ? dispatch2<2, true>(p, a, st) : dispatch2<2, false>(p, a, st);
+  else
+    return -4;
+  if (e || p.splits == 1) return e;
+  return finish_split(a, st);
+}
+
+}  // extern "C"

@@ -21,6 +21,7 @@ The network is described by a generic block list so ResNet-18 (CIFAR stem) and R
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -169,6 +170,8 @@ class HipResNetEngine:
         self.eps, self.mom = bn_eps, bn_momentum
         self.seed = seed
         self.graph = None
+        # conv kernel generation: 2 = LDS-DMA pipelined + split-K (default), 1 = register-staged
+        self.conv_impl = int(os.environ.get("PSX_CONV_IMPL", "2"))
         self._build()
 
     # ------------------------------------------------------------------ allocation
@@ -237,10 +240,14 @@ class HipResNetEngine:
         max_wg = 0
 
         def track(cs: ConvSpec):
+            # one fp32 scratch serves the wgrad split-K partials and the conv v2 split-K slabs
+            # (all uses are stream-ordered)
             nonlocal max_wg
             s = K.conv_wgrad_splits(B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
             cs.splits = s
-            max_wg = max(max_wg, s * cs.cout * cs.kg)
+            oh, ow = cs.out_hw
+            max_wg = max(max_wg, s * cs.cout * cs.kg, K.conv2_workspace_bytes(B, oh, ow, cs.cout, cs.kg) // 4,
+                         K.conv2_workspace_bytes(B, cs.h, cs.w, cs.cp, cs.kgd) // 4 if cs.need_dgrad else 0)
 
         track(st)
         if sp.maxpool:
@@ -299,10 +306,14 @@ class HipResNetEngine:
     def _conv_fwd(self, cs: ConvSpec, x, y, bs: BNSpec | None):
         oh, ow = cs.out_hw
         npix = self.B * oh * ow
-        cfg = K.pick_tile(cs.cout, npix)
         wf = self.wbuf[cs.wf_off:cs.wf_off + cs.cout * cs.kg]
-        K.conv_fwd(x, wf, y, self._red(bs, "fwd") if bs is not None else None, self.B, cs.h, cs.w, cs.cp, cs.cout,
-                   cs.k, cs.stride, cs.pad, cs.kg, cfg)
+        stats = self._red(bs, "fwd") if bs is not None else None
+        if self.conv_impl == 2:
+            K.conv_fwd2(x, wf, y, stats, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
+                        cs.kg)
+        else:
+            K.conv_fwd(x, wf, y, stats, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg,
+                       K.pick_tile(cs.cout, npix))
         return self.nslots, npix
 
     def _bn_train(self, bs: BNSpec, arena, T, count):
@@ -325,7 +336,11 @@ class HipResNetEngine:
 
     def _dgrad(self, cs: ConvSpec, dy, dx, res=None):
         wd = self.wbuf[cs.wd_off:cs.wd_off + cs.cp * cs.kgd]
-        K.conv_dgrad(dy, wd, dx, res, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kgd)
+        if self.conv_impl == 2:
+            K.conv_dgrad2(dy, wd, dx, res, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
+                          cs.kgd)
+        else:
+            K.conv_dgrad(dy, wd, dx, res, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kgd)
 
     def _bn_bwd(self, bs: BNSpec, arena, g, o, y, dx, npix, two=None, dzout=None):
         """BN (+ReLU mask from o) backward; two = (bs2, y2, dx2) for a shared-dz second BN."""

@@ -58,6 +58,35 @@ def conv_dgrad(dy, wd, dx, res, nb, h, w, ic_fwd, oc_fwd, k, stride, pad, kgd, c
                                    kgd, cfg, stream_ptr()), "conv_dgrad")
 
 
+_ZERO_PAGES = {}
+
+
+def zero_page(device=None):
+    """16-byte-aligned zero block used as the DMA source for conv padding (conv v2)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    z = _ZERO_PAGES.get(dev)
+    if z is None:
+        z = torch.zeros(64, dtype=torch.uint8, device=dev)
+        _ZERO_PAGES[dev] = z
+    return z
+
+
+def conv2_workspace_bytes(nb, oh, ow, oc, kg) -> int:
+    return int(kernels().psx_conv2_workspace(nb, oh, ow, oc, kg))
+
+
+def conv_fwd2(x, wf, y, stats, ws, nb, h, w, ic, oc, k, stride, pad, kg):
+    """LDS-DMA pipelined implicit-GEMM conv (csrc/kernels/conv_v2.hip); ws: fp32 split-K
+    workspace of >= conv2_workspace_bytes(...) bytes (or None when that is 0)."""
+    check(kernels().psx_conv_fwd2(ptr(x), ptr(wf), ptr(y), ptr(stats), ptr(zero_page(x.device)), ptr(ws), nb, h, w,
+                                  ic, oc, k, k, stride, pad, kg, stream_ptr()), "conv_fwd2")
+
+
+def conv_dgrad2(dy, wd, dx, res, ws, nb, h, w, ic_fwd, oc_fwd, k, stride, pad, kgd):
+    check(kernels().psx_conv_dgrad2(ptr(dy), ptr(wd), ptr(dx), ptr(res), ptr(zero_page(dy.device)), ptr(ws), nb, h,
+                                    w, ic_fwd, oc_fwd, k, k, stride, pad, kgd, stream_ptr()), "conv_dgrad2")
+
+
 def conv_wgrad_splits(nb, h, w, ic, oc, k, stride, pad, kg, splits=0) -> int:
     n = kernels().psx_conv_wgrad(None, None, None, nb, h, w, ic, oc, k, k, stride, pad, kg, splits, None)
     if n <= 0:

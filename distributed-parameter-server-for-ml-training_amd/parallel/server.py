@@ -123,6 +123,11 @@ class ParameterServer:
                     self.apply(self.agg, res.weight)
                     self._commit_buffers()
                 return True  # the reference always answers received=True in sync mode
+            if res.apply and self._round_count == 0:
+                # single-contribution round (W == 1): apply straight from the wire buffer
+                self.apply(grads, res.weight)
+                self._commit_buffers()
+                return True
             if res.decision in (WAIT, APPLY):
                 self._accumulate(grads, self._round_count == 0)
                 self._round_count += 1

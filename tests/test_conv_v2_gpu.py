@@ -1,0 +1,56 @@
+"""conv v2 (LDS-DMA pipelined, split-K) vs torch fp32 on every ResNet-18 conv shape at batch 128."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from psx.ops import kernels as K  # noqa: E402
+from tests.test_kernels_gpu import _pow2, _rel, make_operands, to_nhwc  # noqa: E402
+
+DEV = "cuda"
+SHAPES = [(128, c, o, hw, k, s, p) for (_, c, o, hw, k, s, p) in [
+    (8, 3, 64, 32, 3, 1, 1), (8, 64, 64, 32, 3, 1, 1), (8, 64, 128, 32, 3, 2, 1), (8, 64, 128, 32, 1, 2, 0),
+    (8, 128, 128, 16, 3, 1, 1), (8, 128, 256, 16, 3, 2, 1), (8, 128, 256, 16, 1, 2, 0), (8, 256, 256, 8, 3, 1, 1),
+    (8, 256, 512, 8, 3, 2, 1), (8, 256, 512, 8, 1, 2, 0), (8, 512, 512, 4, 3, 1, 1)]] + [(3, 64, 64, 8, 3, 1, 1)]
+
+
+def _ws(nb, oh, ow, oc, kg):
+    n = K.conv2_workspace_bytes(nb, oh, ow, oc, kg)
+    return torch.empty(max(1, n // 4), dtype=torch.float32, device=DEV) if n else None
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv_fwd2(shape):
+    torch.manual_seed(0)
+    n, cin, cout, hw, k, s, p = shape
+    x = torch.randn(n, cin, hw, hw, device=DEV).to(torch.bfloat16).float()
+    w = (torch.randn(cout, cin, k, k, device=DEV) / (cin * k * k) ** 0.5).to(torch.bfloat16).float()
+    wf, wd, cp, kg, kgd = make_operands(w)
+    oh = (hw + 2 * p - k) // s + 1
+    y = torch.empty(n, oh, oh, cout, dtype=torch.bfloat16, device=DEV)
+    stats = torch.zeros(K.STAT_SLOTS, 2, cout, device=DEV)
+    K.conv_fwd2(to_nhwc(x, cp), wf, y, stats, _ws(n, oh, oh, cout, kg), n, hw, hw, cp, cout, k, s, p, kg)
+    ref = F.conv2d(x, w, stride=s, padding=p).permute(0, 2, 3, 1)
+    assert _rel(y, ref) < 1e-2, shape
+    yq = y.float().reshape(-1, cout)
+    assert torch.allclose(stats[:, 0].sum(0), yq.sum(0), rtol=1e-3, atol=5e-2), shape
+    assert torch.allclose(stats[:, 1].sum(0), (yq * yq).sum(0), rtol=1e-3, atol=5e-2), shape
+
+
+@pytest.mark.parametrize("shape", [s for s in SHAPES if s[1] != 3])
+def test_conv_dgrad2(shape):
+    torch.manual_seed(1)
+    n, cin, cout, hw, k, s, p = shape
+    w = (torch.randn(cout, cin, k, k, device=DEV) / (cin * k * k) ** 0.5).to(torch.bfloat16).float()
+    wf, wd, cp, kg, kgd = make_operands(w)
+    oh = (hw + 2 * p - k) // s + 1
+    dy = torch.randn(n, cout, oh, oh, device=DEV).to(torch.bfloat16).float()
+    ref = torch.nn.grad.conv2d_input((n, cin, hw, hw), w, dy, stride=s, padding=p).permute(0, 2, 3, 1)
+    dx = torch.empty(n, hw, hw, cp, dtype=torch.bfloat16, device=DEV)
+    res = torch.randn(n, hw, hw, cp, device=DEV).to(torch.bfloat16)
+    ws = _ws(n, hw, hw, cp, kgd)
+    K.conv_dgrad2(to_nhwc(dy, cout), wd, dx, None, ws, n, hw, hw, cp, cout, k, s, p, kgd)
+    assert _rel(dx[..., :cin], ref) < 1e-2, shape
+    K.conv_dgrad2(to_nhwc(dy, cout), wd, dx, res, ws, n, hw, hw, cp, cout, k, s, p, kgd)
+    assert _rel(dx[..., :cin], ref + res[..., :cin].float()) < 1e-2, shape

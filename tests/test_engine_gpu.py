@@ -51,32 +51,37 @@ def test_train_step_matches_torch(setup):
     eng.backward(arena_k)
     torch.cuda.synchronize()
 
+    sd_init = {k: v.clone() for k, v in model.state_dict().items()}
     model.train()
     model.zero_grad()
     out = model(x)
     loss = F.cross_entropy(out, y)
     loss.backward()
     ref32 = {n: p.grad.clone() for n, p in model.named_parameters()}
+    sd32 = {k: v.clone() for k, v in model.state_dict().items()}  # running stats after ONE forward
     # torch's own bf16 autocast path sets the precision bar: a randomly initialised ResNet's
     # early-layer gradients are chaotic, so bf16 activations alone move them by a few percent.
     model.zero_grad()
     with torch.autocast("cuda", dtype=torch.bfloat16):
         F.cross_entropy(model(x), y).backward()
     ref16 = {n: p.grad.clone() for n, p in model.named_parameters()}
-    sd_before = {k: v.clone() for k, v in model.state_dict().items()}
     assert abs(eng.loss.mean().item() - loss.item()) < 0.02 * max(1.0, loss.item())
+    ce, cb = [], []
     for name in ref32:
         g = layout.grad_view(eng.grads, name)
         c_eng, c_bf16 = _cos(g, ref32[name]), _cos(ref16[name], ref32[name])
-        assert c_eng > 0.85 and c_eng > c_bf16 - 0.03, (name, c_eng, c_bf16)
+        ce.append(c_eng)
+        cb.append(c_bf16)
+        assert c_eng > 0.85 and c_eng > c_bf16 - 0.06, (name, c_eng, c_bf16)
+    ce.sort()
+    cb.sort()
+    assert ce[len(ce) // 2] > cb[len(cb) // 2] - 0.01, (ce, cb)  # median agreement >= torch bf16's
     assert _cos(eng.grads[-5000:], torch.cat([ref32["fc.weight"].flatten(), ref32["fc.bias"]])[-5000:]) > 0.999
-    model.load_state_dict(sd_before)
+    model.load_state_dict(sd_init)
     # running statistics were updated in the worker-local arena exactly like torch's
-    sd = model.state_dict()
     for name in ("bn1.running_mean", "layer2.0.bn1.running_var", "layer4.1.bn2.running_mean"):
         got = layout.view(arena_k, name)
-        # pre-BN activations of deep layers carry the bf16 forward's few-percent deviation
-        assert torch.allclose(got, sd[name], rtol=5e-2, atol=5e-3), name
+        assert torch.allclose(got, sd32[name], rtol=2e-2, atol=2e-3), name
 
 
 def test_graph_replay_matches_eager(setup):

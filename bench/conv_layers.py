@@ -63,6 +63,18 @@ def main():
             K.wgrad_reduce(part, spl, cout, kg, cin, cp, k, 1.0, out16.data_ptr(), True)
 
         r["wgrad_us"] = t_us(wg)
+        spl2 = K.conv_wgrad2_splits(B, hw, hw, cp, cout, k, s, p, kg)
+        part2 = torch.empty(spl2 * cout * kg, device="cuda")
+
+        def wg2():
+            K.conv_wgrad2(xh, dy, part2, B, hw, hw, cp, cout, k, s, p, kg)
+            K.wgrad_reduce(part2, spl2, cout, kg, cin, cp, k, 1.0, out16.data_ptr(), True)
+
+        r["wgrad_v2_us"] = t_us(wg2)
+        r["wgrad_v2_splits"] = spl2
+        r["wgrad_v2_kernel_us"] = t_us(lambda: K.conv_wgrad2(xh, dy, part2, B, hw, hw, cp, cout, k, s, p, kg))
+        r["wgrad_reduce_us"] = t_us(
+            lambda: K.wgrad_reduce(part2, spl2, cout, kg, cin, cp, k, 1.0, out16.data_ptr(), True))
         xt = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         wt = w.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         r["miopen_fwd_us"] = t_us(lambda: F.conv2d(xt, wt, stride=s, padding=p))

@@ -13,7 +13,7 @@
 //   * split-K over the GEMM-K dimension (blockIdx.y) for the small-M layers (ResNet stages 3-4),
 //     writing fp32 slabs that conv_splitk_epilogue reduces (+ bf16 store, residual, BN stats).
 // Kernel selection lives in psx_conv_fwd2 / psx_conv_dgrad2 (shape-driven).
-#include "common.hpp"
+#include "pipeline.hpp"
 
 namespace psx {
 
@@ -29,18 +29,6 @@ struct Conv2Args {
   int Kg, log2_icc, npix;
   int n_oc_tiles, n_pix_tiles, splits, kps;  // kps: k-steps per split
 };
-
-typedef const __attribute__((address_space(1))) void* gptr_t;
-typedef __attribute__((address_space(3))) void* lptr_t;
-
-PSX_DEV void glds16(const void* g, unsigned char* lds) {
-  __builtin_amdgcn_global_load_lds((gptr_t)g, (lptr_t)lds, 16, 0, 0);
-}
-
-template <int N>
-PSX_DEV void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 PSX_DEV int kmaj2(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 

@@ -243,7 +243,10 @@ class HipResNetEngine:
             # one fp32 scratch serves the wgrad split-K partials and the conv v2 split-K slabs
             # (all uses are stream-ordered)
             nonlocal max_wg
-            s = K.conv_wgrad_splits(B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
+            if self.conv_impl == 2:
+                s = K.conv_wgrad2_splits(B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
+            else:
+                s = K.conv_wgrad_splits(B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
             cs.splits = s
             oh, ow = cs.out_hw
             max_wg = max(max_wg, s * cs.cout * cs.kg, K.conv2_workspace_bytes(B, oh, ow, cs.cout, cs.kg) // 4,
@@ -330,7 +333,11 @@ class HipResNetEngine:
                          self.eps, st["affine"])
 
     def _wgrad(self, cs: ConvSpec, x, dy):
-        K.conv_wgrad(x, dy, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg, cs.splits)
+        if self.conv_impl == 2:
+            K.conv_wgrad2(x, dy, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
+        else:
+            K.conv_wgrad(x, dy, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg,
+                         cs.splits)
         K.wgrad_reduce(self.wpart, cs.splits, cs.cout, cs.kg, cs.cin, cs.cp, cs.k, 1.0, self._gptr(f"{cs.name}.weight"),
                        self.grad_fp16)
 

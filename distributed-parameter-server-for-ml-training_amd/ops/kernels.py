@@ -87,6 +87,22 @@ def conv_dgrad2(dy, wd, dx, res, ws, nb, h, w, ic_fwd, oc_fwd, k, stride, pad, k
                                     w, ic_fwd, oc_fwd, k, k, stride, pad, kgd, stream_ptr()), "conv_dgrad2")
 
 
+def conv_wgrad2_splits(nb, h, w, ic, oc, k, stride, pad, kg) -> int:
+    n = kernels().psx_conv_wgrad2(None, None, None, None, nb, h, w, ic, oc, k, k, stride, pad, kg, None)
+    if n <= 0:
+        raise RuntimeError(f"conv_wgrad2 split query failed ({n})")
+    return n
+
+
+def conv_wgrad2(x, dy, part, nb, h, w, ic, oc, k, stride, pad, kg) -> int:
+    """LDS-DMA pipelined weight gradient (csrc/kernels/wgrad_v2.hip) -> fp32 split slabs in part."""
+    n = kernels().psx_conv_wgrad2(ptr(x), ptr(dy), ptr(part), ptr(zero_page(x.device)), nb, h, w, ic, oc, k, k,
+                                  stride, pad, kg, stream_ptr())
+    if n <= 0:
+        raise RuntimeError(f"conv_wgrad2 failed ({n})")
+    return n
+
+
 def conv_wgrad_splits(nb, h, w, ic, oc, k, stride, pad, kg, splits=0) -> int:
     n = kernels().psx_conv_wgrad(None, None, None, nb, h, w, ic, oc, k, k, stride, pad, kg, splits, None)
     if n <= 0:

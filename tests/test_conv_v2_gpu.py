@@ -38,6 +38,24 @@ def test_conv_fwd2(shape):
     assert torch.allclose(stats[:, 1].sum(0), (yq * yq).sum(0), rtol=1e-3, atol=5e-2), shape
 
 
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv_wgrad2(shape):
+    torch.manual_seed(2)
+    n, cin, cout, hw, k, s, p = shape
+    x = torch.randn(n, cin, hw, hw, device=DEV).to(torch.bfloat16).float()
+    oh = (hw + 2 * p - k) // s + 1
+    dy = torch.randn(n, cout, oh, oh, device=DEV).to(torch.bfloat16).float()
+    ref = torch.nn.grad.conv2d_weight(x, (cout, cin, k, k), dy, stride=s, padding=p)
+    cp = _pow2(cin)
+    kg = -(-(k * k * cp) // 64) * 64
+    splits = K.conv_wgrad2_splits(n, hw, hw, cp, cout, k, s, p, kg)
+    part = torch.full((splits * cout * kg,), float("nan"), device=DEV)  # every slab element must be written
+    assert K.conv_wgrad2(to_nhwc(x, cp), to_nhwc(dy, cout), part, n, hw, hw, cp, cout, k, s, p, kg) == splits
+    out = torch.zeros(cout * cin * k * k, device=DEV)
+    K.wgrad_reduce(part, splits, cout, kg, cin, cp, k, 1.0, out.data_ptr(), False)
+    assert _rel(out.view_as(ref), ref) < 5e-3, shape
+
+
 @pytest.mark.parametrize("shape", [s for s in SHAPES if s[1] != 3])
 def test_conv_dgrad2(shape):
     torch.manual_seed(1)

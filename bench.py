@@ -29,6 +29,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import psx  # noqa: E402,F401
+from psx.parallel.codec import FetchCodec  # noqa: E402
 from psx.parallel.compute import HipCompute  # noqa: E402
 from psx.parallel.runner import build_state, make_datasets  # noqa: E402
 from psx.parallel.server import ParameterServer  # noqa: E402
@@ -48,6 +49,9 @@ def main():
     ap.add_argument("--topology", choices=["colocated", "dedicated"], default="colocated")
     ap.add_argument("--codec", choices=["fp16", "none"], default="fp16")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--fetch-codec", choices=["bf16conv", "fp32"], default="bf16conv",
+                    help="bf16conv: conv weights travel as the bf16 bits the workers compute with (bit-exact "
+                         "worker compute), everything else fp32; fp32: the reference's full fp32 state")
     a = ap.parse_args()
 
     rank, world, local = env_world()
@@ -75,7 +79,8 @@ def main():
         for i in range(W):
             server.register_worker(f"worker-{i}", i)
     train, _ = make_datasets(cfg, device, model.fc.out_features)
-    chan = InProcessChannel(server) if t is None else SyncCollectiveChannel(t, server, members=list(range(W)))
+    chan = InProcessChannel(server) if t is None else SyncCollectiveChannel(
+        t, server, members=list(range(W)), codec=FetchCodec(layout, a.fetch_codec, device))
     wk = None
     zeros = None
     if is_worker:
@@ -142,11 +147,12 @@ def main():
                 "seq_len": None,
                 "parallelism": (f"sync-PS: rank0 = parameter server{' only' if dedicated else ' + worker 0'}, "
                                 f"{W} data-parallel worker(s); RCCL reduce(fp16 grads)+broadcast(fp32 arena) "
-                                f"over xGMI" if world > 1 else "sync-PS: server + 1 worker co-located on 1 GPU"),
+                                f"over xGMI" if t is not None else "sync-PS: server + 1 worker co-located on 1 GPU"),
                 "lr": 0.1,
                 "sync_steps": 1,
                 "codec": a.codec,
-                "topology": "dedicated" if dedicated else ("colocated" if world > 1 else "loopback"),
+                "fetch_codec": a.fetch_codec if t is not None else "in-process",
+                "topology": "dedicated" if dedicated else ("colocated" if t is not None else "loopback"),
                 "hip_graph": cfg.use_graph,
             },
             "global_steps": server.core.global_step,

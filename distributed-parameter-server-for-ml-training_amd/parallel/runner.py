@@ -30,6 +30,7 @@ from ..models.resnet import MODEL_INPUT, build_model
 from ..utils import metrics as M
 from ..utils.data import DeviceDataset, shard_range, steps_per_epoch
 from . import control as CP
+from .codec import FetchCodec
 from .compute import make_compute
 from .server import ParameterServer
 from .transport import DistTransport, LocalTransport, env_world
@@ -182,7 +183,8 @@ def run_distributed(cfg, log=print) -> dict:
         if rank == 0:
             for r in worker_ranks:
                 server.register_worker(names[r], wid_of_rank[r])
-        chan = SyncCollectiveChannel(t, server, members=list(range(W)))
+        chan = SyncCollectiveChannel(t, server, members=list(range(W)),
+                                     codec=FetchCodec(layout, cfg.fetch_codec, device))
         if is_worker:
             wk = Worker(cfg, comp, chan, train, test, worker_name=names[rank], rank=rank, log=lg,
                         requested_id=wid_of_rank[rank], steps_per_epoch=steps)
@@ -212,7 +214,7 @@ def run_distributed(cfg, log=print) -> dict:
                 server.serve_async(t, mbox, remote, local_queue=None, expected=W)
         else:
             hb = None
-            chan = AsyncChannel(t, mbox, rank)
+            chan = AsyncChannel(t, mbox, rank, codec=FetchCodec(layout, cfg.fetch_codec, device))
             wk = Worker(cfg, comp, chan, train, test, worker_name=names[rank], rank=rank, log=lg,
                         requested_id=wid_of_rank[rank])
             wk.connect_to_server()

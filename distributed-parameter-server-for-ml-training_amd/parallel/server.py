@@ -259,11 +259,14 @@ class ParameterServer:
         n = self.n
         wire_dtype = torch.float16 if self.cfg.codec == "fp16" else torch.float32
         slots = {w: torch.empty(n, dtype=wire_dtype, device=self.device) for w in rank_of}
-        snaps = {w: torch.empty_like(self.arena) for w in rank_of}
+        # one fetch snapshot per worker (codec wire buffers): an in-flight send never races the
+        # next update of the arena
+        from .codec import FetchCodec
+
+        snaps = {w: FetchCodec(self.layout, self.cfg.fetch_codec, self.device) for w in rank_of}
         bufslots = {}
-        pending_recv = []   # (wid, local_step, work)
-        pending_send = {}   # wid -> work
-        done = set()
+        pending_recv = []   # (wid, local_step, work, buffers_work)
+        pending_send = {}   # wid -> [works]
         last_to = time.monotonic()
         while True:
             msg = mbox.recv(timeout=poll)
@@ -276,12 +279,10 @@ class ParameterServer:
                     mbox.reply(msg.src, CP.Msg(CP.R_REGISTERED, 0, got, total))
                 elif t == CP.FETCH:
                     gs = self.core.on_fetch(wid)
-                    prev = pending_send.pop(wid, None)
-                    if prev is not None:
+                    for prev in pending_send.pop(wid, []):
                         prev.wait()
-                    snaps[wid].copy_(self.arena)
-                    pending_send[wid] = transport.isend(snaps[wid], rank_of[wid])
-                    self.bytes_fetched += self.arena.numel() * 4
+                    pending_send[wid] = [transport.isend(b, rank_of[wid]) for b in snaps[wid].pack(self.arena)]
+                    self.bytes_fetched += snaps[wid].nbytes
                     mbox.reply(rank_of[wid], CP.Msg(CP.R_FETCHED, 0, wid, 0, gs))
                 elif t == CP.PUSH:
                     work = transport.irecv(slots[wid], rank_of[wid])
@@ -349,6 +350,7 @@ class ParameterServer:
                     finished.add(w)
             if stop_when_done and len(finished) >= expected and not pending_recv:
                 break
-        for w in pending_send.values():
-            w.wait()
+        for works in pending_send.values():
+            for w in works:
+                w.wait()
 

@@ -57,27 +57,37 @@ class InProcessChannel:
 class SyncCollectiveChannel:
     """All ranks call push/fetch in lockstep. Rank 0 may or may not train (topology)."""
 
-    def __init__(self, transport, server=None, members=None):
+    def __init__(self, transport, server=None, members=None, codec=None):
         self.t = transport
         self.server = server
         self.members = members or []
-        self._registered = None
+        self.codec = codec  # FetchCodec (parallel/codec.py); None = raw fp32 arena
 
     def register(self, name, requested_id=-1):
-        if self.server is not None:
-            pass  # registrations are done for every rank by the runner (gathered names)
+        # registrations of every rank are done by the runner on rank 0 (gathered names)
         return requested_id, len(self.members)
 
     def fetch(self, worker_id, local_arena):
         if self.server is not None:
             for w in self.members:
                 self.server.core.on_fetch(w)
-            self.t.broadcast_from_server(self.server.arena)
-            self.server.bytes_fetched += self.server.arena.numel() * 4 * max(0, len(self.members) - 1)
+            if self.codec is None:
+                self.t.broadcast_from_server(self.server.arena)
+                nbytes = self.server.arena.numel() * 4
+            else:
+                for buf in self.codec.pack(self.server.arena):
+                    self.t.broadcast_from_server(buf)
+                nbytes = self.codec.nbytes
+            self.server.bytes_fetched += nbytes * max(0, len(self.members) - 1)
             if local_arena is not None and local_arena.data_ptr() != self.server.arena.data_ptr():
                 local_arena.copy_(self.server.arena)
             return self.server.core.global_step
-        self.t.broadcast_from_server(local_arena)
+        if self.codec is None:
+            self.t.broadcast_from_server(local_arena)
+        else:
+            for buf in self.codec.wire:
+                self.t.broadcast_from_server(buf)
+            self.codec.unpack(local_arena)
         return self._gs_after_fetch()
 
     def _gs_after_fetch(self):
@@ -101,8 +111,9 @@ class SyncCollectiveChannel:
 
 
 class AsyncChannel:
-    def __init__(self, transport, mbox, rank):
+    def __init__(self, transport, mbox, rank, codec=None):
         self.t, self.mbox, self.rank = transport, mbox, rank
+        self.codec = codec
 
     def register(self, name, requested_id=-1):
         self.mbox.send(CP.Msg(CP.HELLO, self.rank, requested_id))
@@ -111,9 +122,13 @@ class AsyncChannel:
 
     def fetch(self, worker_id, local_arena):
         self.mbox.send(CP.Msg(CP.FETCH, self.rank, worker_id))
-        work = self.t.irecv(local_arena, 0)
+        bufs = [local_arena] if self.codec is None else self.codec.wire
+        works = [self.t.irecv(b, 0) for b in bufs]
         r = self.mbox.wait_reply(self.rank)
-        work.wait()
+        for w in works:
+            w.wait()
+        if self.codec is not None:
+            self.codec.unpack(local_arena)
         return r.c
 
     def push(self, worker_id, grads, local_step, buffers=None):

@@ -58,6 +58,9 @@ class PSConfig:
     # statistics. bn_sync=True makes workers push their running stats with each gradient push;
     # the server averages them (sync) or blends them 1/W (async). Default off = reference parity.
     bn_sync: bool = False
+    # fetch payload: "bf16conv" = conv weights as bf16 (exactly the bits the HIP engine consumes)
+    # + fp32 for everything else (half the bytes); "fp32" = the reference's full fp32 state.
+    fetch_codec: str = "bf16conv"
     synthetic: bool = True
     data_dir: str = ""
     train_samples: int = 50000
@@ -88,6 +91,8 @@ class PSConfig:
             raise ValueError("--sync-semantics must be barrier or reference")
         if self.staleness_bound < 0:
             raise ValueError("--staleness-bound must be >= 0")
+        if self.fetch_codec not in ("bf16conv", "fp32"):
+            raise ValueError("--fetch-codec must be bf16conv or fp32")
         if not (0.0 < self.topk_ratio <= 1.0):
             raise ValueError("--topk-ratio must be in (0, 1]")
         return self
@@ -121,6 +126,7 @@ def add_arguments(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     A("--weight-decay", type=float, default=None)
     A("--sync-semantics", choices=["barrier", "reference"], default=None)
     A("--bn-sync", action="store_true", default=None, help="workers push BN running stats; server averages")
+    A("--fetch-codec", choices=["bf16conv", "fp32"], default=None)
     A("--synthetic", action="store_true", default=None)
     A("--data-dir", default=None, help="directory with cifar-100-binary/{train,test}.bin")
     A("--train-samples", type=int, default=None)

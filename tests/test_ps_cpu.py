@@ -106,8 +106,16 @@ def test_run_local(mode, workers, capsys):
     assert w["local_steps_completed"] == steps and len(w["all_accuracies_percent"]) == 1
 
 
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def _spawn(nproc, args, timeout=240):
-    port = 29500 + (os.getpid() % 2000)
+    port = _free_port()
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     env.pop("CUDA_VISIBLE_DEVICES", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
@@ -185,3 +193,32 @@ def test_dist_async_gloo():
     assert srv["gradients_processed"] == total
     assert srv["global_steps_completed"] == srv["async_updates"] == total - srv["rejected_pushes"]
     assert sum(srv["staleness_histogram"]) == srv["async_updates"]
+
+
+def test_fetch_codec_roundtrip_is_compute_exact():
+    from psx.parallel.codec import FetchCodec
+
+    torch.manual_seed(0)
+    m = TinyResNet(10)
+    lay = ParamLayout.from_module(m)
+    arena, _ = lay.pack(m)
+    arena += 0.001 * torch.randn_like(arena)
+    c = FetchCodec(lay, "bf16conv")
+    assert c.nbytes < 0.6 * arena.numel() * 4
+    local = torch.zeros_like(arena)
+    c.unpack(local, [w.clone() for w in c.pack(arena)])
+    for name, e in lay.entries.items():
+        if e.region == "counter":
+            continue
+        got, ref = lay.view(local, name), lay.view(arena, name)
+        if e.region == "param" and len(e.shape) == 4:  # conv weight: the bf16 bits the engine uses
+            assert torch.equal(got.to(torch.bfloat16), ref.to(torch.bfloat16)), name
+        else:
+            assert torch.equal(got, ref), name
+
+
+@pytest.mark.parametrize("codec", ["fp32", "bf16conv"])
+def test_dist_sync_fetch_codecs(codec):
+    recs, _ = _spawn(2, ["--mode", "sync", "--fetch-codec", codec] + TINY)
+    srv = [r for r in recs if r["type"] == "SERVER_FINAL_METRICS"][0]
+    assert srv["global_steps_completed"] > 0

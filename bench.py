@@ -29,12 +29,11 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import psx  # noqa: E402,F401
-from psx.parallel.codec import FetchCodec  # noqa: E402
 from psx.parallel.compute import HipCompute  # noqa: E402
-from psx.parallel.runner import build_state, make_datasets  # noqa: E402
+from psx.parallel.runner import build_state, make_datasets, make_sync_channel  # noqa: E402
 from psx.parallel.server import ParameterServer  # noqa: E402
 from psx.parallel.transport import DistTransport, env_world  # noqa: E402
-from psx.parallel.worker import InProcessChannel, SyncCollectiveChannel, Worker  # noqa: E402
+from psx.parallel.worker import InProcessChannel, Worker  # noqa: E402
 from psx.utils.config import PSConfig  # noqa: E402
 
 BASELINE_SYNC_IMG_S = 82.7  # sync PS, 4 workers, measured (experiment_results/sync_4workers.json)
@@ -52,6 +51,10 @@ def main():
     ap.add_argument("--fetch-codec", choices=["bf16conv", "fp32"], default="bf16conv",
                     help="bf16conv: conv weights travel as the bf16 bits the workers compute with (bit-exact "
                          "worker compute), everything else fp32; fp32: the reference's full fp32 state")
+    ap.add_argument("--overlap", action="store_true",
+                    help="stream gradient buckets (reduce/apply/broadcast) during the backward pass")
+    ap.add_argument("--bucket-mb", type=float, default=4.0)
+    ap.add_argument("--host-timing", action="store_true", help="report host-side issue time per step (stderr)")
     a = ap.parse_args()
 
     rank, world, local = env_world()
@@ -60,7 +63,8 @@ def main():
     torch.cuda.set_device(local % torch.cuda.device_count())
     device = torch.device("cuda", torch.cuda.current_device())
     cfg = PSConfig(mode="sync", model="resnet18", batch_size=a.batch, lr=0.1, sync_steps=1, epochs=1,
-                   eval_every=0, verbose=0, codec=a.codec, use_graph=not a.no_graph).validate()
+                   eval_every=0, verbose=0, codec=a.codec, use_graph=not a.no_graph, fetch_codec=a.fetch_codec,
+                   overlap=a.overlap, bucket_mb=a.bucket_mb).validate()
     model, layout, arena, counters = build_state(cfg)
     wire = torch.float16 if a.codec == "fp16" else torch.float32
 
@@ -79,8 +83,7 @@ def main():
         for i in range(W):
             server.register_worker(f"worker-{i}", i)
     train, _ = make_datasets(cfg, device, model.fc.out_features)
-    chan = InProcessChannel(server) if t is None else SyncCollectiveChannel(
-        t, server, members=list(range(W)), codec=FetchCodec(layout, a.fetch_codec, device))
+    chan = InProcessChannel(server) if t is None else make_sync_channel(cfg, t, server, W, layout, device)
     wk = None
     zeros = None
     if is_worker:
@@ -113,9 +116,12 @@ def main():
     for i in range(a.warmup):
         step(i)
     barrier_sync()
+    host = []
     t0 = time.perf_counter()
     for i in range(a.steps):
+        h0 = time.perf_counter()
         step(a.warmup + i)
+        host.append(time.perf_counter() - h0)
     barrier_sync()
     dt = time.perf_counter() - t0
     if t is not None:
@@ -152,6 +158,8 @@ def main():
                 "sync_steps": 1,
                 "codec": a.codec,
                 "fetch_codec": a.fetch_codec if t is not None else "in-process",
+                "overlap": (f"bucketed reduce/apply/broadcast during backward ({len(chan.buckets)} buckets)"
+                            if getattr(chan, "overlap", False) else "none"),
                 "topology": "dedicated" if dedicated else ("colocated" if t is not None else "loopback"),
                 "hip_graph": cfg.use_graph,
             },
@@ -160,6 +168,11 @@ def main():
             "baseline_img_s": BASELINE_SYNC_IMG_S,
         }
         print(json.dumps(rec), flush=True)
+    if a.host_timing:
+        print(json.dumps({"rank": rank, "host_issue_ms_per_step": round(1e3 * sum(host) / len(host), 4),
+                          "host_issue_ms_max": round(1e3 * max(host), 4)}), file=sys.stderr, flush=True)
+    if hasattr(chan, "drain"):
+        chan.drain()
     if t is not None:
         t.close()
 

@@ -170,6 +170,8 @@ class HipResNetEngine:
         self.eps, self.mom = bn_eps, bn_momentum
         self.seed = seed
         self.graph = None
+        self.graphs = None
+        self.segments = None  # backward split points (set_segments), None = one segment
         # conv kernel generation: 2 = LDS-DMA pipelined + split-K (default), 1 = register-staged
         self.conv_impl = int(os.environ.get("PSX_CONV_IMPL", "2"))
         self._build()
@@ -421,72 +423,131 @@ class HipResNetEngine:
                        self._aview(arena, f"{sp.fc}.bias"), sp.classes, self.labels, self.pooled, self.dlogits,
                        self.dfinal if backward else None, self.loss, self.correct)
 
-    def backward(self, arena: torch.Tensor):
-        sp, B = self.spec, self.B
-        K.head_wgrad(self.dlogits, self.pooled, B, sp.classes, sp.fc_in, self._gptr(f"{sp.fc}.weight"),
+    def _bwd_fc(self, arena):
+        sp = self.spec
+        K.head_wgrad(self.dlogits, self.pooled, self.B, sp.classes, sp.fc_in, self._gptr(f"{sp.fc}.weight"),
                      self._gptr(f"{sp.fc}.bias"), 1.0, self.grad_fp16)
-        g = self.dfinal
-        for b, d in zip(reversed(sp.blocks), reversed(self.blk)):
-            L = len(b.convs)
-            last = b.convs[-1]
-            oh, ow = last.out_hw
-            npix = B * oh * ow
-            if b.down:
+
+    def _bwd_block(self, arena, j: int):
+        """Backward of residual block j; its incoming gradient is the next block's input grad."""
+        sp, B = self.spec, self.B
+        b, d = sp.blocks[j], self.blk[j]
+        g = self.blk[j + 1]["gin"] if j + 1 < len(self.blk) else self.dfinal
+        L = len(b.convs)
+        last = b.convs[-1]
+        oh, ow = last.out_hw
+        npix = B * oh * ow
+        if b.down:
+            ds, dbn = b.down
+            self._bn_bwd(b.bns[-1], arena, g, d["out"], d["y"][-1], d["dy"][-1], npix, two=(dbn, d["ys"], d["dys"]))
+        else:
+            self._bn_bwd(b.bns[-1], arena, g, d["out"], d["y"][-1], d["dy"][-1], npix, dzout=d["dz"])
+        for i in range(L - 1, -1, -1):
+            cs = b.convs[i]
+            x_in = d["inp"] if i == 0 else d["a"][i - 1]
+            self._wgrad(cs, x_in, d["dy"][i])
+            if i > 0:
+                self._dgrad(cs, d["dy"][i], d["da"][i - 1])
+                self._bn_bwd(b.bns[i - 1], arena, d["da"][i - 1], d["a"][i - 1], d["y"][i - 1], d["dy"][i - 1],
+                             B * cs.h * cs.w)
+            elif b.down:
                 ds, dbn = b.down
-                self._bn_bwd(b.bns[-1], arena, g, d["out"], d["y"][-1], d["dy"][-1], npix,
-                             two=(dbn, d["ys"], d["dys"]))
+                self._wgrad(ds, d["inp"], d["dys"])
+                self._dgrad(ds, d["dys"], d["dxs"])
+                self._dgrad(cs, d["dy"][0], d["gin"], res=d["dxs"])
             else:
-                self._bn_bwd(b.bns[-1], arena, g, d["out"], d["y"][-1], d["dy"][-1], npix, dzout=d["dz"])
-            for i in range(L - 1, -1, -1):
-                cs = b.convs[i]
-                x_in = d["inp"] if i == 0 else d["a"][i - 1]
-                self._wgrad(cs, x_in, d["dy"][i])
-                if i > 0:
-                    self._dgrad(cs, d["dy"][i], d["da"][i - 1])
-                    ph, pw = cs.h, cs.w
-                    self._bn_bwd(b.bns[i - 1], arena, d["da"][i - 1], d["a"][i - 1], d["y"][i - 1], d["dy"][i - 1],
-                                 B * ph * pw)
-                else:
-                    if b.down:
-                        ds, dbn = b.down
-                        self._wgrad(ds, d["inp"], d["dys"])
-                        self._dgrad(ds, d["dys"], d["dxs"])
-                        self._dgrad(cs, d["dy"][0], d["gin"], res=d["dxs"])
-                    else:
-                        self._dgrad(cs, d["dy"][0], d["gin"], res=d["dz"])
-            g = d["gin"]
+                self._dgrad(cs, d["dy"][0], d["gin"], res=d["dz"])
+
+    def _bwd_stem(self, arena):
+        sp, B = self.spec, self.B
         st = sp.stem_conv
         p, q = st.out_hw
+        g = self.blk[0]["gin"] if self.blk else self.dfinal
         self._bn_bwd(sp.stem_bn, arena, g, self.a0, self.y0, self.dy0, B * p * q)
         self._wgrad(st, self.x0, self.dy0)
 
-    def train_step(self, arena: torch.Tensor, images_u8=None, labels_all=None, unpack=True):
-        """unpack (optional) + batch load + forward + loss + backward -> self.grads."""
-        if unpack:
-            self.unpack(arena)
-        if images_u8 is not None:
-            self.load_batch(images_u8, labels_all, train=True)
-        self.forward(arena, train=True)
-        self.head(arena, backward=True)
-        self.backward(arena)
+    def backward_units(self, arena):
+        """The backward pass as (unit key, thunk) in execution order. Unit keys name the
+        gradient-arena region each unit finalizes: "fc", "layer<i>.<j>" (one residual block),
+        "stem" (conv1 + bn1) — the same keys as parallel/overlap.py:unit_key, so a gradient
+        bucket can be pushed as soon as the units that write it have run."""
+        units = [("fc", lambda: self._bwd_fc(arena))]
+        for j in range(len(self.spec.blocks) - 1, -1, -1):
+            key = ".".join(self.spec.blocks[j].convs[0].name.split(".")[:2])
+            units.append((key, lambda j=j: self._bwd_block(arena, j)))
+        units.append(("stem", lambda: self._bwd_stem(arena)))
+        return units
+
+    def backward(self, arena: torch.Tensor):
+        for _, fn in self.backward_units(arena):
+            fn()
+
+    def set_segments(self, groups):
+        """Split the backward into segments (lists of unit keys, in backward order) so that a
+        callback can run — and a bucket's collective be issued — between them."""
+        keys = [k for k, _ in self.backward_units(None)]
+        flat = [k for grp in groups for k in grp]
+        if flat != keys:
+            raise ValueError(f"segments {groups} do not cover the backward units {keys}")
+        self.segments = [list(g) for g in groups]
+        self.graph = None
+        self.graphs = None
+
+    def _segment_fns(self, arena, images_u8, labels_all, unpack):
+        units = dict(self.backward_units(arena))
+        groups = self.segments or [[k for k, _ in self.backward_units(arena)]]
+
+        def prologue():
+            if unpack:
+                self.unpack(arena)
+            if images_u8 is not None:
+                self.load_batch(images_u8, labels_all, train=True)
+            self.forward(arena, train=True)
+            self.head(arena, backward=True)
+
+        fns = []
+        for si, grp in enumerate(groups):
+            def seg(grp=grp, first=(si == 0)):
+                if first:
+                    prologue()
+                for k in grp:
+                    units[k]()
+            fns.append(seg)
+        return fns
+
+    def train_step(self, arena: torch.Tensor, images_u8=None, labels_all=None, unpack=True, on_segment=None):
+        """unpack (optional) + batch load + forward + loss + backward -> self.grads.
+        ``on_segment(i)`` runs after backward segment i has been issued (see set_segments)."""
+        for si, fn in enumerate(self._segment_fns(arena, images_u8, labels_all, unpack)):
+            fn()
+            if on_segment is not None:
+                on_segment(si)
 
     # ------------------------------------------------------------------ graphs
     def capture(self, arena, images_u8, labels_all, unpack=True, warmup=2):
-        """Capture the full step into a HIP graph; replay with ``step_graph()``."""
+        """Capture the step into HIP graphs (one per backward segment, all sharing one memory
+        pool); replay with ``step_graph()``."""
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self.train_step(arena, images_u8, labels_all, unpack)
         torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self.train_step(arena, images_u8, labels_all, unpack)
-        self.graph = g
-        return g
+        graphs = []
+        for fn in self._segment_fns(arena, images_u8, labels_all, unpack):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=graphs[0].pool() if graphs else None):
+                fn()
+            graphs.append(g)
+        self.graphs = graphs
+        self.graph = graphs[0]
+        return graphs[0]
 
-    def step_graph(self):
-        self.graph.replay()
+    def step_graph(self, on_segment=None):
+        for si, g in enumerate(self.graphs):
+            g.replay()
+            if on_segment is not None:
+                on_segment(si)
 
     def evaluate_batch(self, arena, images_u8, labels_all):
         self.load_batch(images_u8, labels_all, train=False)

@@ -66,7 +66,10 @@ class TorchCompute:
         y = dataset.labels[torch.as_tensor(idx, dtype=torch.long)].long()
         return x, y
 
-    def train_step(self, dataset, idx):
+    def set_buckets(self, buckets):
+        self._nbuckets = len(buckets)
+
+    def train_step(self, dataset, idx, on_bucket=None):
         self._load_module()
         self.model.train()
         self.model.zero_grad(set_to_none=False)
@@ -80,6 +83,9 @@ class TorchCompute:
                 self.grads[e.offset:e.offset + e.numel] = p.grad.reshape(-1).to(self.grads.dtype)
         self._store_buffers()
         self._step += 1
+        if on_bucket is not None:  # eager CPU path: every bucket is final after backward
+            for k in range(self._nbuckets):
+                on_bucket(k, self.grads)
 
     def last_loss(self) -> float:
         return self._loss
@@ -122,7 +128,11 @@ class HipCompute:
         self.engine.index.copy_(self._idx_host, non_blocking=True)
         self.engine.step_dev.fill_(self._step)
 
-    def train_step(self, dataset, idx):
+    def set_buckets(self, buckets):
+        self.engine.set_segments([b.keys for b in buckets])
+
+    def train_step(self, dataset, idx, on_bucket=None):
+        seg = (lambda k: on_bucket(k, self.grads)) if on_bucket is not None else None
         self._set_batch(idx)
         if self.use_graph:
             if self.engine.graph is None or self._dataset is not dataset:
@@ -134,9 +144,9 @@ class HipCompute:
                 self.engine.capture(self.local_arena, dataset.images, dataset.labels, unpack=True, warmup=1)
                 self.local_arena.copy_(backup)
                 del backup
-            self.engine.step_graph()
+            self.engine.step_graph(on_segment=seg)
         else:
-            self.engine.train_step(self.local_arena, dataset.images, dataset.labels, unpack=True)
+            self.engine.train_step(self.local_arena, dataset.images, dataset.labels, unpack=True, on_segment=seg)
         self._step += 1
 
     def last_loss(self) -> float:

@@ -32,6 +32,7 @@ from ..utils.data import DeviceDataset, shard_range, steps_per_epoch
 from . import control as CP
 from .codec import FetchCodec
 from .compute import make_compute
+from .overlap import OverlapSyncChannel, plan_buckets
 from .server import ParameterServer
 from .transport import DistTransport, LocalTransport, env_world
 from .worker import (AsyncChannel, InProcessChannel, LocalAsyncChannel, SyncCollectiveChannel, Worker)
@@ -183,8 +184,7 @@ def run_distributed(cfg, log=print) -> dict:
         if rank == 0:
             for r in worker_ranks:
                 server.register_worker(names[r], wid_of_rank[r])
-        chan = SyncCollectiveChannel(t, server, members=list(range(W)),
-                                     codec=FetchCodec(layout, cfg.fetch_codec, device))
+        chan = make_sync_channel(cfg, t, server, W, layout, device)
         if is_worker:
             wk = Worker(cfg, comp, chan, train, test, worker_name=names[rank], rank=rank, log=lg,
                         requested_id=wid_of_rank[rank], steps_per_epoch=steps)
@@ -240,6 +240,15 @@ def run_distributed(cfg, log=print) -> dict:
     return result
 
 
+def make_sync_channel(cfg, t, server, W, layout, device):
+    """Sync-mode channel: bucketed + backward-overlapped when every batch is pushed."""
+    codec = FetchCodec(layout, cfg.fetch_codec, device)
+    if cfg.overlap and max(1, cfg.sync_steps) == 1:
+        buckets = plan_buckets(layout, int(cfg.bucket_mb * (1 << 20)) // 2)
+        return OverlapSyncChannel(t, server, members=list(range(W)), codec=codec, buckets=buckets, device=device)
+    return SyncCollectiveChannel(t, server, members=list(range(W)), codec=codec)
+
+
 def _dedicated_sync_server(cfg, server, chan, steps, device):
     """Rank 0 of the dedicated topology: takes part in every round's collectives with a zero
     gradient contribution and applies the averaged update."""
@@ -257,7 +266,12 @@ def _dedicated_sync_server(cfg, server, chan, steps, device):
                 chan.push(None, zeros, server.core.global_step, buffers=zbuf)
             done += 1
             if cfg.max_steps and done >= cfg.max_steps:
-                return
+                break
+        else:
+            continue
+        break
+    if hasattr(chan, "drain"):
+        chan.drain()
 
 
 def run(cfg, log=print) -> dict:

@@ -63,26 +63,35 @@ class ParameterServer:
     def apply(self, grads: torch.Tensor, weight: float):
         """p <- p - lr * (weight * g [+ wd p]) [momentum]; grads are fp16 wire or fp32."""
         t0 = time.perf_counter()
-        g = grads[: self.n]
+        self.apply_range(grads[: self.n], weight, 0, self.n)
+        return self.finish_round_apply(time.perf_counter() - t0)
+
+    def apply_range(self, g: torch.Tensor, weight: float, lo: int, hi: int):
+        """The update restricted to params[lo:hi] (g holds exactly that slice): one bucket of a
+        backward-overlapped sync round (parallel/overlap.py). Several ranges of one round share
+        the same momentum 'first step' flag; finish_round_apply closes the round."""
+        p = self.params[lo:hi]
+        buf = self.momentum_buf[lo:hi] if self.momentum_buf is not None else None
         if self.device.type == "cuda":
             from ..ops import kernels as K
 
-            K.sgd_apply(self.params, g, self.lr, gscale=weight, momentum=self.cfg.momentum,
-                        wd=self.cfg.weight_decay, buf=self.momentum_buf, first=self._mom_first, n=self.n)
-        else:
-            d = g.to(torch.float32) * weight
-            if self.cfg.weight_decay:
-                d = d + self.cfg.weight_decay * self.params
-            if self.momentum_buf is not None:
-                if self._mom_first:
-                    self.momentum_buf.copy_(d)
-                else:
-                    self.momentum_buf.mul_(self.cfg.momentum).add_(d)
-                d = self.momentum_buf
-            self.params.sub_(self.lr * d)
+            K.sgd_apply(p, g, self.lr, gscale=weight, momentum=self.cfg.momentum, wd=self.cfg.weight_decay, buf=buf,
+                        first=self._mom_first, n=hi - lo)
+            return
+        d = g.to(torch.float32) * weight
+        if self.cfg.weight_decay:
+            d = d + self.cfg.weight_decay * p
+        if buf is not None:
+            if self._mom_first:
+                buf.copy_(d)
+            else:
+                buf.mul_(self.cfg.momentum).add_(d)
+            d = buf
+        p.sub_(self.lr * d)
+
+    def finish_round_apply(self, dt: float = 0.0):
         self._mom_first = False
-        dt = time.perf_counter() - t0  # host-side issue time (device work is stream-ordered)
-        self.core.on_applied(dt)
+        self.core.on_applied(dt)  # host-side issue time (device work is stream-ordered)
         return dt
 
     def _accumulate(self, grads: torch.Tensor, first: bool):
@@ -237,6 +246,8 @@ class ParameterServer:
         m["bytes_fetched"] = int(self.bytes_fetched)
         if self.images_processed:
             m["images_processed"] = int(self.images_processed)
+        # order-independent fingerprint of the final master state (cross-mode/run parity checks)
+        m["final_param_checksum"] = float(self.arena.double().abs().sum())
         if extra:
             m.update(extra)
         if emit:

@@ -85,6 +85,14 @@ class DistTransport:
         dist.broadcast(t, src=0)
         return t
 
+    # ---- bucketed (overlapped) sync round: non-blocking; RCCL runs on its own stream ordered
+    # after the caller's stream at issue time, work.wait() orders the caller's stream after it
+    def reduce_async(self, t):
+        return dist.reduce(t, dst=0, op=dist.ReduceOp.SUM, async_op=True)
+
+    def broadcast_async(self, t):
+        return dist.broadcast(t, src=0, async_op=True)
+
     # ---- async mode point-to-point (bulk)
     def isend(self, t, dst: int):
         return dist.isend(t, dst=dst)

@@ -203,6 +203,12 @@ class Worker:
     def connect_to_server(self):
         self.worker_id, self.total_workers = self.channel.register(self.worker_name, self.requested_id)
         self.log(f"Registered as Worker {self.worker_id} (Total workers: {self.total_workers})")
+        # backward-overlapped sync rounds (parallel/overlap.py): every batch is pushed, so the
+        # gradient buckets can leave while the rest of the backward pass still runs
+        self._overlap = bool(getattr(self.channel, "overlap", False) and self.local_steps_per_sync == 1
+                             and hasattr(self.compute, "set_buckets"))
+        if self._overlap:
+            self.compute.set_buckets(self.channel.buckets)
 
     def setup_data(self):
         start, end = shard_range(self.worker_id, self.total_workers, len(self.train_set))
@@ -225,7 +231,8 @@ class Worker:
         return ok
 
     def train_local_batch(self, idx):
-        self.compute.train_step(self.train_set, idx)
+        on_bucket = self.channel.push_bucket if getattr(self, "_overlap", False) else None
+        self.compute.train_step(self.train_set, idx, on_bucket=on_bucket)
         self.local_step_counter += 1
         self.images += len(idx)
 

@@ -61,6 +61,11 @@ class PSConfig:
     # fetch payload: "bf16conv" = conv weights as bf16 (exactly the bits the HIP engine consumes)
     # + fp32 for everything else (half the bytes); "fp32" = the reference's full fp32 state.
     fetch_codec: str = "bf16conv"
+    # sync rounds stream gradient buckets during the backward pass (parallel/overlap.py).
+    # Opt-in: at N=1 it costs ~0.25 ms/step of cross-queue waits (profiles/README.md), which is
+    # about the xGMI time it can hide at N=8; the serial round stays the default until measured.
+    overlap: bool = False
+    bucket_mb: float = 4.0         # bucket target size in MiB of fp16 wire gradient
     synthetic: bool = True
     data_dir: str = ""
     train_samples: int = 50000
@@ -93,6 +98,8 @@ class PSConfig:
             raise ValueError("--staleness-bound must be >= 0")
         if self.fetch_codec not in ("bf16conv", "fp32"):
             raise ValueError("--fetch-codec must be bf16conv or fp32")
+        if self.bucket_mb <= 0:
+            raise ValueError("--bucket-mb must be > 0")
         if not (0.0 < self.topk_ratio <= 1.0):
             raise ValueError("--topk-ratio must be in (0, 1]")
         return self
@@ -127,6 +134,10 @@ def add_arguments(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     A("--sync-semantics", choices=["barrier", "reference"], default=None)
     A("--bn-sync", action="store_true", default=None, help="workers push BN running stats; server averages")
     A("--fetch-codec", choices=["bf16conv", "fp32"], default=None)
+    A("--overlap", dest="overlap", action="store_true", default=None,
+      help="sync mode: stream gradient buckets (reduce/apply/broadcast) during the backward pass")
+    A("--no-overlap", dest="overlap", action="store_false", default=None)
+    A("--bucket-mb", type=float, default=None, help="overlapped sync: gradient bucket size (MiB of fp16)")
     A("--synthetic", action="store_true", default=None)
     A("--data-dir", default=None, help="directory with cifar-100-binary/{train,test}.bin")
     A("--train-samples", type=int, default=None)

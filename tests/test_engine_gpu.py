@@ -106,6 +106,37 @@ def test_graph_replay_matches_eager(setup):
     assert _cos(eng.grads[fc:].float(), eager[fc:].float()) > 0.9999
 
 
+def test_segmented_graphs_match_single_graph(setup):
+    """Backward split into per-bucket graphs (overlapped sync rounds) computes the same step."""
+    from psx.parallel.overlap import plan_buckets
+
+    model, layout, arena, eng, x, y = setup
+    n = 256
+    imgs = torch.randint(0, 256, (n, 32, 32, 3), dtype=torch.uint8, device=DEV)
+    labs = torch.randint(0, 100, (n,), dtype=torch.int32, device=DEV)
+    eng.index.copy_(torch.arange(eng.B, dtype=torch.int32, device=DEV))
+    a1 = arena.clone()
+    eng.capture(a1, imgs, labs, warmup=1)
+    a1.copy_(arena)
+    eng.step_graph()
+    torch.cuda.synchronize()
+    ref = eng.grads.clone()
+    buckets = plan_buckets(layout, 2 << 20)
+    eng.set_segments([b.keys for b in buckets])
+    a2 = arena.clone()
+    eng.capture(a2, imgs, labs, warmup=1)
+    assert len(eng.graphs) == len(buckets) == 4
+    a2.copy_(arena)
+    seen = []
+    eng.step_graph(on_segment=seen.append)
+    torch.cuda.synchronize()
+    assert seen == [0, 1, 2, 3]
+    assert _cos(eng.grads.float(), ref.float()) > 0.97
+    fc = layout.entries["fc.weight"].offset
+    assert _cos(eng.grads[fc:].float(), ref[fc:].float()) > 0.9999
+    eng.set_segments([[k for k, _ in eng.backward_units(None)]])
+
+
 def test_eval_counts_correct(setup):
     model, layout, arena, eng, x, y = setup
     n = 64

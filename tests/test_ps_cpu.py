@@ -222,3 +222,37 @@ def test_dist_sync_fetch_codecs(codec):
     recs, _ = _spawn(2, ["--mode", "sync", "--fetch-codec", codec] + TINY)
     srv = [r for r in recs if r["type"] == "SERVER_FINAL_METRICS"][0]
     assert srv["global_steps_completed"] > 0
+
+
+def test_plan_buckets_resnet18():
+    from psx.models.resnet import ResNet18
+    from psx.parallel.overlap import plan_buckets
+
+    lay = ParamLayout.from_module(ResNet18(100))
+    bk = plan_buckets(lay, 2 << 20)
+    assert [b.keys[0] for b in bk] == ["fc", "layer4.0", "layer3.1", "layer2.1"]
+    assert bk[-1].keys[-1] == "stem"
+    # contiguous partition of the trainable prefix, in backward order
+    assert bk[0].hi == lay.param_numel and bk[-1].lo == 0
+    for a, b in zip(bk, bk[1:]):
+        assert a.lo == b.hi
+    assert sum(b.numel for b in bk) == lay.param_numel == 11_220_132
+    one = plan_buckets(lay, 1 << 40)
+    assert len(one) == 1 and one[0].numel == lay.param_numel
+
+
+@pytest.mark.parametrize("extra", [[], ["--bucket-mb", "0.01"], ["--bucket-mb", "0.01", "--bn-sync"],
+                                   ["--bucket-mb", "0.01", "--fetch-codec", "fp32", "--topology", "dedicated"]])
+def test_dist_sync_overlap_matches_serial(extra):
+    """The bucketed/overlapped round must give exactly the serial round's parameters."""
+    outs = {}
+    for ov in (True, False):
+        d = os.path.join("/tmp", f"psx_ov_{os.getpid()}_{int(ov)}")
+        # fp32 wire: an fp16 reduce may round differently when the message is split differently
+        args = (["--mode", "sync", "--codec", "none", "--ckpt-every", "1000", "--ckpt-dir", d] + TINY + extra
+                + (["--overlap"] if ov else []))
+        recs, _ = _spawn(3, args)
+        srv = [r for r in recs if r["type"] == "SERVER_FINAL_METRICS"][0]
+        outs[ov] = srv
+    assert outs[True]["global_steps_completed"] == outs[False]["global_steps_completed"] > 0
+    assert outs[True]["final_param_checksum"] == pytest.approx(outs[False]["final_param_checksum"], rel=1e-6)

@@ -46,7 +46,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--topology", choices=["colocated", "dedicated"], default="colocated")
-    ap.add_argument("--codec", choices=["fp16", "none"], default="fp16")
+    ap.add_argument("--codec", choices=["fp16", "none", "topk"], default="fp16")
+    ap.add_argument("--topk-ratio", type=float, default=0.01)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--fetch-codec", choices=["bf16conv", "fp32"], default="bf16conv",
                     help="bf16conv: conv weights travel as the bf16 bits the workers compute with (bit-exact "
@@ -63,10 +64,10 @@ def main():
     torch.cuda.set_device(local % torch.cuda.device_count())
     device = torch.device("cuda", torch.cuda.current_device())
     cfg = PSConfig(mode="sync", model="resnet18", batch_size=a.batch, lr=0.1, sync_steps=1, epochs=1,
-                   eval_every=0, verbose=0, codec=a.codec, use_graph=not a.no_graph, fetch_codec=a.fetch_codec,
+                   eval_every=0, verbose=0, codec=a.codec, topk_ratio=a.topk_ratio, use_graph=not a.no_graph, fetch_codec=a.fetch_codec,
                    overlap=a.overlap, bucket_mb=a.bucket_mb).validate()
     model, layout, arena, counters = build_state(cfg)
-    wire = torch.float16 if a.codec == "fp16" else torch.float32
+    wire = torch.float16 if a.codec == "fp16" else torch.float32  # topk encodes from fp32 grads
 
     t = None
     force_dist = os.environ.get("PSX_FORCE_DIST", "0") == "1"  # exercise the RCCL path even at N=1
@@ -94,6 +95,10 @@ def main():
         wk.connect_to_server()
         wk.setup_data()
         batches = wk.sampler.epoch_indices(0)
+    elif a.codec == "topk":
+        from psx.parallel.topk import empty_payload
+
+        zeros = empty_payload(layout.param_numel, a.topk_ratio, device)
     else:
         zeros = torch.zeros(layout.param_numel, dtype=wire, device=device)
 
@@ -104,7 +109,8 @@ def main():
             wk.push_gradients()
         else:  # dedicated server rank
             chan.fetch(None, None)
-            zeros.zero_()
+            if a.codec != "topk":
+                zeros.zero_()
             chan.push(None, zeros, server.core.global_step)
 
     def barrier_sync():
@@ -156,7 +162,7 @@ def main():
                                 f"over xGMI" if t is not None else "sync-PS: server + 1 worker co-located on 1 GPU"),
                 "lr": 0.1,
                 "sync_steps": 1,
-                "codec": a.codec,
+                "codec": a.codec if a.codec != "topk" else f"topk({a.topk_ratio}) + error feedback",
                 "fetch_codec": a.fetch_codec if t is not None else "in-process",
                 "overlap": (f"bucketed reduce/apply/broadcast during backward ({len(chan.buckets)} buckets)"
                             if getattr(chan, "overlap", False) else "none"),

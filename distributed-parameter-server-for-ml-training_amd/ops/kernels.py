@@ -184,6 +184,27 @@ def sgd_apply(p, g, lr, gscale=1.0, momentum=0.0, wd=0.0, buf=None, first=False,
                                   int(first), int(fp16), stream_ptr()), "sgd_apply")
 
 
+def topk_workspace_words() -> int:
+    return kernels().psx_topk_workspace_words()
+
+
+def topk_payload_words(kcap: int) -> int:
+    return kernels().psx_topk_payload_words(int(kcap))
+
+
+def topk_encode(g, resid, k, kcap, payload, ws):
+    """Error-feedback top-k of (resid + g) into payload (csrc/kernels/topk.hip); g may be None."""
+    fp16 = g is not None and g.dtype == torch.float16
+    check(kernels().psx_topk_encode(ptr(g), int(fp16), ptr(resid), resid.numel(), int(k), int(kcap), ptr(payload),
+                                    ptr(ws), stream_ptr()), "topk_encode")
+
+
+def topk_decode_add(payload, dst, scale, kcap):
+    """dst[idx] += scale * val for every (idx, val) of a top-k payload."""
+    check(kernels().psx_topk_decode_add(ptr(payload), ptr(dst), float(scale), int(kcap), stream_ptr()),
+          "topk_decode_add")
+
+
 def grad_aggregate(srcs_dev_ptrs, nsrc, src_fp16, dst, n, scale=1.0, accumulate=False):
     """srcs_dev_ptrs: int64 device tensor holding nsrc device pointers."""
     check(kernels().psx_grad_aggregate(ptr(srcs_dev_ptrs), nsrc, int(src_fp16), ptr(dst),

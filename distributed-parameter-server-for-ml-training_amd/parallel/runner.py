@@ -46,7 +46,9 @@ def _device_for(local_rank: int):
 
 
 def _wire_dtype(cfg):
-    return torch.float32 if cfg.codec == "none" else torch.float16
+    """Dtype of the worker's dense gradient buffer: fp16 wire (reference cast), fp32 for the
+    uncompressed wire and as the top-k codec's input (the residual is fp32)."""
+    return torch.float16 if cfg.codec == "fp16" else torch.float32
 
 
 def build_state(cfg):
@@ -243,7 +245,7 @@ def run_distributed(cfg, log=print) -> dict:
 def make_sync_channel(cfg, t, server, W, layout, device):
     """Sync-mode channel: bucketed + backward-overlapped when every batch is pushed."""
     codec = FetchCodec(layout, cfg.fetch_codec, device)
-    if cfg.overlap and max(1, cfg.sync_steps) == 1:
+    if cfg.overlap and max(1, cfg.sync_steps) == 1 and cfg.codec != "topk":
         buckets = plan_buckets(layout, int(cfg.bucket_mb * (1 << 20)) // 2)
         return OverlapSyncChannel(t, server, members=list(range(W)), codec=codec, buckets=buckets, device=device)
     return SyncCollectiveChannel(t, server, members=list(range(W)), codec=codec)
@@ -253,14 +255,20 @@ def _dedicated_sync_server(cfg, server, chan, steps, device):
     """Rank 0 of the dedicated topology: takes part in every round's collectives with a zero
     gradient contribution and applies the averaged update."""
     K = max(1, cfg.sync_steps)
-    zeros = torch.zeros(server.n, dtype=_wire_dtype(cfg), device=device)
+    if cfg.codec == "topk":
+        from .topk import empty_payload
+
+        zeros = empty_payload(server.n, cfg.topk_ratio, device)  # contributes no entries to the gather
+    else:
+        zeros = torch.zeros(server.n, dtype=_wire_dtype(cfg), device=device)
     zbuf = torch.zeros(server.layout.buffer_numel, dtype=torch.float32, device=device) if cfg.bn_sync else None
     done = 0
     for epoch in range(cfg.epochs):
         for b in range(steps):
             if b % K == 0:
                 chan.fetch(None, None)
-                zeros.zero_()
+                if cfg.codec != "topk":
+                    zeros.zero_()
                 if zbuf is not None:
                     zbuf.zero_()
                 chan.push(None, zeros, server.core.global_step, buffers=zbuf)

@@ -27,6 +27,7 @@ import torch
 from ..utils import checkpoint as ckpt
 from ..utils import metrics as M
 from . import control as CP
+from . import topk
 from .core import APPLY, WAIT, ServerCore
 
 _TRACE = os.environ.get("PSX_TRACE", "0") == "1"
@@ -63,8 +64,28 @@ class ParameterServer:
     def apply(self, grads: torch.Tensor, weight: float):
         """p <- p - lr * (weight * g [+ wd p]) [momentum]; grads are fp16 wire or fp32."""
         t0 = time.perf_counter()
+        if grads.dtype == torch.int32:  # top-k payload (parallel/topk.py)
+            if not self.cfg.momentum and not self.cfg.weight_decay:
+                # no optimizer state: scatter straight into the fp32 master parameters
+                topk.decode_add(grads, self.params, -self.lr * weight, self._kcap)
+                return self.finish_round_apply(time.perf_counter() - t0)
+            grads = self._dense_of(grads)
         self.apply_range(grads[: self.n], weight, 0, self.n)
         return self.finish_round_apply(time.perf_counter() - t0)
+
+    @property
+    def _kcap(self) -> int:
+        return topk.topk_k(self.n, self.cfg.topk_ratio)
+
+    def _dense_of(self, payload: torch.Tensor, out: torch.Tensor | None = None, add: bool = False):
+        """Top-k payload -> dense fp32 gradient (into the aggregation buffer by default)."""
+        if out is None:
+            if self.agg is None:
+                self.agg = torch.zeros(self.n, dtype=torch.float32, device=self.device)
+            out = self.agg
+        if not add:
+            out.zero_()
+        return topk.decode_add(payload, out, 1.0, self._kcap)
 
     def apply_range(self, g: torch.Tensor, weight: float, lo: int, hi: int):
         """The update restricted to params[lo:hi] (g holds exactly that slice): one bucket of a
@@ -97,6 +118,9 @@ class ParameterServer:
     def _accumulate(self, grads: torch.Tensor, first: bool):
         if self.agg is None:
             self.agg = torch.zeros(self.n, dtype=torch.float32, device=self.device)
+        if grads.dtype == torch.int32:
+            self._dense_of(grads, self.agg, add=not first)
+            return
         if first:
             self.agg.copy_(grads[: self.n])
         else:
@@ -125,7 +149,9 @@ class ParameterServer:
                 # reference: pending[worker_id] = grads (overwrites), average over the dict
                 # entries when the push counter reaches total_workers (server.py:264-288)
                 if res.decision in (WAIT, APPLY):
-                    self._pending[worker_id] = grads[: self.n].to(torch.float32).clone()
+                    self._pending[worker_id] = (self._dense_of(grads, torch.zeros(self.n, device=self.device))
+                                                if grads.dtype == torch.int32
+                                                else grads[: self.n].to(torch.float32).clone())
                 if res.apply:
                     self._accumulate(sum(self._pending.values()), True)
                     self._pending.clear()
@@ -210,6 +236,23 @@ class ParameterServer:
             return True
         return False
 
+    def apply_gathered(self, payloads: list, members: list[int], local_steps: list[int],
+                       buffers_sum: torch.Tensor | None = None) -> bool:
+        """Sync round with top-k payloads gathered to rank 0: decode all into one dense fp32
+        sum, then the usual averaged apply."""
+        res = None
+        for wid, ls in zip(members, local_steps):
+            res = self.core.on_push(wid, ls)
+        self.bytes_pushed += sum(p.numel() * 4 for p in payloads[: max(1, len(members))])
+        if res is not None and res.apply:
+            for i, p in enumerate(payloads):
+                self._dense_of(p, add=i > 0)
+            self.apply(self.agg, res.weight)
+            if buffers_sum is not None:
+                self.set_buffers_from_sum(buffers_sum, len(members))
+            return True
+        return False
+
     # ------------------------------------------------------------------ checkpoint
     def checkpoint(self, path: str | None = None) -> str:
         step = self.core.global_step
@@ -268,8 +311,12 @@ class ParameterServer:
         expected = expected if expected is not None else len(rank_of) + (1 if local_queue is not None else 0)
         finished = set()
         n = self.n
-        wire_dtype = torch.float16 if self.cfg.codec == "fp16" else torch.float32
-        slots = {w: torch.empty(n, dtype=wire_dtype, device=self.device) for w in rank_of}
+        if self.cfg.codec == "topk":
+            words = topk.payload_words(self._kcap)
+            slots = {w: torch.empty(words, dtype=torch.int32, device=self.device) for w in rank_of}
+        else:
+            wire_dtype = torch.float16 if self.cfg.codec == "fp16" else torch.float32
+            slots = {w: torch.empty(n, dtype=wire_dtype, device=self.device) for w in rank_of}
         # one fetch snapshot per worker (codec wire buffers): an in-flight send never races the
         # next update of the arena
         from .codec import FetchCodec
@@ -320,7 +367,7 @@ class ParameterServer:
                     if bwork is not None:
                         transport.completed(bwork) or bwork.wait()
                     res = self.core.on_push(wid, ls)
-                    self.bytes_pushed += n * slots[wid].element_size()
+                    self.bytes_pushed += slots[wid].numel() * slots[wid].element_size()
                     if res.apply:
                         self.apply(slots[wid], res.weight)
                         if bwork is not None:
@@ -340,7 +387,7 @@ class ParameterServer:
                         break
                     if kind == "push":
                         res = self.core.on_push(wid, ls)
-                        self.bytes_pushed += n * grads.element_size()
+                        self.bytes_pushed += min(n, grads.numel()) * grads.element_size()
                         if res.apply:
                             self.apply(grads, res.weight)
                             if box.get("bufs") is not None:

@@ -1,0 +1,101 @@
+"""Top-k gradient compression with error feedback (push codec ``--codec topk``).
+
+The reference's only "gradient compression" is the fp32 -> fp16 cast of every gradient
+(reference: src/workers/worker.py:264-268, src/parameter_server/server.py:232-237, README.md:29).
+BASELINE.json's ResNet-50 config asks for top-k gradient compression; this is it:
+
+* worker: ``acc = resid + g``; send the k = ceil(ratio * n) entries of largest |acc| as
+  (int32 index, fp16 value); keep ``resid = acc - sent`` (error feedback, incl. the fp16
+  rounding of the sent values) — csrc/kernels/topk.hip does the exact radix select, the
+  compaction and the residual update on the device without a host round trip;
+* wire: one fixed-size int32 payload ``[count, kcap, n, 0 | idx[kcap] | fp16 val[kcap]]``
+  (6 bytes per kept entry: 1% of ResNet-18 = 0.67 MB instead of 22.4 MB of fp16);
+* server: ``decode_add`` scatters a payload into a dense fp32 buffer (sync rounds sum the W
+  payloads there, then the usual fused SGD apply), or — async, no optimizer state — straight
+  into the fp32 master parameters with scale ``-lr * staleness_weight``.
+
+Sparse payloads do not map onto an RCCL reduce, so the sync round gathers the W payloads to
+rank 0 (RCCL gather = point-to-point over xGMI) instead of reducing dense gradients.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+def topk_k(n: int, ratio: float) -> int:
+    return max(1, min(n, int(math.ceil(ratio * n))))
+
+
+def payload_words(kcap: int) -> int:
+    return 4 + kcap + (kcap + 1) // 2
+
+
+def empty_payload(n: int, ratio: float, device) -> torch.Tensor:
+    """A zero-entry payload (the dedicated server rank's contribution to a gather)."""
+    k = topk_k(n, ratio)
+    p = torch.zeros(payload_words(k), dtype=torch.int32, device=device)
+    p[1] = k
+    p[2] = n
+    return p
+
+
+def decode_add(payload: torch.Tensor, dst: torch.Tensor, scale: float, kcap: int):
+    """dst[idx] += scale * val for every entry of ``payload`` (indices within one payload are
+    unique, so payloads of several workers are decoded one after another)."""
+    if dst.device.type == "cuda":
+        from ..ops import kernels as K
+
+        K.topk_decode_add(payload, dst, scale, kcap)
+        return dst
+    count = min(int(payload[0]), kcap)
+    idx = payload[4:4 + count].long()
+    vals = payload[4 + kcap:].view(torch.float16)[:count].float()
+    dst.index_add_(0, idx, vals * scale)
+    return dst
+
+
+class TopKCodec:
+    """Worker-side encoder: owns the error-feedback residual and the payload buffer."""
+
+    def __init__(self, n: int, ratio: float, device="cpu"):
+        self.n = n
+        self.ratio = ratio
+        self.k = topk_k(n, ratio)
+        self.kcap = self.k
+        self.device = torch.device(device)
+        self.payload = torch.zeros(payload_words(self.kcap), dtype=torch.int32, device=self.device)
+        self.resid = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.ws = None
+        if self.device.type == "cuda":
+            from ..ops import kernels as K
+
+            self.ws = torch.zeros(K.topk_workspace_words(), dtype=torch.int32, device=self.device)
+
+    @property
+    def nbytes(self) -> int:
+        return self.payload.numel() * 4
+
+    def encode(self, g: torch.Tensor) -> torch.Tensor:
+        g = g[: self.n]
+        if self.device.type == "cuda":
+            from ..ops import kernels as K
+
+            K.topk_encode(g, self.resid, self.k, self.kcap, self.payload, self.ws)
+            return self.payload
+        acc = self.resid.add_(g.to(torch.float32))
+        _, idx = torch.topk(acc.abs(), self.k, sorted=False)
+        idx, _ = torch.sort(idx)
+        vals = acc[idx].clamp(-65504.0, 65504.0).to(torch.float16)
+        acc[idx] -= vals.to(torch.float32)
+        p = self.payload
+        p.zero_()
+        p[0], p[1], p[2] = self.k, self.kcap, self.n
+        p[4:4 + self.k] = idx.to(torch.int32)
+        v = p[4 + self.kcap:].view(torch.float16)
+        v[: self.k] = vals
+        return p
+
+    def decode_add(self, payload, dst, scale=1.0):
+        return decode_add(payload, dst, scale, self.kcap)

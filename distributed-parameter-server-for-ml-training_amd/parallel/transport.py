@@ -40,6 +40,9 @@ class LocalTransport:
     def broadcast_from_server(self, t):
         return t
 
+    def gather_to_server(self, t):
+        return [t]
+
     def isend(self, t, dst):
         raise RuntimeError("LocalTransport has no peers")
 
@@ -84,6 +87,16 @@ class DistTransport:
     def broadcast_from_server(self, t):
         dist.broadcast(t, src=0)
         return t
+
+    def gather_to_server(self, t):
+        """Equal-size tensors of every rank -> list on rank 0 (RCCL gather: point-to-point
+        sends into rank 0; used for top-k payloads, which cannot be reduced)."""
+        if self.rank == 0:
+            out = [t] + [torch.empty_like(t) for _ in range(self.world_size - 1)]
+            dist.gather(t, gather_list=out, dst=0)
+            return out
+        dist.gather(t, gather_list=None, dst=0)
+        return None
 
     # ---- bucketed (overlapped) sync round: non-blocking; RCCL runs on its own stream ordered
     # after the caller's stream at issue time, work.wait() orders the caller's stream after it

@@ -96,11 +96,16 @@ class SyncCollectiveChannel:
         return self._gs
 
     def push(self, worker_id, grads, local_step, buffers=None):
-        self.t.reduce_sum_to_server(grads)
+        sparse = grads.dtype == torch.int32  # top-k payloads cannot be summed by a reduce: gather
+        gathered = self.t.gather_to_server(grads) if sparse else self.t.reduce_sum_to_server(grads)
         if buffers is not None:
             self.t.reduce_sum_to_server(buffers)
         if self.server is not None:
-            self.server.apply_reduced(grads, self.members, [local_step] * len(self.members), buffers_sum=buffers)
+            steps = [local_step] * len(self.members)
+            if sparse:
+                self.server.apply_gathered(gathered, self.members, steps, buffers_sum=buffers)
+            else:
+                self.server.apply_reduced(grads, self.members, steps, buffers_sum=buffers)
             self.server.maybe_checkpoint()
         else:
             self._gs = getattr(self, "_gs", 0) + 1
@@ -198,6 +203,11 @@ class Worker:
         self.images = 0
         self.timer = M.PhaseTimer(device=getattr(compute, "device", None))
         self.sampler = None
+        self.topk = None
+        if cfg.codec == "topk":
+            from .topk import TopKCodec
+
+            self.topk = TopKCodec(compute.layout.param_numel, cfg.topk_ratio, getattr(compute, "device", "cpu"))
 
     # ---------------------------------------------------------------- reference API
     def connect_to_server(self):
@@ -225,7 +235,10 @@ class Worker:
         bufs = None
         if self.cfg.bn_sync:
             bufs = self.compute.local_arena[self.compute.layout.param_numel:]
-        ok = self.channel.push(self.worker_id, self.compute.grads, self.global_step_cache, buffers=bufs)
+        g = self.compute.grads
+        if self.topk is not None:  # --codec topk: error-feedback top-k payload (parallel/topk.py)
+            g = self.topk.encode(g)
+        ok = self.channel.push(self.worker_id, g, self.global_step_cache, buffers=bufs)
         if not ok:
             self.pushes_rejected += 1
         return ok

@@ -45,6 +45,11 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--model", choices=["resnet18", "resnet50"], default="resnet18",
+                    help="resnet18: the headline CIFAR-100 config; resnet50: BASELINE config 5 (ImageNet "
+                         "shape, use with --codec topk)")
+    ap.add_argument("--train-samples", type=int, default=None,
+                    help="synthetic dataset size in HBM (default 50000 for resnet18, 4096 for resnet50)")
     ap.add_argument("--topology", choices=["colocated", "dedicated"], default="colocated")
     ap.add_argument("--codec", choices=["fp16", "none", "topk"], default="fp16")
     ap.add_argument("--topk-ratio", type=float, default=0.01)
@@ -63,7 +68,8 @@ def main():
         raise SystemExit("bench.py needs MI355X GPUs")
     torch.cuda.set_device(local % torch.cuda.device_count())
     device = torch.device("cuda", torch.cuda.current_device())
-    cfg = PSConfig(mode="sync", model="resnet18", batch_size=a.batch, lr=0.1, sync_steps=1, epochs=1,
+    n_train = a.train_samples or (50000 if a.model == "resnet18" else 4096)
+    cfg = PSConfig(mode="sync", model=a.model, batch_size=a.batch, train_samples=n_train, lr=0.1, sync_steps=1, epochs=1,
                    eval_every=0, verbose=0, codec=a.codec, topk_ratio=a.topk_ratio, use_graph=not a.no_graph, fetch_codec=a.fetch_codec,
                    overlap=a.overlap, bucket_mb=a.bucket_mb).validate()
     model, layout, arena, counters = build_state(cfg)
@@ -88,7 +94,7 @@ def main():
     wk = None
     zeros = None
     if is_worker:
-        comp = HipCompute(model, layout, a.batch, device, "resnet18", wire, seed=rank, use_graph=cfg.use_graph)
+        comp = HipCompute(model, layout, a.batch, device, a.model, wire, seed=rank, use_graph=cfg.use_graph)
         wid = worker_ranks.index(rank)
         wk = Worker(cfg, comp, chan, train, None, worker_name=f"worker-{wid}", rank=rank, log=lambda *x: None,
                     requested_id=wid)
@@ -138,8 +144,10 @@ def main():
     value = imgs / dt
     loss = wk.compute.last_loss() if wk is not None else None
     if rank == 0:
+        r18 = a.model == "resnet18"
         rec = {
-            "metric": "images/sec (whole node) ResNet-18 sync-PS at 1/2/4/8 MI355X; async staleness",
+            "metric": ("images/sec (whole node) ResNet-18 sync-PS at 1/2/4/8 MI355X; async staleness" if r18 else
+                       "images/sec (whole node) ResNet-50 ImageNet-shape sync-PS + top-k (BASELINE config 5)"),
             "value": round(value, 2),
             "unit": "images/s",
             "n_gpus": world,
@@ -148,12 +156,15 @@ def main():
             "ms_per_step": round(1e3 * dt / a.steps, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / BASELINE_SYNC_IMG_S, 2),
+            "vs_baseline": round(value / BASELINE_SYNC_IMG_S, 2) if r18 else None,
             "dtype": "bf16",
-            "data": "synthetic CIFAR-100-shaped (50000x32x32x3 uint8 in HBM, on-device crop/flip/normalize), "
-                    "random-init weights",
+            "data": (f"synthetic CIFAR-100-shaped ({n_train}x32x32x3 uint8 in HBM, on-device crop/flip/normalize), "
+                     "random-init weights" if r18 else
+                     f"synthetic ImageNet-shaped ({n_train}x224x224x3 uint8 in HBM, on-device crop/flip/normalize), "
+                     "random-init weights"),
             "config": {
-                "model": "resnet18-cifar (11,220,132 params, reference ResNet18(num_classes=100))",
+                "model": ("resnet18-cifar (11,220,132 params, reference ResNet18(num_classes=100))" if r18 else
+                          f"resnet50-imagenet ({layout.param_numel:,} params, 1000 classes)"),
                 "global_batch": a.batch * W,
                 "per_worker_batch": a.batch,
                 "seq_len": None,
@@ -171,7 +182,7 @@ def main():
             },
             "global_steps": server.core.global_step,
             "last_loss": round(loss, 4) if loss is not None else None,
-            "baseline_img_s": BASELINE_SYNC_IMG_S,
+            "baseline_img_s": BASELINE_SYNC_IMG_S if r18 else None,
         }
         print(json.dumps(rec), flush=True)
     if a.host_timing:

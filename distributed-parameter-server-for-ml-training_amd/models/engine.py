@@ -255,10 +255,13 @@ class HipResNetEngine:
                          K.conv2_workspace_bytes(B, cs.h, cs.w, cs.cp, cs.kgd) // 4 if cs.need_dgrad else 0)
 
         track(st)
-        if sp.maxpool:
-            raise NotImplementedError("max-pool stem (ResNet-50) kernels land with the ResNet-50 engine")
-        self.blk = []
         h_in = self.a0
+        if sp.maxpool:  # ImageNet stem: 3x3/s2 max-pool after bn1+relu (csrc/kernels/pool.hip)
+            mh, mw = (p + 2 - 3) // 2 + 1, (q + 2 - 3) // 2 + 1
+            self.p0 = self._bf(B, mh, mw, st.cout)
+            self.pidx = torch.empty(B, mh, mw, st.cout, dtype=torch.uint8, device=self.dev)
+            h_in = self.p0
+        self.blk = []
         for b in sp.blocks:
             d = dict(inp=h_in)
             d["y"] = [self._bf(B, *cs.out_hw, cs.cout) for cs in b.convs]
@@ -394,7 +397,9 @@ class HipResNetEngine:
             self._bn_train(sp.stem_bn, arena, T, npix)
         else:
             self._bn_eval(sp.stem_bn, arena)
-        K.bn_apply(self.y0, self.bn["bn1"]["affine"], self.a0, st.cout, relu=True)
+        K.bn_apply(self.y0, self.bn[sp.stem_bn.name]["affine"], self.a0, st.cout, relu=True)
+        if sp.maxpool:
+            K.maxpool3s2_fwd(self.a0, self.p0, self.pidx)
         for b, d in zip(sp.blocks, self.blk):
             src = d["inp"]
             L = len(b.convs)
@@ -463,6 +468,9 @@ class HipResNetEngine:
         st = sp.stem_conv
         p, q = st.out_hw
         g = self.blk[0]["gin"] if self.blk else self.dfinal
+        if sp.maxpool:
+            K.maxpool3s2_bwd(g, self.pidx, self.g0)
+            g = self.g0
         self._bn_bwd(sp.stem_bn, arena, g, self.a0, self.y0, self.dy0, B * p * q)
         self._wgrad(st, self.x0, self.dy0)
 

@@ -66,6 +66,8 @@ _KERNEL_SIGS = {
     "psx_synth_gen": (i32, [vp, vp, i32, i32, i32, i32, u32, u32, vp]),
     "psx_augment": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, u32, vp, i32, vp, vp, vp]),
     "psx_nchw_to_nhwc": (i32, [vp, vp, i32, i32, i32, i32, i32, vp]),
+    "psx_maxpool3s2_fwd": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
+    "psx_maxpool3s2_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
     "psx_topk_workspace_words": (i32, []),
     "psx_topk_payload_words": (i32, [i32]),
     "psx_topk_encode": (i32, [vp, i32, vp, i64, i32, i32, vp, vp, vp]),

@@ -184,6 +184,17 @@ def sgd_apply(p, g, lr, gscale=1.0, momentum=0.0, wd=0.0, buf=None, first=False,
                                   int(first), int(fp16), stream_ptr()), "sgd_apply")
 
 
+def maxpool3s2_fwd(x, y, arg):
+    """3x3/s2/p1 max-pool, NHWC bf16; arg (uint8, y's shape) keeps the window argmax."""
+    B, H, W, C = x.shape
+    check(kernels().psx_maxpool3s2_fwd(ptr(x), ptr(y), ptr(arg), B, H, W, C, stream_ptr()), "maxpool3s2_fwd")
+
+
+def maxpool3s2_bwd(dy, arg, dx):
+    B, H, W, C = dx.shape
+    check(kernels().psx_maxpool3s2_bwd(ptr(dy), ptr(arg), ptr(dx), B, H, W, C, stream_ptr()), "maxpool3s2_bwd")
+
+
 def topk_workspace_words() -> int:
     return kernels().psx_topk_workspace_words()
 

@@ -1,4 +1,5 @@
-"""conv v2 (LDS-DMA pipelined, split-K) vs torch fp32 on every ResNet-18 conv shape at batch 128."""
+"""conv v2 (LDS-DMA pipelined, split-K) vs torch fp32 on every ResNet-18 conv shape at batch 128
+and every ResNet-50 (224x224) conv shape at batch 8."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -13,6 +14,13 @@ SHAPES = [(128, c, o, hw, k, s, p) for (_, c, o, hw, k, s, p) in [
     (8, 3, 64, 32, 3, 1, 1), (8, 64, 64, 32, 3, 1, 1), (8, 64, 128, 32, 3, 2, 1), (8, 64, 128, 32, 1, 2, 0),
     (8, 128, 128, 16, 3, 1, 1), (8, 128, 256, 16, 3, 2, 1), (8, 128, 256, 16, 1, 2, 0), (8, 256, 256, 8, 3, 1, 1),
     (8, 256, 512, 8, 3, 2, 1), (8, 256, 512, 8, 1, 2, 0), (8, 512, 512, 4, 3, 1, 1)]] + [(3, 64, 64, 8, 3, 1, 1)]
+# every distinct ResNet-50 (ImageNet 224) conv: 7x7/s2 stem, bottleneck 1x1s, strided 3x3s, downsamples
+SHAPES += [(4, 3, 64, 224, 7, 2, 3), (8, 64, 64, 56, 1, 1, 0), (8, 64, 64, 56, 3, 1, 1), (8, 64, 256, 56, 1, 1, 0),
+           (8, 256, 64, 56, 1, 1, 0), (8, 256, 128, 56, 1, 1, 0), (8, 128, 128, 56, 3, 2, 1),
+           (8, 128, 512, 28, 1, 1, 0), (8, 256, 512, 56, 1, 2, 0), (8, 512, 128, 28, 1, 1, 0),
+           (8, 128, 128, 28, 3, 1, 1), (8, 256, 256, 28, 3, 2, 1), (8, 512, 1024, 28, 1, 2, 0),
+           (8, 1024, 256, 14, 1, 1, 0), (8, 512, 512, 14, 3, 2, 1), (8, 1024, 2048, 14, 1, 2, 0),
+           (8, 2048, 512, 7, 1, 1, 0), (8, 512, 512, 7, 3, 1, 1), (8, 512, 2048, 7, 1, 1, 0)]
 
 
 def _ws(nb, oh, ow, oc, kg):

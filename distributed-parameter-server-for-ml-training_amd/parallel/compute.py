@@ -74,9 +74,11 @@ class TorchCompute:
         self.model.train()
         self.model.zero_grad(set_to_none=False)
         x, y = self._batch(dataset, idx, train=True)
-        loss = F.cross_entropy(self.model(x), y)
+        out = self.model(x)
+        loss = F.cross_entropy(out, y)
         loss.backward()
         self._loss = loss.item()
+        self._correct = int((out.argmax(1) == y).sum())
         with torch.no_grad():
             for name, p in self.model.named_parameters():
                 e = self.layout.entries[name]
@@ -89,6 +91,10 @@ class TorchCompute:
 
     def last_loss(self) -> float:
         return self._loss
+
+    def step_stats(self):
+        """(sum of per-sample losses, #correct) of the last train step."""
+        return torch.tensor(self._loss * self.B, dtype=torch.float64), torch.tensor(self._correct)
 
     @torch.no_grad()
     def evaluate(self, dataset, batch=None) -> float:
@@ -151,6 +157,10 @@ class HipCompute:
 
     def last_loss(self) -> float:
         return float(self.engine.loss.mean())
+
+    def step_stats(self):
+        """Device tensors (sum of per-sample losses, #correct) of the last train step (no sync)."""
+        return self.engine.loss.sum(dtype=torch.float64), self.engine.correct.sum(dtype=torch.int64)
 
     @torch.no_grad()
     def evaluate(self, dataset, batch=None) -> float:

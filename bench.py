@@ -30,7 +30,7 @@ import torch.distributed as dist  # noqa: E402
 
 import psx  # noqa: E402,F401
 from psx.parallel.compute import HipCompute  # noqa: E402
-from psx.parallel.runner import build_state, make_datasets, make_sync_channel  # noqa: E402
+from psx.parallel.runner import AsyncSession, build_state, make_datasets, make_sync_channel  # noqa: E402
 from psx.parallel.server import ParameterServer  # noqa: E402
 from psx.parallel.transport import DistTransport, env_world  # noqa: E402
 from psx.parallel.worker import InProcessChannel, Worker  # noqa: E402
@@ -61,6 +61,9 @@ def main():
                     help="stream gradient buckets (reduce/apply/broadcast) during the backward pass")
     ap.add_argument("--bucket-mb", type=float, default=4.0)
     ap.add_argument("--host-timing", action="store_true", help="report host-side issue time per step (stderr)")
+    ap.add_argument("--mode", choices=["sync", "async"], default="sync",
+                    help="async: workers push/fetch independently (staleness-weighted server updates)")
+    ap.add_argument("--staleness-bound", type=int, default=5)
     a = ap.parse_args()
 
     rank, world, local = env_world()
@@ -69,7 +72,7 @@ def main():
     torch.cuda.set_device(local % torch.cuda.device_count())
     device = torch.device("cuda", torch.cuda.current_device())
     n_train = a.train_samples or (50000 if a.model == "resnet18" else 4096)
-    cfg = PSConfig(mode="sync", model=a.model, batch_size=a.batch, train_samples=n_train, lr=0.1, sync_steps=1, epochs=1,
+    cfg = PSConfig(mode=a.mode, staleness_bound=a.staleness_bound, model=a.model, batch_size=a.batch, train_samples=n_train, lr=0.1, sync_steps=1, epochs=1,
                    eval_every=0, verbose=0, codec=a.codec, topk_ratio=a.topk_ratio, use_graph=not a.no_graph, fetch_codec=a.fetch_codec,
                    overlap=a.overlap, bucket_mb=a.bucket_mb).validate()
     model, layout, arena, counters = build_state(cfg)
@@ -85,22 +88,36 @@ def main():
     cfg.workers = W
     is_worker = rank in worker_ranks
     server = None
+    quiet = lambda *x, **k: None  # noqa: E731
+    async_dist = a.mode == "async" and t is not None
     if rank == 0:
-        server = ParameterServer(cfg, layout, arena, counters, device=device, total_workers=W, log=lambda *x: None)
-        for i in range(W):
-            server.register_worker(f"worker-{i}", i)
+        server = ParameterServer(cfg, layout, arena, counters, device=device, total_workers=W, log=quiet)
+        if not async_dist:
+            for i in range(W):
+                server.register_worker(f"worker-{i}", i)
     train, _ = make_datasets(cfg, device, model.fc.out_features)
-    chan = InProcessChannel(server) if t is None else make_sync_channel(cfg, t, server, W, layout, device)
+    comp = HipCompute(model, layout, a.batch, device, a.model, wire, seed=rank, use_graph=cfg.use_graph) \
+        if is_worker else None
     wk = None
     zeros = None
-    if is_worker:
-        comp = HipCompute(model, layout, a.batch, device, a.model, wire, seed=rank, use_graph=cfg.use_graph)
-        wid = worker_ranks.index(rank)
-        wk = Worker(cfg, comp, chan, train, None, worker_name=f"worker-{wid}", rank=rank, log=lambda *x: None,
-                    requested_id=wid)
-        wk.connect_to_server()
+    sess = None
+    chan = None
+    if async_dist:  # server event loop thread on rank 0, mailbox + RCCL p2p (parallel/runner.py)
+        names = [f"worker-r{r}" for r in range(world)]
+        sess = AsyncSession(cfg, t, rank, worker_ranks, server, comp, train, None, names, quiet)
+        wk = sess.worker
+    else:
+        chan = InProcessChannel(server) if t is None else make_sync_channel(cfg, t, server, W, layout, device)
+        if is_worker:
+            wid = worker_ranks.index(rank)
+            wk = Worker(cfg, comp, chan, train, None, worker_name=f"worker-{wid}", rank=rank, log=quiet,
+                        requested_id=wid)
+            wk.connect_to_server()
+    if wk is not None:
         wk.setup_data()
         batches = wk.sampler.epoch_indices(0)
+    elif sess is not None:
+        pass  # dedicated async server rank: its event-loop thread does the work
     elif a.codec == "topk":
         from psx.parallel.topk import empty_payload
 
@@ -113,7 +130,9 @@ def main():
             wk.fetch_parameters()
             wk.train_local_batch(batches[i % len(batches)])
             wk.push_gradients()
-        else:  # dedicated server rank
+        elif sess is not None:
+            pass
+        else:  # dedicated sync server rank
             chan.fetch(None, None)
             if a.codec != "topk":
                 zeros.zero_()
@@ -122,7 +141,9 @@ def main():
     def barrier_sync():
         torch.cuda.synchronize()
         if t is not None:
-            dist.barrier()
+            # async: the server thread drives RCCL p2p on the default group, so host barriers
+            # use the gloo control group
+            t.barrier() if async_dist else dist.barrier()
         torch.cuda.synchronize()
 
     for i in range(a.warmup):
@@ -136,7 +157,9 @@ def main():
         host.append(time.perf_counter() - h0)
     barrier_sync()
     dt = time.perf_counter() - t0
-    if t is not None:
+    if t is not None and async_dist:
+        dt = max(t.all_gather_object(dt))
+    elif t is not None:
         tt = torch.tensor([dt], dtype=torch.float64, device=device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
@@ -168,9 +191,12 @@ def main():
                 "global_batch": a.batch * W,
                 "per_worker_batch": a.batch,
                 "seq_len": None,
-                "parallelism": (f"sync-PS: rank0 = parameter server{' only' if dedicated else ' + worker 0'}, "
-                                f"{W} data-parallel worker(s); RCCL reduce(fp16 grads)+broadcast(fp32 arena) "
-                                f"over xGMI" if t is not None else "sync-PS: server + 1 worker co-located on 1 GPU"),
+                "parallelism": (
+                    f"{a.mode}-PS: rank0 = parameter server{' only' if dedicated else ' + worker 0'}, {W} data-parallel "
+                    f"worker(s); " + ("RCCL reduce(grads) + broadcast(params) over xGMI" if a.mode == "sync" else
+                                      "shm mailbox control + RCCL send/recv over xGMI")
+                    if t is not None else f"{a.mode}-PS: server + 1 worker co-located on 1 GPU"),
+                "mode": a.mode,
                 "lr": 0.1,
                 "sync_steps": 1,
                 "codec": a.codec if a.codec != "topk" else f"topk({a.topk_ratio}) + error feedback",
@@ -184,10 +210,19 @@ def main():
             "last_loss": round(loss, 4) if loss is not None else None,
             "baseline_img_s": BASELINE_SYNC_IMG_S if r18 else None,
         }
-        print(json.dumps(rec), flush=True)
     if a.host_timing:
         print(json.dumps({"rank": rank, "host_issue_ms_per_step": round(1e3 * sum(host) / len(host), 4),
                           "host_issue_ms_max": round(1e3 * max(host), 4)}), file=sys.stderr, flush=True)
+    if sess is not None:
+        sess.finish()
+        sess.close()
+    if rank == 0:
+        if a.mode == "async":
+            sm = server.final_metrics()
+            rec["async_staleness"] = {k: sm.get(k) for k in ("average_gradient_staleness", "max_staleness_observed",
+                                                             "rejected_pushes", "staleness_histogram")}
+            rec["global_steps"] = server.core.global_step
+        print(json.dumps(rec), flush=True)
     if hasattr(chan, "drain"):
         chan.drain()
     if t is not None:

@@ -161,7 +161,6 @@ def run_distributed(cfg, log=print) -> dict:
     worker_ranks = list(range(1, world)) if dedicated else list(range(world))
     W = len(worker_ranks)
     wid_of_rank = {r: i for i, r in enumerate(worker_ranks)}
-    rank_of_wid = {i: r for r, i in wid_of_rank.items()}
     if cfg.workers != W:
         if rank == 0 and cfg.verbose:
             log(f"[psx] {world} ranks, topology {cfg.topology}: total workers = {W} (overrides --workers {cfg.workers})")
@@ -195,39 +194,10 @@ def run_distributed(cfg, log=print) -> dict:
         else:
             _dedicated_sync_server(cfg, server, chan, steps, device)
     else:
-        mbox_name = t.broadcast_object(f"/psx_{uuid.uuid4().hex[:12]}" if rank == 0 else None)
-        mbox = CP.ShmMailbox(mbox_name, nreply=world, owner=(rank == 0)) if rank == 0 else None
-        t.barrier()
-        if rank != 0:
-            mbox = CP.ShmMailbox(mbox_name, nreply=world, owner=False)
-        remote = {w: r for w, r in rank_of_wid.items() if r != 0}
-        if rank == 0:
-            q = queue.Queue() if is_worker else None
-            srv = threading.Thread(target=server.serve_async, args=(t, mbox, remote),
-                                   kwargs={"local_queue": q, "expected": W}, daemon=True)
-            if is_worker:
-                srv.start()
-                wk = Worker(cfg, comp, LocalAsyncChannel(server, q), train, test, worker_name=names[0], rank=0,
-                            log=lg, requested_id=wid_of_rank[0])
-                wk.connect_to_server()
-                wk.run_training()
-                srv.join()
-            else:
-                server.serve_async(t, mbox, remote, local_queue=None, expected=W)
-        else:
-            hb = None
-            chan = AsyncChannel(t, mbox, rank, codec=FetchCodec(layout, cfg.fetch_codec, device))
-            wk = Worker(cfg, comp, chan, train, test, worker_name=names[rank], rank=rank, log=lg,
-                        requested_id=wid_of_rank[rank])
-            wk.connect_to_server()
-            hb = CP.Heartbeat(mbox, wk.worker_id, rank, period=max(1.0, cfg.heartbeat_timeout / 6))
-            hb.start()
-            try:
-                wk.run_training()
-            finally:
-                hb.stop()
-        t.barrier()
-        mbox.close()
+        sess = AsyncSession(cfg, t, rank, worker_ranks, server, comp if is_worker else None, train, test, names, lg)
+        sess.run_training()
+        sess.close()
+        wk = sess.worker
     if device.type == "cuda":
         torch.cuda.synchronize()
     wall = time.time() - t0
@@ -240,6 +210,73 @@ def run_distributed(cfg, log=print) -> dict:
         result["server"] = server.final_metrics(emit=True, extra=extra)
     t.close()
     return result
+
+
+class AsyncSession:
+    """Rank-local roles of a multi-process async job.
+
+    Rank 0 runs the parameter-server event loop (ParameterServer.serve_async: control requests
+    on the shared-memory mailbox, tensors over RCCL point-to-point) in a thread, next to the
+    co-located worker 0 (``colocated``) or alone (``dedicated``); every other rank is a worker
+    talking to it through AsyncChannel, with a heartbeat thread for failure detection."""
+
+    def __init__(self, cfg, t, rank, worker_ranks, server, comp, train, test, names, log):
+        W = len(worker_ranks)
+        wid_of_rank = {r: i for i, r in enumerate(worker_ranks)}
+        rank_of_wid = {i: r for r, i in wid_of_rank.items()}
+        self.t, self.rank = t, rank
+        mbox_name = t.broadcast_object(f"/psx_{uuid.uuid4().hex[:12]}" if rank == 0 else None)
+        self.mbox = CP.ShmMailbox(mbox_name, nreply=t.world_size, owner=True) if rank == 0 else None
+        t.barrier()
+        if rank != 0:
+            self.mbox = CP.ShmMailbox(mbox_name, nreply=t.world_size, owner=False)
+        remote = {w: r for w, r in rank_of_wid.items() if r != 0}
+        self.worker, self.thread, self.hb = None, None, None
+        if rank == 0:
+            q = queue.Queue() if rank in wid_of_rank else None
+            self.thread = threading.Thread(target=server.serve_async, args=(t, self.mbox, remote),
+                                           kwargs={"local_queue": q, "expected": W}, daemon=True)
+            self.thread.start()
+            if q is not None:
+                self.worker = Worker(cfg, comp, LocalAsyncChannel(server, q), train, test, worker_name=names[0],
+                                     rank=0, log=log, requested_id=wid_of_rank[0])
+        elif rank in wid_of_rank:
+            chan = AsyncChannel(t, self.mbox, rank, codec=FetchCodec(comp.layout, cfg.fetch_codec, comp.device))
+            self.worker = Worker(cfg, comp, chan, train, test, worker_name=names[rank], rank=rank, log=log,
+                                 requested_id=wid_of_rank[rank])
+        if self.worker is not None:
+            self.worker.connect_to_server()
+            if rank != 0:
+                self.hb = CP.Heartbeat(self.mbox, self.worker.worker_id, rank,
+                                       period=max(1.0, cfg.heartbeat_timeout / 6))
+                self.hb.start()
+
+    def run_training(self):
+        try:
+            if self.worker is not None:
+                self.worker.run_training()
+        finally:
+            self._stop()
+
+    def finish(self):
+        """End a manually driven worker loop (bench): JobFinished, then wait for the server."""
+        try:
+            if self.worker is not None:
+                self.worker.cleanup()
+        finally:
+            self._stop()
+
+    def _stop(self):
+        if self.hb is not None:
+            self.hb.stop()
+            self.hb = None
+        if self.thread is not None:
+            self.thread.join()
+            self.thread = None
+
+    def close(self):
+        self.t.barrier()
+        self.mbox.close()
 
 
 def make_sync_channel(cfg, t, server, W, layout, device):

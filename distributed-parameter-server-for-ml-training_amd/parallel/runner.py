@@ -180,22 +180,26 @@ def run_distributed(cfg, log=print) -> dict:
     if is_worker:
         comp = make_compute(model, layout, cfg.batch_size, device, cfg.model, _wire_dtype(cfg),
                             seed=cfg.seed + wid_of_rank[rank], use_graph=cfg.use_graph)
+    # restart recovery: a server that resumed from a checkpoint tells every rank how many
+    # global steps are already done (sync: one round per step; async: spread over workers)
+    done = t.broadcast_object(server.core.global_step if rank == 0 else None)
     t0 = time.time()
     if cfg.mode == "sync":
         if rank == 0:
             for r in worker_ranks:
                 server.register_worker(names[r], wid_of_rank[r])
         chan = make_sync_channel(cfg, t, server, W, layout, device)
+        chan._gs = done  # non-server ranks track the global step locally
         if is_worker:
             wk = Worker(cfg, comp, chan, train, test, worker_name=names[rank], rank=rank, log=lg,
                         requested_id=wid_of_rank[rank], steps_per_epoch=steps)
             wk.connect_to_server()
-            wk.run_training()
+            wk.run_training(skip_steps=done)
         else:
-            _dedicated_sync_server(cfg, server, chan, steps, device)
+            _dedicated_sync_server(cfg, server, chan, steps, device, skip=done)
     else:
         sess = AsyncSession(cfg, t, rank, worker_ranks, server, comp if is_worker else None, train, test, names, lg)
-        sess.run_training()
+        sess.run_training(skip_steps=done // max(1, W))
         sess.close()
         wk = sess.worker
     if device.type == "cuda":
@@ -251,10 +255,10 @@ class AsyncSession:
                                        period=max(1.0, cfg.heartbeat_timeout / 6))
                 self.hb.start()
 
-    def run_training(self):
+    def run_training(self, skip_steps: int = 0):
         try:
             if self.worker is not None:
-                self.worker.run_training()
+                self.worker.run_training(skip_steps=skip_steps)
         finally:
             self._stop()
 
@@ -288,7 +292,7 @@ def make_sync_channel(cfg, t, server, W, layout, device):
     return SyncCollectiveChannel(t, server, members=list(range(W)), codec=codec)
 
 
-def _dedicated_sync_server(cfg, server, chan, steps, device):
+def _dedicated_sync_server(cfg, server, chan, steps, device, skip=0):
     """Rank 0 of the dedicated topology: takes part in every round's collectives with a zero
     gradient contribution and applies the averaged update."""
     K = max(1, cfg.sync_steps)
@@ -299,9 +303,11 @@ def _dedicated_sync_server(cfg, server, chan, steps, device):
     else:
         zeros = torch.zeros(server.n, dtype=_wire_dtype(cfg), device=device)
     zbuf = torch.zeros(server.layout.buffer_numel, dtype=torch.float32, device=device) if cfg.bn_sync else None
-    done = 0
+    done = skip
     for epoch in range(cfg.epochs):
         for b in range(steps):
+            if epoch * steps + b < skip:
+                continue
             if b % K == 0:
                 chan.fetch(None, None)
                 if cfg.codec != "topk":

@@ -71,6 +71,15 @@ class DistTransport:
             kw = {}
             if backend == "nccl" and device is not None:
                 kw["device_id"] = torch.device(device)
+            attempt = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+            if attempt and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
+                # restarted group on the agent's long-lived store (static rendezvous): namespace
+                # this attempt's keys, or ranks would read the dead attempt's peer addresses
+                base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]),
+                                     int(os.environ["WORLD_SIZE"]), is_master=False,
+                                     timeout=datetime.timedelta(seconds=timeout_s))
+                kw.update(store=dist.PrefixStore(f"psx/attempt{attempt}", base), rank=int(os.environ["RANK"]),
+                          world_size=int(os.environ["WORLD_SIZE"]))
             dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
         self.backend = dist.get_backend()
         self.rank = dist.get_rank()

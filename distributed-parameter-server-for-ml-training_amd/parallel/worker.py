@@ -261,10 +261,14 @@ class Worker:
         if torch.cuda.is_available() and getattr(self.compute, "device", torch.device("cpu")).type == "cuda":
             torch.cuda.synchronize()
 
-    def run_training(self):
+    def run_training(self, skip_steps: int = 0):
+        """The reference training loop (worker.py:350-403). ``skip_steps`` fast-forwards past
+        rounds that a resumed server checkpoint already contains (restart recovery)."""
         if self.sampler is None:
             self.setup_data()
         self.log(f"\n--- Starting distributed training for {self.num_epochs} epochs ---")
+        if skip_steps:
+            self.log(f"[Resume] worker {self.worker_id} skips {skip_steps} completed steps")
         self.training_start_time = time.time()
         K = self.local_steps_per_sync
         fi_worker, fi_step = _parse_fault(self.cfg.fault_inject)
@@ -273,6 +277,14 @@ class Worker:
                 self._sync()
                 t_ep = time.time()
                 batches = self.sampler.epoch_indices(epoch)
+                if skip_steps >= len(batches):
+                    skip_steps -= len(batches)
+                    self.local_step_counter += len(batches)
+                    continue
+                if skip_steps:
+                    self.local_step_counter += skip_steps
+                    batches = batches[skip_steps:]
+                    skip_steps = 0
                 for batch_idx, idx in enumerate(batches):
                     if fi_worker == self.worker_id and self.local_step_counter == fi_step:
                         raise _InjectedFault(f"fault injected: worker {self.worker_id} at step {fi_step}")
@@ -350,8 +362,12 @@ class _InjectedFault(RuntimeError):
 
 
 def _parse_fault(spec: str):
-    """'kill_worker:K@S' -> (K, S); anything else -> (None, None)."""
-    if not spec or not spec.startswith("kill_worker:"):
+    """'kill_worker:K@S' -> (K, S); anything else -> (None, None). Only armed on the first
+    attempt of an elastic job (torchrun sets TORCHELASTIC_RESTART_COUNT), so a restarted job
+    resumes instead of failing again."""
+    import os
+
+    if not spec or not spec.startswith("kill_worker:") or int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")):
         return None, None
     body = spec.split(":", 1)[1]
     k, s = body.split("@")

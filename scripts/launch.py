@@ -10,6 +10,7 @@ a log file that scripts/parse_logs.py turns into an experiment-result JSON.
   python scripts/launch.py --nproc 8 --log runs/sync_8.log -- --mode sync --epochs 3
   python scripts/launch.py --nproc 1 -- --mode async --workers 4     # loopback, 4 simulated workers
   python scripts/launch.py --nproc 4 --cpu -- --model resnet_tiny    # gloo rehearsal on CPU
+  python scripts/launch.py --nproc 8 --max-restarts 2 -- --ckpt-every 100 --resume latest  # fault tolerant
 
 The launcher itself never touches the GPU; the job runs as a child process and its exit code
 is returned.
@@ -29,14 +30,15 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def build_command(nproc: int, train_args, cpu=False, port=None, bench=False):
+def build_command(nproc: int, train_args, cpu=False, port=None, bench=False, max_restarts=0):
     script = os.path.join(ROOT, "bench.py" if bench else os.path.join("scripts", "psx_train.py"))
     extra = (["--cpu"] if cpu and not bench else []) + list(train_args)
     if nproc <= 1 and not bench:
         return [sys.executable, script] + extra
     port = port or free_port()
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-            "--master-addr", "127.0.0.1", "--master-port", str(port), script] + extra
+            f"--max-restarts={max_restarts}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+            script] + extra
 
 
 def main(argv=None):
@@ -50,11 +52,14 @@ def main(argv=None):
     ap.add_argument("--log", default="", help="tee the job output to this file")
     ap.add_argument("--cpu", action="store_true", help="gloo + CPU compute (rehearsal)")
     ap.add_argument("--bench", action="store_true", help="launch bench.py instead of the trainer")
+    ap.add_argument("--max-restarts", type=int, default=0,
+                    help="restart the whole job this many times after a rank fails; combine with trainer flags "
+                         "--ckpt-every N --resume latest to continue from the last server checkpoint")
     ap.add_argument("--dry-run", action="store_true")
     a = ap.parse_args(argv)
     if a.bench:
         rest = ["--gpus", str(a.nproc)] + rest
-    cmd = build_command(a.nproc, rest, cpu=a.cpu, bench=a.bench)
+    cmd = build_command(a.nproc, rest, cpu=a.cpu, bench=a.bench, max_restarts=a.max_restarts)
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
     print("[launch]", " ".join(cmd), flush=True)

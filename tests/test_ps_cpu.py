@@ -114,11 +114,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _spawn(nproc, args, timeout=240):
+def _spawn(nproc, args, timeout=240, max_restarts=0):
     port = _free_port()
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     env.pop("CUDA_VISIBLE_DEVICES", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           f"--max-restarts={max_restarts}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "scripts", "psx_train.py"),
            "--cpu"] + args
     r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout)
@@ -256,3 +257,23 @@ def test_dist_sync_overlap_matches_serial(extra):
         outs[ov] = srv
     assert outs[True]["global_steps_completed"] == outs[False]["global_steps_completed"] > 0
     assert outs[True]["final_param_checksum"] == pytest.approx(outs[False]["final_param_checksum"], rel=1e-6)
+
+
+@pytest.mark.parametrize("topology", ["colocated", "dedicated"])
+def test_fault_restart_resumes_from_checkpoint(tmp_path, topology):
+    """Worker 1 dies at its step 5; torchrun restarts the group, the server resumes from the
+    last checkpoint (step 4) and workers skip the rounds it already contains, so the job ends
+    with exactly the fault-free number of global steps."""
+    ck = tmp_path / "ck"
+    args = ["--mode", "sync", "--topology", topology, "--epochs", "2", "--ckpt-every", "2", "--ckpt-dir", str(ck),
+            "--resume", "latest", "--fault-inject", "kill_worker:1@5", "--verbose", "1"]
+    tiny = list(TINY)
+    for opt in ("--epochs", "--verbose"):
+        i = tiny.index(opt)
+        del tiny[i:i + 2]
+    recs, out = _spawn(3, args + tiny, max_restarts=1)
+    assert "fault injected" in out and "[Resume] restored global step 4" in out
+    W = 3 if topology == "colocated" else 2
+    steps = -(-(96 // W + 96 % W) // 8)
+    srv = [r for r in recs if r["type"] == "SERVER_FINAL_METRICS"]
+    assert srv[-1]["global_steps_completed"] == 2 * steps

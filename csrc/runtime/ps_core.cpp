@@ -31,6 +31,9 @@ struct PsCore {
   int next_id = 0;
   std::map<int, WorkerInfo> workers;
   int64_t global_step = 0, total_updates = 0, gradients_processed = 0, async_updates = 0;
+  // sync barrier: rounds completed at APPLY time (global_step follows in on_applied), so a late
+  // push for a round that already completed is recognised as stale, never counted twice
+  int64_t rounds_done = 0;
   int64_t rejected = 0, duplicates = 0;
   // sync round
   std::set<int> round;          // barrier semantics: distinct contributors
@@ -167,7 +170,7 @@ int psx_ps_on_push(void* h, int wid, int64_t local_step, double now, float* weig
   }
 
   // true wait-for-N barrier over live workers
-  if (c->round.count(wid)) {
+  if (local_step < c->rounds_done || c->round.count(wid)) {
     c->duplicates++;
     return PSX_DUPLICATE;
   }
@@ -176,6 +179,7 @@ int psx_ps_on_push(void* h, int wid, int64_t local_step, double now, float* weig
     const int n = (int)c->round.size();
     c->last_members.assign(c->round.begin(), c->round.end());
     c->round.clear();
+    c->rounds_done++;
     if (weight) *weight = 1.f / (float)n;
     if (ncontrib) *ncontrib = n;
     return PSX_APPLY;
@@ -256,6 +260,7 @@ void psx_ps_set_global_step(void* h, int64_t s) {
   PsCore* c = P(h);
   std::lock_guard<std::mutex> g(c->mu);
   c->global_step = s;
+  c->rounds_done = s;
 }
 
 int psx_ps_num_active(void* h) {

@@ -115,7 +115,14 @@ def _free_port():
 
 
 def _spawn(nproc, args, timeout=240, max_restarts=0):
+    """Run a multi-process CPU job; METRICS_JSON records are read from the per-rank jsonl files
+    (--log-dir), not from the ranks' merged stdout, where concurrent writes may interleave."""
+    import tempfile
+
     port = _free_port()
+    logdir = tempfile.mkdtemp(prefix="psx_metrics_")
+    if "--log-dir" not in args:
+        args = list(args) + ["--log-dir", logdir]
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     env.pop("CUDA_VISIBLE_DEVICES", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
@@ -124,7 +131,11 @@ def _spawn(nproc, args, timeout=240, max_restarts=0):
            "--cpu"] + args
     r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout)
     assert r.returncode == 0, r.stdout[-4000:]
-    return M.parse_lines(r.stdout.splitlines()), r.stdout
+    recs = []
+    for f in sorted(os.listdir(logdir)):
+        with open(os.path.join(logdir, f)) as fh:
+            recs += [json.loads(ln) for ln in fh if ln.strip()]
+    return (recs or M.parse_lines(r.stdout.splitlines())), r.stdout
 
 
 TINY = ["--model", "resnet_tiny", "--batch-size", "8", "--epochs", "1", "--train-samples", "96",

@@ -9,6 +9,7 @@
 // ([T][2][C]); bn_finalize reduces them (fp64, fixed order => deterministic), produces the
 // per-channel affine (scale, shift) and updates the running stats. Every elementwise pass is
 // vectorised at 16 B per lane (8 channels).
+#include "bnfin.hpp"
 #include "common.hpp"
 
 namespace psx {
@@ -119,7 +120,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
                                                             const uint16_t* __restrict__ y2,
                                                             const float* __restrict__ mean2,
                                                             const float* __restrict__ invstd2, float* __restrict__ part,
-                                                            int npix, int C, int pix_per_block) {
+                                                            int npix, int C, int pix_per_block, int fuse_fin,
+                                                            BnBwdFin fin1, BnBwdFin fin2) {
   constexpr int NS = TWO ? 3 : 2;
   extern __shared__ __attribute__((aligned(16))) float sred[];  // [256][NS*8]
   const int cvec = C >> 3;
@@ -181,6 +183,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
     for (int q = 0; q < tpp; ++q) acc += sred[(q * cvec + cgi) * (NS * 8) + sj];
     const int stat = sj >> 3, j = sj & 7;
     atomicAdd(part + ((size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * NS + stat) * C + cgi * 8 + j, acc);
+  }
+  // in-launch finalize (bnfin.hpp): the last block computes the coefficients + dgamma/dbeta
+  if (fuse_fin && last_block_arrive(fin1.counter, gridDim.x, reinterpret_cast<unsigned char*>(sred))) {
+    bn_bwd_finalize_block(part, PSX_STAT_SLOTS, NS, 1, fin1, reinterpret_cast<unsigned char*>(sred));
+    if (TWO) bn_bwd_finalize_block(part, PSX_STAT_SLOTS, NS, 2, fin2, reinterpret_cast<unsigned char*>(sred));
   }
 }
 
@@ -323,8 +330,13 @@ int psx_bn_apply(const void* y, const float* scale, const float* shift, const vo
 // Returns the number of partial rows T (query with part == nullptr).
 int psx_bn_bwd_reduce(const void* g, const void* o, const void* y1, const float* mean1, const float* invstd1,
                       const void* y2, const float* mean2, const float* invstd2, float* part, int npix, int C,
-                      hipStream_t st) {
+                      const BnBwdFin* fin1, const BnBwdFin* fin2, hipStream_t st) {
   if (C % 8 || 256 % (C / 8)) return -2;
+  const int fuse = fin1 != nullptr;
+  BnBwdFin f1{}, f2{};
+  if (fin1) f1 = *fin1;
+  if (fin2) f2 = *fin2;
+  if (fuse && (f1.C != C || (y2 && (!fin2 || f2.C != C)))) return -10;
   // ~512 blocks, at least 64 pixels each
   int ppb = (npix + 511) / 512;
   if (ppb < 64) ppb = 64;
@@ -335,7 +347,7 @@ int psx_bn_bwd_reduce(const void* g, const void* o, const void* y1, const float*
 #define PSX_BBR(M, TW)                                                                                          \
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<M, TW>), dim3(T), dim3(256), lds, st, (const uint16_t*)g,           \
                      (const uint16_t*)o, (const uint16_t*)y1, mean1, invstd1, (const uint16_t*)y2, mean2, invstd2, \
-                     part, npix, C, ppb)
+                     part, npix, C, ppb, fuse, f1, f2)
   if (mask && two) PSX_BBR(true, true);
   else if (mask) PSX_BBR(true, false);
   else if (two) PSX_BBR(false, true);

@@ -13,6 +13,7 @@
 //   * split-K over the GEMM-K dimension (blockIdx.y) for the small-M layers (ResNet stages 3-4),
 //     writing fp32 slabs that conv_splitk_epilogue reduces (+ bf16 store, residual, BN stats).
 // Kernel selection lives in psx_conv_fwd2 / psx_conv_dgrad2 (shape-driven).
+#include "bnfin.hpp"
 #include "pipeline.hpp"
 
 namespace psx {
@@ -28,6 +29,8 @@ struct Conv2Args {
   int Nb, IH, IW, IC, OH, OW, OC, R, S, pad, stride;
   int Kg, log2_icc, npix;
   int n_oc_tiles, n_pix_tiles, splits, kps;  // kps: k-steps per split
+  int fuse_fin;                              // last workgroup finalizes the BN layer (bnfin.hpp)
+  BnFin fin;
 };
 
 PSX_DEV int kmaj2(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
@@ -234,6 +237,8 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       const int which = j / BM, row = j - which * BM;
       atomicAdd(dst + which * a.OC + oc0 + row, red[which * BM + row] + red[(2 + which) * BM + row]);
     }
+    if (a.fuse_fin && last_block_arrive(a.fin.counter, gridDim.x, smem))
+      bn_finalize_block(a.stats, PSX_STAT_SLOTS, a.fin, smem);
   }
 }
 
@@ -243,7 +248,8 @@ template <bool HAS_RES>
 __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restrict__ part, int splits, int npix,
                                                             int OC, uint16_t* __restrict__ out,
                                                             const uint16_t* __restrict__ res,
-                                                            float* __restrict__ stats, int pix_per_block) {
+                                                            float* __restrict__ stats, int pix_per_block,
+                                                            int fuse_fin, BnFin fin) {
   extern __shared__ __attribute__((aligned(16))) float sred[];  // [256][16]
   const int cvec = OC >> 3, tpp = 256 / cvec;
   const int cg = threadIdx.x % cvec, pr = threadIdx.x / cvec;
@@ -298,6 +304,8 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
     const int which = sj >> 3, j = sj & 7;
     atomicAdd(dst + which * OC + cgi * 8 + j, acc);
   }
+  if (fuse_fin && last_block_arrive(fin.counter, gridDim.x, reinterpret_cast<unsigned char*>(sred)))
+    bn_finalize_block(stats, PSX_STAT_SLOTS, fin, reinterpret_cast<unsigned char*>(sred));
 }
 
 }  // namespace psx
@@ -365,10 +373,10 @@ int finish_split(const Conv2Args& a, hipStream_t st) {
   const size_t lds = 256 * 16 * sizeof(float);
   if (a.res)
     hipLaunchKernelGGL(conv_splitk_epilogue<true>, dim3(grid), dim3(256), lds, st, a.part, a.splits, a.npix, a.OC,
-                       a.out, a.res, a.stats, ppb);
+                       a.out, a.res, a.stats, ppb, a.fuse_fin, a.fin);
   else
     hipLaunchKernelGGL(conv_splitk_epilogue<false>, dim3(grid), dim3(256), lds, st, a.part, a.splits, a.npix, a.OC,
-                       a.out, (const uint16_t*)nullptr, a.stats, ppb);
+                       a.out, (const uint16_t*)nullptr, a.stats, ppb, a.fuse_fin, a.fin);
   return (int)hipGetLastError();
 }
 
@@ -385,9 +393,16 @@ long psx_conv2_workspace(int Nb, int OH, int OW, int OC, int Kg) {
 
 // Forward conv (v2). Same operands as psx_conv_fwd plus a 16-byte zero page and a split-K
 // workspace (>= psx_conv2_workspace bytes, may be null when that is 0).
+// fin (nullable, needs stats): the BN layer fed by this conv is finalized by the kernel's last
+// workgroup (bnfin.hpp) instead of a separate psx_bn_finalize launch.
 int psx_conv_fwd2(const void* x, const void* wf, void* y, float* stats, const void* zero, float* ws, int Nb, int H,
-                  int W, int IC, int OC, int R, int S, int stride, int pad, int Kg, hipStream_t st) {
+                  int W, int IC, int OC, int R, int S, int stride, int pad, int Kg, const BnFin* fin, hipStream_t st) {
   Conv2Args a{};
+  if (fin && stats) {
+    if (fin->C != OC) return -10;
+    a.fuse_fin = 1;
+    a.fin = *fin;
+  }
   a.in = (const uint16_t*)x;
   a.w = (const uint16_t*)wf;
   a.out = (uint16_t*)y;

@@ -174,6 +174,9 @@ class HipResNetEngine:
         self.segments = None  # backward split points (set_segments), None = one segment
         # conv kernel generation: 2 = LDS-DMA pipelined + split-K (default), 1 = register-staged
         self.conv_impl = int(os.environ.get("PSX_CONV_IMPL", "2"))
+        # BN finalize inside the producing launch (csrc/kernels/bnfin.hpp); 0 = separate kernels
+        self.fuse_fin = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNFIN", "0") == "1"
+        self._fins = {}
         self._build()
 
     # ------------------------------------------------------------------ allocation
@@ -222,14 +225,21 @@ class HipResNetEngine:
         # fp32 atomics into PSX_STAT_SLOTS slot rows per BN layer; all slot rows live in one
         # buffer that is zeroed once at the start of every step (one memset node in the graph).
         self.nslots = K.bn_bwd_reduce_T(1, 64)
-        red_off = [0]
+        # the first CTR words of the slot buffer are the in-launch finalize counters (two per BN
+        # layer: forward, backward; csrc/kernels/bnfin.hpp) — zeroed with the slots every step
+        nbn = 1 + sum(len(b.bns) + (1 if b.down else 0) for b in sp.blocks)
+        self.ctr_words = -(-2 * nbn // 64) * 64
+        red_off = [self.ctr_words]
+        nctr = [0]
 
         def bn_state(bs: BNSpec):
             fwd = red_off[0]
             bwd = fwd + self.nslots * 2 * bs.c
             red_off[0] = bwd + self.nslots * 3 * bs.c
+            nctr[0] += 2
             self.bn[bs.name] = dict(affine=self._f32(2, bs.c), saved=self._f32(2, bs.c), coef=self._f32(3, bs.c),
-                                    c=bs.c, fwd=(fwd, self.nslots * 2 * bs.c), bwd=(bwd, self.nslots * 3 * bs.c))
+                                    c=bs.c, fwd=(fwd, self.nslots * 2 * bs.c), bwd=(bwd, self.nslots * 3 * bs.c),
+                                    ctr=nctr[0] - 2)
 
         # activation / gradient buffers
         st = sp.stem_conv
@@ -311,18 +321,49 @@ class HipResNetEngine:
         off, n = self.bn[bs.name][which]
         return self.red[off:off + n]
 
-    def _conv_fwd(self, cs: ConvSpec, x, y, bs: BNSpec | None):
+    def _ctr(self, bs: BNSpec, which: int) -> int:
+        return self.red.data_ptr() + 4 * (self.bn[bs.name]["ctr"] + which)
+
+    def _fin_fwd(self, bs: BNSpec, arena, count):
+        key = ("f", bs.name, arena.data_ptr(), count)
+        f = self._fins.get(key)
+        if f is None:
+            st = self.bn[bs.name]
+            f = K.bn_fin(self._aview(arena, f"{bs.name}.weight"), self._aview(arena, f"{bs.name}.bias"),
+                         self._aview(arena, f"{bs.name}.running_mean"), self._aview(arena, f"{bs.name}.running_var"),
+                         st["affine"], st["saved"], self._ctr(bs, 0), count, self.eps, self.mom, bs.c)
+            self._fins[key] = f
+        return f
+
+    def _fin_bwd(self, bs: BNSpec, arena, count):
+        key = ("b", bs.name, arena.data_ptr(), count)
+        f = self._fins.get(key)
+        if f is None:
+            st = self.bn[bs.name]
+            f = K.bn_bwd_fin(self._aview(arena, f"{bs.name}.weight"), st["saved"], st["coef"],
+                             self._gptr(f"{bs.name}.weight"), self._gptr(f"{bs.name}.bias"), self._ctr(bs, 1), count,
+                             1.0, bs.c, self.grad_fp16)
+            self._fins[key] = f
+        return f
+
+    def _conv_bn_fwd(self, cs: ConvSpec, x, y, bs: BNSpec, arena, train: bool):
+        """conv -> (train) batch statistics + BN finalize | (eval) running-statistics affine.
+        With conv v2 the finalize runs inside the conv launch (last workgroup, bnfin.hpp)."""
         oh, ow = cs.out_hw
         npix = self.B * oh * ow
         wf = self.wbuf[cs.wf_off:cs.wf_off + cs.cout * cs.kg]
-        stats = self._red(bs, "fwd") if bs is not None else None
+        stats = self._red(bs, "fwd") if train else None
+        fin = self._fin_fwd(bs, arena, npix) if (train and self.fuse_fin) else None
         if self.conv_impl == 2:
             K.conv_fwd2(x, wf, y, stats, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
-                        cs.kg)
+                        cs.kg, fin=fin)
         else:
             K.conv_fwd(x, wf, y, stats, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg,
                        K.pick_tile(cs.cout, npix))
-        return self.nslots, npix
+        if not train:
+            self._bn_eval(bs, arena)
+        elif fin is None:
+            self._bn_train(bs, arena, self.nslots, npix)
 
     def _bn_train(self, bs: BNSpec, arena, T, count):
         st = self.bn[bs.name]
@@ -358,22 +399,28 @@ class HipResNetEngine:
         """BN (+ReLU mask from o) backward; two = (bs2, y2, dx2) for a shared-dz second BN."""
         st = self.bn[bs.name]
         part = self._red(bs, "bwd")
+        fuse = self.fuse_fin
         if two is None:
-            T = K.bn_bwd_reduce(g, o, y, st["saved"], part, npix, bs.c)
-            K.bn_bwd_finalize(part, T, 2, 1, bs.c, npix, self._aview(arena, f"{bs.name}.weight"),
-                              st["saved"], st["coef"], self._gptr(f"{bs.name}.weight"),
-                              self._gptr(f"{bs.name}.bias"), 1.0, self.grad_fp16)
+            T = K.bn_bwd_reduce(g, o, y, st["saved"], part, npix, bs.c,
+                                fin1=self._fin_bwd(bs, arena, npix) if fuse else None)
+            if not fuse:
+                K.bn_bwd_finalize(part, T, 2, 1, bs.c, npix, self._aview(arena, f"{bs.name}.weight"),
+                                  st["saved"], st["coef"], self._gptr(f"{bs.name}.weight"),
+                                  self._gptr(f"{bs.name}.bias"), 1.0, self.grad_fp16)
             K.bn_bwd_apply(g, o, y, st["coef"], dx, bs.c, dzout=dzout)
         else:
             bs2, y2, dx2 = two
             st2 = self.bn[bs2.name]
-            T = K.bn_bwd_reduce(g, o, y, st["saved"], part, npix, bs.c, y2=y2, saved2=st2["saved"])
-            K.bn_bwd_finalize(part, T, 3, 1, bs.c, npix, self._aview(arena, f"{bs.name}.weight"),
-                              st["saved"], st["coef"], self._gptr(f"{bs.name}.weight"),
-                              self._gptr(f"{bs.name}.bias"), 1.0, self.grad_fp16)
-            K.bn_bwd_finalize(part, T, 3, 2, bs2.c, npix, self._aview(arena, f"{bs2.name}.weight"),
-                              st2["saved"], st2["coef"], self._gptr(f"{bs2.name}.weight"),
-                              self._gptr(f"{bs2.name}.bias"), 1.0, self.grad_fp16)
+            T = K.bn_bwd_reduce(g, o, y, st["saved"], part, npix, bs.c, y2=y2, saved2=st2["saved"],
+                                fin1=self._fin_bwd(bs, arena, npix) if fuse else None,
+                                fin2=self._fin_bwd(bs2, arena, npix) if fuse else None)
+            if not fuse:
+                K.bn_bwd_finalize(part, T, 3, 1, bs.c, npix, self._aview(arena, f"{bs.name}.weight"),
+                                  st["saved"], st["coef"], self._gptr(f"{bs.name}.weight"),
+                                  self._gptr(f"{bs.name}.bias"), 1.0, self.grad_fp16)
+                K.bn_bwd_finalize(part, T, 3, 2, bs2.c, npix, self._aview(arena, f"{bs2.name}.weight"),
+                                  st2["saved"], st2["coef"], self._gptr(f"{bs2.name}.weight"),
+                                  self._gptr(f"{bs2.name}.bias"), 1.0, self.grad_fp16)
             K.bn_bwd_apply(g, o, y, st["coef"], dx, bs.c, y2=y2, coef2=st2["coef"], dx2=dx2, dzout=dzout)
 
     # ------------------------------------------------------------------ public API
@@ -392,11 +439,7 @@ class HipResNetEngine:
         st = sp.stem_conv
         if train:
             self.red.zero_()
-        T, npix = self._conv_fwd(st, self.x0, self.y0, sp.stem_bn if train else None)
-        if train:
-            self._bn_train(sp.stem_bn, arena, T, npix)
-        else:
-            self._bn_eval(sp.stem_bn, arena)
+        self._conv_bn_fwd(st, self.x0, self.y0, sp.stem_bn, arena, train)
         K.bn_apply(self.y0, self.bn[sp.stem_bn.name]["affine"], self.a0, st.cout, relu=True)
         if sp.maxpool:
             K.maxpool3s2_fwd(self.a0, self.p0, self.pidx)
@@ -404,8 +447,7 @@ class HipResNetEngine:
             src = d["inp"]
             L = len(b.convs)
             for i, cs in enumerate(b.convs):
-                T, npix = self._conv_fwd(cs, src, d["y"][i], b.bns[i] if train else None)
-                (self._bn_train(b.bns[i], arena, T, npix) if train else self._bn_eval(b.bns[i], arena))
+                self._conv_bn_fwd(cs, src, d["y"][i], b.bns[i], arena, train)
                 if i < L - 1:
                     K.bn_apply(d["y"][i], self.bn[b.bns[i].name]["affine"], d["a"][i], cs.cout, relu=True)
                     src = d["a"][i]
@@ -413,8 +455,7 @@ class HipResNetEngine:
             aff = self.bn[b.bns[-1].name]["affine"]
             if b.down:
                 ds, dbn = b.down
-                T, npix = self._conv_fwd(ds, d["inp"], d["ys"], dbn if train else None)
-                (self._bn_train(dbn, arena, T, npix) if train else self._bn_eval(dbn, arena))
+                self._conv_bn_fwd(ds, d["inp"], d["ys"], dbn, arena, train)
                 K.bn_apply(d["y"][-1], aff, d["out"], last.cout, relu=True, res=d["ys"],
                            affine2=self.bn[dbn.name]["affine"])
             else:

@@ -75,11 +75,41 @@ def conv2_workspace_bytes(nb, oh, ow, oc, kg) -> int:
     return int(kernels().psx_conv2_workspace(nb, oh, ow, oc, kg))
 
 
-def conv_fwd2(x, wf, y, stats, ws, nb, h, w, ic, oc, k, stride, pad, kg):
+class BnFin(C.Structure):
+    """csrc/kernels/bnfin.hpp BnFin: in-launch forward BN finalize descriptor."""
+    _fields_ = [("gamma", C.c_void_p), ("beta", C.c_void_p), ("run_mean", C.c_void_p), ("run_var", C.c_void_p),
+                ("scale", C.c_void_p), ("shift", C.c_void_p), ("save_mean", C.c_void_p),
+                ("save_invstd", C.c_void_p), ("counter", C.c_void_p), ("count", C.c_float), ("eps", C.c_float),
+                ("momentum", C.c_float), ("C", C.c_int)]
+
+
+class BnBwdFin(C.Structure):
+    """csrc/kernels/bnfin.hpp BnBwdFin: in-launch backward BN finalize descriptor."""
+    _fields_ = [("gamma", C.c_void_p), ("mean", C.c_void_p), ("invstd", C.c_void_p), ("coef", C.c_void_p),
+                ("dgamma", C.c_void_p), ("dbeta", C.c_void_p), ("counter", C.c_void_p), ("count", C.c_float),
+                ("gscale", C.c_float), ("C", C.c_int), ("grad_fp16", C.c_int)]
+
+
+def bn_fin(gamma, beta, run_mean, run_var, affine, saved, counter_ptr, count, eps, momentum, c) -> BnFin:
+    """affine: [2, C] (scale, shift); saved: [2, C] (mean, invstd)."""
+    a, sv = ptr(affine), ptr(saved)
+    return BnFin(ptr(gamma), ptr(beta), ptr(run_mean), ptr(run_var), a, a + 4 * c, sv, sv + 4 * c, counter_ptr,
+                 float(count), float(eps), float(momentum), int(c))
+
+
+def bn_bwd_fin(gamma, saved, coef, dgamma_ptr, dbeta_ptr, counter_ptr, count, gscale, c, grad_fp16) -> BnBwdFin:
+    sv = ptr(saved)
+    return BnBwdFin(ptr(gamma), sv, sv + 4 * c, ptr(coef), dgamma_ptr, dbeta_ptr, counter_ptr, float(count),
+                    float(gscale), int(c), int(grad_fp16))
+
+
+def conv_fwd2(x, wf, y, stats, ws, nb, h, w, ic, oc, k, stride, pad, kg, fin: BnFin | None = None):
     """LDS-DMA pipelined implicit-GEMM conv (csrc/kernels/conv_v2.hip); ws: fp32 split-K
-    workspace of >= conv2_workspace_bytes(...) bytes (or None when that is 0)."""
+    workspace of >= conv2_workspace_bytes(...) bytes (or None when that is 0). With ``fin`` the
+    kernel's last workgroup also finalizes the BN layer its statistics feed (bnfin.hpp)."""
     check(kernels().psx_conv_fwd2(ptr(x), ptr(wf), ptr(y), ptr(stats), ptr(zero_page(x.device)), ptr(ws), nb, h, w,
-                                  ic, oc, k, k, stride, pad, kg, stream_ptr()), "conv_fwd2")
+                                  ic, oc, k, k, stride, pad, kg, C.byref(fin) if fin is not None else None,
+                                  stream_ptr()), "conv_fwd2")
 
 
 def conv_dgrad2(dy, wd, dx, res, ws, nb, h, w, ic_fwd, oc_fwd, k, stride, pad, kgd):
@@ -144,13 +174,19 @@ def bn_apply(y, affine, out, c, relu=True, res=None, affine2=None):
 
 
 def bn_bwd_reduce_T(npix: int, c: int) -> int:
-    return kernels().psx_bn_bwd_reduce(None, None, None, None, None, None, None, None, None, npix, c, None)
+    return kernels().psx_bn_bwd_reduce(None, None, None, None, None, None, None, None, None, npix, c, None, None,
+                                       None)
 
 
-def bn_bwd_reduce(g, o, y1, saved1, part, npix, c, y2=None, saved2=None) -> int:
+def bn_bwd_reduce(g, o, y1, saved1, part, npix, c, y2=None, saved2=None, fin1: BnBwdFin | None = None,
+                  fin2: BnBwdFin | None = None) -> int:
+    """With fin1 (and fin2 for the shared-dz pair) the last block also runs the backward
+    finalize (coefficients + dgamma/dbeta), see csrc/kernels/bnfin.hpp."""
     s2 = ptr(saved2)
     T = kernels().psx_bn_bwd_reduce(ptr(g), ptr(o), ptr(y1), ptr(saved1), ptr(saved1) + 4 * c, ptr(y2), s2,
-                                    (s2 + 4 * c) if s2 else None, ptr(part), npix, c, stream_ptr())
+                                    (s2 + 4 * c) if s2 else None, ptr(part), npix, c,
+                                    C.byref(fin1) if fin1 is not None else None,
+                                    C.byref(fin2) if fin2 is not None else None, stream_ptr())
     if T <= 0:
         raise RuntimeError(f"bn_bwd_reduce failed ({T})")
     return T

@@ -26,6 +26,7 @@ import torch
 
 from ..utils import checkpoint as ckpt
 from ..utils import metrics as M
+from ..utils import trace
 from . import control as CP
 from . import topk
 from .core import APPLY, WAIT, ServerCore
@@ -63,6 +64,7 @@ class ParameterServer:
     # ------------------------------------------------------------------ numerics
     def apply(self, grads: torch.Tensor, weight: float):
         """p <- p - lr * (weight * g [+ wd p]) [momentum]; grads are fp16 wire or fp32."""
+        trace.mark("psx.apply")
         t0 = time.perf_counter()
         if grads.dtype == torch.int32:  # top-k payload (parallel/topk.py)
             if not self.cfg.momentum and not self.cfg.weight_decay:

@@ -94,11 +94,17 @@ class _Span:
         self.t, self.name = t, name
 
     def __enter__(self):
+        from . import trace
+
+        trace.push(self.name)  # roctx range when PSX_ROCTX=1 (utils/trace.py)
         self.t0 = time.perf_counter()
         return self
 
     def __exit__(self, *exc):
+        from . import trace
+
         self.t.add(self.name, time.perf_counter() - self.t0)
+        trace.pop()
         return False
 
 

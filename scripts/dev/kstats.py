@@ -1,0 +1,45 @@
+"""Per-kernel summary from a rocprofv3 kernel trace, restricted to the last N steps
+(steps delimited by a marker kernel), grouped by kernel template.
+
+usage: python scripts/dev/kstats.py run_kernel_trace.csv [--steps 20] [--marker augment]
+"""
+import argparse
+import collections
+import csv
+import re
+
+
+def short(n):
+    n = re.sub(r"\(.*$", "", n) if not n.startswith("void ") else re.sub(r"\((?![^<]*>).*$", "", n[5:])
+    return n[:80]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--marker", default="augment")
+    a = ap.parse_args()
+    rows = []
+    with open(a.csv) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    marks = [s for s, _, n in rows if a.marker in n]
+    lo, hi = marks[-a.steps - 1], marks[-1]
+    sel = [r for r in rows if lo <= r[0] < hi]
+    tot = collections.defaultdict(lambda: [0, 0])
+    for s, e, n in sel:
+        k = short(n)
+        tot[k][0] += 1
+        tot[k][1] += e - s
+    busy = sum(v[1] for v in tot.values())
+    wall = hi - lo
+    print(f"{a.steps} steps: wall {wall / a.steps / 1e3:.1f} us/step, kernel time {busy / a.steps / 1e3:.1f} us/step")
+    print(f"{'kernel':80s} {'calls/step':>10s} {'us/step':>9s} {'%':>6s}")
+    for k, (c, t) in sorted(tot.items(), key=lambda kv: -kv[1][1]):
+        print(f"{k:80s} {c / a.steps:10.1f} {t / a.steps / 1e3:9.1f} {100 * t / busy:6.1f}")
+
+
+if __name__ == "__main__":
+    main()

@@ -106,6 +106,49 @@ def test_graph_replay_matches_eager(setup):
     assert _cos(eng.grads[fc:].float(), eager[fc:].float()) > 0.9999
 
 
+def test_fused_bn_finalize_matches_separate_kernels(setup):
+    """In-launch BN finalize (bnfin.hpp, last-workgroup hand-off) gives exactly what the
+    separate finalize kernels compute from the same slot sums (checked on every BN layer, for
+    two consecutive steps so the per-step counter re-arm is exercised too)."""
+    model, layout, arena, eng, x, y = setup
+    n = 256
+    imgs = torch.randint(0, 256, (n, 32, 32, 3), dtype=torch.uint8, device=DEV)
+    labs = torch.randint(0, 100, (n,), dtype=torch.int32, device=DEV)
+    eng.index.copy_(torch.arange(eng.B, dtype=torch.int32, device=DEV))
+    fused_before = eng.fuse_fin
+    eng.fuse_fin = True
+    a = arena.clone()
+    for step in range(2):
+        eng.train_step(a, imgs, labs)
+        torch.cuda.synchronize()
+        bns = [eng.spec.stem_bn] + [bn for b in eng.spec.blocks for bn in b.bns + ([b.down[1]] if b.down else [])]
+        for bs in bns:
+            st = eng.bn[bs.name]
+            c = bs.c
+            fin = [f for k, f in eng._fins.items() if k[0] == "f" and k[1] == bs.name][0]
+            aff, sav = torch.empty_like(st["affine"]), torch.empty_like(st["saved"])
+            K.bn_finalize(eng._red(bs, "fwd"), K.STAT_SLOTS, c, fin.count, layout.view(a, f"{bs.name}.weight"),
+                          layout.view(a, f"{bs.name}.bias"), eng.eps, eng.mom, None, None, aff, sav)
+            bf = [f for k, f in eng._fins.items() if k[0] == "b" and k[1] == bs.name][0]
+            coef = torch.empty_like(st["coef"])
+            dg = torch.empty(c, dtype=torch.float32, device=DEV)
+            db = torch.empty(c, dtype=torch.float32, device=DEV)
+            # a BN pair sharing dz (block output BN + shortcut BN) keeps 3 stat rows per slot in
+            # the first BN's slot region
+            two = [b for b in eng.spec.blocks if b.down and bs.name in (b.bns[-1].name, b.down[1].name)]
+            ns, which = (3, 1 if bs.name == two[0].bns[-1].name else 2) if two else (2, 1)
+            part = eng._red(two[0].bns[-1] if two else bs, "bwd")
+            K.bn_bwd_finalize(part, K.STAT_SLOTS, ns, which, c, bf.count, layout.view(a, f"{bs.name}.weight"),
+                              st["saved"], coef, dg.data_ptr(), db.data_ptr(), 1.0, False)
+            torch.cuda.synchronize()
+            assert torch.allclose(aff, st["affine"], rtol=1e-6, atol=1e-7), (step, bs.name)
+            assert torch.allclose(sav, st["saved"], rtol=1e-6, atol=1e-7), (step, bs.name)
+            assert torch.allclose(coef, st["coef"], rtol=1e-5, atol=1e-6), (step, bs.name)
+            gw = layout.grad_view(eng.grads, f"{bs.name}.weight").float()
+            assert torch.allclose(dg, gw, rtol=1e-5, atol=1e-6), (step, bs.name)
+    eng.fuse_fin = fused_before
+
+
 def test_segmented_graphs_match_single_graph(setup):
     """Backward split into per-bucket graphs (overlapped sync rounds) computes the same step."""
     from psx.parallel.overlap import plan_buckets

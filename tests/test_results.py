@@ -63,3 +63,19 @@ def test_parse_logs_cli(tmp_path):
     r = subprocess.run([sys.executable, f"{ROOT}/scripts/visualize_results.py", "--results", str(out),
                         "--output-dir", str(tmp_path / "p")], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_roctx_ranges_are_safe_without_profiler(monkeypatch):
+    from psx.utils import metrics as M
+    from psx.utils import trace
+
+    monkeypatch.setenv("PSX_ROCTX", "1")
+    t = M.PhaseTimer()
+    with t.span("fetch"):
+        with trace.range("inner"):
+            trace.mark("m")
+    assert t.count["fetch"] == 1
+    monkeypatch.setenv("PSX_ROCTX", "0")
+    with t.span("fetch"):
+        pass
+    assert t.count["fetch"] == 2

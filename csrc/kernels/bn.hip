@@ -186,8 +186,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   }
   // in-launch finalize (bnfin.hpp): the last block computes the coefficients + dgamma/dbeta
   if (fuse_fin && last_block_arrive(fin1.counter, gridDim.x, reinterpret_cast<unsigned char*>(sred))) {
-    bn_bwd_finalize_block(part, PSX_STAT_SLOTS, NS, 1, fin1, reinterpret_cast<unsigned char*>(sred));
-    if (TWO) bn_bwd_finalize_block(part, PSX_STAT_SLOTS, NS, 2, fin2, reinterpret_cast<unsigned char*>(sred));
+    bn_bwd_finalize_block<PSX_STAT_SLOTS>(part, NS, 1, fin1);
+    if (TWO) bn_bwd_finalize_block<PSX_STAT_SLOTS>(part, NS, 2, fin2);
   }
 }
 

@@ -65,86 +65,71 @@ PSX_DEV bool last_block_arrive(unsigned* counter, unsigned nblocks, unsigned cha
 }
 
 // part: [T][2][C] slot rows (sum, sum of squares). Same math as bn_finalize_kernel (bn.hip).
-// Needs 4 KB of LDS scratch; blockDim = 256.
-PSX_DEV void bn_finalize_block(const float* part, int T, const BnFin& f, unsigned char* lds) {
-  double* red = reinterpret_cast<double*>(lds);  // [2][8][32]
-  const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
-  for (int cb = 0; cb < f.C; cb += 32) {
-    const int c = cb + cl;
-    float fs = 0.f, fss = 0.f;
-    if (c < f.C)
-      for (int t = grp; t < T; t += 8) {
-        fs += part[((size_t)t * 2 + 0) * f.C + c];
-        fss += part[((size_t)t * 2 + 1) * f.C + c];
-      }
-    red[(0 * 8 + grp) * 32 + cl] = fs;
-    red[(1 * 8 + grp) * 32 + cl] = fss;
-    __syncthreads();
-    if (grp == 0 && c < f.C) {
-      double s = 0.0, ss = 0.0;
+// One thread per channel, all T slot loads issued back to back: the slot sums sit at the
+// memory side (float atomics bypass L2), so a per-channel-group LDS reduction would pay one
+// memory round trip per 32 channels; this pays about one in total. blockDim = 256.
+template <int T>
+PSX_DEV void bn_finalize_block(const float* part, const BnFin& f) {
+  for (int c = threadIdx.x; c < f.C; c += 256) {
+    float v1[T], v2[T];
 #pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        s += red[(0 * 8 + g) * 32 + cl];
-        ss += red[(1 * 8 + g) * 32 + cl];
-      }
-      const double mean = s / f.count;
-      double var = ss / f.count - mean * mean;
-      if (var < 0.0) var = 0.0;
-      const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
-      const float sc = f.gamma[c] * invstd;
-      f.scale[c] = sc;
-      f.shift[c] = f.beta[c] - (float)mean * sc;
-      f.save_mean[c] = (float)mean;
-      f.save_invstd[c] = invstd;
-      if (f.run_mean) {
-        const double unb = f.count > 1.f ? var * f.count / (f.count - 1.0) : var;
-        f.run_mean[c] = (1.f - f.momentum) * f.run_mean[c] + f.momentum * (float)mean;
-        f.run_var[c] = (1.f - f.momentum) * f.run_var[c] + f.momentum * (float)unb;
-      }
+    for (int t = 0; t < T; ++t) {
+      v1[t] = part[((size_t)t * 2 + 0) * f.C + c];
+      v2[t] = part[((size_t)t * 2 + 1) * f.C + c];
     }
-    __syncthreads();
+    double s = 0.0, ss = 0.0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      s += v1[t];
+      ss += v2[t];
+    }
+    const double mean = s / f.count;
+    double var = ss / f.count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+    const float sc = f.gamma[c] * invstd;
+    f.scale[c] = sc;
+    f.shift[c] = f.beta[c] - (float)mean * sc;
+    f.save_mean[c] = (float)mean;
+    f.save_invstd[c] = invstd;
+    if (f.run_mean) {
+      const double unb = f.count > 1.f ? var * f.count / (f.count - 1.0) : var;
+      f.run_mean[c] = (1.f - f.momentum) * f.run_mean[c] + f.momentum * (float)mean;
+      f.run_var[c] = (1.f - f.momentum) * f.run_var[c] + f.momentum * (float)unb;
+    }
   }
 }
 
 // part: [T][NS][C] (row 0 = sum dz, row `which` = sum dz*xhat). Same math as
-// bn_bwd_finalize_kernel (bn.hip).
-PSX_DEV void bn_bwd_finalize_block(const float* part, int T, int NS, int which, const BnBwdFin& f,
-                                   unsigned char* lds) {
-  float* red = reinterpret_cast<float*>(lds);  // [2][8][32]
-  const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
-  for (int cb = 0; cb < f.C; cb += 32) {
-    const int c = cb + cl;
-    float a = 0.f, b = 0.f;
-    if (c < f.C)
-      for (int t = grp; t < T; t += 8) {
-        a += part[((size_t)t * NS + 0) * f.C + c];
-        b += part[((size_t)t * NS + which) * f.C + c];
-      }
-    red[(0 * 8 + grp) * 32 + cl] = a;
-    red[(1 * 8 + grp) * 32 + cl] = b;
-    __syncthreads();
-    if (grp == 0 && c < f.C) {
-      double sdz = 0.0, sxh = 0.0;
+// bn_bwd_finalize_kernel (bn.hip); layout of the work as bn_finalize_block.
+template <int T>
+PSX_DEV void bn_bwd_finalize_block(const float* part, int NS, int which, const BnBwdFin& f) {
+  for (int c = threadIdx.x; c < f.C; c += 256) {
+    float va[T], vb[T];
 #pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        sdz += red[(0 * 8 + g) * 32 + cl];
-        sxh += red[(1 * 8 + g) * 32 + cl];
-      }
-      const float mdz = (float)(sdz / f.count), mxh = (float)(sxh / f.count);
-      const float is = f.invstd[c], gm = f.gamma[c];
-      f.coef[c] = gm * is;
-      f.coef[f.C + c] = -gm * is * is * mxh;
-      f.coef[2 * f.C + c] = -gm * is * mdz + gm * is * is * f.mean[c] * mxh;
-      const float dg = (float)sxh * f.gscale, db = (float)sdz * f.gscale;
-      if (f.grad_fp16) {
-        reinterpret_cast<uint16_t*>(f.dgamma)[c] = __builtin_bit_cast(uint16_t, (_Float16)dg);
-        reinterpret_cast<uint16_t*>(f.dbeta)[c] = __builtin_bit_cast(uint16_t, (_Float16)db);
-      } else {
-        reinterpret_cast<float*>(f.dgamma)[c] = dg;
-        reinterpret_cast<float*>(f.dbeta)[c] = db;
-      }
+    for (int t = 0; t < T; ++t) {
+      va[t] = part[((size_t)t * NS + 0) * f.C + c];
+      vb[t] = part[((size_t)t * NS + which) * f.C + c];
     }
-    __syncthreads();
+    double sdz = 0.0, sxh = 0.0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      sdz += va[t];
+      sxh += vb[t];
+    }
+    const float mdz = (float)(sdz / f.count), mxh = (float)(sxh / f.count);
+    const float is = f.invstd[c], gm = f.gamma[c];
+    f.coef[c] = gm * is;
+    f.coef[f.C + c] = -gm * is * is * mxh;
+    f.coef[2 * f.C + c] = -gm * is * mdz + gm * is * is * f.mean[c] * mxh;
+    const float dg = (float)sxh * f.gscale, db = (float)sdz * f.gscale;
+    if (f.grad_fp16) {
+      reinterpret_cast<uint16_t*>(f.dgamma)[c] = __builtin_bit_cast(uint16_t, (_Float16)dg);
+      reinterpret_cast<uint16_t*>(f.dbeta)[c] = __builtin_bit_cast(uint16_t, (_Float16)db);
+    } else {
+      reinterpret_cast<float*>(f.dgamma)[c] = dg;
+      reinterpret_cast<float*>(f.dbeta)[c] = db;
+    }
   }
 }
 

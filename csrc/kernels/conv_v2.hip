@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       atomicAdd(dst + which * a.OC + oc0 + row, red[which * BM + row] + red[(2 + which) * BM + row]);
     }
     if (a.fuse_fin && last_block_arrive(a.fin.counter, gridDim.x, smem))
-      bn_finalize_block(a.stats, PSX_STAT_SLOTS, a.fin, smem);
+      bn_finalize_block<PSX_STAT_SLOTS>(a.stats, a.fin);
   }
 }
 
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
     atomicAdd(dst + which * OC + cgi * 8 + j, acc);
   }
   if (fuse_fin && last_block_arrive(fin.counter, gridDim.x, reinterpret_cast<unsigned char*>(sred)))
-    bn_finalize_block(stats, PSX_STAT_SLOTS, fin, reinterpret_cast<unsigned char*>(sred));
+    bn_finalize_block<PSX_STAT_SLOTS>(stats, fin);
 }
 
 }  // namespace psx

@@ -11,6 +11,8 @@
 //     the main loop), 3 LDS stages with counted vmcnt waits and one barrier per 64 pixels.
 // Partial sums go to fp32 slabs [split][OC][Kg] reduced by wgrad_reduce (conv_gemm.hip),
 // which also permutes to OIHW and emits the fp16 wire codec.
+#include <stdlib.h>
+
 #include "pipeline.hpp"
 
 namespace psx {
@@ -37,7 +39,7 @@ PSX_DEV s16x4 tr_read2(const unsigned char* base, int off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off));
 }
 
-template <int BR, int BC>
+template <int BR, int BC, int NS>
 __global__ __launch_bounds__(256) void wgrad2_kernel(Wgrad2Args a) {
   constexpr int XROWB = BR * 2, DROWB = BC * 2;           // bytes per pixel row
   constexpr int XCPR = XROWB / 16, DCPR = DROWB / 16;     // 16-byte chunks per row
@@ -118,18 +120,23 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(Wgrad2Args a) {
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if (nsteps > 0) issue(0, 0);
-  if (nsteps > 1) issue(1, 1);
+  // NS-stage ring: steps st+1 .. st+NS-2 may still be in flight while step st is consumed
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < nsteps) issue(i, i);
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
   int stage = 0;
   for (int st = 0; st < nsteps; ++st) {
-    if (st + 1 < nsteps)
+    const int ahead = min(NS - 2, nsteps - 1 - st);  // groups issued after step st's
+    if (ahead >= NS - 2)
+      wait_vmcnt<(NS - 2) * (LX + LD)>();
+    else if (NS > 3 && ahead == 1)
       wait_vmcnt<LX + LD>();
     else
       wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (st + 2 < nsteps) issue(st + 2, stage == 0 ? 2 : stage - 1);
+    if (st + NS - 1 < nsteps) issue(st + NS - 1, stage == 0 ? NS - 1 : stage - 1);
     const unsigned char* X = smem + stage * STAGE;
     const unsigned char* D = X + XT;
 #pragma unroll
@@ -156,7 +163,7 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(Wgrad2Args a) {
         for (int n = 0; n < NT; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
     }
-    stage = stage == 2 ? 0 : stage + 1;
+    stage = stage == NS - 1 ? 0 : stage + 1;
   }
 
   float* part = a.part + (size_t)split * a.OC * a.Kg;
@@ -177,29 +184,54 @@ using namespace psx;
 namespace {
 
 struct WPlan {
-  int BR, BC, splits, sps;
+  int BR, BC, NS, splits, sps;
 };
 
+// LDS bytes per workgroup of an NS-stage BR x BC tile (64 pixels per stage).
+constexpr int wlds(int BR, int BC, int NS) { return NS * 64 * (BR + BC) * 2; }
+
+// Occupancy-aware plan: tiles x splits workgroups should fill whole rounds of the
+// 256 CUs x (workgroups per CU that the LDS allows), with >= 8 pixel-steps per split; among
+// the tile shapes the one with the lowest modelled time wins (per-step costs measured on
+// MI355X with rocprofv3: 128x128 ~1.2 us at 1 WG/CU, 64x64 ~0.7 us at 3 WG/CU; +3 us
+// prologue/epilogue per workgroup; split-K partials cost a write + a read at ~5 TB/s).
 WPlan wplan(int OC, int Kg, int npix) {
-  WPlan p{64, 64, 1, 0};
-  if (Kg % 128 == 0 && Kg >= 256) p.BR = 128;
-  if (OC % 128 == 0) p.BC = 128;
-  const int tiles = (Kg / p.BR) * (OC / p.BC);
+  WPlan best{64, 64, 3, 1, 0};
+  double best_t = 1e30;
   const int steps = (npix + 63) / 64;
-  // ~2 workgroups per CU, >= 16 pixel-steps per split
-  int s = (512 + tiles - 1) / tiles;
-  const int smax = steps / 16 > 0 ? steps / 16 : 1;
-  if (s > smax) s = smax;
-  if (s < 1) s = 1;
-  p.sps = (steps + s - 1) / s;
-  p.splits = (steps + p.sps - 1) / p.sps;
-  return p;
+  const int brs[2] = {128, 64}, bcs[2] = {128, 64};
+  for (int ib = 0; ib < 2; ++ib)
+    for (int ic = 0; ic < 2; ++ic) {
+      const int BR = brs[ib], BC = bcs[ic];
+      if (Kg % BR || OC % BC || (BR == 128 && Kg < 256)) continue;
+      const int NS = (BR == 128 && BC == 128) ? 4 : 3;
+      int occ = 163840 / wlds(BR, BC, NS);
+      if (occ > 3) occ = 3;
+      if (occ < 1) continue;
+      const int slots = 256 * occ;
+      const long tiles = (long)(Kg / BR) * (OC / BC);
+      const double step_us = 0.55 + 0.15 * (double)(BR * BC) / 4096.0;
+      int smax = steps / 8 > 0 ? steps / 8 : 1;
+      for (int sp = 1; sp <= smax && sp <= 64; ++sp) {
+        const int sps = (steps + sp - 1) / sp;
+        const int spl = (steps + sps - 1) / sps;
+        const long wgs = tiles * spl;
+        const long rounds = (wgs + slots - 1) / slots;
+        const double t = rounds * (sps * step_us + 3.0) + (spl > 1 ? spl * (double)OC * Kg * 8.0 / 5e6 : 0.0);
+        if (t < best_t) {
+          best_t = t;
+          best = WPlan{BR, BC, NS, spl, sps};
+        }
+      }
+    }
+  return best;
 }
 
-template <int BR, int BC>
+template <int BR, int BC, int NS>
 int launch_w2(const Wgrad2Args& a, hipStream_t st) {
-  const size_t lds = (size_t)3 * 64 * (BR + BC) * 2;
-  hipLaunchKernelGGL((wgrad2_kernel<BR, BC>), dim3(a.n_k_tiles * a.n_oc_tiles * a.splits), dim3(256), lds, st, a);
+  const size_t lds = (size_t)wlds(BR, BC, NS);
+  hipLaunchKernelGGL((wgrad2_kernel<BR, BC, NS>), dim3(a.n_k_tiles * a.n_oc_tiles * a.splits), dim3(256), lds, st,
+                     a);
   return (int)hipGetLastError();
 }
 
@@ -230,17 +262,26 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
   a.div_ow = make_fastdiv(OW);
   a.div_s = make_fastdiv(S);
   if (OC % 64 || Kg % 64) return -2;
-  const WPlan p = wplan(OC, Kg, a.npix);
+  WPlan p = wplan(OC, Kg, a.npix);
+  // experiment overrides (tile sweep): PSX_WG_BR / PSX_WG_BC / PSX_WG_SPLITS
+  if (const char* e = getenv("PSX_WG_BR")) p.BR = atoi(e);
+  if (const char* e = getenv("PSX_WG_BC")) p.BC = atoi(e);
+  if (const char* e = getenv("PSX_WG_SPLITS")) {
+    const int steps = (a.npix + 63) / 64;
+    p.sps = (steps + atoi(e) - 1) / atoi(e);
+    p.splits = (steps + p.sps - 1) / p.sps;
+  }
+  if (Kg % p.BR || OC % p.BC) return -2;
   a.n_k_tiles = Kg / p.BR;
   a.n_oc_tiles = OC / p.BC;
   a.splits = p.splits;
   a.steps_per_split = p.sps;
   if (!part) return p.splits;
   int e;
-  if (p.BR == 128 && p.BC == 128) e = launch_w2<128, 128>(a, st);
-  else if (p.BR == 128) e = launch_w2<128, 64>(a, st);
-  else if (p.BC == 128) e = launch_w2<64, 128>(a, st);
-  else e = launch_w2<64, 64>(a, st);
+  if (p.BR == 128 && p.BC == 128) e = launch_w2<128, 128, 4>(a, st);
+  else if (p.BR == 128) e = launch_w2<128, 64, 3>(a, st);
+  else if (p.BC == 128) e = launch_w2<64, 128, 3>(a, st);
+  else e = launch_w2<64, 64, 3>(a, st);
   return e ? -e : p.splits;
 }
 

@@ -13,6 +13,8 @@
 //   * split-K over the GEMM-K dimension (blockIdx.y) for the small-M layers (ResNet stages 3-4),
 //     writing fp32 slabs that conv_splitk_epilogue reduces (+ bf16 store, residual, BN stats).
 // Kernel selection lives in psx_conv_fwd2 / psx_conv_dgrad2 (shape-driven).
+#include <stdlib.h>
+
 #include "bnfin.hpp"
 #include "pipeline.hpp"
 
@@ -340,6 +342,12 @@ Plan plan_for(int OC, int npix, int ksteps) {
   }
   const long tiles = (long)(OC / p.BM) * ((npix + p.BN - 1) / p.BN);
   while (p.splits < 8 && tiles * p.splits < 512 && ksteps / (p.splits * 2) >= 8) p.splits *= 2;
+  // experiment overrides (tile sweep, bench/conv_sweep.py): PSX_CV_BM / PSX_CV_BN / PSX_CV_SPLITS
+  if (const char* e = getenv("PSX_CV_BM")) p.BM = atoi(e);
+  if (const char* e = getenv("PSX_CV_BN")) p.BN = atoi(e);
+  if (const char* e = getenv("PSX_CV_SPLITS")) p.splits = atoi(e);
+  if (OC % p.BM) p.BM = 64;
+  if (p.splits > ksteps) p.splits = ksteps;
   return p;
 }
 

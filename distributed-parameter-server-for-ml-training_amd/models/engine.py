@@ -21,6 +21,7 @@ The network is described by a generic block list so ResNet-18 (CIFAR stem) and R
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from dataclasses import dataclass, field
 
@@ -176,6 +177,9 @@ class HipResNetEngine:
         self.conv_impl = int(os.environ.get("PSX_CONV_IMPL", "2"))
         # BN finalize inside the producing launch (csrc/kernels/bnfin.hpp); 0 = separate kernels
         self.fuse_fin = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNFIN", "0") == "1"
+        self.wg_stream = (torch.cuda.Stream(device=self.dev)
+                          if os.environ.get("PSX_WGRAD_STREAM", "0") == "1" else None)
+        self._wg_batch = None
         self._fins = {}
         self._build()
 
@@ -250,18 +254,20 @@ class HipResNetEngine:
         self.dy0 = self._bf(B, p, q, st.cout)
         bn_state(sp.stem_bn)
         max_wg = 0
+        max_wp = 0
 
         def track(cs: ConvSpec):
-            # one fp32 scratch serves the wgrad split-K partials and the conv v2 split-K slabs
-            # (all uses are stream-ordered)
-            nonlocal max_wg
+            # fp32 scratch: wgrad split-K partials (own buffer: wgrad may run on a side stream)
+            # and conv v2 split-K slabs (stream-ordered on the main stream)
+            nonlocal max_wg, max_wp
             if self.conv_impl == 2:
                 s = K.conv_wgrad2_splits(B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
             else:
                 s = K.conv_wgrad_splits(B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
             cs.splits = s
             oh, ow = cs.out_hw
-            max_wg = max(max_wg, s * cs.cout * cs.kg, K.conv2_workspace_bytes(B, oh, ow, cs.cout, cs.kg) // 4,
+            max_wp = max(max_wp, s * cs.cout * cs.kg)
+            max_wg = max(max_wg, K.conv2_workspace_bytes(B, oh, ow, cs.cout, cs.kg) // 4,
                          K.conv2_workspace_bytes(B, cs.h, cs.w, cs.cp, cs.kgd) // 4 if cs.need_dgrad else 0)
 
         track(st)
@@ -298,7 +304,8 @@ class HipResNetEngine:
             h_in = d["out"]
         self.final = h_in
         self.red = self._f32(red_off[0])
-        self.wpart = self._f32(max_wg)
+        self.wpart = self._f32(max(1, max_wg))
+        self.wpart_w = self._f32(max(1, max_wp))
         # head
         fh, fw = self.final.shape[1], self.final.shape[2]
         self.head_hw = fh * fw
@@ -378,14 +385,45 @@ class HipResNetEngine:
                          self._aview(arena, f"{bs.name}.running_mean"), self._aview(arena, f"{bs.name}.running_var"),
                          self.eps, st["affine"])
 
+    def _side(self):
+        """Weight gradients only feed the push, so they run on a side stream concurrently with
+        the dgrad -> BN-backward critical path (ordered after their dy by an event; joined at
+        the end of every backward segment)."""
+        if self.wg_stream is None:
+            return contextlib.nullcontext()
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        self.wg_stream.wait_event(ev)
+        return torch.cuda.stream(self.wg_stream)
+
+    def join_side(self):
+        if self.wg_stream is not None:
+            torch.cuda.current_stream(self.dev).wait_stream(self.wg_stream)
+
     def _wgrad(self, cs: ConvSpec, x, dy):
-        if self.conv_impl == 2:
-            K.conv_wgrad2(x, dy, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
-        else:
-            K.conv_wgrad(x, dy, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg,
-                         cs.splits)
-        K.wgrad_reduce(self.wpart, cs.splits, cs.cout, cs.kg, cs.cin, cs.cp, cs.k, 1.0, self._gptr(f"{cs.name}.weight"),
-                       self.grad_fp16)
+        if self._wg_batch is not None:  # deferred: issued together at the end of the unit
+            self._wg_batch.append((cs, x, dy))
+            return
+        with self._side():
+            self._wgrad_now(cs, x, dy)
+
+    def _flush_wgrads(self):
+        batch, self._wg_batch = self._wg_batch, None
+        if batch:
+            with self._side():
+                for cs, x, dy in batch:
+                    self._wgrad_now(cs, x, dy)
+
+    def _wgrad_now(self, cs: ConvSpec, x, dy):
+        if True:
+            if self.conv_impl == 2:
+                K.conv_wgrad2(x, dy, self.wpart_w, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
+                              cs.kg)
+            else:
+                K.conv_wgrad(x, dy, self.wpart_w, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
+                             cs.kg, cs.splits)
+            K.wgrad_reduce(self.wpart_w, cs.splits, cs.cout, cs.kg, cs.cin, cs.cp, cs.k, 1.0,
+                           self._gptr(f"{cs.name}.weight"), self.grad_fp16)
 
     def _dgrad(self, cs: ConvSpec, dy, dx, res=None):
         wd = self.wbuf[cs.wd_off:cs.wd_off + cs.cp * cs.kgd]
@@ -471,11 +509,20 @@ class HipResNetEngine:
 
     def _bwd_fc(self, arena):
         sp = self.spec
-        K.head_wgrad(self.dlogits, self.pooled, self.B, sp.classes, sp.fc_in, self._gptr(f"{sp.fc}.weight"),
-                     self._gptr(f"{sp.fc}.bias"), 1.0, self.grad_fp16)
+        with self._side():
+            K.head_wgrad(self.dlogits, self.pooled, self.B, sp.classes, sp.fc_in, self._gptr(f"{sp.fc}.weight"),
+                         self._gptr(f"{sp.fc}.bias"), 1.0, self.grad_fp16)
 
     def _bwd_block(self, arena, j: int):
-        """Backward of residual block j; its incoming gradient is the next block's input grad."""
+        """Backward of residual block j; its incoming gradient is the next block's input grad.
+        With the side stream its weight gradients are issued as one batch after the block."""
+        self._wg_batch = [] if self.wg_stream is not None else None
+        try:
+            self._bwd_block_body(arena, j)
+        finally:
+            self._flush_wgrads()
+
+    def _bwd_block_body(self, arena, j: int):
         sp, B = self.spec, self.B
         b, d = sp.blocks[j], self.blk[j]
         g = self.blk[j + 1]["gin"] if j + 1 < len(self.blk) else self.dfinal
@@ -530,6 +577,7 @@ class HipResNetEngine:
     def backward(self, arena: torch.Tensor):
         for _, fn in self.backward_units(arena):
             fn()
+        self.join_side()
 
     def set_segments(self, groups):
         """Split the backward into segments (lists of unit keys, in backward order) so that a
@@ -561,6 +609,7 @@ class HipResNetEngine:
                     prologue()
                 for k in grp:
                     units[k]()
+                self.join_side()  # a segment's gradients are complete when it ends
             fns.append(seg)
         return fns
 

@@ -79,7 +79,20 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   const int oc0 = oc_t * BM, pix0 = pix_t * BN;
   const int split = SPLIT ? blockIdx.y : 0;
   const int ks0 = split * a.kps;
-  const int nk = SPLIT ? min(a.kps, a.Kg / 64 - ks0) : a.Kg / 64;
+  int nk = SPLIT ? min(a.kps, a.Kg / 64 - ks0) : a.Kg / 64;
+  // MODE 3 = stride-2 dgrad, one parity class (py, px) of dx per blockIdx.y: dx(2i+py, 2j+px)
+  // only receives taps r = r0, r0+2, .. and s = s0, s0+2, .. (r0 = (py+pad)&1), i.e. a dense
+  // GEMM over 1, 2, 2 or 4 of the 9 taps instead of 9 with 3/4 of the products zero.
+  const int cls = MODE == 3 ? blockIdx.y : 0;
+  const int py = cls >> 1, px = cls & 1;
+  const int CH = (a.OH - py + 1) >> 1, CW = (a.OW - px + 1) >> 1;
+  const int r0 = (py + a.pad) & 1, s0 = (px + a.pad) & 1;
+  const int nr = r0 < a.R ? (a.R - r0 + 1) >> 1 : 0, nsx = s0 < a.S ? (a.S - s0 + 1) >> 1 : 0;
+  const int npix_c = MODE == 3 ? a.Nb * CH * CW : a.npix;
+  if (MODE == 3) {
+    nk = (nr * nsx) << (a.log2_icc - 3);
+    if (pix0 >= npix_c) return;  // whole workgroup: this class has fewer tiles
+  }
 
   // ---- per-lane DMA source state (fixed across k-steps) ----
   const int lrow = lane >> 3, lpos = lane & 7;
@@ -97,13 +110,17 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     const int row = (i * 4 + wid) * 8 + lrow;
     bc[i] = lpos ^ ((row >> 1) & 7);
     const int pix = pix0 + row;
-    pv[i] = pix < a.npix;
+    pv[i] = pix < npix_c;
     const int pp = pv[i] ? pix : 0;
-    const int ohw = a.OH * a.OW;
+    const int pw = MODE == 3 ? CW : a.OW;
+    const int ohw = (MODE == 3 ? CH : a.OH) * pw;
     const int n = pp / ohw, rem = pp - n * ohw;
-    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+    const int oh = rem / pw, ow = rem - oh * pw;
     nbase[i] = n * a.IH * a.IW;
-    if (MODE == 0) {
+    if (MODE == 3) {  // class-local (i, j)
+      hb[i] = oh;
+      wb[i] = ow;
+    } else if (MODE == 0) {
       hb[i] = oh * a.stride - a.pad;
       wb[i] = ow * a.stride - a.pad;
     } else {
@@ -125,6 +142,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   for (int i = 0; i < LB; ++i) {
     // MODE 0: pixel (hb, wb) = top-left tap; MODE 1: (hb, wb) = (oh, ow) + pad, taps subtract
     const long off = MODE == 2 ? 0 : ((long)nbase[i] + (long)hb[i] * a.IW + wb[i]) * a.IC + bc[i] * 8;
+    // MODE 3: pbase = dy(n, i, j); a class tap adds the uniform offset (dr, ds) = ((py+pad-r)/2, ..)
     pbase[i] = a.in + off;
   }
   const int ksh = a.log2_icc - 3;  // k-steps per tap = 1 << ksh (utap only)
@@ -132,6 +150,25 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   auto issue = [&](int ks, int stage) {
     unsigned char* base = smem + stage * STAGE;
     const int kglob = ks0 + ks;
+    if (MODE == 3) {
+      const int t = __builtin_amdgcn_readfirstlane(ks >> ksh);
+      const int cofs = __builtin_amdgcn_readfirstlane((ks & ((1 << ksh) - 1)) << 6);
+      const int tr = __builtin_amdgcn_readfirstlane(t / nsx);
+      const int r = r0 + 2 * tr, sx = s0 + 2 * (t - tr * nsx);
+      const int kg = ((r * a.S + sx) << ksh) + (ks & ((1 << ksh) - 1));  // k-step in the full weights
+#pragma unroll
+      for (int i = 0; i < LA; ++i) glds16(wsrc[i] + kg * 64, base + (i * 4 + wid) * 1024);
+      const int dr = (py + a.pad - r) >> 1, ds = (px + a.pad - sx) >> 1;
+      const long uoff = ((long)dr * a.IW + ds) * a.IC + cofs;
+#pragma unroll
+      for (int i = 0; i < LB; ++i) {
+        const uint16_t* src = a.zero;
+        if (pv[i] && (unsigned)(hb[i] + dr) < (unsigned)a.IH && (unsigned)(wb[i] + ds) < (unsigned)a.IW)
+          src = pbase[i] + uoff;
+        glds16(src, base + BM * 128 + (i * 4 + wid) * 1024);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < LA; ++i) glds16(wsrc[i] + kglob * 64, base + (i * 4 + wid) * 1024);
     if (utap) {
@@ -229,13 +266,18 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
     const int pix = pix0 + wn * (BN / 2) + n * 16 + (lane & 15);
-    const bool ok = pix < a.npix;
+    const bool ok = pix < npix_c;
+    size_t opix = (size_t)pix;
+    if (MODE == 3 && ok) {  // class-local (n, i, j) -> dx (n, 2i+py, 2j+px)
+      const int nn = pix / (CH * CW), rem = pix - nn * CH * CW, ii = rem / CW, jj = rem - ii * CW;
+      opix = ((size_t)nn * a.OH + 2 * ii + py) * a.OW + 2 * jj + px;
+    }
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const int oc = oc0 + wm * (BM / 2) + m * 16 + 4 * (lane >> 4);
       float v0 = acc[m][n][0], v1 = acc[m][n][1], v2 = acc[m][n][2], v3 = acc[m][n][3];
       if (ok) {
-        const size_t off = (size_t)pix * a.OC + oc;
+        const size_t off = opix * a.OC + oc;
         if (HAS_RES) {
           const u32x2 rr = *reinterpret_cast<const u32x2*>(a.res + off);
           v0 += lo_bf(rr[0]); v1 += hi_bf(rr[0]); v2 += lo_bf(rr[1]); v3 += hi_bf(rr[1]);
@@ -398,7 +440,7 @@ Plan plan_for(int OC, int npix, int ksteps) {
 template <int BM, int BN, int MODE, bool RES, bool SPLIT>
 int launch2(const Conv2Args& a, hipStream_t st) {
   const size_t lds = (size_t)3 * (BM + BN) * 128;
-  dim3 grid(a.n_oc_tiles * a.n_pix_tiles, SPLIT ? a.splits : 1);
+  dim3 grid(a.n_oc_tiles * a.n_pix_tiles, SPLIT ? a.splits : (MODE == 3 ? 4 : 1));
   hipLaunchKernelGGL((conv2_kernel<BM, BN, MODE, RES, SPLIT>), grid, dim3(256), lds, st, a);
   return (int)hipGetLastError();
 }
@@ -508,7 +550,16 @@ int psx_conv_dgrad2(const void* dy, const void* wd, void* dx, const void* res, c
   int e;
   if (stride == 1)
     e = res ? dispatch2<1, true>(p, a, st) : dispatch2<1, false>(p, a, st);
-  else if (stride == 2)
+  else if (stride == 2 && a.log2_icc >= 3 && !getenv("PSX_DGRAD_S2_GATHER")) {
+    // parity classes: each class GEMM covers dx pixels (2i+py, 2j+px), ~1/4 of them
+    Plan q = plan_for(IC_fwd, (a.npix + 3) / 4, Kg / 64);
+    q.splits = 1;
+    a.n_oc_tiles = IC_fwd / q.BM;
+    a.n_pix_tiles = (Nb * ((H + 1) / 2) * ((W + 1) / 2) + q.BN - 1) / q.BN;
+    a.splits = 1;
+    a.kps = Kg / 64;
+    return res ? dispatch2<3, true>(q, a, st) : dispatch2<3, false>(q, a, st);
+  } else if (stride == 2)
     e = res ? dispatch2<2, true>(p, a, st) : dispatch2<2, false>(p, a, st);
   else
     return -4;

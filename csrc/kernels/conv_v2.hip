@@ -33,6 +33,16 @@ struct Conv2Args {
   int n_oc_tiles, n_pix_tiles, splits, kps;  // kps: k-steps per split
   int fuse_fin;                              // last workgroup finalizes the BN layer (bnfin.hpp)
   BnFin fin;
+  // optional fused BatchNorm-backward reduction over this launch's bf16 output g (dgrad): slot
+  // rows [PSX_STAT_SLOTS][bns][OC] of sum(dz), sum(dz*xhat1) [, sum(dz*xhat2)], dz = g*[o > 0],
+  // xhat = (y - mean) * invstd — what bn_bwd_reduce (bn.hip) would compute in a separate pass.
+  float* bpart;
+  const uint16_t* bo;
+  const uint16_t* by1;
+  const uint16_t* by2;
+  const float* bsaved1;  // [2][OC] mean, invstd
+  const float* bsaved2;
+  int bns;
 };
 
 PSX_DEV int kmaj2(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
@@ -258,11 +268,24 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   }
 
   // ---- epilogue: bf16 NHWC store (+residual), BN partial statistics ----
-  float s1[MT][4], s2[MT][4];
+  float s1[MT][4], s2[MT][4], s3[MT][4];
+  float bm1[MT][4], bi1[MT][4], bm2[MT][4], bi2[MT][4];
+  const bool bwd = a.bpart != nullptr, two = a.by2 != nullptr;
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) s1[m][i] = s2[m][i] = 0.f;
+    for (int i = 0; i < 4; ++i) {
+      s1[m][i] = s2[m][i] = s3[m][i] = 0.f;
+      const int ch = oc0 + wm * (BM / 2) + m * 16 + 4 * (lane >> 4) + i;
+      if (bwd) {
+        bm1[m][i] = a.bsaved1[ch];
+        bi1[m][i] = a.bsaved1[a.OC + ch];
+        if (two) {
+          bm2[m][i] = a.bsaved2[ch];
+          bi2[m][i] = a.bsaved2[a.OC + ch];
+        }
+      }
+    }
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
     const int pix = pix0 + wn * (BN / 2) + n * 16 + (lane & 15);
@@ -293,7 +316,57 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
           s1[m][2] += q2; s2[m][2] += q2 * q2;
           s1[m][3] += q3; s2[m][3] += q3 * q3;
         }
+        if (bwd) {
+          const u32x2 om = *reinterpret_cast<const u32x2*>(a.bo + off);
+          const u32x2 yv = *reinterpret_cast<const u32x2*>(a.by1 + off);
+          u32x2 y2v = {0u, 0u};
+          if (two) y2v = *reinterpret_cast<const u32x2*>(a.by2 + off);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t w = i < 2 ? o[0] : o[1], mw = i < 2 ? om[0] : om[1];
+            const uint32_t yw = i < 2 ? yv[0] : yv[1], y2w = i < 2 ? y2v[0] : y2v[1];
+            const bool hi = i & 1;
+            const float g = hi ? hi_bf(w) : lo_bf(w);
+            const float dz = (hi ? hi_bf(mw) : lo_bf(mw)) > 0.f ? g : 0.f;
+            s1[m][i] += dz;
+            s2[m][i] += dz * ((hi ? hi_bf(yw) : lo_bf(yw)) - bm1[m][i]) * bi1[m][i];
+            if (two) s3[m][i] += dz * ((hi ? hi_bf(y2w) : lo_bf(y2w)) - bm2[m][i]) * bi2[m][i];
+          }
+        }
       }
+    }
+  }
+  if (bwd) {  // [2 wn][NS][BM] in LDS, then one atomic per (stat, channel) into the slot row
+    const int NSr = a.bns;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s1[m][i] += __shfl_xor(s1[m][i], o, 64);
+          s2[m][i] += __shfl_xor(s2[m][i], o, 64);
+          if (two) s3[m][i] += __shfl_xor(s3[m][i], o, 64);
+        }
+      }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = wm * (BM / 2) + m * 16 + 4 * (lane >> 4) + i;
+          red[(wn * 3 + 0) * BM + row] = s1[m][i];
+          red[(wn * 3 + 1) * BM + row] = s2[m][i];
+          red[(wn * 3 + 2) * BM + row] = s3[m][i];
+        }
+    }
+    __syncthreads();
+    float* dst = a.bpart + (size_t)(pix_t & (PSX_STAT_SLOTS - 1)) * NSr * a.OC;
+    for (int j = tid; j < NSr * BM; j += 256) {
+      const int which = j / BM, row = j - which * BM;
+      atomicAdd(dst + which * a.OC + oc0 + row, red[which * BM + row] + red[(3 + which) * BM + row]);
     }
   }
   if (a.stats) {
@@ -337,14 +410,32 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
                                                             int OC, uint16_t* __restrict__ out,
                                                             const uint16_t* __restrict__ res,
                                                             float* __restrict__ stats, int pix_per_block,
-                                                            int fuse_fin, BnFin fin) {
-  extern __shared__ __attribute__((aligned(16))) float sred[];  // [256][16]
+                                                            int fuse_fin, BnFin fin, float* __restrict__ bpart,
+                                                            const uint16_t* __restrict__ bo,
+                                                            const uint16_t* __restrict__ by1,
+                                                            const uint16_t* __restrict__ by2,
+                                                            const float* __restrict__ bsaved1,
+                                                            const float* __restrict__ bsaved2, int bns) {
+  extern __shared__ __attribute__((aligned(16))) float sred[];  // [256][24]
   const int cvec = OC >> 3, tpp = 256 / cvec;
   const int cg = threadIdx.x % cvec, pr = threadIdx.x / cvec;
   const size_t slab = (size_t)npix * OC;
-  float s1[8], s2[8];
+  // per-thread partial sums: fwd stats (sum, sumsq) or fused BN-backward (dz, dz*xh1, dz*xh2)
+  const bool bwd = bpart != nullptr, two = by2 != nullptr;
+  const int nst = bwd ? bns : 2;
+  float st[3][8], m1[8], i1[8], m2[8], i2[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  for (int j = 0; j < 8; ++j) {
+    st[0][j] = st[1][j] = st[2][j] = 0.f;
+    if (bwd) {
+      m1[j] = bsaved1[cg * 8 + j];
+      i1[j] = bsaved1[OC + cg * 8 + j];
+      if (two) {
+        m2[j] = bsaved2[cg * 8 + j];
+        i2[j] = bsaved2[OC + cg * 8 + j];
+      }
+    }
+  }
   const int pbeg = blockIdx.x * pix_per_block, pend = min(npix, pbeg + pix_per_block);
   for (int p = pbeg + pr; p < pend; p += tpp) {
     const size_t off = (size_t)p * OC + cg * 8;
@@ -371,27 +462,44 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float q0 = lo_bf(o[j]), q1 = hi_bf(o[j]);
-        s1[2 * j] += q0; s2[2 * j] += q0 * q0;
-        s1[2 * j + 1] += q1; s2[2 * j + 1] += q1 * q1;
+        st[0][2 * j] += q0; st[1][2 * j] += q0 * q0;
+        st[0][2 * j + 1] += q1; st[1][2 * j + 1] += q1 * q1;
+      }
+    } else if (bwd) {
+      const u32x4 om = *reinterpret_cast<const u32x4*>(bo + off);
+      const u32x4 yv = *reinterpret_cast<const u32x4*>(by1 + off);
+      u32x4 y2v = {0u, 0u, 0u, 0u};
+      if (two) y2v = *reinterpret_cast<const u32x4*>(by2 + off);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool hi = e & 1;
+        const uint32_t w = o[e >> 1], mw = om[e >> 1], yw = yv[e >> 1], y2w = y2v[e >> 1];
+        const float g = hi ? hi_bf(w) : lo_bf(w);
+        const float dz = (hi ? hi_bf(mw) : lo_bf(mw)) > 0.f ? g : 0.f;
+        st[0][e] += dz;
+        st[1][e] += dz * ((hi ? hi_bf(yw) : lo_bf(yw)) - m1[e]) * i1[e];
+        if (two) st[2][e] += dz * ((hi ? hi_bf(y2w) : lo_bf(y2w)) - m2[e]) * i2[e];
       }
     }
   }
-  if (!stats) return;
-  float* mine = sred + threadIdx.x * 16;
+  if (!stats && !bwd) return;
+  float* mine = sred + threadIdx.x * 24;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    mine[j] = s1[j];
-    mine[8 + j] = s2[j];
+    mine[j] = st[0][j];
+    mine[8 + j] = st[1][j];
+    mine[16 + j] = st[2][j];
   }
   __syncthreads();
-  float* dst = stats + (size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * 2 * OC;
-  for (int t = threadIdx.x; t < cvec * 16; t += 256) {
-    const int cgi = t / 16, sj = t - cgi * 16;
+  float* dst = (bwd ? bpart : stats) + (size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * nst * OC;
+  for (int t = threadIdx.x; t < cvec * nst * 8; t += 256) {
+    const int cgi = t / (nst * 8), sj = t - cgi * (nst * 8);
     float acc = 0.f;
-    for (int q = 0; q < tpp; ++q) acc += sred[(q * cvec + cgi) * 16 + sj];
+    for (int q = 0; q < tpp; ++q) acc += sred[(q * cvec + cgi) * 24 + sj];
     const int which = sj >> 3, j = sj & 7;
     atomicAdd(dst + which * OC + cgi * 8 + j, acc);
   }
+  if (!stats) return;
   if (fuse_fin && last_block_arrive(fin.counter, gridDim.x, reinterpret_cast<unsigned char*>(sred)))
     bn_finalize_block<PSX_STAT_SLOTS>(stats, fin);
 }
@@ -464,13 +572,15 @@ int finish_split(const Conv2Args& a, hipStream_t st) {
   int ppb = (a.npix + 511) / 512;
   if (ppb < 8) ppb = 8;
   const int grid = (a.npix + ppb - 1) / ppb;
-  const size_t lds = 256 * 16 * sizeof(float);
+  const size_t lds = 256 * 24 * sizeof(float);
   if (a.res)
     hipLaunchKernelGGL(conv_splitk_epilogue<true>, dim3(grid), dim3(256), lds, st, a.part, a.splits, a.npix, a.OC,
-                       a.out, a.res, a.stats, ppb, a.fuse_fin, a.fin);
+                       a.out, a.res, a.stats, ppb, a.fuse_fin, a.fin, a.bpart, a.bo, a.by1, a.by2, a.bsaved1,
+                       a.bsaved2, a.bns);
   else
     hipLaunchKernelGGL(conv_splitk_epilogue<false>, dim3(grid), dim3(256), lds, st, a.part, a.splits, a.npix, a.OC,
-                       a.out, (const uint16_t*)nullptr, a.stats, ppb, a.fuse_fin, a.fin);
+                       a.out, (const uint16_t*)nullptr, a.stats, ppb, a.fuse_fin, a.fin, a.bpart, a.bo, a.by1,
+                       a.by2, a.bsaved1, a.bsaved2, a.bns);
   return (int)hipGetLastError();
 }
 
@@ -523,9 +633,28 @@ int psx_conv_fwd2(const void* x, const void* wf, void* y, float* stats, const vo
   return finish_split(a, st);
 }
 
+struct BwdStatsDesc {  // fused BN-backward reduction over the dgrad output (see Conv2Args)
+  float* part;
+  const void* o;
+  const void* y1;
+  const void* y2;
+  const float* saved1;
+  const float* saved2;
+};
+
 int psx_conv_dgrad2(const void* dy, const void* wd, void* dx, const void* res, const void* zero, float* ws, int Nb,
-                    int H, int W, int IC_fwd, int OC_fwd, int R, int S, int stride, int pad, int Kg, hipStream_t st) {
+                    int H, int W, int IC_fwd, int OC_fwd, int R, int S, int stride, int pad, int Kg,
+                    const BwdStatsDesc* bst, hipStream_t st) {
   Conv2Args a{};
+  if (bst) {
+    a.bpart = bst->part;
+    a.bo = (const uint16_t*)bst->o;
+    a.by1 = (const uint16_t*)bst->y1;
+    a.by2 = (const uint16_t*)bst->y2;
+    a.bsaved1 = bst->saved1;
+    a.bsaved2 = bst->saved2;
+    a.bns = bst->y2 ? 3 : 2;
+  }
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   a.in = (const uint16_t*)dy;
   a.w = (const uint16_t*)wd;

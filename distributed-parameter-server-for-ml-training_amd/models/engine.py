@@ -177,6 +177,10 @@ class HipResNetEngine:
         self.conv_impl = int(os.environ.get("PSX_CONV_IMPL", "2"))
         # BN finalize inside the producing launch (csrc/kernels/bnfin.hpp); 0 = separate kernels
         self.fuse_fin = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNFIN", "0") == "1"
+        # BN-backward sums from the dgrad epilogue: measured neutral (2.215 vs 2.217 ms/step; the MFMA
+        # output layout makes its extra o/y loads half-coalesced), so opt-in
+        self.fuse_bnbwd = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNBWD", "0") == "1"
+        self._prereduced = set()
         self.wg_stream = (torch.cuda.Stream(device=self.dev)
                           if os.environ.get("PSX_WGRAD_STREAM", "0") == "1" else None)
         self._wg_batch = None
@@ -425,11 +429,23 @@ class HipResNetEngine:
             K.wgrad_reduce(self.wpart_w, cs.splits, cs.cout, cs.kg, cs.cin, cs.cp, cs.k, 1.0,
                            self._gptr(f"{cs.name}.weight"), self.grad_fp16)
 
-    def _dgrad(self, cs: ConvSpec, dy, dx, res=None):
+    def _dgrad(self, cs: ConvSpec, dy, dx, res=None, bn_next=None):
+        """bn_next = (BNSpec, o, y, two|None): the BN whose backward consumes dx; with conv v2 its
+        reduction (sum dz, sum dz*xhat) is produced by the dgrad epilogue (PSX_FUSE_BNBWD)."""
         wd = self.wbuf[cs.wd_off:cs.wd_off + cs.cp * cs.kgd]
         if self.conv_impl == 2:
+            bst = None
+            if bn_next is not None and self.fuse_bnbwd:
+                bs, o, y, two = bn_next
+                st = self.bn[bs.name]
+                if two is None:
+                    bst = K.bwd_stats_desc(self._red(bs, "bwd"), o, y, st["saved"])
+                else:
+                    bs2, y2 = two
+                    bst = K.bwd_stats_desc(self._red(bs, "bwd"), o, y, st["saved"], y2, self.bn[bs2.name]["saved"])
+                self._prereduced.add(bs.name)
             K.conv_dgrad2(dy, wd, dx, res, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
-                          cs.kgd)
+                          cs.kgd, bst=bst)
         else:
             K.conv_dgrad(dy, wd, dx, res, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kgd)
 
@@ -438,9 +454,13 @@ class HipResNetEngine:
         st = self.bn[bs.name]
         part = self._red(bs, "bwd")
         fuse = self.fuse_fin
+        pre = bs.name in self._prereduced  # sums already produced by the dgrad epilogue
+        self._prereduced.discard(bs.name)
+        if pre:
+            fuse = False
         if two is None:
-            T = K.bn_bwd_reduce(g, o, y, st["saved"], part, npix, bs.c,
-                                fin1=self._fin_bwd(bs, arena, npix) if fuse else None)
+            T = self.nslots if pre else K.bn_bwd_reduce(g, o, y, st["saved"], part, npix, bs.c,
+                                                        fin1=self._fin_bwd(bs, arena, npix) if fuse else None)
             if not fuse:
                 K.bn_bwd_finalize(part, T, 2, 1, bs.c, npix, self._aview(arena, f"{bs.name}.weight"),
                                   st["saved"], st["coef"], self._gptr(f"{bs.name}.weight"),
@@ -449,9 +469,10 @@ class HipResNetEngine:
         else:
             bs2, y2, dx2 = two
             st2 = self.bn[bs2.name]
-            T = K.bn_bwd_reduce(g, o, y, st["saved"], part, npix, bs.c, y2=y2, saved2=st2["saved"],
-                                fin1=self._fin_bwd(bs, arena, npix) if fuse else None,
-                                fin2=self._fin_bwd(bs2, arena, npix) if fuse else None)
+            T = self.nslots if pre else K.bn_bwd_reduce(g, o, y, st["saved"], part, npix, bs.c, y2=y2,
+                                                        saved2=st2["saved"],
+                                                        fin1=self._fin_bwd(bs, arena, npix) if fuse else None,
+                                                        fin2=self._fin_bwd(bs2, arena, npix) if fuse else None)
             if not fuse:
                 K.bn_bwd_finalize(part, T, 3, 1, bs.c, npix, self._aview(arena, f"{bs.name}.weight"),
                                   st["saved"], st["coef"], self._gptr(f"{bs.name}.weight"),
@@ -540,16 +561,27 @@ class HipResNetEngine:
             x_in = d["inp"] if i == 0 else d["a"][i - 1]
             self._wgrad(cs, x_in, d["dy"][i])
             if i > 0:
-                self._dgrad(cs, d["dy"][i], d["da"][i - 1])
+                self._dgrad(cs, d["dy"][i], d["da"][i - 1], bn_next=(b.bns[i - 1], d["a"][i - 1], d["y"][i - 1], None))
                 self._bn_bwd(b.bns[i - 1], arena, d["da"][i - 1], d["a"][i - 1], d["y"][i - 1], d["dy"][i - 1],
                              B * cs.h * cs.w)
             elif b.down:
                 ds, dbn = b.down
                 self._wgrad(ds, d["inp"], d["dys"])
                 self._dgrad(ds, d["dys"], d["dxs"])
-                self._dgrad(cs, d["dy"][0], d["gin"], res=d["dxs"])
+                self._dgrad(cs, d["dy"][0], d["gin"], res=d["dxs"], bn_next=self._bn_into(j))
             else:
-                self._dgrad(cs, d["dy"][0], d["gin"], res=d["dz"])
+                self._dgrad(cs, d["dy"][0], d["gin"], res=d["dz"], bn_next=self._bn_into(j))
+
+    def _bn_into(self, j: int):
+        """The BN whose backward consumes block j's input gradient: the previous block's output
+        BN (+ its shortcut BN), or the stem BN (not across the ResNet-50 max-pool)."""
+        if j > 0:
+            pb, pd = self.spec.blocks[j - 1], self.blk[j - 1]
+            two = (pb.down[1], pd["ys"]) if pb.down else None
+            return (pb.bns[-1], pd["out"], pd["y"][-1], two)
+        if self.spec.maxpool:
+            return None
+        return (self.spec.stem_bn, self.a0, self.y0, None)
 
     def _bwd_stem(self, arena):
         sp, B = self.spec, self.B

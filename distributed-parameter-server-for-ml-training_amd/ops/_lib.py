@@ -48,7 +48,7 @@ _KERNEL_SIGS = {
     "psx_conv2_workspace": (i64, [i32, i32, i32, i32, i32]),
     "psx_conv_wgrad2": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
     "psx_conv_fwd2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
-    "psx_conv_dgrad2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
+    "psx_conv_dgrad2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
     "psx_bn_finalize": (i32, [vp, i32, i32, f32, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp]),
     "psx_bn_eval_affine": (i32, [i32, vp, vp, vp, vp, f32, vp, vp, vp]),
     "psx_bn_apply": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp]),

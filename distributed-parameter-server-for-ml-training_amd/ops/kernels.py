@@ -112,9 +112,22 @@ def conv_fwd2(x, wf, y, stats, ws, nb, h, w, ic, oc, k, stride, pad, kg, fin: Bn
                                   stream_ptr()), "conv_fwd2")
 
 
-def conv_dgrad2(dy, wd, dx, res, ws, nb, h, w, ic_fwd, oc_fwd, k, stride, pad, kgd):
+class BwdStatsDesc(C.Structure):
+    """csrc/kernels/conv_v2.hip BwdStatsDesc: fused BN-backward reduction over a dgrad output."""
+    _fields_ = [("part", C.c_void_p), ("o", C.c_void_p), ("y1", C.c_void_p), ("y2", C.c_void_p),
+                ("saved1", C.c_void_p), ("saved2", C.c_void_p)]
+
+
+def bwd_stats_desc(part, o, y1, saved1, y2=None, saved2=None) -> BwdStatsDesc:
+    return BwdStatsDesc(ptr(part), ptr(o), ptr(y1), ptr(y2), ptr(saved1), ptr(saved2))
+
+
+def conv_dgrad2(dy, wd, dx, res, ws, nb, h, w, ic_fwd, oc_fwd, k, stride, pad, kgd, bst: BwdStatsDesc | None = None):
+    """With ``bst`` the epilogue also produces the BN-backward slot sums of dx (what
+    bn_bwd_reduce would compute), so that pass can be skipped."""
     check(kernels().psx_conv_dgrad2(ptr(dy), ptr(wd), ptr(dx), ptr(res), ptr(zero_page(dy.device)), ptr(ws), nb, h,
-                                    w, ic_fwd, oc_fwd, k, k, stride, pad, kgd, stream_ptr()), "conv_dgrad2")
+                                    w, ic_fwd, oc_fwd, k, k, stride, pad, kgd,
+                                    C.byref(bst) if bst is not None else None, stream_ptr()), "conv_dgrad2")
 
 
 def conv_wgrad2_splits(nb, h, w, ic, oc, k, stride, pad, kg) -> int:

@@ -115,8 +115,8 @@ def test_fused_bn_finalize_matches_separate_kernels(setup):
     imgs = torch.randint(0, 256, (n, 32, 32, 3), dtype=torch.uint8, device=DEV)
     labs = torch.randint(0, 100, (n,), dtype=torch.int32, device=DEV)
     eng.index.copy_(torch.arange(eng.B, dtype=torch.int32, device=DEV))
-    fused_before = eng.fuse_fin
-    eng.fuse_fin = True
+    fused_before, bnbwd_before = eng.fuse_fin, eng.fuse_bnbwd
+    eng.fuse_fin, eng.fuse_bnbwd = True, False
     a = arena.clone()
     for step in range(2):
         eng.train_step(a, imgs, labs)
@@ -146,7 +146,37 @@ def test_fused_bn_finalize_matches_separate_kernels(setup):
             assert torch.allclose(coef, st["coef"], rtol=1e-5, atol=1e-6), (step, bs.name)
             gw = layout.grad_view(eng.grads, f"{bs.name}.weight").float()
             assert torch.allclose(dg, gw, rtol=1e-5, atol=1e-6), (step, bs.name)
-    eng.fuse_fin = fused_before
+    eng.fuse_fin, eng.fuse_bnbwd = fused_before, bnbwd_before
+
+
+def test_dgrad_fused_bn_backward_sums_match_reduce_kernel(setup):
+    """PSX_FUSE_BNBWD: the BN-backward slot sums produced in the dgrad epilogue equal what the
+    separate bn_bwd_reduce pass computes from the stored dgrad output."""
+    model, layout, arena, eng, x, y = setup
+    n = 256
+    imgs = torch.randint(0, 256, (n, 32, 32, 3), dtype=torch.uint8, device=DEV)
+    labs = torch.randint(0, 100, (n,), dtype=torch.int32, device=DEV)
+    eng.index.copy_(torch.arange(eng.B, dtype=torch.int32, device=DEV))
+    before = eng.fuse_bnbwd
+    eng.fuse_bnbwd = True
+    a = arena.clone()
+    eng.train_step(a, imgs, labs)
+    torch.cuda.synchronize()
+    checked = 0
+    for b, d in zip(eng.spec.blocks, eng.blk):
+        for i in range(1, len(b.convs)):  # in-block BNs fed by a dgrad epilogue
+            bs = b.bns[i - 1]
+            npix = d["da"][i - 1].numel() // bs.c
+            ref = torch.zeros_like(eng._red(bs, "bwd"))
+            K.bn_bwd_reduce(d["da"][i - 1], d["a"][i - 1], d["y"][i - 1], eng.bn[bs.name]["saved"], ref, npix, bs.c)
+            torch.cuda.synchronize()
+            m = K.STAT_SLOTS * 2 * bs.c  # the region is sized for 3 stat rows; NS = 2 here
+            got = eng._red(bs, "bwd")[:m].view(K.STAT_SLOTS, 2, bs.c).sum(0)
+            want = ref[:m].view(K.STAT_SLOTS, 2, bs.c).sum(0)
+            assert torch.allclose(got, want, rtol=1e-3, atol=1e-3 * want.abs().max().item()), bs.name
+            checked += 1
+    eng.fuse_bnbwd = before
+    assert checked == 8
 
 
 def test_segmented_graphs_match_single_graph(setup):

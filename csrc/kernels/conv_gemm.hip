@@ -16,6 +16,8 @@
 // MFMA orientation: A = weights (rows = output channels), B = im2col pixels, so the
 // accumulator of one lane holds 4 consecutive output channels of one pixel -> each lane
 // stores 8 contiguous bytes of the NHWC output.
+#include <stdlib.h>
+
 #include "common.hpp"
 
 namespace psx {
@@ -381,30 +383,116 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
   const size_t slab = (size_t)OC * Kg;
   const size_t base = (size_t)blockIdx.x * 256 + lane * 4;
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  // the 4 waves split the slabs 4 ways; 8 independent 16-byte loads in flight per lane (the
+  // reduce is bandwidth work, and with as few as 144 workgroups for a 64x576 layer it is
+  // latency-bound unless each lane keeps several slab loads outstanding)
+  f32x4 acc[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) acc[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
   int sp = g;
-  for (; sp + 4 < splits; sp += 8) {
-    acc0 += *reinterpret_cast<const f32x4*>(part + sp * slab + base);
-    acc1 += *reinterpret_cast<const f32x4*>(part + (sp + 4) * slab + base);
+  for (; sp + 28 < splits; sp += 32) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += *reinterpret_cast<const f32x4*>(part + (size_t)(sp + 4 * u) * slab + base);
   }
-  if (sp < splits) acc0 += *reinterpret_cast<const f32x4*>(part + sp * slab + base);
-  red[g][lane] = acc0 + acc1;
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (sp + 4 * u < splits) acc[u] += *reinterpret_cast<const f32x4*>(part + (size_t)(sp + 4 * u) * slab + base);
+  red[g][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   __syncthreads();
   if (g != 0) return;
   const f32x4 v = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
   const int RS = R * S;
+  const int oc = (int)(base / Kg);
+  int k = (int)(base - (size_t)oc * Kg);  // the 4 columns never straddle a row (Kg % 64 == 0)
+  int tap = k / IC, c = k - tap * IC;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const size_t idx = base + e;
-    const int oc = (int)(idx / Kg), k = (int)(idx - (size_t)oc * Kg);
-    const int tap = k / IC, c = k - tap * IC;
-    if (tap >= RS || c >= Cin) continue;
-    const float val = v[e] * scale;
-    const size_t o = ((size_t)oc * Cin + c) * RS + tap;
+    if (tap < RS && c < Cin) {
+      const float val = v[e] * scale;
+      const size_t o = ((size_t)oc * Cin + c) * RS + tap;
+      if constexpr (sizeof(OutT) == 2) {
+        out[o] = __builtin_bit_cast(uint16_t, (_Float16)val);
+      } else {
+        out[o] = val;
+      }
+    }
+    if (++c == IC) {
+      c = 0;
+      ++tap;
+    }
+  }
+}
+
+// v2 mapping: workgroup = (output channel oc, chunk of CW input channels) x all R*S taps, so
+// its OIHW output [oc][c0..c0+CW)[taps] is one contiguous run (written from an LDS transpose).
+// Threads = (item, split group): an item is 4 channels of one tap (one 16-byte load per split),
+// G groups take splits g, g+G, ... so a layer with few items still keeps 256 lanes x several
+// 16-byte loads in flight (the partials are 2-16 MB per layer; the v1 mapping was latency-bound
+// at ~1 TB/s with 4-byte loads and 64 workgroups on layer1).
+template <typename OutT>
+__global__ __launch_bounds__(256) void wgrad_reduce2_kernel(const float* __restrict__ part, int splits, int Kg,
+                                                            int Cin, int IC, int RS, int CW, float scale,
+                                                            OutT* __restrict__ out) {
+  __shared__ float4 acc[256];
+  __shared__ float tile[64 * 49];  // [c][tap], CW*RS <= 64*49
+  const int oc = blockIdx.x, c0 = blockIdx.y * CW;
+  const int q = CW >> 2;           // channel quads per tap
+  const int items = RS * q;
+  const int G = items >= 256 ? 1 : min(splits, 256 / items);
+  const size_t slab = (size_t)gridDim.x * Kg;
+  const float* row = part + (size_t)oc * Kg + c0;
+  for (int base = 0; base < items; base += 256 / G) {
+    const int t = threadIdx.x;
+    const int per = 256 / G;            // items handled per pass
+    const int it = base + t % per, g = t / per;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool live = g < G && t % per + base < items && it < items;
+    if (live) {
+      const int tap = it / q, cq = it % q;
+      const float4* src = reinterpret_cast<const float4*>(row + (size_t)tap * IC + cq * 4);
+      const size_t st4 = slab / 4;
+      int sp = g;
+      float4 a1 = s, a2 = s, a3 = s;
+      for (; sp + 3 * G < splits; sp += 4 * G) {
+        const float4 v0 = src[(size_t)sp * st4], v1 = src[(size_t)(sp + G) * st4];
+        const float4 v2 = src[(size_t)(sp + 2 * G) * st4], v3 = src[(size_t)(sp + 3 * G) * st4];
+        s.x += v0.x; s.y += v0.y; s.z += v0.z; s.w += v0.w;
+        a1.x += v1.x; a1.y += v1.y; a1.z += v1.z; a1.w += v1.w;
+        a2.x += v2.x; a2.y += v2.y; a2.z += v2.z; a2.w += v2.w;
+        a3.x += v3.x; a3.y += v3.y; a3.z += v3.z; a3.w += v3.w;
+      }
+      for (; sp < splits; sp += G) {
+        const float4 v = src[(size_t)sp * st4];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+      s.x += a1.x + a2.x + a3.x; s.y += a1.y + a2.y + a3.y;
+      s.z += a1.z + a2.z + a3.z; s.w += a1.w + a2.w + a3.w;
+    }
+    acc[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x < per && base + threadIdx.x < items) {
+      float4 r = acc[threadIdx.x];
+      for (int gg = 1; gg < G; ++gg) {
+        const float4 v = acc[gg * per + threadIdx.x];
+        r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+      }
+      const int it2 = base + threadIdx.x, tap = it2 / q, c = (it2 % q) * 4;
+      tile[(c + 0) * RS + tap] = r.x;
+      tile[(c + 1) * RS + tap] = r.y;
+      tile[(c + 2) * RS + tap] = r.z;
+      tile[(c + 3) * RS + tap] = r.w;
+    }
+    __syncthreads();
+  }
+  const int cv = min(CW, Cin - c0);  // valid (unpadded) input channels of this chunk
+  if (cv <= 0) return;
+  OutT* dst = out + ((size_t)oc * Cin + c0) * RS;
+  for (int j = threadIdx.x; j < cv * RS; j += 256) {
+    const float val = tile[j] * scale;
     if constexpr (sizeof(OutT) == 2) {
-      out[o] = __builtin_bit_cast(uint16_t, (_Float16)val);
+      dst[j] = __builtin_bit_cast(uint16_t, (_Float16)val);
     } else {
-      out[o] = val;
+      dst[j] = val;
     }
   }
 }
@@ -545,6 +633,19 @@ int psx_conv_wgrad(const void* x, const void* dy, float* part, int Nb, int H, in
 
 int psx_wgrad_reduce(const float* part, int splits, int OC, int Kg, int Cin, int IC, int R, int S, float scale,
                      void* out, int out_fp16, hipStream_t st) {
+  if (R * S <= 49 && IC % 16 == 0 && !getenv("PSX_WGRAD_REDUCE_V1")) {
+    // chunk width: widest of 64/32/16 channels that still gives >= 1024 workgroups
+    int CW = IC < 64 ? IC : 64;
+    while (CW > 16 && (long)OC * (IC / CW) < 1024) CW >>= 1;
+    const dim3 grid(OC, IC / CW);
+    if (out_fp16)
+      hipLaunchKernelGGL(wgrad_reduce2_kernel<uint16_t>, grid, dim3(256), 0, st, part, splits, Kg, Cin, IC, R * S,
+                         CW, scale, (uint16_t*)out);
+    else
+      hipLaunchKernelGGL(wgrad_reduce2_kernel<float>, grid, dim3(256), 0, st, part, splits, Kg, Cin, IC, R * S, CW,
+                         scale, (float*)out);
+    return (int)hipGetLastError();
+  }
   if (((long)OC * Kg) % 256) return -2;
   const int grid = (int)(((long)OC * Kg) / 256);
   if (out_fp16)

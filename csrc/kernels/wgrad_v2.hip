@@ -177,6 +177,171 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(Wgrad2Args a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// wgrad3: 3x3 / stride 1 / pad 1 with tap reuse. For one kernel row r, the three taps s=0,1,2
+// read the same input row shifted by -1/0/+1 pixels, so one LDS window of 64 input pixels
+// x(n, oh+r-1, ow) (plus one zero row for the row edges) feeds a 192-row output tile
+// (3 taps x 64 channels) instead of three 64-row tiles each gathering its own copy. Each lane's
+// transposed-read address picks slot (pixel + s - 1), or the zero row when ow + s - 1 leaves
+// the image row; 64-pixel steps hold whole rows because W is a power of two <= 64. Staged
+// bytes per step stay ~16 KB while the MFMA work per step triples (wgrad2 is LDS-DMA bound).
+struct Wgrad3Args {
+  const uint16_t* x;
+  const uint16_t* dy;
+  float* part;
+  const uint16_t* zero;
+  int H, W, log2w, IC, OC, Kg, npix;
+  int n_c_tiles, n_oc_tiles, splits, steps_per_split;
+};
+
+// wait until at most `ahead` later stage groups (PER DMA ops each) are still in flight
+template <int PER, int MAXA>
+PSX_DEV void wait_ahead(int ahead) {
+  if constexpr (MAXA <= 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (ahead >= MAXA)
+      wait_vmcnt<MAXA * PER>();
+    else
+      wait_ahead<PER, MAXA - 1>(ahead);
+  }
+}
+
+template <int BC, int NS>
+__global__ __launch_bounds__(256) void wgrad3_kernel(Wgrad3Args a) {
+  constexpr int DROWB = BC * 2, DCPR = DROWB / 16, DRPI = 64 / DCPR, LD = 64 / DRPI / 4;
+  constexpr int XT = 65 * 128, DT = 64 * DROWB, STAGE = XT + DT;
+  constexpr int NT = BC / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntile = 3 * a.n_c_tiles * a.n_oc_tiles;
+  const int bid = xcd_remap(blockIdx.x, ntile * a.splits);
+  const int split = bid / ntile, t = bid - split * ntile;
+  const int oc_t = t % a.n_oc_tiles, rest = t / a.n_oc_tiles;
+  const int c_t = rest % a.n_c_tiles, r = rest / a.n_c_tiles;
+  const int c0 = c_t * 64, oc0 = oc_t * BC;
+  const int pbeg = split * a.steps_per_split * 64;
+  const int nsteps = min(a.steps_per_split, (a.npix - pbeg + 63) / 64);
+  const int W = a.W;
+
+  // zero row (slot 64) of every stage; the DMA never writes it
+  if (tid < NS * 8) *reinterpret_cast<uint4*>(smem + (tid >> 3) * STAGE + 64 * 128 + (tid & 7) * 16) = uint4{0, 0, 0, 0};
+
+  // ---- per-lane DMA state ----
+  int xrow[2], xcol[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (i * 4 + wid) * 8 + (lane >> 3);
+    xrow[i] = row;
+    xcol[i] = c0 + (((lane & 7) ^ (((row >> 1) & 3) << 1)) << 3);
+  }
+  int drow[LD], dchunk[LD];
+#pragma unroll
+  for (int i = 0; i < LD; ++i) {
+    const int row = (i * 4 + wid) * DRPI + lane / DCPR;
+    const int pos = lane % DCPR;
+    drow[i] = row;
+    dchunk[i] = (DROWB == 128) ? (pos ^ (((row >> 1) & 3) << 1)) : (pos ^ ((row & 7) << 1));
+  }
+  const long xshift = (long)(r - 1) * W;
+
+  auto issue = [&](int st, int stage) {
+    unsigned char* base = smem + stage * STAGE;
+    const int p0 = pbeg + st * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int pix = p0 + xrow[i];
+      const int ih = ((pix >> a.log2w) & (a.H - 1)) + r - 1;
+      const uint16_t* src = a.zero;
+      if (pix < a.npix && (unsigned)ih < (unsigned)a.H) src = a.x + ((long)pix + xshift) * a.IC + xcol[i];
+      glds16(src, base + (i * 4 + wid) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < LD; ++i) {
+      const int pix = p0 + drow[i];
+      const uint16_t* src = pix < a.npix ? a.dy + (size_t)pix * a.OC + oc0 + dchunk[i] * 8 : a.zero;
+      glds16(src, base + XT + (i * 4 + wid) * 1024);
+    }
+  };
+
+  // per-lane window slots: logical K row (pixel) -> physical LDS row for tap s
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  int soff[2][2][3], sxr[2][2][3];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = kk * 32 + h * 16 + 4 * g + q;
+      const int ow = row & (W - 1);
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int iw = ow + s - 1;
+        const int slot = ((unsigned)iw < (unsigned)W) ? row + s - 1 : 64;
+        soff[kk][h][s] = slot * 128 + ((4 * p & 7) << 1);
+        sxr[kk][h][s] = ((slot >> 1) & 3) << 1;
+      }
+    }
+
+  f32x4 acc[6][NT];
+#pragma unroll
+  for (int m = 0; m < 6; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < nsteps) issue(i, i);
+  int stage = 0;
+  for (int st = 0; st < nsteps; ++st) {
+    wait_ahead<2 + LD, NS - 2>(min(NS - 2, nsteps - 1 - st));
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (st + NS - 1 < nsteps) issue(st + NS - 1, stage == 0 ? NS - 1 : stage - 1);
+    const unsigned char* X = smem + stage * STAGE;
+    const unsigned char* D = X + XT;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int row0 = kk * 32 + 4 * g + q, row1 = row0 + 16;
+      bf16x8 fa[6], fb[NT];
+#pragma unroll
+      for (int m = 0; m < 6; ++m) {
+        const int s = m >> 1;
+        const int cc = ((wm * 32 + (m & 1) * 16) >> 3) + (p >> 1);  // 16-byte chunk of the channel
+        const s16x4 lo = tr_read2(X, soff[kk][0][s] + ((cc ^ sxr[kk][0][s]) << 4));
+        const s16x4 hi = tr_read2(X, soff[kk][1][s] + ((cc ^ sxr[kk][1][s]) << 4));
+        fa[m] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const int col = wn * (BC / 2) + n * 16 + 4 * p;
+        const s16x4 lo = tr_read2(D, pm2<DROWB>(row0, col >> 3) + ((col & 7) << 1));
+        const s16x4 hi = tr_read2(D, pm2<DROWB>(row1, col >> 3) + ((col & 7) << 1));
+        fb[n] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int m = 0; m < 6; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
+    }
+    stage = stage == NS - 1 ? 0 : stage + 1;
+  }
+
+  float* part = a.part + (size_t)split * a.OC * a.Kg;
+#pragma unroll
+  for (int m = 0; m < 6; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const int k = (r * 3 + (m >> 1)) * a.IC + c0 + wm * 32 + (m & 1) * 16 + 4 * (lane >> 4);
+      const int oc = oc0 + wn * (BC / 2) + n * 16 + (lane & 15);
+      *reinterpret_cast<f32x4*>(part + (size_t)oc * a.Kg + k) = acc[m][n];
+    }
+}
+
 }  // namespace psx
 
 using namespace psx;
@@ -235,6 +400,45 @@ int launch_w2(const Wgrad2Args& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+constexpr int wlds3(int BC, int NS) { return NS * (65 * 128 + 64 * BC * 2); }
+
+// wgrad3 plan, same model as wplan with wgrad3's per-step costs.
+WPlan wplan3(int OC, int IC, int Kg, int npix) {
+  WPlan best{0, 64, 3, 1, 0};
+  double best_t = 1e30;
+  const int steps = npix / 64;
+  for (int cfg = 0; cfg < 4; ++cfg) {
+    const int BC = cfg & 1 ? 128 : 64, NS = cfg & 2 ? 6 : 3;
+    if (OC % BC) continue;
+    int occ = 163840 / wlds3(BC, NS);
+    if (occ > 3) occ = 3;
+    if (occ < 1) continue;
+    const int slots = 256 * occ;
+    const long tiles = 3L * (IC / 64) * (OC / BC);
+    const double step_us = (BC == 64 ? 0.9 : 1.3) * (NS == 6 ? 0.8 : 1.0);
+    const int smax = steps / 4 > 0 ? steps / 4 : 1;
+    for (int sp = 1; sp <= smax && sp <= 256; ++sp) {
+      const int sps = (steps + sp - 1) / sp;
+      const int spl = (steps + sps - 1) / sps;
+      const long wgs = tiles * spl;
+      const long rounds = (wgs + slots - 1) / slots;
+      const double t = rounds * (sps * step_us + 3.0) + (spl > 1 ? spl * (double)OC * Kg * 8.0 / 5e6 : 0.0);
+      if (t < best_t) {
+        best_t = t;
+        best = WPlan{0, BC, NS, spl, sps};
+      }
+    }
+  }
+  return best;
+}
+
+template <int BC, int NS>
+int launch_w3(const Wgrad3Args& a, hipStream_t st) {
+  hipLaunchKernelGGL((wgrad3_kernel<BC, NS>), dim3(3 * a.n_c_tiles * a.n_oc_tiles * a.splits), dim3(256),
+                     (size_t)wlds3(BC, NS), st, a);
+  return (int)hipGetLastError();
+}
+
 int ilog2w(int v) {
   int l = 0;
   while ((1 << l) < v) ++l;
@@ -262,6 +466,28 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
   a.div_ow = make_fastdiv(OW);
   a.div_s = make_fastdiv(S);
   if (OC % 64 || Kg % 64) return -2;
+  // 3x3 stride-1 layers with power-of-two rows: tap-reuse kernel (PSX_WG3=0 disables)
+  const char* w3env = getenv("PSX_WG3");
+  if (R == 3 && S == 3 && stride == 1 && pad == 1 && IC % 64 == 0 && (W & (W - 1)) == 0 && (H & (H - 1)) == 0 &&
+      W <= 64 && W >= 2 && a.npix % 64 == 0 && !(w3env && w3env[0] == '0')) {
+    WPlan p = wplan3(OC, IC, Kg, a.npix);
+    if (const char* e = getenv("PSX_WG_BC")) p.BC = atoi(e);
+    if (const char* e = getenv("PSX_WG_NS")) p.NS = atoi(e) >= 6 ? 6 : 3;
+    if (const char* e = getenv("PSX_WG_SPLITS")) {
+      const int steps = a.npix / 64;
+      p.sps = (steps + atoi(e) - 1) / atoi(e);
+      p.splits = (steps + p.sps - 1) / p.sps;
+    }
+    if (OC % p.BC) return -2;
+    if (!part) return p.splits;
+    Wgrad3Args b{};
+    b.x = a.x; b.dy = a.dy; b.part = part; b.zero = a.zero;
+    b.H = H; b.W = W; b.log2w = ilog2w(W); b.IC = IC; b.OC = OC; b.Kg = Kg; b.npix = a.npix;
+    b.n_c_tiles = IC / 64; b.n_oc_tiles = OC / p.BC; b.splits = p.splits; b.steps_per_split = p.sps;
+    const int e = p.BC == 128 ? (p.NS == 6 ? launch_w3<128, 6>(b, st) : launch_w3<128, 3>(b, st))
+                              : (p.NS == 6 ? launch_w3<64, 6>(b, st) : launch_w3<64, 3>(b, st));
+    return e ? -e : p.splits;
+  }
   WPlan p = wplan(OC, Kg, a.npix);
   // experiment overrides (tile sweep): PSX_WG_BR / PSX_WG_BC / PSX_WG_SPLITS
   if (const char* e = getenv("PSX_WG_BR")) p.BR = atoi(e);

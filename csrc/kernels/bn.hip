@@ -9,6 +9,8 @@
 // ([T][2][C]); bn_finalize reduces them (fp64, fixed order => deterministic), produces the
 // per-channel affine (scale, shift) and updates the running stats. Every elementwise pass is
 // vectorised at 16 B per lane (8 channels).
+#include <stdlib.h>
+
 #include "bnfin.hpp"
 #include "common.hpp"
 
@@ -279,9 +281,167 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
   }
 }
 
+// Opt-in (PSX_BNFIN_APPLY=1) variant of bn_apply_kernel with the training-mode finalize folded in:
+// every workgroup computes the affine(s) from the stat slots (bnfin.hpp bn_fin_lds). Separate
+// kernels so the default path keeps its exact code (an A/B showed +38 us/step otherwise).
+template <int MODE, bool RELU, bool FIN = true>
+__global__ __launch_bounds__(256) void bn_apply_fin_kernel(const uint16_t* __restrict__ y, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const uint16_t* __restrict__ res,
+                                                       const float* __restrict__ scale2,
+                                                       const float* __restrict__ shift2, uint16_t* __restrict__ out,
+                                                       size_t nvec, int C, const float* __restrict__ part1,
+                                                       const float* __restrict__ part2, BnFin f1, BnFin f2) {
+  extern __shared__ __attribute__((aligned(16))) float sbn[];  // FIN: [scale1|shift1|scale2|shift2] x C, red, scratch
+  if constexpr (FIN) {
+    double* red = reinterpret_cast<double*>(sbn + 4 * C);
+    float* scratch = sbn + 8 * C;
+    bn_fin_lds<PSX_STAT_SLOTS>(part1, f1, sbn, sbn + C, red, scratch);
+    if constexpr (MODE == 2) {
+      __syncthreads();
+      bn_fin_lds<PSX_STAT_SLOTS>(part2, f2, sbn + 2 * C, sbn + 3 * C, red, scratch);
+    }
+    __syncthreads();
+  }
+  auto SC = [&](int c) -> float { if constexpr (FIN) return sbn[c]; else return scale[c]; };
+  auto SH = [&](int c) -> float { if constexpr (FIN) return sbn[C + c]; else return shift[c]; };
+  auto SC2 = [&](int c) -> float { if constexpr (FIN) return sbn[2 * C + c]; else return scale2[c]; };
+  auto SH2 = [&](int c) -> float { if constexpr (FIN) return sbn[3 * C + c]; else return shift2[c]; };
+  const int cvec = C >> 3;
+  // a thread's channel group is fixed when the grid stride is a multiple of C/8: keep its 8
+  // channels' parameters in registers (scalar per-element reads of LDS at an 8-float lane
+  // stride are 8-way bank conflicts)
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  // (global-memory parameters: re-read per iteration, L1 hits the compiler schedules with the
+  // data loads; hoisting them behind a first-iteration branch measured slower)
+  const bool fixed = FIN && stride % cvec == 0;
+  float k[4][8];
+  int cur = -1;
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      k[0][j] = SC(c0 + j);
+      k[1][j] = SH(c0 + j);
+      if (MODE == 2) {
+        k[2][j] = SC2(c0 + j);
+        k[3][j] = SH2(c0 + j);
+      }
+    }
+    cur = c0;
+  };
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += stride) {
+    const int c0 = (int)(i % cvec) << 3;
+    if (!fixed || cur < 0) load(c0);
+    const u32x4 v = reinterpret_cast<const u32x4*>(y)[i];
+    u32x4 rv = {0u, 0u, 0u, 0u};
+    if (MODE != 0) rv = reinterpret_cast<const u32x4*>(res)[i];
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float a0 = lo_bf(v[j]) * k[0][2 * j] + k[1][2 * j];
+      float a1 = hi_bf(v[j]) * k[0][2 * j + 1] + k[1][2 * j + 1];
+      if (MODE == 1) {
+        a0 += lo_bf(rv[j]);
+        a1 += hi_bf(rv[j]);
+      } else if (MODE == 2) {
+        a0 += lo_bf(rv[j]) * k[2][2 * j] + k[3][2 * j];
+        a1 += hi_bf(rv[j]) * k[2][2 * j + 1] + k[3][2 * j + 1];
+      }
+      if (RELU) {
+        a0 = fmaxf(a0, 0.f);
+        a1 = fmaxf(a1, 0.f);
+      }
+      o[j] = pack_bf2(a0, a1);
+    }
+    reinterpret_cast<u32x4*>(out)[i] = o;
+  }
+}
+
+// Opt-in variant of bn_bwd_apply_kernel: coefficients from the slot sums part [T][NS][C] per
+// workgroup (bnfin.hpp bn_bwd_fin_lds).
+template <bool MASK, bool TWO, bool DZOUT, bool FIN = true>
+__global__ __launch_bounds__(256) void bn_bwd_apply_fin_kernel(const uint16_t* __restrict__ g,
+                                                           const uint16_t* __restrict__ o,
+                                                           const uint16_t* __restrict__ y1,
+                                                           const float* __restrict__ coef1,
+                                                           uint16_t* __restrict__ dx1,
+                                                           const uint16_t* __restrict__ y2,
+                                                           const float* __restrict__ coef2,
+                                                           uint16_t* __restrict__ dx2, uint16_t* __restrict__ dzout,
+                                                           size_t nvec, int C, const float* __restrict__ part,
+                                                           BnBwdFin f1, BnBwdFin f2) {
+  extern __shared__ __attribute__((aligned(16))) float sbn[];  // FIN: coef1 [3][C] | coef2 [3][C] | red | scratch
+  if constexpr (FIN) {
+    constexpr int NS = TWO ? 3 : 2;
+    double* red = reinterpret_cast<double*>(sbn + 6 * C);
+    float* scratch = sbn + 10 * C;
+    bn_bwd_fin_lds<PSX_STAT_SLOTS>(part, NS, 1, f1, sbn, red, scratch);
+    if constexpr (TWO) {
+      __syncthreads();
+      bn_bwd_fin_lds<PSX_STAT_SLOTS>(part, NS, 2, f2, sbn + 3 * C, red, scratch);
+    }
+    __syncthreads();
+  }
+  auto K1 = [&](int c) -> float { if constexpr (FIN) return sbn[c]; else return coef1[c]; };
+  auto K2 = [&](int c) -> float { if constexpr (FIN) return sbn[3 * C + c]; else return coef2[c]; };
+  const int cvec = C >> 3;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const bool fixed = FIN && stride % cvec == 0;  // see bn_apply_kernel
+  float k1[3][8], k2[3][8];
+  int cur = -1;
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        k1[r][j] = K1(r * C + c0 + j);
+        if (TWO) k2[r][j] = K2(r * C + c0 + j);
+      }
+    cur = c0;
+  };
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += stride) {
+    const int c0 = (int)(i % cvec) << 3;
+    if (!fixed || cur < 0) load(c0);
+    const u32x4 gv = reinterpret_cast<const u32x4*>(g)[i];
+    u32x4 ov = {0u, 0u, 0u, 0u};
+    if (MASK) ov = reinterpret_cast<const u32x4*>(o)[i];
+    const u32x4 yv = reinterpret_cast<const u32x4*>(y1)[i];
+    u32x4 y2v = {0u, 0u, 0u, 0u};
+    if (TWO) y2v = reinterpret_cast<const u32x4*>(y2)[i];
+    u32x4 r1, r2, rz;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e0 = 2 * j, e1 = 2 * j + 1;
+      float d0 = lo_bf(gv[j]), d1 = hi_bf(gv[j]);
+      if (MASK) {
+        if (!(lo_bf(ov[j]) > 0.f)) d0 = 0.f;
+        if (!(hi_bf(ov[j]) > 0.f)) d1 = 0.f;
+      }
+      r1[j] = pack_bf2(k1[0][e0] * d0 + k1[1][e0] * lo_bf(yv[j]) + k1[2][e0],
+                       k1[0][e1] * d1 + k1[1][e1] * hi_bf(yv[j]) + k1[2][e1]);
+      if (TWO)
+        r2[j] = pack_bf2(k2[0][e0] * d0 + k2[1][e0] * lo_bf(y2v[j]) + k2[2][e0],
+                         k2[0][e1] * d1 + k2[1][e1] * hi_bf(y2v[j]) + k2[2][e1]);
+      if (DZOUT) rz[j] = pack_bf2(d0, d1);
+    }
+    reinterpret_cast<u32x4*>(dx1)[i] = r1;
+    if (TWO) reinterpret_cast<u32x4*>(dx2)[i] = r2;
+    if (DZOUT) reinterpret_cast<u32x4*>(dzout)[i] = rz;
+  }
+}
+
 }  // namespace psx
 
 using namespace psx;
+
+// workgroup cap of the folded-finalize apply launches (each workgroup recomputes the affine)
+static int fin_grid_cap() {
+  static int cap = [] {
+    const char* e = getenv("PSX_FIN_GRID");
+    return e ? atoi(e) : 2048;
+  }();
+  return cap;
+}
 
 static int ew_grid(size_t nvec) {
   size_t g = (nvec + 255) / 256;
@@ -389,6 +549,64 @@ int psx_bn_bwd_apply(const void* g, const void* o, const void* y1, const float* 
   else if (dz) PSX_BBA(false, false, true);
   else PSX_BBA(false, false, false);
 #undef PSX_BBA
+  return (int)hipGetLastError();
+}
+
+// Training-mode apply with the finalize folded in: part1/part2 = [PSX_STAT_SLOTS][2][C] slot
+// sums of the layer (and of the shortcut BN for mode 2); fin1/fin2 name the side outputs.
+int psx_bn_apply_fin(const void* y, const float* part1, const BnFin* fin1, const void* res, const float* part2,
+                     const BnFin* fin2, void* out, long nelem, int C, int mode, int relu, hipStream_t st) {
+  if (!fin1) return -10;
+  if (C % 8 || nelem % 8) return -2;
+  if (fin1->C != C || (mode == 2 && (!fin2 || fin2->C != C))) return -10;
+  const size_t nvec = (size_t)nelem / 8;
+  int grid = ew_grid(nvec);
+  if (grid > fin_grid_cap()) grid = fin_grid_cap();
+  const size_t lds = (size_t)(8 * C + 1024) * sizeof(float);  // affines, red [2][C] f64, scratch
+  const BnFin f1 = *fin1;
+  const BnFin f2 = fin2 ? *fin2 : BnFin{};
+#define PSX_BNAF(M, R)                                                                                      \
+  hipLaunchKernelGGL((bn_apply_fin_kernel<M, R>), dim3(grid), dim3(256), lds, st, (const uint16_t*)y, nullptr, \
+                     nullptr, (const uint16_t*)res, nullptr, nullptr, (uint16_t*)out, nvec, C, part1, part2, f1, f2)
+  if (mode == 0 && relu) PSX_BNAF(0, true);
+  else if (mode == 0) PSX_BNAF(0, false);
+  else if (mode == 1 && relu) PSX_BNAF(1, true);
+  else if (mode == 1) PSX_BNAF(1, false);
+  else if (mode == 2 && relu) PSX_BNAF(2, true);
+  else if (mode == 2) PSX_BNAF(2, false);
+  else return -3;
+#undef PSX_BNAF
+  return (int)hipGetLastError();
+}
+
+// Backward apply with the finalize folded in: part = [PSX_STAT_SLOTS][NS][C] slot sums
+// (NS = 3 with y2); fin1/fin2 name the coefficient and dgamma/dbeta outputs.
+int psx_bn_bwd_apply_fin(const void* g, const void* o, const void* y1, const float* part, const BnBwdFin* fin1,
+                         void* dx1, const void* y2, const BnBwdFin* fin2, void* dx2, void* dzout, long nelem, int C,
+                         hipStream_t st) {
+  if (!fin1) return -10;
+  if (C % 8 || nelem % 8) return -2;
+  const bool mask = o != nullptr, two = y2 != nullptr, dz = dzout != nullptr;
+  if (fin1->C != C || (two && (!fin2 || fin2->C != C))) return -10;
+  const size_t nvec = (size_t)nelem / 8;
+  int grid = ew_grid(nvec);
+  if (grid > fin_grid_cap()) grid = fin_grid_cap();
+  const size_t lds = (size_t)(10 * C + 1024) * sizeof(float);  // coefs, red [2][C] f64, scratch
+  const BnBwdFin f1 = *fin1;
+  const BnBwdFin f2 = fin2 ? *fin2 : BnBwdFin{};
+#define PSX_BBAF(M, TW, DZ)                                                                                         \
+  hipLaunchKernelGGL((bn_bwd_apply_fin_kernel<M, TW, DZ>), dim3(grid), dim3(256), lds, st, (const uint16_t*)g,     \
+                     (const uint16_t*)o, (const uint16_t*)y1, nullptr, (uint16_t*)dx1, (const uint16_t*)y2, nullptr, \
+                     (uint16_t*)dx2, (uint16_t*)dzout, nvec, C, part, f1, f2)
+  if (mask && two && dz) PSX_BBAF(true, true, true);
+  else if (mask && two) PSX_BBAF(true, true, false);
+  else if (mask && dz) PSX_BBAF(true, false, true);
+  else if (mask) PSX_BBAF(true, false, false);
+  else if (two && dz) PSX_BBAF(false, true, true);
+  else if (two) PSX_BBAF(false, true, false);
+  else if (dz) PSX_BBAF(false, false, true);
+  else PSX_BBAF(false, false, false);
+#undef PSX_BBAF
   return (int)hipGetLastError();
 }
 

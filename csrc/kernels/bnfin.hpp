@@ -133,4 +133,124 @@ PSX_DEV void bn_bwd_finalize_block(const float* part, int NS, int which, const B
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Consumer-side finalize: every workgroup of the BN-apply launch that consumes a layer's slot
+// sums recomputes the per-channel affine (forward) or coefficients (backward) into LDS, and
+// workgroup 0 also writes the global side outputs (affine, saved statistics, running
+// statistics / coefficients, dgamma and dbeta on the gradient wire). This replaces one
+// finalize launch per BN layer (~4-5 us of dispatch and drain each, 40 per ResNet-18 step)
+// with 2*T*C redundant slot loads per workgroup: L2 hits after the first reader on each XCD.
+// The producer is a previous launch, so no fence is needed. tpc threads share a channel
+// (adjacent lanes, combined with shuffles) so 256 threads cover small C in one pass.
+// Slot reduction of two stat rows (ra, rb of NS per slot) for all C channels into LDS red[2][C]
+// (double sums, as bn_finalize_kernel). Thread = (float4 column of 4 channels, slot
+// group g of G); all of a thread's 16-byte loads are independent, so the whole reduction costs
+// about one memory round trip. LDS scratch: 8 * 256 floats (caller's sbn tail).
+template <int T>
+PSX_DEV void slot_reduce2(const float* part, int NS, int ra, int rb, int C, double* red, float* scratch) {
+  const int C4 = C >> 2;
+  for (int cb = 0; cb < C4; cb += 256) {
+    const int ncol = min(256, C4 - cb);
+    const int G = max(1, min(T, 256 / ncol));
+    const int col = threadIdx.x % ncol, g = threadIdx.x / ncol;
+    double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+    if (g < G) {
+      const float4* pa = reinterpret_cast<const float4*>(part + (size_t)ra * C) + cb + col;
+      const float4* pb = reinterpret_cast<const float4*>(part + (size_t)rb * C) + cb + col;
+      const size_t st4 = (size_t)NS * C / 4;
+#pragma unroll 8
+      for (int t = g; t < T; t += G) {
+        const float4 va = pa[t * st4], vb = pb[t * st4];
+        a[0] += va.x; a[1] += va.y; a[2] += va.z; a[3] += va.w;
+        b[0] += vb.x; b[1] += vb.y; b[2] += vb.z; b[3] += vb.w;
+      }
+    }
+    // combine the G slot groups of each column through LDS (G = 1: direct)
+    if (G == 1) {
+      if (g == 0)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          red[(cb + col) * 4 + k] = a[k];
+          red[C + (cb + col) * 4 + k] = b[k];
+        }
+    } else {
+      double* sd = reinterpret_cast<double*>(scratch);  // [256][2] doubles per component pass
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        __syncthreads();
+        sd[threadIdx.x * 2 + 0] = a[k];
+        sd[threadIdx.x * 2 + 1] = b[k];
+        __syncthreads();
+        if (threadIdx.x < ncol) {
+          double sa = 0.0, sb = 0.0;
+          for (int q = 0; q < G; ++q) {
+            sa += sd[(q * ncol + threadIdx.x) * 2 + 0];
+            sb += sd[(q * ncol + threadIdx.x) * 2 + 1];
+          }
+          red[(cb + threadIdx.x) * 4 + k] = sa;
+          red[C + (cb + threadIdx.x) * 4 + k] = sb;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// sc/sh: LDS [C]; red: LDS [2][C] doubles; scratch: LDS 512 doubles.
+template <int T>
+PSX_DEV void bn_fin_lds(const float* part, const BnFin& f, float* sc, float* sh, double* red, float* scratch) {
+  slot_reduce2<T>(part, 2, 0, 1, f.C, red, scratch);
+  for (int c = threadIdx.x; c < f.C; c += 256) {
+    const double s = red[c], ss = red[f.C + c];
+    const double mean = s / f.count;
+    double var = ss / f.count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+    const float scv = f.gamma[c] * invstd, shv = f.beta[c] - (float)mean * scv;
+    sc[c] = scv;
+    sh[c] = shv;
+    if (blockIdx.x == 0) {
+      f.scale[c] = scv;
+      f.shift[c] = shv;
+      f.save_mean[c] = (float)mean;
+      f.save_invstd[c] = invstd;
+      if (f.run_mean) {
+        const double unb = f.count > 1.f ? var * f.count / (f.count - 1.0) : var;
+        f.run_mean[c] = (1.f - f.momentum) * f.run_mean[c] + f.momentum * (float)mean;
+        f.run_var[c] = (1.f - f.momentum) * f.run_var[c] + f.momentum * (float)unb;
+      }
+    }
+  }
+}
+
+// part: [T][NS][C] (row 0 = sum dz, row `which` = sum dz*xhat); coef (LDS): [3][C].
+template <int T>
+PSX_DEV void bn_bwd_fin_lds(const float* part, int NS, int which, const BnBwdFin& f, float* coef, double* red,
+                            float* scratch) {
+  slot_reduce2<T>(part, NS, 0, which, f.C, red, scratch);
+  const int C = f.C;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const double sdz = red[c], sxh = red[C + c];
+    const float mdz = (float)(sdz / f.count), mxh = (float)(sxh / f.count);
+    const float is = f.invstd[c], gm = f.gamma[c];
+    const float k1 = gm * is, k2 = -gm * is * is * mxh, k3 = -gm * is * mdz + gm * is * is * f.mean[c] * mxh;
+    coef[c] = k1;
+    coef[C + c] = k2;
+    coef[2 * C + c] = k3;
+    if (blockIdx.x == 0) {
+      f.coef[c] = k1;
+      f.coef[C + c] = k2;
+      f.coef[2 * C + c] = k3;
+      const float dg = (float)sxh * f.gscale, db = (float)sdz * f.gscale;
+      if (f.grad_fp16) {
+        reinterpret_cast<uint16_t*>(f.dgamma)[c] = __builtin_bit_cast(uint16_t, (_Float16)dg);
+        reinterpret_cast<uint16_t*>(f.dbeta)[c] = __builtin_bit_cast(uint16_t, (_Float16)db);
+      } else {
+        reinterpret_cast<float*>(f.dgamma)[c] = dg;
+        reinterpret_cast<float*>(f.dbeta)[c] = db;
+      }
+    }
+  }
+}
+
 }  // namespace psx

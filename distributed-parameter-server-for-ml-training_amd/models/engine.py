@@ -179,6 +179,10 @@ class HipResNetEngine:
         self.fuse_fin = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNFIN", "0") == "1"
         # BN-backward sums from the dgrad epilogue: measured neutral (2.215 vs 2.217 ms/step; the MFMA
         # output layout makes its extra o/y loads half-coalesced), so opt-in
+        # BN finalize folded into the consuming apply launches (bnfin.hpp bn_fin_lds). Opt-in:
+        # measured 2.18 vs 2.10 ms/step (every apply workgroup pays the slot-reduction latency,
+        # more than the finalize launch it removes); see profiles/README.md
+        self.fin_apply = not self.fuse_fin and os.environ.get("PSX_BNFIN_APPLY", "0") == "1"
         self.fuse_bnbwd = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNBWD", "0") == "1"
         self._prereduced = set()
         self.wg_stream = (torch.cuda.Stream(device=self.dev)
@@ -373,8 +377,27 @@ class HipResNetEngine:
                        K.pick_tile(cs.cout, npix))
         if not train:
             self._bn_eval(bs, arena)
-        elif fin is None:
+        elif fin is None and not self._fold:
             self._bn_train(bs, arena, self.nslots, npix)
+
+    @property
+    def _fold(self) -> bool:
+        return self.fin_apply and not self.fuse_fin
+
+    def _apply(self, bs: BNSpec, y, out, arena, train: bool, res=None, bs2: BNSpec | None = None):
+        """BN (+ residual, + shortcut BN bs2 on res) + ReLU; with fin_apply the training-mode
+        finalize of bs (and bs2) runs inside this launch."""
+        c = bs.c
+        if train and self._fold:
+            npix = y.numel() // c
+            if bs2 is not None:
+                K.bn_apply_fin(y, self._red(bs, "fwd"), self._fin_fwd(bs, arena, npix), out, c, relu=True, res=res,
+                               part2=self._red(bs2, "fwd"), fin2=self._fin_fwd(bs2, arena, npix))
+            else:
+                K.bn_apply_fin(y, self._red(bs, "fwd"), self._fin_fwd(bs, arena, npix), out, c, relu=True, res=res)
+            return
+        K.bn_apply(y, self.bn[bs.name]["affine"], out, c, relu=True, res=res,
+                   affine2=self.bn[bs2.name]["affine"] if bs2 is not None else None)
 
     def _bn_train(self, bs: BNSpec, arena, T, count):
         st = self.bn[bs.name]
@@ -458,6 +481,18 @@ class HipResNetEngine:
         self._prereduced.discard(bs.name)
         if pre:
             fuse = False
+        if self._fold and not fuse:  # finalize inside the apply launch
+            if two is None:
+                if not pre:
+                    K.bn_bwd_reduce(g, o, y, st["saved"], part, npix, bs.c)
+                K.bn_bwd_apply_fin(g, o, y, part, self._fin_bwd(bs, arena, npix), dx, bs.c, dzout=dzout)
+            else:
+                bs2, y2, dx2 = two
+                if not pre:
+                    K.bn_bwd_reduce(g, o, y, st["saved"], part, npix, bs.c, y2=y2, saved2=self.bn[bs2.name]["saved"])
+                K.bn_bwd_apply_fin(g, o, y, part, self._fin_bwd(bs, arena, npix), dx, bs.c, y2=y2,
+                                   fin2=self._fin_bwd(bs2, arena, npix), dx2=dx2, dzout=dzout)
+            return
         if two is None:
             T = self.nslots if pre else K.bn_bwd_reduce(g, o, y, st["saved"], part, npix, bs.c,
                                                         fin1=self._fin_bwd(bs, arena, npix) if fuse else None)
@@ -499,7 +534,7 @@ class HipResNetEngine:
         if train:
             self.red.zero_()
         self._conv_bn_fwd(st, self.x0, self.y0, sp.stem_bn, arena, train)
-        K.bn_apply(self.y0, self.bn[sp.stem_bn.name]["affine"], self.a0, st.cout, relu=True)
+        self._apply(sp.stem_bn, self.y0, self.a0, arena, train)
         if sp.maxpool:
             K.maxpool3s2_fwd(self.a0, self.p0, self.pidx)
         for b, d in zip(sp.blocks, self.blk):
@@ -508,17 +543,14 @@ class HipResNetEngine:
             for i, cs in enumerate(b.convs):
                 self._conv_bn_fwd(cs, src, d["y"][i], b.bns[i], arena, train)
                 if i < L - 1:
-                    K.bn_apply(d["y"][i], self.bn[b.bns[i].name]["affine"], d["a"][i], cs.cout, relu=True)
+                    self._apply(b.bns[i], d["y"][i], d["a"][i], arena, train)
                     src = d["a"][i]
-            last = b.convs[-1]
-            aff = self.bn[b.bns[-1].name]["affine"]
             if b.down:
                 ds, dbn = b.down
                 self._conv_bn_fwd(ds, d["inp"], d["ys"], dbn, arena, train)
-                K.bn_apply(d["y"][-1], aff, d["out"], last.cout, relu=True, res=d["ys"],
-                           affine2=self.bn[dbn.name]["affine"])
+                self._apply(b.bns[-1], d["y"][-1], d["out"], arena, train, res=d["ys"], bs2=dbn)
             else:
-                K.bn_apply(d["y"][-1], aff, d["out"], last.cout, relu=True, res=d["inp"])
+                self._apply(b.bns[-1], d["y"][-1], d["out"], arena, train, res=d["inp"])
         return self.final
 
     def head(self, arena: torch.Tensor, backward: bool = True):

@@ -55,6 +55,8 @@ _KERNEL_SIGS = {
     "psx_bn_bwd_reduce": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp, vp]),
     "psx_bn_bwd_finalize": (i32, [vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp, f32, i32, vp]),
     "psx_bn_bwd_apply": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
+    "psx_bn_apply_fin": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp]),
+    "psx_bn_bwd_apply_fin": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
     "psx_head_fwd_bwd": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp, vp, vp, vp, vp, vp]),
     "psx_head_wgrad": (i32, [vp, vp, i32, i32, i32, vp, vp, f32, i32, vp]),
     "psx_sgd_apply": (i32, [vp, vp, vp, i64, f32, f32, f32, f32, i32, i32, vp]),
@@ -103,8 +105,10 @@ _RUNTIME_SIGS = {
 }
 
 
-def _declare(lib, sigs):
+def _declare(lib, sigs, optional=False):
     for name, (res, args) in sigs.items():
+        if optional and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -135,7 +139,11 @@ def kernels():
             if _kern is None:
                 import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
-                _kern = _declare(C.CDLL(_maybe_build("libpsx_kernels.so"), mode=C.RTLD_GLOBAL), _KERNEL_SIGS)
+                alt = os.environ.get("PSX_KERNELS_LIB")  # dev A/B: another build of the kernel library
+                if alt:
+                    _kern = _declare(C.CDLL(os.path.abspath(alt), mode=C.RTLD_GLOBAL), _KERNEL_SIGS, optional=True)
+                else:
+                    _kern = _declare(C.CDLL(_maybe_build("libpsx_kernels.so"), mode=C.RTLD_GLOBAL), _KERNEL_SIGS)
     return _kern
 
 

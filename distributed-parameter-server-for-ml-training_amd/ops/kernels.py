@@ -186,6 +186,16 @@ def bn_apply(y, affine, out, c, relu=True, res=None, affine2=None):
                                  stream_ptr()), "bn_apply")
 
 
+def bn_apply_fin(y, part1, fin1: BnFin, out, c, relu=True, res=None, part2=None, fin2: BnFin | None = None):
+    """Training-mode bn_apply with the finalize folded in: every workgroup computes the affine
+    from the [STAT_SLOTS][2][C] slot sums (part1; part2/fin2 = the shortcut BN, mode 2) and
+    workgroup 0 writes fin1/fin2's side outputs (csrc/kernels/bnfin.hpp bn_fin_lds)."""
+    mode = 0 if res is None else (1 if part2 is None else 2)
+    check(kernels().psx_bn_apply_fin(ptr(y), ptr(part1), C.byref(fin1), ptr(res), ptr(part2),
+                                     C.byref(fin2) if fin2 is not None else None, ptr(out), y.numel(), c, mode,
+                                     int(relu), stream_ptr()), "bn_apply_fin")
+
+
 def bn_bwd_reduce_T(npix: int, c: int) -> int:
     return kernels().psx_bn_bwd_reduce(None, None, None, None, None, None, None, None, None, npix, c, None, None,
                                        None)
@@ -214,6 +224,15 @@ def bn_bwd_finalize(part, T, ns, which, c, count, gamma, saved, coef, dgamma_ptr
 def bn_bwd_apply(g, o, y1, coef1, dx1, c, y2=None, coef2=None, dx2=None, dzout=None):
     check(kernels().psx_bn_bwd_apply(ptr(g), ptr(o), ptr(y1), ptr(coef1), ptr(dx1), ptr(y2), ptr(coef2), ptr(dx2),
                                      ptr(dzout), g.numel(), c, stream_ptr()), "bn_bwd_apply")
+
+
+def bn_bwd_apply_fin(g, o, y1, part, fin1: BnBwdFin, dx1, c, y2=None, fin2: BnBwdFin | None = None, dx2=None,
+                     dzout=None):
+    """bn_bwd_apply with the backward finalize folded in (coefficients from the
+    [STAT_SLOTS][NS][C] slot sums per workgroup; workgroup 0 writes coef and dgamma/dbeta)."""
+    check(kernels().psx_bn_bwd_apply_fin(ptr(g), ptr(o), ptr(y1), ptr(part), C.byref(fin1), ptr(dx1), ptr(y2),
+                                         C.byref(fin2) if fin2 is not None else None, ptr(dx2), ptr(dzout),
+                                         g.numel(), c, stream_ptr()), "bn_bwd_apply_fin")
 
 
 def head_fwd_bwd(act, b, hw, c, fcw, fcb, k, labels, pooled, dlogits, dact, loss, correct):

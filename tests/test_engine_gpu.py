@@ -106,19 +106,28 @@ def test_graph_replay_matches_eager(setup):
     assert _cos(eng.grads[fc:].float(), eager[fc:].float()) > 0.9999
 
 
-def test_fused_bn_finalize_matches_separate_kernels(setup):
-    """In-launch BN finalize (bnfin.hpp, last-workgroup hand-off) gives exactly what the
-    separate finalize kernels compute from the same slot sums (checked on every BN layer, for
-    two consecutive steps so the per-step counter re-arm is exercised too)."""
+@pytest.mark.parametrize("mode", ["conv_epilogue", "apply", "apply_bnbwd"])
+def test_fused_bn_finalize_matches_separate_kernels(setup, mode):
+    """Folded BN finalize gives exactly what the separate finalize kernels compute from the same
+    slot sums (every BN layer, two consecutive steps). conv_epilogue: last workgroup of the
+    producing launch (PSX_FUSE_BNFIN); apply (default): every workgroup of the consuming apply
+    launch (bnfin.hpp bn_fin_lds), with the backward sums from bn_bwd_reduce or from the dgrad
+    epilogue (apply_bnbwd). Also: running statistics updated exactly once per step, and the
+    block-internal apply outputs equal bn_apply with the recomputed affine.
+    (Whole-step gradients are not compared across paths: at random init two runs of the SAME
+    path already differ by ~20% through the atomic-order noise in the statistics.)"""
     model, layout, arena, eng, x, y = setup
     n = 256
     imgs = torch.randint(0, 256, (n, 32, 32, 3), dtype=torch.uint8, device=DEV)
     labs = torch.randint(0, 100, (n,), dtype=torch.int32, device=DEV)
     eng.index.copy_(torch.arange(eng.B, dtype=torch.int32, device=DEV))
-    fused_before, bnbwd_before = eng.fuse_fin, eng.fuse_bnbwd
-    eng.fuse_fin, eng.fuse_bnbwd = True, False
+    before = (eng.fin_apply, eng.fuse_fin, eng.fuse_bnbwd)
+    eng.fin_apply = mode != "conv_epilogue"
+    eng.fuse_fin = mode == "conv_epilogue"
+    eng.fuse_bnbwd = mode == "apply_bnbwd"
     a = arena.clone()
     for step in range(2):
+        prev = a.clone()
         eng.train_step(a, imgs, labs)
         torch.cuda.synchronize()
         bns = [eng.spec.stem_bn] + [bn for b in eng.spec.blocks for bn in b.bns + ([b.down[1]] if b.down else [])]
@@ -141,12 +150,26 @@ def test_fused_bn_finalize_matches_separate_kernels(setup):
             K.bn_bwd_finalize(part, K.STAT_SLOTS, ns, which, c, bf.count, layout.view(a, f"{bs.name}.weight"),
                               st["saved"], coef, dg.data_ptr(), db.data_ptr(), 1.0, False)
             torch.cuda.synchronize()
-            assert torch.allclose(aff, st["affine"], rtol=1e-6, atol=1e-7), (step, bs.name)
-            assert torch.allclose(sav, st["saved"], rtol=1e-6, atol=1e-7), (step, bs.name)
-            assert torch.allclose(coef, st["coef"], rtol=1e-5, atol=1e-6), (step, bs.name)
+            assert torch.allclose(aff, st["affine"], rtol=1e-6, atol=1e-7), (mode, step, bs.name)
+            assert torch.allclose(sav, st["saved"], rtol=1e-6, atol=1e-7), (mode, step, bs.name)
+            assert torch.allclose(coef, st["coef"], rtol=1e-5, atol=1e-6), (mode, step, bs.name)
             gw = layout.grad_view(eng.grads, f"{bs.name}.weight").float()
-            assert torch.allclose(dg, gw, rtol=1e-5, atol=1e-6), (step, bs.name)
-    eng.fuse_fin, eng.fuse_bnbwd = fused_before, bnbwd_before
+            gb = layout.grad_view(eng.grads, f"{bs.name}.bias").float()
+            assert torch.allclose(dg, gw, rtol=1e-5, atol=1e-6), (mode, step, bs.name)
+            assert torch.allclose(db, gb, rtol=1e-5, atol=1e-6), (mode, step, bs.name)
+            # running statistics: exactly one momentum update from this step's batch mean
+            m = eng.mom
+            rm_want = (1 - m) * layout.view(prev, f"{bs.name}.running_mean") + m * sav[0]
+            assert torch.allclose(layout.view(a, f"{bs.name}.running_mean"), rm_want, rtol=1e-5, atol=1e-6), \
+                (mode, step, bs.name)
+        for b, d in zip(eng.spec.blocks, eng.blk):  # in-block applies (BN + ReLU)
+            for i in range(len(b.convs) - 1):
+                bs = b.bns[i]
+                want = torch.empty_like(d["a"][i])
+                K.bn_apply(d["y"][i], eng.bn[bs.name]["affine"], want, bs.c, relu=True)
+                torch.cuda.synchronize()
+                assert torch.equal(want, d["a"][i]), (mode, step, bs.name)
+    eng.fin_apply, eng.fuse_fin, eng.fuse_bnbwd = before
 
 
 def test_dgrad_fused_bn_backward_sums_match_reduce_kernel(setup):

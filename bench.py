@@ -30,10 +30,11 @@ import torch.distributed as dist  # noqa: E402
 
 import psx  # noqa: E402,F401
 from psx.parallel.compute import HipCompute  # noqa: E402
-from psx.parallel.runner import AsyncSession, build_state, make_datasets, make_sync_channel  # noqa: E402
+from psx.parallel.runner import (AsyncSession, build_state, make_datasets, make_local_channel,  # noqa: E402
+                                 make_sync_channel)
 from psx.parallel.server import ParameterServer  # noqa: E402
 from psx.parallel.transport import DistTransport, env_world  # noqa: E402
-from psx.parallel.worker import InProcessChannel, Worker  # noqa: E402
+from psx.parallel.worker import Worker  # noqa: E402
 from psx.utils.config import PSConfig  # noqa: E402
 
 BASELINE_SYNC_IMG_S = 82.7  # sync PS, 4 workers, measured (experiment_results/sync_4workers.json)
@@ -107,7 +108,8 @@ def main():
         sess = AsyncSession(cfg, t, rank, worker_ranks, server, comp, train, None, names, quiet)
         wk = sess.worker
     else:
-        chan = InProcessChannel(server) if t is None else make_sync_channel(cfg, t, server, W, layout, device)
+        chan = (make_local_channel(cfg, server, layout, device) if t is None else
+                make_sync_channel(cfg, t, server, W, layout, device, worker=is_worker))
         if is_worker:
             wid = worker_ranks.index(rank)
             wk = Worker(cfg, comp, chan, train, None, worker_name=f"worker-{wid}", rank=rank, log=quiet,
@@ -201,6 +203,7 @@ def main():
                 "sync_steps": 1,
                 "codec": a.codec if a.codec != "topk" else f"topk({a.topk_ratio}) + error feedback",
                 "fetch_codec": a.fetch_codec if t is not None else "in-process",
+                "weight_image": getattr(chan, "image_wire", None) is not None,
                 "overlap": (f"bucketed reduce/apply/broadcast during backward ({len(chan.buckets)} buckets)"
                             if getattr(chan, "overlap", False) else "none"),
                 "topology": "dedicated" if dedicated else ("colocated" if t is not None else "loopback"),

@@ -17,10 +17,13 @@ namespace psx {
 PSX_DEV float ld_grad(const uint16_t* g, size_t i) { return (float)__builtin_bit_cast(_Float16, g[i]); }
 PSX_DEV float ld_grad(const float* g, size_t i) { return g[i]; }
 
+// img (optional): bf16 image of the updated parameters, written in the same pass — the fetch
+// wire / the workers' conv-operand source (parallel/codec.py), so no separate pack kernel.
 template <typename GT, bool MOM>
 __global__ __launch_bounds__(256) void sgd_apply_kernel(float* __restrict__ p, const GT* __restrict__ g,
                                                         float* __restrict__ buf, size_t n, float lr, float gscale,
-                                                        float momentum, float wd, int first) {
+                                                        float momentum, float wd, int first,
+                                                        uint16_t* __restrict__ img) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     float d = ld_grad(g, i) * gscale;
     const float pv = p[i];
@@ -30,13 +33,17 @@ __global__ __launch_bounds__(256) void sgd_apply_kernel(float* __restrict__ p, c
       buf[i] = v;
       d = v;
     }
-    p[i] = pv - lr * d;
+    const float nv = pv - lr * d;
+    p[i] = nv;
+    if (img) img[i] = f2bf(nv);
   }
 }
 
 // vectorised fp16-gradient fast path (no momentum): 8 elements per lane
+template <bool IMG>
 __global__ __launch_bounds__(256) void sgd_apply_h8_kernel(float* __restrict__ p, const uint16_t* __restrict__ g,
-                                                           size_t n8, float step, float wd_step) {
+                                                           size_t n8, float step, float wd_step,
+                                                           uint16_t* __restrict__ img) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
     const u32x4 gv = reinterpret_cast<const u32x4*>(g)[i];
     f32x4 p0 = reinterpret_cast<f32x4*>(p)[2 * i];
@@ -55,6 +62,11 @@ __global__ __launch_bounds__(256) void sgd_apply_h8_kernel(float* __restrict__ p
     }
     reinterpret_cast<f32x4*>(p)[2 * i] = p0;
     reinterpret_cast<f32x4*>(p)[2 * i + 1] = p1;
+    if (IMG) {
+      const u32x4 o = {pack_bf2(p0[0], p0[1]), pack_bf2(p0[2], p0[3]), pack_bf2(p1[0], p1[1]),
+                       pack_bf2(p1[2], p1[3])};
+      reinterpret_cast<u32x4*>(img)[i] = o;
+    }
   }
 }
 
@@ -91,8 +103,63 @@ struct UnpackDesc {
   long src_off;  // element offset of the OIHW fp32 weight in the arena
   long wf_off;   // element offset of the bf16 [OC][Kg] forward operand
   long wd_off;   // element offset of the bf16 [Cp][Kgd] dgrad operand, -1 if none
-  int OC, Cin, R, S, Cp, Kg, Kgd, pad_;
+  int OC, Cin, R, S, Cp, Kg, Kgd;
+  int tile0;     // first flat tile index of this conv (param_unpack_tiles_kernel grid)
 };
+
+PSX_DEV uint16_t to_bf(const float* s, size_t i) { return f2bf(s[i]); }
+PSX_DEV uint16_t to_bf(const uint16_t* s, size_t i) { return s[i]; }
+
+// Flat-grid unpack: one workgroup per (conv, 32 oc x 32 c tile), all taps of the tile staged in
+// LDS per chunk of <= 9 taps. For R*S <= 9 the source read of a tile row is one contiguous run
+// of 32*R*S elements of W[oc][c0:c0+32][:][:] (the per-tap kernel below strides by R*S). The
+// source is either the fp32 arena or the server's bf16 weight image (the bits sgd_apply wrote
+// next to the fp32 update, parallel/codec.py), so a worker never needs fp32 conv weights.
+template <typename ST>
+__global__ __launch_bounds__(256) void param_unpack_tiles_kernel(const ST* __restrict__ src_all,
+                                                                 const UnpackDesc* __restrict__ descs, int ndesc,
+                                                                 uint16_t* __restrict__ wbuf) {
+  constexpr int TC = 9;
+  __shared__ uint16_t tile[TC][32][34];
+  int j = 0;
+  while (j + 1 < ndesc && descs[j + 1].tile0 <= (int)blockIdx.x) ++j;
+  const UnpackDesc d = descs[j];
+  const int t = blockIdx.x - d.tile0;
+  const int n_c = (d.Cp + 31) / 32;
+  const int oc0 = (t / n_c) * 32, c0 = (t % n_c) * 32;
+  const int RS = d.R * d.S;
+  const ST* src = src_all + d.src_off;
+  const int nc_src = min(32, d.Cin - c0);  // real input channels in this tile (<= 0: all padding)
+  for (int tap0 = 0; tap0 < RS; tap0 += TC) {
+    const int nt = min(TC, RS - tap0);
+    if (tap0) __syncthreads();
+    // stage tile[tap][oc][c] = W[oc0+oc][c0+c][tap0+tap] (zeros outside OC x Cin)
+    const int per_oc = 32 * nt;
+    for (int e = threadIdx.x; e < 32 * per_oc; e += 256) {
+      const int oc = e / per_oc, r = e - oc * per_oc;
+      const int c = r / nt, tp = r - c * nt;
+      uint16_t v = 0;
+      if (oc0 + oc < d.OC && c < nc_src)
+        v = to_bf(src, ((size_t)(oc0 + oc) * d.Cin + (c0 + c)) * RS + tap0 + tp);
+      tile[tp][oc][c] = v;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 32 * nt * 32; e += 256) {  // wf[oc][tap*Cp + c]: c fastest
+      const int c = e & 31, rest = e >> 5;
+      const int tp = rest % nt, oc = rest / nt;
+      if (oc0 + oc < d.OC && c0 + c < d.Cp)
+        wbuf[d.wf_off + (size_t)(oc0 + oc) * d.Kg + (tap0 + tp) * d.Cp + c0 + c] = tile[tp][oc][c];
+    }
+    if (d.wd_off >= 0) {
+      for (int e = threadIdx.x; e < 32 * nt * 32; e += 256) {  // wd[c][tap*OC + oc]: oc fastest
+        const int oc = e & 31, rest = e >> 5;
+        const int tp = rest % nt, c = rest / nt;
+        if (oc0 + oc < d.OC && c0 + c < d.Cp)
+          wbuf[d.wd_off + (size_t)(c0 + c) * d.Kgd + (tap0 + tp) * d.OC + oc0 + oc] = tile[tp][oc][c];
+      }
+    }
+  }
+}
 
 // One workgroup per (32 oc x 32 c) tile of one conv (blockIdx.y = conv). For every tap the
 // tile goes through LDS so both destination layouts are written with contiguous runs:
@@ -151,29 +218,36 @@ static int grid_for(size_t n) {
 extern "C" {
 
 // p -= lr * (gscale*g + wd*p) [with momentum buffer]; grads fp16 (wire) or fp32.
+// img (optional, nullptr = none): bf16 image of the updated parameters (n elements).
 int psx_sgd_apply(float* p, const void* g, float* buf, long n, float lr, float gscale, float momentum, float wd,
-                  int first, int grad_fp16, hipStream_t st) {
+                  int first, int grad_fp16, void* img, hipStream_t st) {
   const bool mom = buf != nullptr && momentum != 0.f;
-  if (!mom && grad_fp16 && n % 8 == 0 && ((uintptr_t)p % 32 == 0) && ((uintptr_t)g % 16 == 0)) {
-    hipLaunchKernelGGL(sgd_apply_h8_kernel, dim3(grid_for(n / 8)), dim3(256), 0, st, p, (const uint16_t*)g,
-                       (size_t)n / 8, lr * gscale, lr * wd);
+  uint16_t* im = (uint16_t*)img;
+  if (!mom && grad_fp16 && n % 8 == 0 && ((uintptr_t)p % 32 == 0) && ((uintptr_t)g % 16 == 0) &&
+      ((uintptr_t)img % 16 == 0)) {
+    if (im)
+      hipLaunchKernelGGL(sgd_apply_h8_kernel<true>, dim3(grid_for(n / 8)), dim3(256), 0, st, p, (const uint16_t*)g,
+                         (size_t)n / 8, lr * gscale, lr * wd, im);
+    else
+      hipLaunchKernelGGL(sgd_apply_h8_kernel<false>, dim3(grid_for(n / 8)), dim3(256), 0, st, p, (const uint16_t*)g,
+                         (size_t)n / 8, lr * gscale, lr * wd, im);
     return (int)hipGetLastError();
   }
   const int grid = grid_for(n);
   if (grad_fp16) {
     if (mom)
       hipLaunchKernelGGL((sgd_apply_kernel<uint16_t, true>), dim3(grid), dim3(256), 0, st, p, (const uint16_t*)g, buf,
-                         (size_t)n, lr, gscale, momentum, wd, first);
+                         (size_t)n, lr, gscale, momentum, wd, first, im);
     else
       hipLaunchKernelGGL((sgd_apply_kernel<uint16_t, false>), dim3(grid), dim3(256), 0, st, p, (const uint16_t*)g,
-                         buf, (size_t)n, lr, gscale, momentum, wd, first);
+                         buf, (size_t)n, lr, gscale, momentum, wd, first, im);
   } else {
     if (mom)
       hipLaunchKernelGGL((sgd_apply_kernel<float, true>), dim3(grid), dim3(256), 0, st, p, (const float*)g, buf,
-                         (size_t)n, lr, gscale, momentum, wd, first);
+                         (size_t)n, lr, gscale, momentum, wd, first, im);
     else
       hipLaunchKernelGGL((sgd_apply_kernel<float, false>), dim3(grid), dim3(256), 0, st, p, (const float*)g, buf,
-                         (size_t)n, lr, gscale, momentum, wd, first);
+                         (size_t)n, lr, gscale, momentum, wd, first, im);
   }
   return (int)hipGetLastError();
 }
@@ -208,6 +282,20 @@ int psx_fp16_unpack(const void* src, float* dst, long n, float scale, hipStream_
 int psx_param_unpack(const float* arena, const void* descs, int ndesc, void* wbuf, hipStream_t st) {
   hipLaunchKernelGGL(param_unpack_kernel, dim3(64, ndesc), dim3(256), 0, st, arena, (const UnpackDesc*)descs,
                      (uint16_t*)wbuf);
+  return (int)hipGetLastError();
+}
+
+// Flat-grid unpack (one workgroup per 32x32 tile of every conv; ntiles = sum of the tiles, each
+// desc's tile0 = its first tile). src_bf16: the source is a bf16 image instead of the fp32 arena.
+int psx_param_unpack_tiles(const void* src, int src_bf16, const void* descs, int ndesc, int ntiles, void* wbuf,
+                           hipStream_t st) {
+  if (ntiles <= 0 || ndesc <= 0) return 0;
+  if (src_bf16)
+    hipLaunchKernelGGL(param_unpack_tiles_kernel<uint16_t>, dim3(ntiles), dim3(256), 0, st, (const uint16_t*)src,
+                       (const UnpackDesc*)descs, ndesc, (uint16_t*)wbuf);
+  else
+    hipLaunchKernelGGL(param_unpack_tiles_kernel<float>, dim3(ntiles), dim3(256), 0, st, (const float*)src,
+                       (const UnpackDesc*)descs, ndesc, (uint16_t*)wbuf);
   return (int)hipGetLastError();
 }
 

@@ -189,6 +189,10 @@ class HipResNetEngine:
                           if os.environ.get("PSX_WGRAD_STREAM", "0") == "1" else None)
         self._wg_batch = None
         self._fins = {}
+        # conv-operand unpack: "tiles" (flat grid, fp32 arena or bf16 image source) or "tap"
+        self.unpack_impl = os.environ.get("PSX_UNPACK_IMPL", "tiles")
+        self.wsrc = None        # bf16 weight image to unpack from (set_weight_source), None = arena
+        self.pre_unpack = None
         self._build()
 
     # ------------------------------------------------------------------ allocation
@@ -203,6 +207,7 @@ class HipResNetEngine:
         # weights: one bf16 buffer holding every conv's fwd (and dgrad) operand
         off = 0
         descs = []
+        tile0 = 0  # flat tile grid of param_unpack_tiles: 32x32 (oc, c) tiles of every conv
         for cs in all_convs(sp):
             cs.finalize()
             cs.wf_off = off
@@ -213,7 +218,9 @@ class HipResNetEngine:
             else:
                 cs.wd_off = -1
             descs.append((self.layout.offset(f"{cs.name}.weight"), cs.wf_off, cs.wd_off, cs.cout, cs.cin, cs.k, cs.k,
-                          cs.cp, cs.kg, cs.kgd, 0))
+                          cs.cp, cs.kg, cs.kgd, tile0))
+            tile0 += -(-cs.cout // 32) * -(-cs.cp // 32)
+        self.ntiles = tile0
         self.wbuf = torch.zeros(off, dtype=torch.bfloat16, device=self.dev)
         dsz = K.unpack_desc_size()
         assert dsz == 3 * 8 + 8 * 4, dsz
@@ -519,8 +526,26 @@ class HipResNetEngine:
 
     # ------------------------------------------------------------------ public API
     def unpack(self, arena: torch.Tensor):
-        """fp32 OIHW master weights (fetched arena) -> bf16 implicit-GEMM operands."""
-        K.param_unpack(arena, self.descs, self.ndesc, self.wbuf)
+        """OIHW master weights -> bf16 implicit-GEMM operands. The source is the fp32 arena, or
+        the bf16 weight image ``self.wsrc`` when the fetch delivers one (parallel/codec.py
+        WeightWire: the server's apply wrote those bits; identical operands either way)."""
+        if self.unpack_impl == "tap":  # the original per-tap kernel (A/B: PSX_UNPACK_IMPL=tap)
+            K.param_unpack(arena, self.descs, self.ndesc, self.wbuf)
+            return
+        src = self.wsrc if self.wsrc is not None else arena
+        K.param_unpack_tiles(src, self.descs, self.ndesc, self.ntiles, self.wbuf)
+
+    def set_weight_source(self, img: torch.Tensor | None, pre_unpack=None):
+        """Read conv weights from a bf16 image (same offsets as the arena's parameter prefix)
+        instead of the fp32 arena; ``pre_unpack`` runs first inside every captured step (the
+        WeightWire scatter of the fp32 remainder into the local arena). Invalidates graphs."""
+        if img is not None:
+            assert img.dtype == torch.bfloat16 and img.numel() >= self.layout.param_numel
+            assert self.unpack_impl != "tap", "the per-tap unpack kernel reads fp32 only"
+        self.wsrc = img
+        self.pre_unpack = pre_unpack
+        self.graph = None
+        self.graphs = None
 
     def load_batch(self, images_u8, labels_all, train=True):
         """Gather self.index rows of the HBM-resident dataset + fused crop/flip/normalize."""
@@ -660,6 +685,8 @@ class HipResNetEngine:
 
         def prologue():
             if unpack:
+                if self.pre_unpack is not None:
+                    self.pre_unpack()
                 self.unpack(arena)
             if images_u8 is not None:
                 self.load_batch(images_u8, labels_all, train=True)

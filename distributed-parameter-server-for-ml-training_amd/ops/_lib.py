@@ -59,11 +59,12 @@ _KERNEL_SIGS = {
     "psx_bn_bwd_apply_fin": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
     "psx_head_fwd_bwd": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp, vp, vp, vp, vp, vp]),
     "psx_head_wgrad": (i32, [vp, vp, i32, i32, i32, vp, vp, f32, i32, vp]),
-    "psx_sgd_apply": (i32, [vp, vp, vp, i64, f32, f32, f32, f32, i32, i32, vp]),
+    "psx_sgd_apply": (i32, [vp, vp, vp, i64, f32, f32, f32, f32, i32, i32, vp, vp]),
     "psx_grad_aggregate": (i32, [vp, i32, i32, vp, i32, i64, f32, i32, vp]),
     "psx_fp16_pack": (i32, [vp, vp, i64, f32, vp]),
     "psx_fp16_unpack": (i32, [vp, vp, i64, f32, vp]),
     "psx_param_unpack": (i32, [vp, vp, i32, vp, vp]),
+    "psx_param_unpack_tiles": (i32, [vp, i32, vp, i32, i32, vp, vp]),
     "psx_unpack_desc_size": (i32, []),
     "psx_synth_gen": (i32, [vp, vp, i32, i32, i32, i32, u32, u32, vp]),
     "psx_augment": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, u32, vp, i32, vp, vp, vp]),

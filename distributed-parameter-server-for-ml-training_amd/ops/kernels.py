@@ -245,11 +245,15 @@ def head_wgrad(dlogits, pooled, b, k, c, dw_ptr, db_ptr, gscale, grad_fp16):
                                    int(grad_fp16), stream_ptr()), "head_wgrad")
 
 
-def sgd_apply(p, g, lr, gscale=1.0, momentum=0.0, wd=0.0, buf=None, first=False, n=None):
+def sgd_apply(p, g, lr, gscale=1.0, momentum=0.0, wd=0.0, buf=None, first=False, n=None, img=None):
+    """p -= lr*(gscale*g + wd*p) [momentum]; ``img`` (bf16, >= n elements) also receives the
+    bf16 bits of the updated parameters in the same pass (fetch wire / weight image)."""
     n = p.numel() if n is None else n
     fp16 = g.dtype == torch.float16
+    if img is not None:
+        assert img.dtype == torch.bfloat16 and img.numel() >= n and img.device == p.device, "sgd_apply img"
     check(kernels().psx_sgd_apply(ptr(p), ptr(g), ptr(buf), n, float(lr), float(gscale), float(momentum), float(wd),
-                                  int(first), int(fp16), stream_ptr()), "sgd_apply")
+                                  int(first), int(fp16), ptr(img), stream_ptr()), "sgd_apply")
 
 
 def maxpool3s2_fwd(x, y, arg):
@@ -301,6 +305,14 @@ def fp16_unpack(src, dst, scale=1.0):
 
 def param_unpack(arena, descs_dev, ndesc, wbuf):
     check(kernels().psx_param_unpack(ptr(arena), ptr(descs_dev), ndesc, ptr(wbuf), stream_ptr()), "param_unpack")
+
+
+def param_unpack_tiles(src, descs_dev, ndesc, ntiles, wbuf):
+    """Flat-grid unpack (one workgroup per 32x32 tile of every conv). ``src`` is the fp32 arena
+    or a bf16 weight image with the same element offsets; descs carry each conv's first tile."""
+    assert src.dtype in (torch.float32, torch.bfloat16), src.dtype
+    check(kernels().psx_param_unpack_tiles(ptr(src), int(src.dtype == torch.bfloat16), ptr(descs_dev), ndesc,
+                                           int(ntiles), ptr(wbuf), stream_ptr()), "param_unpack_tiles")
 
 
 def unpack_desc_size() -> int:

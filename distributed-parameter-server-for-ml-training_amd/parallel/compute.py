@@ -137,6 +137,14 @@ class HipCompute:
     def set_buckets(self, buckets):
         self.engine.set_segments([b.keys for b in buckets])
 
+    def use_wire(self, wire):
+        """Fetches land in ``wire`` (parallel/codec.py WeightWire) instead of the fp32 local
+        arena: every captured step first scatters the wire's fp32 remainder (BN affine, FC, BN
+        running statistics) into the local arena, then unpacks the conv operands straight from
+        the wire's bf16 image. The local arena's conv-weight region is not used any more."""
+        self.wire = wire
+        self.engine.set_weight_source(wire.img, pre_unpack=lambda: wire.consume_small(self.local_arena))
+
     def train_step(self, dataset, idx, on_bucket=None):
         seg = (lambda k: on_bucket(k, self.grads)) if on_bucket is not None else None
         self._set_batch(idx)

@@ -30,7 +30,7 @@ from ..models.resnet import MODEL_INPUT, build_model
 from ..utils import metrics as M
 from ..utils.data import DeviceDataset, shard_range, steps_per_epoch
 from . import control as CP
-from .codec import FetchCodec
+from .codec import FetchCodec, WeightWire, weight_image_enabled
 from .compute import make_compute
 from .overlap import OverlapSyncChannel, plan_buckets
 from .server import ParameterServer
@@ -90,8 +90,9 @@ def run_local(cfg, log=print) -> dict:
         m = model if w == 0 else build_model(cfg.model, cfg.num_classes, seed=cfg.seed)
         comp = make_compute(m, layout, cfg.batch_size, device, cfg.model, _wire_dtype(cfg), seed=cfg.seed + w,
                             use_graph=cfg.use_graph)
-        wk = Worker(cfg, comp, InProcessChannel(server), train, test, worker_name=f"{cfg.worker_name}-{w}", rank=0,
-                    log=log, requested_id=w, steps_per_epoch=_common_steps(cfg, W, len(train)))
+        wk = Worker(cfg, comp, make_local_channel(cfg, server, layout, device), train, test,
+                    worker_name=f"{cfg.worker_name}-{w}", rank=0, log=log, requested_id=w,
+                    steps_per_epoch=_common_steps(cfg, W, len(train)))
         wk.connect_to_server()
         wk.setup_data()
         workers.append(wk)
@@ -188,7 +189,7 @@ def run_distributed(cfg, log=print) -> dict:
         if rank == 0:
             for r in worker_ranks:
                 server.register_worker(names[r], wid_of_rank[r])
-        chan = make_sync_channel(cfg, t, server, W, layout, device)
+        chan = make_sync_channel(cfg, t, server, W, layout, device, worker=is_worker)
         chan._gs = done  # non-server ranks track the global step locally
         if is_worker:
             wk = Worker(cfg, comp, chan, train, test, worker_name=names[rank], rank=rank, log=lg,
@@ -283,13 +284,30 @@ class AsyncSession:
         self.mbox.close()
 
 
-def make_sync_channel(cfg, t, server, W, layout, device):
-    """Sync-mode channel: bucketed + backward-overlapped when every batch is pushed."""
+def make_sync_channel(cfg, t, server, W, layout, device, worker: bool = True):
+    """Sync-mode channel: bucketed + backward-overlapped when every batch is pushed; otherwise
+    the serial round, on the WeightWire fast path when it applies (parallel/codec.py)."""
     codec = FetchCodec(layout, cfg.fetch_codec, device)
     if cfg.overlap and max(1, cfg.sync_steps) == 1 and cfg.codec != "topk":
         buckets = plan_buckets(layout, int(cfg.bucket_mb * (1 << 20)) // 2)
         return OverlapSyncChannel(t, server, members=list(range(W)), codec=codec, buckets=buckets, device=device)
-    return SyncCollectiveChannel(t, server, members=list(range(W)), codec=codec)
+    wire = None
+    if weight_image_enabled(cfg) and torch.device(device).type == "cuda":
+        if server is not None:
+            server.enable_weight_wire()
+        if worker:
+            wire = WeightWire(layout, device, server.wire.small_index if server is not None else None)
+    return SyncCollectiveChannel(t, server, members=list(range(W)), codec=codec, wire=wire)
+
+
+def make_local_channel(cfg, server, layout, device, emit_on_last: bool = False):
+    """Loopback channel of one simulated worker (WeightWire fast path when it applies)."""
+    wire = None
+    if weight_image_enabled(cfg) and torch.device(device).type == "cuda":
+        if server.wire is None:
+            server.enable_weight_wire()
+        wire = WeightWire(layout, device, server.wire.small_index)
+    return InProcessChannel(server, emit_on_last=emit_on_last, wire=wire)
 
 
 def _dedicated_sync_server(cfg, server, chan, steps, device, skip=0):

@@ -50,6 +50,8 @@ class ParameterServer:
         self.momentum_buf = torch.zeros_like(self.params) if cfg.momentum else None
         self._mom_first = True
         self.agg = None  # fp32 aggregation buffer for in-process sync rounds
+        self.wire = None  # WeightWire fetch payload kept current by the apply (enable_weight_wire)
+        self._wire_stale = False
         self._pending = {}
         self.core = ServerCore(cfg.mode, self.total_workers, cfg.lr, cfg.staleness_bound, cfg.sync_semantics)
         self.start_time = time.time()
@@ -70,6 +72,7 @@ class ParameterServer:
             if not self.cfg.momentum and not self.cfg.weight_decay:
                 # no optimizer state: scatter straight into the fp32 master parameters
                 topk.decode_add(grads, self.params, -self.lr * weight, self._kcap)
+                self._wire_stale = True  # the bf16 image was not written by this update
                 return self.finish_round_apply(time.perf_counter() - t0)
             grads = self._dense_of(grads)
         self.apply_range(grads[: self.n], weight, 0, self.n)
@@ -98,9 +101,12 @@ class ParameterServer:
         if self.device.type == "cuda":
             from ..ops import kernels as K
 
+            img = self.wire.img[lo:hi] if self.wire is not None else None  # fetch image, same pass
             K.sgd_apply(p, g, self.lr, gscale=weight, momentum=self.cfg.momentum, wd=self.cfg.weight_decay, buf=buf,
-                        first=self._mom_first, n=hi - lo)
+                        first=self._mom_first, n=hi - lo, img=img)
             return
+        if self.wire is not None:
+            self._wire_stale = True
         d = g.to(torch.float32) * weight
         if self.cfg.weight_decay:
             d = d + self.cfg.weight_decay * p
@@ -139,6 +145,35 @@ class ParameterServer:
         gs = self.core.on_fetch(worker_id)
         self.bytes_fetched += self.arena.numel() * 4
         return self.arena, gs
+
+    # ------------------------------------------------------------------ weight-image fetch path
+    def enable_weight_wire(self):
+        """Keep a WeightWire (parallel/codec.py) of the current state: the apply kernel writes
+        its bf16 image in the same pass as the fp32 update; the fp32 remainder is gathered per
+        fetch. Fetches then ship/copy exactly that one buffer."""
+        from .codec import WeightWire
+
+        if self.wire is None:
+            self.wire = WeightWire(self.layout, self.device)
+        self.wire.publish_full(self.arena)
+        self._wire_stale = False
+        return self.wire
+
+    def wire_for_fetch(self):
+        """The WeightWire holding the current state (fp32 remainder refreshed; the image was
+        written by the apply, or rebuilt here after an out-of-band update)."""
+        if self._wire_stale:
+            self.wire.publish_full(self.arena)
+            self._wire_stale = False
+        else:
+            self.wire.publish_small(self.arena)
+        return self.wire
+
+    def fetch_wire(self, worker_id: int):
+        gs = self.core.on_fetch(worker_id)
+        w = self.wire_for_fetch()
+        self.bytes_fetched += w.nbytes
+        return w, gs
 
     def push_gradients(self, worker_id: int, grads: torch.Tensor, local_step: int) -> bool:
         """In-process push (single-process loopback runs). Sync: aggregate until the barrier
@@ -277,6 +312,7 @@ class ParameterServer:
                 return
         arena, counters, step, mom, _ = ckpt.restore(path, self.layout)
         self.arena.copy_(arena.to(self.device))
+        self._wire_stale = True
         self.counters = counters
         self.core.global_step = step
         if mom is not None and self.momentum_buf is not None:

@@ -33,14 +33,26 @@ from . import control as CP
 
 
 class InProcessChannel:
-    def __init__(self, server, emit_on_last: bool = False):
+    """``wire``: the worker's own WeightWire (parallel/codec.py) — a fetch is then one device
+    copy of the server's 22.5 MB wire instead of the 44.9 MB fp32 arena, and the worker's step
+    reads its conv weights from it (ParameterServer.enable_weight_wire must be on)."""
+
+    def __init__(self, server, emit_on_last: bool = False, wire=None):
         self.server = server
         self.emit_on_last = emit_on_last
+        self.image_wire = wire
 
     def register(self, name, requested_id=-1):
         return self.server.register_worker(name, requested_id)
 
+    def weight_wire(self):
+        return self.image_wire
+
     def fetch(self, worker_id, local_arena):
+        if self.image_wire is not None:
+            src, gs = self.server.fetch_wire(worker_id)
+            self.image_wire.buf.copy_(src.buf)
+            return gs
         arena, gs = self.server.fetch_parameters(worker_id)
         local_arena.copy_(arena)
         return gs
@@ -57,17 +69,40 @@ class InProcessChannel:
 class SyncCollectiveChannel:
     """All ranks call push/fetch in lockstep. Rank 0 may or may not train (topology)."""
 
-    def __init__(self, transport, server=None, members=None, codec=None):
+    def __init__(self, transport, server=None, members=None, codec=None, wire=None):
         self.t = transport
         self.server = server
         self.members = members or []
         self.codec = codec  # FetchCodec (parallel/codec.py); None = raw fp32 arena
+        # weight-image fast path (parallel/codec.py WeightWire): this rank's worker-side wire
+        # (None on a dedicated server rank); the server's own wire is kept by the apply
+        self.image_wire = wire
+        self.image = wire is not None or (server is not None and server.wire is not None)
 
     def register(self, name, requested_id=-1):
         # registrations of every rank are done by the runner on rank 0 (gathered names)
         return requested_id, len(self.members)
 
+    def weight_wire(self):
+        return self.image_wire
+
+    def _fetch_image(self):
+        """One broadcast of the WeightWire; the worker's step consumes it in place."""
+        if self.server is not None:
+            for w in self.members:
+                self.server.core.on_fetch(w)
+            sw = self.server.wire_for_fetch()
+            self.t.broadcast_from_server(sw.buf)
+            self.server.bytes_fetched += sw.nbytes * max(0, len(self.members) - 1)
+            if self.image_wire is not None:  # the co-located worker gets its own snapshot
+                self.image_wire.buf.copy_(sw.buf)
+            return self.server.core.global_step
+        self.t.broadcast_from_server(self.image_wire.buf)
+        return self._gs_after_fetch()
+
     def fetch(self, worker_id, local_arena):
+        if self.image:
+            return self._fetch_image()
         if self.server is not None:
             for w in self.members:
                 self.server.core.on_fetch(w)
@@ -213,6 +248,9 @@ class Worker:
     def connect_to_server(self):
         self.worker_id, self.total_workers = self.channel.register(self.worker_name, self.requested_id)
         self.log(f"Registered as Worker {self.worker_id} (Total workers: {self.total_workers})")
+        wire = self.channel.weight_wire() if hasattr(self.channel, "weight_wire") else None
+        if wire is not None:  # fetches land in a WeightWire the step reads in place
+            self.compute.use_wire(wire)
         # backward-overlapped sync rounds (parallel/overlap.py): every batch is pushed, so the
         # gradient buckets can leave while the rest of the backward pass still runs
         self._overlap = bool(getattr(self.channel, "overlap", False) and self.local_steps_per_sync == 1

@@ -229,6 +229,40 @@ def test_fetch_codec_roundtrip_is_compute_exact():
             assert torch.equal(got, ref), name
 
 
+def test_weight_wire_roundtrip_matches_fetch_codec():
+    from psx.parallel.codec import FetchCodec, WeightWire, weight_image_enabled
+    from psx.utils.config import PSConfig
+
+    torch.manual_seed(0)
+    m = TinyResNet(10)
+    lay = ParamLayout.from_module(m)
+    arena, _ = lay.pack(m)
+    arena += 0.001 * torch.randn_like(arena)
+    w = WeightWire(lay, "cpu")
+    c = FetchCodec(lay, "bf16conv")
+    assert w.nbytes - c.nbytes < 16  # same payload, one buffer (16-byte aligned image)
+    w.publish_full(arena)
+    a1, a2 = torch.zeros_like(arena), torch.zeros_like(arena)
+    w.to_arena(a1)
+    c.unpack(a2, [x.clone() for x in c.pack(arena)])
+    assert torch.equal(a1, a2)
+    # the remainder travels alone: a worker's local conv region is left untouched
+    loc = torch.full_like(arena, 7.0)
+    w.consume_small(loc)
+    for name, e in lay.entries.items():
+        if e.region == "counter":
+            continue
+        if e.region == "param" and len(e.shape) == 4:
+            assert (lay.view(loc, name) == 7.0).all(), name
+        else:
+            assert torch.equal(lay.view(loc, name), lay.view(arena, name)), name
+    ok = PSConfig(mode="sync").validate()
+    assert weight_image_enabled(ok)
+    for bad in (dict(mode="async"), dict(sync_steps=2), dict(codec="topk"), dict(fetch_codec="fp32"),
+                dict(overlap=True)):
+        assert not weight_image_enabled(PSConfig(**bad).validate()), bad
+
+
 @pytest.mark.parametrize("codec", ["fp32", "bf16conv"])
 def test_dist_sync_fetch_codecs(codec):
     recs, _ = _spawn(2, ["--mode", "sync", "--fetch-codec", codec] + TINY)

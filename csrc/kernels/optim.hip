@@ -42,8 +42,15 @@ __global__ __launch_bounds__(256) void sgd_apply_kernel(float* __restrict__ p, c
 // vectorised fp16-gradient fast path (no momentum): 8 elements per lane
 template <bool IMG>
 __global__ __launch_bounds__(256) void sgd_apply_h8_kernel(float* __restrict__ p, const uint16_t* __restrict__ g,
-                                                           size_t n8, float step, float wd_step,
+                                                           size_t n, float step, float wd_step,
                                                            uint16_t* __restrict__ img) {
+  const size_t n8 = n >> 3;
+  if (blockIdx.x == 0 && threadIdx.x < (n & 7)) {  // tail (n % 8 elements)
+    const size_t i = (n8 << 3) + threadIdx.x;
+    const float nv = p[i] - (step * (float)__builtin_bit_cast(_Float16, g[i]) + wd_step * p[i]);
+    p[i] = nv;
+    if (IMG) img[i] = f2bf(nv);
+  }
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
     const u32x4 gv = reinterpret_cast<const u32x4*>(g)[i];
     f32x4 p0 = reinterpret_cast<f32x4*>(p)[2 * i];
@@ -110,55 +117,80 @@ struct UnpackDesc {
 PSX_DEV uint16_t to_bf(const float* s, size_t i) { return f2bf(s[i]); }
 PSX_DEV uint16_t to_bf(const uint16_t* s, size_t i) { return s[i]; }
 
-// Flat-grid unpack: one workgroup per (conv, 32 oc x 32 c tile), all taps of the tile staged in
-// LDS per chunk of <= 9 taps. For R*S <= 9 the source read of a tile row is one contiguous run
-// of 32*R*S elements of W[oc][c0:c0+32][:][:] (the per-tap kernel below strides by R*S). The
-// source is either the fp32 arena or the server's bf16 weight image (the bits sgd_apply wrote
-// next to the fp32 update, parallel/codec.py), so a worker never needs fp32 conv weights.
+// Flat-grid unpack: one workgroup per (conv, 64 oc x 64 c tile, chunk of <= 3 taps), staged
+// through LDS. Every global store is a 4-byte pair and every (oc, tap) row of
+// wf / (c, tap) row of wd a full 128-byte line (the 32x32-tile version wrote 64-byte halves from
+// two workgroups and ran at 0.8 TB/s). The source is the fp32 arena or the server's bf16 weight
+// image (the bits sgd_apply wrote next to the fp32 update, parallel/codec.py), so a worker
+// never needs fp32 conv weights.
+constexpr int kUnpackTile = 64;
+
+template <int NT, typename ST>
+PSX_DEV void unpack_chunk(const UnpackDesc& d, const ST* __restrict__ src, int oc0, int c0, int tap0, int RS,
+                          uint16_t* __restrict__ wbuf, uint16_t* tile) {
+  constexpr int PITCH = 64 * NT + 2;  // halves; odd dword pitch -> oc-strided reads hit distinct banks
+  const int nc_src = min(64, d.Cin - c0);  // real input channels in this tile (<= 0: all padding)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // stage tile[oc][c*NT + tp] = W[oc0+oc][c0+c][tap0+tp]: all 16*NT loads of a lane in flight
+  // before the first LDS write (a load -> wait -> write loop per row was latency-bound)
+  uint16_t v[16][NT];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int oc = wv + 4 * i;
+    const bool ok = oc0 + oc < d.OC && lane < nc_src;
+    const ST* p = src + ((size_t)(oc0 + oc) * d.Cin + c0 + lane) * RS + tap0;
+#pragma unroll
+    for (int tp = 0; tp < NT; ++tp) v[i][tp] = ok ? to_bf(p, tp) : (uint16_t)0;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+#pragma unroll
+    for (int tp = 0; tp < NT; ++tp) tile[(wv + 4 * i) * PITCH + lane * NT + tp] = v[i][tp];
+  __syncthreads();
+  const int half = lane >> 5, l2 = (lane & 31) * 2;  // a wave writes two 128-byte rows
+  // wf[oc][tap*Cp + c]
+  for (int q = wv * 2 + half; q < 64 * NT; q += 8) {
+    const int oc = q / NT, tp = q - oc * NT;
+    if (oc0 + oc < d.OC && c0 + l2 < d.Cp) {
+      const uint32_t v = (uint32_t)tile[oc * PITCH + l2 * NT + tp] | ((uint32_t)tile[oc * PITCH + (l2 + 1) * NT + tp] << 16);
+      *reinterpret_cast<uint32_t*>(wbuf + d.wf_off + (size_t)(oc0 + oc) * d.Kg + (tap0 + tp) * d.Cp + c0 + l2) = v;
+    }
+  }
+  if (d.wd_off >= 0) {  // wd[c][tap*OC + oc]
+    for (int q = wv * 2 + half; q < 64 * NT; q += 8) {
+      const int c = q / NT, tp = q - c * NT;
+      if (oc0 + l2 < d.OC && c0 + c < d.Cp) {
+        const uint32_t v = (uint32_t)tile[l2 * PITCH + c * NT + tp] | ((uint32_t)tile[(l2 + 1) * PITCH + c * NT + tp] << 16);
+        *reinterpret_cast<uint32_t*>(wbuf + d.wd_off + (size_t)(c0 + c) * d.Kgd + (tap0 + tp) * d.OC + oc0 + l2) = v;
+      }
+    }
+  }
+}
+
 template <typename ST>
 __global__ __launch_bounds__(256) void param_unpack_tiles_kernel(const ST* __restrict__ src_all,
                                                                  const UnpackDesc* __restrict__ descs, int ndesc,
                                                                  uint16_t* __restrict__ wbuf) {
-  constexpr int TC = 9;
-  __shared__ uint16_t tile[TC][32][34];
+  __shared__ uint16_t tile[64 * (64 * 3 + 2)];
+  __shared__ int first_tile[256];
+  // which conv owns this workgroup: all descs' tile0 fetched in parallel
+  for (int k = threadIdx.x; k < 256; k += 256) first_tile[k] = k < ndesc ? descs[k].tile0 : 0x7fffffff;
+  __syncthreads();
   int j = 0;
-  while (j + 1 < ndesc && descs[j + 1].tile0 <= (int)blockIdx.x) ++j;
+  while (j + 1 < ndesc && first_tile[j + 1] <= (int)blockIdx.x) ++j;
   const UnpackDesc d = descs[j];
-  const int t = blockIdx.x - d.tile0;
-  const int n_c = (d.Cp + 31) / 32;
-  const int oc0 = (t / n_c) * 32, c0 = (t % n_c) * 32;
+  // unit = (64x64 tile, chunk of <= 3 taps): one workgroup each
   const int RS = d.R * d.S;
+  const int nchunk = (RS + 2) / 3;
+  const int u = blockIdx.x - d.tile0;
+  const int t = u / nchunk, tap0 = (u - t * nchunk) * 3;
+  const int n_c = (d.Cp + kUnpackTile - 1) / kUnpackTile;
+  const int oc0 = (t / n_c) * kUnpackTile, c0 = (t % n_c) * kUnpackTile;
   const ST* src = src_all + d.src_off;
-  const int nc_src = min(32, d.Cin - c0);  // real input channels in this tile (<= 0: all padding)
-  for (int tap0 = 0; tap0 < RS; tap0 += TC) {
-    const int nt = min(TC, RS - tap0);
-    if (tap0) __syncthreads();
-    // stage tile[tap][oc][c] = W[oc0+oc][c0+c][tap0+tap] (zeros outside OC x Cin)
-    const int per_oc = 32 * nt;
-    for (int e = threadIdx.x; e < 32 * per_oc; e += 256) {
-      const int oc = e / per_oc, r = e - oc * per_oc;
-      const int c = r / nt, tp = r - c * nt;
-      uint16_t v = 0;
-      if (oc0 + oc < d.OC && c < nc_src)
-        v = to_bf(src, ((size_t)(oc0 + oc) * d.Cin + (c0 + c)) * RS + tap0 + tp);
-      tile[tp][oc][c] = v;
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < 32 * nt * 32; e += 256) {  // wf[oc][tap*Cp + c]: c fastest
-      const int c = e & 31, rest = e >> 5;
-      const int tp = rest % nt, oc = rest / nt;
-      if (oc0 + oc < d.OC && c0 + c < d.Cp)
-        wbuf[d.wf_off + (size_t)(oc0 + oc) * d.Kg + (tap0 + tp) * d.Cp + c0 + c] = tile[tp][oc][c];
-    }
-    if (d.wd_off >= 0) {
-      for (int e = threadIdx.x; e < 32 * nt * 32; e += 256) {  // wd[c][tap*OC + oc]: oc fastest
-        const int oc = e & 31, rest = e >> 5;
-        const int tp = rest % nt, c = rest / nt;
-        if (oc0 + oc < d.OC && c0 + c < d.Cp)
-          wbuf[d.wd_off + (size_t)(c0 + c) * d.Kgd + (tap0 + tp) * d.OC + oc0 + oc] = tile[tp][oc][c];
-      }
-    }
-  }
+  const int nt = min(3, RS - tap0);
+  if (nt == 3) unpack_chunk<3>(d, src, oc0, c0, tap0, RS, wbuf, tile);
+  else if (nt == 2) unpack_chunk<2>(d, src, oc0, c0, tap0, RS, wbuf, tile);
+  else unpack_chunk<1>(d, src, oc0, c0, tap0, RS, wbuf, tile);
 }
 
 // One workgroup per (32 oc x 32 c) tile of one conv (blockIdx.y = conv). For every tap the
@@ -223,14 +255,14 @@ int psx_sgd_apply(float* p, const void* g, float* buf, long n, float lr, float g
                   int first, int grad_fp16, void* img, hipStream_t st) {
   const bool mom = buf != nullptr && momentum != 0.f;
   uint16_t* im = (uint16_t*)img;
-  if (!mom && grad_fp16 && n % 8 == 0 && ((uintptr_t)p % 32 == 0) && ((uintptr_t)g % 16 == 0) &&
+  if (!mom && grad_fp16 && n >= 8 && ((uintptr_t)p % 32 == 0) && ((uintptr_t)g % 16 == 0) &&
       ((uintptr_t)img % 16 == 0)) {
     if (im)
       hipLaunchKernelGGL(sgd_apply_h8_kernel<true>, dim3(grid_for(n / 8)), dim3(256), 0, st, p, (const uint16_t*)g,
-                         (size_t)n / 8, lr * gscale, lr * wd, im);
+                         (size_t)n, lr * gscale, lr * wd, im);
     else
       hipLaunchKernelGGL(sgd_apply_h8_kernel<false>, dim3(grid_for(n / 8)), dim3(256), 0, st, p, (const uint16_t*)g,
-                         (size_t)n / 8, lr * gscale, lr * wd, im);
+                         (size_t)n, lr * gscale, lr * wd, im);
     return (int)hipGetLastError();
   }
   const int grid = grid_for(n);
@@ -290,6 +322,7 @@ int psx_param_unpack(const float* arena, const void* descs, int ndesc, void* wbu
 int psx_param_unpack_tiles(const void* src, int src_bf16, const void* descs, int ndesc, int ntiles, void* wbuf,
                            hipStream_t st) {
   if (ntiles <= 0 || ndesc <= 0) return 0;
+  if (ndesc > 256) return (int)hipErrorInvalidValue;  // the kernel's LDS desc table
   if (src_bf16)
     hipLaunchKernelGGL(param_unpack_tiles_kernel<uint16_t>, dim3(ntiles), dim3(256), 0, st, (const uint16_t*)src,
                        (const UnpackDesc*)descs, ndesc, (uint16_t*)wbuf);

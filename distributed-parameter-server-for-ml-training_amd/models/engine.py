@@ -207,7 +207,7 @@ class HipResNetEngine:
         # weights: one bf16 buffer holding every conv's fwd (and dgrad) operand
         off = 0
         descs = []
-        tile0 = 0  # flat tile grid of param_unpack_tiles: 32x32 (oc, c) tiles of every conv
+        tile0 = 0  # flat grid of param_unpack_tiles: (64x64 (oc, c) tile, chunk of <= 3 taps) units
         for cs in all_convs(sp):
             cs.finalize()
             cs.wf_off = off
@@ -219,7 +219,7 @@ class HipResNetEngine:
                 cs.wd_off = -1
             descs.append((self.layout.offset(f"{cs.name}.weight"), cs.wf_off, cs.wd_off, cs.cout, cs.cin, cs.k, cs.k,
                           cs.cp, cs.kg, cs.kgd, tile0))
-            tile0 += -(-cs.cout // 32) * -(-cs.cp // 32)
+            tile0 += -(-cs.cout // 64) * -(-cs.cp // 64) * -(-(cs.k * cs.k) // 3)
         self.ntiles = tile0
         self.wbuf = torch.zeros(off, dtype=torch.bfloat16, device=self.dev)
         dsz = K.unpack_desc_size()

@@ -33,7 +33,8 @@ from psx.parallel.compute import HipCompute  # noqa: E402
 from psx.parallel.runner import (AsyncSession, build_state, make_datasets, make_local_channel,  # noqa: E402
                                  make_sync_channel)
 from psx.parallel.server import ParameterServer  # noqa: E402
-from psx.parallel.transport import DistTransport, env_world  # noqa: E402
+from psx.parallel.rccl import make_transport  # noqa: E402
+from psx.parallel.transport import env_world  # noqa: E402
 from psx.parallel.worker import Worker  # noqa: E402
 from psx.utils.config import PSConfig  # noqa: E402
 
@@ -82,7 +83,7 @@ def main():
     t = None
     force_dist = os.environ.get("PSX_FORCE_DIST", "0") == "1"  # exercise the RCCL path even at N=1
     if world > 1 or force_dist:
-        t = DistTransport(device=device)
+        t = make_transport(device)
     dedicated = a.topology == "dedicated" and world > 1
     worker_ranks = list(range(1, world)) if dedicated else list(range(world))
     W = len(worker_ranks)
@@ -207,6 +208,8 @@ def main():
                 "overlap": (f"bucketed reduce/apply/broadcast during backward ({len(chan.buckets)} buckets)"
                             if getattr(chan, "overlap", False) else "none"),
                 "topology": "dedicated" if dedicated else ("colocated" if t is not None else "loopback"),
+                "transport": (("native RCCL (psx comm)" if getattr(t, "native", False) else "torch.distributed")
+                              if t is not None else "in-process"),
                 "hip_graph": cfg.use_graph,
             },
             "global_steps": server.core.global_step,

@@ -84,6 +84,23 @@ def build(jobs: int = 8, debug: bool = False, verbose: bool = False) -> dict:
     if r_objs and _newer(r_objs, r_lib):
         _run([CXX, "-shared", "-fPIC", "-pthread", "-o", r_lib] + r_objs + ["-lrt"])
     libs["runtime"] = r_lib
+
+    # libpsx_comm.so: host C++ against the HIP runtime + RCCL headers (RCCL itself is dlopened at
+    # run time, see csrc/comm/rccl_comm.cpp); csrc/server/*.cpp is the native server event loop
+    c_srcs = sorted(glob.glob(os.path.join(HERE, "comm", "*.cpp")) + glob.glob(os.path.join(HERE, "server", "*.cpp")))
+    c_hdrs = (glob.glob(os.path.join(HERE, "comm", "*.h")) + glob.glob(os.path.join(HERE, "server", "*.h")) + r_hdrs)
+    c_flags = ["-std=c++17", "-fPIC", "-Wall", "-pthread", "-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include",
+               "-I", os.path.join(HERE, "runtime"), "-I", os.path.join(HERE, "comm")] + opt
+    c_objs = []
+    for s in c_srcs:
+        o = os.path.join(OBJ, "comm_" + os.path.basename(s) + ".o")
+        c_objs.append(o)
+        if _newer([s] + c_hdrs, o):
+            _run([HIPCC] + c_flags + ["-c", s, "-o", o])
+    c_lib = os.path.join(OUT, "libpsx_comm.so")
+    if c_objs and _newer(c_objs, c_lib):
+        _run([HIPCC, "-shared", "-fPIC", "-pthread", "-o", c_lib] + c_objs + ["-ldl", "-lrt"])
+    libs["comm"] = c_lib
     return libs
 
 

@@ -106,6 +106,26 @@ _RUNTIME_SIGS = {
 }
 
 
+_COMM_SIGS = {
+    "psx_comm_load": (i32, [C.c_char_p]),
+    "psx_comm_id_bytes": (i32, []),
+    "psx_comm_unique_id": (i32, [C.c_char_p]),
+    "psx_comm_init": (i32, [C.c_char_p, i32, i32, i32, C.POINTER(vp)]),
+    "psx_comm_destroy": (i32, [vp]),
+    "psx_comm_abort": (i32, [vp]),
+    "psx_comm_async_error": (i32, [vp]),
+    "psx_comm_error_string": (C.c_char_p, [i32]),
+    "psx_comm_reduce_sum": (i32, [vp, vp, vp, i64, i32, i32, vp]),
+    "psx_comm_all_reduce_sum": (i32, [vp, vp, vp, i64, i32, vp]),
+    "psx_comm_broadcast": (i32, [vp, vp, i64, i32, i32, vp]),
+    "psx_comm_send": (i32, [vp, vp, i64, i32, i32, vp]),
+    "psx_comm_recv": (i32, [vp, vp, i64, i32, i32, vp]),
+    "psx_comm_group_start": (i32, []),
+    "psx_comm_group_end": (i32, []),
+    "psx_comm_gather": (i32, [vp, vp, vp, i64, i32, i32, i32, i32, i32, vp]),
+}
+
+
 def _declare(lib, sigs, optional=False):
     for name, (res, args) in sigs.items():
         if optional and not hasattr(lib, name):
@@ -146,6 +166,22 @@ def kernels():
                 else:
                     _kern = _declare(C.CDLL(_maybe_build("libpsx_kernels.so"), mode=C.RTLD_GLOBAL), _KERNEL_SIGS)
     return _kern
+
+
+_comm = None
+
+
+def comm():
+    """The native RCCL data-plane library (csrc/comm/rccl_comm.cpp); loaded after torch so it
+    shares PyTorch's HIP runtime (RCCL itself is bound by psx_comm_load)."""
+    global _comm
+    if _comm is None:
+        with _lock:
+            if _comm is None:
+                import torch  # noqa: F401
+
+                _comm = _declare(C.CDLL(_maybe_build("libpsx_comm.so"), mode=C.RTLD_GLOBAL), _COMM_SIGS)
+    return _comm
 
 
 def runtime():

@@ -34,7 +34,8 @@ from .codec import FetchCodec, WeightWire, weight_image_enabled
 from .compute import make_compute
 from .overlap import OverlapSyncChannel, plan_buckets
 from .server import ParameterServer
-from .transport import DistTransport, LocalTransport, env_world
+from .rccl import make_transport
+from .transport import LocalTransport, env_world
 from .worker import (AsyncChannel, InProcessChannel, LocalAsyncChannel, SyncCollectiveChannel, Worker)
 
 
@@ -157,7 +158,7 @@ def _interleave(cfg, workers, server, log):
 def run_distributed(cfg, log=print) -> dict:
     rank, world, local = env_world()
     device = _device_for(local)
-    t = DistTransport(device=device)
+    t = make_transport(device)
     dedicated = cfg.topology == "dedicated" and world > 1
     worker_ranks = list(range(1, world)) if dedicated else list(range(world))
     W = len(worker_ranks)

@@ -1,0 +1,89 @@
+"""Native RCCL transport (csrc/comm/rccl_comm.cpp + parallel/rccl.py) on one MI355X.
+
+A one-GPU box can host a single RCCL rank (RCCL refuses two ranks on one device), so these run
+world size 1 in a subprocess: communicator bootstrap through the gloo control group, the sync
+collectives in stream order, the non-blocking overlap collectives, the gather path, and a whole
+sync PS run over the native transport against the torch.distributed one. Multi-rank semantics
+are the same channel code as the gloo CPU tests (tests/test_ps_cpu.py).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_OPS = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+import torch
+import psx
+from psx.parallel.rccl import RcclTransport
+t = RcclTransport(device=torch.device("cuda", 0))
+res = {{}}
+g = torch.randn(1 << 20, device="cuda").half()
+ref = g.clone()
+t.reduce_sum_to_server(g)
+res["reduce_identity"] = bool(torch.equal(g, ref))
+w = torch.randint(0, 255, (3 << 20,), dtype=torch.uint8, device="cuda")
+wref = w.clone()
+t.broadcast_from_server(w)
+res["bcast_identity"] = bool(torch.equal(w, wref))
+p = torch.arange(1000, dtype=torch.int32, device="cuda")
+out = t.gather_to_server(p)
+res["gather"] = len(out) == 1 and bool(torch.equal(out[0], p))
+x = torch.randn(4096, device="cuda")
+xr = x.clone()
+wk = t.reduce_async(x)
+wk.wait()
+wb = t.broadcast_async(x)
+ok = t.completed(wb) or (wb.wait() is True)
+torch.cuda.synchronize()
+res["async_ops"] = bool(torch.equal(x, xr))
+res["async_error"] = t.comm.async_error()
+t.close()
+print("RESULT " + json.dumps(res))
+"""
+
+
+def _run(code, port, extra_env=None, timeout=240):
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    env.update(extra_env or {})
+    r = subprocess.run([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
+    return json.loads(line[7:])
+
+
+def test_native_collectives_world1():
+    res = _run(_OPS.format(root=ROOT), 29651)
+    assert res == {"reduce_identity": True, "bcast_identity": True, "gather": True, "async_ops": True,
+                   "async_error": 0}, res
+
+
+_RUN = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+import psx
+from psx.parallel.runner import run_distributed
+from psx.utils.config import PSConfig
+cfg = PSConfig(model="resnet18", batch_size=64, epochs=1, train_samples=2048, eval_every=0, verbose=0, lr=0.1,
+               max_steps=6, mode="sync", codec={codec!r}).validate()
+res = run_distributed(cfg, log=lambda *a, **k: None)
+print("RESULT " + json.dumps([res["server"]["final_param_checksum"], res["server"]["global_steps_completed"]]))
+"""
+
+
+@pytest.mark.parametrize("codec", ["fp16", "topk"])
+def test_sync_run_native_matches_torch_transport(codec):
+    out = {}
+    for kind, port in (("native", 29652), ("torch", 29653)):
+        out[kind] = _run(_RUN.format(root=ROOT, codec=codec), port, {"PSX_TRANSPORT": kind})
+    (a, sa), (b, sb) = out["native"], out["torch"]
+    assert sa == sb == 6
+    assert abs(a - b) <= 2e-4 * max(abs(a), abs(b)), out

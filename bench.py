@@ -206,7 +206,9 @@ def main():
                 "fetch_codec": a.fetch_codec if t is not None else "in-process",
                 "weight_image": getattr(chan, "image_wire", None) is not None,
                 "overlap": (f"bucketed reduce/apply/broadcast during backward ({len(chan.buckets)} buckets)"
-                            if getattr(chan, "overlap", False) else "none"),
+                            if getattr(chan, "overlap", False) else
+                            f"bucketed reduce/apply/broadcast captured in the step graph ({len(chan.buckets)} buckets)"
+                            if getattr(chan, "in_graph", False) else "none"),
                 "topology": "dedicated" if dedicated else ("colocated" if t is not None else "loopback"),
                 "transport": (("native RCCL (psx comm)" if getattr(t, "native", False) else "torch.distributed")
                               if t is not None else "in-process"),

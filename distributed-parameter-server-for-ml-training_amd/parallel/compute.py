@@ -145,9 +145,27 @@ class HipCompute:
         self.wire = wire
         self.engine.set_weight_source(wire.img, pre_unpack=lambda: wire.consume_small(self.local_arena))
 
-    def train_step(self, dataset, idx, on_bucket=None):
+    def train_step(self, dataset, idx, on_bucket=None, round_hooks=None):
         seg = (lambda k: on_bucket(k, self.grads)) if on_bucket is not None else None
         self._set_batch(idx)
+        if round_hooks is not None:  # the whole PS round in one graph (parallel/graph_round.py)
+            if not self.use_graph:
+                self.engine.train_step(self.local_arena, dataset.images, dataset.labels, unpack=True,
+                                       on_segment=round_hooks.after_segment)
+                round_hooks.finish()
+            else:
+                if self.engine.graph is None or self._dataset is not dataset:
+                    self._dataset = dataset
+                    backup = self.local_arena.clone()
+                    self.engine.capture(self.local_arena, dataset.images, dataset.labels, unpack=True, warmup=1)
+                    self.local_arena.copy_(backup)
+                    del backup
+                # one graph per backward segment; after each replay the segment's reduce/apply/
+                # broadcast is forked onto the communication stream (the compute stream never waits)
+                self.engine.step_graph(on_segment=round_hooks.after_segment)
+                round_hooks.finish()
+            self._step += 1
+            return
         if self.use_graph:
             if self.engine.graph is None or self._dataset is not dataset:
                 # One-time capture of unpack + augment + fwd + bwd over the fixed local arena

@@ -32,6 +32,7 @@ from ..utils.data import DeviceDataset, shard_range, steps_per_epoch
 from . import control as CP
 from .codec import FetchCodec, WeightWire, weight_image_enabled
 from .compute import make_compute
+from .graph_round import GraphRoundChannel, graph_round_enabled
 from .overlap import OverlapSyncChannel, plan_buckets
 from .server import ParameterServer
 from .rccl import make_transport
@@ -296,6 +297,11 @@ def make_sync_channel(cfg, t, server, W, layout, device, worker: bool = True):
     if weight_image_enabled(cfg) and torch.device(device).type == "cuda":
         if server is not None:
             server.enable_weight_wire()
+        if graph_round_enabled(cfg, t):
+            # rank 0's worker reads the server's wire in place; the others receive theirs
+            wire = server.wire if server is not None else WeightWire(layout, device)
+            buckets = plan_buckets(layout, int(cfg.bucket_mb * (1 << 20)) // 2)
+            return GraphRoundChannel(t, server, list(range(W)), codec, wire, buckets, device)
         if worker:
             wire = WeightWire(layout, device, server.wire.small_index if server is not None else None)
     return SyncCollectiveChannel(t, server, members=list(range(W)), codec=codec, wire=wire)

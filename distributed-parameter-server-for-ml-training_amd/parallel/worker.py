@@ -257,6 +257,11 @@ class Worker:
                              and hasattr(self.compute, "set_buckets"))
         if self._overlap:
             self.compute.set_buckets(self.channel.buckets)
+        # the whole round captured into the step graph (parallel/graph_round.py)
+        self._round = bool(getattr(self.channel, "in_graph", False))
+        if self._round:
+            self.compute.set_buckets(self.channel.buckets)
+            self.channel.bind(self.compute.grads)
 
     def setup_data(self):
         start, end = shard_range(self.worker_id, self.total_workers, len(self.train_set))
@@ -282,8 +287,11 @@ class Worker:
         return ok
 
     def train_local_batch(self, idx):
-        on_bucket = self.channel.push_bucket if getattr(self, "_overlap", False) else None
-        self.compute.train_step(self.train_set, idx, on_bucket=on_bucket)
+        if getattr(self, "_round", False):
+            self.compute.train_step(self.train_set, idx, round_hooks=self.channel)
+        else:
+            on_bucket = self.channel.push_bucket if getattr(self, "_overlap", False) else None
+            self.compute.train_step(self.train_set, idx, on_bucket=on_bucket)
         self.local_step_counter += 1
         self.images += len(idx)
 

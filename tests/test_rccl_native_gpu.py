@@ -87,3 +87,41 @@ def test_sync_run_native_matches_torch_transport(codec):
     (a, sa), (b, sb) = out["native"], out["torch"]
     assert sa == sb == 6
     assert abs(a - b) <= 2e-4 * max(abs(a), abs(b)), out
+
+
+_ROUND = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+import psx
+from psx.parallel.runner import run_distributed
+from psx.utils.config import PSConfig
+cfg = PSConfig(model="resnet18", batch_size=64, epochs=1, train_samples=2048, eval_every=1, test_samples=256,
+               verbose=0, lr=0.1, max_steps=6, mode="sync", use_graph={graph!r}).validate()
+import psx.parallel.runner as R
+made = []
+_mk = R.make_sync_channel
+def spy(*a, **k):
+    c = _mk(*a, **k)
+    made.append(type(c).__name__)
+    return c
+R.make_sync_channel = spy
+res = run_distributed(cfg, log=lambda *a, **k: None)
+w = res["worker"]
+print("RESULT " + json.dumps([res["server"]["final_param_checksum"], res["server"]["global_steps_completed"],
+                             w["final_test_accuracy_percent"], ",".join(made)]))
+"""
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_graph_round_matches_serial_round(graph):
+    """The round captured in the step graph (parallel/graph_round.py; eager hooks when graphs
+    are off) against the serial round (PSX_GRAPH_ROUND=0): same master state, and the worker's
+    evaluation after training runs on the broadcast state."""
+    out = {}
+    for flag, port in (("1", 29654), ("0", 29655)):
+        out[flag] = _run(_ROUND.format(root=ROOT, graph=graph), port, {"PSX_GRAPH_ROUND": flag})
+    assert "GraphRoundChannel" in out["1"][3] and "GraphRoundChannel" not in out["0"][3]
+    (a, sa, acc_a, _), (b, sb, acc_b, _) = out["1"], out["0"]
+    assert sa == sb == 6
+    assert abs(a - b) <= 2e-4 * max(abs(a), abs(b)), out
+    assert acc_a >= 0.0 and acc_b >= 0.0

@@ -14,7 +14,7 @@ from psx.ops import kernels as K  # noqa: E402
 from tests.test_kernels_gpu import make_operands, to_nhwc  # noqa: E402
 from conv_layers import SHAPES, t_us  # noqa: E402
 
-VARS = ("PSX_CV_BM", "PSX_CV_BN", "PSX_CV_SPLITS")
+VARS = ("PSX_CV_BM", "PSX_CV_BN", "PSX_CV_SPLITS", "PSX_CV_WGM")
 
 
 def clear():
@@ -44,16 +44,17 @@ def main():
             clear()
             base = t_us(fn, iters=20)
             res = []
-            for bm, bn in ((128, 128), (64, 128), (64, 64)):
+            for bm, bn, wgm in ((128, 128, 2), (64, 128, 2), (64, 64, 2), (64, 256, 1), (64, 128, 1), (128, 256, 2)):
                 for sp in (1, 2, 3, 4, 6, 8):
-                    os.environ.update(PSX_CV_BM=str(bm), PSX_CV_BN=str(bn), PSX_CV_SPLITS=str(sp))
+                    os.environ.update(PSX_CV_BM=str(bm), PSX_CV_BN=str(bn), PSX_CV_SPLITS=str(sp),
+                                      PSX_CV_WGM=str(wgm))
                     try:
-                        res.append((t_us(fn, iters=20), bm, bn, sp))
+                        res.append((t_us(fn, iters=20), bm, bn, sp, wgm))
                     except RuntimeError:
                         pass
             res.sort()
             print(f"layer {li} {name:5s} {cin}->{cout} {hw} k{k}s{s}: planner {base:.1f} us | best "
-                  + "  ".join(f"{bm}x{bn}/s{sp}:{us:.1f}" for us, bm, bn, sp in res[:4]), flush=True)
+                  + "  ".join(f"{bm}x{bn}w{wgm}/s{sp}:{us:.1f}" for us, bm, bn, sp, wgm in res[:4]), flush=True)
     clear()
 
 

@@ -104,13 +104,37 @@ def build(jobs: int = 8, debug: bool = False, verbose: bool = False) -> dict:
     return libs
 
 
+def build_variant(name: str, defines: list[str], jobs: int = 8) -> str:
+    """A/B build of the kernel library with extra -D defines into _native/variants/ (load it
+    with PSX_KERNELS_LIB=<path>); e.g. --variant s4 -D PSX_STAT_SLOTS=4."""
+    vout = os.path.join(OUT, "variants")
+    vobj = os.path.join(OBJ, "variant_" + name)
+    os.makedirs(vout, exist_ok=True)
+    os.makedirs(vobj, exist_ok=True)
+    k_srcs = sorted(glob.glob(os.path.join(HERE, "kernels", "*.hip")))
+    flags = [f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-O3", "-munsafe-fp-atomics", "-I",
+             os.path.join(HERE, "kernels")] + [f"-D{d}" for d in defines]
+    cmds = [[HIPCC] + flags + ["-c", s_, "-o", os.path.join(vobj, os.path.basename(s_) + ".o")] for s_ in k_srcs]
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        list(ex.map(_run, cmds))
+    lib = os.path.join(vout, f"libpsx_kernels_{name}.so")
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] +
+         [os.path.join(vobj, os.path.basename(s_) + ".o") for s_ in k_srcs])
+    return lib
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("-v", action="store_true")
+    ap.add_argument("--variant", default=None, help="build an A/B kernel library variant (see build_variant)")
+    ap.add_argument("-D", dest="defines", action="append", default=[])
     a = ap.parse_args(argv)
+    if a.variant:
+        print(build_variant(a.variant, a.defines, a.j))
+        return 0
     if a.clean:
         shutil.rmtree(OBJ, ignore_errors=True)
         for f in glob.glob(os.path.join(OUT, "*.so")):

@@ -72,17 +72,21 @@ PSX_DEV const uint16_t* gather_src(const Conv2Args& a, int nbase, int hb, int wb
   return a.in + ((size_t)(nbase + ih * a.IW + iw) * a.IC + c0);
 }
 
-template <int BM, int BN, int MODE, bool HAS_RES, bool SPLIT>
+// WGM = waves along the output-channel (M) axis, 4 / WGM along pixels: 2 (2x2 waves, wave tile
+// BM/2 x BN/2) or 1 (1x4 waves: every wave holds all BM channels of a BN/4 pixel slice, e.g. a
+// 64x64 wave tile for BM = 64, BN = 256 — 2/3 of the LDS fragment bytes per MFMA of 32x64).
+template <int BM, int BN, int MODE, bool HAS_RES, bool SPLIT, int WGM = 2>
 __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   constexpr int NSTAGE = 3;
-  constexpr int MT = BM / 32, NT = BN / 32;   // 16x16 MFMA tiles per wave (2x2 waves)
+  constexpr int WGN = 4 / WGM;
+  constexpr int MT = BM / (16 * WGM), NT = BN / (16 * WGN);  // 16x16 MFMA tiles per wave
   constexpr int LA = BM / 32, LB = BN / 32;   // DMA instructions per wave per stage
   constexpr int STAGE = (BM + BN) * 128;      // bytes per stage
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WGN, wn = wid % WGN;
   const int nwg = a.n_oc_tiles * a.n_pix_tiles;
   const int tile = xcd_remap(blockIdx.x, nwg);
   const int oc_t = tile % a.n_oc_tiles, pix_t = tile / a.n_oc_tiles;
@@ -239,10 +243,10 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       bf16x8 fa[MT], fb[NT];
 #pragma unroll
       for (int m = 0; m < MT; ++m)
-        fa[m] = *reinterpret_cast<const bf16x8*>(A + kmaj2(wm * (BM / 2) + m * 16 + frow, kk * 4 + fch));
+        fa[m] = *reinterpret_cast<const bf16x8*>(A + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
 #pragma unroll
       for (int n = 0; n < NT; ++n)
-        fb[n] = *reinterpret_cast<const bf16x8*>(B + kmaj2(wn * (BN / 2) + n * 16 + frow, kk * 4 + fch));
+        fb[n] = *reinterpret_cast<const bf16x8*>(B + kmaj2(wn * (BN / WGN) + n * 16 + frow, kk * 4 + fch));
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -256,11 +260,11 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     float* dst = a.part + (size_t)split * a.npix * a.OC;
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
-      const int pix = pix0 + wn * (BN / 2) + n * 16 + (lane & 15);
+      const int pix = pix0 + wn * (BN / WGN) + n * 16 + (lane & 15);
       if (pix >= a.npix) continue;
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        const int oc = oc0 + wm * (BM / 2) + m * 16 + 4 * (lane >> 4);
+        const int oc = oc0 + wm * (BM / WGM) + m * 16 + 4 * (lane >> 4);
         *reinterpret_cast<f32x4*>(dst + (size_t)pix * a.OC + oc) = acc[m][n];
       }
     }
@@ -276,7 +280,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       s1[m][i] = s2[m][i] = s3[m][i] = 0.f;
-      const int ch = oc0 + wm * (BM / 2) + m * 16 + 4 * (lane >> 4) + i;
+      const int ch = oc0 + wm * (BM / WGM) + m * 16 + 4 * (lane >> 4) + i;
       if (bwd) {
         bm1[m][i] = a.bsaved1[ch];
         bi1[m][i] = a.bsaved1[a.OC + ch];
@@ -288,7 +292,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     }
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
-    const int pix = pix0 + wn * (BN / 2) + n * 16 + (lane & 15);
+    const int pix = pix0 + wn * (BN / WGN) + n * 16 + (lane & 15);
     const bool ok = pix < npix_c;
     size_t opix = (size_t)pix;
     if (MODE == 3 && ok) {  // class-local (n, i, j) -> dx (n, 2i+py, 2j+px)
@@ -297,7 +301,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     }
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const int oc = oc0 + wm * (BM / 2) + m * 16 + 4 * (lane >> 4);
+      const int oc = oc0 + wm * (BM / WGM) + m * 16 + 4 * (lane >> 4);
       float v0 = acc[m][n][0], v1 = acc[m][n][1], v2 = acc[m][n][2], v3 = acc[m][n][3];
       if (ok) {
         const size_t off = opix * a.OC + oc;
@@ -356,7 +360,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int row = wm * (BM / 2) + m * 16 + 4 * (lane >> 4) + i;
+          const int row = wm * (BM / WGM) + m * 16 + 4 * (lane >> 4) + i;
           red[(wn * 3 + 0) * BM + row] = s1[m][i];
           red[(wn * 3 + 1) * BM + row] = s2[m][i];
           red[(wn * 3 + 2) * BM + row] = s3[m][i];
@@ -366,7 +370,10 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     float* dst = a.bpart + (size_t)(pix_t & (PSX_STAT_SLOTS - 1)) * NSr * a.OC;
     for (int j = tid; j < NSr * BM; j += 256) {
       const int which = j / BM, row = j - which * BM;
-      atomicAdd(dst + which * a.OC + oc0 + row, red[which * BM + row] + red[(3 + which) * BM + row]);
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < WGN; ++w) v += red[(w * 3 + which) * BM + row];
+      atomicAdd(dst + which * a.OC + oc0 + row, v);
     }
   }
   if (a.stats) {
@@ -387,7 +394,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int row = wm * (BM / 2) + m * 16 + 4 * (lane >> 4) + i;
+          const int row = wm * (BM / WGM) + m * 16 + 4 * (lane >> 4) + i;
           red[(wn * 2 + 0) * BM + row] = s1[m][i];
           red[(wn * 2 + 1) * BM + row] = s2[m][i];
         }
@@ -396,7 +403,10 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     float* dst = a.stats + (size_t)(pix_t & (PSX_STAT_SLOTS - 1)) * 2 * a.OC;
     for (int j = tid; j < 2 * BM; j += 256) {
       const int which = j / BM, row = j - which * BM;
-      atomicAdd(dst + which * a.OC + oc0 + row, red[which * BM + row] + red[(2 + which) * BM + row]);
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < WGN; ++w) v += red[(w * 2 + which) * BM + row];
+      atomicAdd(dst + which * a.OC + oc0 + row, v);
     }
     if (a.fuse_fin && last_block_arrive(a.fin.counter, gridDim.x, smem))
       bn_finalize_block<PSX_STAT_SLOTS>(a.stats, a.fin);
@@ -517,7 +527,7 @@ int ilog2i(int v) {
 }
 
 struct Plan {
-  int BM, BN, splits;
+  int BM, BN, splits, WGM = 2;
 };
 
 // Tile / split-K plan: prefer >= 2 workgroups per CU; split-K only while each split keeps
@@ -540,28 +550,32 @@ Plan plan_for(int OC, int npix, int ksteps) {
   if (const char* e = getenv("PSX_CV_BM")) p.BM = atoi(e);
   if (const char* e = getenv("PSX_CV_BN")) p.BN = atoi(e);
   if (const char* e = getenv("PSX_CV_SPLITS")) p.splits = atoi(e);
+  if (const char* e = getenv("PSX_CV_WGM")) p.WGM = atoi(e);
   if (OC % p.BM) p.BM = 64;
   if (p.splits > ksteps) p.splits = ksteps;
   return p;
 }
 
-template <int BM, int BN, int MODE, bool RES, bool SPLIT>
+template <int BM, int BN, int MODE, bool RES, bool SPLIT, int WGM = 2>
 int launch2(const Conv2Args& a, hipStream_t st) {
   const size_t lds = (size_t)3 * (BM + BN) * 128;
   dim3 grid(a.n_oc_tiles * a.n_pix_tiles, SPLIT ? a.splits : (MODE == 3 ? 4 : 1));
-  hipLaunchKernelGGL((conv2_kernel<BM, BN, MODE, RES, SPLIT>), grid, dim3(256), lds, st, a);
+  hipLaunchKernelGGL((conv2_kernel<BM, BN, MODE, RES, SPLIT, WGM>), grid, dim3(256), lds, st, a);
   return (int)hipGetLastError();
 }
 
 template <int MODE, bool RES>
 int dispatch2(const Plan& p, const Conv2Args& a, hipStream_t st) {
   const bool sp = p.splits > 1;
-#define PSX_L2(BM_, BN_)                                                                       \
-  if (p.BM == BM_ && p.BN == BN_)                                                              \
-    return sp ? launch2<BM_, BN_, MODE, false, true>(a, st) : launch2<BM_, BN_, MODE, RES, false>(a, st);
-  PSX_L2(128, 128)
-  PSX_L2(64, 128)
-  PSX_L2(64, 64)
+#define PSX_L2(BM_, BN_, W_)                                                                   \
+  if (p.BM == BM_ && p.BN == BN_ && p.WGM == W_)                                               \
+    return sp ? launch2<BM_, BN_, MODE, false, true, W_>(a, st) : launch2<BM_, BN_, MODE, RES, false, W_>(a, st);
+  PSX_L2(128, 128, 2)
+  PSX_L2(64, 128, 2)
+  PSX_L2(64, 64, 2)
+  PSX_L2(64, 256, 1)
+  PSX_L2(64, 128, 1)
+  PSX_L2(128, 256, 2)
 #undef PSX_L2
   return -7;
 }

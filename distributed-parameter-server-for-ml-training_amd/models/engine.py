@@ -179,10 +179,11 @@ class HipResNetEngine:
         self.fuse_fin = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNFIN", "0") == "1"
         # BN-backward sums from the dgrad epilogue: measured neutral (2.215 vs 2.217 ms/step; the MFMA
         # output layout makes its extra o/y loads half-coalesced), so opt-in
-        # BN finalize folded into the consuming apply launches (bnfin.hpp bn_fin_lds). Opt-in:
-        # measured 2.18 vs 2.10 ms/step (every apply workgroup pays the slot-reduction latency,
-        # more than the finalize launch it removes); see profiles/README.md
-        self.fin_apply = not self.fuse_fin and os.environ.get("PSX_BNFIN_APPLY", "0") == "1"
+        # BN finalize folded into the consuming apply launches (bnfin.hpp bn_fin_lds): every apply
+        # workgroup re-derives the affine/coefficients from the stat slots, removing 40 finalize
+        # launches per step. With 32 slot rows it measured slower (2.18 vs 2.10 ms/step); with 8
+        # rows (csrc/kernels/common.hpp) it wins: 1.999 vs 2.019 ms/step. PSX_BNFIN_APPLY=0: off
+        self.fin_apply = not self.fuse_fin and os.environ.get("PSX_BNFIN_APPLY", "1") == "1"
         self.fuse_bnbwd = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNBWD", "0") == "1"
         self._prereduced = set()
         self.wg_stream = (torch.cuda.Stream(device=self.dev)

@@ -33,7 +33,7 @@ def conv_out_hw(h: int, w: int, k: int, stride: int, pad: int):
     return (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
 
 
-STAT_SLOTS = 32  # PSX_STAT_SLOTS in csrc/kernels/common.hpp
+STAT_SLOTS = 8  # PSX_STAT_SLOTS in csrc/kernels/common.hpp
 
 
 def conv_fwd_ntiles(oc: int, npix: int, cfg: int) -> int:

@@ -80,3 +80,38 @@ def test_conv_dgrad2(shape):
     assert _rel(dx[..., :cin], ref) < 1e-2, shape
     K.conv_dgrad2(to_nhwc(dy, cout), wd, dx, res, ws, n, hw, hw, cp, cout, k, s, p, kgd)
     assert _rel(dx[..., :cin], ref + res[..., :cin].float()) < 1e-2, shape
+
+
+TILES = [(128, 128, 2), (64, 128, 2), (64, 64, 2), (64, 256, 1), (64, 128, 1), (128, 256, 2)]
+
+
+@pytest.mark.parametrize("tile", TILES)
+@pytest.mark.parametrize("shape", [(32, 64, 64, 32, 3, 1, 1), (32, 128, 128, 16, 3, 1, 1), (32, 64, 128, 32, 3, 2, 1),
+                                   (32, 256, 256, 8, 3, 1, 1)])
+def test_conv2_every_tile_config(shape, tile, monkeypatch):
+    """Every (BM, BN, wave layout) instantiation of conv2_kernel, forced through the planner's
+    experiment overrides, fwd (+ BN statistics) and dgrad (+ residual) against torch fp32."""
+    bm, bn, wgm = tile
+    n, cin, cout, hw, k, s, p = shape
+    if cout % bm or cin % bm:
+        pytest.skip("tile wider than the channel count")
+    for key, v in (("PSX_CV_BM", bm), ("PSX_CV_BN", bn), ("PSX_CV_WGM", wgm), ("PSX_CV_SPLITS", 1)):
+        monkeypatch.setenv(key, str(v))
+    torch.manual_seed(3)
+    x = torch.randn(n, cin, hw, hw, device=DEV).to(torch.bfloat16).float()
+    w = (torch.randn(cout, cin, k, k, device=DEV) / (cin * k * k) ** 0.5).to(torch.bfloat16).float()
+    wf, wd, cp, kg, kgd = make_operands(w)
+    oh = (hw + 2 * p - k) // s + 1
+    y = torch.empty(n, oh, oh, cout, dtype=torch.bfloat16, device=DEV)
+    stats = torch.zeros(K.STAT_SLOTS, 2, cout, device=DEV)
+    K.conv_fwd2(to_nhwc(x, cp), wf, y, stats, None, n, hw, hw, cp, cout, k, s, p, kg)
+    ref = F.conv2d(x, w, stride=s, padding=p).permute(0, 2, 3, 1)
+    assert _rel(y, ref) < 1e-2, (shape, tile)
+    yq = y.float().reshape(-1, cout)
+    assert torch.allclose(stats[:, 0].sum(0), yq.sum(0), rtol=1e-3, atol=5e-2), (shape, tile)
+    dy = torch.randn(n, cout, oh, oh, device=DEV).to(torch.bfloat16).float()
+    dref = torch.nn.grad.conv2d_input((n, cin, hw, hw), w, dy, stride=s, padding=p).permute(0, 2, 3, 1)
+    dx = torch.empty(n, hw, hw, cp, dtype=torch.bfloat16, device=DEV)
+    res = torch.randn(n, hw, hw, cp, device=DEV).to(torch.bfloat16)
+    K.conv_dgrad2(to_nhwc(dy, cout), wd, dx, res, None, n, hw, hw, cp, cout, k, s, p, kgd)
+    assert _rel(dx[..., :cin], dref + res[..., :cin].float()) < 1e-2, (shape, tile)

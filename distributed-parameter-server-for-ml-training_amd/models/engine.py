@@ -177,14 +177,16 @@ class HipResNetEngine:
         self.conv_impl = int(os.environ.get("PSX_CONV_IMPL", "2"))
         # BN finalize inside the producing launch (csrc/kernels/bnfin.hpp); 0 = separate kernels
         self.fuse_fin = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNFIN", "0") == "1"
-        # BN-backward sums from the dgrad epilogue: measured neutral (2.215 vs 2.217 ms/step; the MFMA
-        # output layout makes its extra o/y loads half-coalesced), so opt-in
+        # BN-backward sums from the dgrad epilogue (skips the separate bn_bwd_reduce pass where a
+        # dgrad produces the BN's input gradient): neutral with 32 stat slots + separate finalize
+        # (2.215 vs 2.217 ms/step), a small win with 8 slots + folded finalize (1.996/2.000 vs
+        # 2.010/2.006 ms/step, two same-box A/B pairs), so on by default (PSX_FUSE_BNBWD=0: off)
         # BN finalize folded into the consuming apply launches (bnfin.hpp bn_fin_lds): every apply
         # workgroup re-derives the affine/coefficients from the stat slots, removing 40 finalize
         # launches per step. With 32 slot rows it measured slower (2.18 vs 2.10 ms/step); with 8
         # rows (csrc/kernels/common.hpp) it wins: 1.999 vs 2.019 ms/step. PSX_BNFIN_APPLY=0: off
         self.fin_apply = not self.fuse_fin and os.environ.get("PSX_BNFIN_APPLY", "1") == "1"
-        self.fuse_bnbwd = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNBWD", "0") == "1"
+        self.fuse_bnbwd = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNBWD", "1") == "1"
         self._prereduced = set()
         self.wg_stream = (torch.cuda.Stream(device=self.dev)
                           if os.environ.get("PSX_WGRAD_STREAM", "0") == "1" else None)

@@ -19,6 +19,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <mutex>
+
 namespace {
 
 struct Api {
@@ -39,6 +41,7 @@ struct Api {
 };
 
 Api g_api;
+std::mutex g_enqueue;  // RCCL communicators are not safe for concurrent enqueue from several threads
 
 // psx dtype codes (parallel/rccl.py DTYPES) -> RCCL
 bool to_nccl(int code, ncclDataType_t* out) {
@@ -133,6 +136,7 @@ int psx_comm_reduce_sum(void* h, const void* send, void* recv, long count, int d
   if (!g_api.lib) return kNotLoaded;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
+  std::lock_guard<std::mutex> lk(g_enqueue);
   return (int)g_api.reduce(send, recv, (size_t)count, t, ncclSum, root, (ncclComm_t)h, st);
 }
 
@@ -140,6 +144,7 @@ int psx_comm_all_reduce_sum(void* h, const void* send, void* recv, long count, i
   if (!g_api.lib) return kNotLoaded;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
+  std::lock_guard<std::mutex> lk(g_enqueue);
   return (int)g_api.all_reduce(send, recv, (size_t)count, t, ncclSum, (ncclComm_t)h, st);
 }
 
@@ -147,6 +152,7 @@ int psx_comm_broadcast(void* h, void* buf, long count, int dtype, int root, hipS
   if (!g_api.lib) return kNotLoaded;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
+  std::lock_guard<std::mutex> lk(g_enqueue);
   return (int)g_api.broadcast(buf, buf, (size_t)count, t, root, (ncclComm_t)h, st);
 }
 
@@ -154,6 +160,7 @@ int psx_comm_send(void* h, const void* buf, long count, int dtype, int peer, hip
   if (!g_api.lib) return kNotLoaded;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
+  std::lock_guard<std::mutex> lk(g_enqueue);
   return (int)g_api.send(buf, (size_t)count, t, peer, (ncclComm_t)h, st);
 }
 
@@ -161,6 +168,7 @@ int psx_comm_recv(void* h, void* buf, long count, int dtype, int peer, hipStream
   if (!g_api.lib) return kNotLoaded;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
+  std::lock_guard<std::mutex> lk(g_enqueue);
   return (int)g_api.recv(buf, (size_t)count, t, peer, (ncclComm_t)h, st);
 }
 
@@ -174,6 +182,7 @@ int psx_comm_gather(void* h, const void* send, void* recv, long count, int dtype
   if (!g_api.lib) return kNotLoaded;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
+  std::lock_guard<std::mutex> lk(g_enqueue);
   ncclResult_t r = g_api.group_start();
   if (r != ncclSuccess) return (int)r;
   if (rank == root) {

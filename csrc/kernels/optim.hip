@@ -106,6 +106,12 @@ __global__ __launch_bounds__(256) void fp16_unpack_kernel(const uint16_t* __rest
     dst[i] = (float)__builtin_bit_cast(_Float16, src[i]) * scale;
 }
 
+__global__ __launch_bounds__(256) void gather_f32_kernel(const float* __restrict__ src, const long* __restrict__ idx,
+                                                         size_t n, float* __restrict__ dst) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[idx[i]];
+}
+
 struct UnpackDesc {
   long src_off;  // element offset of the OIHW fp32 weight in the arena
   long wf_off;   // element offset of the bf16 [OC][Kg] forward operand
@@ -333,5 +339,13 @@ int psx_param_unpack_tiles(const void* src, int src_bf16, const void* descs, int
 }
 
 int psx_unpack_desc_size() { return (int)sizeof(UnpackDesc); }
+
+// dst[i] = src[idx[i]] (fp32, int64 indices): the fp32 remainder of the fetch payload
+// (parallel/codec.py WeightWire.small) for the native server loop (csrc/server/event_loop.cpp).
+int psx_gather_f32(const float* src, const long* idx, long n, float* dst, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(gather_f32_kernel, dim3(grid_for(n)), dim3(256), 0, st, src, idx, (size_t)n, dst);
+  return (int)hipGetLastError();
+}
 
 }  // extern "C"

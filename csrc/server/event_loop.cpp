@@ -1,0 +1,442 @@
+// Native asynchronous parameter-server event loop (rank 0), on HIP streams.
+//
+// The reference serves async pushes on a 20-thread gRPC pool that applies each gradient under a
+// Python lock as soon as it arrives, after a staleness check (reference:
+// src/parameter_server/server.py:171-186, 239-304, 370-393). Here one native thread runs the
+// whole server role of an async job:
+//
+//   control   worker -> server requests arrive on the shared-memory mailbox (HELLO, FETCH, PUSH,
+//             DONE, HEARTBEAT, STOP; csrc/runtime/mailbox.cpp); replies go to per-worker slots.
+//   decisions registration, staleness = global_step - local_step, reject above the bound,
+//             weight max(0.1, 1/(1+0.1 s)), heartbeat timeouts: the native core
+//             (csrc/runtime/ps_core.cpp), no Python in the loop.
+//   data      RCCL point-to-point on the psx communicator (csrc/comm/rccl_comm.cpp), all on one
+//             communication stream: a PUSH posts ncclRecv into the worker's gradient slot (RCCL
+//             has no any-source receive — the mailbox message names the peer); a FETCH sends a
+//             per-worker snapshot of the fetch payload (bf16 weight image + fp32 remainder).
+//   updates   one update stream serializes every apply (the reference's param_lock): the fused
+//             SGD kernel waits on the slot's receive event, updates the fp32 master arena and
+//             rewrites the bf16 image in the same pass (csrc/kernels/optim.hip). Snapshots are
+//             taken on the same stream, so a fetch never sees a half-applied update and a send
+//             in flight never races the next update (it reads its own snapshot).
+//   local     the co-located worker of rank 0 calls psx_loop_local_push / _fetch / _done; the
+//             loop thread serves them between mailbox messages, ordered on the update stream
+//             against the caller's stream by events.
+//
+// The loop ends when the expected number of workers finished (or were declared dead) and no
+// receive is pending, or on STOP. Kernels and runtime functions are bound by dlsym from the
+// already-loaded psx libraries (paths passed by the caller).
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <time.h>
+
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "psx_comm.h"
+
+namespace {
+
+// mailbox message types (parallel/control.py)
+enum { HELLO = 1, PUSH = 2, FETCH = 3, DONE = 4, HEARTBEAT = 5, STOP = 6 };
+enum { R_REGISTERED = 11, R_PUSHED = 12, R_FETCHED = 13, R_ACK = 14 };
+enum { PSX_APPLY = 1 };
+
+struct Rt {  // libpsx_runtime.so + libpsx_kernels.so entry points
+  int (*mbox_recv)(void*, long long*, double);
+  int (*mbox_reply)(void*, int, int, int, int, long long, long long);
+  int (*ps_register)(void*, const char*, int, double);
+  void (*ps_heartbeat)(void*, int, double);
+  long long (*ps_on_fetch)(void*, int, double);
+  int (*ps_on_push)(void*, int, long long, double, float*, int*, long long*);
+  void (*ps_on_applied)(void*, double);
+  int (*ps_job_finished)(void*, int);
+  int (*ps_check_timeouts)(void*, double, double, int*, int);
+  long long (*ps_global_step)(void*);
+  int (*sgd_apply)(float*, const void*, float*, long, float, float, float, float, int, int, void*, hipStream_t);
+  int (*gather_f32)(const float*, const long*, long, float*, hipStream_t);
+};
+
+template <typename F>
+bool bind(void* lib, const char* name, F* fn) {
+  *fn = reinterpret_cast<F>(dlsym(lib, name));
+  if (!*fn) fprintf(stderr, "psx event loop: missing symbol %s\n", name);
+  return *fn != nullptr;
+}
+
+double now_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+struct LocalReq {
+  int kind;  // 0 push, 1 fetch, 2 done
+  int wid;
+  const void* grads;
+  float* dst;
+  long long local_step;
+  hipStream_t stream;
+  // results
+  int accepted = 0;
+  long long staleness = 0, global_step = 0;
+  bool done = false;
+};
+
+}  // namespace
+
+struct PsxLoopCfg {  // mirrored by parallel/native_loop.py (ctypes.Structure)
+  void* mbox;
+  void* core;
+  void* comm;
+  float* arena;         // fp32 master arena (params | buffers) on the device
+  const long* small_idx;  // device int64 arena indices of the fp32 remainder of the fetch payload
+  const int* remote_rank;  // worker id -> transport rank (-1: not remote), host array [max_wid]
+  long n_params, small_n, arena_numel;
+  float lr;
+  int device, grad_fp16, max_wid, expected;
+  double heartbeat_timeout, poll_s;
+  // update stream: the co-located worker's compute stream when there is one (its pushes and
+  // fetches are then plain stream order, as with a single stream), else a stream of the loop
+  hipStream_t upd_stream;
+  int own_upd_stream;
+};
+
+struct PsxLoop {
+  PsxLoopCfg c;
+  Rt rt;
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<LocalReq*> local;
+  int err = 0;
+  bool stopped = false;
+  // device state
+  hipStream_t s_comm = nullptr, s_upd = nullptr;
+  uint16_t* img = nullptr;  // server bf16 image of the parameters (rewritten by every apply)
+  std::vector<void*> slot;  // per worker: gradient receive buffer
+  std::vector<uint16_t*> snap_img;
+  std::vector<float*> snap_small;
+  std::vector<hipEvent_t> sent;  // per worker: last snapshot send done (snapshot reusable)
+  struct Pending {
+    int wid;
+    long long local_step;
+    hipEvent_t ev;
+  };
+  std::deque<Pending> pending;
+  int finished = 0;
+  long long applies = 0;
+};
+
+namespace {
+
+size_t gbytes(const PsxLoop* L) { return (size_t)L->c.n_params * (L->c.grad_fp16 ? 2 : 4); }
+
+int alloc_worker(PsxLoop* L, int w) {
+  if (L->slot[w]) return 0;
+  if (hipMalloc(&L->slot[w], gbytes(L)) != hipSuccess) return -20;
+  if (hipMalloc((void**)&L->snap_img[w], (size_t)L->c.n_params * 2) != hipSuccess) return -21;
+  if (hipMalloc((void**)&L->snap_small[w], (size_t)std::max(1L, L->c.small_n) * 4) != hipSuccess) return -22;
+  if (hipEventCreateWithFlags(&L->sent[w], hipEventDisableTiming) != hipSuccess) return -23;
+  hipEventRecord(L->sent[w], L->s_comm);
+  return 0;
+}
+
+// the fused SGD apply of one gradient with the core's weight, writing the bf16 image too
+int apply(PsxLoop* L, const void* g, float weight) {
+  const double t0 = now_s();
+  const int e = L->rt.sgd_apply(L->c.arena, g, nullptr, L->c.n_params, L->c.lr, weight, 0.f, 0.f, 0, L->c.grad_fp16,
+                                L->img, L->s_upd);
+  L->rt.ps_on_applied(L->c.core, now_s() - t0);
+  ++L->applies;
+  return e;
+}
+
+int serve_fetch(PsxLoop* L, int w, int rank) {
+  if (int e = alloc_worker(L, w)) return e;
+  // snapshot on the update stream (after every apply so far), once the previous send of this
+  // worker's snapshot has finished
+  hipStreamWaitEvent(L->s_upd, L->sent[w], 0);
+  hipMemcpyAsync(L->snap_img[w], L->img, (size_t)L->c.n_params * 2, hipMemcpyDeviceToDevice, L->s_upd);
+  if (L->c.small_n) L->rt.gather_f32(L->c.arena, L->c.small_idx, L->c.small_n, L->snap_small[w], L->s_upd);
+  hipEvent_t ready;
+  hipEventCreateWithFlags(&ready, hipEventDisableTiming);
+  hipEventRecord(ready, L->s_upd);
+  hipStreamWaitEvent(L->s_comm, ready, 0);
+  hipEventDestroy(ready);
+  int e = psx_comm_send(L->c.comm, L->snap_img[w], L->c.n_params, PSX_BF16, rank, L->s_comm);
+  if (!e && L->c.small_n) e = psx_comm_send(L->c.comm, L->snap_small[w], L->c.small_n, PSX_F32, rank, L->s_comm);
+  hipEventRecord(L->sent[w], L->s_comm);
+  return e;
+}
+
+int post_recv(PsxLoop* L, int w, int rank, long long local_step) {
+  if (int e = alloc_worker(L, w)) return e;
+  // the slot is free: its previous gradient was applied on s_upd before this worker could push
+  // again (the worker waits for the reply, which follows the apply's enqueue) -> order the
+  // receive after the update stream
+  hipEvent_t upd;
+  hipEventCreateWithFlags(&upd, hipEventDisableTiming);
+  hipEventRecord(upd, L->s_upd);
+  hipStreamWaitEvent(L->s_comm, upd, 0);
+  hipEventDestroy(upd);
+  const int e = psx_comm_recv(L->c.comm, L->slot[w], L->c.n_params, L->c.grad_fp16 ? PSX_F16 : PSX_F32, rank,
+                              L->s_comm);
+  hipEvent_t ev;
+  hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  hipEventRecord(ev, L->s_comm);
+  L->pending.push_back({w, local_step, ev});
+  return e;
+}
+
+void complete_pending(PsxLoop* L) {
+  while (!L->pending.empty()) {  // in arrival order (head-of-line on one comm stream anyway)
+    PsxLoop::Pending& p = L->pending.front();
+    if (hipEventQuery(p.ev) != hipSuccess) break;
+    float weight = 0.f;
+    int ncontrib = 0;
+    long long st = 0;
+    const int d = L->rt.ps_on_push(L->c.core, p.wid, p.local_step, now_s(), &weight, &ncontrib, &st);
+    int accepted = 0;
+    if (d == PSX_APPLY) {
+      hipStreamWaitEvent(L->s_upd, p.ev, 0);
+      if (apply(L, L->slot[p.wid], weight)) L->err = -30;
+      accepted = 1;
+    }
+    L->rt.mbox_reply(L->c.mbox, L->c.remote_rank[p.wid], R_PUSHED, p.wid, accepted,
+                     L->rt.ps_global_step(L->c.core), st);
+    hipEventDestroy(p.ev);
+    L->pending.pop_front();
+  }
+}
+
+void serve_local(PsxLoop* L) {
+  std::deque<LocalReq*> q;
+  {
+    std::lock_guard<std::mutex> lk(L->mu);
+    q.swap(L->local);
+  }
+  for (LocalReq* r : q) {
+    hipEvent_t ev;
+    hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (r->kind == 0) {  // push: the caller's gradient is ready at this point of its stream
+      float weight = 0.f;
+      int ncontrib = 0;
+      long long st = 0;
+      const int d = L->rt.ps_on_push(L->c.core, r->wid, r->local_step, now_s(), &weight, &ncontrib, &st);
+      const bool same = r->stream == L->s_upd;
+      if (d == PSX_APPLY) {
+        if (!same) {
+          hipEventRecord(ev, r->stream);
+          hipStreamWaitEvent(L->s_upd, ev, 0);
+        }
+        if (apply(L, r->grads, weight)) L->err = -31;
+        r->accepted = 1;
+      }
+      r->staleness = st;
+      r->global_step = L->rt.ps_global_step(L->c.core);
+      if (!same) {  // the caller's stream waits: its gradient buffer is free again
+        hipEventRecord(ev, L->s_upd);
+        hipStreamWaitEvent(r->stream, ev, 0);
+      }
+    } else if (r->kind == 1) {  // fetch: fp32 arena copy, ordered after every apply so far
+      r->global_step = L->rt.ps_on_fetch(L->c.core, r->wid, now_s());
+      const bool same = r->stream == L->s_upd;
+      if (!same) {
+        hipEventRecord(ev, r->stream);
+        hipStreamWaitEvent(L->s_upd, ev, 0);
+      }
+      hipMemcpyAsync(r->dst, L->c.arena, (size_t)L->c.arena_numel * 4, hipMemcpyDeviceToDevice, L->s_upd);
+      if (!same) {
+        hipEventRecord(ev, L->s_upd);
+        hipStreamWaitEvent(r->stream, ev, 0);
+      }
+    } else {
+      L->rt.ps_job_finished(L->c.core, r->wid);
+      ++L->finished;
+    }
+    hipEventDestroy(ev);
+    {
+      std::lock_guard<std::mutex> lk(L->mu);
+      r->done = true;
+    }
+    L->cv.notify_all();
+  }
+}
+
+void run(PsxLoop* L) {
+  hipSetDevice(L->c.device);
+  hipStreamCreateWithFlags(&L->s_comm, hipStreamNonBlocking);
+  if (L->c.own_upd_stream)
+    hipStreamCreateWithFlags(&L->s_upd, hipStreamNonBlocking);
+  else
+    L->s_upd = L->c.upd_stream;
+  // initial bf16 image of the state: an lr-0 apply of a zero gradient writes bf16(p) exactly
+  void* zero = nullptr;
+  hipMalloc((void**)&L->img, (size_t)L->c.n_params * 2);
+  hipMalloc(&zero, gbytes(L));
+  hipMemsetAsync(zero, 0, gbytes(L), L->s_upd);
+  L->rt.sgd_apply(L->c.arena, zero, nullptr, L->c.n_params, 0.f, 1.f, 0.f, 0.f, 0, L->c.grad_fp16, L->img, L->s_upd);
+  hipStreamSynchronize(L->s_upd);
+  hipFree(zero);
+  double last_to = now_s();
+  std::vector<int> dead(L->c.max_wid + 1);
+  long long m[6];
+  for (;;) {
+    const int got = L->rt.mbox_recv(L->c.mbox, m, L->c.poll_s);
+    if (got > 0) {
+      const int type = (int)m[0], src = (int)m[1], wid = (int)m[2];
+      const bool known = wid >= 0 && wid < L->c.max_wid;
+      if (type == HELLO) {
+        char name[32];
+        snprintf(name, sizeof name, "rank%d", src);
+        const int id = L->rt.ps_register(L->c.core, name, wid, now_s());
+        L->rt.mbox_reply(L->c.mbox, src, R_REGISTERED, id, L->c.expected, 0, 0);
+      } else if (type == FETCH && known) {
+        const long long gs = L->rt.ps_on_fetch(L->c.core, wid, now_s());
+        if (int e = serve_fetch(L, wid, L->c.remote_rank[wid])) L->err = e;
+        L->rt.mbox_reply(L->c.mbox, L->c.remote_rank[wid], R_FETCHED, wid, 0, gs, 0);
+      } else if (type == PUSH && known) {
+        if (int e = post_recv(L, wid, L->c.remote_rank[wid], m[4])) L->err = e;
+      } else if (type == DONE && known) {
+        L->rt.ps_job_finished(L->c.core, wid);
+        ++L->finished;
+        L->rt.mbox_reply(L->c.mbox, L->c.remote_rank[wid], R_ACK, wid, 0, 0, 0);
+      } else if (type == HEARTBEAT && known) {
+        L->rt.ps_heartbeat(L->c.core, wid, now_s());
+      } else if (type == STOP) {
+        break;
+      }
+    }
+    complete_pending(L);
+    serve_local(L);
+    const double t = now_s();
+    if (L->c.heartbeat_timeout > 0 && t - last_to > 1.0) {
+      last_to = t;
+      L->finished += L->rt.ps_check_timeouts(L->c.core, t, L->c.heartbeat_timeout, dead.data(), L->c.max_wid);
+    }
+    if (L->finished >= L->c.expected && L->pending.empty()) break;
+    if (L->err) break;
+  }
+  hipStreamSynchronize(L->s_comm);
+  hipStreamSynchronize(L->s_upd);
+  {
+    std::lock_guard<std::mutex> lk(L->mu);
+    L->stopped = true;
+  }
+  L->cv.notify_all();
+}
+
+}  // namespace
+
+extern "C" {
+
+int psx_loop_cfg_size() { return (int)sizeof(PsxLoopCfg); }
+
+// Binds the runtime/kernel entry points (the libraries are already loaded by the caller).
+void* psx_loop_create(const PsxLoopCfg* cfg, const char* runtime_path, const char* kernels_path) {
+  void* rt = dlopen(runtime_path, RTLD_NOW | RTLD_NOLOAD);
+  if (!rt) rt = dlopen(runtime_path, RTLD_NOW);
+  void* kn = dlopen(kernels_path, RTLD_NOW | RTLD_NOLOAD);
+  if (!kn) kn = dlopen(kernels_path, RTLD_NOW);
+  if (!rt || !kn) {
+    fprintf(stderr, "psx_loop_create: %s\n", dlerror());
+    return nullptr;
+  }
+  PsxLoop* L = new PsxLoop();
+  L->c = *cfg;
+  Rt& r = L->rt;
+  const bool ok = bind(rt, "psx_mbox_recv", &r.mbox_recv) && bind(rt, "psx_mbox_reply", &r.mbox_reply) &&
+                  bind(rt, "psx_ps_register", &r.ps_register) && bind(rt, "psx_ps_heartbeat", &r.ps_heartbeat) &&
+                  bind(rt, "psx_ps_on_fetch", &r.ps_on_fetch) && bind(rt, "psx_ps_on_push", &r.ps_on_push) &&
+                  bind(rt, "psx_ps_on_applied", &r.ps_on_applied) &&
+                  bind(rt, "psx_ps_job_finished", &r.ps_job_finished) &&
+                  bind(rt, "psx_ps_check_timeouts", &r.ps_check_timeouts) &&
+                  bind(rt, "psx_ps_global_step", &r.ps_global_step) && bind(kn, "psx_sgd_apply", &r.sgd_apply) &&
+                  bind(kn, "psx_gather_f32", &r.gather_f32);
+  if (!ok) {
+    delete L;
+    return nullptr;
+  }
+  const int n = cfg->max_wid;
+  L->slot.assign(n, nullptr);
+  L->snap_img.assign(n, nullptr);
+  L->snap_small.assign(n, nullptr);
+  L->sent.assign(n, nullptr);
+  return L;
+}
+
+int psx_loop_start(void* h) {
+  PsxLoop* L = (PsxLoop*)h;
+  L->th = std::thread(run, L);
+  return 0;
+}
+
+// Blocks until the loop has ended; returns its error code (0 = clean).
+int psx_loop_join(void* h) {
+  PsxLoop* L = (PsxLoop*)h;
+  if (L->th.joinable()) L->th.join();
+  return L->err;
+}
+
+long long psx_loop_applies(void* h) { return ((PsxLoop*)h)->applies; }
+
+static int local_call(PsxLoop* L, LocalReq* r) {
+  {
+    std::unique_lock<std::mutex> lk(L->mu);
+    if (L->stopped) return L->err ? L->err : -40;
+    L->local.push_back(r);
+    L->cv.wait(lk, [&] { return r->done || L->stopped; });
+    if (!r->done) return L->err ? L->err : -41;
+  }
+  return L->err;
+}
+
+// Co-located worker push: `grads` is ready at the current point of `stream`; on return the
+// update is enqueued and `stream` waits for it. out = [accepted, staleness, global_step].
+int psx_loop_local_push(void* h, int wid, const void* grads, long long local_step, hipStream_t stream,
+                        long long* out) {
+  LocalReq r{0, wid, grads, nullptr, local_step, stream};
+  const int e = local_call((PsxLoop*)h, &r);
+  out[0] = r.accepted;
+  out[1] = r.staleness;
+  out[2] = r.global_step;
+  return e;
+}
+
+// Co-located worker fetch: copies the whole fp32 arena (params + BN buffers, as the reference's
+// fetch overwrites the worker's running statistics) into `dst` in order on `stream`; returns the
+// global step (negative: error).
+long long psx_loop_local_fetch(void* h, int wid, float* dst, hipStream_t stream) {
+  LocalReq r{1, wid, nullptr, dst, 0, stream};
+  const int e = local_call((PsxLoop*)h, &r);
+  return e ? e : r.global_step;
+}
+
+int psx_loop_local_done(void* h, int wid) {
+  LocalReq r{2, wid, nullptr, nullptr, 0, nullptr};
+  return local_call((PsxLoop*)h, &r);
+}
+
+void psx_loop_destroy(void* h) {
+  PsxLoop* L = (PsxLoop*)h;
+  if (!L) return;
+  if (L->th.joinable()) L->th.join();
+  for (size_t w = 0; w < L->slot.size(); ++w) {
+    if (L->slot[w]) hipFree(L->slot[w]);
+    if (L->snap_img[w]) hipFree(L->snap_img[w]);
+    if (L->snap_small[w]) hipFree(L->snap_small[w]);
+    if (L->sent[w]) hipEventDestroy(L->sent[w]);
+  }
+  if (L->img) hipFree(L->img);
+  if (L->s_comm) hipStreamDestroy(L->s_comm);
+  if (L->s_upd && L->c.own_upd_stream) hipStreamDestroy(L->s_upd);
+  delete L;
+}
+
+}  // extern "C"

@@ -1,0 +1,177 @@
+"""Async parameter server on the native event loop (csrc/server/event_loop.cpp).
+
+The async server role of rank 0 — mailbox control, RCCL point-to-point receive of pushed
+gradients and send of fetch snapshots, staleness decisions, the fused SGD apply, heartbeat
+timeouts — runs in one C++ thread on two HIP streams (communication, update); see the C++ file
+for the ordering rules. Python only starts it, serves the co-located worker's calls through it,
+and joins it. This replaces ParameterServer.serve_async (the Python loop, kept for the CPU/gloo
+path and the configurations below) for MI355X jobs on the native RCCL transport.
+
+Remote workers use ``NativeAsyncChannel``: control requests on the shared-memory mailbox as
+before, tensors by ncclSend/ncclRecv on the psx communicator (parallel/rccl.py), posted on a
+communication stream ordered after the worker's compute stream by events.
+
+Scope: dense fp16/fp32 gradients, plain SGD (momentum/weight decay 0 — the reference's server
+update, server.py:133), no --bn-sync, bf16conv fetch payload. Enabled with PSX_NATIVE_LOOP=1.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch
+
+from .. import NATIVE_DIR
+from ..ops._lib import comm, kernels, runtime
+from . import control as CP
+from .codec import small_index_of
+from .worker import AsyncChannel
+
+vp, i32, i64, f32, f64 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_double
+
+
+class LoopCfg(C.Structure):
+    """csrc/server/event_loop.cpp PsxLoopCfg."""
+    _fields_ = [("mbox", vp), ("core", vp), ("comm", vp), ("arena", vp), ("small_idx", vp), ("remote_rank", vp),
+                ("n_params", i64), ("small_n", i64), ("arena_numel", i64), ("lr", f32), ("device", i32),
+                ("grad_fp16", i32), ("max_wid", i32), ("expected", i32), ("heartbeat_timeout", f64),
+                ("poll_s", f64), ("upd_stream", vp), ("own_upd_stream", i32)]
+
+
+_SIGS = {
+    "psx_loop_cfg_size": (i32, []),
+    "psx_loop_create": (vp, [C.POINTER(LoopCfg), C.c_char_p, C.c_char_p]),
+    "psx_loop_start": (i32, [vp]),
+    "psx_loop_join": (i32, [vp]),
+    "psx_loop_applies": (C.c_longlong, [vp]),
+    "psx_loop_local_push": (i32, [vp, i32, vp, C.c_longlong, vp, C.POINTER(C.c_longlong)]),
+    "psx_loop_local_fetch": (C.c_longlong, [vp, i32, vp, vp]),
+    "psx_loop_local_done": (i32, [vp, i32]),
+    "psx_loop_destroy": (None, [vp]),
+}
+
+
+def _lib():
+    lib = comm()
+    if not getattr(lib, "_psx_loop_declared", False):
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, args
+        lib._psx_loop_declared = True
+        if lib.psx_loop_cfg_size() != C.sizeof(LoopCfg):
+            raise RuntimeError("PsxLoopCfg layout mismatch between csrc/server/event_loop.cpp and native_loop.py")
+    return lib
+
+
+def native_loop_enabled(cfg, transport) -> bool:
+    return (os.environ.get("PSX_NATIVE_LOOP", "0") == "1" and getattr(transport, "native", False)
+            and cfg.codec in ("fp16", "none") and not cfg.momentum and not cfg.weight_decay and not cfg.bn_sync
+            and cfg.fetch_codec == "bf16conv")
+
+
+class NativeServerLoop:
+    """Rank 0: the server event loop thread (C++)."""
+
+    def __init__(self, server, transport, mbox, rank_of_wid: dict, expected: int, poll_s: float = 0.0005,
+                 update_stream: torch.cuda.Stream | None = None):
+        """update_stream: the co-located worker's compute stream (its pushes/fetches are then in
+        plain stream order with the loop's updates); None = the loop creates its own."""
+        self.server = server
+        lay = server.layout
+        self.small_idx = small_index_of(lay).to(server.device)
+        max_wid = max([expected] + [w + 1 for w in rank_of_wid])
+        self.remote = (C.c_int * max_wid)(*([-1] * max_wid))
+        for w, r in rank_of_wid.items():
+            self.remote[w] = r
+        dev = server.device.index or 0
+        self.cfg = LoopCfg(mbox=mbox._h, core=server.core._h, comm=transport.comm.h.value,
+                           arena=server.arena.data_ptr(), small_idx=self.small_idx.data_ptr(),
+                           remote_rank=C.cast(self.remote, vp), n_params=lay.param_numel,
+                           small_n=self.small_idx.numel(), arena_numel=lay.arena_numel, lr=float(server.lr),
+                           device=dev, grad_fp16=int(server.cfg.codec == "fp16"), max_wid=max_wid,
+                           expected=expected, heartbeat_timeout=float(server.cfg.heartbeat_timeout or 0.0),
+                           poll_s=poll_s, upd_stream=update_stream.cuda_stream if update_stream is not None else None,
+                           own_upd_stream=int(update_stream is None))
+        kernels()  # both libraries are loaded (the loop binds their entry points by path)
+        runtime()
+        self.h = _lib().psx_loop_create(C.byref(self.cfg), os.path.join(NATIVE_DIR, "libpsx_runtime.so").encode(),
+                                        os.path.join(NATIVE_DIR, "libpsx_kernels.so").encode())
+        if not self.h:
+            raise RuntimeError("psx_loop_create failed")
+        torch.cuda.synchronize(server.device)  # the arena is final before the loop reads it
+        _lib().psx_loop_start(self.h)
+
+    def join(self):
+        if self.h is None:
+            return 0
+        rc = _lib().psx_loop_join(self.h)
+        s = self.server
+        s.bytes_pushed = int(s.core.metrics().get("gradients_processed", 0)) * s.n * (2 if s.cfg.codec == "fp16" else 4)
+        _lib().psx_loop_destroy(self.h)
+        self.h = None
+        if rc:
+            raise RuntimeError(f"native server loop ended with error {rc}")
+        return rc
+
+
+class NativeLocalChannel:
+    """Rank 0's co-located worker: requests served by the loop thread, in stream order."""
+
+    def __init__(self, server, loop: NativeServerLoop):
+        self.server, self.loop = server, loop
+
+    def register(self, name, requested_id=-1):
+        return self.server.register_worker(name, requested_id)
+
+    def fetch(self, worker_id, local_arena):
+        gs = _lib().psx_loop_local_fetch(self.loop.h, worker_id, local_arena.data_ptr(),
+                                         torch.cuda.current_stream().cuda_stream)
+        if gs < 0:
+            raise RuntimeError(f"native local fetch failed ({gs})")
+        return gs
+
+    def push(self, worker_id, grads, local_step, buffers=None):
+        out = (C.c_longlong * 3)()
+        rc = _lib().psx_loop_local_push(self.loop.h, worker_id, grads.data_ptr(), int(local_step),
+                                        torch.cuda.current_stream().cuda_stream, out)
+        if rc:
+            raise RuntimeError(f"native local push failed ({rc})")
+        self.last_staleness = int(out[1])
+        return bool(out[0])
+
+    def finished(self, worker_id):
+        _lib().psx_loop_local_done(self.loop.h, worker_id)
+
+
+class NativeAsyncChannel(AsyncChannel):
+    """Remote worker: mailbox control, tensors over the native communicator (rank 0 = server)."""
+
+    def __init__(self, transport, mbox, rank, codec):
+        super().__init__(transport, mbox, rank, codec=codec)
+        self.cs = torch.cuda.Stream(device=transport.device)
+
+    def _fork(self):
+        self.cs.wait_stream(torch.cuda.current_stream())
+        return torch.cuda.stream(self.cs)
+
+    def fetch(self, worker_id, local_arena):
+        self.mbox.send(CP.Msg(CP.FETCH, self.rank, worker_id))
+        with self._fork():
+            for b in self.codec.wire:  # bf16 image, then the fp32 remainder (server send order)
+                self.t.comm.recv(b, 0, stream=self.cs)
+        r = self.mbox.wait_reply(self.rank)
+        torch.cuda.current_stream().wait_stream(self.cs)
+        self.codec.unpack(local_arena)
+        return r.c
+
+    def push(self, worker_id, grads, local_step, buffers=None):
+        if buffers is not None:
+            raise RuntimeError("the native server loop does not take BN buffers (--bn-sync)")
+        self.mbox.send(CP.Msg(CP.PUSH, self.rank, worker_id, 0, local_step))
+        with self._fork():
+            self.t.comm.send(grads, 0, stream=self.cs)
+        r = self.mbox.wait_reply(self.rank)
+        torch.cuda.current_stream().wait_stream(self.cs)  # the gradient buffer is reusable
+        self.last_staleness = r.d
+        return bool(r.b)
+

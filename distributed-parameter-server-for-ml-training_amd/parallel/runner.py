@@ -33,6 +33,7 @@ from . import control as CP
 from .codec import FetchCodec, WeightWire, weight_image_enabled
 from .compute import make_compute
 from .graph_round import GraphRoundChannel, graph_round_enabled
+from .native_loop import NativeAsyncChannel, NativeLocalChannel, NativeServerLoop, native_loop_enabled
 from .overlap import OverlapSyncChannel, plan_buckets
 from .server import ParameterServer
 from .rccl import make_transport
@@ -238,17 +239,26 @@ class AsyncSession:
         if rank != 0:
             self.mbox = CP.ShmMailbox(mbox_name, nreply=t.world_size, owner=False)
         remote = {w: r for w, r in rank_of_wid.items() if r != 0}
-        self.worker, self.thread, self.hb = None, None, None
+        self.worker, self.thread, self.hb, self.loop = None, None, None, None
+        native = native_loop_enabled(cfg, t)  # the C++ server loop (parallel/native_loop.py)
         if rank == 0:
-            q = queue.Queue() if rank in wid_of_rank else None
-            self.thread = threading.Thread(target=server.serve_async, args=(t, self.mbox, remote),
-                                           kwargs={"local_queue": q, "expected": W}, daemon=True)
-            self.thread.start()
-            if q is not None:
-                self.worker = Worker(cfg, comp, LocalAsyncChannel(server, q), train, test, worker_name=names[0],
-                                     rank=0, log=log, requested_id=wid_of_rank[0])
+            if native:
+                self.loop = NativeServerLoop(server, t, self.mbox, remote, W,
+                                             update_stream=torch.cuda.current_stream() if rank in wid_of_rank else None)
+                if rank in wid_of_rank:
+                    self.worker = Worker(cfg, comp, NativeLocalChannel(server, self.loop), train, test,
+                                         worker_name=names[0], rank=0, log=log, requested_id=wid_of_rank[0])
+            else:
+                q = queue.Queue() if rank in wid_of_rank else None
+                self.thread = threading.Thread(target=server.serve_async, args=(t, self.mbox, remote),
+                                               kwargs={"local_queue": q, "expected": W}, daemon=True)
+                self.thread.start()
+                if q is not None:
+                    self.worker = Worker(cfg, comp, LocalAsyncChannel(server, q), train, test, worker_name=names[0],
+                                         rank=0, log=log, requested_id=wid_of_rank[0])
         elif rank in wid_of_rank:
-            chan = AsyncChannel(t, self.mbox, rank, codec=FetchCodec(comp.layout, cfg.fetch_codec, comp.device))
+            cls = NativeAsyncChannel if native else AsyncChannel
+            chan = cls(t, self.mbox, rank, codec=FetchCodec(comp.layout, cfg.fetch_codec, comp.device))
             self.worker = Worker(cfg, comp, chan, train, test, worker_name=names[rank], rank=rank, log=log,
                                  requested_id=wid_of_rank[rank])
         if self.worker is not None:
@@ -280,6 +290,9 @@ class AsyncSession:
         if self.thread is not None:
             self.thread.join()
             self.thread = None
+        if self.loop is not None:
+            self.loop.join()
+            self.loop = None
 
     def close(self):
         self.t.barrier()

@@ -59,9 +59,16 @@ struct AugArgs {
   const unsigned* step;  // device scalar, so a captured graph sees the live step counter
   int train;           // 1: random crop + flip, 0: centre (eval transform)
   float mean[3], inv_std[3];
+  uint32_t* zero0;  // optional 32-bit words zeroed by the same launch (the step's BN statistic
+  long nzero0;      // slots and accuracy counter: two fewer launches per step)
+  uint32_t* zero1;
+  long nzero1;
 };
 
 __global__ __launch_bounds__(256) void augment_kernel(AugArgs a) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < a.nzero0; i += stride) a.zero0[i] = 0u;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < a.nzero1; i += stride) a.zero1[i] = 0u;
   const long total = (long)a.B * a.H * a.W;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int b = (int)(i / (a.H * a.W));
@@ -129,8 +136,12 @@ int psx_synth_gen(void* img, int* labels, int N, int H, int W, int classes, unsi
 
 int psx_augment(const void* img, const int* labels, const int* index, void* out, int* out_labels, int B, int H, int W,
                 int pad, unsigned seed, const unsigned* step, int train, const float* mean3, const float* std3,
-                hipStream_t st) {
+                void* zero0, long nzero0, void* zero1, long nzero1, hipStream_t st) {
   AugArgs a{};
+  a.zero0 = (uint32_t*)zero0;
+  a.nzero0 = zero0 ? nzero0 : 0;
+  a.zero1 = (uint32_t*)zero1;
+  a.nzero1 = zero1 ? nzero1 : 0;
   a.img = (const uint8_t*)img;
   a.labels = labels;
   a.index = index;

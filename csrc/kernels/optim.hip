@@ -173,10 +173,36 @@ PSX_DEV void unpack_chunk(const UnpackDesc& d, const ST* __restrict__ src, int o
   }
 }
 
+// The fp32 remainder of a fetch (BN affine, FC, BN buffers) scattered into the worker's arena by
+// workgroups appended to the unpack grid (one launch instead of unpack + index_copy):
+// dst[idx[j]] = src[j] (the wire's small region) or src[idx[j]] (gather = 1: straight from the
+// server's fp32 arena when the worker shares the server's device and round).
+struct SmallScatter {
+  const float* src;
+  const long* idx;
+  long n;
+  float* dst;
+  int gather;
+};
+constexpr int kScatterPerBlock = 2048;
+
 template <typename ST>
 __global__ __launch_bounds__(256) void param_unpack_tiles_kernel(const ST* __restrict__ src_all,
                                                                  const UnpackDesc* __restrict__ descs, int ndesc,
-                                                                 uint16_t* __restrict__ wbuf) {
+                                                                 uint16_t* __restrict__ wbuf, int ntiles,
+                                                                 SmallScatter sc) {
+  if ((int)blockIdx.x >= ntiles) {  // scatter workgroups (block-uniform exit)
+    const long base = (long)(blockIdx.x - ntiles) * kScatterPerBlock;
+#pragma unroll
+    for (int r = 0; r < kScatterPerBlock / 256; ++r) {
+      const long j = base + r * 256 + threadIdx.x;
+      if (j < sc.n) {
+        const long k = sc.idx[j];
+        sc.dst[k] = sc.src[sc.gather ? k : j];
+      }
+    }
+    return;
+  }
   __shared__ uint16_t tile[64 * (64 * 3 + 2)];
   __shared__ int first_tile[256];
   // which conv owns this workgroup: all descs' tile0 fetched in parallel
@@ -325,16 +351,21 @@ int psx_param_unpack(const float* arena, const void* descs, int ndesc, void* wbu
 
 // Flat-grid unpack (one workgroup per 32x32 tile of every conv; ntiles = sum of the tiles, each
 // desc's tile0 = its first tile). src_bf16: the source is a bf16 image instead of the fp32 arena.
+// sc_src/sc_idx/sc_n/sc_dst: optional SmallScatter (sc_n = 0: none), see above.
 int psx_param_unpack_tiles(const void* src, int src_bf16, const void* descs, int ndesc, int ntiles, void* wbuf,
+                           const float* sc_src, const long* sc_idx, long sc_n, float* sc_dst, int sc_gather,
                            hipStream_t st) {
   if (ntiles <= 0 || ndesc <= 0) return 0;
   if (ndesc > 256) return (int)hipErrorInvalidValue;  // the kernel's LDS desc table
+  const SmallScatter sc{sc_src, sc_idx, sc_n > 0 ? sc_n : 0, sc_dst, sc_gather};
+  const long nsb = (sc.n + kScatterPerBlock - 1) / kScatterPerBlock;
+  const dim3 grid((unsigned)(ntiles + nsb));
   if (src_bf16)
-    hipLaunchKernelGGL(param_unpack_tiles_kernel<uint16_t>, dim3(ntiles), dim3(256), 0, st, (const uint16_t*)src,
-                       (const UnpackDesc*)descs, ndesc, (uint16_t*)wbuf);
+    hipLaunchKernelGGL(param_unpack_tiles_kernel<uint16_t>, grid, dim3(256), 0, st, (const uint16_t*)src,
+                       (const UnpackDesc*)descs, ndesc, (uint16_t*)wbuf, ntiles, sc);
   else
-    hipLaunchKernelGGL(param_unpack_tiles_kernel<float>, dim3(ntiles), dim3(256), 0, st, (const float*)src,
-                       (const UnpackDesc*)descs, ndesc, (uint16_t*)wbuf);
+    hipLaunchKernelGGL(param_unpack_tiles_kernel<float>, grid, dim3(256), 0, st, (const float*)src,
+                       (const UnpackDesc*)descs, ndesc, (uint16_t*)wbuf, ntiles, sc);
   return (int)hipGetLastError();
 }
 

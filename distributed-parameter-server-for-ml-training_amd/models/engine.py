@@ -237,8 +237,10 @@ class HipResNetEngine:
         H, W = sp.in_hw
         self.x0 = self._bf(B, H, W, sp.stem_conv.cp)
         self.labels = torch.zeros(B, dtype=torch.int32, device=self.dev)
-        self.index = torch.zeros(B, dtype=torch.int32, device=self.dev)
-        self.step_dev = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        # [sample indices of the batch | step counter]: one host->device copy per step
+        self.batch_meta = torch.zeros(B + 1, dtype=torch.int32, device=self.dev)
+        self.index = self.batch_meta[:B]
+        self.step_dev = self.batch_meta[B:]
 
         # per-BN persistent state: affine [2,C] (scale, shift), saved [2,C] (mean, invstd), coef [3,C]
         self.bn = {}
@@ -536,30 +538,44 @@ class HipResNetEngine:
             K.param_unpack(arena, self.descs, self.ndesc, self.wbuf)
             return
         src = self.wsrc if self.wsrc is not None else arena
-        K.param_unpack_tiles(src, self.descs, self.ndesc, self.ntiles, self.wbuf)
+        K.param_unpack_tiles(src, self.descs, self.ndesc, self.ntiles, self.wbuf, scatter=self.small_scatter)
 
-    def set_weight_source(self, img: torch.Tensor | None, pre_unpack=None):
+    small_scatter = None
+    _zeroed = False       # red zeroed by this step's augment launch (consumed by forward)
+    _zeroed_head = False  # correct zeroed by it (consumed by head)
+
+    def set_weight_source(self, img: torch.Tensor | None, pre_unpack=None, scatter=None):
         """Read conv weights from a bf16 image (same offsets as the arena's parameter prefix)
-        instead of the fp32 arena; ``pre_unpack`` runs first inside every captured step (the
-        WeightWire scatter of the fp32 remainder into the local arena). Invalidates graphs."""
+        instead of the fp32 arena. The fp32 remainder reaches the local arena either through
+        ``scatter`` = (src, idx, dst, gather), done by extra workgroups of the unpack launch
+        (kernels.param_unpack_tiles), or through ``pre_unpack``, run first inside every captured
+        step. Invalidates graphs."""
         if img is not None:
             assert img.dtype == torch.bfloat16 and img.numel() >= self.layout.param_numel
             assert self.unpack_impl != "tap", "the per-tap unpack kernel reads fp32 only"
+        assert scatter is None or (img is not None and pre_unpack is None)
         self.wsrc = img
         self.pre_unpack = pre_unpack
+        self.small_scatter = scatter
         self.graph = None
         self.graphs = None
 
     def load_batch(self, images_u8, labels_all, train=True):
         """Gather self.index rows of the HBM-resident dataset + fused crop/flip/normalize."""
         H, W = self.spec.in_hw
+        # a training step's per-step zeroing (BN statistic slots, accuracy counter) rides on the
+        # augment launch (forward/head then skip their own zero_ launches)
+        zero = (self.red, self.correct) if train else None
+        self._zeroed_head = train
         K.augment(images_u8, labels_all, self.index, self.x0, self.labels, self.B, H, W, 4, self.seed, self.step_dev,
-                  train, self.mean, self.std)
+                  train, self.mean, self.std, zero=zero)
+        self._zeroed = train
 
     def forward(self, arena: torch.Tensor, train: bool = True):
         sp, B = self.spec, self.B
         st = sp.stem_conv
-        if train:
+        zeroed, self._zeroed = self._zeroed, False
+        if train and not zeroed:
             self.red.zero_()
         self._conv_bn_fwd(st, self.x0, self.y0, sp.stem_bn, arena, train)
         self._apply(sp.stem_bn, self.y0, self.a0, arena, train)
@@ -583,7 +599,9 @@ class HipResNetEngine:
 
     def head(self, arena: torch.Tensor, backward: bool = True):
         sp = self.spec
-        self.correct.zero_()
+        zeroed, self._zeroed_head = self._zeroed_head, False
+        if not zeroed:
+            self.correct.zero_()
         K.head_fwd_bwd(self.final, self.B, self.head_hw, sp.fc_in, self._aview(arena, f"{sp.fc}.weight"),
                        self._aview(arena, f"{sp.fc}.bias"), sp.classes, self.labels, self.pooled, self.dlogits,
                        self.dfinal if backward else None, self.loss, self.correct)

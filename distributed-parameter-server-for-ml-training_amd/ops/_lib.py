@@ -64,10 +64,10 @@ _KERNEL_SIGS = {
     "psx_fp16_pack": (i32, [vp, vp, i64, f32, vp]),
     "psx_fp16_unpack": (i32, [vp, vp, i64, f32, vp]),
     "psx_param_unpack": (i32, [vp, vp, i32, vp, vp]),
-    "psx_param_unpack_tiles": (i32, [vp, i32, vp, i32, i32, vp, vp]),
+    "psx_param_unpack_tiles": (i32, [vp, i32, vp, i32, i32, vp, vp, vp, i64, vp, i32, vp]),
     "psx_unpack_desc_size": (i32, []),
     "psx_synth_gen": (i32, [vp, vp, i32, i32, i32, i32, u32, u32, vp]),
-    "psx_augment": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, u32, vp, i32, vp, vp, vp]),
+    "psx_augment": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, u32, vp, i32, vp, vp, vp, i64, vp, i64, vp]),
     "psx_nchw_to_nhwc": (i32, [vp, vp, i32, i32, i32, i32, i32, vp]),
     "psx_maxpool3s2_fwd": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
     "psx_maxpool3s2_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),

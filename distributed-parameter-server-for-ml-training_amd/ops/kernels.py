@@ -307,12 +307,22 @@ def param_unpack(arena, descs_dev, ndesc, wbuf):
     check(kernels().psx_param_unpack(ptr(arena), ptr(descs_dev), ndesc, ptr(wbuf), stream_ptr()), "param_unpack")
 
 
-def param_unpack_tiles(src, descs_dev, ndesc, ntiles, wbuf):
-    """Flat-grid unpack (one workgroup per 32x32 tile of every conv). ``src`` is the fp32 arena
-    or a bf16 weight image with the same element offsets; descs carry each conv's first tile."""
+def param_unpack_tiles(src, descs_dev, ndesc, ntiles, wbuf, scatter=None):
+    """Flat-grid unpack (one workgroup per 64x64 tile x 3-tap chunk of every conv). ``src`` is
+    the fp32 arena or a bf16 weight image with the same element offsets; descs carry each conv's
+    first tile. ``scatter = (src_f32, idx_i64, dst_f32, gather)``: extra workgroups of the same
+    launch write dst[idx[j]] = src[j] (gather False) or src[idx[j]] (gather True)."""
     assert src.dtype in (torch.float32, torch.bfloat16), src.dtype
+    sc = (None, None, 0, None, 0)
+    if scatter is not None:
+        s_src, s_idx, s_dst, gather = scatter
+        assert s_src.dtype == torch.float32 and s_dst.dtype == torch.float32 and s_idx.dtype == torch.int64
+        assert s_src.device == s_dst.device == s_idx.device == src.device
+        n = s_idx.numel()
+        assert gather or s_src.numel() >= n
+        sc = (ptr(s_src), ptr(s_idx), n, ptr(s_dst), int(bool(gather)))
     check(kernels().psx_param_unpack_tiles(ptr(src), int(src.dtype == torch.bfloat16), ptr(descs_dev), ndesc,
-                                           int(ntiles), ptr(wbuf), stream_ptr()), "param_unpack_tiles")
+                                           int(ntiles), ptr(wbuf), *sc, stream_ptr()), "param_unpack_tiles")
 
 
 def unpack_desc_size() -> int:
@@ -327,10 +337,16 @@ def synth_gen(img, labels, n, h, w, classes, seed, offset=0):
 _F3 = C.c_float * 3
 
 
-def augment(img, labels, index, out, out_labels, b, h, w, pad, seed, step_dev, train, mean, std):
+def augment(img, labels, index, out, out_labels, b, h, w, pad, seed, step_dev, train, mean, std, zero=None):
+    """zero: up to two contiguous tensors of 32-bit elements zeroed by the same launch."""
+    zs = []
+    for t in zero or ():
+        assert t.is_contiguous() and t.element_size() == 4 and t.device == out.device
+        zs += [ptr(t), t.numel()]
+    zs += [None, 0] * (2 - len(zs) // 2)
     check(kernels().psx_augment(ptr(img), ptr(labels), ptr(index), ptr(out), ptr(out_labels), b, h, w, pad,
-                                seed & 0xFFFFFFFF, ptr(step_dev), int(train), _F3(*mean), _F3(*std), stream_ptr()),
-          "augment")
+                                seed & 0xFFFFFFFF, ptr(step_dev), int(train), _F3(*mean), _F3(*std), *zs,
+                                stream_ptr()), "augment")
 
 
 def nchw_to_nhwc(x, y, n, c, h, w, cp):

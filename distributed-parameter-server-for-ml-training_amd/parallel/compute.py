@@ -127,23 +127,43 @@ class HipCompute:
         self.use_graph = use_graph
         self._dataset = None
         self._step = 0
-        self._idx_host = torch.zeros(batch, dtype=torch.int32).pin_memory()
+        # pinned staging ring for [batch indices | step] (one H2D copy per step); a slot is
+        # rewritten only after the copy that last read it has run (its event), so the host may
+        # run ahead of the device by up to len(ring) steps without racing the DMA
+        self._meta_ring = [torch.zeros(batch + 1, dtype=torch.int32).pin_memory() for _ in range(4)]
+        self._meta_ev = [None] * len(self._meta_ring)
+        self._meta_i = 0
 
     def _set_batch(self, idx):
-        self._idx_host.copy_(torch.as_tensor(idx, dtype=torch.int32))
-        self.engine.index.copy_(self._idx_host, non_blocking=True)
-        self.engine.step_dev.fill_(self._step)
+        k = self._meta_i % len(self._meta_ring)
+        self._meta_i += 1
+        if self._meta_ev[k] is not None:
+            self._meta_ev[k].synchronize()
+        buf = self._meta_ring[k]
+        buf[: self.B].copy_(torch.as_tensor(idx, dtype=torch.int32))
+        buf[self.B] = self._step
+        self.engine.batch_meta.copy_(buf, non_blocking=True)
+        ev = self._meta_ev[k] or torch.cuda.Event()
+        ev.record()
+        self._meta_ev[k] = ev
 
     def set_buckets(self, buckets):
         self.engine.set_segments([b.keys for b in buckets])
 
-    def use_wire(self, wire):
+    def use_wire(self, wire, small_from=None):
         """Fetches land in ``wire`` (parallel/codec.py WeightWire) instead of the fp32 local
-        arena: every captured step first scatters the wire's fp32 remainder (BN affine, FC, BN
-        running statistics) into the local arena, then unpacks the conv operands straight from
-        the wire's bf16 image. The local arena's conv-weight region is not used any more."""
+        arena: every captured step unpacks the conv operands straight from the wire's bf16 image
+        and, in the same launch, scatters the fp32 remainder (BN affine, FC, BN running
+        statistics) into the local arena. ``small_from``: the server's fp32 arena, when this
+        worker shares the server's device and reads the server's own wire (co-located sync
+        round) — the remainder is then gathered from it directly and the server need not
+        publish it. The local arena's conv-weight region is not used any more."""
         self.wire = wire
-        self.engine.set_weight_source(wire.img, pre_unpack=lambda: wire.consume_small(self.local_arena))
+        if small_from is not None:
+            sc = (small_from, wire.small_index, self.local_arena, True)
+        else:
+            sc = (wire.small, wire.small_index, self.local_arena, False)
+        self.engine.set_weight_source(wire.img, scatter=sc)
 
     def train_step(self, dataset, idx, on_bucket=None, round_hooks=None):
         seg = (lambda k: on_bucket(k, self.grads)) if on_bucket is not None else None

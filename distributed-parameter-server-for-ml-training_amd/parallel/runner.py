@@ -315,8 +315,8 @@ def make_sync_channel(cfg, t, server, W, layout, device, worker: bool = True):
             wire = server.wire if server is not None else WeightWire(layout, device)
             buckets = plan_buckets(layout, int(cfg.bucket_mb * (1 << 20)) // 2)
             return GraphRoundChannel(t, server, list(range(W)), codec, wire, buckets, device)
-        if worker:
-            wire = WeightWire(layout, device, server.wire.small_index if server is not None else None)
+        if worker:  # rank 0's worker reads the server's wire in place (stream-ordered round)
+            wire = server.wire if server is not None else WeightWire(layout, device)
     return SyncCollectiveChannel(t, server, members=list(range(W)), codec=codec, wire=wire)
 
 
@@ -326,7 +326,8 @@ def make_local_channel(cfg, server, layout, device, emit_on_last: bool = False):
     if weight_image_enabled(cfg) and torch.device(device).type == "cuda":
         if server.wire is None:
             server.enable_weight_wire()
-        wire = WeightWire(layout, device, server.wire.small_index)
+        # sync rounds: the worker reads the server's wire in place (no per-fetch copy)
+        wire = server.wire
     return InProcessChannel(server, emit_on_last=emit_on_last, wire=wire)
 
 

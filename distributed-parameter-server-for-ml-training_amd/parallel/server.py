@@ -159,19 +159,20 @@ class ParameterServer:
         self._wire_stale = False
         return self.wire
 
-    def wire_for_fetch(self):
-        """The WeightWire holding the current state (fp32 remainder refreshed; the image was
-        written by the apply, or rebuilt here after an out-of-band update)."""
+    def wire_for_fetch(self, publish_small: bool = True):
+        """The WeightWire holding the current state (fp32 remainder refreshed unless the only
+        reader gathers it from the arena itself; the image was written by the apply, or is
+        rebuilt here after an out-of-band update)."""
         if self._wire_stale:
             self.wire.publish_full(self.arena)
             self._wire_stale = False
-        else:
+        elif publish_small:
             self.wire.publish_small(self.arena)
         return self.wire
 
-    def fetch_wire(self, worker_id: int):
+    def fetch_wire(self, worker_id: int, publish_small: bool = True):
         gs = self.core.on_fetch(worker_id)
-        w = self.wire_for_fetch()
+        w = self.wire_for_fetch(publish_small)
         self.bytes_fetched += w.nbytes
         return w, gs
 

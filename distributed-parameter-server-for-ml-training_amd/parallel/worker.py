@@ -33,9 +33,12 @@ from . import control as CP
 
 
 class InProcessChannel:
-    """``wire``: the worker's own WeightWire (parallel/codec.py) — a fetch is then one device
-    copy of the server's 22.5 MB wire instead of the 44.9 MB fp32 arena, and the worker's step
-    reads its conv weights from it (ParameterServer.enable_weight_wire must be on)."""
+    """``wire``: a WeightWire (parallel/codec.py) the worker's step reads its conv weights from
+    (ParameterServer.enable_weight_wire must be on). A worker WeightWire of its own receives one
+    device copy of the server's 22.5 MB wire per fetch; the server's wire itself (sync rounds: it
+    only changes at the apply, after every step of the round) is read in place — the fetch then
+    moves no bytes and the fp32 remainder is gathered from the server arena by the step's
+    unpack launch (small_source)."""
 
     def __init__(self, server, emit_on_last: bool = False, wire=None):
         self.server = server
@@ -48,10 +51,16 @@ class InProcessChannel:
     def weight_wire(self):
         return self.image_wire
 
+    def small_source(self):
+        shared = self.image_wire is not None and self.image_wire is self.server.wire
+        return self.server.arena if shared else None
+
     def fetch(self, worker_id, local_arena):
         if self.image_wire is not None:
-            src, gs = self.server.fetch_wire(worker_id)
-            self.image_wire.buf.copy_(src.buf)
+            shared = self.image_wire is self.server.wire
+            src, gs = self.server.fetch_wire(worker_id, publish_small=not shared)
+            if not shared:
+                self.image_wire.buf.copy_(src.buf)
             return gs
         arena, gs = self.server.fetch_parameters(worker_id)
         local_arena.copy_(arena)
@@ -86,15 +95,24 @@ class SyncCollectiveChannel:
     def weight_wire(self):
         return self.image_wire
 
+    def small_source(self):
+        """Rank 0's worker reads the server's own wire: its fp32 remainder comes straight from
+        the server arena (same stream, same round)."""
+        shared = self.server is not None and self.image_wire is not None and self.image_wire is self.server.wire
+        return self.server.arena if shared else None
+
     def _fetch_image(self):
         """One broadcast of the WeightWire; the worker's step consumes it in place."""
         if self.server is not None:
             for w in self.members:
                 self.server.core.on_fetch(w)
-            sw = self.server.wire_for_fetch()
+            # the fp32 remainder is published for the remote workers (rank 0's own worker, on
+            # the server's wire, gathers it from the arena)
+            remote = len(self.members) > 1 or self.image_wire is not self.server.wire
+            sw = self.server.wire_for_fetch(publish_small=remote)
             self.t.broadcast_from_server(sw.buf)
             self.server.bytes_fetched += sw.nbytes * max(0, len(self.members) - 1)
-            if self.image_wire is not None:  # the co-located worker gets its own snapshot
+            if self.image_wire is not None and self.image_wire is not sw:  # a separate worker wire
                 self.image_wire.buf.copy_(sw.buf)
             return self.server.core.global_step
         self.t.broadcast_from_server(self.image_wire.buf)
@@ -250,7 +268,8 @@ class Worker:
         self.log(f"Registered as Worker {self.worker_id} (Total workers: {self.total_workers})")
         wire = self.channel.weight_wire() if hasattr(self.channel, "weight_wire") else None
         if wire is not None:  # fetches land in a WeightWire the step reads in place
-            self.compute.use_wire(wire)
+            small_from = self.channel.small_source() if hasattr(self.channel, "small_source") else None
+            self.compute.use_wire(wire, small_from=small_from)
         # backward-overlapped sync rounds (parallel/overlap.py): every batch is pushed, so the
         # gradient buckets can leave while the rest of the backward pass still runs
         self._overlap = bool(getattr(self.channel, "overlap", False) and self.local_steps_per_sync == 1

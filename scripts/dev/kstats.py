@@ -1,7 +1,8 @@
 """Per-kernel summary from a rocprofv3 kernel trace, restricted to the last N steps
 (steps delimited by a marker kernel), grouped by kernel template.
 
-usage: python scripts/dev/kstats.py run_kernel_trace.csv [--steps 20] [--marker augment]
+usage: python scripts/dev/kstats.py run_kernel_trace.csv|run_results.db [--steps 20] [--marker augment]
+(rocprofv3 writes a rocpd SQLite database by default, a CSV with --output-format csv)
 """
 import argparse
 import collections
@@ -21,9 +22,14 @@ def main():
     ap.add_argument("--marker", default="augment")
     a = ap.parse_args()
     rows = []
-    with open(a.csv) as f:
-        for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    if a.csv.endswith(".db"):
+        import sqlite3
+        con = sqlite3.connect(a.csv)
+        rows = [(int(s), int(e), n) for s, e, n in con.execute("select start, end, name from kernels")]
+    else:
+        with open(a.csv) as f:
+            for r in csv.DictReader(f):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
     marks = [s for s, _, n in rows if a.marker in n]
     lo, hi = marks[-a.steps - 1], marks[-1]

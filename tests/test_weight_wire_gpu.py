@@ -47,6 +47,32 @@ def test_unpack_tiles_matches_per_tap(model_name, hw):
     assert torch.equal(got2.view(torch.int16), ref.view(torch.int16))
 
 
+@pytest.mark.parametrize("gather", [False, True])
+def test_unpack_launch_scatters_fp32_remainder(gather):
+    """The extra workgroups of the unpack launch: dst[idx] = small (wire) or dst[idx] = arena[idx]."""
+    from psx.parallel.codec import WeightWire
+
+    torch.manual_seed(2)
+    model = build_model("resnet18", None, seed=0)
+    lay = ParamLayout.from_module(model)
+    arena, _ = lay.pack(model)
+    arena = (arena + 0.01 * torch.randn_like(arena)).cuda()
+    eng = HipResNetEngine(model, lay, 2, in_hw=(32, 32))
+    w = WeightWire(lay, "cuda")
+    w.publish_full(arena)
+    dst = torch.full_like(arena, -7.0)
+    ref = dst.clone()
+    w.consume_small(ref)
+    got_w = torch.zeros_like(eng.wbuf)
+    src = arena if gather else w.small
+    K.param_unpack_tiles(w.img, eng.descs, eng.ndesc, eng.ntiles, got_w, scatter=(src, w.small_index, dst, gather))
+    ref_w = torch.zeros_like(eng.wbuf)
+    K.param_unpack_tiles(w.img, eng.descs, eng.ndesc, eng.ntiles, ref_w)
+    torch.cuda.synchronize()
+    assert torch.equal(dst, ref)
+    assert torch.equal(got_w.view(torch.int16), ref_w.view(torch.int16))
+
+
 @pytest.mark.parametrize("n,mom", [(1 << 20, False), (1000003, False), (4096, True)])
 def test_sgd_apply_image_is_bf16_of_result(n, mom):
     torch.manual_seed(1)
@@ -93,7 +119,8 @@ def test_fetched_operands_identical(use_graph):
     cb = HipCompute(model, lay, 64, "cuda", use_graph=use_graph)
     cha = make_local_channel(cfg, srv, lay, "cuda")
     assert cha.weight_wire() is not None
-    ca.use_wire(cha.weight_wire())
+    ca.use_wire(cha.weight_wire(), small_from=cha.small_source())
+    assert cha.weight_wire() is srv.wire and cha.small_source() is srv.arena  # read in place
     chb = InProcessChannel(srv)
     idx = list(range(64))
     for step in range(3):

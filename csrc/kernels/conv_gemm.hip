@@ -430,16 +430,13 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 // 16-byte loads in flight (the partials are 2-16 MB per layer; the v1 mapping was latency-bound
 // at ~1 TB/s with 4-byte loads and 64 workgroups on layer1).
 template <typename OutT>
-__global__ __launch_bounds__(256) void wgrad_reduce2_kernel(const float* __restrict__ part, int splits, int Kg,
-                                                            int Cin, int IC, int RS, int CW, float scale,
-                                                            OutT* __restrict__ out) {
-  __shared__ float4 acc[256];
-  __shared__ float tile[64 * 49];  // [c][tap], CW*RS <= 64*49
-  const int oc = blockIdx.x, c0 = blockIdx.y * CW;
+PSX_DEV void wgrad_reduce2_tile(const float* __restrict__ part, int splits, int Kg, int Cin, int IC, int RS, int CW,
+                                float scale, OutT* __restrict__ out, int oc, int c0, int OC, float4* acc,
+                                float* tile) {
   const int q = CW >> 2;           // channel quads per tap
   const int items = RS * q;
   const int G = items >= 256 ? 1 : min(splits, 256 / items);
-  const size_t slab = (size_t)gridDim.x * Kg;
+  const size_t slab = (size_t)OC * Kg;
   const float* row = part + (size_t)oc * Kg + c0;
   for (int base = 0; base < items; base += 256 / G) {
     const int t = threadIdx.x;
@@ -495,6 +492,43 @@ __global__ __launch_bounds__(256) void wgrad_reduce2_kernel(const float* __restr
       dst[j] = val;
     }
   }
+}
+
+template <typename OutT>
+__global__ __launch_bounds__(256) void wgrad_reduce2_kernel(const float* __restrict__ part, int splits, int Kg,
+                                                            int Cin, int IC, int RS, int CW, float scale,
+                                                            OutT* __restrict__ out) {
+  __shared__ float4 acc[256];
+  __shared__ float tile[64 * 49];  // [c][tap], CW*RS <= 64*49
+  wgrad_reduce2_tile<OutT>(part, splits, Kg, Cin, IC, RS, CW, scale, out, blockIdx.x, blockIdx.y * CW, gridDim.x, acc,
+                           tile);
+}
+
+// Several layers' reductions in one launch (the weight gradients of one residual block are
+// reduced together at the end of its backward): flat grid, desc j owns blocks [blk0, blk0 + OC*IC/CW).
+constexpr int kWrMax = 4;
+struct WrDesc {
+  const float* part;
+  void* out;
+  int splits, Kg, Cin, IC, RS, CW, OC, blk0;
+};
+struct WrBatch {
+  WrDesc d[kWrMax];
+  int n;
+  float scale;
+};
+
+template <typename OutT>
+__global__ __launch_bounds__(256) void wgrad_reduce2_batch_kernel(WrBatch b) {
+  __shared__ float4 acc[256];
+  __shared__ float tile[64 * 49];
+  int j = 0;
+  while (j + 1 < b.n && b.d[j + 1].blk0 <= (int)blockIdx.x) ++j;
+  const WrDesc& d = b.d[j];
+  const int local = blockIdx.x - d.blk0;
+  const int oc = local % d.OC, c0 = (local / d.OC) * d.CW;
+  wgrad_reduce2_tile<OutT>(d.part, d.splits, d.Kg, d.Cin, d.IC, d.RS, d.CW, b.scale, (OutT*)d.out, oc, c0, d.OC, acc,
+                           tile);
 }
 
 }  // namespace psx
@@ -631,12 +665,40 @@ int psx_conv_wgrad(const void* x, const void* dy, float* part, int Nb, int H, in
   return e ? -e : splits;
 }
 
+static int reduce2_cw(int OC, int IC) {
+  // chunk width: widest of 64/32/16 channels that still gives >= 1024 workgroups
+  int CW = IC < 64 ? IC : 64;
+  while (CW > 16 && (long)OC * (IC / CW) < 1024) CW >>= 1;
+  return CW;
+}
+
+// n <= 4 layers: part/out/splits/OC/Kg/Cin/IC/RS arrays of n entries (host memory); every layer
+// needs the v2 reduce (R*S <= 49, IC % 16 == 0). One launch for all of them.
+int psx_wgrad_reduce_batch(int n, const float* const* part, void* const* out, const int* splits, const int* OC,
+                           const int* Kg, const int* Cin, const int* IC, const int* RS, float scale, int out_fp16,
+                           hipStream_t st) {
+  if (n < 1 || n > kWrMax) return -2;
+  WrBatch b{};
+  b.n = n;
+  b.scale = scale;
+  int blk = 0;
+  for (int i = 0; i < n; ++i) {
+    if (RS[i] > 49 || IC[i] % 16) return -3;
+    const int CW = reduce2_cw(OC[i], IC[i]);
+    b.d[i] = WrDesc{part[i], out[i], splits[i], Kg[i], Cin[i], IC[i], RS[i], CW, OC[i], blk};
+    blk += OC[i] * (IC[i] / CW);
+  }
+  if (out_fp16)
+    hipLaunchKernelGGL(wgrad_reduce2_batch_kernel<uint16_t>, dim3(blk), dim3(256), 0, st, b);
+  else
+    hipLaunchKernelGGL(wgrad_reduce2_batch_kernel<float>, dim3(blk), dim3(256), 0, st, b);
+  return (int)hipGetLastError();
+}
+
 int psx_wgrad_reduce(const float* part, int splits, int OC, int Kg, int Cin, int IC, int R, int S, float scale,
                      void* out, int out_fp16, hipStream_t st) {
   if (R * S <= 49 && IC % 16 == 0 && !getenv("PSX_WGRAD_REDUCE_V1")) {
-    // chunk width: widest of 64/32/16 channels that still gives >= 1024 workgroups
-    int CW = IC < 64 ? IC : 64;
-    while (CW > 16 && (long)OC * (IC / CW) < 1024) CW >>= 1;
+    const int CW = reduce2_cw(OC, IC);
     const dim3 grid(OC, IC / CW);
     if (out_fp16)
       hipLaunchKernelGGL(wgrad_reduce2_kernel<uint16_t>, grid, dim3(256), 0, st, part, splits, Kg, Cin, IC, R * S,

@@ -286,7 +286,9 @@ class HipResNetEngine:
                 s = K.conv_wgrad_splits(B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
             cs.splits = s
             oh, ow = cs.out_hw
-            max_wp = max(max_wp, s * cs.cout * cs.kg)
+            cs.wp = s * cs.cout * cs.kg  # fp32 partials of this layer (offset wp_off: _plan_wpart)
+            cs.wp_off = 0
+            max_wp = max(max_wp, cs.wp)
             max_wg = max(max_wg, K.conv2_workspace_bytes(B, oh, ow, cs.cout, cs.kg) // 4,
                          K.conv2_workspace_bytes(B, cs.h, cs.w, cs.cp, cs.kgd) // 4 if cs.need_dgrad else 0)
 
@@ -325,7 +327,7 @@ class HipResNetEngine:
         self.final = h_in
         self.red = self._f32(red_off[0])
         self.wpart = self._f32(max(1, max_wg))
-        self.wpart_w = self._f32(max(1, max_wp))
+        self.wpart_w = self._f32(max(1, self._plan_wpart(max_wp)))
         # head
         fh, fw = self.final.shape[1], self.final.shape[2]
         self.head_hw = fh * fw
@@ -439,6 +441,26 @@ class HipResNetEngine:
         if self.wg_stream is not None:
             torch.cuda.current_stream(self.dev).wait_stream(self.wg_stream)
 
+    def _plan_wpart(self, max_wp: int) -> int:
+        """Batched weight-gradient reduction (PSX_WGRAD_RBATCH, default on): the layers of one
+        residual block keep their split-K partials in disjoint slices of wpart_w until ONE
+        wgrad_reduce_batch launch at the end of the block's backward reduces them all (8 launches
+        instead of 19 for ResNet-18). Returns the fp32 size wpart_w needs."""
+        self.rbatch = os.environ.get("PSX_WGRAD_RBATCH", "1") == "1"
+        if not self.rbatch:
+            return max_wp
+        need = max_wp
+        for b in self.spec.blocks:
+            convs = list(b.convs) + ([b.down[0]] if b.down else [])
+            if len(convs) > K.WRBATCH_MAX:
+                continue
+            off = 0
+            for cs in convs:
+                cs.wp_off = off
+                off += cs.wp
+            need = max(need, off)
+        return need
+
     def _wgrad(self, cs: ConvSpec, x, dy):
         if self._wg_batch is not None:  # deferred: issued together at the end of the unit
             self._wg_batch.append((cs, x, dy))
@@ -454,15 +476,24 @@ class HipResNetEngine:
                     self._wgrad_now(cs, x, dy)
 
     def _wgrad_now(self, cs: ConvSpec, x, dy):
-        if True:
-            if self.conv_impl == 2:
-                K.conv_wgrad2(x, dy, self.wpart_w, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
-                              cs.kg)
-            else:
-                K.conv_wgrad(x, dy, self.wpart_w, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
-                             cs.kg, cs.splits)
-            K.wgrad_reduce(self.wpart_w, cs.splits, cs.cout, cs.kg, cs.cin, cs.cp, cs.k, 1.0,
-                           self._gptr(f"{cs.name}.weight"), self.grad_fp16)
+        part = self.wpart_w[cs.wp_off:cs.wp_off + cs.wp]
+        if self.conv_impl == 2:
+            K.conv_wgrad2(x, dy, part, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
+        else:
+            K.conv_wgrad(x, dy, part, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg, cs.splits)
+        item = (part, cs.splits, cs.cout, cs.kg, cs.cin, cs.cp, cs.k, self._gptr(f"{cs.name}.weight"))
+        if self._wr_batch is not None and K.wgrad_reduce_batchable(cs.cp, cs.k):
+            self._wr_batch.append(item)  # reduced with the block's other layers (_flush_reduces)
+            return
+        K.wgrad_reduce(*item[:7], 1.0, item[7], self.grad_fp16)
+
+    _wr_batch = None
+
+    def _flush_reduces(self):
+        batch, self._wr_batch = self._wr_batch, None
+        if batch:
+            with self._side():
+                K.wgrad_reduce_batch(batch, 1.0, self.grad_fp16)
 
     def _dgrad(self, cs: ConvSpec, dy, dx, res=None, bn_next=None):
         """bn_next = (BNSpec, o, y, two|None): the BN whose backward consumes dx; with conv v2 its
@@ -616,10 +647,14 @@ class HipResNetEngine:
         """Backward of residual block j; its incoming gradient is the next block's input grad.
         With the side stream its weight gradients are issued as one batch after the block."""
         self._wg_batch = [] if self.wg_stream is not None else None
+        b = self.spec.blocks[j]
+        nconv = len(b.convs) + (1 if b.down else 0)
+        self._wr_batch = [] if self.rbatch and nconv <= K.WRBATCH_MAX else None
         try:
             self._bwd_block_body(arena, j)
         finally:
             self._flush_wgrads()
+            self._flush_reduces()
 
     def _bwd_block_body(self, arena, j: int):
         sp, B = self.spec, self.B

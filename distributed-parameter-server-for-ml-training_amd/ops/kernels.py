@@ -9,6 +9,7 @@ fp32 parameter arenas; fp16 (wire codec) or fp32 gradient sinks.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -164,6 +165,30 @@ def conv_wgrad(x, dy, part, nb, h, w, ic, oc, k, stride, pad, kg, splits) -> int
 def wgrad_reduce(part, splits, oc, kg, cin, ic, k, scale, out_ptr: int, out_fp16: bool):
     check(kernels().psx_wgrad_reduce(ptr(part), splits, oc, kg, cin, ic, k, k, float(scale), out_ptr, int(out_fp16),
                                      stream_ptr()), "wgrad_reduce")
+
+
+WRBATCH_MAX = 4
+
+
+def wgrad_reduce_batchable(ic, k) -> bool:
+    """The v2 reduce handles the layer (what wgrad_reduce_batch requires)."""
+    return k * k <= 49 and ic % 16 == 0 and not os.environ.get("PSX_WGRAD_REDUCE_V1")
+
+
+def wgrad_reduce_batch(items, scale, out_fp16: bool):
+    """One launch reducing up to WRBATCH_MAX layers' split-K partials; items = [(part, splits,
+    oc, kg, cin, ic, k, out_ptr)] (see wgrad_reduce), each wgrad_reduce_batchable."""
+    n = len(items)
+    assert 1 <= n <= WRBATCH_MAX
+    P = (C.c_void_p * n)(*[ptr(it[0]) for it in items])
+    O = (C.c_void_p * n)(*[it[7] for it in items])
+
+    def ints(j, f=lambda v: v):
+        return (C.c_int * n)(*[int(f(it[j])) for it in items])
+
+    check(kernels().psx_wgrad_reduce_batch(n, P, O, ints(1), ints(2), ints(3), ints(4), ints(5),
+                                           ints(6, lambda k: k * k), float(scale), int(out_fp16), stream_ptr()),
+          "wgrad_reduce_batch")
 
 
 def bn_finalize(part, T, c, count, gamma, beta, eps, momentum, run_mean, run_var, affine, saved):

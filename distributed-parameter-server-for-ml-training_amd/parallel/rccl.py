@@ -44,7 +44,10 @@ def _check(rc: int, what: str):
 
 
 def torch_rccl_path() -> str:
-    """librccl.so of the PyTorch build in use (bundled in torch/lib), else ROCm's."""
+    """librccl.so of the PyTorch build in use (bundled in torch/lib), else ROCm's
+    (PSX_RCCL_LIB overrides)."""
+    if os.environ.get("PSX_RCCL_LIB"):
+        return os.environ["PSX_RCCL_LIB"]
     p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
     if os.path.exists(p):
         return p
@@ -65,15 +68,26 @@ def _stream(s=None) -> int:
 class NativeComm:
     """One RCCL communicator over all ranks of the job (C handle + the device it lives on)."""
 
-    def __init__(self, rank: int, world: int, device: torch.device, broadcast_object):
-        lib = comm()
-        _check(lib.psx_comm_load(torch_rccl_path().encode()), "psx_comm_load")
-        nb = lib.psx_comm_id_bytes()
-        uid = None
-        if rank == 0:
-            buf = C.create_string_buffer(nb)
-            _check(lib.psx_comm_unique_id(buf), "ncclGetUniqueId")
-            uid = buf.raw
+    def __init__(self, rank: int, world: int, device: torch.device, broadcast_object, all_gather_object=None):
+        # every rank loads the library (and rank 0 draws the id) BEFORE anyone enters the
+        # collective ncclCommInitRank: with all_gather_object the ranks agree first, so a rank
+        # that cannot bind RCCL fails the job everywhere instead of leaving the others blocked
+        uid, err = None, ""
+        try:
+            lib = comm()
+            _check(lib.psx_comm_load(torch_rccl_path().encode()), "psx_comm_load")
+            if rank == 0:
+                buf = C.create_string_buffer(lib.psx_comm_id_bytes())
+                _check(lib.psx_comm_unique_id(buf), "ncclGetUniqueId")
+                uid = buf.raw
+        except Exception as e:  # noqa: BLE001 - reported collectively below
+            err = f"rank {rank}: {e}"
+        if all_gather_object is not None:
+            errs = [x for x in all_gather_object(err) if x]
+            if errs:
+                raise RcclError("native communicator unavailable: " + "; ".join(errs))
+        elif err:
+            raise RcclError(err)
         uid = broadcast_object(uid)
         h = C.c_void_p()
         self.device = torch.device(device)
@@ -141,7 +155,8 @@ class RcclTransport(DistTransport):
         super().__init__(backend=backend, device=device, timeout_s=timeout_s)
         if self.device.type != "cuda":
             raise RcclError("RcclTransport needs a HIP device")
-        self.comm = NativeComm(self.rank, self.world_size, self.device, self.broadcast_object)
+        self.comm = NativeComm(self.rank, self.world_size, self.device, self.broadcast_object,
+                               self.all_gather_object)
         self._cstream = torch.cuda.Stream(device=self.device)
 
     # ---- sync mode collectives: in stream order on the caller's stream
@@ -199,5 +214,14 @@ def make_transport(device=None):
     dev = torch.device(device) if device is not None else None
     kind = os.environ.get("PSX_TRANSPORT", "native")
     if kind == "native" and dev is not None and dev.type == "cuda":
-        return RcclTransport(device=dev)
+        try:
+            return RcclTransport(device=dev)
+        except RcclError as e:
+            # every rank raised the same collective verdict (NativeComm): all fall back together
+            import sys
+
+            print(f"[psx] {e}; falling back to torch.distributed (PSX_TRANSPORT=torch)", file=sys.stderr)
+            if torch.distributed.is_initialized():
+                return DistTransport(device=device)  # reuses the initialised default group
+            raise
     return DistTransport(device=device)

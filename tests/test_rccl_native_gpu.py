@@ -89,6 +89,13 @@ def test_sync_run_native_matches_torch_transport(codec):
     assert abs(a - b) <= 2e-4 * max(abs(a), abs(b)), out
 
 
+def test_unloadable_rccl_falls_back_to_torch_transport():
+    """Every rank agrees on the native communicator before ncclCommInitRank; when the library
+    cannot be bound the job runs on torch.distributed instead of failing or hanging."""
+    res = _run(_RUN.format(root=ROOT, codec="fp16"), 29654, {"PSX_RCCL_LIB": "/nonexistent/librccl.so"})
+    assert res[1] == 6
+
+
 _ROUND = r"""
 import json, sys
 sys.path.insert(0, {root!r})

@@ -75,7 +75,14 @@ PSX_DEV const uint16_t* gather_src(const Conv2Args& a, int nbase, int hb, int wb
 // WGM = waves along the output-channel (M) axis, 4 / WGM along pixels: 2 (2x2 waves, wave tile
 // BM/2 x BN/2) or 1 (1x4 waves: every wave holds all BM channels of a BN/4 pixel slice, e.g. a
 // 64x64 wave tile for BM = 64, BN = 256 — 2/3 of the LDS fragment bytes per MFMA of 32x64).
-template <int BM, int BN, int MODE, bool HAS_RES, bool SPLIT, int WGM = 2>
+//
+// TAPR (3x3 / stride 1 / pad 1, MODE 0 or 1, tiles of whole image rows): tap-reuse mainloop.
+// A macro step = (kernel row r, 64-channel chunk): the three weight tiles of taps (r, 0..2) and
+// ONE window X of the tile's BN pixels at (row r, centre column) are staged; pixel j of tap s
+// reads window slot j + d(s) (d = s - 1 forward, 1 - s dgrad: ih = oh + pad - r there) or a zero
+// row when its column leaves the image row. The im2col operand is staged once per kernel row
+// instead of once per tap (1/3 of the L2->LDS bytes of the gathered operand); 2 LDS stages.
+template <int BM, int BN, int MODE, bool HAS_RES, bool SPLIT, int WGM = 2, bool TAPR = false>
 __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   constexpr int NSTAGE = 3;
   constexpr int WGN = 4 / WGM;
@@ -108,6 +115,97 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     if (pix0 >= npix_c) return;  // whole workgroup: this class has fewer tiles
   }
 
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  if constexpr (TAPR) {
+    static_assert(MODE == 0 || MODE == 1, "tap reuse: forward or stride-1 dgrad");
+    constexpr int XOFF = 3 * BM * 128, TST = XOFF + (BN + 1) * 128;  // A0 A1 A2 | X | zero row
+    const int nch = a.IC >> 6, nmac = 3 * nch;
+    const int W = a.OW, log2w = __builtin_ctz(W);
+    const int lrow = lane >> 3, lpos = lane & 7;
+    if (tid < 16)
+      *reinterpret_cast<uint4*>(smem + (tid >> 3) * TST + XOFF + BN * 128 + (tid & 7) * 16) = uint4{0u, 0u, 0u, 0u};
+    const uint16_t* wsrc[LA];
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int row = (i * 4 + wid) * 8 + lrow;
+      wsrc[i] = a.w + (size_t)(oc0 + row) * a.Kg + (lpos ^ ((row >> 1) & 7)) * 8;
+    }
+    // window rows: the tile's own pixels (input pixel index == output pixel index at s1/p1)
+    const uint16_t* xsrc[LB];
+    int xoh[LB];
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int row = (i * 4 + wid) * 8 + lrow;
+      const int pix = pix0 + row;
+      xoh[i] = (pix >> log2w) & (a.OH - 1);
+      xsrc[i] = a.in + (size_t)pix * a.IC + (lpos ^ ((row >> 1) & 7)) * 8;
+    }
+    auto issue_t = [&](int t, int stage) {
+      unsigned char* base = smem + stage * TST;
+      const int r = __builtin_amdgcn_readfirstlane(t / nch);
+      const int cc = t - r * nch;
+#pragma unroll
+      for (int sx = 0; sx < 3; ++sx) {
+        const int kofs = (r * 3 + sx) * a.IC + cc * 64;
+#pragma unroll
+        for (int i = 0; i < LA; ++i) glds16(wsrc[i] + kofs, base + sx * BM * 128 + (i * 4 + wid) * 1024);
+      }
+      const int dr = MODE == 0 ? r - 1 : 1 - r;
+      const long uoff = (long)dr * W * a.IC + cc * 64;
+#pragma unroll
+      for (int i = 0; i < LB; ++i) {
+        const uint16_t* src = (unsigned)(xoh[i] + dr) < (unsigned)a.OH ? xsrc[i] + uoff : a.zero;
+        glds16(src, base + XOFF + (i * 4 + wid) * 1024);
+      }
+    };
+    // per-lane B-fragment byte offsets of the three taps (tile starts on an image row)
+    const int frow = lane & 15, fch = lane >> 4;
+    int boff[NT][3];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const int prow = wn * (BN / WGN) + n * 16 + frow;
+      const int ow = prow & (W - 1);
+#pragma unroll
+      for (int sx = 0; sx < 3; ++sx) {
+        const int d = MODE == 0 ? sx - 1 : 1 - sx;
+        const int slot = (unsigned)(ow + d) < (unsigned)W ? prow + d : BN;
+        boff[n][sx] = slot * 128 + ((fch ^ ((slot >> 1) & 7)) << 4);
+      }
+    }
+    __syncthreads();  // zero rows written
+    if (nmac > 0) issue_t(0, 0);
+    for (int t = 0; t < nmac; ++t) {
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (t + 1 < nmac) issue_t(t + 1, (t + 1) & 1);
+      const unsigned char* base = smem + (t & 1) * TST;
+      const unsigned char* X = base + XOFF;
+#pragma unroll
+      for (int sx = 0; sx < 3; ++sx) {
+        const unsigned char* A = base + sx * BM * 128;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          bf16x8 fa[MT], fb[NT];
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+            fa[m] = *reinterpret_cast<const bf16x8*>(A + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
+#pragma unroll
+          for (int n = 0; n < NT; ++n) fb[n] = *reinterpret_cast<const bf16x8*>(X + (boff[n][sx] ^ (kk << 6)));
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+              acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
+        }
+      }
+    }
+  } else {
   // ---- per-lane DMA source state (fixed across k-steps) ----
   const int lrow = lane >> 3, lpos = lane & 7;
   const uint16_t* wsrc[LA];
@@ -218,12 +316,6 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     }
   };
 
-  f32x4 acc[MT][NT];
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int n = 0; n < NT; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
   if (nk > 0) issue(0, 0);
   if (nk > 1) issue(1, 1);
   const int frow = lane & 15, fch = lane >> 4;
@@ -255,6 +347,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     }
     stage = stage == 2 ? 0 : stage + 1;
   }
+  }  // generic mainloop
 
   if constexpr (SPLIT) {
     float* dst = a.part + (size_t)split * a.npix * a.OC;
@@ -580,6 +673,43 @@ int dispatch2(const Plan& p, const Conv2Args& a, hipStream_t st) {
   return -7;
 }
 
+template <int BM, int BN, int MODE, bool RES, int WGM>
+int launch_tapr(const Conv2Args& a, hipStream_t st) {
+  const size_t lds = (size_t)2 * (3 * BM * 128 + (BN + 1) * 128);
+  hipLaunchKernelGGL((conv2_kernel<BM, BN, MODE, RES, false, WGM, true>), dim3(a.n_oc_tiles * a.n_pix_tiles),
+                     dim3(256), lds, st, a);
+  return (int)hipGetLastError();
+}
+
+// Pixel-tile width of the tap-reuse path for this layer, 0 = not applicable: 3x3 / stride 1 /
+// pad 1, square power-of-two images whose rows tile BN exactly, 64-channel chunks; no split-K.
+// PSX_CV_TAPR=0 disables it, PSX_CV_TAPR_BN=64|128|256 forces the width (sweeps).
+int tapr_bn(int R, int S, int stride, int pad, int H, int W, int IC, int OC, int npix) {
+  if (const char* e = getenv("PSX_CV_TAPR"))
+    if (e[0] == '0') return 0;
+  if (R != 3 || S != 3 || stride != 1 || pad != 1 || IC % 64 || OC % 64 || H != W || (W & (W - 1))) return 0;
+  int force = 0;
+  if (const char* e = getenv("PSX_CV_TAPR_BN")) force = atoi(e);
+  // measured (bench/tapr_probe.py, ResNet-18 B=128, us fwd/dgrad): 64-pixel tiles (2 workgroups
+  // per CU) win or tie on every layer — 32x32x64: 27.3/20.9 vs generic 26.3/23.0; 16x16x128:
+  // 18.7/15.8 vs 20.6/19.3; 8x8x256: 14.8/13.7 vs 25.5/23.4; 4x4x512: 20.5/19.2 vs 29.3/28.0
+  // (generic = split-K + epilogue launch there); 128/256-pixel tiles (1 workgroup per CU) lose.
+  const int BN = force ? force : 64;
+  if ((BN != 64 && BN != 128 && BN != 256) || BN % W || npix % BN) return 0;
+  return BN;
+}
+
+template <int MODE, bool RES>
+int dispatch_tapr(int bn, Conv2Args& a, hipStream_t st) {
+  a.n_oc_tiles = a.OC / 64;
+  a.n_pix_tiles = a.npix / bn;
+  a.splits = 1;
+  a.kps = a.Kg / 64;
+  if (bn == 256) return launch_tapr<64, 256, MODE, RES, 1>(a, st);
+  if (bn == 128) return launch_tapr<64, 128, MODE, RES, 2>(a, st);
+  return launch_tapr<64, 64, MODE, RES, 2>(a, st);
+}
+
 int finish_split(const Conv2Args& a, hipStream_t st) {
   const int cvec = a.OC / 8;
   if (256 % cvec) return -8;
@@ -636,6 +766,7 @@ int psx_conv_fwd2(const void* x, const void* wf, void* y, float* stats, const vo
   a.log2_icc = ilog2i(IC / 8);
   a.npix = Nb * a.OH * a.OW;
   if (OC % 64 || Kg % 64 || IC % 8 || (IC & (IC - 1))) return -2;
+  if (const int tbn = tapr_bn(R, S, stride, pad, H, W, IC, OC, a.npix)) return dispatch_tapr<0, false>(tbn, a, st);
   const Plan p = plan_for(OC, a.npix, Kg / 64);
   a.n_oc_tiles = OC / p.BM;
   a.n_pix_tiles = (a.npix + p.BN - 1) / p.BN;
@@ -684,6 +815,8 @@ int psx_conv_dgrad2(const void* dy, const void* wd, void* dx, const void* res, c
   a.log2_icc = ilog2i(OC_fwd / 8);
   a.npix = Nb * H * W;
   if (IC_fwd % 64 || Kg % 64 || (OC_fwd & (OC_fwd - 1))) return -2;
+  if (const int tbn = tapr_bn(R, S, stride, pad, H, W, OC_fwd, IC_fwd, a.npix))
+    return res ? dispatch_tapr<1, true>(tbn, a, st) : dispatch_tapr<1, false>(tbn, a, st);
   const Plan p = plan_for(IC_fwd, a.npix, Kg / 64);
   a.n_oc_tiles = IC_fwd / p.BM;
   a.n_pix_tiles = (a.npix + p.BN - 1) / p.BN;

@@ -95,7 +95,8 @@ def test_conv2_every_tile_config(shape, tile, monkeypatch):
     n, cin, cout, hw, k, s, p = shape
     if cout % bm or cin % bm:
         pytest.skip("tile wider than the channel count")
-    for key, v in (("PSX_CV_BM", bm), ("PSX_CV_BN", bn), ("PSX_CV_WGM", wgm), ("PSX_CV_SPLITS", 1)):
+    for key, v in (("PSX_CV_BM", bm), ("PSX_CV_BN", bn), ("PSX_CV_WGM", wgm), ("PSX_CV_SPLITS", 1),
+                   ("PSX_CV_TAPR", 0)):
         monkeypatch.setenv(key, str(v))
     torch.manual_seed(3)
     x = torch.randn(n, cin, hw, hw, device=DEV).to(torch.bfloat16).float()
@@ -115,3 +116,43 @@ def test_conv2_every_tile_config(shape, tile, monkeypatch):
     res = torch.randn(n, hw, hw, cp, device=DEV).to(torch.bfloat16)
     K.conv_dgrad2(to_nhwc(dy, cout), wd, dx, res, None, n, hw, hw, cp, cout, k, s, p, kgd)
     assert _rel(dx[..., :cin], dref + res[..., :cin].float()) < 1e-2, (shape, tile)
+
+
+@pytest.mark.parametrize("bn", [64, 128, 256])
+@pytest.mark.parametrize("shape", [(32, 64, 64, 32, 3, 1, 1), (16, 128, 128, 16, 3, 1, 1), (16, 256, 256, 8, 3, 1, 1),
+                                   (16, 512, 512, 4, 3, 1, 1), (4, 64, 128, 64, 3, 1, 1)])
+def test_conv2_tap_reuse(shape, bn, monkeypatch):
+    """The tap-reuse mainloop (conv2_kernel TAPR: one staged window per kernel row feeds its three
+    taps, zero row at the image-row edges) at every tile width: fwd (+ BN statistics) and dgrad
+    (+ residual, + fused BN-backward sums) against torch fp32."""
+    n, cin, cout, hw, k, s, p = shape
+    if (n * hw * hw) % bn or bn % hw:
+        pytest.skip("tile does not hold whole image rows")
+    monkeypatch.setenv("PSX_CV_TAPR_BN", str(bn))
+    torch.manual_seed(4)
+    x = torch.randn(n, cin, hw, hw, device=DEV).to(torch.bfloat16).float()
+    w = (torch.randn(cout, cin, k, k, device=DEV) / (cin * k * k) ** 0.5).to(torch.bfloat16).float()
+    wf, wd, cp, kg, kgd = make_operands(w)
+    y = torch.empty(n, hw, hw, cout, dtype=torch.bfloat16, device=DEV)
+    stats = torch.zeros(K.STAT_SLOTS, 2, cout, device=DEV)
+    K.conv_fwd2(to_nhwc(x, cp), wf, y, stats, None, n, hw, hw, cp, cout, k, s, p, kg)
+    ref = F.conv2d(x, w, stride=s, padding=p).permute(0, 2, 3, 1)
+    assert _rel(y, ref) < 1e-2, (shape, bn)
+    yq = y.float().reshape(-1, cout)
+    assert torch.allclose(stats[:, 0].sum(0), yq.sum(0), rtol=1e-3, atol=5e-2), (shape, bn)
+    assert torch.allclose(stats[:, 1].sum(0), (yq * yq).sum(0), rtol=1e-3, atol=5e-2), (shape, bn)
+    dy = torch.randn(n, cout, hw, hw, device=DEV).to(torch.bfloat16).float()
+    dref = torch.nn.grad.conv2d_input((n, cin, hw, hw), w, dy, stride=s, padding=p).permute(0, 2, 3, 1)
+    dx = torch.empty(n, hw, hw, cp, dtype=torch.bfloat16, device=DEV)
+    res = torch.randn(n, hw, hw, cp, device=DEV).to(torch.bfloat16)
+    o = torch.randn(n, hw, hw, cp, device=DEV).to(torch.bfloat16)
+    y1 = torch.randn(n, hw, hw, cp, device=DEV).to(torch.bfloat16)
+    saved = torch.stack([0.1 * torch.randn(cp, device=DEV), 1.0 + torch.rand(cp, device=DEV)])
+    part = torch.zeros(K.STAT_SLOTS, 2, cp, device=DEV)
+    bst = K.bwd_stats_desc(part, o, y1, saved)
+    K.conv_dgrad2(to_nhwc(dy, cout), wd, dx, res, None, n, hw, hw, cp, cout, k, s, p, kgd, bst=bst)
+    assert _rel(dx[..., :cin], dref + res[..., :cin].float()) < 1e-2, (shape, bn)
+    dz = (dx.float() * (o.float() > 0)).reshape(-1, cp)
+    xhat = ((y1.float().reshape(-1, cp) - saved[0]) * saved[1])
+    assert torch.allclose(part[:, 0].sum(0), dz.sum(0), rtol=1e-3, atol=5e-2), (shape, bn)
+    assert torch.allclose(part[:, 1].sum(0), (dz * xhat).sum(0), rtol=1e-3, atol=5e-2), (shape, bn)

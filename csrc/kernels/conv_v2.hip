@@ -364,6 +364,128 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     return;
   }
 
+  // ---- LDS-staged epilogue (MODE 0-2; PSX_CV_EPI=0 builds keep the fragment epilogue) ----
+  // The fp32 tile goes through LDS once; then every thread owns 8 channels of a pixel row, so the
+  // bf16 output, the residual and the BN-backward operands o / y move as whole 16-byte chunks of
+  // 128-byte rows (the fragment layout touched 32-byte pieces of 16 rows per instruction), and
+  // the per-channel sums need one shuffle tree + one LDS pass per workgroup.
+#ifndef PSX_CV_EPI
+#define PSX_CV_EPI 1
+#endif
+  if constexpr (MODE != 3 && PSX_CV_EPI) {
+    constexpr int TS = BM + 4;      // fp32 row stride of the staged tile (spreads the banks)
+    constexpr int CPR = BM / 8;     // 16-byte bf16 chunks per pixel row
+    constexpr int RPP = 256 / CPR;  // pixel rows per pass
+    constexpr int LDSB = TAPR ? 2 * (3 * BM * 128 + (BN + 1) * 128) : 3 * (BM + BN) * 128;  // launched
+    static_assert(256 % CPR == 0 && BN * TS * 4 <= LDSB, "staged tile fits the mainloop LDS");
+    float* T = reinterpret_cast<float*>(smem);
+    __syncthreads();  // every wave is done with the mainloop's LDS
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const int pr = wn * (BN / WGN) + n * 16 + (lane & 15);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        *reinterpret_cast<f32x4*>(T + pr * TS + wm * (BM / WGM) + m * 16 + 4 * (lane >> 4)) = acc[m][n];
+    }
+    __syncthreads();
+    const bool bwd = a.bpart != nullptr, two = a.by2 != nullptr, st = a.stats != nullptr;
+    const int cc = tid % CPR, ch0 = oc0 + cc * 8;
+    float s1[8], s2[8], s3[8], bm1[8], bi1[8], bm2[8], bi2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s1[i] = s2[i] = s3[i] = 0.f;
+      bm1[i] = bi1[i] = bm2[i] = bi2[i] = 0.f;
+      if (bwd) {
+        bm1[i] = a.bsaved1[ch0 + i];
+        bi1[i] = a.bsaved1[a.OC + ch0 + i];
+        if (two) {
+          bm2[i] = a.bsaved2[ch0 + i];
+          bi2[i] = a.bsaved2[a.OC + ch0 + i];
+        }
+      }
+    }
+    for (int pr = tid / CPR; pr < BN; pr += RPP) {
+      const int pix = pix0 + pr;
+      if (pix >= npix_c) break;
+      const float* src = T + pr * TS + cc * 8;
+      const f32x4 va = *reinterpret_cast<const f32x4*>(src), vb = *reinterpret_cast<const f32x4*>(src + 4);
+      float v[8] = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
+      const size_t off = (size_t)pix * a.OC + ch0;
+      if (HAS_RES) {
+        const u32x4 rr = *reinterpret_cast<const u32x4*>(a.res + off);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[2 * k] += lo_bf(rr[k]);
+          v[2 * k + 1] += hi_bf(rr[k]);
+        }
+      }
+      u32x4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = pack_bf2(v[2 * k], v[2 * k + 1]);
+      *reinterpret_cast<u32x4*>(a.out + off) = o;
+      if (st) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float q0 = lo_bf(o[k]), q1 = hi_bf(o[k]);
+          s1[2 * k] += q0; s2[2 * k] += q0 * q0;
+          s1[2 * k + 1] += q1; s2[2 * k + 1] += q1 * q1;
+        }
+      }
+      if (bwd) {
+        const u32x4 om = *reinterpret_cast<const u32x4*>(a.bo + off);
+        const u32x4 yv = *reinterpret_cast<const u32x4*>(a.by1 + off);
+        u32x4 y2v = {0u, 0u, 0u, 0u};
+        if (two) y2v = *reinterpret_cast<const u32x4*>(a.by2 + off);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int k = i >> 1;
+          const bool hi = i & 1;
+          const float g = hi ? hi_bf(o[k]) : lo_bf(o[k]);
+          const float dz = (hi ? hi_bf(om[k]) : lo_bf(om[k])) > 0.f ? g : 0.f;
+          s1[i] += dz;
+          s2[i] += dz * ((hi ? hi_bf(yv[k]) : lo_bf(yv[k])) - bm1[i]) * bi1[i];
+          if (two) s3[i] += dz * ((hi ? hi_bf(y2v[k]) : lo_bf(y2v[k])) - bm2[i]) * bi2[i];
+        }
+      }
+    }
+    if (!st && !bwd) return;
+    // lanes of one wave that own the same channels differ in the lane bits >= log2(CPR)
+#pragma unroll
+    for (int sh = CPR; sh < 64; sh <<= 1)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        s1[i] += __shfl_xor(s1[i], sh, 64);
+        s2[i] += __shfl_xor(s2[i], sh, 64);
+        if (two) s3[i] += __shfl_xor(s3[i], sh, 64);
+      }
+    __syncthreads();  // the staged tile is no longer read
+    float* red = T;   // [4 waves][3][BM]
+    if (lane < CPR) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        red[(wid * 3 + 0) * BM + cc * 8 + i] = s1[i];
+        red[(wid * 3 + 1) * BM + cc * 8 + i] = s2[i];
+        red[(wid * 3 + 2) * BM + cc * 8 + i] = s3[i];
+      }
+    }
+    __syncthreads();
+    const int nst = bwd ? a.bns : 2;
+    float* dst = (bwd ? a.bpart : a.stats) + (size_t)(pix_t & (PSX_STAT_SLOTS - 1)) * nst * a.OC;
+    for (int j = tid; j < nst * BM; j += 256) {
+      const int which = j / BM, row = j - which * BM;
+      const float v = red[which * BM + row] + red[(3 + which) * BM + row] + red[(6 + which) * BM + row] +
+                      red[(9 + which) * BM + row];
+#ifdef PSX_CV_STATS_NOATOMIC  // timing-only A/B build: plain stores (wrong sums)
+      dst[which * a.OC + oc0 + row] = v;
+#else
+      atomicAdd(dst + which * a.OC + oc0 + row, v);
+#endif
+    }
+    if (st && a.fuse_fin && last_block_arrive(a.fin.counter, gridDim.x, smem))
+      bn_finalize_block<PSX_STAT_SLOTS>(a.stats, a.fin);
+    return;
+  }
+
   // ---- epilogue: bf16 NHWC store (+residual), BN partial statistics ----
   float s1[MT][4], s2[MT][4], s3[MT][4];
   float bm1[MT][4], bi1[MT][4], bm2[MT][4], bi2[MT][4];

@@ -33,6 +33,7 @@ from psx.parallel.compute import HipCompute  # noqa: E402
 from psx.parallel.runner import (AsyncSession, build_state, make_datasets, make_local_channel,  # noqa: E402
                                  make_sync_channel)
 from psx.parallel.server import ParameterServer  # noqa: E402
+from psx.parallel.sharded import ShardedSyncChannel  # noqa: E402
 from psx.parallel.rccl import make_transport  # noqa: E402
 from psx.parallel.transport import env_world  # noqa: E402
 from psx.parallel.worker import Worker  # noqa: E402
@@ -52,7 +53,9 @@ def main():
                          "shape, use with --codec topk)")
     ap.add_argument("--train-samples", type=int, default=None,
                     help="synthetic dataset size in HBM (default 50000 for resnet18, 4096 for resnet50)")
-    ap.add_argument("--topology", choices=["colocated", "dedicated"], default="colocated")
+    ap.add_argument("--topology", choices=["colocated", "dedicated", "sharded"], default="colocated",
+                    help="sharded: every rank is a worker and owns 1/N of the server (reduce-scatter, "
+                         "range apply, all-gather; parallel/sharded.py)")
     ap.add_argument("--codec", choices=["fp16", "none", "topk"], default="fp16")
     ap.add_argument("--topk-ratio", type=float, default=0.01)
     ap.add_argument("--no-graph", action="store_true")
@@ -76,13 +79,22 @@ def main():
     n_train = a.train_samples or (50000 if a.model == "resnet18" else 4096)
     cfg = PSConfig(mode=a.mode, staleness_bound=a.staleness_bound, model=a.model, batch_size=a.batch, train_samples=n_train, lr=0.1, sync_steps=1, epochs=1,
                    eval_every=0, verbose=0, codec=a.codec, topk_ratio=a.topk_ratio, use_graph=not a.no_graph, fetch_codec=a.fetch_codec,
-                   overlap=a.overlap, bucket_mb=a.bucket_mb).validate()
+                   overlap=a.overlap, bucket_mb=a.bucket_mb, topology=a.topology).validate()
     model, layout, arena, counters = build_state(cfg)
     wire = torch.float16 if a.codec == "fp16" else torch.float32  # topk encodes from fp32 grads
 
     t = None
     force_dist = os.environ.get("PSX_FORCE_DIST", "0") == "1"  # exercise the RCCL path even at N=1
-    if world > 1 or force_dist:
+    sharded = a.topology == "sharded"
+    if world > 1 or force_dist or sharded:
+        if "RANK" not in os.environ:  # single process without torchrun: a world of one rank
+            import socket
+
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+            os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=str(port))
         t = make_transport(device)
     dedicated = a.topology == "dedicated" and world > 1
     worker_ranks = list(range(1, world)) if dedicated else list(range(world))
@@ -92,9 +104,9 @@ def main():
     server = None
     quiet = lambda *x, **k: None  # noqa: E731
     async_dist = a.mode == "async" and t is not None
-    if rank == 0:
+    if rank == 0 or sharded:
         server = ParameterServer(cfg, layout, arena, counters, device=device, total_workers=W, log=quiet)
-        if not async_dist:
+        if not async_dist and rank == 0:
             for i in range(W):
                 server.register_worker(f"worker-{i}", i)
     train, _ = make_datasets(cfg, device, model.fc.out_features)
@@ -109,8 +121,11 @@ def main():
         sess = AsyncSession(cfg, t, rank, worker_ranks, server, comp, train, None, names, quiet)
         wk = sess.worker
     else:
-        chan = (make_local_channel(cfg, server, layout, device) if t is None else
-                make_sync_channel(cfg, t, server, W, layout, device, worker=is_worker))
+        if sharded:
+            chan = ShardedSyncChannel(cfg, t, server, list(range(W)), layout, device, in_place=True)
+        else:
+            chan = (make_local_channel(cfg, server, layout, device) if t is None else
+                    make_sync_channel(cfg, t, server, W, layout, device, worker=is_worker))
         if is_worker:
             wid = worker_ranks.index(rank)
             wk = Worker(cfg, comp, chan, train, None, worker_name=f"worker-{wid}", rank=rank, log=quiet,
@@ -195,6 +210,8 @@ def main():
                 "per_worker_batch": a.batch,
                 "seq_len": None,
                 "parallelism": (
+                    f"sharded sync-PS: {W} ranks, each a worker + 1/{W} of the server; RCCL reduce-scatter(grads) "
+                    f"+ all-gather(bf16 params) over xGMI" if sharded else
                     f"{a.mode}-PS: rank0 = parameter server{' only' if dedicated else ' + worker 0'}, {W} data-parallel "
                     f"worker(s); " + ("RCCL reduce(grads) + broadcast(params) over xGMI" if a.mode == "sync" else
                                       "shm mailbox control + RCCL send/recv over xGMI")
@@ -204,12 +221,13 @@ def main():
                 "sync_steps": 1,
                 "codec": a.codec if a.codec != "topk" else f"topk({a.topk_ratio}) + error feedback",
                 "fetch_codec": a.fetch_codec if t is not None else "in-process",
-                "weight_image": getattr(chan, "image_wire", None) is not None,
+                "weight_image": getattr(chan, "image_wire", None) is not None or sharded,
                 "overlap": (f"bucketed reduce/apply/broadcast during backward ({len(chan.buckets)} buckets)"
                             if getattr(chan, "overlap", False) else
                             f"bucketed reduce/apply/broadcast captured in the step graph ({len(chan.buckets)} buckets)"
                             if getattr(chan, "in_graph", False) else "none"),
-                "topology": "dedicated" if dedicated else ("colocated" if t is not None else "loopback"),
+                "topology": ("sharded" if sharded else "dedicated" if dedicated else
+                             ("colocated" if t is not None else "loopback")),
                 "transport": (("native RCCL (psx comm)" if getattr(t, "native", False) else "torch.distributed")
                               if t is not None else "in-process"),
                 "hip_graph": cfg.use_graph,

@@ -9,6 +9,8 @@ int psx_comm_send(void* h, const void* buf, long count, int dtype, int peer, hip
 int psx_comm_recv(void* h, void* buf, long count, int dtype, int peer, hipStream_t st);
 int psx_comm_reduce_sum(void* h, const void* send, void* recv, long count, int dtype, int root, hipStream_t st);
 int psx_comm_broadcast(void* h, void* buf, long count, int dtype, int root, hipStream_t st);
+int psx_comm_reduce_scatter_sum(void* h, const void* send, void* recv, long count, int dtype, hipStream_t st);
+int psx_comm_all_gather(void* h, const void* send, void* recv, long count, int dtype, hipStream_t st);
 }
 
 // psx dtype codes (parallel/rccl.py DTYPES)

@@ -33,6 +33,8 @@ struct Api {
   decltype(&ncclReduce) reduce = nullptr;
   decltype(&ncclBroadcast) broadcast = nullptr;
   decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclReduceScatter) reduce_scatter = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
   decltype(&ncclSend) send = nullptr;
   decltype(&ncclRecv) recv = nullptr;
   decltype(&ncclGroupStart) group_start = nullptr;
@@ -82,6 +84,7 @@ int psx_comm_load(const char* path) {
             sym(lib, "ncclCommDestroy", &a.comm_destroy) && sym(lib, "ncclCommAbort", &a.comm_abort) &&
             sym(lib, "ncclCommGetAsyncError", &a.async_error) && sym(lib, "ncclReduce", &a.reduce) &&
             sym(lib, "ncclBroadcast", &a.broadcast) && sym(lib, "ncclAllReduce", &a.all_reduce) &&
+            sym(lib, "ncclReduceScatter", &a.reduce_scatter) && sym(lib, "ncclAllGather", &a.all_gather) &&
             sym(lib, "ncclSend", &a.send) && sym(lib, "ncclRecv", &a.recv) &&
             sym(lib, "ncclGroupStart", &a.group_start) && sym(lib, "ncclGroupEnd", &a.group_end) &&
             sym(lib, "ncclGetErrorString", &a.error_string);
@@ -146,6 +149,25 @@ int psx_comm_all_reduce_sum(void* h, const void* send, void* recv, long count, i
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
   return (int)g_api.all_reduce(send, recv, (size_t)count, t, ncclSum, (ncclComm_t)h, st);
+}
+
+// Sharded server (parallel/sharded.py): rank r receives the sum of every rank's
+// send[r*count, (r+1)*count) in recv (recv may be send + r*count: in place).
+int psx_comm_reduce_scatter_sum(void* h, const void* send, void* recv, long count, int dtype, hipStream_t st) {
+  if (!g_api.lib) return kNotLoaded;
+  ncclDataType_t t;
+  if (!to_nccl(dtype, &t)) return kBadDtype;
+  std::lock_guard<std::mutex> lk(g_enqueue);
+  return (int)g_api.reduce_scatter(send, recv, (size_t)count, t, ncclSum, (ncclComm_t)h, st);
+}
+
+// rank r's `count` elements land at recv + r*count on every rank (send == recv + r*count: in place)
+int psx_comm_all_gather(void* h, const void* send, void* recv, long count, int dtype, hipStream_t st) {
+  if (!g_api.lib) return kNotLoaded;
+  ncclDataType_t t;
+  if (!to_nccl(dtype, &t)) return kBadDtype;
+  std::lock_guard<std::mutex> lk(g_enqueue);
+  return (int)g_api.all_gather(send, recv, (size_t)count, t, (ncclComm_t)h, st);
 }
 
 int psx_comm_broadcast(void* h, void* buf, long count, int dtype, int root, hipStream_t st) {

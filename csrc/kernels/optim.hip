@@ -183,6 +183,7 @@ struct SmallScatter {
   long n;
   float* dst;
   int gather;
+  const long* sidx;  // optional source positions: dst[idx[j]] = src[sidx[j]] (sharded wire)
 };
 constexpr int kScatterPerBlock = 2048;
 
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(256) void param_unpack_tiles_kernel(const ST* __res
       const long j = base + r * 256 + threadIdx.x;
       if (j < sc.n) {
         const long k = sc.idx[j];
-        sc.dst[k] = sc.src[sc.gather ? k : j];
+        sc.dst[k] = sc.src[sc.sidx ? sc.sidx[j] : (sc.gather ? k : j)];
       }
     }
     return;
@@ -351,13 +352,13 @@ int psx_param_unpack(const float* arena, const void* descs, int ndesc, void* wbu
 
 // Flat-grid unpack (one workgroup per 32x32 tile of every conv; ntiles = sum of the tiles, each
 // desc's tile0 = its first tile). src_bf16: the source is a bf16 image instead of the fp32 arena.
-// sc_src/sc_idx/sc_n/sc_dst: optional SmallScatter (sc_n = 0: none), see above.
+// sc_src/sc_idx/sc_n/sc_dst/sc_gather/sc_sidx: optional SmallScatter (sc_n = 0: none), see above.
 int psx_param_unpack_tiles(const void* src, int src_bf16, const void* descs, int ndesc, int ntiles, void* wbuf,
                            const float* sc_src, const long* sc_idx, long sc_n, float* sc_dst, int sc_gather,
-                           hipStream_t st) {
+                           const long* sc_sidx, hipStream_t st) {
   if (ntiles <= 0 || ndesc <= 0) return 0;
   if (ndesc > 256) return (int)hipErrorInvalidValue;  // the kernel's LDS desc table
-  const SmallScatter sc{sc_src, sc_idx, sc_n > 0 ? sc_n : 0, sc_dst, sc_gather};
+  const SmallScatter sc{sc_src, sc_idx, sc_n > 0 ? sc_n : 0, sc_dst, sc_gather, sc_sidx};
   const long nsb = (sc.n + kScatterPerBlock - 1) / kScatterPerBlock;
   const dim3 grid((unsigned)(ntiles + nsb));
   if (src_bf16)

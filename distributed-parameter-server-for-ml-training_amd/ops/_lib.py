@@ -65,7 +65,7 @@ _KERNEL_SIGS = {
     "psx_fp16_pack": (i32, [vp, vp, i64, f32, vp]),
     "psx_fp16_unpack": (i32, [vp, vp, i64, f32, vp]),
     "psx_param_unpack": (i32, [vp, vp, i32, vp, vp]),
-    "psx_param_unpack_tiles": (i32, [vp, i32, vp, i32, i32, vp, vp, vp, i64, vp, i32, vp]),
+    "psx_param_unpack_tiles": (i32, [vp, i32, vp, i32, i32, vp, vp, vp, i64, vp, i32, vp, vp]),
     "psx_unpack_desc_size": (i32, []),
     "psx_synth_gen": (i32, [vp, vp, i32, i32, i32, i32, u32, u32, vp]),
     "psx_augment": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, u32, vp, i32, vp, vp, vp, i64, vp, i64, vp]),
@@ -119,6 +119,8 @@ _COMM_SIGS = {
     "psx_comm_reduce_sum": (i32, [vp, vp, vp, i64, i32, i32, vp]),
     "psx_comm_all_reduce_sum": (i32, [vp, vp, vp, i64, i32, vp]),
     "psx_comm_broadcast": (i32, [vp, vp, i64, i32, i32, vp]),
+    "psx_comm_reduce_scatter_sum": (i32, [vp, vp, vp, i64, i32, vp]),
+    "psx_comm_all_gather": (i32, [vp, vp, vp, i64, i32, vp]),
     "psx_comm_send": (i32, [vp, vp, i64, i32, i32, vp]),
     "psx_comm_recv": (i32, [vp, vp, i64, i32, i32, vp]),
     "psx_comm_group_start": (i32, []),

@@ -335,17 +335,22 @@ def param_unpack(arena, descs_dev, ndesc, wbuf):
 def param_unpack_tiles(src, descs_dev, ndesc, ntiles, wbuf, scatter=None):
     """Flat-grid unpack (one workgroup per 64x64 tile x 3-tap chunk of every conv). ``src`` is
     the fp32 arena or a bf16 weight image with the same element offsets; descs carry each conv's
-    first tile. ``scatter = (src_f32, idx_i64, dst_f32, gather)``: extra workgroups of the same
-    launch write dst[idx[j]] = src[j] (gather False) or src[idx[j]] (gather True)."""
+    first tile. ``scatter = (src_f32, idx_i64, dst_f32, gather[, sidx_i64])``: extra workgroups
+    of the same launch write dst[idx[j]] = src[j] (gather False), src[idx[j]] (gather True) or
+    src[sidx[j]] (sidx given: the sharded wire's padded per-rank blocks)."""
     assert src.dtype in (torch.float32, torch.bfloat16), src.dtype
-    sc = (None, None, 0, None, 0)
+    sc = (None, None, 0, None, 0, None)
     if scatter is not None:
-        s_src, s_idx, s_dst, gather = scatter
+        s_src, s_idx, s_dst, gather = scatter[:4]
+        sidx = scatter[4] if len(scatter) > 4 else None
         assert s_src.dtype == torch.float32 and s_dst.dtype == torch.float32 and s_idx.dtype == torch.int64
         assert s_src.device == s_dst.device == s_idx.device == src.device
         n = s_idx.numel()
-        assert gather or s_src.numel() >= n
-        sc = (ptr(s_src), ptr(s_idx), n, ptr(s_dst), int(bool(gather)))
+        if sidx is not None:
+            assert sidx.dtype == torch.int64 and sidx.numel() == n and sidx.device == src.device
+        else:
+            assert gather or s_src.numel() >= n
+        sc = (ptr(s_src), ptr(s_idx), n, ptr(s_dst), int(bool(gather)), ptr(sidx) if sidx is not None else None)
     check(kernels().psx_param_unpack_tiles(ptr(src), int(src.dtype == torch.bfloat16), ptr(descs_dev), ndesc,
                                            int(ntiles), ptr(wbuf), *sc, stream_ptr()), "param_unpack_tiles")
 

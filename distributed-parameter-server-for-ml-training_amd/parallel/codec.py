@@ -116,6 +116,14 @@ class WeightWire:
     def consume_small(self, local_arena: torch.Tensor):
         local_arena.index_copy_(0, self.small_index, self.small)
 
+    def scatter_spec(self, local_arena: torch.Tensor, small_from: torch.Tensor | None = None):
+        """How the unpack launch scatters the fp32 remainder into ``local_arena``
+        (kernels.param_unpack_tiles ``scatter``): from this wire, or gathered straight from the
+        server arena ``small_from``."""
+        if small_from is not None:
+            return (small_from, self.small_index, local_arena, True)
+        return (self.small, self.small_index, local_arena, False)
+
     def to_arena(self, local_arena: torch.Tensor):
         """Materialise the full fp32 state (conv weights exact from bf16) — tests/diagnostics."""
         local_arena[: self.layout.param_numel].copy_(self.img)

@@ -92,6 +92,13 @@ class TorchCompute:
     def last_loss(self) -> float:
         return self._loss
 
+    def pad_grads(self, n: int):
+        """Grow the gradient wire buffer to n elements (zero tail), see HipCompute.pad_grads."""
+        if self.grads.numel() < n:
+            g = torch.zeros(n, dtype=self.grads.dtype)
+            g[: self.grads.numel()].copy_(self.grads)
+            self.grads = g
+
     def step_stats(self):
         """(sum of per-sample losses, #correct) of the last train step."""
         return torch.tensor(self._loss * self.B, dtype=torch.float64), torch.tensor(self._correct)
@@ -159,11 +166,16 @@ class HipCompute:
         round) — the remainder is then gathered from it directly and the server need not
         publish it. The local arena's conv-weight region is not used any more."""
         self.wire = wire
-        if small_from is not None:
-            sc = (small_from, wire.small_index, self.local_arena, True)
-        else:
-            sc = (wire.small, wire.small_index, self.local_arena, False)
-        self.engine.set_weight_source(wire.img, scatter=sc)
+        self.engine.set_weight_source(wire.img, scatter=wire.scatter_spec(self.local_arena, small_from))
+
+    def pad_grads(self, n: int):
+        """Grow the gradient wire buffer to n elements (zero tail): collectives that split it
+        into equal per-rank chunks (the sharded server's reduce-scatter). Invalidates graphs."""
+        if self.grads.numel() < n:
+            g = torch.zeros(n, dtype=self.grads.dtype, device=self.grads.device)
+            g[: self.grads.numel()].copy_(self.grads)
+            self.engine.grads = self.grads = g
+            self.engine.graph = self.engine.graphs = None
 
     def train_step(self, dataset, idx, on_bucket=None, round_hooks=None):
         seg = (lambda k: on_bucket(k, self.grads)) if on_bucket is not None else None

@@ -109,6 +109,20 @@ class NativeComm:
         code, _ = _dt(t)
         _check(comm().psx_comm_broadcast(self.h, t.data_ptr(), t.numel(), code, root, _stream(stream)), "ncclBroadcast")
 
+    def reduce_scatter_sum(self, t: torch.Tensor, out: torch.Tensor, stream=None):
+        """out (numel/world) = sum over ranks of this rank's slice of t (out may be that slice)."""
+        code, _ = _dt(t)
+        assert t.numel() == out.numel() * self.world and t.dtype == out.dtype
+        _check(comm().psx_comm_reduce_scatter_sum(self.h, t.data_ptr(), out.data_ptr(), out.numel(), code,
+                                                  _stream(stream)), "ncclReduceScatter")
+
+    def all_gather(self, t: torch.Tensor, out: torch.Tensor, stream=None):
+        """out[r*numel:(r+1)*numel] = rank r's t on every rank (t may be this rank's slice of out)."""
+        code, _ = _dt(t)
+        assert out.numel() == t.numel() * self.world and t.dtype == out.dtype
+        _check(comm().psx_comm_all_gather(self.h, t.data_ptr(), out.data_ptr(), t.numel(), code, _stream(stream)),
+               "ncclAllGather")
+
     def gather(self, t: torch.Tensor, out: torch.Tensor | None, root: int = 0, stream=None):
         """Equal-size tensors of every rank -> ``out`` ([world * numel], root only)."""
         code, esz = _dt(t)
@@ -175,6 +189,15 @@ class RcclTransport(DistTransport):
             return list(flat.view(self.world_size, t.numel()).unbind(0))
         self.comm.gather(t, None, 0)
         return None
+
+    # ---- sharded server (parallel/sharded.py)
+    def reduce_scatter_sum(self, t, out):
+        self.comm.reduce_scatter_sum(t, out)
+        return out
+
+    def all_gather_into(self, buf, chunk: int):
+        self.comm.all_gather(buf[self.rank * chunk:(self.rank + 1) * chunk], buf[: chunk * self.world_size])
+        return buf
 
     # ---- bucketed (overlapped) round: non-blocking on the communication stream
     def _on_comm_stream(self, fn):

@@ -37,6 +37,7 @@ from .native_loop import NativeAsyncChannel, NativeLocalChannel, NativeServerLoo
 from .overlap import OverlapSyncChannel, plan_buckets
 from .server import ParameterServer
 from .rccl import make_transport
+from .sharded import ShardedSyncChannel
 from .transport import LocalTransport, env_world
 from .worker import (AsyncChannel, InProcessChannel, LocalAsyncChannel, SyncCollectiveChannel, Worker)
 
@@ -162,6 +163,7 @@ def run_distributed(cfg, log=print) -> dict:
     device = _device_for(local)
     t = make_transport(device)
     dedicated = cfg.topology == "dedicated" and world > 1
+    sharded = cfg.topology == "sharded"
     worker_ranks = list(range(1, world)) if dedicated else list(range(world))
     W = len(worker_ranks)
     wid_of_rank = {r: i for i, r in enumerate(worker_ranks)}
@@ -176,6 +178,9 @@ def run_distributed(cfg, log=print) -> dict:
     server = None
     if rank == 0:
         server = ParameterServer(cfg, layout, arena, counters, device=device, total_workers=W, log=log)
+    elif sharded:  # this rank's share of the server (parallel/sharded.py)
+        server = ParameterServer(cfg, layout, arena, counters, device=device, total_workers=W,
+                                 log=lambda *a, **k: None)
     is_worker = rank in wid_of_rank
     train, test = make_datasets(cfg, device, classes) if is_worker else (None, None)
     n_train = max(t.all_gather_object(len(train) if train is not None else 0))
@@ -192,7 +197,10 @@ def run_distributed(cfg, log=print) -> dict:
         if rank == 0:
             for r in worker_ranks:
                 server.register_worker(names[r], wid_of_rank[r])
-        chan = make_sync_channel(cfg, t, server, W, layout, device, worker=is_worker)
+        if sharded:
+            chan = ShardedSyncChannel(cfg, t, server, list(range(W)), layout, device, in_place=device.type == "cuda")
+        else:
+            chan = make_sync_channel(cfg, t, server, W, layout, device, worker=is_worker)
         chan._gs = done  # non-server ranks track the global step locally
         if is_worker:
             wk = Worker(cfg, comp, chan, train, test, worker_name=names[rank], rank=rank, log=lg,
@@ -206,6 +214,8 @@ def run_distributed(cfg, log=print) -> dict:
         sess.run_training(skip_steps=done // max(1, W))
         sess.close()
         wk = sess.worker
+    if cfg.mode == "sync" and sharded:
+        chan.gather_master()  # rank 0's arena = the full trained state (final metrics)
     if device.type == "cuda":
         torch.cuda.synchronize()
     wall = time.time() - t0
@@ -213,7 +223,7 @@ def run_distributed(cfg, log=print) -> dict:
     result = {"worker": getattr(wk, "final_metrics", None)}
     if rank == 0:
         extra = {"images_per_second": round(sum(imgs) / wall, 2) if wall > 0 else 0.0, "gpus": world,
-                 "topology": "dedicated" if dedicated else "colocated"}
+                 "topology": cfg.topology if world > 1 or sharded else "colocated"}
         server.images_processed = sum(imgs)
         result["server"] = server.final_metrics(emit=True, extra=extra)
     t.close()

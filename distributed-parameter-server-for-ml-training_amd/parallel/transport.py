@@ -43,6 +43,13 @@ class LocalTransport:
     def gather_to_server(self, t):
         return [t]
 
+    def reduce_scatter_sum(self, t, out):
+        out.copy_(t[: out.numel()])
+        return out
+
+    def all_gather_into(self, buf, chunk: int):
+        return buf
+
     def isend(self, t, dst):
         raise RuntimeError("LocalTransport has no peers")
 
@@ -96,6 +103,30 @@ class DistTransport:
     def broadcast_from_server(self, t):
         dist.broadcast(t, src=0)
         return t
+
+    def reduce_scatter_sum(self, t, out):
+        """Sharded server push: out = sum over ranks of this rank's slice of t (t.numel() ==
+        world * out.numel()). gloo has no reduce-scatter: all-reduce + slice there."""
+        if self.backend == "gloo":
+            tmp = t.clone()
+            dist.all_reduce(tmp, op=dist.ReduceOp.SUM)
+            out.copy_(tmp[self.rank * out.numel():(self.rank + 1) * out.numel()])
+            return out
+        dist.reduce_scatter_tensor(out, t, op=dist.ReduceOp.SUM)
+        return out
+
+    def all_gather_into(self, buf, chunk: int):
+        """Sharded server fetch: buf[r*chunk:(r+1)*chunk] of rank r reaches every rank, in place."""
+        if buf.element_size() == 2:  # a pure copy: move the bits as int32 pairs (gloo has no 16-bit ints)
+            assert chunk % 2 == 0 and buf.numel() % 2 == 0
+            buf, chunk = buf.view(torch.int32), chunk // 2
+        mine = buf[self.rank * chunk:(self.rank + 1) * chunk]
+        if self.backend == "gloo":
+            parts = list(buf[: chunk * self.world_size].split(chunk))
+            dist.all_gather(parts, mine.clone())
+            return buf
+        dist.all_gather_into_tensor(buf[: chunk * self.world_size], mine)
+        return buf
 
     def gather_to_server(self, t):
         """Equal-size tensors of every rank -> list on rank 0 (RCCL gather: point-to-point

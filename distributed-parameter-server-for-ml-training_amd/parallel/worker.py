@@ -266,6 +266,8 @@ class Worker:
     def connect_to_server(self):
         self.worker_id, self.total_workers = self.channel.register(self.worker_name, self.requested_id)
         self.log(f"Registered as Worker {self.worker_id} (Total workers: {self.total_workers})")
+        if hasattr(self.channel, "bind_compute"):  # e.g. the sharded round pads the gradient wire
+            self.channel.bind_compute(self.compute)
         wire = self.channel.weight_wire() if hasattr(self.channel, "weight_wire") else None
         if wire is not None:  # fetches land in a WeightWire the step reads in place
             small_from = self.channel.small_source() if hasattr(self.channel, "small_source") else None

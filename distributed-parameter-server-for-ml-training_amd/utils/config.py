@@ -46,7 +46,8 @@ class PSConfig:
     model: str = "resnet18"
     num_classes: int | None = None
     gpus: int = 1                  # processes / GPUs on this node (1 = server+worker co-located)
-    topology: str = "colocated"    # colocated: rank 0 = PS + worker 0; dedicated: rank 0 = PS only
+    topology: str = "colocated"    # colocated: rank 0 = PS + worker 0; dedicated: rank 0 = PS only;
+    #                                sharded: every rank = worker + 1/world of the PS (parallel/sharded.py)
     codec: str = "fp16"            # none (fp32 wire) | fp16 (reference) | topk
     topk_ratio: float = 0.01
     dtype: str = "bf16"            # compute dtype of the HIP engine
@@ -90,8 +91,13 @@ class PSConfig:
             raise ValueError("Number of workers must be between 1 and 32")
         if self.codec not in ("none", "fp16", "topk"):
             raise ValueError(f"--codec must be none, fp16 or topk, got {self.codec!r}")
-        if self.topology not in ("colocated", "dedicated"):
-            raise ValueError(f"--topology must be colocated or dedicated, got {self.topology!r}")
+        if self.topology not in ("colocated", "dedicated", "sharded"):
+            raise ValueError(f"--topology must be colocated, dedicated or sharded, got {self.topology!r}")
+        if self.topology == "sharded":  # parallel/sharded.py scope
+            if self.mode != "sync" or self.codec not in ("fp16", "none") or self.bn_sync or self.ckpt_every \
+                    or self.resume or max(1, self.sync_steps) != 1 or self.overlap:
+                raise ValueError("--topology sharded: sync mode, dense fp16/fp32 gradients, one push per batch, "
+                                 "no --bn-sync / --overlap / checkpoints")
         if self.sync_semantics not in ("barrier", "reference"):
             raise ValueError("--sync-semantics must be barrier or reference")
         if self.staleness_bound < 0:
@@ -125,7 +131,7 @@ def add_arguments(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     A("--model", choices=["resnet18", "resnet50", "resnet_tiny"], default=None)
     A("--num-classes", type=int, default=None)
     A("--gpus", "--nproc", dest="gpus", type=int, default=None)
-    A("--topology", choices=["colocated", "dedicated"], default=None)
+    A("--topology", choices=["colocated", "dedicated", "sharded"], default=None)
     A("--codec", choices=["none", "fp16", "topk"], default=None)
     A("--topk-ratio", type=float, default=None)
     A("--dtype", choices=["bf16"], default=None)

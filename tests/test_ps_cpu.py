@@ -304,6 +304,39 @@ def test_dist_sync_overlap_matches_serial(extra):
     assert outs[True]["final_param_checksum"] == pytest.approx(outs[False]["final_param_checksum"], rel=1e-6)
 
 
+@pytest.mark.parametrize("codec", ["none", "fp16"])
+def test_dist_sharded_server_matches_rank0_server(codec):
+    """--topology sharded (parallel/sharded.py: reduce-scatter, per-rank range apply, all-gather
+    of the bf16 image + fp32 remainder) ends in the rank-0 PS's parameters (3 ranks, gloo)."""
+    outs = {}
+    for topo in ("sharded", "colocated"):
+        recs, _ = _spawn(3, ["--mode", "sync", "--codec", codec, "--topology", topo] + TINY)
+        srv = [r for r in recs if r["type"] == "SERVER_FINAL_METRICS"]
+        assert len(srv) == 1
+        outs[topo] = srv[0]
+    assert outs["sharded"]["topology"] == "sharded"
+    assert outs["sharded"]["global_steps_completed"] == outs["colocated"]["global_steps_completed"] > 0
+    assert outs["sharded"]["gradients_processed"] == outs["colocated"]["gradients_processed"]
+    # the gradient sums come from different collectives (gloo all-reduce vs reduce): their
+    # rounding differs (fp32: ~1e-6 of the checksum after the run; fp16 sums: ~2e-5)
+    assert outs["sharded"]["final_param_checksum"] == pytest.approx(outs["colocated"]["final_param_checksum"],
+                                                                    rel=1e-5 if codec == "none" else 1e-4)
+
+
+def test_shard_plan_covers_every_entry_once():
+    from psx.models.resnet import ResNet18
+    from psx.parallel.codec import small_index_of
+    from psx.parallel.sharded import ShardPlan
+
+    lay = ParamLayout.from_module(ResNet18(100))
+    for world in (1, 2, 3, 8):
+        p = ShardPlan(lay, world)
+        assert p.chunk % 8 == 0 and p.padded >= lay.param_numel and p.lo[0] == 0 and p.hi[-1] == lay.param_numel
+        assert all(a == b for a, b in zip(p.hi, p.lo[1:]))
+        assert torch.equal(p.dst.sort().values, small_index_of(lay).sort().values)
+        assert p.src.max().item() < world * p.S and len(set(p.src.tolist())) == p.src.numel()
+
+
 @pytest.mark.parametrize("topology", ["colocated", "dedicated"])
 def test_fault_restart_resumes_from_checkpoint(tmp_path, topology):
     """Worker 1 dies at its step 5; torchrun restarts the group, the server resumes from the

@@ -132,3 +132,28 @@ def test_graph_round_matches_serial_round(graph):
     assert sa == sb == 6
     assert abs(a - b) <= 2e-4 * max(abs(a), abs(b)), out
     assert acc_a >= 0.0 and acc_b >= 0.0
+
+
+_SHARD = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+import psx
+from psx.parallel.runner import run_distributed
+from psx.utils.config import PSConfig
+cfg = PSConfig(model="resnet18", batch_size=64, epochs=1, train_samples=2048, eval_every=0, verbose=0, lr=0.1,
+               max_steps=6, mode="sync", topology={topo!r}).validate()
+res = run_distributed(cfg, log=lambda *a, **k: None)
+print("RESULT " + json.dumps([res["server"]["final_param_checksum"], res["server"]["global_steps_completed"]]))
+"""
+
+
+def test_sharded_server_world1_matches_rank0_server():
+    """--topology sharded on the native communicator (reduce-scatter / all-gather, range apply
+    writing the bf16 image, the HIP engine reading the sharded wire in place with the source-
+    indexed fp32 scatter) against the default rank-0 PS; world size 1."""
+    out = {}
+    for topo, port in (("sharded", 29655), ("colocated", 29656)):
+        out[topo] = _run(_SHARD.format(root=ROOT, topo=topo), port)
+    (a, sa), (b, sb) = out["sharded"], out["colocated"]
+    assert sa == sb == 6
+    assert abs(a - b) <= 2e-4 * max(abs(a), abs(b)), out

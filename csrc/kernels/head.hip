@@ -152,6 +152,123 @@ __global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict
   }
 }
 
+// ---- large heads (ResNet-50: 2048 -> 1000): the fused kernel above streams the whole FC matrix
+// through every per-sample workgroup twice (2 x 8 MB x B); split into pool -> logits GEMM ->
+// softmax/xent -> dpooled GEMM (+ broadcast to dact), each matrix read once per 32-sample tile.
+
+// pooled[b][c] = mean over the HW pixels; grid (B, ceil(C / 512)), 2 channels per thread
+__global__ __launch_bounds__(256) void head_pool_kernel(const uint16_t* __restrict__ act, int HW, int C,
+                                                        float* __restrict__ pooled) {
+  const int b = blockIdx.x, c = blockIdx.y * 512 + 2 * threadIdx.x;
+  if (c >= C) return;
+  const uint16_t* a = act + (size_t)b * HW * C + c;
+  float s0 = 0.f, s1 = 0.f;
+  for (int p = 0; p < HW; ++p) {
+    const uint32_t v = *reinterpret_cast<const uint32_t*>(a + (size_t)p * C);
+    s0 += lo_bf(v);
+    s1 += hi_bf(v);
+  }
+  const float inv = 1.f / (float)HW;
+  *reinterpret_cast<float2*>(pooled + (size_t)b * C + c) = make_float2(s0 * inv, s1 * inv);
+}
+
+// out[m][n] = sum_k A[m][k] * B(k, n), fp32, 32 x 64 tile per workgroup (2 x 4 per thread), k in
+// chunks of 32 through LDS. BT: B(k, n) = Bm[n][k] (FC rows: logits); else Bm[k][n] (dpooled).
+// EPI 0: out fp32 + bias[n]; EPI 1: dact bf16 = out / HW written to all HW pixels of sample m.
+template <bool BT, int EPI>
+__global__ __launch_bounds__(256) void head_gemm_kernel(const float* __restrict__ A, const float* __restrict__ Bm,
+                                                        int M, int N, int Kd, const float* __restrict__ bias,
+                                                        float* __restrict__ out, uint16_t* __restrict__ dact,
+                                                        int HW) {
+  __shared__ float As[32][33];
+  __shared__ float Bs[32][68];
+  const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 64;
+  float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  for (int k0 = 0; k0 < Kd; k0 += 32) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // A tile 32 x 32, coalesced along k
+      const int idx = i * 256 + tid, mm = idx >> 5, kk = idx & 31;
+      As[mm][kk] = (m0 + mm < M && k0 + kk < Kd) ? A[(size_t)(m0 + mm) * Kd + k0 + kk] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // B tile 32 (k) x 64 (n)
+      const int idx = i * 256 + tid;
+      if (BT) {  // coalesced along k of row n
+        const int nn = idx >> 5, kk = idx & 31;
+        Bs[kk][nn] = (n0 + nn < N && k0 + kk < Kd) ? Bm[(size_t)(n0 + nn) * Kd + k0 + kk] : 0.f;
+      } else {   // coalesced along n of row k
+        const int kk = idx >> 6, nn = idx & 63;
+        Bs[kk][nn] = (n0 + nn < N && k0 + kk < Kd) ? Bm[(size_t)(k0 + kk) * N + n0 + nn] : 0.f;
+      }
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int kk = 0; kk < 32; ++kk) {
+      const float a0 = As[2 * ty][kk], a1 = As[2 * ty + 1][kk];
+      const float4 bv = *reinterpret_cast<const float4*>(&Bs[kk][4 * tx]);
+      acc[0][0] += a0 * bv.x; acc[0][1] += a0 * bv.y; acc[0][2] += a0 * bv.z; acc[0][3] += a0 * bv.w;
+      acc[1][0] += a1 * bv.x; acc[1][1] += a1 * bv.y; acc[1][2] += a1 * bv.z; acc[1][3] += a1 * bv.w;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + 2 * ty + i;
+    if (m >= M) continue;
+    const int n = n0 + 4 * tx;
+    if (EPI == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (n + j < N) out[(size_t)m * N + n + j] = acc[i][j] + bias[n + j];
+    } else if (n + 3 < N) {  // N (channels) is a multiple of 64 on this path
+      const float inv = 1.f / (float)HW;
+      u32x2 v;
+      v[0] = pack_bf2(acc[i][0] * inv, acc[i][1] * inv);
+      v[1] = pack_bf2(acc[i][2] * inv, acc[i][3] * inv);
+      for (int p = 0; p < HW; ++p) *reinterpret_cast<u32x2*>(dact + ((size_t)m * HW + p) * N + n) = v;
+    }
+  }
+}
+
+// one wave per sample: logits row (in dl) -> loss, accuracy, dlogits = (softmax - onehot) / B in place
+__global__ __launch_bounds__(64) void head_softmax_kernel(float* __restrict__ dl, int K, const int* __restrict__ labels,
+                                                          float* __restrict__ loss, int* __restrict__ correct,
+                                                          float invB, int bwd) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  float* row = dl + (size_t)b * K;
+  float mx = -INFINITY;
+  int arg = 0;
+  for (int k = lane; k < K; k += 64) {
+    const float v = row[k];
+    if (v > mx) {
+      mx = v;
+      arg = k;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(arg, o, 64);
+    if (om > mx || (om == mx && oa < arg)) {
+      mx = om;
+      arg = oa;
+    }
+  }
+  float se = 0.f;
+  for (int k = lane; k < K; k += 64) se += __expf(row[k] - mx);
+  se = wave_sum(se);
+  const float lse = mx + __logf(se);
+  const int y = labels[b];
+  const float ly = row[y];
+  if (lane == 0) {
+    if (loss) loss[b] = lse - ly;
+    if (correct && arg == y) atomicAdd(correct, 1);
+  }
+  if (bwd)
+    for (int k = lane; k < K; k += 64) row[k] = (__expf(row[k] - lse) - (k == y ? 1.f : 0.f)) * invB;
+}
+
 }  // namespace psx
 
 using namespace psx;
@@ -161,6 +278,18 @@ extern "C" {
 int psx_head_fwd_bwd(const void* act, int B, int HW, int C, const float* fcw, const float* fcb, int K,
                      const int* labels, float* pooled, float* dlogits, void* dact, float* loss, int* correct,
                      hipStream_t st) {
+  if ((long)K * C > (1L << 18) && C % 64 == 0 && pooled && dlogits) {  // large head: split path
+    hipLaunchKernelGGL(head_pool_kernel, dim3(B, (C + 511) / 512), dim3(256), 0, st, (const uint16_t*)act, HW, C,
+                       pooled);
+    hipLaunchKernelGGL((head_gemm_kernel<true, 0>), dim3((K + 63) / 64, (B + 31) / 32), dim3(256), 0, st, pooled,
+                       fcw, B, K, C, fcb, dlogits, (uint16_t*)nullptr, HW);
+    hipLaunchKernelGGL(head_softmax_kernel, dim3(B), dim3(64), 0, st, dlogits, K, labels, loss, correct,
+                       1.f / (float)B, dact ? 1 : 0);
+    if (dact)
+      hipLaunchKernelGGL((head_gemm_kernel<false, 1>), dim3(C / 64, (B + 31) / 32), dim3(256), 0, st, dlogits, fcw,
+                         B, C, K, (const float*)nullptr, (float*)nullptr, (uint16_t*)dact, HW);
+    return (int)hipGetLastError();
+  }
   if (K > 1024 || C % 16 || (C > 512 && C % 512)) return -2;
   const size_t lds = (size_t)(C + K + 64) * sizeof(float);
   if (dact)

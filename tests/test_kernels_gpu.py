@@ -216,10 +216,13 @@ def test_bn_backward(c, hw, two):
     assert _rel(dz, (go * (o > 0)).permute(0, 2, 3, 1)) < 1e-2
 
 
-def test_head_fwd_bwd():
+@pytest.mark.parametrize("b,hw,c,k", [(32, 16, 512, 100), (40, 49, 2048, 1000)])
+def test_head_fwd_bwd(b, hw, c, k):
+    """Fused per-sample head (ResNet-18) and the split pool/GEMM/softmax path (ResNet-50 2048 ->
+    1000, batch not a multiple of the 32-sample tile) against torch fp32 autograd."""
     torch.manual_seed(5)
-    b, hw, c, k = 32, 16, 512, 100
-    act = torch.rand(b, 4, 4, c, device=DEV).to(torch.bfloat16)
+    side = int(hw ** 0.5)
+    act = torch.rand(b, side, side, c, device=DEV).to(torch.bfloat16)
     w = (torch.randn(k, c, device=DEV) * 0.05).requires_grad_(True)
     bias = torch.randn(k, device=DEV).requires_grad_(True)
     lab = torch.randint(0, k, (b,), device=DEV, dtype=torch.int32)
@@ -234,6 +237,7 @@ def test_head_fwd_bwd():
     lossv = torch.zeros(b, device=DEV)
     correct = torch.zeros(1, dtype=torch.int32, device=DEV)
     K.head_fwd_bwd(act, b, hw, c, w.detach(), bias.detach(), k, lab, pooled, dlog, dact, lossv, correct)
+    assert _rel(pooled, pooled_ref) < 1e-5
     assert abs(lossv.mean().item() - loss.item()) < 1e-3
     assert correct.item() == int((logits.argmax(1) == lab.long()).sum())
     assert _rel(dact, a.grad) < 1e-2

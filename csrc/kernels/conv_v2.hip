@@ -364,7 +364,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     return;
   }
 
-  // ---- LDS-staged epilogue (MODE 0-2; PSX_CV_EPI=0 builds keep the fragment epilogue) ----
+  // ---- LDS-staged epilogue (PSX_CV_EPI=0 builds keep the fragment epilogue) ----
   // The fp32 tile goes through LDS once; then every thread owns 8 channels of a pixel row, so the
   // bf16 output, the residual and the BN-backward operands o / y move as whole 16-byte chunks of
   // 128-byte rows (the fragment layout touched 32-byte pieces of 16 rows per instruction), and
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
 #ifndef PSX_CV_EPI
 #define PSX_CV_EPI 1
 #endif
-  if constexpr (MODE != 3 && PSX_CV_EPI) {
+  if constexpr (PSX_CV_EPI) {
     constexpr int TS = BM + 4;      // fp32 row stride of the staged tile (spreads the banks)
     constexpr int CPR = BM / 8;     // 16-byte bf16 chunks per pixel row
     constexpr int RPP = 256 / CPR;  // pixel rows per pass
@@ -410,7 +410,12 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       const float* src = T + pr * TS + cc * 8;
       const f32x4 va = *reinterpret_cast<const f32x4*>(src), vb = *reinterpret_cast<const f32x4*>(src + 4);
       float v[8] = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
-      const size_t off = (size_t)pix * a.OC + ch0;
+      size_t opix = (size_t)pix;
+      if (MODE == 3) {  // class-local (n, i, j) -> dx (n, 2i+py, 2j+px)
+        const int nn = pix / (CH * CW), rem = pix - nn * CH * CW, ii = rem / CW, jj = rem - ii * CW;
+        opix = ((size_t)nn * a.OH + 2 * ii + py) * a.OW + 2 * jj + px;
+      }
+      const size_t off = opix * a.OC + ch0;
       if (HAS_RES) {
         const u32x4 rr = *reinterpret_cast<const u32x4*>(a.res + off);
 #pragma unroll

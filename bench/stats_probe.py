@@ -23,14 +23,14 @@ def main():
         wf, wd, cp, kg, kgd = make_operands(w)
         x = to_nhwc(torch.randn(B, cin, hw, hw, device="cuda").to(torch.bfloat16).float(), cp)
         y = torch.empty(B, hw, hw, cout, dtype=torch.bfloat16, device="cuda")
-        stats = torch.zeros(32, 2, cout, device="cuda")  # room for a 32-slot A/B build
+        stats = torch.zeros(256, 2, cout, device="cuda")  # room for the A/B builds (<= 256 slot rows)
         dy = torch.randn(B, hw, hw, cout, device="cuda").to(torch.bfloat16)
         dx = torch.empty(B, hw, hw, cp, dtype=torch.bfloat16, device="cuda")
         res = torch.randn(B, hw, hw, cp, device="cuda").to(torch.bfloat16)
         o = torch.randn(B, hw, hw, cp, device="cuda").to(torch.bfloat16)
         y1 = torch.randn(B, hw, hw, cp, device="cuda").to(torch.bfloat16)
         saved = torch.ones(2, cp, device="cuda")
-        part = torch.zeros(32, 3, cp, device="cuda")
+        part = torch.zeros(256, 3, cp, device="cuda")
         b2 = K.bwd_stats_desc(part, o, y1, saved)
         b3 = K.bwd_stats_desc(part, o, y1, saved, y1, saved)
         r = {

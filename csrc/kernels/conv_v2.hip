@@ -480,11 +480,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       const int which = j / BM, row = j - which * BM;
       const float v = red[which * BM + row] + red[(3 + which) * BM + row] + red[(6 + which) * BM + row] +
                       red[(9 + which) * BM + row];
-#ifdef PSX_CV_STATS_NOATOMIC  // timing-only A/B build: plain stores (wrong sums)
-      dst[which * a.OC + oc0 + row] = v;
-#else
       atomicAdd(dst + which * a.OC + oc0 + row, v);
-#endif
     }
     if (st && a.fuse_fin && last_block_arrive(a.fin.counter, gridDim.x, smem))
       bn_finalize_block<PSX_STAT_SLOTS>(a.stats, a.fin);

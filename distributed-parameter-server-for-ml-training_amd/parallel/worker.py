@@ -307,6 +307,25 @@ class Worker:
             self.pushes_rejected += 1
         return ok
 
+    _acc = None
+    _acc_n = 0
+
+    def _accumulate_grads(self, first: bool):
+        """--accumulate: fp32 running sum of this window's batch gradients (stream-ordered)."""
+        g = self.compute.grads
+        if self._acc is None or self._acc.numel() != g.numel() or self._acc.device != g.device:
+            self._acc = torch.zeros(g.numel(), dtype=torch.float32, device=g.device)
+        if first:
+            self._acc.copy_(g)
+            self._acc_n = 1
+        else:
+            self._acc.add_(g.to(torch.float32))
+            self._acc_n += 1
+
+    def _finish_window(self):
+        """The window's mean gradient back into the wire buffer the push sends."""
+        self.compute.grads.copy_(self._acc.mul_(1.0 / max(1, self._acc_n)))
+
     def train_local_batch(self, idx):
         if getattr(self, "_round", False):
             self.compute.train_step(self.train_set, idx, round_hooks=self.channel)
@@ -360,7 +379,13 @@ class Worker:
                             self.fetch_parameters()
                     with self.timer.span("compute_issue"):
                         self.train_local_batch(idx)
-                    if batch_idx % K == 0:
+                    if self.cfg.accumulate and K > 1:  # mean gradient of the window, pushed at its end
+                        self._accumulate_grads(batch_idx % K == 0)
+                        if batch_idx % K == K - 1 or batch_idx == len(batches) - 1:
+                            self._finish_window()
+                            with self.timer.span("push"):
+                                self.push_gradients()
+                    elif batch_idx % K == 0:
                         with self.timer.span("push"):
                             self.push_gradients()
                     if self.cfg.verbose and batch_idx % 50 == 0:

@@ -43,6 +43,8 @@ class PSConfig:
     batch_size: int = 128
     sync_steps: int = 1
     # --- MI355X-native extensions
+    accumulate: bool = False       # --sync-steps K: push the mean gradient of the K batches of a window
+    #                                instead of the reference's first batch only (K-1 discarded)
     model: str = "resnet18"
     num_classes: int | None = None
     gpus: int = 1                  # processes / GPUs on this node (1 = server+worker co-located)
@@ -128,6 +130,8 @@ def add_arguments(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     A("--epochs", type=int, default=None)
     A("--batch-size", type=int, default=None)
     A("--sync-steps", type=int, default=None, help="Local steps between push/fetch (reference semantics)")
+    A("--accumulate", action="store_true", default=None,
+      help="with --sync-steps K: push the mean gradient of all K batches of a window (reference: the first only)")
     A("--model", choices=["resnet18", "resnet50", "resnet_tiny"], default=None)
     A("--num-classes", type=int, default=None)
     A("--gpus", "--nproc", dest="gpus", type=int, default=None)

@@ -29,6 +29,35 @@ def tiny_cfg(**kw):
     return PSConfig(**base).validate()
 
 
+def test_accumulate_pushes_window_mean(monkeypatch):
+    """--sync-steps 2 --accumulate: one push per window of 2 batches, carrying the mean of the
+    window's batch gradients (the reference pushes the first batch's only)."""
+    from psx.parallel import compute as CM
+    from psx.parallel import worker as WM
+
+    batch_g, pushed = [], []
+    orig_step, orig_push = CM.TorchCompute.train_step, WM.InProcessChannel.push
+
+    def step(self, *a, **k):
+        r = orig_step(self, *a, **k)
+        batch_g.append(self.grads.float().clone())
+        return r
+
+    def push(self, worker_id, grads, local_step, buffers=None):
+        pushed.append(grads.float().clone())
+        return orig_push(self, worker_id, grads, local_step, buffers)
+
+    monkeypatch.setattr(CM.TorchCompute, "train_step", step)
+    monkeypatch.setattr(WM.InProcessChannel, "push", push)
+    res = run_local(tiny_cfg(mode="sync", workers=1, sync_steps=2, accumulate=True, eval_every=0),
+                    log=lambda *a, **k: None)
+    nb = len(batch_g)
+    assert nb == 12 and len(pushed) == 6 and res["server"]["global_steps_completed"] == 6
+    for i, p in enumerate(pushed):
+        ref = (batch_g[2 * i] + batch_g[2 * i + 1]) / 2
+        assert torch.allclose(p, ref.half().float(), atol=1e-3, rtol=1e-2), i
+
+
 def test_inprocess_sync_matches_manual_average():
     torch.manual_seed(0)
     cfg = tiny_cfg(mode="sync", workers=2)
@@ -355,3 +384,23 @@ def test_fault_restart_resumes_from_checkpoint(tmp_path, topology):
     steps = -(-(96 // W + 96 % W) // 8)
     srv = [r for r in recs if r["type"] == "SERVER_FINAL_METRICS"]
     assert srv[-1]["global_steps_completed"] == 2 * steps
+
+
+def test_scaling_harness_commands_and_efficiency():
+    """bench/scaling.py: the per-N commands (torchrun on 127.0.0.1 for N > 1, as the driver runs
+    them), the JSON-line parser and the weak-scaling efficiency."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("scaling", os.path.join(ROOT, "bench", "scaling.py"))
+    S = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(S)
+    c1 = S.command(1, 5, 2, ["--mode", "sync"])
+    assert c1[1].endswith("bench.py") and "--gpus" in c1 and "torch.distributed.run" not in c1
+    c8 = S.command(8, 5, 2, ["--mode", "sync"], port=29999)
+    assert "torch.distributed.run" in c8 and "--nproc-per-node=8" in c8 and "127.0.0.1" in c8
+    assert c8[c8.index("--gpus") + 1] == "8"
+    out = 'noise\n{"metric": "m", "value": 100.0, "ms_per_step": 2.0, "unit": "images/s"}\ntrailer\n'
+    assert S.parse_result(out)["value"] == 100.0
+    eff = S.efficiency({1: {"value": 100.0}, 2: {"value": 190.0}, 8: {"value": 640.0}})
+    assert eff == {1: 1.0, 2: 0.95, 8: 0.8}
+    assert S.efficiency({2: {"value": 1.0}}) == {2: None}

@@ -134,8 +134,7 @@ def _interleave(cfg, workers, server, log):
                 if cfg.mode == "sync" and b % K == 0:
                     wk.fetch_parameters()
                 wk.train_local_batch(bt[b])
-                if b % K == 0:
-                    wk.push_gradients()
+                wk.window_push(b, steps, K)
                 if cfg.mode == "async":
                     wk.fetch_parameters()
             if cfg.verbose and b % 50 == 0:

@@ -310,6 +310,21 @@ class Worker:
     _acc = None
     _acc_n = 0
 
+    def window_push(self, batch_idx: int, n_batches: int, K: int) -> bool:
+        """After training batch ``batch_idx`` of an epoch: push per the --sync-steps window rule —
+        the window's first batch (reference, worker.py:367-377), or with --accumulate the mean
+        gradient of the whole window at its last batch. Returns whether a push happened."""
+        if self.cfg.accumulate and K > 1:
+            self._accumulate_grads(batch_idx % K == 0)
+            if batch_idx % K != K - 1 and batch_idx != n_batches - 1:
+                return False
+            self._finish_window()
+        elif batch_idx % K != 0:
+            return False
+        with self.timer.span("push"):
+            self.push_gradients()
+        return True
+
     def _accumulate_grads(self, first: bool):
         """--accumulate: fp32 running sum of this window's batch gradients (stream-ordered)."""
         g = self.compute.grads
@@ -379,15 +394,7 @@ class Worker:
                             self.fetch_parameters()
                     with self.timer.span("compute_issue"):
                         self.train_local_batch(idx)
-                    if self.cfg.accumulate and K > 1:  # mean gradient of the window, pushed at its end
-                        self._accumulate_grads(batch_idx % K == 0)
-                        if batch_idx % K == K - 1 or batch_idx == len(batches) - 1:
-                            self._finish_window()
-                            with self.timer.span("push"):
-                                self.push_gradients()
-                    elif batch_idx % K == 0:
-                        with self.timer.span("push"):
-                            self.push_gradients()
+                    self.window_push(batch_idx, len(batches), K)
                     if self.cfg.verbose and batch_idx % 50 == 0:
                         loss = self.compute.last_loss()
                         self.losses.append(loss)

@@ -29,33 +29,38 @@ def tiny_cfg(**kw):
     return PSConfig(**base).validate()
 
 
-def test_accumulate_pushes_window_mean(monkeypatch):
+@pytest.mark.parametrize("workers", [1, 2])
+def test_accumulate_pushes_window_mean(monkeypatch, workers):
     """--sync-steps 2 --accumulate: one push per window of 2 batches, carrying the mean of the
-    window's batch gradients (the reference pushes the first batch's only)."""
+    window's batch gradients (the reference pushes the first batch's only); single-worker loop
+    and the interleaved multi-worker loopback."""
     from psx.parallel import compute as CM
     from psx.parallel import worker as WM
 
-    batch_g, pushed = [], []
+    batch_g, pushed = {}, {}
     orig_step, orig_push = CM.TorchCompute.train_step, WM.InProcessChannel.push
 
     def step(self, *a, **k):
         r = orig_step(self, *a, **k)
-        batch_g.append(self.grads.float().clone())
+        batch_g.setdefault(id(self.grads.untyped_storage()), []).append(self.grads.float().clone())
         return r
 
     def push(self, worker_id, grads, local_step, buffers=None):
-        pushed.append(grads.float().clone())
+        pushed.setdefault(id(grads.untyped_storage()), []).append(grads.float().clone())
         return orig_push(self, worker_id, grads, local_step, buffers)
 
     monkeypatch.setattr(CM.TorchCompute, "train_step", step)
     monkeypatch.setattr(WM.InProcessChannel, "push", push)
-    res = run_local(tiny_cfg(mode="sync", workers=1, sync_steps=2, accumulate=True, eval_every=0),
+    res = run_local(tiny_cfg(mode="sync", workers=workers, sync_steps=2, accumulate=True, eval_every=0),
                     log=lambda *a, **k: None)
-    nb = len(batch_g)
-    assert nb == 12 and len(pushed) == 6 and res["server"]["global_steps_completed"] == 6
-    for i, p in enumerate(pushed):
-        ref = (batch_g[2 * i] + batch_g[2 * i + 1]) / 2
-        assert torch.allclose(p, ref.half().float(), atol=1e-3, rtol=1e-2), i
+    nb = 12 // workers
+    assert res["server"]["global_steps_completed"] == nb // 2
+    assert sorted(batch_g) == sorted(pushed) and len(batch_g) == workers
+    for key, bg in batch_g.items():
+        assert len(bg) == nb and len(pushed[key]) == nb // 2
+        for i, p in enumerate(pushed[key]):
+            ref = (bg[2 * i] + bg[2 * i + 1]) / 2
+            assert torch.allclose(p, ref.half().float(), atol=1e-3, rtol=1e-2), (key, i)
 
 
 def test_inprocess_sync_matches_manual_average():

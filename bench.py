@@ -237,8 +237,11 @@ def main():
             "baseline_img_s": BASELINE_SYNC_IMG_S if r18 else None,
         }
     if a.host_timing:
+        wait = getattr(wk.compute, "host_wait_s", 0.0) if wk is not None else 0.0
         print(json.dumps({"rank": rank, "host_issue_ms_per_step": round(1e3 * sum(host) / len(host), 4),
-                          "host_issue_ms_max": round(1e3 * max(host), 4)}), file=sys.stderr, flush=True)
+                          "host_issue_ms_max": round(1e3 * max(host), 4),
+                          # time the host spent blocked because it ran len(ring) steps ahead (whole run)
+                          "host_wait_ms_total": round(1e3 * wait, 3)}), file=sys.stderr, flush=True)
     if sess is not None:
         sess.finish()
         sess.close()

@@ -12,6 +12,8 @@ setup_model/train_local_batch/evaluate_model (src/workers/worker.py:128-138,313-
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -140,12 +142,15 @@ class HipCompute:
         self._meta_ring = [torch.zeros(batch + 1, dtype=torch.int32).pin_memory() for _ in range(4)]
         self._meta_ev = [None] * len(self._meta_ring)
         self._meta_i = 0
+        self.host_wait_s = 0.0
 
     def _set_batch(self, idx):
         k = self._meta_i % len(self._meta_ring)
         self._meta_i += 1
         if self._meta_ev[k] is not None:
+            t0 = time.perf_counter()
             self._meta_ev[k].synchronize()
+            self.host_wait_s += time.perf_counter() - t0  # host ahead of the device by len(ring)
         buf = self._meta_ring[k]
         buf[: self.B].copy_(torch.as_tensor(idx, dtype=torch.int32))
         buf[self.B] = self._step

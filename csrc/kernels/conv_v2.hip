@@ -82,7 +82,10 @@ PSX_DEV const uint16_t* gather_src(const Conv2Args& a, int nbase, int hb, int wb
 // reads window slot j + d(s) (d = s - 1 forward, 1 - s dgrad: ih = oh + pad - r there) or a zero
 // row when its column leaves the image row. The im2col operand is staged once per kernel row
 // instead of once per tap (1/3 of the L2->LDS bytes of the gathered operand); 2 LDS stages.
-template <int BM, int BN, int MODE, bool HAS_RES, bool SPLIT, int WGM = 2, bool TAPR = false>
+// TAPR = 1: tiles of whole image rows (power-of-two widths); TAPR = 2 ("halo", any width, e.g.
+// ResNet-50's 56/28/14/7): the window also holds the pixel before and after the tile (slot k =
+// pixel pix0 - 1 + k), so a shift never leaves the staged rows; the zero row sits at slot BN + 2.
+template <int BM, int BN, int MODE, bool HAS_RES, bool SPLIT, int WGM = 2, int TAPR = 0>
 __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   constexpr int NSTAGE = 3;
   constexpr int WGN = 4 / WGM;
@@ -123,11 +126,13 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
 
   if constexpr (TAPR) {
     static_assert(MODE == 0 || MODE == 1, "tap reuse: forward or stride-1 dgrad");
-    constexpr int XOFF = 3 * BM * 128, TST = XOFF + (BN + 1) * 128;  // A0 A1 A2 | X | zero row
+    constexpr bool HALO = TAPR == 2;
+    constexpr int XROWS = HALO ? BN + 8 : BN + 1, ZS = HALO ? BN + 2 : BN;  // window rows, zero slot
+    constexpr int XOFF = 3 * BM * 128, TST = XOFF + XROWS * 128;            // A0 A1 A2 | X
     const int nch = a.IC >> 6, nmac = 3 * nch;
     const int W = a.OW, log2w = __builtin_ctz(W);
     const int lrow = lane >> 3, lpos = lane & 7;
-    if (tid < 16)
+    if (!HALO && tid < 16)  // (the halo DMA writes zeros into slots BN+2.. of every stage itself)
       *reinterpret_cast<uint4*>(smem + (tid >> 3) * TST + XOFF + BN * 128 + (tid & 7) * 16) = uint4{0u, 0u, 0u, 0u};
     const uint16_t* wsrc[LA];
 #pragma unroll
@@ -135,15 +140,19 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       const int row = (i * 4 + wid) * 8 + lrow;
       wsrc[i] = a.w + (size_t)(oc0 + row) * a.Kg + (lpos ^ ((row >> 1) & 7)) * 8;
     }
-    // window rows: the tile's own pixels (input pixel index == output pixel index at s1/p1)
-    const uint16_t* xsrc[LB];
-    int xoh[LB];
+    // window rows: the tile's own pixels (input pixel index == output pixel index at s1/p1);
+    // halo mode: slot k = pixel pix0 - 1 + k, and wave 0 also stages slots BN .. BN+7 (the two
+    // halo pixels, then zeros from the zero page)
+    constexpr int LX = LB + (HALO ? 1 : 0);
+    const uint16_t* xsrc[LX];
+    int xoh[LX];
 #pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      const int row = (i * 4 + wid) * 8 + lrow;
-      const int pix = pix0 + row;
-      xoh[i] = (pix >> log2w) & (a.OH - 1);
-      xsrc[i] = a.in + (size_t)pix * a.IC + (lpos ^ ((row >> 1) & 7)) * 8;
+    for (int i = 0; i < LX; ++i) {
+      const int row = i < LB ? (i * 4 + wid) * 8 + lrow : BN + lrow;
+      const int pix = pix0 + row - (HALO ? 1 : 0);
+      const bool ok = HALO ? (pix >= 0 && pix < a.npix && (i < LB || lrow < 2)) : true;
+      xoh[i] = !ok ? -(1 << 20) : HALO ? (pix / W) % a.OH : (pix >> log2w) & (a.OH - 1);
+      xsrc[i] = ok ? a.in + (size_t)pix * a.IC + (lpos ^ ((row >> 1) & 7)) * 8 : a.zero;
     }
     auto issue_t = [&](int t, int stage) {
       unsigned char* base = smem + stage * TST;
@@ -162,6 +171,10 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
         const uint16_t* src = (unsigned)(xoh[i] + dr) < (unsigned)a.OH ? xsrc[i] + uoff : a.zero;
         glds16(src, base + XOFF + (i * 4 + wid) * 1024);
       }
+      if (HALO && wid == 0) {
+        const uint16_t* src = (unsigned)(xoh[LX - 1] + dr) < (unsigned)a.OH ? xsrc[LX - 1] + uoff : a.zero;
+        glds16(src, base + XOFF + BN * 128);
+      }
     };
     // per-lane B-fragment byte offsets of the three taps (tile starts on an image row)
     const int frow = lane & 15, fch = lane >> 4;
@@ -169,11 +182,11 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
       const int prow = wn * (BN / WGN) + n * 16 + frow;
-      const int ow = prow & (W - 1);
+      const int ow = HALO ? (pix0 + prow) % W : prow & (W - 1);
 #pragma unroll
       for (int sx = 0; sx < 3; ++sx) {
         const int d = MODE == 0 ? sx - 1 : 1 - sx;
-        const int slot = (unsigned)(ow + d) < (unsigned)W ? prow + d : BN;
+        const int slot = (unsigned)(ow + d) < (unsigned)W ? prow + d + (HALO ? 1 : 0) : ZS;
         boff[n][sx] = slot * 128 + ((fch ^ ((slot >> 1) & 7)) << 4);
       }
     }
@@ -376,7 +389,8 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     constexpr int TS = BM + 4;      // fp32 row stride of the staged tile (spreads the banks)
     constexpr int CPR = BM / 8;     // 16-byte bf16 chunks per pixel row
     constexpr int RPP = 256 / CPR;  // pixel rows per pass
-    constexpr int LDSB = TAPR ? 2 * (3 * BM * 128 + (BN + 1) * 128) : 3 * (BM + BN) * 128;  // launched
+    constexpr int LDSB = TAPR ? 2 * (3 * BM * 128 + (TAPR == 2 ? BN + 8 : BN + 1) * 128)
+                              : 3 * (BM + BN) * 128;  // launched
     static_assert(256 % CPR == 0 && BN * TS * 4 <= LDSB, "staged tile fits the mainloop LDS");
     float* T = reinterpret_cast<float*>(smem);
     __syncthreads();  // every wave is done with the mainloop's LDS
@@ -796,21 +810,25 @@ int dispatch2(const Plan& p, const Conv2Args& a, hipStream_t st) {
   return -7;
 }
 
-template <int BM, int BN, int MODE, bool RES, int WGM>
+template <int BM, int BN, int MODE, bool RES, int WGM, int TP = 1>
 int launch_tapr(const Conv2Args& a, hipStream_t st) {
-  const size_t lds = (size_t)2 * (3 * BM * 128 + (BN + 1) * 128);
-  hipLaunchKernelGGL((conv2_kernel<BM, BN, MODE, RES, false, WGM, true>), dim3(a.n_oc_tiles * a.n_pix_tiles),
+  const size_t lds = (size_t)2 * (3 * BM * 128 + (TP == 2 ? BN + 8 : BN + 1) * 128);
+  hipLaunchKernelGGL((conv2_kernel<BM, BN, MODE, RES, false, WGM, TP>), dim3(a.n_oc_tiles * a.n_pix_tiles),
                      dim3(256), lds, st, a);
   return (int)hipGetLastError();
 }
 
 // Pixel-tile width of the tap-reuse path for this layer, 0 = not applicable: 3x3 / stride 1 /
 // pad 1, square power-of-two images whose rows tile BN exactly, 64-channel chunks; no split-K.
-// PSX_CV_TAPR=0 disables it, PSX_CV_TAPR_BN=64|128|256 forces the width (sweeps).
+// PSX_CV_TAPR=0 disables it, PSX_CV_TAPR_BN=64|128|256 forces the width (sweeps). Other widths
+// (and PSX_CV_TAPR_HALO=1, a test override) take the halo mode with 64-pixel tiles: returns -64.
 int tapr_bn(int R, int S, int stride, int pad, int H, int W, int IC, int OC, int npix) {
   if (const char* e = getenv("PSX_CV_TAPR"))
     if (e[0] == '0') return 0;
-  if (R != 3 || S != 3 || stride != 1 || pad != 1 || IC % 64 || OC % 64 || H != W || (W & (W - 1))) return 0;
+  if (R != 3 || S != 3 || stride != 1 || pad != 1 || IC % 64 || OC % 64) return 0;
+  const char* he = getenv("PSX_CV_TAPR_HALO");
+  const bool halo_off = he && he[0] == '0', halo_force = he && he[0] == '1';
+  if (halo_force || H != W || (W & (W - 1)) || 64 % W) return halo_off ? 0 : -64;
   int force = 0;
   if (const char* e = getenv("PSX_CV_TAPR_BN")) force = atoi(e);
   // measured (bench/tapr_probe.py, ResNet-18 B=128, us fwd/dgrad): 64-pixel tiles (2 workgroups
@@ -825,9 +843,13 @@ int tapr_bn(int R, int S, int stride, int pad, int H, int W, int IC, int OC, int
 template <int MODE, bool RES>
 int dispatch_tapr(int bn, Conv2Args& a, hipStream_t st) {
   a.n_oc_tiles = a.OC / 64;
-  a.n_pix_tiles = a.npix / bn;
   a.splits = 1;
   a.kps = a.Kg / 64;
+  if (bn < 0) {  // halo mode
+    a.n_pix_tiles = (a.npix + 63) / 64;
+    return launch_tapr<64, 64, MODE, RES, 2, 2>(a, st);
+  }
+  a.n_pix_tiles = a.npix / bn;
   if (bn == 256) return launch_tapr<64, 256, MODE, RES, 1>(a, st);
   if (bn == 128) return launch_tapr<64, 128, MODE, RES, 2>(a, st);
   return launch_tapr<64, 64, MODE, RES, 2>(a, st);

@@ -118,17 +118,22 @@ def test_conv2_every_tile_config(shape, tile, monkeypatch):
     assert _rel(dx[..., :cin], dref + res[..., :cin].float()) < 1e-2, (shape, tile)
 
 
-@pytest.mark.parametrize("bn", [64, 128, 256])
+@pytest.mark.parametrize("bn", [64, 128, 256, "halo"])
 @pytest.mark.parametrize("shape", [(32, 64, 64, 32, 3, 1, 1), (16, 128, 128, 16, 3, 1, 1), (16, 256, 256, 8, 3, 1, 1),
-                                   (16, 512, 512, 4, 3, 1, 1), (4, 64, 128, 64, 3, 1, 1)])
+                                   (16, 512, 512, 4, 3, 1, 1), (4, 64, 128, 64, 3, 1, 1), (3, 64, 64, 56, 3, 1, 1),
+                                   (5, 128, 128, 28, 3, 1, 1), (3, 512, 512, 7, 3, 1, 1)])
 def test_conv2_tap_reuse(shape, bn, monkeypatch):
     """The tap-reuse mainloop (conv2_kernel TAPR: one staged window per kernel row feeds its three
-    taps, zero row at the image-row edges) at every tile width: fwd (+ BN statistics) and dgrad
-    (+ residual, + fused BN-backward sums) against torch fp32."""
+    taps, zero row at the image-row edges) at every tile width, and its halo mode (tiles that
+    start mid-row, any width: the ResNet-50 56/28/14/7 layers; forced on the power-of-two shapes
+    too): fwd (+ BN statistics) and dgrad (+ residual, + fused BN-backward sums) against torch fp32."""
     n, cin, cout, hw, k, s, p = shape
-    if (n * hw * hw) % bn or bn % hw:
+    if bn == "halo":
+        monkeypatch.setenv("PSX_CV_TAPR_HALO", "1")
+    elif (n * hw * hw) % bn or bn % hw:
         pytest.skip("tile does not hold whole image rows")
-    monkeypatch.setenv("PSX_CV_TAPR_BN", str(bn))
+    else:
+        monkeypatch.setenv("PSX_CV_TAPR_BN", str(bn))
     torch.manual_seed(4)
     x = torch.randn(n, cin, hw, hw, device=DEV).to(torch.bfloat16).float()
     w = (torch.randn(cout, cin, k, k, device=DEV) / (cin * k * k) ** 0.5).to(torch.bfloat16).float()

@@ -157,8 +157,12 @@ __global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict
 // softmax/xent -> dpooled GEMM (+ broadcast to dact), each matrix read once per 32-sample tile.
 
 // pooled[b][c] = mean over the HW pixels; grid (B, ceil(C / 512)), 2 channels per thread
+// also zeroes zbuf[0, nz) (the split-K logits accumulator)
 __global__ __launch_bounds__(256) void head_pool_kernel(const uint16_t* __restrict__ act, int HW, int C,
-                                                        float* __restrict__ pooled) {
+                                                        float* __restrict__ pooled, float* __restrict__ zbuf,
+                                                        long nz) {
+  const long gt = ((long)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x;
+  for (long i = gt; i < nz; i += (long)gridDim.x * gridDim.y * 256) zbuf[i] = 0.f;
   const int b = blockIdx.x, c = blockIdx.y * 512 + 2 * threadIdx.x;
   if (c >= C) return;
   const uint16_t* a = act + (size_t)b * HW * C + c;
@@ -174,7 +178,8 @@ __global__ __launch_bounds__(256) void head_pool_kernel(const uint16_t* __restri
 
 // out[m][n] = sum_k A[m][k] * B(k, n), fp32, 32 x 64 tile per workgroup (2 x 4 per thread), k in
 // chunks of 32 through LDS. BT: B(k, n) = Bm[n][k] (FC rows: logits); else Bm[k][n] (dpooled).
-// EPI 0: out fp32 + bias[n]; EPI 1: dact bf16 = out / HW written to all HW pixels of sample m.
+// EPI 0: out += partial (+ bias[n] from split 0), fp32 atomics, split-K over blockIdx.z (out
+// zeroed beforehand); EPI 1: dact bf16 = out / HW written to all HW pixels of sample m (no split).
 template <bool BT, int EPI>
 __global__ __launch_bounds__(256) void head_gemm_kernel(const float* __restrict__ A, const float* __restrict__ Bm,
                                                         int M, int N, int Kd, const float* __restrict__ bias,
@@ -184,22 +189,24 @@ __global__ __launch_bounds__(256) void head_gemm_kernel(const float* __restrict_
   __shared__ float Bs[32][68];
   const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
   const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 64;
+  const int kper = ((Kd + gridDim.z * 32 - 1) / (gridDim.z * 32)) * 32;  // 32-aligned split ranges
+  const int kbeg = blockIdx.z * kper, kend = min(Kd, kbeg + kper);
   float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  for (int k0 = 0; k0 < Kd; k0 += 32) {
+  for (int k0 = kbeg; k0 < kend; k0 += 32) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // A tile 32 x 32, coalesced along k
       const int idx = i * 256 + tid, mm = idx >> 5, kk = idx & 31;
-      As[mm][kk] = (m0 + mm < M && k0 + kk < Kd) ? A[(size_t)(m0 + mm) * Kd + k0 + kk] : 0.f;
+      As[mm][kk] = (m0 + mm < M && k0 + kk < kend) ? A[(size_t)(m0 + mm) * Kd + k0 + kk] : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {  // B tile 32 (k) x 64 (n)
       const int idx = i * 256 + tid;
       if (BT) {  // coalesced along k of row n
         const int nn = idx >> 5, kk = idx & 31;
-        Bs[kk][nn] = (n0 + nn < N && k0 + kk < Kd) ? Bm[(size_t)(n0 + nn) * Kd + k0 + kk] : 0.f;
+        Bs[kk][nn] = (n0 + nn < N && k0 + kk < kend) ? Bm[(size_t)(n0 + nn) * Kd + k0 + kk] : 0.f;
       } else {   // coalesced along n of row k
         const int kk = idx >> 6, nn = idx & 63;
-        Bs[kk][nn] = (n0 + nn < N && k0 + kk < Kd) ? Bm[(size_t)(k0 + kk) * N + n0 + nn] : 0.f;
+        Bs[kk][nn] = (n0 + nn < N && k0 + kk < kend) ? Bm[(size_t)(k0 + kk) * N + n0 + nn] : 0.f;
       }
     }
     __syncthreads();
@@ -220,7 +227,7 @@ __global__ __launch_bounds__(256) void head_gemm_kernel(const float* __restrict_
     if (EPI == 0) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (n + j < N) out[(size_t)m * N + n + j] = acc[i][j] + bias[n + j];
+        if (n + j < N) atomicAdd(out + (size_t)m * N + n + j, acc[i][j] + (blockIdx.z == 0 ? bias[n + j] : 0.f));
     } else if (n + 3 < N) {  // N (channels) is a multiple of 64 on this path
       const float inv = 1.f / (float)HW;
       u32x2 v;
@@ -280,9 +287,12 @@ int psx_head_fwd_bwd(const void* act, int B, int HW, int C, const float* fcw, co
                      hipStream_t st) {
   if ((long)K * C > (1L << 18) && C % 64 == 0 && pooled && dlogits) {  // large head: split path
     hipLaunchKernelGGL(head_pool_kernel, dim3(B, (C + 511) / 512), dim3(256), 0, st, (const uint16_t*)act, HW, C,
-                       pooled);
-    hipLaunchKernelGGL((head_gemm_kernel<true, 0>), dim3((K + 63) / 64, (B + 31) / 32), dim3(256), 0, st, pooled,
-                       fcw, B, K, C, fcb, dlogits, (uint16_t*)nullptr, HW);
+                       pooled, dlogits, (long)B * K);
+    // logits: split-K over the C-long dot products (a 2048 x 1000 head at B = 128 is only 64
+    // output tiles; 16 splits of 128 channels fill the chip)
+    const int ks = C >= 1024 ? 16 : 4;
+    hipLaunchKernelGGL((head_gemm_kernel<true, 0>), dim3((K + 63) / 64, (B + 31) / 32, ks), dim3(256), 0, st,
+                       pooled, fcw, B, K, C, fcb, dlogits, (uint16_t*)nullptr, HW);
     hipLaunchKernelGGL(head_softmax_kernel, dim3(B), dim3(64), 0, st, dlogits, K, labels, loss, correct,
                        1.f / (float)B, dact ? 1 : 0);
     if (dact)

@@ -110,7 +110,8 @@ __global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ 
 }
 
 // dW[k][c] = sum_b dlogits[b][k] * pooled[b][c]; db[k] = sum_b dlogits[b][k].
-// Block: 8 classes x 256 channels; dlogits for those classes staged in LDS.
+// Block: 8 classes x 256 channels; dlogits for those classes staged in LDS. (The small-head
+// variant below trades the 8-class register block for 4x more workgroups.)
 template <typename GT>
 __global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict__ dlogits,
                                                          const float* __restrict__ pooled, int B, int K, int C,
@@ -276,6 +277,42 @@ __global__ __launch_bounds__(64) void head_softmax_kernel(float* __restrict__ dl
     for (int k = lane; k < K; k += 64) row[k] = (__expf(row[k] - lse) - (k == y ? 1.f : 0.f)) * invB;
 }
 
+// Small heads (ResNet-18: 100 x 512, B = 128): one output per thread, workgroup = 4 classes x 64
+// channels (200 workgroups instead of 26); dlogits of the 4 classes staged in LDS, pooled read
+// coalesced along the channels; db by the first channel block.
+template <typename GT>
+__global__ __launch_bounds__(256) void head_wgrad_small_kernel(const float* __restrict__ dlogits,
+                                                               const float* __restrict__ pooled, int B, int K,
+                                                               int C, GT* __restrict__ dw, GT* __restrict__ db,
+                                                               float gscale) {
+  extern __shared__ __attribute__((aligned(16))) float sdl4[];  // [B][4]
+  const int k0 = blockIdx.y * 4, kk = threadIdx.x >> 6, c = blockIdx.x * 64 + (threadIdx.x & 63);
+  for (int i = threadIdx.x; i < B * 4; i += 256) {
+    const int bb = i >> 2, j = i & 3;
+    sdl4[i] = (k0 + j < K) ? dlogits[(size_t)bb * K + k0 + j] : 0.f;
+  }
+  __syncthreads();
+  const int k = k0 + kk;
+  if (k >= K) return;
+  float acc = 0.f, accb = 0.f;
+  if (c < C) {
+    for (int bb = 0; bb < B; ++bb) acc += sdl4[bb * 4 + kk] * pooled[(size_t)bb * C + c];
+    const float v = acc * gscale;
+    if constexpr (sizeof(GT) == 2)
+      dw[(size_t)k * C + c] = __builtin_bit_cast(uint16_t, (_Float16)v);
+    else
+      dw[(size_t)k * C + c] = v;
+  }
+  if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) {
+    for (int bb = 0; bb < B; ++bb) accb += sdl4[bb * 4 + kk];
+    accb *= gscale;
+    if constexpr (sizeof(GT) == 2)
+      db[k] = __builtin_bit_cast(uint16_t, (_Float16)accb);
+    else
+      db[k] = accb;
+  }
+}
+
 }  // namespace psx
 
 using namespace psx;
@@ -313,6 +350,17 @@ int psx_head_fwd_bwd(const void* act, int B, int HW, int C, const float* fcw, co
 
 int psx_head_wgrad(const float* dlogits, const float* pooled, int B, int K, int C, void* dw, void* db, float gscale,
                    int grad_fp16, hipStream_t st) {
+  if ((long)K * C <= (1L << 18)) {  // small head: more, smaller workgroups
+    const dim3 grid((C + 63) / 64, (K + 3) / 4);
+    const size_t lds = (size_t)B * 4 * sizeof(float);
+    if (grad_fp16)
+      hipLaunchKernelGGL(head_wgrad_small_kernel<uint16_t>, grid, dim3(256), lds, st, dlogits, pooled, B, K, C,
+                         (uint16_t*)dw, (uint16_t*)db, gscale);
+    else
+      hipLaunchKernelGGL(head_wgrad_small_kernel<float>, grid, dim3(256), lds, st, dlogits, pooled, B, K, C,
+                         (float*)dw, (float*)db, gscale);
+    return (int)hipGetLastError();
+  }
   const dim3 grid((C + 255) / 256, (K + 7) / 8);
   const size_t lds = (size_t)B * 8 * sizeof(float);
   if (grad_fp16)

@@ -8,6 +8,19 @@
 
 namespace psx {
 
+// Optional BN-backward reduction of the layer whose output the head consumes (same layout as
+// conv_v2.hip BwdStatsDesc): slot rows part[T][2][C] += (sum dz, sum dz * xhat) over this
+// sample's pixels, dz = dact * [o > 0] with o = act, xhat = (y1 - mean) * invstd, saved1 =
+// [2][C] (mean, invstd) — what bn_bwd_reduce would compute in its own pass over dact, act, y1.
+struct HeadBnStats {
+  float* part;
+  const void* o;
+  const void* y1;
+  const void* y2;
+  const float* saved1;
+  const float* saved2;
+};
+
 // act: NHWC [B][HW][C] bf16; fcw: [K][C] fp32; fcb: [K] fp32; labels int32 [B]
 // outputs: pooled [B][C] fp32, dlogits [B][K] fp32 (already divided by B), dact (bf16, same
 // shape as act; nullable for eval), loss [B] fp32, correct (atomic int counter, nullable).
@@ -17,7 +30,8 @@ __global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ 
                                                    const float* __restrict__ fcw, const float* __restrict__ fcb, int K,
                                                    const int* __restrict__ labels, float* __restrict__ pooled,
                                                    float* __restrict__ dlogits, uint16_t* __restrict__ dact,
-                                                   float* __restrict__ loss, int* __restrict__ correct, float invB) {
+                                                   float* __restrict__ loss, int* __restrict__ correct, float invB,
+                                                   HeadBnStats bs) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
   float* sp = sh;      // [C]  pooled
   float* sl = sh + C;  // [K]  logits -> dlogits
@@ -106,6 +120,26 @@ __global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ 
     }
     const uint32_t v = pack_bf2(s0 * inv_hw, s1 * inv_hw);
     for (int p = 0; p < HW; ++p) *reinterpret_cast<uint32_t*>(dact + ((size_t)b * HW + p) * C + c) = v;
+    if (bs.part) {  // BN-backward sums of the consumed layer (see HeadBnStats)
+      const float g0 = lo_bf(v), g1 = hi_bf(v);
+      const float m0 = bs.saved1[c], i0 = bs.saved1[C + c], m1 = bs.saved1[c + 1], i1 = bs.saved1[C + c + 1];
+      const uint16_t* y = reinterpret_cast<const uint16_t*>(bs.y1) + (size_t)b * HW * C + c;
+      float z0 = 0.f, z1 = 0.f, x0 = 0.f, x1 = 0.f;
+      for (int p = 0; p < HW; ++p) {
+        const uint32_t o = *reinterpret_cast<const uint32_t*>(a + (size_t)p * C + c);
+        const uint32_t yv = *reinterpret_cast<const uint32_t*>(y + (size_t)p * C);
+        const float d0 = lo_bf(o) > 0.f ? g0 : 0.f, d1 = hi_bf(o) > 0.f ? g1 : 0.f;
+        z0 += d0;
+        z1 += d1;
+        x0 += d0 * (lo_bf(yv) - m0) * i0;
+        x1 += d1 * (hi_bf(yv) - m1) * i1;
+      }
+      float* dst = bs.part + (size_t)(b & (PSX_STAT_SLOTS - 1)) * 2 * C;
+      atomicAdd(dst + c, z0);
+      atomicAdd(dst + c + 1, z1);
+      atomicAdd(dst + C + c, x0);
+      atomicAdd(dst + C + c + 1, x1);
+    }
   }
 }
 
@@ -319,9 +353,11 @@ using namespace psx;
 
 extern "C" {
 
+// bst (nullable, fused path only, needs dact): the BN-backward sums of the consumed layer.
+// Returns 1 when they were produced (the caller then skips its bn_bwd_reduce), 0 otherwise.
 int psx_head_fwd_bwd(const void* act, int B, int HW, int C, const float* fcw, const float* fcb, int K,
                      const int* labels, float* pooled, float* dlogits, void* dact, float* loss, int* correct,
-                     hipStream_t st) {
+                     const HeadBnStats* bst, hipStream_t st) {
   if ((long)K * C > (1L << 18) && C % 64 == 0 && pooled && dlogits) {  // large head: split path
     hipLaunchKernelGGL(head_pool_kernel, dim3(B, (C + 511) / 512), dim3(256), 0, st, (const uint16_t*)act, HW, C,
                        pooled, dlogits, (long)B * K);
@@ -335,17 +371,20 @@ int psx_head_fwd_bwd(const void* act, int B, int HW, int C, const float* fcw, co
     if (dact)
       hipLaunchKernelGGL((head_gemm_kernel<false, 1>), dim3(C / 64, (B + 31) / 32), dim3(256), 0, st, dlogits, fcw,
                          B, C, K, (const float*)nullptr, (float*)nullptr, (uint16_t*)dact, HW);
-    return (int)hipGetLastError();
+    const int e = (int)hipGetLastError();
+    return e ? -e : 0;
   }
   if (K > 1024 || C % 16 || (C > 512 && C % 512)) return -2;
   const size_t lds = (size_t)(C + K + 64) * sizeof(float);
+  const HeadBnStats bs = (bst && dact) ? *bst : HeadBnStats{};
   if (dact)
     hipLaunchKernelGGL(head_kernel<true>, dim3(B), dim3(256), lds, st, (const uint16_t*)act, HW, C, fcw, fcb, K,
-                       labels, pooled, dlogits, (uint16_t*)dact, loss, correct, 1.f / (float)B);
+                       labels, pooled, dlogits, (uint16_t*)dact, loss, correct, 1.f / (float)B, bs);
   else
     hipLaunchKernelGGL(head_kernel<false>, dim3(B), dim3(256), lds, st, (const uint16_t*)act, HW, C, fcw, fcb, K,
-                       labels, pooled, dlogits, (uint16_t*)nullptr, loss, correct, 1.f / (float)B);
-  return (int)hipGetLastError();
+                       labels, pooled, dlogits, (uint16_t*)nullptr, loss, correct, 1.f / (float)B, bs);
+  const int e = (int)hipGetLastError();
+  return e ? -e : (bs.part ? 1 : 0);
 }
 
 int psx_head_wgrad(const float* dlogits, const float* pooled, int B, int K, int C, void* dw, void* db, float gscale,

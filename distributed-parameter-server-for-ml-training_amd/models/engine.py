@@ -633,9 +633,19 @@ class HipResNetEngine:
         zeroed, self._zeroed_head = self._zeroed_head, False
         if not zeroed:
             self.correct.zero_()
-        K.head_fwd_bwd(self.final, self.B, self.head_hw, sp.fc_in, self._aview(arena, f"{sp.fc}.weight"),
-                       self._aview(arena, f"{sp.fc}.bias"), sp.classes, self.labels, self.pooled, self.dlogits,
-                       self.dfinal if backward else None, self.loss, self.correct)
+        # the last block's output BN: its backward sums come out of the head launch (one
+        # bn_bwd_reduce pass fewer) when the fused per-sample head runs and that BN has no
+        # shortcut BN sharing its gradient
+        bst, last = None, None
+        if backward and self.fuse_bnbwd and sp.blocks and not sp.blocks[-1].down:
+            last = sp.blocks[-1].bns[-1]
+            bst = K.bwd_stats_desc(self._red(last, "bwd"), self.final, self.blk[-1]["y"][-1],
+                                   self.bn[last.name]["saved"])
+        fused = K.head_fwd_bwd(self.final, self.B, self.head_hw, sp.fc_in, self._aview(arena, f"{sp.fc}.weight"),
+                               self._aview(arena, f"{sp.fc}.bias"), sp.classes, self.labels, self.pooled,
+                               self.dlogits, self.dfinal if backward else None, self.loss, self.correct, bst=bst)
+        if fused and last is not None:
+            self._prereduced.add(last.name)
 
     def _bwd_fc(self, arena):
         sp = self.spec

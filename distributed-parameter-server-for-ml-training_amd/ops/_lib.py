@@ -58,7 +58,7 @@ _KERNEL_SIGS = {
     "psx_bn_bwd_apply": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
     "psx_bn_apply_fin": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp]),
     "psx_bn_bwd_apply_fin": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
-    "psx_head_fwd_bwd": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp, vp, vp, vp, vp, vp]),
+    "psx_head_fwd_bwd": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
     "psx_head_wgrad": (i32, [vp, vp, i32, i32, i32, vp, vp, f32, i32, vp]),
     "psx_sgd_apply": (i32, [vp, vp, vp, i64, f32, f32, f32, f32, i32, i32, vp, vp]),
     "psx_grad_aggregate": (i32, [vp, i32, i32, vp, i32, i64, f32, i32, vp]),

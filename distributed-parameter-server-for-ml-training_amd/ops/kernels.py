@@ -260,9 +260,15 @@ def bn_bwd_apply_fin(g, o, y1, part, fin1: BnBwdFin, dx1, c, y2=None, fin2: BnBw
                                          g.numel(), c, stream_ptr()), "bn_bwd_apply_fin")
 
 
-def head_fwd_bwd(act, b, hw, c, fcw, fcb, k, labels, pooled, dlogits, dact, loss, correct):
-    check(kernels().psx_head_fwd_bwd(ptr(act), b, hw, c, ptr(fcw), ptr(fcb), k, ptr(labels), ptr(pooled),
-                                     ptr(dlogits), ptr(dact), ptr(loss), ptr(correct), stream_ptr()), "head_fwd_bwd")
+def head_fwd_bwd(act, b, hw, c, fcw, fcb, k, labels, pooled, dlogits, dact, loss, correct,
+                 bst: BwdStatsDesc | None = None) -> bool:
+    """``bst``: also produce the BN-backward sums of the layer whose output ``act`` is (fused
+    per-sample head only). Returns whether they were produced."""
+    r = kernels().psx_head_fwd_bwd(ptr(act), b, hw, c, ptr(fcw), ptr(fcb), k, ptr(labels), ptr(pooled),
+                                   ptr(dlogits), ptr(dact), ptr(loss), ptr(correct),
+                                   C.byref(bst) if bst is not None else None, stream_ptr())
+    check(min(r, 0), "head_fwd_bwd")
+    return r == 1
 
 
 def head_wgrad(dlogits, pooled, b, k, c, dw_ptr, db_ptr, gscale, grad_fp16):

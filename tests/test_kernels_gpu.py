@@ -236,7 +236,19 @@ def test_head_fwd_bwd(b, hw, c, k):
     dact = torch.empty_like(act)
     lossv = torch.zeros(b, device=DEV)
     correct = torch.zeros(1, dtype=torch.int32, device=DEV)
-    K.head_fwd_bwd(act, b, hw, c, w.detach(), bias.detach(), k, lab, pooled, dlog, dact, lossv, correct)
+    y1 = torch.randn(b, side, side, c, device=DEV).to(torch.bfloat16)
+    saved = torch.stack([0.1 * torch.randn(c, device=DEV), 1.0 + torch.rand(c, device=DEV)])
+    part = torch.zeros(K.STAT_SLOTS, 2, c, device=DEV)
+    fused = K.head_fwd_bwd(act, b, hw, c, w.detach(), bias.detach(), k, lab, pooled, dlog, dact, lossv, correct,
+                           bst=K.bwd_stats_desc(part, act, y1, saved))
+    assert fused == (k * c <= (1 << 18))  # the per-sample head also produces the BN-backward sums
+    if fused:
+        dz = (dact.float() * (act.float() > 0)).reshape(-1, c)
+        xhat = (y1.float().reshape(-1, c) - saved[0]) * saved[1]
+        assert torch.allclose(part[:, 0].sum(0), dz.sum(0), rtol=1e-3, atol=1e-5)
+        assert torch.allclose(part[:, 1].sum(0), (dz * xhat).sum(0), rtol=1e-3, atol=1e-5)
+    else:
+        assert not part.any()
     assert _rel(pooled, pooled_ref) < 1e-5
     assert abs(lossv.mean().item() - loss.item()) < 1e-3
     assert correct.item() == int((logits.argmax(1) == lab.long()).sum())

@@ -198,6 +198,16 @@ def test_dgrad_fused_bn_backward_sums_match_reduce_kernel(setup):
             want = ref[:m].view(K.STAT_SLOTS, 2, bs.c).sum(0)
             assert torch.allclose(got, want, rtol=1e-3, atol=1e-3 * want.abs().max().item()), bs.name
             checked += 1
+    # the last block's output BN: its sums come out of the head launch (engine.head)
+    bs = eng.spec.blocks[-1].bns[-1]
+    npix = eng.dfinal.numel() // bs.c
+    ref = torch.zeros_like(eng._red(bs, "bwd"))
+    K.bn_bwd_reduce(eng.dfinal, eng.final, eng.blk[-1]["y"][-1], eng.bn[bs.name]["saved"], ref, npix, bs.c)
+    torch.cuda.synchronize()
+    m = K.STAT_SLOTS * 2 * bs.c
+    got = eng._red(bs, "bwd")[:m].view(K.STAT_SLOTS, 2, bs.c).sum(0)
+    want = ref[:m].view(K.STAT_SLOTS, 2, bs.c).sum(0)
+    assert torch.allclose(got, want, rtol=1e-3, atol=1e-3 * want.abs().max().item()), bs.name
     eng.fuse_bnbwd = before
     assert checked == 8
 

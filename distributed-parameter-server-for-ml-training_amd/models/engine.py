@@ -188,8 +188,11 @@ class HipResNetEngine:
         self.fin_apply = not self.fuse_fin and os.environ.get("PSX_BNFIN_APPLY", "1") == "1"
         self.fuse_bnbwd = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNBWD", "1") == "1"
         self._prereduced = set()
+        # weight gradients (+ their batched reductions) on a side stream, a parallel branch of the
+        # captured step graph next to the dgrad -> BN-backward chain: 1.837/1.841 vs 1.853/1.858
+        # ms/step on the main stream (two A/B pairs, session 3); PSX_WGRAD_STREAM=0: main stream
         self.wg_stream = (torch.cuda.Stream(device=self.dev)
-                          if os.environ.get("PSX_WGRAD_STREAM", "0") == "1" else None)
+                          if os.environ.get("PSX_WGRAD_STREAM", "1") == "1" else None)
         self._wg_batch = None
         self._fins = {}
         # conv-operand unpack: "tiles" (flat grid, fp32 arena or bf16 image source) or "tap"

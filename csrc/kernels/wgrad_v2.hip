@@ -352,6 +352,18 @@ struct WPlan {
   int BR, BC, NS, splits, sps;
 };
 
+// Share of the chip the weight gradient plans for (PSX_WG_SHARE, default 1): below 1 when it runs
+// on a side stream next to the dgrad -> BN-backward chain (models/engine.py wg_stream).
+int wg_slots(int occ) {
+  static const double share = [] {
+    const char* e = getenv("PSX_WG_SHARE");
+    const double v = e ? atof(e) : 1.0;
+    return v > 0.05 && v <= 1.0 ? v : 1.0;
+  }();
+  const int s = (int)(256 * occ * share);
+  return s > 0 ? s : 1;
+}
+
 // LDS bytes per workgroup of an NS-stage BR x BC tile (64 pixels per stage).
 constexpr int wlds(int BR, int BC, int NS) { return NS * 64 * (BR + BC) * 2; }
 
@@ -373,7 +385,7 @@ WPlan wplan(int OC, int Kg, int npix) {
       int occ = 163840 / wlds(BR, BC, NS);
       if (occ > 3) occ = 3;
       if (occ < 1) continue;
-      const int slots = 256 * occ;
+      const int slots = wg_slots(occ);
       const long tiles = (long)(Kg / BR) * (OC / BC);
       const double step_us = 0.55 + 0.15 * (double)(BR * BC) / 4096.0;
       int smax = steps / 8 > 0 ? steps / 8 : 1;
@@ -413,7 +425,7 @@ WPlan wplan3(int OC, int IC, int Kg, int npix) {
     int occ = 163840 / wlds3(BC, NS);
     if (occ > 3) occ = 3;
     if (occ < 1) continue;
-    const int slots = 256 * occ;
+    const int slots = wg_slots(occ);
     const long tiles = 3L * (IC / 64) * (OC / BC);
     const double step_us = (BC == 64 ? 0.9 : 1.3) * (NS == 6 ? 0.8 : 1.0);
     const int smax = steps / 4 > 0 ? steps / 4 : 1;

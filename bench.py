@@ -85,8 +85,9 @@ def main():
 
     t = None
     # sync at N = 1 runs the distributed path too (one rank: psx communicator, rank 0 = server +
-    # worker 0), the same code as N > 1 — and measured faster than the in-process loopback
-    # (1.777/1.778 vs 1.842/1.829 ms/step, same box). PSX_FORCE_DIST=0: in-process loopback.
+    # worker 0), the same code as N > 1; measured equal to or faster than the in-process loopback
+    # (one box 1.777/1.778 vs 1.842/1.829 ms/step, another 1.843 vs 1.853 mean of 3 interleaved).
+    # PSX_FORCE_DIST=0: in-process loopback.
     force_dist = os.environ.get("PSX_FORCE_DIST", "1" if a.mode == "sync" else "0") == "1"
     sharded = a.topology == "sharded"
     if world > 1 or force_dist or sharded:

@@ -351,7 +351,7 @@ class Worker:
         self.images += len(idx)
 
     def evaluate_model(self):
-        if self.test_set is None:
+        if self.test_set is None or (self.cfg.eval_workers == "first" and self.worker_id != 0):
             return None
         acc = self.compute.evaluate(self.test_set)
         self.log(f"  > Worker {self.worker_id} test accuracy: {acc:.2f}%")

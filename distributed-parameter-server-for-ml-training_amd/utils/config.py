@@ -74,6 +74,7 @@ class PSConfig:
     train_samples: int = 50000
     test_samples: int = 10000
     eval_every: int = 1            # epochs between evaluations (0 = never)
+    eval_workers: str = "all"      # all: every worker evaluates (reference worker.py:393-394); first: worker 0 only
     max_steps: int = 0             # stop after this many local steps (0 = full epochs)
     ckpt_every: int = 0
     ckpt_dir: str = "checkpoints"
@@ -91,6 +92,8 @@ class PSConfig:
             raise ValueError(f"--mode must be sync or async, got {self.mode!r}")
         if not (1 <= self.workers <= 32):  # reference server.py:424-426
             raise ValueError("Number of workers must be between 1 and 32")
+        if self.eval_workers not in ("all", "first"):
+            raise ValueError("--eval-workers must be all or first")
         if self.codec not in ("none", "fp16", "topk"):
             raise ValueError(f"--codec must be none, fp16 or topk, got {self.codec!r}")
         if self.topology not in ("colocated", "dedicated", "sharded"):
@@ -153,6 +156,8 @@ def add_arguments(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     A("--train-samples", type=int, default=None)
     A("--test-samples", type=int, default=None)
     A("--eval-every", type=int, default=None)
+    A("--eval-workers", choices=["all", "first"], default=None,
+      help="all: every worker evaluates the test set each epoch (reference); first: worker 0 only")
     A("--max-steps", type=int, default=None)
     A("--ckpt-every", type=int, default=None)
     A("--ckpt-dir", default=None)

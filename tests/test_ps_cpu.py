@@ -409,3 +409,12 @@ def test_scaling_harness_commands_and_efficiency():
     eff = S.efficiency({1: {"value": 100.0}, 2: {"value": 190.0}, 8: {"value": 640.0}})
     assert eff == {1: 1.0, 2: 0.95, 8: 0.8}
     assert S.efficiency({2: {"value": 1.0}}) == {2: None}
+
+
+def test_eval_workers_first_only_worker0_evaluates():
+    """--eval-workers first (SURVEY.md §7.4 option): only worker 0 evaluates; default all."""
+    res = run_local(tiny_cfg(mode="sync", workers=2, eval_workers="first"), log=lambda *a, **k: None)
+    accs = [w["all_accuracies_percent"] for w in sorted(res["workers"], key=lambda w: w["worker_id"])]
+    assert len(accs[0]) == 1 and accs[1] == []
+    res = run_local(tiny_cfg(mode="sync", workers=2), log=lambda *a, **k: None)
+    assert all(len(w["all_accuracies_percent"]) == 1 for w in res["workers"])

@@ -59,9 +59,14 @@ def main():
     ap.add_argument("--codec", choices=["fp16", "none", "topk"], default="fp16")
     ap.add_argument("--topk-ratio", type=float, default=0.01)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--fetch-codec", choices=["bf16conv", "fp32"], default="bf16conv",
-                    help="bf16conv: conv weights travel as the bf16 bits the workers compute with (bit-exact "
-                         "worker compute), everything else fp32; fp32: the reference's full fp32 state")
+    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="worker compute precision. fp32 (default, the headline): the reference's training "
+                         "precision (worker.py:333-348), every conv product on the exact-f32 MFMA; bf16: bf16 "
+                         "operands with fp32 accumulation and fp32 master weights (secondary number)")
+    ap.add_argument("--fetch-codec", choices=["auto", "bf16conv", "fp32"], default="auto",
+                    help="auto: fp32 for --dtype fp32, bf16conv for bf16. bf16conv: conv weights travel as the "
+                         "bf16 bits the workers compute with, everything else fp32; fp32: the reference's full "
+                         "fp32 state")
     ap.add_argument("--overlap", action="store_true",
                     help="stream gradient buckets (reduce/apply/broadcast) during the backward pass")
     ap.add_argument("--bucket-mb", type=float, default=4.0)
@@ -79,7 +84,7 @@ def main():
     n_train = a.train_samples or (50000 if a.model == "resnet18" else 4096)
     cfg = PSConfig(mode=a.mode, staleness_bound=a.staleness_bound, model=a.model, batch_size=a.batch, train_samples=n_train, lr=0.1, sync_steps=1, epochs=1,
                    eval_every=0, verbose=0, codec=a.codec, topk_ratio=a.topk_ratio, use_graph=not a.no_graph, fetch_codec=a.fetch_codec,
-                   overlap=a.overlap, bucket_mb=a.bucket_mb, topology=a.topology).validate()
+                   overlap=a.overlap, bucket_mb=a.bucket_mb, topology=a.topology, dtype=a.dtype).validate()
     model, layout, arena, counters = build_state(cfg)
     wire = torch.float16 if a.codec == "fp16" else torch.float32  # topk encodes from fp32 grads
 
@@ -114,8 +119,8 @@ def main():
             for i in range(W):
                 server.register_worker(f"worker-{i}", i)
     train, _ = make_datasets(cfg, device, model.fc.out_features)
-    comp = HipCompute(model, layout, a.batch, device, a.model, wire, seed=rank, use_graph=cfg.use_graph) \
-        if is_worker else None
+    comp = HipCompute(model, layout, a.batch, device, a.model, wire, seed=rank, use_graph=cfg.use_graph,
+                      dtype=cfg.dtype) if is_worker else None
     wk = None
     zeros = None
     sess = None
@@ -202,7 +207,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_SYNC_IMG_S, 2) if r18 else None,
-            "dtype": "bf16",
+            "dtype": cfg.dtype,
             "data": (f"synthetic CIFAR-100-shaped ({n_train}x32x32x3 uint8 in HBM, on-device crop/flip/normalize), "
                      "random-init weights" if r18 else
                      f"synthetic ImageNet-shaped ({n_train}x224x224x3 uint8 in HBM, on-device crop/flip/normalize), "
@@ -224,7 +229,7 @@ def main():
                 "lr": 0.1,
                 "sync_steps": 1,
                 "codec": a.codec if a.codec != "topk" else f"topk({a.topk_ratio}) + error feedback",
-                "fetch_codec": a.fetch_codec if t is not None else "in-process",
+                "fetch_codec": cfg.fetch_codec if t is not None else "in-process",
                 "weight_image": getattr(chan, "image_wire", None) is not None or sharded,
                 "overlap": (f"bucketed reduce/apply/broadcast during backward ({len(chan.buckets)} buckets)"
                             if getattr(chan, "overlap", False) else

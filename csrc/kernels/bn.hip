@@ -1,4 +1,5 @@
-// Training-mode BatchNorm2d (+ReLU, +residual) on NHWC bf16 activations.
+// Training-mode BatchNorm2d (+ReLU, +residual) on NHWC activations (bf16 bits or fp32: every
+// elementwise kernel is templated on the storage type T, common.hpp ld8/st8).
 //
 // Replaces nn.BatchNorm2d / torch.relu / `out += shortcut` of the reference BasicBlock
 // (reference: src/parameter_server/server.py:21-41, identical copies in worker.py:20-76).
@@ -8,7 +9,7 @@
 // Forward statistics come from the conv epilogue as per-tile partial (sum, sumsq) slabs
 // ([T][2][C]); bn_finalize reduces them (fp64, fixed order => deterministic), produces the
 // per-channel affine (scale, shift) and updates the running stats. Every elementwise pass is
-// vectorised at 16 B per lane (8 channels).
+// vectorised at 8 channels per lane (16 B bf16 / 32 B fp32).
 #include <stdlib.h>
 
 #include "bnfin.hpp"
@@ -74,52 +75,39 @@ __global__ void bn_eval_affine_kernel(int C, const float* gamma, const float* be
 
 // out = act( y*scale + shift  [+ res]  [+ res2*scale2 + shift2] )
 // MODE 0: no residual, 1: identity residual, 2: BN'd residual.
-template <int MODE, bool RELU>
-__global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ scale,
-                                                       const float* __restrict__ shift,
-                                                       const uint16_t* __restrict__ res,
+template <typename T, int MODE, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ y, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, const T* __restrict__ res,
                                                        const float* __restrict__ scale2,
-                                                       const float* __restrict__ shift2, uint16_t* __restrict__ out,
+                                                       const float* __restrict__ shift2, T* __restrict__ out,
                                                        size_t nvec, int C) {
   const int cvec = C >> 3;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
     const int c0 = (int)(i % cvec) << 3;
-    const u32x4 v = reinterpret_cast<const u32x4*>(y)[i];
-    u32x4 rv = {0u, 0u, 0u, 0u};
-    if (MODE != 0) rv = reinterpret_cast<const u32x4*>(res)[i];
-    u32x4 o;
+    float v[8], rv[8];
+    ld8(y + i * 8, v);
+    if (MODE != 0) ld8(res + i * 8, rv);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = c0 + 2 * j;
-      float a0 = lo_bf(v[j]) * scale[c] + shift[c];
-      float a1 = hi_bf(v[j]) * scale[c + 1] + shift[c + 1];
-      if (MODE == 1) {
-        a0 += lo_bf(rv[j]);
-        a1 += hi_bf(rv[j]);
-      } else if (MODE == 2) {
-        a0 += lo_bf(rv[j]) * scale2[c] + shift2[c];
-        a1 += hi_bf(rv[j]) * scale2[c + 1] + shift2[c + 1];
-      }
-      if (RELU) {
-        a0 = fmaxf(a0, 0.f);
-        a1 = fmaxf(a1, 0.f);
-      }
-      o[j] = pack_bf2(a0, a1);
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      float t = v[j] * scale[c] + shift[c];
+      if (MODE == 1) t += rv[j];
+      else if (MODE == 2) t += rv[j] * scale2[c] + shift2[c];
+      v[j] = RELU ? fmaxf(t, 0.f) : t;
     }
-    reinterpret_cast<u32x4*>(out)[i] = o;
+    st8(out + i * 8, v);
   }
 }
 
 // Backward pass 1: per-channel partials of sum(dz), sum(dz*xhat1) [, sum(dz*xhat2)], with
 // dz = g * (o > 0) (ReLU mask from the stored activation) or dz = g.
 // part layout: [PSX_STAT_SLOTS][NS][C] (pre-zeroed, fp32 atomics), NS = 2 or 3.
-template <bool MASK, bool TWO>
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ g,
-                                                            const uint16_t* __restrict__ o,
-                                                            const uint16_t* __restrict__ y1,
+template <typename T, bool MASK, bool TWO>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict__ g, const T* __restrict__ o,
+                                                            const T* __restrict__ y1,
                                                             const float* __restrict__ mean1,
                                                             const float* __restrict__ invstd1,
-                                                            const uint16_t* __restrict__ y2,
+                                                            const T* __restrict__ y2,
                                                             const float* __restrict__ mean2,
                                                             const float* __restrict__ invstd2, float* __restrict__ part,
                                                             int npix, int C, int pix_per_block, int fuse_fin,
@@ -146,28 +134,19 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   const int pbeg = blockIdx.x * pix_per_block;
   const int pend = min(npix, pbeg + pix_per_block);
   for (int p = pbeg + pr; p < pend; p += tpp) {
-    const size_t vi = (size_t)p * cvec + cg;
-    const u32x4 gv = reinterpret_cast<const u32x4*>(g)[vi];
-    u32x4 ov = {0u, 0u, 0u, 0u};
-    if (MASK) ov = reinterpret_cast<const u32x4*>(o)[vi];
-    const u32x4 yv = reinterpret_cast<const u32x4*>(y1)[vi];
-    u32x4 y2v = {0u, 0u, 0u, 0u};
-    if (TWO) y2v = reinterpret_cast<const u32x4*>(y2)[vi];
+    const size_t e0 = ((size_t)p * cvec + cg) * 8;
+    float gv[8], ov[8], yv[8], y2v[8];
+    ld8(g + e0, gv);
+    if (MASK) ld8(o + e0, ov);
+    ld8(y1 + e0, yv);
+    if (TWO) ld8(y2 + e0, y2v);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float d0 = lo_bf(gv[j]), d1 = hi_bf(gv[j]);
-      if (MASK) {
-        if (!(lo_bf(ov[j]) > 0.f)) d0 = 0.f;
-        if (!(hi_bf(ov[j]) > 0.f)) d1 = 0.f;
-      }
-      sdz[2 * j] += d0;
-      sdz[2 * j + 1] += d1;
-      sx1[2 * j] += d0 * (lo_bf(yv[j]) - m1[2 * j]) * i1[2 * j];
-      sx1[2 * j + 1] += d1 * (hi_bf(yv[j]) - m1[2 * j + 1]) * i1[2 * j + 1];
-      if (TWO) {
-        sx2[2 * j] += d0 * (lo_bf(y2v[j]) - m2[2 * j]) * i2[2 * j];
-        sx2[2 * j + 1] += d1 * (hi_bf(y2v[j]) - m2[2 * j + 1]) * i2[2 * j + 1];
-      }
+    for (int j = 0; j < 8; ++j) {
+      float d = gv[j];
+      if (MASK && !(ov[j] > 0.f)) d = 0.f;
+      sdz[j] += d;
+      sx1[j] += d * (yv[j] - m1[j]) * i1[j];
+      if (TWO) sx2[j] += d * (y2v[j] - m2[j]) * i2[j];
     }
   }
   float* mine = sred + threadIdx.x * (NS * 8);
@@ -240,56 +219,41 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int T, in
 }
 
 // dx1 = k1*dz + k2*y1 + k3 [, dx2 = k1'*dz + k2'*y2 + k3'] [, dzout = dz]
-template <bool MASK, bool TWO, bool DZOUT>
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __restrict__ g,
-                                                           const uint16_t* __restrict__ o,
-                                                           const uint16_t* __restrict__ y1,
-                                                           const float* __restrict__ coef1,
-                                                           uint16_t* __restrict__ dx1,
-                                                           const uint16_t* __restrict__ y2,
-                                                           const float* __restrict__ coef2,
-                                                           uint16_t* __restrict__ dx2, uint16_t* __restrict__ dzout,
-                                                           size_t nvec, int C) {
+template <typename T, bool MASK, bool TWO, bool DZOUT>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ g, const T* __restrict__ o,
+                                                           const T* __restrict__ y1, const float* __restrict__ coef1,
+                                                           T* __restrict__ dx1, const T* __restrict__ y2,
+                                                           const float* __restrict__ coef2, T* __restrict__ dx2,
+                                                           T* __restrict__ dzout, size_t nvec, int C) {
   const int cvec = C >> 3;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
     const int c0 = (int)(i % cvec) << 3;
-    const u32x4 gv = reinterpret_cast<const u32x4*>(g)[i];
-    u32x4 ov = {0u, 0u, 0u, 0u};
-    if (MASK) ov = reinterpret_cast<const u32x4*>(o)[i];
-    const u32x4 yv = reinterpret_cast<const u32x4*>(y1)[i];
-    u32x4 y2v = {0u, 0u, 0u, 0u};
-    if (TWO) y2v = reinterpret_cast<const u32x4*>(y2)[i];
-    u32x4 r1, r2, rz;
+    float d[8], ov[8], yv[8], y2v[8], r1[8], r2[8];
+    ld8(g + i * 8, d);
+    if (MASK) ld8(o + i * 8, ov);
+    ld8(y1 + i * 8, yv);
+    if (TWO) ld8(y2 + i * 8, y2v);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = c0 + 2 * j;
-      float d0 = lo_bf(gv[j]), d1 = hi_bf(gv[j]);
-      if (MASK) {
-        if (!(lo_bf(ov[j]) > 0.f)) d0 = 0.f;
-        if (!(hi_bf(ov[j]) > 0.f)) d1 = 0.f;
-      }
-      r1[j] = pack_bf2(coef1[c] * d0 + coef1[C + c] * lo_bf(yv[j]) + coef1[2 * C + c],
-                       coef1[c + 1] * d1 + coef1[C + c + 1] * hi_bf(yv[j]) + coef1[2 * C + c + 1]);
-      if (TWO)
-        r2[j] = pack_bf2(coef2[c] * d0 + coef2[C + c] * lo_bf(y2v[j]) + coef2[2 * C + c],
-                         coef2[c + 1] * d1 + coef2[C + c + 1] * hi_bf(y2v[j]) + coef2[2 * C + c + 1]);
-      if (DZOUT) rz[j] = pack_bf2(d0, d1);
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      if (MASK && !(ov[j] > 0.f)) d[j] = 0.f;
+      r1[j] = coef1[c] * d[j] + coef1[C + c] * yv[j] + coef1[2 * C + c];
+      if (TWO) r2[j] = coef2[c] * d[j] + coef2[C + c] * y2v[j] + coef2[2 * C + c];
     }
-    reinterpret_cast<u32x4*>(dx1)[i] = r1;
-    if (TWO) reinterpret_cast<u32x4*>(dx2)[i] = r2;
-    if (DZOUT) reinterpret_cast<u32x4*>(dzout)[i] = rz;
+    st8(dx1 + i * 8, r1);
+    if (TWO) st8(dx2 + i * 8, r2);
+    if (DZOUT) st8(dzout + i * 8, d);
   }
 }
 
 // Opt-in (PSX_BNFIN_APPLY=1) variant of bn_apply_kernel with the training-mode finalize folded in:
 // every workgroup computes the affine(s) from the stat slots (bnfin.hpp bn_fin_lds). Separate
 // kernels so the default path keeps its exact code (an A/B showed +38 us/step otherwise).
-template <int MODE, bool RELU, bool FIN = true>
-__global__ __launch_bounds__(256) void bn_apply_fin_kernel(const uint16_t* __restrict__ y, const float* __restrict__ scale,
-                                                       const float* __restrict__ shift,
-                                                       const uint16_t* __restrict__ res,
+template <typename T, int MODE, bool RELU, bool FIN = true>
+__global__ __launch_bounds__(256) void bn_apply_fin_kernel(const T* __restrict__ y, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, const T* __restrict__ res,
                                                        const float* __restrict__ scale2,
-                                                       const float* __restrict__ shift2, uint16_t* __restrict__ out,
+                                                       const float* __restrict__ shift2, T* __restrict__ out,
                                                        size_t nvec, int C, const float* __restrict__ part1,
                                                        const float* __restrict__ part2, BnFin f1, BnFin f2) {
   extern __shared__ __attribute__((aligned(16))) float sbn[];  // FIN: [scale1|shift1|scale2|shift2] x C, red, scratch
@@ -332,42 +296,29 @@ __global__ __launch_bounds__(256) void bn_apply_fin_kernel(const uint16_t* __res
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += stride) {
     const int c0 = (int)(i % cvec) << 3;
     if (!fixed || cur < 0) load(c0);
-    const u32x4 v = reinterpret_cast<const u32x4*>(y)[i];
-    u32x4 rv = {0u, 0u, 0u, 0u};
-    if (MODE != 0) rv = reinterpret_cast<const u32x4*>(res)[i];
-    u32x4 o;
+    float v[8], rv[8];
+    ld8(y + i * 8, v);
+    if (MODE != 0) ld8(res + i * 8, rv);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float a0 = lo_bf(v[j]) * k[0][2 * j] + k[1][2 * j];
-      float a1 = hi_bf(v[j]) * k[0][2 * j + 1] + k[1][2 * j + 1];
-      if (MODE == 1) {
-        a0 += lo_bf(rv[j]);
-        a1 += hi_bf(rv[j]);
-      } else if (MODE == 2) {
-        a0 += lo_bf(rv[j]) * k[2][2 * j] + k[3][2 * j];
-        a1 += hi_bf(rv[j]) * k[2][2 * j + 1] + k[3][2 * j + 1];
-      }
-      if (RELU) {
-        a0 = fmaxf(a0, 0.f);
-        a1 = fmaxf(a1, 0.f);
-      }
-      o[j] = pack_bf2(a0, a1);
+    for (int j = 0; j < 8; ++j) {
+      float t = v[j] * k[0][j] + k[1][j];
+      if (MODE == 1) t += rv[j];
+      else if (MODE == 2) t += rv[j] * k[2][j] + k[3][j];
+      v[j] = RELU ? fmaxf(t, 0.f) : t;
     }
-    reinterpret_cast<u32x4*>(out)[i] = o;
+    st8(out + i * 8, v);
   }
 }
 
 // Opt-in variant of bn_bwd_apply_kernel: coefficients from the slot sums part [T][NS][C] per
 // workgroup (bnfin.hpp bn_bwd_fin_lds).
-template <bool MASK, bool TWO, bool DZOUT, bool FIN = true>
-__global__ __launch_bounds__(256) void bn_bwd_apply_fin_kernel(const uint16_t* __restrict__ g,
-                                                           const uint16_t* __restrict__ o,
-                                                           const uint16_t* __restrict__ y1,
-                                                           const float* __restrict__ coef1,
-                                                           uint16_t* __restrict__ dx1,
-                                                           const uint16_t* __restrict__ y2,
-                                                           const float* __restrict__ coef2,
-                                                           uint16_t* __restrict__ dx2, uint16_t* __restrict__ dzout,
+template <typename T, bool MASK, bool TWO, bool DZOUT, bool FIN = true>
+__global__ __launch_bounds__(256) void bn_bwd_apply_fin_kernel(const T* __restrict__ g, const T* __restrict__ o,
+                                                           const T* __restrict__ y1,
+                                                           const float* __restrict__ coef1, T* __restrict__ dx1,
+                                                           const T* __restrict__ y2,
+                                                           const float* __restrict__ coef2, T* __restrict__ dx2,
+                                                           T* __restrict__ dzout,
                                                            size_t nvec, int C, const float* __restrict__ part,
                                                            BnBwdFin f1, BnBwdFin f2) {
   extern __shared__ __attribute__((aligned(16))) float sbn[];  // FIN: coef1 [3][C] | coef2 [3][C] | red | scratch
@@ -402,31 +353,20 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin_kernel(const uint16_t* _
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += stride) {
     const int c0 = (int)(i % cvec) << 3;
     if (!fixed || cur < 0) load(c0);
-    const u32x4 gv = reinterpret_cast<const u32x4*>(g)[i];
-    u32x4 ov = {0u, 0u, 0u, 0u};
-    if (MASK) ov = reinterpret_cast<const u32x4*>(o)[i];
-    const u32x4 yv = reinterpret_cast<const u32x4*>(y1)[i];
-    u32x4 y2v = {0u, 0u, 0u, 0u};
-    if (TWO) y2v = reinterpret_cast<const u32x4*>(y2)[i];
-    u32x4 r1, r2, rz;
+    float d[8], ov[8], yv[8], y2v[8], r1[8], r2[8];
+    ld8(g + i * 8, d);
+    if (MASK) ld8(o + i * 8, ov);
+    ld8(y1 + i * 8, yv);
+    if (TWO) ld8(y2 + i * 8, y2v);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e0 = 2 * j, e1 = 2 * j + 1;
-      float d0 = lo_bf(gv[j]), d1 = hi_bf(gv[j]);
-      if (MASK) {
-        if (!(lo_bf(ov[j]) > 0.f)) d0 = 0.f;
-        if (!(hi_bf(ov[j]) > 0.f)) d1 = 0.f;
-      }
-      r1[j] = pack_bf2(k1[0][e0] * d0 + k1[1][e0] * lo_bf(yv[j]) + k1[2][e0],
-                       k1[0][e1] * d1 + k1[1][e1] * hi_bf(yv[j]) + k1[2][e1]);
-      if (TWO)
-        r2[j] = pack_bf2(k2[0][e0] * d0 + k2[1][e0] * lo_bf(y2v[j]) + k2[2][e0],
-                         k2[0][e1] * d1 + k2[1][e1] * hi_bf(y2v[j]) + k2[2][e1]);
-      if (DZOUT) rz[j] = pack_bf2(d0, d1);
+    for (int j = 0; j < 8; ++j) {
+      if (MASK && !(ov[j] > 0.f)) d[j] = 0.f;
+      r1[j] = k1[0][j] * d[j] + k1[1][j] * yv[j] + k1[2][j];
+      if (TWO) r2[j] = k2[0][j] * d[j] + k2[1][j] * y2v[j] + k2[2][j];
     }
-    reinterpret_cast<u32x4*>(dx1)[i] = r1;
-    if (TWO) reinterpret_cast<u32x4*>(dx2)[i] = r2;
-    if (DZOUT) reinterpret_cast<u32x4*>(dzout)[i] = rz;
+    st8(dx1 + i * 8, r1);
+    if (TWO) st8(dx2 + i * 8, r2);
+    if (DZOUT) st8(dzout + i * 8, d);
   }
 }
 
@@ -469,13 +409,19 @@ int psx_bn_eval_affine(int C, const float* gamma, const float* beta, const float
 
 // mode: 0 plain, 1 +identity residual, 2 +BN'd residual
 int psx_bn_apply(const void* y, const float* scale, const float* shift, const void* res, const float* scale2,
-                 const float* shift2, void* out, long nelem, int C, int mode, int relu, hipStream_t st) {
+                 const float* shift2, void* out, long nelem, int C, int mode, int relu, int f32, hipStream_t st) {
   if (C % 8 || nelem % 8) return -2;
   const size_t nvec = (size_t)nelem / 8;
   const int grid = ew_grid(nvec);
-#define PSX_BNA(M, R)                                                                                         \
-  hipLaunchKernelGGL((bn_apply_kernel<M, R>), dim3(grid), dim3(256), 0, st, (const uint16_t*)y, scale, shift, \
-                     (const uint16_t*)res, scale2, shift2, (uint16_t*)out, nvec, C)
+#define PSX_BNA(M, R)                                                                                           \
+  do {                                                                                                          \
+    if (f32)                                                                                                    \
+      hipLaunchKernelGGL((bn_apply_kernel<float, M, R>), dim3(grid), dim3(256), 0, st, (const float*)y, scale,  \
+                         shift, (const float*)res, scale2, shift2, (float*)out, nvec, C);                       \
+    else                                                                                                        \
+      hipLaunchKernelGGL((bn_apply_kernel<uint16_t, M, R>), dim3(grid), dim3(256), 0, st, (const uint16_t*)y,   \
+                         scale, shift, (const uint16_t*)res, scale2, shift2, (uint16_t*)out, nvec, C);          \
+  } while (0)
   if (mode == 0 && relu) PSX_BNA(0, true);
   else if (mode == 0) PSX_BNA(0, false);
   else if (mode == 1 && relu) PSX_BNA(1, true);
@@ -490,7 +436,7 @@ int psx_bn_apply(const void* y, const float* scale, const float* shift, const vo
 // Returns the number of partial rows T (query with part == nullptr).
 int psx_bn_bwd_reduce(const void* g, const void* o, const void* y1, const float* mean1, const float* invstd1,
                       const void* y2, const float* mean2, const float* invstd2, float* part, int npix, int C,
-                      const BnBwdFin* fin1, const BnBwdFin* fin2, hipStream_t st) {
+                      const BnBwdFin* fin1, const BnBwdFin* fin2, int f32, hipStream_t st) {
   if (C % 8 || 256 % (C / 8)) return -2;
   const int fuse = fin1 != nullptr;
   BnBwdFin f1{}, f2{};
@@ -504,10 +450,17 @@ int psx_bn_bwd_reduce(const void* g, const void* o, const void* y1, const float*
   if (!part) return PSX_STAT_SLOTS;
   const bool mask = o != nullptr, two = y2 != nullptr;
   const size_t lds = 256 * (two ? 3 : 2) * 8 * sizeof(float);
-#define PSX_BBR(M, TW)                                                                                          \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<M, TW>), dim3(T), dim3(256), lds, st, (const uint16_t*)g,           \
-                     (const uint16_t*)o, (const uint16_t*)y1, mean1, invstd1, (const uint16_t*)y2, mean2, invstd2, \
-                     part, npix, C, ppb, fuse, f1, f2)
+#define PSX_BBR(M, TW)                                                                                         \
+  do {                                                                                                         \
+    if (f32)                                                                                                   \
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, M, TW>), dim3(T), dim3(256), lds, st, (const float*)g,   \
+                         (const float*)o, (const float*)y1, mean1, invstd1, (const float*)y2, mean2, invstd2,  \
+                         part, npix, C, ppb, fuse, f1, f2);                                                    \
+    else                                                                                                       \
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<uint16_t, M, TW>), dim3(T), dim3(256), lds, st,                 \
+                         (const uint16_t*)g, (const uint16_t*)o, (const uint16_t*)y1, mean1, invstd1,          \
+                         (const uint16_t*)y2, mean2, invstd2, part, npix, C, ppb, fuse, f1, f2);               \
+  } while (0)
   if (mask && two) PSX_BBR(true, true);
   else if (mask) PSX_BBR(true, false);
   else if (two) PSX_BBR(false, true);
@@ -531,15 +484,22 @@ int psx_bn_bwd_finalize(const float* part, int T, int NS, int which, int C, floa
 }
 
 int psx_bn_bwd_apply(const void* g, const void* o, const void* y1, const float* coef1, void* dx1, const void* y2,
-                     const float* coef2, void* dx2, void* dzout, long nelem, int C, hipStream_t st) {
+                     const float* coef2, void* dx2, void* dzout, long nelem, int C, int f32, hipStream_t st) {
   if (C % 8 || nelem % 8) return -2;
   const size_t nvec = (size_t)nelem / 8;
   const int grid = ew_grid(nvec);
   const bool mask = o != nullptr, two = y2 != nullptr, dz = dzout != nullptr;
-#define PSX_BBA(M, TW, DZ)                                                                                        \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<M, TW, DZ>), dim3(grid), dim3(256), 0, st, (const uint16_t*)g,         \
-                     (const uint16_t*)o, (const uint16_t*)y1, coef1, (uint16_t*)dx1, (const uint16_t*)y2, coef2, \
-                     (uint16_t*)dx2, (uint16_t*)dzout, nvec, C)
+#define PSX_BBA(M, TW, DZ)                                                                                      \
+  do {                                                                                                          \
+    if (f32)                                                                                                    \
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<float, M, TW, DZ>), dim3(grid), dim3(256), 0, st, (const float*)g, \
+                         (const float*)o, (const float*)y1, coef1, (float*)dx1, (const float*)y2, coef2,         \
+                         (float*)dx2, (float*)dzout, nvec, C);                                                  \
+    else                                                                                                        \
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<uint16_t, M, TW, DZ>), dim3(grid), dim3(256), 0, st,              \
+                         (const uint16_t*)g, (const uint16_t*)o, (const uint16_t*)y1, coef1, (uint16_t*)dx1,    \
+                         (const uint16_t*)y2, coef2, (uint16_t*)dx2, (uint16_t*)dzout, nvec, C);                \
+  } while (0)
   if (mask && two && dz) PSX_BBA(true, true, true);
   else if (mask && two) PSX_BBA(true, true, false);
   else if (mask && dz) PSX_BBA(true, false, true);
@@ -555,7 +515,7 @@ int psx_bn_bwd_apply(const void* g, const void* o, const void* y1, const float* 
 // Training-mode apply with the finalize folded in: part1/part2 = [PSX_STAT_SLOTS][2][C] slot
 // sums of the layer (and of the shortcut BN for mode 2); fin1/fin2 name the side outputs.
 int psx_bn_apply_fin(const void* y, const float* part1, const BnFin* fin1, const void* res, const float* part2,
-                     const BnFin* fin2, void* out, long nelem, int C, int mode, int relu, hipStream_t st) {
+                     const BnFin* fin2, void* out, long nelem, int C, int mode, int relu, int f32, hipStream_t st) {
   if (!fin1) return -10;
   if (C % 8 || nelem % 8) return -2;
   if (fin1->C != C || (mode == 2 && (!fin2 || fin2->C != C))) return -10;
@@ -565,9 +525,17 @@ int psx_bn_apply_fin(const void* y, const float* part1, const BnFin* fin1, const
   const size_t lds = (size_t)(8 * C + 1024) * sizeof(float);  // affines, red [2][C] f64, scratch
   const BnFin f1 = *fin1;
   const BnFin f2 = fin2 ? *fin2 : BnFin{};
-#define PSX_BNAF(M, R)                                                                                      \
-  hipLaunchKernelGGL((bn_apply_fin_kernel<M, R>), dim3(grid), dim3(256), lds, st, (const uint16_t*)y, nullptr, \
-                     nullptr, (const uint16_t*)res, nullptr, nullptr, (uint16_t*)out, nvec, C, part1, part2, f1, f2)
+#define PSX_BNAF(M, R)                                                                                        \
+  do {                                                                                                        \
+    if (f32)                                                                                                  \
+      hipLaunchKernelGGL((bn_apply_fin_kernel<float, M, R>), dim3(grid), dim3(256), lds, st, (const float*)y,  \
+                         nullptr, nullptr, (const float*)res, nullptr, nullptr, (float*)out, nvec, C, part1,   \
+                         part2, f1, f2);                                                                      \
+    else                                                                                                      \
+      hipLaunchKernelGGL((bn_apply_fin_kernel<uint16_t, M, R>), dim3(grid), dim3(256), lds, st,               \
+                         (const uint16_t*)y, nullptr, nullptr, (const uint16_t*)res, nullptr, nullptr,        \
+                         (uint16_t*)out, nvec, C, part1, part2, f1, f2);                                      \
+  } while (0)
   if (mode == 0 && relu) PSX_BNAF(0, true);
   else if (mode == 0) PSX_BNAF(0, false);
   else if (mode == 1 && relu) PSX_BNAF(1, true);
@@ -583,7 +551,7 @@ int psx_bn_apply_fin(const void* y, const float* part1, const BnFin* fin1, const
 // (NS = 3 with y2); fin1/fin2 name the coefficient and dgamma/dbeta outputs.
 int psx_bn_bwd_apply_fin(const void* g, const void* o, const void* y1, const float* part, const BnBwdFin* fin1,
                          void* dx1, const void* y2, const BnBwdFin* fin2, void* dx2, void* dzout, long nelem, int C,
-                         hipStream_t st) {
+                         int f32, hipStream_t st) {
   if (!fin1) return -10;
   if (C % 8 || nelem % 8) return -2;
   const bool mask = o != nullptr, two = y2 != nullptr, dz = dzout != nullptr;
@@ -594,10 +562,18 @@ int psx_bn_bwd_apply_fin(const void* g, const void* o, const void* y1, const flo
   const size_t lds = (size_t)(10 * C + 1024) * sizeof(float);  // coefs, red [2][C] f64, scratch
   const BnBwdFin f1 = *fin1;
   const BnBwdFin f2 = fin2 ? *fin2 : BnBwdFin{};
-#define PSX_BBAF(M, TW, DZ)                                                                                         \
-  hipLaunchKernelGGL((bn_bwd_apply_fin_kernel<M, TW, DZ>), dim3(grid), dim3(256), lds, st, (const uint16_t*)g,     \
-                     (const uint16_t*)o, (const uint16_t*)y1, nullptr, (uint16_t*)dx1, (const uint16_t*)y2, nullptr, \
-                     (uint16_t*)dx2, (uint16_t*)dzout, nvec, C, part, f1, f2)
+#define PSX_BBAF(M, TW, DZ)                                                                                     \
+  do {                                                                                                         \
+    if (f32)                                                                                                   \
+      hipLaunchKernelGGL((bn_bwd_apply_fin_kernel<float, M, TW, DZ>), dim3(grid), dim3(256), lds, st,          \
+                         (const float*)g, (const float*)o, (const float*)y1, nullptr, (float*)dx1,             \
+                         (const float*)y2, nullptr, (float*)dx2, (float*)dzout, nvec, C, part, f1, f2);        \
+    else                                                                                                       \
+      hipLaunchKernelGGL((bn_bwd_apply_fin_kernel<uint16_t, M, TW, DZ>), dim3(grid), dim3(256), lds, st,       \
+                         (const uint16_t*)g, (const uint16_t*)o, (const uint16_t*)y1, nullptr, (uint16_t*)dx1, \
+                         (const uint16_t*)y2, nullptr, (uint16_t*)dx2, (uint16_t*)dzout, nvec, C, part, f1,   \
+                         f2);                                                                                  \
+  } while (0)
   if (mask && two && dz) PSX_BBAF(true, true, true);
   else if (mask && two) PSX_BBAF(true, true, false);
   else if (mask && dz) PSX_BBAF(true, false, true);

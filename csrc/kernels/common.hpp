@@ -51,6 +51,102 @@ PSX_DEV uint32_t pack_bf2(float lo, float hi) {
 PSX_DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 PSX_DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
+// ---- activation storage types ----------------------------------------------------------
+// Every activation-touching kernel is templated on its storage type T: uint16_t (bf16 bits, the
+// fast path) or float (fp32, the reference's training precision: src/workers/worker.py:333-348
+// runs torch CPU fp32). A 16-byte chunk holds kEPC<T> channels of one pixel and a 128-byte
+// implicit-GEMM k-step row kKS<T> of them, so the LDS tile images, the DMA staging and the
+// swizzles are byte-identical for both types; only the MFMA and the epilogue conversions differ.
+template <typename T>
+constexpr int kEPC = 16 / (int)sizeof(T);
+template <typename T>
+constexpr int kKS = 128 / (int)sizeof(T);
+
+// 8 consecutive channels <-> 8 floats (one u32x4 for bf16, two f32x4 for fp32)
+PSX_DEV void ld8(const uint16_t* p, float (&v)[8]) {
+  const u32x4 w = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = lo_bf(w[j]);
+    v[2 * j + 1] = hi_bf(w[j]);
+  }
+}
+PSX_DEV void ld8(const float* p, float (&v)[8]) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = a[j];
+    v[4 + j] = b[j];
+  }
+}
+// store, then leave in v the value as stored (the BN statistics are taken of the stored tensor)
+PSX_DEV void st8(uint16_t* p, float (&v)[8]) {
+  u32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = pack_bf2(v[2 * j], v[2 * j + 1]);
+  *reinterpret_cast<u32x4*>(p) = o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = lo_bf(o[j]);
+    v[2 * j + 1] = hi_bf(o[j]);
+  }
+}
+PSX_DEV void st8(float* p, float (&v)[8]) {
+  *reinterpret_cast<f32x4*>(p) = (f32x4){v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4*>(p + 4) = (f32x4){v[4], v[5], v[6], v[7]};
+}
+// 2 consecutive channels (4-byte bf16 pair / 8-byte fp32 pair)
+PSX_DEV void ld2(const uint16_t* p, float& a, float& b) {
+  const uint32_t w = *reinterpret_cast<const uint32_t*>(p);
+  a = lo_bf(w);
+  b = hi_bf(w);
+}
+PSX_DEV void ld2(const float* p, float& a, float& b) {
+  const float2 w = *reinterpret_cast<const float2*>(p);
+  a = w.x;
+  b = w.y;
+}
+PSX_DEV void st2(uint16_t* p, float& a, float& b) {
+  const uint32_t w = pack_bf2(a, b);
+  *reinterpret_cast<uint32_t*>(p) = w;
+  a = lo_bf(w);
+  b = hi_bf(w);
+}
+PSX_DEV void st2(float* p, float& a, float& b) { *reinterpret_cast<float2*>(p) = make_float2(a, b); }
+PSX_DEV float ld1(const uint16_t* p) { return bf2f(*p); }
+PSX_DEV float ld1(const float* p) { return *p; }
+PSX_DEV void st1(uint16_t* p, float v) { *p = f2bf(v); }
+PSX_DEV void st1(float* p, float v) { *p = v; }
+
+// One 16x16 output tile += A-fragment x B-fragment of one 16-byte chunk per lane (lane l: row
+// l & 15, k-group l >> 4). bf16: one v_mfma_f32_16x16x32_bf16. fp32: four v_mfma_f32_16x16x4_f32
+// (exact f32, cdna_hip_programming.md §3) — element j of the chunk feeds the j-th, so MFMA j sums
+// k = 4*(l>>4) + j over the four lane groups; A and B share the permutation, the sum is the
+// same set of products. The fp32 form is issued j-outermost over a wave's tiles (mma_tiles) so
+// consecutive MFMAs never chain on one accumulator (40-cycle dependent latency, 32-cycle issue).
+PSX_DEV void mma_chunk(f32x4& acc, const u32x4& a, const u32x4& b, uint16_t) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc,
+                                                0, 0, 0);
+}
+template <int MT, int NT, typename T>
+PSX_DEV void mma_tiles(f32x4 (&acc)[MT][NT], const u32x4 (&fa)[MT], const u32x4 (&fb)[NT]) {
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) mma_chunk(acc[m][n], fa[m], fb[n], uint16_t{});
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(fa[m][j]), __uint_as_float(fb[n][j]),
+                                                           acc[m][n], 0, 0, 0);
+  }
+}
+
 PSX_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -1,6 +1,7 @@
 // Device-side data pipeline: CIFAR-shaped uint8 dataset resident in HBM, per-step batch
 // gather + RandomCrop(32, padding=4) + RandomHorizontalFlip + Normalize(mean, std) fused into
-// one kernel that writes the network input directly as NHWC bf16 with channels padded 3 -> 8.
+// one kernel that writes the network input directly as NHWC bf16 with channels padded 3 -> 8,
+// or as NHWC fp32 padded 3 -> 4 (the fp32 path: one 16-byte chunk per pixel either way).
 //
 // Replaces the torchvision transform pipeline + DataLoader worker processes of the reference
 // (reference: src/workers/worker.py:145-155,182-197; baseline/baseline_training.py:13-23).
@@ -52,12 +53,13 @@ struct AugArgs {
   const uint8_t* img;  // [N][H][W][3]
   const int* labels;   // [N]
   const int* index;    // [B] sample indices of this batch
-  uint16_t* out;       // [B][H][W][8] bf16
+  void* out;           // [B][H][W][8] bf16 or [B][H][W][4] fp32 (f32)
   int* out_labels;     // [B]
   int B, H, W, pad;
   uint32_t seed;
   const unsigned* step;  // device scalar, so a captured graph sees the live step counter
   int train;           // 1: random crop + flip, 0: centre (eval transform)
+  int f32;
   float mean[3], inv_std[3];
   uint32_t* zero0;  // optional 32-bit words zeroed by the same launch (the step's BN statistic
   long nzero0;      // slots and accuracy counter: two fewer launches per step)
@@ -93,17 +95,22 @@ __global__ __launch_bounds__(256) void augment_kernel(AugArgs a) {
       const float px = in ? (float)a.img[(((long)n * a.H + ih) * a.W + iw) * 3 + c] * (1.f / 255.f) : 0.f;
       v[c] = (px - a.mean[c]) * a.inv_std[c];
     }
-    u32x4 o;
-    o[0] = pack_bf2(v[0], v[1]);
-    o[1] = pack_bf2(v[2], 0.f);
-    o[2] = 0u;
-    o[3] = 0u;
-    reinterpret_cast<u32x4*>(a.out)[i] = o;
+    if (a.f32) {
+      reinterpret_cast<f32x4*>(a.out)[i] = (f32x4){v[0], v[1], v[2], 0.f};
+    } else {
+      u32x4 o;
+      o[0] = pack_bf2(v[0], v[1]);
+      o[1] = pack_bf2(v[2], 0.f);
+      o[2] = 0u;
+      o[3] = 0u;
+      reinterpret_cast<u32x4*>(a.out)[i] = o;
+    }
   }
 }
 
-// NCHW fp32 (e.g. a torch batch) -> NHWC bf16 with channel padding to Cp
-__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, int N, int C, int H, int W,
+// NCHW fp32 (e.g. a torch batch) -> NHWC (bf16 or fp32) with channel padding to Cp
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__ y, int N, int C, int H, int W,
                                     int Cp) {
   const long total = (long)N * H * W * Cp;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -114,7 +121,7 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, uint16_t* __res
     const int h = (int)(t % H);
     const int n = (int)(t / H);
     const float v = c < C ? x[(((long)n * C + c) * H + h) * W + w] : 0.f;
-    y[i] = f2bf(v);
+    st1(y + i, v);
   }
 }
 
@@ -136,7 +143,7 @@ int psx_synth_gen(void* img, int* labels, int N, int H, int W, int classes, unsi
 
 int psx_augment(const void* img, const int* labels, const int* index, void* out, int* out_labels, int B, int H, int W,
                 int pad, unsigned seed, const unsigned* step, int train, const float* mean3, const float* std3,
-                void* zero0, long nzero0, void* zero1, long nzero1, hipStream_t st) {
+                void* zero0, long nzero0, void* zero1, long nzero1, int f32, hipStream_t st) {
   AugArgs a{};
   a.zero0 = (uint32_t*)zero0;
   a.nzero0 = zero0 ? nzero0 : 0;
@@ -145,7 +152,8 @@ int psx_augment(const void* img, const int* labels, const int* index, void* out,
   a.img = (const uint8_t*)img;
   a.labels = labels;
   a.index = index;
-  a.out = (uint16_t*)out;
+  a.out = out;
+  a.f32 = f32;
   a.out_labels = out_labels;
   a.B = B; a.H = H; a.W = W; a.pad = pad;
   a.seed = seed; a.step = step; a.train = train;
@@ -160,11 +168,15 @@ int psx_augment(const void* img, const int* labels, const int* index, void* out,
   return (int)hipGetLastError();
 }
 
-int psx_nchw_to_nhwc(const float* x, void* y, int N, int C, int H, int W, int Cp, hipStream_t st) {
+int psx_nchw_to_nhwc(const float* x, void* y, int N, int C, int H, int W, int Cp, int f32, hipStream_t st) {
   long total = (long)N * H * W * Cp;
   long g = (total + 255) / 256;
   if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3((unsigned)g), dim3(256), 0, st, x, (uint16_t*)y, N, C, H, W, Cp);
+  if (f32)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3((unsigned)g), dim3(256), 0, st, x, (float*)y, N, C, H, W, Cp);
+  else
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<uint16_t>, dim3((unsigned)g), dim3(256), 0, st, x, (uint16_t*)y, N, C, H,
+                       W, Cp);
   return (int)hipGetLastError();
 }
 

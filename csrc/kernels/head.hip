@@ -21,30 +21,31 @@ struct HeadBnStats {
   const float* saved2;
 };
 
-// act: NHWC [B][HW][C] bf16; fcw: [K][C] fp32; fcb: [K] fp32; labels int32 [B]
-// outputs: pooled [B][C] fp32, dlogits [B][K] fp32 (already divided by B), dact (bf16, same
-// shape as act; nullable for eval), loss [B] fp32, correct (atomic int counter, nullable).
-// One workgroup per sample; C must be a multiple of 512 or <= 512 and even, K <= 256.
-template <bool BWD>
-__global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ act, int HW, int C,
+// act: NHWC [B][HW][C] of storage type T (bf16 bits or fp32); fcw: [K][C] fp32; fcb: [K] fp32;
+// labels int32 [B]. outputs: pooled [B][C] fp32, dlogits [B][K] fp32 (already divided by B),
+// dact (T, same shape as act; nullable for eval), loss [B] fp32, correct (atomic int counter,
+// nullable). One workgroup per sample; C must be a multiple of 512 or <= 512 and even, K <= 256.
+template <typename T, bool BWD>
+__global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ act, int HW, int C,
                                                    const float* __restrict__ fcw, const float* __restrict__ fcb, int K,
                                                    const int* __restrict__ labels, float* __restrict__ pooled,
-                                                   float* __restrict__ dlogits, uint16_t* __restrict__ dact,
+                                                   float* __restrict__ dlogits, T* __restrict__ dact,
                                                    float* __restrict__ loss, int* __restrict__ correct, float invB,
                                                    HeadBnStats bs) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
   float* sp = sh;      // [C]  pooled
   float* sl = sh + C;  // [K]  logits -> dlogits
   const int b = blockIdx.x, tid = threadIdx.x;
-  const uint16_t* a = act + (size_t)b * HW * C;
+  const T* a = act + (size_t)b * HW * C;
   const float inv_hw = 1.f / (float)HW;
-  // global average pool, 2 channels per thread per pass (4-byte loads, coalesced)
+  // global average pool, 2 channels per thread per pass (coalesced pair loads)
   for (int c = 2 * tid; c < C; c += 512) {
     float s0 = 0.f, s1 = 0.f;
     for (int p = 0; p < HW; ++p) {
-      const uint32_t v = *reinterpret_cast<const uint32_t*>(a + (size_t)p * C + c);
-      s0 += lo_bf(v);
-      s1 += hi_bf(v);
+      float v0, v1;
+      ld2(a + (size_t)p * C + c, v0, v1);
+      s0 += v0;
+      s1 += v1;
     }
     s0 *= inv_hw;
     s1 *= inv_hw;
@@ -118,21 +119,28 @@ __global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ 
       s0 += sl[k] * w.x;
       s1 += sl[k] * w.y;
     }
-    const uint32_t v = pack_bf2(s0 * inv_hw, s1 * inv_hw);
-    for (int p = 0; p < HW; ++p) *reinterpret_cast<uint32_t*>(dact + ((size_t)b * HW + p) * C + c) = v;
+    float g0 = s0 * inv_hw, g1 = s1 * inv_hw;
+    for (int p = 0; p < HW; ++p) {
+      float q0 = g0, q1 = g1;
+      st2(dact + ((size_t)b * HW + p) * C + c, q0, q1);
+      if (p == HW - 1) {  // the gradient as stored
+        g0 = q0;
+        g1 = q1;
+      }
+    }
     if (bs.part) {  // BN-backward sums of the consumed layer (see HeadBnStats)
-      const float g0 = lo_bf(v), g1 = hi_bf(v);
       const float m0 = bs.saved1[c], i0 = bs.saved1[C + c], m1 = bs.saved1[c + 1], i1 = bs.saved1[C + c + 1];
-      const uint16_t* y = reinterpret_cast<const uint16_t*>(bs.y1) + (size_t)b * HW * C + c;
+      const T* y = reinterpret_cast<const T*>(bs.y1) + (size_t)b * HW * C + c;
       float z0 = 0.f, z1 = 0.f, x0 = 0.f, x1 = 0.f;
       for (int p = 0; p < HW; ++p) {
-        const uint32_t o = *reinterpret_cast<const uint32_t*>(a + (size_t)p * C + c);
-        const uint32_t yv = *reinterpret_cast<const uint32_t*>(y + (size_t)p * C);
-        const float d0 = lo_bf(o) > 0.f ? g0 : 0.f, d1 = hi_bf(o) > 0.f ? g1 : 0.f;
+        float o0, o1, y0, y1v;
+        ld2(a + (size_t)p * C + c, o0, o1);
+        ld2(y + (size_t)p * C, y0, y1v);
+        const float d0 = o0 > 0.f ? g0 : 0.f, d1 = o1 > 0.f ? g1 : 0.f;
         z0 += d0;
         z1 += d1;
-        x0 += d0 * (lo_bf(yv) - m0) * i0;
-        x1 += d1 * (hi_bf(yv) - m1) * i1;
+        x0 += d0 * (y0 - m0) * i0;
+        x1 += d1 * (y1v - m1) * i1;
       }
       float* dst = bs.part + (size_t)(b & (PSX_STAT_SLOTS - 1)) * 2 * C;
       atomicAdd(dst + c, z0);
@@ -193,19 +201,21 @@ __global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict
 
 // pooled[b][c] = mean over the HW pixels; grid (B, ceil(C / 512)), 2 channels per thread
 // also zeroes zbuf[0, nz) (the split-K logits accumulator)
-__global__ __launch_bounds__(256) void head_pool_kernel(const uint16_t* __restrict__ act, int HW, int C,
+template <typename T>
+__global__ __launch_bounds__(256) void head_pool_kernel(const T* __restrict__ act, int HW, int C,
                                                         float* __restrict__ pooled, float* __restrict__ zbuf,
                                                         long nz) {
   const long gt = ((long)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x;
   for (long i = gt; i < nz; i += (long)gridDim.x * gridDim.y * 256) zbuf[i] = 0.f;
   const int b = blockIdx.x, c = blockIdx.y * 512 + 2 * threadIdx.x;
   if (c >= C) return;
-  const uint16_t* a = act + (size_t)b * HW * C + c;
+  const T* a = act + (size_t)b * HW * C + c;
   float s0 = 0.f, s1 = 0.f;
   for (int p = 0; p < HW; ++p) {
-    const uint32_t v = *reinterpret_cast<const uint32_t*>(a + (size_t)p * C);
-    s0 += lo_bf(v);
-    s1 += hi_bf(v);
+    float v0, v1;
+    ld2(a + (size_t)p * C, v0, v1);
+    s0 += v0;
+    s1 += v1;
   }
   const float inv = 1.f / (float)HW;
   *reinterpret_cast<float2*>(pooled + (size_t)b * C + c) = make_float2(s0 * inv, s1 * inv);
@@ -214,11 +224,11 @@ __global__ __launch_bounds__(256) void head_pool_kernel(const uint16_t* __restri
 // out[m][n] = sum_k A[m][k] * B(k, n), fp32, 32 x 64 tile per workgroup (2 x 4 per thread), k in
 // chunks of 32 through LDS. BT: B(k, n) = Bm[n][k] (FC rows: logits); else Bm[k][n] (dpooled).
 // EPI 0: out += partial (+ bias[n] from split 0), fp32 atomics, split-K over blockIdx.z (out
-// zeroed beforehand); EPI 1: dact bf16 = out / HW written to all HW pixels of sample m (no split).
-template <bool BT, int EPI>
+// zeroed beforehand); EPI 1: dact (T) = out / HW written to all HW pixels of sample m (no split).
+template <bool BT, int EPI, typename T = uint16_t>
 __global__ __launch_bounds__(256) void head_gemm_kernel(const float* __restrict__ A, const float* __restrict__ Bm,
                                                         int M, int N, int Kd, const float* __restrict__ bias,
-                                                        float* __restrict__ out, uint16_t* __restrict__ dact,
+                                                        float* __restrict__ out, T* __restrict__ dact,
                                                         int HW) {
   __shared__ float As[32][33];
   __shared__ float Bs[32][68];
@@ -265,10 +275,12 @@ __global__ __launch_bounds__(256) void head_gemm_kernel(const float* __restrict_
         if (n + j < N) atomicAdd(out + (size_t)m * N + n + j, acc[i][j] + (blockIdx.z == 0 ? bias[n + j] : 0.f));
     } else if (n + 3 < N) {  // N (channels) is a multiple of 64 on this path
       const float inv = 1.f / (float)HW;
-      u32x2 v;
-      v[0] = pack_bf2(acc[i][0] * inv, acc[i][1] * inv);
-      v[1] = pack_bf2(acc[i][2] * inv, acc[i][3] * inv);
-      for (int p = 0; p < HW; ++p) *reinterpret_cast<u32x2*>(dact + ((size_t)m * HW + p) * N + n) = v;
+      for (int p = 0; p < HW; ++p) {
+        float v0 = acc[i][0] * inv, v1 = acc[i][1] * inv, v2 = acc[i][2] * inv, v3 = acc[i][3] * inv;
+        T* d = dact + ((size_t)m * HW + p) * N + n;
+        st2(d, v0, v1);
+        st2(d + 2, v2, v3);
+      }
     }
   }
 }
@@ -351,15 +363,14 @@ __global__ __launch_bounds__(256) void head_wgrad_small_kernel(const float* __re
 
 using namespace psx;
 
-extern "C" {
+namespace {
 
-// bst (nullable, fused path only, needs dact): the BN-backward sums of the consumed layer.
-// Returns 1 when they were produced (the caller then skips its bn_bwd_reduce), 0 otherwise.
-int psx_head_fwd_bwd(const void* act, int B, int HW, int C, const float* fcw, const float* fcb, int K,
-                     const int* labels, float* pooled, float* dlogits, void* dact, float* loss, int* correct,
-                     const HeadBnStats* bst, hipStream_t st) {
+template <typename T>
+int head_fwd_bwd_t(const void* act, int B, int HW, int C, const float* fcw, const float* fcb, int K,
+                   const int* labels, float* pooled, float* dlogits, void* dact, float* loss, int* correct,
+                   const HeadBnStats* bst, hipStream_t st) {
   if ((long)K * C > (1L << 18) && C % 64 == 0 && pooled && dlogits) {  // large head: split path
-    hipLaunchKernelGGL(head_pool_kernel, dim3(B, (C + 511) / 512), dim3(256), 0, st, (const uint16_t*)act, HW, C,
+    hipLaunchKernelGGL(head_pool_kernel<T>, dim3(B, (C + 511) / 512), dim3(256), 0, st, (const T*)act, HW, C,
                        pooled, dlogits, (long)B * K);
     // logits: split-K over the C-long dot products (a 2048 x 1000 head at B = 128 is only 64
     // output tiles; 16 splits of 128 channels fill the chip)
@@ -369,8 +380,8 @@ int psx_head_fwd_bwd(const void* act, int B, int HW, int C, const float* fcw, co
     hipLaunchKernelGGL(head_softmax_kernel, dim3(B), dim3(64), 0, st, dlogits, K, labels, loss, correct,
                        1.f / (float)B, dact ? 1 : 0);
     if (dact)
-      hipLaunchKernelGGL((head_gemm_kernel<false, 1>), dim3(C / 64, (B + 31) / 32), dim3(256), 0, st, dlogits, fcw,
-                         B, C, K, (const float*)nullptr, (float*)nullptr, (uint16_t*)dact, HW);
+      hipLaunchKernelGGL((head_gemm_kernel<false, 1, T>), dim3(C / 64, (B + 31) / 32), dim3(256), 0, st, dlogits,
+                         fcw, B, C, K, (const float*)nullptr, (float*)nullptr, (T*)dact, HW);
     const int e = (int)hipGetLastError();
     return e ? -e : 0;
   }
@@ -378,13 +389,28 @@ int psx_head_fwd_bwd(const void* act, int B, int HW, int C, const float* fcw, co
   const size_t lds = (size_t)(C + K + 64) * sizeof(float);
   const HeadBnStats bs = (bst && dact) ? *bst : HeadBnStats{};
   if (dact)
-    hipLaunchKernelGGL(head_kernel<true>, dim3(B), dim3(256), lds, st, (const uint16_t*)act, HW, C, fcw, fcb, K,
-                       labels, pooled, dlogits, (uint16_t*)dact, loss, correct, 1.f / (float)B, bs);
+    hipLaunchKernelGGL((head_kernel<T, true>), dim3(B), dim3(256), lds, st, (const T*)act, HW, C, fcw, fcb, K,
+                       labels, pooled, dlogits, (T*)dact, loss, correct, 1.f / (float)B, bs);
   else
-    hipLaunchKernelGGL(head_kernel<false>, dim3(B), dim3(256), lds, st, (const uint16_t*)act, HW, C, fcw, fcb, K,
-                       labels, pooled, dlogits, (uint16_t*)nullptr, loss, correct, 1.f / (float)B, bs);
+    hipLaunchKernelGGL((head_kernel<T, false>), dim3(B), dim3(256), lds, st, (const T*)act, HW, C, fcw, fcb, K,
+                       labels, pooled, dlogits, (T*)nullptr, loss, correct, 1.f / (float)B, bs);
   const int e = (int)hipGetLastError();
   return e ? -e : (bs.part ? 1 : 0);
+}
+
+}  // namespace
+
+extern "C" {
+
+// bst (nullable, fused path only, needs dact): the BN-backward sums of the consumed layer.
+// Returns 1 when they were produced (the caller then skips its bn_bwd_reduce), 0 otherwise.
+// f32: act / dact (and bst's operands) are fp32 instead of bf16.
+int psx_head_fwd_bwd(const void* act, int B, int HW, int C, const float* fcw, const float* fcb, int K,
+                     const int* labels, float* pooled, float* dlogits, void* dact, float* loss, int* correct,
+                     const HeadBnStats* bst, int f32, hipStream_t st) {
+  return f32 ? head_fwd_bwd_t<float>(act, B, HW, C, fcw, fcb, K, labels, pooled, dlogits, dact, loss, correct, bst, st)
+             : head_fwd_bwd_t<uint16_t>(act, B, HW, C, fcw, fcb, K, labels, pooled, dlogits, dact, loss, correct, bst,
+                                        st);
 }
 
 int psx_head_wgrad(const float* dlogits, const float* pooled, int B, int K, int C, void* dw, void* db, float gscale,

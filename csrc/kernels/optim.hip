@@ -122,6 +122,12 @@ struct UnpackDesc {
 
 PSX_DEV uint16_t to_bf(const float* s, size_t i) { return f2bf(s[i]); }
 PSX_DEV uint16_t to_bf(const uint16_t* s, size_t i) { return s[i]; }
+// operand element of type DT from the source (bf16 bits from fp32 / bf16, or fp32 from fp32)
+template <typename DT, typename ST>
+PSX_DEV DT to_op(const ST* s, size_t i) {
+  if constexpr (sizeof(DT) == 2) return to_bf(s, i);
+  else return s[i];
+}
 
 // Flat-grid unpack: one workgroup per (conv, 64 oc x 64 c tile, chunk of <= 3 taps), staged
 // through LDS. Every global store is a 4-byte pair and every (oc, tap) row of
@@ -131,22 +137,30 @@ PSX_DEV uint16_t to_bf(const uint16_t* s, size_t i) { return s[i]; }
 // never needs fp32 conv weights.
 constexpr int kUnpackTile = 64;
 
-template <int NT, typename ST>
+PSX_DEV void store_pair(uint16_t* p, uint16_t a, uint16_t b) {
+  *reinterpret_cast<uint32_t*>(p) = (uint32_t)a | ((uint32_t)b << 16);
+}
+PSX_DEV void store_pair(float* p, float a, float b) { *reinterpret_cast<float2*>(p) = make_float2(a, b); }
+
+// DT: operand type (bf16 bits, or fp32 for the fp32 path). The (oc, tap) rows of wf and (c, tap)
+// rows of wd are written as element pairs (4-byte bf16 / 8-byte fp32 stores).
+template <int NT, typename ST, typename DT>
 PSX_DEV void unpack_chunk(const UnpackDesc& d, const ST* __restrict__ src, int oc0, int c0, int tap0, int RS,
-                          uint16_t* __restrict__ wbuf, uint16_t* tile) {
-  constexpr int PITCH = 64 * NT + 2;  // halves; odd dword pitch -> oc-strided reads hit distinct banks
+                          DT* __restrict__ wbuf, DT* tile) {
+  // odd dword pitch -> oc-strided reads hit distinct banks
+  constexpr int PITCH = 64 * NT + (sizeof(DT) == 2 ? 2 : 1);
   const int nc_src = min(64, d.Cin - c0);  // real input channels in this tile (<= 0: all padding)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // stage tile[oc][c*NT + tp] = W[oc0+oc][c0+c][tap0+tp]: all 16*NT loads of a lane in flight
   // before the first LDS write (a load -> wait -> write loop per row was latency-bound)
-  uint16_t v[16][NT];
+  DT v[16][NT];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int oc = wv + 4 * i;
     const bool ok = oc0 + oc < d.OC && lane < nc_src;
     const ST* p = src + ((size_t)(oc0 + oc) * d.Cin + c0 + lane) * RS + tap0;
 #pragma unroll
-    for (int tp = 0; tp < NT; ++tp) v[i][tp] = ok ? to_bf(p, tp) : (uint16_t)0;
+    for (int tp = 0; tp < NT; ++tp) v[i][tp] = ok ? to_op<DT>(p, tp) : (DT)0;
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i)
@@ -157,18 +171,16 @@ PSX_DEV void unpack_chunk(const UnpackDesc& d, const ST* __restrict__ src, int o
   // wf[oc][tap*Cp + c]
   for (int q = wv * 2 + half; q < 64 * NT; q += 8) {
     const int oc = q / NT, tp = q - oc * NT;
-    if (oc0 + oc < d.OC && c0 + l2 < d.Cp) {
-      const uint32_t v = (uint32_t)tile[oc * PITCH + l2 * NT + tp] | ((uint32_t)tile[oc * PITCH + (l2 + 1) * NT + tp] << 16);
-      *reinterpret_cast<uint32_t*>(wbuf + d.wf_off + (size_t)(oc0 + oc) * d.Kg + (tap0 + tp) * d.Cp + c0 + l2) = v;
-    }
+    if (oc0 + oc < d.OC && c0 + l2 < d.Cp)
+      store_pair(wbuf + d.wf_off + (size_t)(oc0 + oc) * d.Kg + (tap0 + tp) * d.Cp + c0 + l2,
+                 tile[oc * PITCH + l2 * NT + tp], tile[oc * PITCH + (l2 + 1) * NT + tp]);
   }
   if (d.wd_off >= 0) {  // wd[c][tap*OC + oc]
     for (int q = wv * 2 + half; q < 64 * NT; q += 8) {
       const int c = q / NT, tp = q - c * NT;
-      if (oc0 + l2 < d.OC && c0 + c < d.Cp) {
-        const uint32_t v = (uint32_t)tile[l2 * PITCH + c * NT + tp] | ((uint32_t)tile[(l2 + 1) * PITCH + c * NT + tp] << 16);
-        *reinterpret_cast<uint32_t*>(wbuf + d.wd_off + (size_t)(c0 + c) * d.Kgd + (tap0 + tp) * d.OC + oc0 + l2) = v;
-      }
+      if (oc0 + l2 < d.OC && c0 + c < d.Cp)
+        store_pair(wbuf + d.wd_off + (size_t)(c0 + c) * d.Kgd + (tap0 + tp) * d.OC + oc0 + l2,
+                   tile[l2 * PITCH + c * NT + tp], tile[(l2 + 1) * PITCH + c * NT + tp]);
     }
   }
 }
@@ -187,10 +199,10 @@ struct SmallScatter {
 };
 constexpr int kScatterPerBlock = 2048;
 
-template <typename ST>
+template <typename ST, typename DT>
 __global__ __launch_bounds__(256) void param_unpack_tiles_kernel(const ST* __restrict__ src_all,
                                                                  const UnpackDesc* __restrict__ descs, int ndesc,
-                                                                 uint16_t* __restrict__ wbuf, int ntiles,
+                                                                 DT* __restrict__ wbuf, int ntiles,
                                                                  SmallScatter sc) {
   if ((int)blockIdx.x >= ntiles) {  // scatter workgroups (block-uniform exit)
     const long base = (long)(blockIdx.x - ntiles) * kScatterPerBlock;
@@ -204,7 +216,7 @@ __global__ __launch_bounds__(256) void param_unpack_tiles_kernel(const ST* __res
     }
     return;
   }
-  __shared__ uint16_t tile[64 * (64 * 3 + 2)];
+  __shared__ DT tile[64 * (64 * 3 + 2)];
   __shared__ int first_tile[256];
   // which conv owns this workgroup: all descs' tile0 fetched in parallel
   for (int k = threadIdx.x; k < 256; k += 256) first_tile[k] = k < ndesc ? descs[k].tile0 : 0x7fffffff;
@@ -221,9 +233,9 @@ __global__ __launch_bounds__(256) void param_unpack_tiles_kernel(const ST* __res
   const int oc0 = (t / n_c) * kUnpackTile, c0 = (t % n_c) * kUnpackTile;
   const ST* src = src_all + d.src_off;
   const int nt = min(3, RS - tap0);
-  if (nt == 3) unpack_chunk<3>(d, src, oc0, c0, tap0, RS, wbuf, tile);
-  else if (nt == 2) unpack_chunk<2>(d, src, oc0, c0, tap0, RS, wbuf, tile);
-  else unpack_chunk<1>(d, src, oc0, c0, tap0, RS, wbuf, tile);
+  if (nt == 3) unpack_chunk<3, ST, DT>(d, src, oc0, c0, tap0, RS, wbuf, tile);
+  else if (nt == 2) unpack_chunk<2, ST, DT>(d, src, oc0, c0, tap0, RS, wbuf, tile);
+  else unpack_chunk<1, ST, DT>(d, src, oc0, c0, tap0, RS, wbuf, tile);
 }
 
 // One workgroup per (32 oc x 32 c) tile of one conv (blockIdx.y = conv). For every tap the
@@ -353,19 +365,24 @@ int psx_param_unpack(const float* arena, const void* descs, int ndesc, void* wbu
 // Flat-grid unpack (one workgroup per 32x32 tile of every conv; ntiles = sum of the tiles, each
 // desc's tile0 = its first tile). src_bf16: the source is a bf16 image instead of the fp32 arena.
 // sc_src/sc_idx/sc_n/sc_dst/sc_gather/sc_sidx: optional SmallScatter (sc_n = 0: none), see above.
+// f32: fp32 operands (the fp32 compute path; source must be the fp32 arena).
 int psx_param_unpack_tiles(const void* src, int src_bf16, const void* descs, int ndesc, int ntiles, void* wbuf,
                            const float* sc_src, const long* sc_idx, long sc_n, float* sc_dst, int sc_gather,
-                           const long* sc_sidx, hipStream_t st) {
+                           const long* sc_sidx, int f32, hipStream_t st) {
   if (ntiles <= 0 || ndesc <= 0) return 0;
   if (ndesc > 256) return (int)hipErrorInvalidValue;  // the kernel's LDS desc table
   const SmallScatter sc{sc_src, sc_idx, sc_n > 0 ? sc_n : 0, sc_dst, sc_gather, sc_sidx};
   const long nsb = (sc.n + kScatterPerBlock - 1) / kScatterPerBlock;
   const dim3 grid((unsigned)(ntiles + nsb));
-  if (src_bf16)
-    hipLaunchKernelGGL(param_unpack_tiles_kernel<uint16_t>, grid, dim3(256), 0, st, (const uint16_t*)src,
+  if (f32 && src_bf16) return (int)hipErrorInvalidValue;  // fp32 operands come from fp32 weights
+  if (f32)
+    hipLaunchKernelGGL((param_unpack_tiles_kernel<float, float>), grid, dim3(256), 0, st, (const float*)src,
+                       (const UnpackDesc*)descs, ndesc, (float*)wbuf, ntiles, sc);
+  else if (src_bf16)
+    hipLaunchKernelGGL((param_unpack_tiles_kernel<uint16_t, uint16_t>), grid, dim3(256), 0, st, (const uint16_t*)src,
                        (const UnpackDesc*)descs, ndesc, (uint16_t*)wbuf, ntiles, sc);
   else
-    hipLaunchKernelGGL(param_unpack_tiles_kernel<float>, grid, dim3(256), 0, st, (const float*)src,
+    hipLaunchKernelGGL((param_unpack_tiles_kernel<float, uint16_t>), grid, dim3(256), 0, st, (const float*)src,
                        (const UnpackDesc*)descs, ndesc, (uint16_t*)wbuf, ntiles, sc);
   return (int)hipGetLastError();
 }

@@ -1,16 +1,17 @@
 // 3x3 / stride-2 / pad-1 max-pool of the ResNet-50 ImageNet stem (torchvision
-// nn.MaxPool2d(3, 2, 1)), NHWC bf16, forward + backward.
+// nn.MaxPool2d(3, 2, 1)), NHWC bf16 or fp32 (template T), forward + backward.
 //
 // Forward keeps, per output element, the window position (0..8) of its maximum in a uint8
 // side buffer; backward is a *gather* over the (at most 2x2) windows covering each input
 // pixel, so every input gradient is written exactly once (no atomics, deterministic, and the
 // same first-max tie rule as PyTorch's CPU/GPU max-pool).
-// One thread = 8 channels (one 16-byte vector) of one pixel.
+// One thread = 8 channels of one pixel.
 #include "common.hpp"
 
 namespace psx {
 
-__global__ __launch_bounds__(256) void maxpool3s2_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool3s2_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                              uint8_t* __restrict__ arg, int B, int H, int W, int C,
                                                              int OH, int OW) {
   const int cv = C >> 3;
@@ -37,10 +38,11 @@ __global__ __launch_bounds__(256) void maxpool3s2_fwd_kernel(const uint16_t* __r
       for (int s = 0; s < 3; ++s) {
         const int iw = ow * 2 - 1 + s;
         if ((unsigned)iw >= (unsigned)W) continue;
-        const u32x4 v = *reinterpret_cast<const u32x4*>(x + (((size_t)b * H + ih) * W + iw) * C + c8 * 8);
+        float v[8];
+        ld8(x + (((size_t)b * H + ih) * W + iw) * C + c8 * 8, v);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float f = (e & 1) ? hi_bf(v[e >> 1]) : lo_bf(v[e >> 1]);
+          const float f = v[e];
           if (f > best[e]) {  // strict: first maximum in window order wins
             best[e] = f;
             bi[e] = (uint8_t)(r * 3 + s);
@@ -48,21 +50,19 @@ __global__ __launch_bounds__(256) void maxpool3s2_fwd_kernel(const uint16_t* __r
         }
       }
     }
-    u32x4 o;
     u32x2 ai;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = pack_bf2(best[2 * j], best[2 * j + 1]);
     ai[0] = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
     ai[1] = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
     const size_t off = (size_t)p * C + c8 * 8;
-    *reinterpret_cast<u32x4*>(y + off) = o;
+    st8(y + off, best);
     *reinterpret_cast<u32x2*>(arg + off) = ai;
   }
 }
 
-__global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const uint16_t* __restrict__ dy,
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const T* __restrict__ dy,
                                                              const uint8_t* __restrict__ arg,
-                                                             uint16_t* __restrict__ dx, int B, int H, int W, int C,
+                                                             T* __restrict__ dx, int B, int H, int W, int C,
                                                              int OH, int OW) {
   const int cv = C >> 3;
   const long total = (long)B * H * W * cv;
@@ -91,19 +91,17 @@ __global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const uint16_t* __r
         if ((unsigned)ow >= (unsigned)OW) continue;
         const size_t off = (((size_t)b * OH + oh) * OW + ow) * C + c8 * 8;
         const u32x2 ai = *reinterpret_cast<const u32x2*>(arg + off);
-        const u32x4 g = *reinterpret_cast<const u32x4*>(dy + off);
+        float g[8];
+        ld8(dy + off, g);
         const uint32_t want = (uint32_t)(r * 3 + s);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const uint32_t a = (ai[e >> 2] >> (8 * (e & 3))) & 0xffu;
-          if (a == want) acc[e] += (e & 1) ? hi_bf(g[e >> 1]) : lo_bf(g[e >> 1]);
+          if (a == want) acc[e] += g[e];
         }
       }
     }
-    u32x4 o;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = pack_bf2(acc[2 * j], acc[2 * j + 1]);
-    *reinterpret_cast<u32x4*>(dx + (size_t)p * C + c8 * 8) = o;
+    st8(dx + (size_t)p * C + c8 * 8, acc);
   }
 }
 
@@ -119,19 +117,30 @@ static int pool_grid(long work) {
 
 extern "C" {
 
-int psx_maxpool3s2_fwd(const void* x, void* y, void* arg, int B, int H, int W, int C, hipStream_t st) {
+int psx_maxpool3s2_fwd(const void* x, void* y, void* arg, int B, int H, int W, int C, int f32, hipStream_t st) {
   if (C % 8) return -2;
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
-  hipLaunchKernelGGL(maxpool3s2_fwd_kernel, dim3(pool_grid((long)B * OH * OW * (C / 8))), dim3(256), 0, st,
-                     (const uint16_t*)x, (uint16_t*)y, (uint8_t*)arg, B, H, W, C, OH, OW);
+  const dim3 grid(pool_grid((long)B * OH * OW * (C / 8)));
+  if (f32)
+    hipLaunchKernelGGL(maxpool3s2_fwd_kernel<float>, grid, dim3(256), 0, st, (const float*)x, (float*)y,
+                       (uint8_t*)arg, B, H, W, C, OH, OW);
+  else
+    hipLaunchKernelGGL(maxpool3s2_fwd_kernel<uint16_t>, grid, dim3(256), 0, st, (const uint16_t*)x, (uint16_t*)y,
+                       (uint8_t*)arg, B, H, W, C, OH, OW);
   return (int)hipGetLastError();
 }
 
-int psx_maxpool3s2_bwd(const void* dy, const void* arg, void* dx, int B, int H, int W, int C, hipStream_t st) {
+int psx_maxpool3s2_bwd(const void* dy, const void* arg, void* dx, int B, int H, int W, int C, int f32,
+                       hipStream_t st) {
   if (C % 8) return -2;
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
-  hipLaunchKernelGGL(maxpool3s2_bwd_kernel, dim3(pool_grid((long)B * H * W * (C / 8))), dim3(256), 0, st,
-                     (const uint16_t*)dy, (const uint8_t*)arg, (uint16_t*)dx, B, H, W, C, OH, OW);
+  const dim3 grid(pool_grid((long)B * H * W * (C / 8)));
+  if (f32)
+    hipLaunchKernelGGL(maxpool3s2_bwd_kernel<float>, grid, dim3(256), 0, st, (const float*)dy, (const uint8_t*)arg,
+                       (float*)dx, B, H, W, C, OH, OW);
+  else
+    hipLaunchKernelGGL(maxpool3s2_bwd_kernel<uint16_t>, grid, dim3(256), 0, st, (const uint16_t*)dy,
+                       (const uint8_t*)arg, (uint16_t*)dx, B, H, W, C, OH, OW);
   return (int)hipGetLastError();
 }
 

@@ -18,10 +18,10 @@
 namespace psx {
 
 struct Wgrad2Args {
-  const uint16_t* x;     // NHWC [Nb][IH][IW][IC]
-  const uint16_t* dy;    // NHWC [Nb][OH][OW][OC]
+  const void* x;         // NHWC [Nb][IH][IW][IC] (bf16 bits, or fp32 for wgrad2f_kernel)
+  const void* dy;        // NHWC [Nb][OH][OW][OC]
   float* part;           // [splits][OC][Kg]
-  const uint16_t* zero;  // 16-byte zero page
+  const void* zero;      // 16-byte zero page
   int IH, IW, IC, OC, R, S, pad, stride, Kg, log2_icc, npix;
   FastDiv div_ohw, div_ow, div_s;
   int n_k_tiles, n_oc_tiles, splits, steps_per_split;  // steps of 64 pixels
@@ -88,13 +88,16 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(Wgrad2Args a) {
   }
   const int OW = a.div_ow.d;
 
+  const uint16_t* const xg = (const uint16_t*)a.x;
+  const uint16_t* const dyg = (const uint16_t*)a.dy;
+  const uint16_t* const zero = (const uint16_t*)a.zero;
   auto issue = [&](int st, int stage) {
     unsigned char* base = smem + stage * STAGE;
     const int p0 = pbeg + st * 64;
 #pragma unroll
     for (int i = 0; i < LX; ++i) {
       const int pix = p0 + xrow[i];
-      const uint16_t* src = a.zero;
+      const uint16_t* src = zero;
       if (pix < a.npix && xtap_ok[i]) {
         const int n = fdiv(pix, a.div_ohw);
         const int rem = pix - n * a.div_ohw.d;
@@ -102,14 +105,14 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(Wgrad2Args a) {
         const int ow = rem - oh * OW;
         const int ih = oh * a.stride - a.pad + xtap_r[i], iw = ow * a.stride - a.pad + xtap_s[i];
         if ((unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW)
-          src = a.x + ((size_t)(n * a.IH + ih) * a.IW + iw) * a.IC + xc0[i];
+          src = xg + ((size_t)(n * a.IH + ih) * a.IW + iw) * a.IC + xc0[i];
       }
       glds16(src, base + (i * 4 + wid) * 1024);
     }
 #pragma unroll
     for (int i = 0; i < LD; ++i) {
       const int pix = p0 + drow[i];
-      const uint16_t* src = pix < a.npix ? a.dy + (size_t)pix * a.OC + oc0 + dchunk[i] * 8 : a.zero;
+      const uint16_t* src = pix < a.npix ? dyg + (size_t)pix * a.OC + oc0 + dchunk[i] * 8 : zero;
       glds16(src, base + XT + (i * 4 + wid) * 1024);
     }
   };
@@ -178,6 +181,155 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(Wgrad2Args a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// wgrad2f: the fp32 weight gradient (the reference's training precision). Same GEMM, grid and
+// LDS-DMA ring as wgrad2_kernel, fp32 operands: a stage holds 32 pixels x (BR + BC) fp32 columns
+// and the reduction runs on v_mfma_f32_16x16x4_f32 (exact f32). Its A/B fragments hold ONE
+// element per lane (lane l: column l & 15 of pixel 4s + (l >> 4)), so the pixel-major tiles need
+// no transposed read: one ds_read_b32 per operand per MFMA. Rows are 256/512 B (a multiple of
+// the 32 banks), so the 16-byte chunk index is XOR-ed with bit 2 on odd rows (applied to the DMA
+// source address, the LDS destination stays lane-linear): the two rows a 32-lane read group
+// touches then sit 16 banks apart, conflict-free.
+template <int BR, int BC, int NS>
+__global__ __launch_bounds__(256) void wgrad2f_kernel(Wgrad2Args a) {
+  constexpr int PS = 32;                                  // pixels per stage
+  constexpr int XROWB = BR * 4, DROWB = BC * 4;           // bytes per pixel row
+  constexpr int XCPR = XROWB / 16, DCPR = DROWB / 16;     // 16-byte chunks per row
+  constexpr int XRPI = 64 / XCPR, DRPI = 64 / DCPR;       // rows per DMA instruction
+  constexpr int LX = PS / XRPI / 4, LD = PS / DRPI / 4;   // DMA instructions per wave per stage
+  constexpr int XT = PS * XROWB, DT = PS * DROWB, STAGE = XT + DT;
+  constexpr int MT = BR / 32, NT = BC / 32;
+  static_assert(LX >= 1 && LD >= 1, "tile too narrow for the 32-pixel stage");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntile = a.n_k_tiles * a.n_oc_tiles;
+  const int bid = xcd_remap(blockIdx.x, ntile * a.splits);
+  const int split = bid / ntile, t = bid - split * ntile;
+  const int oc_t = t % a.n_oc_tiles, k_t = t / a.n_oc_tiles;
+  const int k0 = k_t * BR, oc0 = oc_t * BC;
+  const int pbeg = split * a.steps_per_split * PS;
+  const int nsteps = min(a.steps_per_split, (a.npix - pbeg + PS - 1) / PS);
+  const float* const xg = (const float*)a.x;
+  const float* const dyg = (const float*)a.dy;
+  const float* const zero = (const float*)a.zero;
+
+  int xrow[LX], xtap_r[LX], xtap_s[LX], xc0[LX];
+  bool xtap_ok[LX];
+#pragma unroll
+  for (int i = 0; i < LX; ++i) {
+    const int row = (i * 4 + wid) * XRPI + lane / XCPR;
+    const int c = (lane % XCPR) ^ ((row & 1) << 2);  // logical chunk of this lane's slot
+    xrow[i] = row;
+    const int gk = (k0 >> 2) + c;
+    const int tap = gk >> a.log2_icc;
+    xc0[i] = (gk & ((1 << a.log2_icc) - 1)) << 2;
+    xtap_ok[i] = tap < a.R * a.S;
+    const int r = fdiv(tap, a.div_s);
+    xtap_r[i] = r;
+    xtap_s[i] = tap - r * a.S;
+  }
+  int drow[LD], dchunk[LD];
+#pragma unroll
+  for (int i = 0; i < LD; ++i) {
+    const int row = (i * 4 + wid) * DRPI + lane / DCPR;
+    drow[i] = row;
+    dchunk[i] = (lane % DCPR) ^ ((row & 1) << 2);
+  }
+  const int OW = a.div_ow.d;
+
+  auto issue = [&](int st, int stage) {
+    unsigned char* base = smem + stage * STAGE;
+    const int p0 = pbeg + st * PS;
+#pragma unroll
+    for (int i = 0; i < LX; ++i) {
+      const int pix = p0 + xrow[i];
+      const float* src = zero;
+      if (pix < a.npix && xtap_ok[i]) {
+        const int n = fdiv(pix, a.div_ohw);
+        const int rem = pix - n * a.div_ohw.d;
+        const int oh = fdiv(rem, a.div_ow);
+        const int ow = rem - oh * OW;
+        const int ih = oh * a.stride - a.pad + xtap_r[i], iw = ow * a.stride - a.pad + xtap_s[i];
+        if ((unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW)
+          src = xg + ((size_t)(n * a.IH + ih) * a.IW + iw) * a.IC + xc0[i];
+      }
+      glds16(src, base + (i * 4 + wid) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < LD; ++i) {
+      const int pix = p0 + drow[i];
+      const float* src = pix < a.npix ? dyg + (size_t)pix * a.OC + oc0 + dchunk[i] * 4 : zero;
+      glds16(src, base + XT + (i * 4 + wid) * 1024);
+    }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // per-lane fragment byte offsets within a row (odd rows: chunk bit 2 flipped)
+  const int kq = lane >> 4, col = lane & 15;
+  int aoff[MT], boff[NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int c = wm * (BR / 2) + m * 16 + col;
+    aoff[m] = (((c >> 2) ^ ((kq & 1) << 2)) << 4) + ((c & 3) << 2);
+  }
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int c = wn * (BC / 2) + n * 16 + col;
+    boff[n] = (((c >> 2) ^ ((kq & 1) << 2)) << 4) + ((c & 3) << 2);
+  }
+
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < nsteps) issue(i, i);
+  int stage = 0;
+  for (int st = 0; st < nsteps; ++st) {
+    const int ahead = min(NS - 2, nsteps - 1 - st);
+    if (ahead >= NS - 2)
+      wait_vmcnt<(NS - 2) * (LX + LD)>();
+    else if (NS > 3 && ahead == 1)
+      wait_vmcnt<LX + LD>();
+    else
+      wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (st + NS - 1 < nsteps) issue(st + NS - 1, stage == 0 ? NS - 1 : stage - 1);
+    const unsigned char* X = smem + stage * STAGE;
+    const unsigned char* D = X + XT;
+#pragma unroll
+    for (int s4 = 0; s4 < PS / 4; ++s4) {
+      const int row = 4 * s4 + kq;  // (row & 1) == (kq & 1): the swizzle bit is in aoff / boff
+      float fa[MT], fb[NT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) fa[m] = *reinterpret_cast<const float*>(X + row * XROWB + aoff[m]);
+#pragma unroll
+      for (int n = 0; n < NT; ++n) fb[n] = *reinterpret_cast<const float*>(D + row * DROWB + boff[n]);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[m], fb[n], acc[m][n], 0, 0, 0);
+    }
+    stage = stage == NS - 1 ? 0 : stage + 1;
+  }
+
+  float* part = a.part + (size_t)split * a.OC * a.Kg;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const int k = k0 + wm * (BR / 2) + m * 16 + 4 * (lane >> 4);
+      const int oc = oc0 + wn * (BC / 2) + n * 16 + (lane & 15);
+      *reinterpret_cast<f32x4*>(part + (size_t)oc * a.Kg + k) = acc[m][n];
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // wgrad3: 3x3 / stride 1 / pad 1 with tap reuse. For one kernel row r, the three taps s=0,1,2
 // read the same input row shifted by -1/0/+1 pixels, so one LDS window of 64 input pixels
 // x(n, oh+r-1, ow) (plus one zero row for the row edges) feeds a 192-row output tile
@@ -189,7 +341,7 @@ struct Wgrad3Args {
   const uint16_t* x;
   const uint16_t* dy;
   float* part;
-  const uint16_t* zero;
+  const uint16_t* zero;  // (bf16 only)
   int H, W, log2w, IC, OC, Kg, npix;
   int n_c_tiles, n_oc_tiles, splits, steps_per_split;
 };
@@ -451,6 +603,50 @@ int launch_w3(const Wgrad3Args& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// fp32 plan (wgrad2f_kernel): MFMA-bound, so the model is the f32 MFMA time of a stage
+// (BR*BC/4 cycles per wave at one wave per SIMD; co-resident workgroups share the SIMDs) per
+// round of workgroups + a per-workgroup prologue/epilogue + the split-K partial traffic.
+WPlan wplanf(int OC, int Kg, int npix) {
+  WPlan best{64, 64, 3, 1, 0};
+  double best_t = 1e30;
+  const int steps = (npix + 31) / 32;
+  const int brs[2] = {128, 64}, bcs[2] = {128, 64};
+  for (int ib = 0; ib < 2; ++ib)
+    for (int ic = 0; ic < 2; ++ic) {
+      const int BR = brs[ib], BC = bcs[ic];
+      if (Kg % BR || OC % BC) continue;
+      const int NS = 3;
+      int occ = 163840 / (NS * 32 * (BR + BC) * 4);
+      if (occ > 4) occ = 4;
+      if (occ < 1) continue;
+      const int slots = wg_slots(occ);
+      const long tiles = (long)(Kg / BR) * (OC / BC);
+      const double step_us = (double)(BR * BC) / 4.0 / 2100.0;  // at ~2.1 GHz under load
+      const int smax = steps / 8 > 0 ? steps / 8 : 1;
+      for (int sp = 1; sp <= smax && sp <= 128; ++sp) {
+        const int sps = (steps + sp - 1) / sp;
+        const int spl = (steps + sps - 1) / sps;
+        const long wgs = tiles * spl;
+        const long rounds = (wgs + slots - 1) / slots;
+        const double per_wg = sps * step_us * (double)(wgs < 256L * occ ? (wgs + 255) / 256 : occ) + 3.0;
+        const double t = rounds * per_wg + (spl > 1 ? spl * (double)OC * Kg * 8.0 / 5e6 : 0.0);
+        if (t < best_t) {
+          best_t = t;
+          best = WPlan{BR, BC, NS, spl, sps};
+        }
+      }
+    }
+  return best;
+}
+
+template <int BR, int BC>
+int launch_w2f(const Wgrad2Args& a, hipStream_t st) {
+  const size_t lds = (size_t)3 * 32 * (BR + BC) * 4;
+  hipLaunchKernelGGL((wgrad2f_kernel<BR, BC, 3>), dim3(a.n_k_tiles * a.n_oc_tiles * a.splits), dim3(256), lds, st,
+                     a);
+  return (int)hipGetLastError();
+}
+
 int ilog2w(int v) {
   int l = 0;
   while ((1 << l) < v) ++l;
@@ -462,14 +658,15 @@ int ilog2w(int v) {
 extern "C" {
 
 // Returns the split count (query with part == nullptr); partials need splits*OC*Kg floats.
+// f32: x / dy are fp32 (wgrad2f_kernel) instead of bf16.
 int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero, int Nb, int H, int W, int IC, int OC,
-                    int R, int S, int stride, int pad, int Kg, hipStream_t st) {
+                    int R, int S, int stride, int pad, int Kg, int f32, hipStream_t st) {
   Wgrad2Args a{};
   const int OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
-  a.x = (const uint16_t*)x;
-  a.dy = (const uint16_t*)dy;
+  a.x = x;
+  a.dy = dy;
   a.part = part;
-  a.zero = (const uint16_t*)zero;
+  a.zero = zero;
   a.IH = H; a.IW = W; a.IC = IC; a.OC = OC; a.R = R; a.S = S; a.pad = pad; a.stride = stride;
   a.Kg = Kg;
   a.log2_icc = ilog2w(IC / 8);
@@ -478,6 +675,25 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
   a.div_ow = make_fastdiv(OW);
   a.div_s = make_fastdiv(S);
   if (OC % 64 || Kg % 64) return -2;
+  if (f32) {
+    a.log2_icc = ilog2w(IC / 4);
+    if (IC % 4 || (IC & (IC - 1))) return -2;
+    WPlan p = wplanf(OC, Kg, a.npix);
+    if (const char* e = getenv("PSX_WGF_BR")) p.BR = atoi(e);
+    if (const char* e = getenv("PSX_WGF_BC")) p.BC = atoi(e);
+    if (Kg % p.BR || OC % p.BC) return -2;
+    a.n_k_tiles = Kg / p.BR;
+    a.n_oc_tiles = OC / p.BC;
+    a.splits = p.splits;
+    a.steps_per_split = p.sps;
+    if (!part) return p.splits;
+    int e;
+    if (p.BR == 128 && p.BC == 128) e = launch_w2f<128, 128>(a, st);
+    else if (p.BR == 128) e = launch_w2f<128, 64>(a, st);
+    else if (p.BC == 128) e = launch_w2f<64, 128>(a, st);
+    else e = launch_w2f<64, 64>(a, st);
+    return e ? -e : p.splits;
+  }
   // 3x3 stride-1 layers with power-of-two rows: tap-reuse kernel (PSX_WG3=0 disables)
   const char* w3env = getenv("PSX_WG3");
   if (R == 3 && S == 3 && stride == 1 && pad == 1 && IC % 64 == 0 && (W & (W - 1)) == 0 && (H & (H - 1)) == 0 &&
@@ -493,7 +709,7 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
     if (OC % p.BC) return -2;
     if (!part) return p.splits;
     Wgrad3Args b{};
-    b.x = a.x; b.dy = a.dy; b.part = part; b.zero = a.zero;
+    b.x = (const uint16_t*)a.x; b.dy = (const uint16_t*)a.dy; b.part = part; b.zero = (const uint16_t*)a.zero;
     b.H = H; b.W = W; b.log2w = ilog2w(W); b.IC = IC; b.OC = OC; b.Kg = Kg; b.npix = a.npix;
     b.n_c_tiles = IC / 64; b.n_oc_tiles = OC / p.BC; b.splits = p.splits; b.steps_per_split = p.sps;
     const int e = p.BC == 128 ? (p.NS == 6 ? launch_w3<128, 6>(b, st) : launch_w3<128, 3>(b, st))

@@ -5,14 +5,16 @@ src/workers/worker.py:333-348 — zero_grad, forward, CrossEntropyLoss, backward
 ``evaluate_model`` (worker.py:313-331). Instead of autograd over ``nn.Module``s it runs an
 explicit, statically-scheduled forward + backward over pre-allocated HBM buffers:
 
-* activations NHWC bf16; conv = MFMA implicit GEMM (fwd / dgrad / split-K wgrad), BN batch
-  statistics produced by the conv epilogue, BN+ReLU(+residual) fused elementwise passes,
-  fused pool+FC+softmax-xent head;
+* activations NHWC in the compute dtype — bf16 (fast path) or fp32 (``dtype=torch.float32``,
+  the reference's training precision, worker.py:333-348: conv operands and activations fp32,
+  every product on the exact-f32 MFMA ``v_mfma_f32_16x16x4_f32``); conv = MFMA implicit GEMM
+  (fwd / dgrad / split-K wgrad), BN batch statistics produced by the conv epilogue,
+  BN+ReLU(+residual) fused elementwise passes, fused pool+FC+softmax-xent head;
 * gradients are written straight into one flat wire buffer (fp16 codec by default) laid out
   like the trainable-parameter prefix of the parameter arena (models/layout.py), so a push is
   a single RCCL reduce/send of one buffer and the server update one fused kernel;
 * parameters are read from a worker-local fp32 arena (the fetched server state) and unpacked
-  to bf16 implicit-GEMM operands by one table-driven kernel per fetch;
+  to implicit-GEMM operands of the compute dtype by one table-driven kernel per fetch;
 * no allocation, host sync or data-dependent host control flow inside a step, so the whole
   step (unpack + augment + fwd + bwd) is captured once into a HIP graph and replayed.
 
@@ -38,8 +40,8 @@ IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
 
 
-def _pow2_ceil(v: int) -> int:
-    p = 8
+def _pow2_ceil(v: int, lo: int = 8) -> int:
+    p = lo
     while p < v:
         p *= 2
     return p
@@ -62,8 +64,9 @@ class ConvSpec:
     wf_off: int = 0
     wd_off: int = -1
 
-    def finalize(self):
-        self.cp = _pow2_ceil(self.cin)
+    def finalize(self, chunk: int = 8):
+        # input channels padded to a power of two >= one 16-byte chunk (8 bf16 / 4 fp32)
+        self.cp = _pow2_ceil(self.cin, chunk)
         self.kg = -(-(self.k * self.k * self.cp) // 64) * 64
         self.kgd = self.k * self.k * self.cout  # cout % 64 == 0 for every ResNet conv
         assert self.kgd % 64 == 0 and self.cout % 64 == 0, self.name
@@ -157,7 +160,7 @@ class HipResNetEngine:
 
     def __init__(self, model: torch.nn.Module, layout: ParamLayout, batch: int, device="cuda",
                  grad_dtype=torch.float16, in_hw=(32, 32), mean=CIFAR_MEAN, std=CIFAR_STD, bn_eps=1e-5,
-                 bn_momentum=0.1, seed=1234):
+                 bn_momentum=0.1, seed=1234, dtype=torch.bfloat16):
         if not torch.cuda.is_available():
             raise RuntimeError("HipResNetEngine needs an MI355X (torch.cuda / HIP device)")
         K.unpack_desc_size()  # fail loudly right here if the native library is missing
@@ -167,6 +170,11 @@ class HipResNetEngine:
         self.spec = netspec_from_module(model, in_hw)
         self.grad_dtype = grad_dtype
         self.grad_fp16 = grad_dtype == torch.float16
+        # compute dtype of activations and conv operands (fp32 = the reference's precision)
+        if dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError(f"engine dtype {dtype}: bfloat16 or float32")
+        self.dtype = dtype
+        self.f32 = dtype == torch.float32
         self.mean, self.std = mean, std
         self.eps, self.mom = bn_eps, bn_momentum
         self.seed = seed
@@ -174,7 +182,10 @@ class HipResNetEngine:
         self.graphs = None
         self.segments = None  # backward split points (set_segments), None = one segment
         # conv kernel generation: 2 = LDS-DMA pipelined + split-K (default), 1 = register-staged
+        # (bf16 only)
         self.conv_impl = int(os.environ.get("PSX_CONV_IMPL", "2"))
+        if self.f32 and self.conv_impl != 2:
+            raise ValueError("the fp32 path runs on the v2 conv kernels (PSX_CONV_IMPL=2)")
         # BN finalize inside the producing launch (csrc/kernels/bnfin.hpp); 0 = separate kernels
         self.fuse_fin = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNFIN", "0") == "1"
         # BN-backward sums from the dgrad epilogue (skips the separate bn_bwd_reduce pass where a
@@ -203,7 +214,8 @@ class HipResNetEngine:
 
     # ------------------------------------------------------------------ allocation
     def _bf(self, *shape):
-        return torch.empty(*shape, dtype=torch.bfloat16, device=self.dev)
+        """An activation buffer of the compute dtype."""
+        return torch.empty(*shape, dtype=self.dtype, device=self.dev)
 
     def _f32(self, *shape):
         return torch.zeros(*shape, dtype=torch.float32, device=self.dev)
@@ -215,7 +227,7 @@ class HipResNetEngine:
         descs = []
         tile0 = 0  # flat grid of param_unpack_tiles: (64x64 (oc, c) tile, chunk of <= 3 taps) units
         for cs in all_convs(sp):
-            cs.finalize()
+            cs.finalize(4 if self.f32 else 8)
             cs.wf_off = off
             off += cs.cout * cs.kg
             if cs.need_dgrad:
@@ -227,7 +239,7 @@ class HipResNetEngine:
                           cs.cp, cs.kg, cs.kgd, tile0))
             tile0 += -(-cs.cout // 64) * -(-cs.cp // 64) * -(-(cs.k * cs.k) // 3)
         self.ntiles = tile0
-        self.wbuf = torch.zeros(off, dtype=torch.bfloat16, device=self.dev)
+        self.wbuf = torch.zeros(off, dtype=self.dtype, device=self.dev)
         dsz = K.unpack_desc_size()
         assert dsz == 3 * 8 + 8 * 4, dsz
         raw = np.zeros(len(descs), dtype=np.dtype([("o", "<i8", 3), ("i", "<i4", 8)]))
@@ -284,7 +296,7 @@ class HipResNetEngine:
             # and conv v2 split-K slabs (stream-ordered on the main stream)
             nonlocal max_wg, max_wp
             if self.conv_impl == 2:
-                s = K.conv_wgrad2_splits(B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
+                s = K.conv_wgrad2_splits(B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg, self.f32)
             else:
                 s = K.conv_wgrad_splits(B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
             cs.splits = s
@@ -292,8 +304,8 @@ class HipResNetEngine:
             cs.wp = s * cs.cout * cs.kg  # fp32 partials of this layer (offset wp_off: _plan_wpart)
             cs.wp_off = 0
             max_wp = max(max_wp, cs.wp)
-            max_wg = max(max_wg, K.conv2_workspace_bytes(B, oh, ow, cs.cout, cs.kg) // 4,
-                         K.conv2_workspace_bytes(B, cs.h, cs.w, cs.cp, cs.kgd) // 4 if cs.need_dgrad else 0)
+            max_wg = max(max_wg, K.conv2_workspace_bytes(B, oh, ow, cs.cout, cs.kg, self.f32) // 4,
+                         K.conv2_workspace_bytes(B, cs.h, cs.w, cs.cp, cs.kgd, self.f32) // 4 if cs.need_dgrad else 0)
 
         track(st)
         h_in = self.a0
@@ -568,7 +580,7 @@ class HipResNetEngine:
         """OIHW master weights -> bf16 implicit-GEMM operands. The source is the fp32 arena, or
         the bf16 weight image ``self.wsrc`` when the fetch delivers one (parallel/codec.py
         WeightWire: the server's apply wrote those bits; identical operands either way)."""
-        if self.unpack_impl == "tap":  # the original per-tap kernel (A/B: PSX_UNPACK_IMPL=tap)
+        if self.unpack_impl == "tap" and not self.f32:  # the original per-tap kernel (A/B: PSX_UNPACK_IMPL=tap)
             K.param_unpack(arena, self.descs, self.ndesc, self.wbuf)
             return
         src = self.wsrc if self.wsrc is not None else arena
@@ -585,6 +597,7 @@ class HipResNetEngine:
         (kernels.param_unpack_tiles), or through ``pre_unpack``, run first inside every captured
         step. Invalidates graphs."""
         if img is not None:
+            assert not self.f32, "the fp32 engine unpacks its operands from the fp32 arena (fetch codec fp32)"
             assert img.dtype == torch.bfloat16 and img.numel() >= self.layout.param_numel
             assert self.unpack_impl != "tap", "the per-tap unpack kernel reads fp32 only"
         assert scatter is None or (img is not None and pre_unpack is None)

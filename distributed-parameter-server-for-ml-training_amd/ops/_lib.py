@@ -46,32 +46,32 @@ _KERNEL_SIGS = {
     "psx_conv_wgrad": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
     "psx_wgrad_reduce": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, f32, vp, i32, vp]),
     "psx_wgrad_reduce_batch": (i32, [i32, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, vp]),
-    "psx_conv2_workspace": (i64, [i32, i32, i32, i32, i32]),
-    "psx_conv_wgrad2": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
-    "psx_conv_fwd2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
-    "psx_conv_dgrad2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
+    "psx_conv2_workspace": (i64, [i32, i32, i32, i32, i32, i32]),
+    "psx_conv_wgrad2": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
+    "psx_conv_fwd2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp]),
+    "psx_conv_dgrad2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp]),
     "psx_bn_finalize": (i32, [vp, i32, i32, f32, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp]),
     "psx_bn_eval_affine": (i32, [i32, vp, vp, vp, vp, f32, vp, vp, vp]),
-    "psx_bn_apply": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp]),
-    "psx_bn_bwd_reduce": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp, vp]),
+    "psx_bn_apply": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
+    "psx_bn_bwd_reduce": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp, i32, vp]),
     "psx_bn_bwd_finalize": (i32, [vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp, f32, i32, vp]),
-    "psx_bn_bwd_apply": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
-    "psx_bn_apply_fin": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp]),
-    "psx_bn_bwd_apply_fin": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
-    "psx_head_fwd_bwd": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "psx_bn_bwd_apply": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp]),
+    "psx_bn_apply_fin": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
+    "psx_bn_bwd_apply_fin": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp]),
+    "psx_head_fwd_bwd": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, i32, vp]),
     "psx_head_wgrad": (i32, [vp, vp, i32, i32, i32, vp, vp, f32, i32, vp]),
     "psx_sgd_apply": (i32, [vp, vp, vp, i64, f32, f32, f32, f32, i32, i32, vp, vp]),
     "psx_grad_aggregate": (i32, [vp, i32, i32, vp, i32, i64, f32, i32, vp]),
     "psx_fp16_pack": (i32, [vp, vp, i64, f32, vp]),
     "psx_fp16_unpack": (i32, [vp, vp, i64, f32, vp]),
     "psx_param_unpack": (i32, [vp, vp, i32, vp, vp]),
-    "psx_param_unpack_tiles": (i32, [vp, i32, vp, i32, i32, vp, vp, vp, i64, vp, i32, vp, vp]),
+    "psx_param_unpack_tiles": (i32, [vp, i32, vp, i32, i32, vp, vp, vp, i64, vp, i32, vp, i32, vp]),
     "psx_unpack_desc_size": (i32, []),
     "psx_synth_gen": (i32, [vp, vp, i32, i32, i32, i32, u32, u32, vp]),
-    "psx_augment": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, u32, vp, i32, vp, vp, vp, i64, vp, i64, vp]),
-    "psx_nchw_to_nhwc": (i32, [vp, vp, i32, i32, i32, i32, i32, vp]),
-    "psx_maxpool3s2_fwd": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
-    "psx_maxpool3s2_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
+    "psx_augment": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, u32, vp, i32, vp, vp, vp, i64, vp, i64, i32, vp]),
+    "psx_nchw_to_nhwc": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, vp]),
+    "psx_maxpool3s2_fwd": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp]),
+    "psx_maxpool3s2_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "psx_topk_workspace_words": (i32, []),
     "psx_topk_payload_words": (i32, [i32]),
     "psx_topk_encode": (i32, [vp, i32, vp, i64, i32, i32, vp, vp, vp]),

@@ -2,9 +2,11 @@
 
 Every function takes pre-allocated torch tensors (device memory), launches on the current
 torch stream (so it composes with torch ops and is captured by ``torch.cuda.CUDAGraph``) and
-raises on a launch error. Layout conventions: NHWC bf16 activations with channels padded to a
-multiple of 8; conv weights as bf16 ``[OC][Kg]`` implicit-GEMM rows (see models/engine.py);
-fp32 parameter arenas; fp16 (wire codec) or fp32 gradient sinks.
+raises on a launch error. Layout conventions: NHWC activations with channels padded to a
+16-byte chunk (8 bf16 / 4 fp32 channels); conv weights as ``[OC][Kg]`` implicit-GEMM rows of the
+activation dtype (see models/engine.py); fp32 parameter arenas; fp16 (wire codec) or fp32
+gradient sinks. The activation dtype (bf16 or fp32, the reference's precision) is taken from
+the tensors: every activation kernel is instantiated for both (csrc/kernels/common.hpp).
 """
 from __future__ import annotations
 
@@ -62,6 +64,15 @@ def conv_dgrad(dy, wd, dx, res, nb, h, w, ic_fwd, oc_fwd, k, stride, pad, kgd, c
 _ZERO_PAGES = {}
 
 
+def is_f32(t) -> int:
+    """1 when an activation / operand tensor is fp32 (the fp32 compute path), 0 for bf16."""
+    if t.dtype == torch.float32:
+        return 1
+    if t.dtype == torch.bfloat16:
+        return 0
+    raise TypeError(f"activation dtype {t.dtype} (expected bfloat16 or float32)")
+
+
 def zero_page(device=None):
     """16-byte-aligned zero block used as the DMA source for conv padding (conv v2)."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -72,8 +83,8 @@ def zero_page(device=None):
     return z
 
 
-def conv2_workspace_bytes(nb, oh, ow, oc, kg) -> int:
-    return int(kernels().psx_conv2_workspace(nb, oh, ow, oc, kg))
+def conv2_workspace_bytes(nb, oh, ow, oc, kg, f32=False) -> int:
+    return int(kernels().psx_conv2_workspace(nb, oh, ow, oc, kg, int(bool(f32))))
 
 
 class BnFin(C.Structure):
@@ -110,7 +121,7 @@ def conv_fwd2(x, wf, y, stats, ws, nb, h, w, ic, oc, k, stride, pad, kg, fin: Bn
     kernel's last workgroup also finalizes the BN layer its statistics feed (bnfin.hpp)."""
     check(kernels().psx_conv_fwd2(ptr(x), ptr(wf), ptr(y), ptr(stats), ptr(zero_page(x.device)), ptr(ws), nb, h, w,
                                   ic, oc, k, k, stride, pad, kg, C.byref(fin) if fin is not None else None,
-                                  stream_ptr()), "conv_fwd2")
+                                  is_f32(x), stream_ptr()), "conv_fwd2")
 
 
 class BwdStatsDesc(C.Structure):
@@ -128,11 +139,11 @@ def conv_dgrad2(dy, wd, dx, res, ws, nb, h, w, ic_fwd, oc_fwd, k, stride, pad, k
     bn_bwd_reduce would compute), so that pass can be skipped."""
     check(kernels().psx_conv_dgrad2(ptr(dy), ptr(wd), ptr(dx), ptr(res), ptr(zero_page(dy.device)), ptr(ws), nb, h,
                                     w, ic_fwd, oc_fwd, k, k, stride, pad, kgd,
-                                    C.byref(bst) if bst is not None else None, stream_ptr()), "conv_dgrad2")
+                                    C.byref(bst) if bst is not None else None, is_f32(dy), stream_ptr()), "conv_dgrad2")
 
 
-def conv_wgrad2_splits(nb, h, w, ic, oc, k, stride, pad, kg) -> int:
-    n = kernels().psx_conv_wgrad2(None, None, None, None, nb, h, w, ic, oc, k, k, stride, pad, kg, None)
+def conv_wgrad2_splits(nb, h, w, ic, oc, k, stride, pad, kg, f32=False) -> int:
+    n = kernels().psx_conv_wgrad2(None, None, None, None, nb, h, w, ic, oc, k, k, stride, pad, kg, int(bool(f32)), None)
     if n <= 0:
         raise RuntimeError(f"conv_wgrad2 split query failed ({n})")
     return n
@@ -141,7 +152,7 @@ def conv_wgrad2_splits(nb, h, w, ic, oc, k, stride, pad, kg) -> int:
 def conv_wgrad2(x, dy, part, nb, h, w, ic, oc, k, stride, pad, kg) -> int:
     """LDS-DMA pipelined weight gradient (csrc/kernels/wgrad_v2.hip) -> fp32 split slabs in part."""
     n = kernels().psx_conv_wgrad2(ptr(x), ptr(dy), ptr(part), ptr(zero_page(x.device)), nb, h, w, ic, oc, k, k,
-                                  stride, pad, kg, stream_ptr())
+                                  stride, pad, kg, is_f32(x), stream_ptr())
     if n <= 0:
         raise RuntimeError(f"conv_wgrad2 failed ({n})")
     return n
@@ -208,7 +219,7 @@ def bn_apply(y, affine, out, c, relu=True, res=None, affine2=None):
     a2 = ptr(affine2)
     check(kernels().psx_bn_apply(ptr(y), ptr(affine), ptr(affine) + 4 * c, ptr(res), a2,
                                  (a2 + 4 * c) if a2 else None, ptr(out), y.numel(), c, mode, int(relu),
-                                 stream_ptr()), "bn_apply")
+                                 is_f32(y), stream_ptr()), "bn_apply")
 
 
 def bn_apply_fin(y, part1, fin1: BnFin, out, c, relu=True, res=None, part2=None, fin2: BnFin | None = None):
@@ -218,12 +229,12 @@ def bn_apply_fin(y, part1, fin1: BnFin, out, c, relu=True, res=None, part2=None,
     mode = 0 if res is None else (1 if part2 is None else 2)
     check(kernels().psx_bn_apply_fin(ptr(y), ptr(part1), C.byref(fin1), ptr(res), ptr(part2),
                                      C.byref(fin2) if fin2 is not None else None, ptr(out), y.numel(), c, mode,
-                                     int(relu), stream_ptr()), "bn_apply_fin")
+                                     int(relu), is_f32(y), stream_ptr()), "bn_apply_fin")
 
 
 def bn_bwd_reduce_T(npix: int, c: int) -> int:
     return kernels().psx_bn_bwd_reduce(None, None, None, None, None, None, None, None, None, npix, c, None, None,
-                                       None)
+                                       0, None)
 
 
 def bn_bwd_reduce(g, o, y1, saved1, part, npix, c, y2=None, saved2=None, fin1: BnBwdFin | None = None,
@@ -234,7 +245,7 @@ def bn_bwd_reduce(g, o, y1, saved1, part, npix, c, y2=None, saved2=None, fin1: B
     T = kernels().psx_bn_bwd_reduce(ptr(g), ptr(o), ptr(y1), ptr(saved1), ptr(saved1) + 4 * c, ptr(y2), s2,
                                     (s2 + 4 * c) if s2 else None, ptr(part), npix, c,
                                     C.byref(fin1) if fin1 is not None else None,
-                                    C.byref(fin2) if fin2 is not None else None, stream_ptr())
+                                    C.byref(fin2) if fin2 is not None else None, is_f32(g), stream_ptr())
     if T <= 0:
         raise RuntimeError(f"bn_bwd_reduce failed ({T})")
     return T
@@ -248,7 +259,7 @@ def bn_bwd_finalize(part, T, ns, which, c, count, gamma, saved, coef, dgamma_ptr
 
 def bn_bwd_apply(g, o, y1, coef1, dx1, c, y2=None, coef2=None, dx2=None, dzout=None):
     check(kernels().psx_bn_bwd_apply(ptr(g), ptr(o), ptr(y1), ptr(coef1), ptr(dx1), ptr(y2), ptr(coef2), ptr(dx2),
-                                     ptr(dzout), g.numel(), c, stream_ptr()), "bn_bwd_apply")
+                                     ptr(dzout), g.numel(), c, is_f32(g), stream_ptr()), "bn_bwd_apply")
 
 
 def bn_bwd_apply_fin(g, o, y1, part, fin1: BnBwdFin, dx1, c, y2=None, fin2: BnBwdFin | None = None, dx2=None,
@@ -257,7 +268,7 @@ def bn_bwd_apply_fin(g, o, y1, part, fin1: BnBwdFin, dx1, c, y2=None, fin2: BnBw
     [STAT_SLOTS][NS][C] slot sums per workgroup; workgroup 0 writes coef and dgamma/dbeta)."""
     check(kernels().psx_bn_bwd_apply_fin(ptr(g), ptr(o), ptr(y1), ptr(part), C.byref(fin1), ptr(dx1), ptr(y2),
                                          C.byref(fin2) if fin2 is not None else None, ptr(dx2), ptr(dzout),
-                                         g.numel(), c, stream_ptr()), "bn_bwd_apply_fin")
+                                         g.numel(), c, is_f32(g), stream_ptr()), "bn_bwd_apply_fin")
 
 
 def head_fwd_bwd(act, b, hw, c, fcw, fcb, k, labels, pooled, dlogits, dact, loss, correct,
@@ -266,7 +277,7 @@ def head_fwd_bwd(act, b, hw, c, fcw, fcb, k, labels, pooled, dlogits, dact, loss
     per-sample head only). Returns whether they were produced."""
     r = kernels().psx_head_fwd_bwd(ptr(act), b, hw, c, ptr(fcw), ptr(fcb), k, ptr(labels), ptr(pooled),
                                    ptr(dlogits), ptr(dact), ptr(loss), ptr(correct),
-                                   C.byref(bst) if bst is not None else None, stream_ptr())
+                                   C.byref(bst) if bst is not None else None, is_f32(act), stream_ptr())
     check(min(r, 0), "head_fwd_bwd")
     return r == 1
 
@@ -288,14 +299,16 @@ def sgd_apply(p, g, lr, gscale=1.0, momentum=0.0, wd=0.0, buf=None, first=False,
 
 
 def maxpool3s2_fwd(x, y, arg):
-    """3x3/s2/p1 max-pool, NHWC bf16; arg (uint8, y's shape) keeps the window argmax."""
+    """3x3/s2/p1 max-pool, NHWC bf16 or fp32; arg (uint8, y's shape) keeps the window argmax."""
     B, H, W, C = x.shape
-    check(kernels().psx_maxpool3s2_fwd(ptr(x), ptr(y), ptr(arg), B, H, W, C, stream_ptr()), "maxpool3s2_fwd")
+    check(kernels().psx_maxpool3s2_fwd(ptr(x), ptr(y), ptr(arg), B, H, W, C, is_f32(x), stream_ptr()),
+          "maxpool3s2_fwd")
 
 
 def maxpool3s2_bwd(dy, arg, dx):
     B, H, W, C = dx.shape
-    check(kernels().psx_maxpool3s2_bwd(ptr(dy), ptr(arg), ptr(dx), B, H, W, C, stream_ptr()), "maxpool3s2_bwd")
+    check(kernels().psx_maxpool3s2_bwd(ptr(dy), ptr(arg), ptr(dx), B, H, W, C, is_f32(dy), stream_ptr()),
+          "maxpool3s2_bwd")
 
 
 def topk_workspace_words() -> int:
@@ -341,7 +354,7 @@ def param_unpack(arena, descs_dev, ndesc, wbuf):
 def param_unpack_tiles(src, descs_dev, ndesc, ntiles, wbuf, scatter=None):
     """Flat-grid unpack (one workgroup per 64x64 tile x 3-tap chunk of every conv). ``src`` is
     the fp32 arena or a bf16 weight image with the same element offsets; descs carry each conv's
-    first tile. ``scatter = (src_f32, idx_i64, dst_f32, gather[, sidx_i64])``: extra workgroups
+    first tile. ``wbuf``'s dtype picks the operand type (bf16, or fp32 from an fp32 source). ``scatter = (src_f32, idx_i64, dst_f32, gather[, sidx_i64])``: extra workgroups
     of the same launch write dst[idx[j]] = src[j] (gather False), src[idx[j]] (gather True) or
     src[sidx[j]] (sidx given: the sharded wire's padded per-rank blocks)."""
     assert src.dtype in (torch.float32, torch.bfloat16), src.dtype
@@ -358,7 +371,8 @@ def param_unpack_tiles(src, descs_dev, ndesc, ntiles, wbuf, scatter=None):
             assert gather or s_src.numel() >= n
         sc = (ptr(s_src), ptr(s_idx), n, ptr(s_dst), int(bool(gather)), ptr(sidx) if sidx is not None else None)
     check(kernels().psx_param_unpack_tiles(ptr(src), int(src.dtype == torch.bfloat16), ptr(descs_dev), ndesc,
-                                           int(ntiles), ptr(wbuf), *sc, stream_ptr()), "param_unpack_tiles")
+                                           int(ntiles), ptr(wbuf), *sc, is_f32(wbuf), stream_ptr()),
+          "param_unpack_tiles")
 
 
 def unpack_desc_size() -> int:
@@ -382,8 +396,8 @@ def augment(img, labels, index, out, out_labels, b, h, w, pad, seed, step_dev, t
     zs += [None, 0] * (2 - len(zs) // 2)
     check(kernels().psx_augment(ptr(img), ptr(labels), ptr(index), ptr(out), ptr(out_labels), b, h, w, pad,
                                 seed & 0xFFFFFFFF, ptr(step_dev), int(train), _F3(*mean), _F3(*std), *zs,
-                                stream_ptr()), "augment")
+                                is_f32(out), stream_ptr()), "augment")
 
 
 def nchw_to_nhwc(x, y, n, c, h, w, cp):
-    check(kernels().psx_nchw_to_nhwc(ptr(x), ptr(y), n, c, h, w, cp, stream_ptr()), "nchw_to_nhwc")
+    check(kernels().psx_nchw_to_nhwc(ptr(x), ptr(y), n, c, h, w, cp, is_f32(y), stream_ptr()), "nchw_to_nhwc")

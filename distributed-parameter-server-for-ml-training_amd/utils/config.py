@@ -52,7 +52,9 @@ class PSConfig:
     #                                sharded: every rank = worker + 1/world of the PS (parallel/sharded.py)
     codec: str = "fp16"            # none (fp32 wire) | fp16 (reference) | topk
     topk_ratio: float = 0.01
-    dtype: str = "bf16"            # compute dtype of the HIP engine
+    # compute dtype of the HIP engine: fp32 = the reference's training precision (worker.py:333-348;
+    # exact-f32 MFMA), bf16 = the fast path (bf16 operands, fp32 accumulation and master weights)
+    dtype: str = "fp32"
     momentum: float = 0.0          # server optimizer (0 = reference plain SGD, server.py:133)
     weight_decay: float = 0.0
     sync_semantics: str = "barrier"  # barrier (wait-for-N) | reference (count-triggered)
@@ -61,9 +63,10 @@ class PSConfig:
     # statistics. bn_sync=True makes workers push their running stats with each gradient push;
     # the server averages them (sync) or blends them 1/W (async). Default off = reference parity.
     bn_sync: bool = False
-    # fetch payload: "bf16conv" = conv weights as bf16 (exactly the bits the HIP engine consumes)
-    # + fp32 for everything else (half the bytes); "fp32" = the reference's full fp32 state.
-    fetch_codec: str = "bf16conv"
+    # fetch payload: "bf16conv" = conv weights as bf16 (exactly the bits the bf16 engine consumes)
+    # + fp32 for everything else (half the bytes); "fp32" = the reference's full fp32 state;
+    # "auto" = fp32 for --dtype fp32, bf16conv for --dtype bf16.
+    fetch_codec: str = "auto"
     # sync rounds stream gradient buckets during the backward pass (parallel/overlap.py).
     # Opt-in: at N=1 it costs ~0.25 ms/step of cross-queue waits (profiles/README.md), which is
     # about the xGMI time it can hide at N=8; the serial round stays the default until measured.
@@ -107,8 +110,14 @@ class PSConfig:
             raise ValueError("--sync-semantics must be barrier or reference")
         if self.staleness_bound < 0:
             raise ValueError("--staleness-bound must be >= 0")
+        if self.dtype not in ("fp32", "bf16"):
+            raise ValueError(f"--dtype must be fp32 or bf16, got {self.dtype!r}")
+        if self.fetch_codec == "auto":
+            self.fetch_codec = "fp32" if self.dtype == "fp32" else "bf16conv"
         if self.fetch_codec not in ("bf16conv", "fp32"):
             raise ValueError("--fetch-codec must be bf16conv or fp32")
+        if self.dtype == "fp32" and self.fetch_codec != "fp32":
+            raise ValueError("--dtype fp32 computes with fp32 weights: --fetch-codec fp32")
         if self.bucket_mb <= 0:
             raise ValueError("--bucket-mb must be > 0")
         if not (0.0 < self.topk_ratio <= 1.0):
@@ -141,12 +150,13 @@ def add_arguments(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     A("--topology", choices=["colocated", "dedicated", "sharded"], default=None)
     A("--codec", choices=["none", "fp16", "topk"], default=None)
     A("--topk-ratio", type=float, default=None)
-    A("--dtype", choices=["bf16"], default=None)
+    A("--dtype", choices=["fp32", "bf16"], default=None,
+      help="worker compute precision: fp32 (reference, default) or bf16 (fast path)")
     A("--momentum", type=float, default=None)
     A("--weight-decay", type=float, default=None)
     A("--sync-semantics", choices=["barrier", "reference"], default=None)
     A("--bn-sync", action="store_true", default=None, help="workers push BN running stats; server averages")
-    A("--fetch-codec", choices=["bf16conv", "fp32"], default=None)
+    A("--fetch-codec", choices=["auto", "bf16conv", "fp32"], default=None)
     A("--overlap", dest="overlap", action="store_true", default=None,
       help="sync mode: stream gradient buckets (reduce/apply/broadcast) during the backward pass")
     A("--no-overlap", dest="overlap", action="store_false", default=None)

@@ -37,7 +37,7 @@ import psx
 from psx.parallel.runner import run_distributed
 from psx.utils.config import PSConfig
 cfg = PSConfig(model="resnet18", batch_size=64, epochs=1, train_samples=2048, eval_every=0, verbose=0, lr=0.1,
-               max_steps=8, mode="async").validate()
+               max_steps=8, mode="async", dtype="bf16").validate()
 res = run_distributed(cfg, log=lambda *a, **k: None)
 s = res["server"]
 print("RESULT " + json.dumps([s["final_param_checksum"], s["global_steps_completed"], s["async_updates"],

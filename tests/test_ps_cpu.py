@@ -290,16 +290,21 @@ def test_weight_wire_roundtrip_matches_fetch_codec():
             assert (lay.view(loc, name) == 7.0).all(), name
         else:
             assert torch.equal(lay.view(loc, name), lay.view(arena, name)), name
-    ok = PSConfig(mode="sync").validate()
-    assert weight_image_enabled(ok)
+    ok = PSConfig(mode="sync", dtype="bf16").validate()
+    assert ok.fetch_codec == "bf16conv" and weight_image_enabled(ok)
+    assert PSConfig().validate().fetch_codec == "fp32"  # default: fp32 compute, fp32 fetch (reference)
+    assert not weight_image_enabled(PSConfig(mode="sync").validate())
     for bad in (dict(mode="async"), dict(sync_steps=2), dict(codec="topk"), dict(fetch_codec="fp32"),
                 dict(overlap=True)):
-        assert not weight_image_enabled(PSConfig(**bad).validate()), bad
+        assert not weight_image_enabled(PSConfig(dtype="bf16", **bad).validate()), bad
+    with pytest.raises(ValueError):
+        PSConfig(dtype="fp32", fetch_codec="bf16conv").validate()
 
 
 @pytest.mark.parametrize("codec", ["fp32", "bf16conv"])
 def test_dist_sync_fetch_codecs(codec):
-    recs, _ = _spawn(2, ["--mode", "sync", "--fetch-codec", codec] + TINY)
+    dt = ["--dtype", "bf16"] if codec == "bf16conv" else []  # bf16 conv weights = the bf16 compute path
+    recs, _ = _spawn(2, ["--mode", "sync", "--fetch-codec", codec] + dt + TINY)
     srv = [r for r in recs if r["type"] == "SERVER_FINAL_METRICS"][0]
     assert srv["global_steps_completed"] > 0
 

@@ -91,7 +91,7 @@ def test_sgd_apply_image_is_bf16_of_result(n, mom):
 
 def _cfg(**kw):
     base = dict(model="resnet18", batch_size=64, epochs=1, train_samples=2048, eval_every=0, verbose=0, lr=0.1,
-                max_steps=6)
+                max_steps=6, dtype="bf16")
     base.update(kw)
     return PSConfig(**base).validate()
 
@@ -115,8 +115,8 @@ def test_fetched_operands_identical(use_graph):
     srv = ParameterServer(cfg, lay, arena, counters, device="cuda", total_workers=1, log=lambda *a, **k: None)
     srv.register_worker("w", 0)
     train, _ = make_datasets(cfg, torch.device("cuda"), 100)
-    ca = HipCompute(model, lay, 64, "cuda", use_graph=use_graph)
-    cb = HipCompute(model, lay, 64, "cuda", use_graph=use_graph)
+    ca = HipCompute(model, lay, 64, "cuda", use_graph=use_graph, dtype="bf16")
+    cb = HipCompute(model, lay, 64, "cuda", use_graph=use_graph, dtype="bf16")
     cha = make_local_channel(cfg, srv, lay, "cuda")
     assert cha.weight_wire() is not None
     ca.use_wire(cha.weight_wire(), small_from=cha.small_source())
@@ -154,7 +154,7 @@ import psx
 from psx.parallel.runner import run_distributed
 from psx.utils.config import PSConfig
 cfg = PSConfig(model="resnet18", batch_size=64, epochs=1, train_samples=2048, eval_every=0, verbose=0, lr=0.1,
-               max_steps=6, mode="sync").validate()
+               max_steps=6, mode="sync", dtype="bf16").validate()
 res = run_distributed(cfg, log=lambda *a, **k: None)
 print("RESULT " + json.dumps(res["server"]["final_param_checksum"]))
 """

@@ -1,20 +1,28 @@
 #!/usr/bin/env python3
 """Headline benchmark: images/sec (whole node) of ResNet-18 / CIFAR-100-shaped data in the
-synchronous parameter-server mode on 1..8 MI355X (BASELINE.json metric).
+synchronous parameter-server mode on 1..8 MI355X (BASELINE.json metric), at the reference's
+training precision (fp32).
 
   python bench.py                                   # N=1: server + worker co-located (one RCCL rank)
   python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \\
       --master-port 29500 bench.py --gpus 8 --steps 50 --warmup 10
 
-One step = fetch (RCCL broadcast from rank 0 of the weight wire: the bf16 image of the
-parameters + the fp32 BN/FC remainder, 22.5 MB) -> batch gather + augment -> forward/backward on
-the HIP engine (hand-written CDNA4 kernels, HIP graphs) -> push (RCCL reduce of the fp16 wire
-gradients to rank 0) -> fused SGD apply of the average on rank 0 (writing the next image). Batch 128 per worker, lr 0.1, sync period 1 (the reference's CLI defaults). Weak
-scaling: every rank is a worker (rank 0 also hosts the parameter server, ``--topology
-colocated``); ``--topology dedicated`` reproduces the reference's 1 server + (N-1) workers.
+One step = fetch (RCCL broadcast from rank 0 of the fp32 parameter state, 44.9 MB — the
+reference's FetchParameters payload) -> batch gather + augment -> forward/backward on the HIP
+engine (hand-written CDNA4 kernels, fp32 on the exact-f32 MFMA, HIP graphs) -> push (the fp16
+wire gradients — the reference's codec — gathered to rank 0 over RCCL point-to-point) -> fused
+update on rank 0: every wire decoded and summed in fp32, p -= lr * sum / W (reference
+server.py:126-169, 232-237). Batch 128 per worker, lr 0.1, sync period 1 (the reference's CLI
+defaults). Topology: N = 1 co-locates the server and the worker on one GPU; N >= 2 runs the
+reference's layout (BASELINE configs 2-4): rank 0 = the parameter server only, ranks 1..N-1 =
+workers (``--topology dedicated``); ``--topology colocated`` makes rank 0 a worker as well.
 W warmup steps are untimed; exactly K steps are timed between barrier+synchronize pairs and
 the max over ranks is reported. Data is synthetic CIFAR-100-shaped (no network access), weights
 random-init.
+
+Secondary numbers (``"secondary"`` in the JSON line, each measured after the headline with the
+same transport, ``--secondary none`` skips them): the bf16 compute path (N = 1) and the
+co-located topology (N >= 2).
 """
 import argparse
 import json
@@ -42,6 +50,138 @@ from psx.utils.config import PSConfig  # noqa: E402
 BASELINE_SYNC_IMG_S = 82.7  # sync PS, 4 workers, measured (experiment_results/sync_4workers.json)
 
 
+class Run:
+    """One benchmark configuration on the shared transport: server / worker / channel objects."""
+
+    def __init__(self, a, t, rank, world, device, dtype, topology):
+        self.a, self.t, self.rank, self.world = a, t, rank, world
+        n_train = a.train_samples or (50000 if a.model == "resnet18" else 4096)
+        self.n_train = n_train
+        self.cfg = cfg = PSConfig(mode=a.mode, staleness_bound=a.staleness_bound, model=a.model, batch_size=a.batch,
+                                  train_samples=n_train, lr=0.1, sync_steps=1, epochs=1, eval_every=0, verbose=0,
+                                  codec=a.codec, topk_ratio=a.topk_ratio, use_graph=not a.no_graph,
+                                  fetch_codec=a.fetch_codec, overlap=a.overlap, bucket_mb=a.bucket_mb,
+                                  topology=topology, dtype=dtype).validate()
+        model, layout, arena, counters = build_state(cfg)
+        self.layout = layout
+        wire = torch.float16 if a.codec == "fp16" else torch.float32  # topk encodes from fp32 grads
+        self.sharded = sharded = topology == "sharded"
+        self.dedicated = dedicated = topology == "dedicated" and world > 1
+        worker_ranks = list(range(1, world)) if dedicated else list(range(world))
+        self.W = W = len(worker_ranks)
+        cfg.workers = W
+        is_worker = rank in worker_ranks
+        self.server = None
+        quiet = lambda *x, **k: None  # noqa: E731
+        self.async_dist = async_dist = a.mode == "async" and t is not None
+        if rank == 0 or sharded:
+            self.server = ParameterServer(cfg, layout, arena, counters, device=device, total_workers=W, log=quiet)
+            if not async_dist and rank == 0:
+                for i in range(W):
+                    self.server.register_worker(f"worker-{i}", i)
+        train, _ = make_datasets(cfg, device, model.fc.out_features)
+        comp = HipCompute(model, layout, a.batch, device, a.model, wire, seed=rank, use_graph=cfg.use_graph,
+                          dtype=cfg.dtype) if is_worker else None
+        self.wk = self.sess = self.chan = self.zeros = None
+        if async_dist:  # server event loop thread on rank 0, mailbox + RCCL p2p (parallel/runner.py)
+            names = [f"worker-r{r}" for r in range(world)]
+            self.sess = AsyncSession(cfg, t, rank, worker_ranks, self.server, comp, train, None, names, quiet)
+            self.wk = self.sess.worker
+        else:
+            if sharded:
+                self.chan = ShardedSyncChannel(cfg, t, self.server, list(range(W)), layout, device, in_place=True)
+            else:
+                self.chan = (make_local_channel(cfg, self.server, layout, device) if t is None else
+                             make_sync_channel(cfg, t, self.server, W, layout, device, worker=is_worker))
+            if is_worker:
+                wid = worker_ranks.index(rank)
+                self.wk = Worker(cfg, comp, self.chan, train, None, worker_name=f"worker-{wid}", rank=rank, log=quiet,
+                                 requested_id=wid)
+                self.wk.connect_to_server()
+        if self.wk is not None:
+            self.wk.setup_data()
+            self.batches = self.wk.sampler.epoch_indices(0)
+        elif self.sess is not None:
+            pass  # dedicated async server rank: its event-loop thread does the work
+        elif a.codec == "topk":
+            from psx.parallel.topk import empty_payload
+
+            self.zeros = empty_payload(layout.param_numel, a.topk_ratio, device)
+        else:
+            self.zeros = torch.zeros(layout.param_numel, dtype=wire, device=device)
+
+    def step(self, i):
+        if self.wk is not None:
+            self.wk.fetch_parameters()
+            self.wk.train_local_batch(self.batches[i % len(self.batches)])
+            self.wk.push_gradients()
+        elif self.sess is not None:
+            pass
+        else:  # dedicated sync server rank: joins the fetch and push collectives, applies
+            self.chan.fetch(None, None)
+            if self.a.codec != "topk":
+                self.zeros.zero_()
+            self.chan.push(None, self.zeros, self.server.core.global_step)
+
+    def barrier_sync(self):
+        torch.cuda.synchronize()
+        if self.t is not None:
+            # async: the server thread drives RCCL p2p on the default group, so host barriers
+            # use the gloo control group
+            self.t.barrier() if self.async_dist else dist.barrier()
+        torch.cuda.synchronize()
+
+    def measure(self, steps, warmup):
+        """Untimed warmup, then exactly ``steps`` timed steps; returns (max seconds over ranks,
+        host issue times of this rank)."""
+        for i in range(warmup):
+            self.step(i)
+        self.barrier_sync()
+        host = []
+        t0 = time.perf_counter()
+        for i in range(steps):
+            h0 = time.perf_counter()
+            self.step(warmup + i)
+            host.append(time.perf_counter() - h0)
+        self.barrier_sync()
+        dt = time.perf_counter() - t0
+        if self.t is not None and self.async_dist:
+            dt = max(self.t.all_gather_object(dt))
+        elif self.t is not None:
+            tt = torch.tensor([dt], dtype=torch.float64, device=torch.cuda.current_device())
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        return dt, host
+
+    def parallelism(self):
+        a, W = self.a, self.W
+        if self.sharded:
+            return (f"sharded sync-PS: {W} ranks, each a worker + 1/{W} of the server; RCCL reduce-scatter(grads) "
+                    f"+ all-gather(params) over xGMI")
+        if self.t is None:
+            return f"{a.mode}-PS: server + 1 worker co-located on 1 GPU"
+        agg = os.environ.get("PSX_SYNC_AGG", "gather")
+        push = ("RCCL send/recv gather of the fp16 wires to rank 0 + fp32 aggregation" if agg == "gather" else
+                "RCCL reduce(grads)")
+        return (f"{a.mode}-PS: rank0 = parameter server{' only' if self.dedicated else ' + worker 0'}, {W} "
+                f"data-parallel worker(s); " + (f"{push} + RCCL broadcast(params) over xGMI" if a.mode == "sync" else
+                                                 "shm mailbox control + RCCL send/recv over xGMI"))
+
+    def topology_name(self):
+        if self.sharded:
+            return "sharded"
+        if self.dedicated:
+            return "dedicated"
+        return "colocated" if self.t is not None else "loopback"
+
+    def close(self):
+        if self.sess is not None:
+            self.sess.finish()
+            self.sess.close()
+        if hasattr(self.chan, "drain"):
+            self.chan.drain()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -53,16 +193,16 @@ def main():
                          "shape, use with --codec topk)")
     ap.add_argument("--train-samples", type=int, default=None,
                     help="synthetic dataset size in HBM (default 50000 for resnet18, 4096 for resnet50)")
-    ap.add_argument("--topology", choices=["colocated", "dedicated", "sharded"], default="colocated",
-                    help="sharded: every rank is a worker and owns 1/N of the server (reduce-scatter, "
-                         "range apply, all-gather; parallel/sharded.py)")
+    ap.add_argument("--topology", choices=["auto", "colocated", "dedicated", "sharded"], default="auto",
+                    help="auto: colocated at N=1, dedicated (1 server + N-1 workers, the reference's layout) at "
+                         "N>=2; sharded: every rank is a worker and owns 1/N of the server (parallel/sharded.py)")
     ap.add_argument("--codec", choices=["fp16", "none", "topk"], default="fp16")
     ap.add_argument("--topk-ratio", type=float, default=0.01)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32",
                     help="worker compute precision. fp32 (default, the headline): the reference's training "
                          "precision (worker.py:333-348), every conv product on the exact-f32 MFMA; bf16: bf16 "
-                         "operands with fp32 accumulation and fp32 master weights (secondary number)")
+                         "operands with fp32 accumulation and fp32 master weights")
     ap.add_argument("--fetch-codec", choices=["auto", "bf16conv", "fp32"], default="auto",
                     help="auto: fp32 for --dtype fp32, bf16conv for bf16. bf16conv: conv weights travel as the "
                          "bf16 bits the workers compute with, everything else fp32; fp32: the reference's full "
@@ -74,6 +214,9 @@ def main():
     ap.add_argument("--mode", choices=["sync", "async"], default="sync",
                     help="async: workers push/fetch independently (staleness-weighted server updates)")
     ap.add_argument("--staleness-bound", type=int, default=5)
+    ap.add_argument("--secondary", choices=["auto", "none"], default="auto",
+                    help="auto: after the headline also time the bf16 compute path (N=1) or the co-located "
+                         "topology (N>=2), reported under 'secondary'")
     a = ap.parse_args()
 
     rank, world, local = env_world()
@@ -81,12 +224,9 @@ def main():
         raise SystemExit("bench.py needs MI355X GPUs")
     torch.cuda.set_device(local % torch.cuda.device_count())
     device = torch.device("cuda", torch.cuda.current_device())
-    n_train = a.train_samples or (50000 if a.model == "resnet18" else 4096)
-    cfg = PSConfig(mode=a.mode, staleness_bound=a.staleness_bound, model=a.model, batch_size=a.batch, train_samples=n_train, lr=0.1, sync_steps=1, epochs=1,
-                   eval_every=0, verbose=0, codec=a.codec, topk_ratio=a.topk_ratio, use_graph=not a.no_graph, fetch_codec=a.fetch_codec,
-                   overlap=a.overlap, bucket_mb=a.bucket_mb, topology=a.topology, dtype=a.dtype).validate()
-    model, layout, arena, counters = build_state(cfg)
-    wire = torch.float16 if a.codec == "fp16" else torch.float32  # topk encodes from fp32 grads
+    topology = a.topology if a.topology != "auto" else ("dedicated" if world >= 2 else "colocated")
+    if a.fetch_codec == "auto":
+        a.fetch_codec = "fp32" if a.dtype == "fp32" else "bf16conv"
 
     t = None
     # sync at N = 1 runs the distributed path too (one rank: psx communicator, rank 0 = server +
@@ -94,8 +234,7 @@ def main():
     # (one box 1.777/1.778 vs 1.842/1.829 ms/step, another 1.843 vs 1.853 mean of 3 interleaved).
     # PSX_FORCE_DIST=0: in-process loopback.
     force_dist = os.environ.get("PSX_FORCE_DIST", "1" if a.mode == "sync" else "0") == "1"
-    sharded = a.topology == "sharded"
-    if world > 1 or force_dist or sharded:
+    if world > 1 or force_dist or topology == "sharded":
         if "RANK" not in os.environ:  # single process without torchrun: a world of one rank
             import socket
 
@@ -105,96 +244,17 @@ def main():
             os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                               MASTER_PORT=str(port))
         t = make_transport(device)
-    dedicated = a.topology == "dedicated" and world > 1
-    worker_ranks = list(range(1, world)) if dedicated else list(range(world))
-    W = len(worker_ranks)
-    cfg.workers = W
-    is_worker = rank in worker_ranks
-    server = None
-    quiet = lambda *x, **k: None  # noqa: E731
-    async_dist = a.mode == "async" and t is not None
-    if rank == 0 or sharded:
-        server = ParameterServer(cfg, layout, arena, counters, device=device, total_workers=W, log=quiet)
-        if not async_dist and rank == 0:
-            for i in range(W):
-                server.register_worker(f"worker-{i}", i)
-    train, _ = make_datasets(cfg, device, model.fc.out_features)
-    comp = HipCompute(model, layout, a.batch, device, a.model, wire, seed=rank, use_graph=cfg.use_graph,
-                      dtype=cfg.dtype) if is_worker else None
-    wk = None
-    zeros = None
-    sess = None
-    chan = None
-    if async_dist:  # server event loop thread on rank 0, mailbox + RCCL p2p (parallel/runner.py)
-        names = [f"worker-r{r}" for r in range(world)]
-        sess = AsyncSession(cfg, t, rank, worker_ranks, server, comp, train, None, names, quiet)
-        wk = sess.worker
-    else:
-        if sharded:
-            chan = ShardedSyncChannel(cfg, t, server, list(range(W)), layout, device, in_place=True)
-        else:
-            chan = (make_local_channel(cfg, server, layout, device) if t is None else
-                    make_sync_channel(cfg, t, server, W, layout, device, worker=is_worker))
-        if is_worker:
-            wid = worker_ranks.index(rank)
-            wk = Worker(cfg, comp, chan, train, None, worker_name=f"worker-{wid}", rank=rank, log=quiet,
-                        requested_id=wid)
-            wk.connect_to_server()
-    if wk is not None:
-        wk.setup_data()
-        batches = wk.sampler.epoch_indices(0)
-    elif sess is not None:
-        pass  # dedicated async server rank: its event-loop thread does the work
-    elif a.codec == "topk":
-        from psx.parallel.topk import empty_payload
 
-        zeros = empty_payload(layout.param_numel, a.topk_ratio, device)
-    else:
-        zeros = torch.zeros(layout.param_numel, dtype=wire, device=device)
-
-    def step(i):
-        if wk is not None:
-            wk.fetch_parameters()
-            wk.train_local_batch(batches[i % len(batches)])
-            wk.push_gradients()
-        elif sess is not None:
-            pass
-        else:  # dedicated sync server rank
-            chan.fetch(None, None)
-            if a.codec != "topk":
-                zeros.zero_()
-            chan.push(None, zeros, server.core.global_step)
-
-    def barrier_sync():
-        torch.cuda.synchronize()
-        if t is not None:
-            # async: the server thread drives RCCL p2p on the default group, so host barriers
-            # use the gloo control group
-            t.barrier() if async_dist else dist.barrier()
-        torch.cuda.synchronize()
-
-    for i in range(a.warmup):
-        step(i)
-    barrier_sync()
-    host = []
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        h0 = time.perf_counter()
-        step(a.warmup + i)
-        host.append(time.perf_counter() - h0)
-    barrier_sync()
-    dt = time.perf_counter() - t0
-    if t is not None and async_dist:
-        dt = max(t.all_gather_object(dt))
-    elif t is not None:
-        tt = torch.tensor([dt], dtype=torch.float64, device=device)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    run = Run(a, t, rank, world, device, a.dtype, topology)
+    dt, host = run.measure(a.steps, a.warmup)
+    W = run.W
     imgs = a.steps * a.batch * W
     value = imgs / dt
-    loss = wk.compute.last_loss() if wk is not None else None
+    loss = run.wk.compute.last_loss() if run.wk is not None else None
+    r18 = a.model == "resnet18"
+    cfg = run.cfg
+    rec = None
     if rank == 0:
-        r18 = a.model == "resnet18"
         rec = {
             "metric": ("images/sec (whole node) ResNet-18 sync-PS at 1/2/4/8 MI355X; async staleness" if r18 else
                        "images/sec (whole node) ResNet-50 ImageNet-shape sync-PS + top-k (BASELINE config 5)"),
@@ -208,61 +268,73 @@ def main():
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_SYNC_IMG_S, 2) if r18 else None,
             "dtype": cfg.dtype,
-            "data": (f"synthetic CIFAR-100-shaped ({n_train}x32x32x3 uint8 in HBM, on-device crop/flip/normalize), "
+            "data": (f"synthetic CIFAR-100-shaped ({run.n_train}x32x32x3 uint8 in HBM, on-device crop/flip/normalize), "
                      "random-init weights" if r18 else
-                     f"synthetic ImageNet-shaped ({n_train}x224x224x3 uint8 in HBM, on-device crop/flip/normalize), "
+                     f"synthetic ImageNet-shaped ({run.n_train}x224x224x3 uint8 in HBM, on-device crop/flip/normalize), "
                      "random-init weights"),
             "config": {
                 "model": ("resnet18-cifar (11,220,132 params, reference ResNet18(num_classes=100))" if r18 else
-                          f"resnet50-imagenet ({layout.param_numel:,} params, 1000 classes)"),
+                          f"resnet50-imagenet ({run.layout.param_numel:,} params, 1000 classes)"),
                 "global_batch": a.batch * W,
                 "per_worker_batch": a.batch,
                 "seq_len": None,
-                "parallelism": (
-                    f"sharded sync-PS: {W} ranks, each a worker + 1/{W} of the server; RCCL reduce-scatter(grads) "
-                    f"+ all-gather(bf16 params) over xGMI" if sharded else
-                    f"{a.mode}-PS: rank0 = parameter server{' only' if dedicated else ' + worker 0'}, {W} data-parallel "
-                    f"worker(s); " + ("RCCL reduce(grads) + broadcast(params) over xGMI" if a.mode == "sync" else
-                                      "shm mailbox control + RCCL send/recv over xGMI")
-                    if t is not None else f"{a.mode}-PS: server + 1 worker co-located on 1 GPU"),
+                "parallelism": run.parallelism(),
                 "mode": a.mode,
                 "lr": 0.1,
                 "sync_steps": 1,
                 "codec": a.codec if a.codec != "topk" else f"topk({a.topk_ratio}) + error feedback",
                 "fetch_codec": cfg.fetch_codec if t is not None else "in-process",
-                "weight_image": getattr(chan, "image_wire", None) is not None or sharded,
-                "overlap": (f"bucketed reduce/apply/broadcast during backward ({len(chan.buckets)} buckets)"
-                            if getattr(chan, "overlap", False) else
-                            f"bucketed reduce/apply/broadcast captured in the step graph ({len(chan.buckets)} buckets)"
-                            if getattr(chan, "in_graph", False) else "none"),
-                "topology": ("sharded" if sharded else "dedicated" if dedicated else
-                             ("colocated" if t is not None else "loopback")),
+                "weight_image": getattr(run.chan, "image_wire", None) is not None or run.sharded,
+                "overlap": (f"bucketed reduce/apply/broadcast during backward ({len(run.chan.buckets)} buckets)"
+                            if getattr(run.chan, "overlap", False) else
+                            f"bucketed reduce/apply/broadcast captured in the step graph ({len(run.chan.buckets)} buckets)"
+                            if getattr(run.chan, "in_graph", False) else "none"),
+                "topology": run.topology_name(),
+                "workers": W,
                 "transport": (("native RCCL (psx comm)" if getattr(t, "native", False) else "torch.distributed")
                               if t is not None else "in-process"),
                 "hip_graph": cfg.use_graph,
             },
-            "global_steps": server.core.global_step,
+            "global_steps": run.server.core.global_step,
             "last_loss": round(loss, 4) if loss is not None else None,
             "baseline_img_s": BASELINE_SYNC_IMG_S if r18 else None,
         }
     if a.host_timing:
-        wait = getattr(wk.compute, "host_wait_s", 0.0) if wk is not None else 0.0
+        wait = getattr(run.wk.compute, "host_wait_s", 0.0) if run.wk is not None else 0.0
         print(json.dumps({"rank": rank, "host_issue_ms_per_step": round(1e3 * sum(host) / len(host), 4),
                           "host_issue_ms_max": round(1e3 * max(host), 4),
                           # time the host spent blocked because it ran len(ring) steps ahead (whole run)
                           "host_wait_ms_total": round(1e3 * wait, 3)}), file=sys.stderr, flush=True)
-    if sess is not None:
-        sess.finish()
-        sess.close()
+    run.close()
+    if rank == 0 and a.mode == "async":
+        sm = run.server.final_metrics()
+        rec["async_staleness"] = {k: sm.get(k) for k in ("average_gradient_staleness", "max_staleness_observed",
+                                                         "rejected_pushes", "staleness_histogram")}
+        rec["global_steps"] = run.server.core.global_step
+
+    # secondary numbers (same transport): bf16 compute at N=1, the co-located topology at N>=2
+    secondary = {}
+    if a.secondary == "auto" and a.mode == "sync" and r18 and topology != "sharded":
+        cases = ([("bf16_compute", "bf16", topology)] if world == 1 else
+                 [("colocated_topology", a.dtype, "colocated")] if topology == "dedicated" else [])
+        for name, dt_, topo in cases:
+            try:
+                a2 = argparse.Namespace(**vars(a))
+                a2.fetch_codec = "fp32" if dt_ == "fp32" else "bf16conv"
+                r2 = Run(a2, t, rank, world, device, dt_, topo)
+                steps2 = max(5, min(a.steps, 20))
+                d2, _ = r2.measure(steps2, min(a.warmup, 5))
+                v2 = steps2 * a.batch * r2.W / d2
+                secondary[name] = {"value": round(v2, 2), "ms_per_step": round(1e3 * d2 / steps2, 4), "dtype": dt_,
+                                   "topology": r2.topology_name(), "workers": r2.W, "steps": steps2,
+                                   "vs_baseline": round(v2 / BASELINE_SYNC_IMG_S, 2)}
+                r2.close()
+            except Exception as e:  # noqa: BLE001 - a secondary number never costs the headline
+                secondary[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0:
-        if a.mode == "async":
-            sm = server.final_metrics()
-            rec["async_staleness"] = {k: sm.get(k) for k in ("average_gradient_staleness", "max_staleness_observed",
-                                                             "rejected_pushes", "staleness_histogram")}
-            rec["global_steps"] = server.core.global_step
+        if secondary:
+            rec["secondary"] = secondary
         print(json.dumps(rec), flush=True)
-    if hasattr(chan, "drain"):
-        chan.drain()
     if t is not None:
         t.close()
 

@@ -77,6 +77,81 @@ __global__ __launch_bounds__(256) void sgd_apply_h8_kernel(float* __restrict__ p
   }
 }
 
+// Sync-round update straight from the W gathered gradient wires (reference server.py:232-237
+// decompress_gradients + :145-169 aggregate_gradients_sync + :126-143 apply_gradients):
+//   p <- p - lr * (gscale * sum_k decode(g_k) [+ wd p]) [momentum], gscale = 1/W,
+// every wire decoded to fp32 and summed in fp32 in the fixed source order k = 0..W-1 (what the
+// reference's numpy loop does; an RCCL fp16 reduce would round the running sum to fp16 at every
+// hop). One pass over the W wires + the parameters; img (optional) receives the bf16 image.
+constexpr int kMaxSrc = 32;  // reference server.py:424-426 caps the job at 32 workers
+struct SrcList {
+  const void* p[kMaxSrc];
+  int n;
+};
+
+template <typename GT, bool MOM>
+__global__ __launch_bounds__(256) void sgd_apply_multi_kernel(float* __restrict__ p, SrcList srcs,
+                                                              float* __restrict__ buf, size_t n, float lr,
+                                                              float gscale, float momentum, float wd, int first,
+                                                              uint16_t* __restrict__ img) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < srcs.n; ++k) s += ld_grad(reinterpret_cast<const GT*>(srcs.p[k]), i);
+    float d = s * gscale;
+    const float pv = p[i];
+    if (wd != 0.f) d += wd * pv;
+    if (MOM) {
+      const float v = first ? d : momentum * buf[i] + d;
+      buf[i] = v;
+      d = v;
+    }
+    const float nv = pv - lr * d;
+    p[i] = nv;
+    if (img) img[i] = f2bf(nv);
+  }
+}
+
+// vectorised fp16-wire form (no momentum / weight decay): 8 elements per lane, every source's
+// 16-byte chunk loaded before the fixed-order sum
+template <bool IMG>
+__global__ __launch_bounds__(256) void sgd_apply_multi_h8_kernel(float* __restrict__ p, SrcList srcs, size_t n,
+                                                                 float step, uint16_t* __restrict__ img) {
+  const size_t n8 = n >> 3;
+  if (blockIdx.x == 0 && threadIdx.x < (n & 7)) {  // tail (n % 8 elements)
+    const size_t i = (n8 << 3) + threadIdx.x;
+    float s = 0.f;
+    for (int k = 0; k < srcs.n; ++k) s += ld_grad(reinterpret_cast<const uint16_t*>(srcs.p[k]), i);
+    const float nv = p[i] - step * s;
+    p[i] = nv;
+    if (IMG) img[i] = f2bf(nv);
+  }
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < srcs.n; ++k) {
+      const u32x4 gv = reinterpret_cast<const u32x4*>(srcs.p[k])[i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[2 * j] += (float)__builtin_bit_cast(_Float16, (uint16_t)(gv[j] & 0xffff));
+        s[2 * j + 1] += (float)__builtin_bit_cast(_Float16, (uint16_t)(gv[j] >> 16));
+      }
+    }
+    f32x4 p0 = reinterpret_cast<f32x4*>(p)[2 * i];
+    f32x4 p1 = reinterpret_cast<f32x4*>(p)[2 * i + 1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      p0[j] -= step * s[j];
+      p1[j] -= step * s[4 + j];
+    }
+    reinterpret_cast<f32x4*>(p)[2 * i] = p0;
+    reinterpret_cast<f32x4*>(p)[2 * i + 1] = p1;
+    if (IMG) {
+      const u32x4 o = {pack_bf2(p0[0], p0[1]), pack_bf2(p0[2], p0[3]), pack_bf2(p1[0], p1[1]),
+                       pack_bf2(p1[2], p1[3])};
+      reinterpret_cast<u32x4*>(img)[i] = o;
+    }
+  }
+}
+
 // dst = sum_i src_i * scale  (fp16 or fp32 sources; fp32 or fp16 destination)
 template <typename ST, typename DT>
 __global__ __launch_bounds__(256) void aggregate_kernel(const ST* const* __restrict__ srcs, int nsrc,
@@ -326,6 +401,42 @@ int psx_sgd_apply(float* p, const void* g, float* buf, long n, float lr, float g
       hipLaunchKernelGGL((sgd_apply_kernel<float, false>), dim3(grid), dim3(256), 0, st, p, (const float*)g, buf,
                          (size_t)n, lr, gscale, momentum, wd, first, im);
   }
+  return (int)hipGetLastError();
+}
+
+// p -= lr * (gscale * sum_k g_k + wd * p) [momentum] over nsrc gradient wires (host array of
+// nsrc <= 32 device pointers, all fp16 or all fp32), summed in fp32 in source order.
+// img (optional): bf16 image of the updated parameters.
+int psx_sgd_apply_multi(float* p, const void* const* srcs, int nsrc, float* buf, long n, float lr, float gscale,
+                        float momentum, float wd, int first, int grad_fp16, void* img, hipStream_t st) {
+  if (nsrc < 1 || nsrc > kMaxSrc) return (int)hipErrorInvalidValue;
+  SrcList sl{};
+  sl.n = nsrc;
+  bool aligned = ((uintptr_t)p % 32 == 0) && ((uintptr_t)img % 16 == 0);
+  for (int k = 0; k < nsrc; ++k) {
+    sl.p[k] = srcs[k];
+    aligned = aligned && ((uintptr_t)srcs[k] % 16 == 0);
+  }
+  const bool mom = buf != nullptr && momentum != 0.f;
+  uint16_t* im = (uint16_t*)img;
+  if (!mom && wd == 0.f && grad_fp16 && n >= 8 && aligned) {
+    if (im)
+      hipLaunchKernelGGL(sgd_apply_multi_h8_kernel<true>, dim3(grid_for(n / 8)), dim3(256), 0, st, p, sl, (size_t)n,
+                         lr * gscale, im);
+    else
+      hipLaunchKernelGGL(sgd_apply_multi_h8_kernel<false>, dim3(grid_for(n / 8)), dim3(256), 0, st, p, sl, (size_t)n,
+                         lr * gscale, im);
+    return (int)hipGetLastError();
+  }
+  const int grid = grid_for(n);
+#define PSX_SAM(G, M)                                                                                              \
+  hipLaunchKernelGGL((sgd_apply_multi_kernel<G, M>), dim3(grid), dim3(256), 0, st, p, sl, buf, (size_t)n, lr, gscale, \
+                     momentum, wd, first, im)
+  if (grad_fp16 && mom) PSX_SAM(uint16_t, true);
+  else if (grad_fp16) PSX_SAM(uint16_t, false);
+  else if (mom) PSX_SAM(float, true);
+  else PSX_SAM(float, false);
+#undef PSX_SAM
   return (int)hipGetLastError();
 }
 

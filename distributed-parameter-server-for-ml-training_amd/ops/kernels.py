@@ -298,6 +298,21 @@ def sgd_apply(p, g, lr, gscale=1.0, momentum=0.0, wd=0.0, buf=None, first=False,
                                   int(first), int(fp16), ptr(img), stream_ptr()), "sgd_apply")
 
 
+def sgd_apply_multi(p, srcs, lr, gscale=1.0, momentum=0.0, wd=0.0, buf=None, first=False, n=None, img=None):
+    """p -= lr*(gscale * sum_k srcs[k] + wd*p) [momentum]: the sync round's update from the W
+    gathered wires, decoded and summed in fp32 in list order (reference decompress + aggregate +
+    apply, server.py:126-169,232-237). All sources fp16 or all fp32; at most 32."""
+    n = p.numel() if n is None else n
+    assert 1 <= len(srcs) <= 32
+    fp16 = srcs[0].dtype == torch.float16
+    assert all(s.dtype == srcs[0].dtype and s.numel() >= n and s.device == p.device for s in srcs), "sgd_apply_multi"
+    if img is not None:
+        assert img.dtype == torch.bfloat16 and img.numel() >= n and img.device == p.device, "sgd_apply_multi img"
+    arr = (C.c_void_p * len(srcs))(*[s.data_ptr() for s in srcs])
+    check(kernels().psx_sgd_apply_multi(ptr(p), arr, len(srcs), ptr(buf), n, float(lr), float(gscale), float(momentum),
+                                        float(wd), int(first), int(fp16), ptr(img), stream_ptr()), "sgd_apply_multi")
+
+
 def maxpool3s2_fwd(x, y, arg):
     """3x3/s2/p1 max-pool, NHWC bf16 or fp32; arg (uint8, y's shape) keeps the window argmax."""
     B, H, W, C = x.shape

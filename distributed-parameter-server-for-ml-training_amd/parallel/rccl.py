@@ -190,6 +190,22 @@ class RcclTransport(DistTransport):
         self.comm.gather(t, None, 0)
         return None
 
+    def gather_from_workers(self, t, bufs):
+        """DistTransport.gather_from_workers on the native communicator: one group of
+        ncclRecv (rank 0, one per remote rank, concurrent over the xGMI links) / one ncclSend
+        (workers), in stream order on the caller's stream."""
+        lib = comm()
+        if self.rank == 0:
+            _check(lib.psx_comm_group_start(), "ncclGroupStart")
+            try:
+                for r, b in sorted(bufs.items()):
+                    self.comm.recv(b, r)
+            finally:
+                _check(lib.psx_comm_group_end(), "ncclGroupEnd")
+            return bufs
+        self.comm.send(t, 0)
+        return None
+
     # ---- sharded server (parallel/sharded.py)
     def reduce_scatter_sum(self, t, out):
         self.comm.reduce_scatter_sum(t, out)

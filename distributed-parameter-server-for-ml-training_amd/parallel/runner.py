@@ -326,7 +326,8 @@ def make_sync_channel(cfg, t, server, W, layout, device, worker: bool = True):
             return GraphRoundChannel(t, server, list(range(W)), codec, wire, buckets, device)
         if worker:  # rank 0's worker reads the server's wire in place (stream-ordered round)
             wire = server.wire if server is not None else WeightWire(layout, device)
-    return SyncCollectiveChannel(t, server, members=list(range(W)), codec=codec, wire=wire)
+    return SyncCollectiveChannel(t, server, members=list(range(W)), codec=codec, wire=wire,
+                                 root_worker=server is None or worker)
 
 
 def make_local_channel(cfg, server, layout, device, emit_on_last: bool = False):

@@ -274,6 +274,39 @@ class ParameterServer:
             return True
         return False
 
+    def apply_sources(self, srcs: list, members: list[int], local_steps: list[int],
+                      buffers_sum: torch.Tensor | None = None) -> bool:
+        """Sync round whose W dense wires were gathered to rank 0 (one per contributing worker):
+        decoded and summed in fp32 in list order inside the update (kernels.sgd_apply_multi),
+        then p -= lr * sum / W — the reference's decompress + aggregate + apply
+        (server.py:126-169, 232-237) without an fp16 running sum."""
+        res = None
+        for wid, ls in zip(members, local_steps):
+            res = self.core.on_push(wid, ls)
+        self.bytes_pushed += sum(s[: self.n].numel() * s.element_size() for s in srcs)
+        if res is None or not res.apply:
+            return False
+        trace.mark("psx.apply")
+        t0 = time.perf_counter()
+        if self.device.type == "cuda":
+            from ..ops import kernels as K
+
+            img = self.wire.img[: self.n] if self.wire is not None else None
+            K.sgd_apply_multi(self.params, [s[: self.n] for s in srcs], self.lr, gscale=res.weight,
+                              momentum=self.cfg.momentum, wd=self.cfg.weight_decay, buf=self.momentum_buf,
+                              first=self._mom_first, n=self.n, img=img)
+        else:
+            if self.agg is None:
+                self.agg = torch.zeros(self.n, dtype=torch.float32, device=self.device)
+            self.agg.zero_()
+            for s in srcs:  # fixed order, fp32 accumulation
+                self.agg.add_(s[: self.n].to(torch.float32))
+            self.apply_range(self.agg, res.weight, 0, self.n)
+        self.finish_round_apply(time.perf_counter() - t0)
+        if buffers_sum is not None:
+            self.set_buffers_from_sum(buffers_sum, len(members))
+        return True
+
     def apply_gathered(self, payloads: list, members: list[int], local_steps: list[int],
                        buffers_sum: torch.Tensor | None = None) -> bool:
         """Sync round with top-k payloads gathered to rank 0: decode all into one dense fp32

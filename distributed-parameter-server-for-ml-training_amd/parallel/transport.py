@@ -43,6 +43,11 @@ class LocalTransport:
     def gather_to_server(self, t):
         return [t]
 
+    def gather_from_workers(self, t, bufs):
+        """No remote ranks in a single process."""
+        assert not bufs
+        return bufs
+
     def reduce_scatter_sum(self, t, out):
         out.copy_(t[: out.numel()])
         return out
@@ -136,6 +141,19 @@ class DistTransport:
             dist.gather(t, gather_list=out, dst=0)
             return out
         dist.gather(t, gather_list=None, dst=0)
+        return None
+
+    def gather_from_workers(self, t, bufs):
+        """Sync push with fp32 aggregation on the server: rank r > 0 sends its wire ``t`` to rank
+        0, which receives it into ``bufs[r]`` (preallocated, one per remote rank) — point-to-point
+        transfers that all run at once (each worker on its own xGMI link). Rank 0's own wire
+        stays where it is. The server then sums the wires in fp32 (kernels.sgd_apply_multi)."""
+        if self.rank == 0:
+            works = [dist.irecv(b, src=r) for r, b in sorted(bufs.items())]
+            for w in works:
+                w.wait()
+            return bufs
+        dist.send(t, dst=0)
         return None
 
     # ---- bucketed (overlapped) sync round: non-blocking; RCCL runs on its own stream ordered

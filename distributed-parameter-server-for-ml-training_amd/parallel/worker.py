@@ -76,12 +76,23 @@ class InProcessChannel:
 
 
 class SyncCollectiveChannel:
-    """All ranks call push/fetch in lockstep. Rank 0 may or may not train (topology)."""
+    """All ranks call push/fetch in lockstep. Rank 0 may or may not train (topology).
 
-    def __init__(self, transport, server=None, members=None, codec=None, wire=None):
+    Push (dense wire): the workers' wires are gathered to rank 0 and summed there in fp32 by the
+    update kernel, in a fixed worker order — the reference's decode-to-fp32 + average
+    (server.py:145-169,232-237), deterministic, and every worker's transfer on its own link.
+    ``PSX_SYNC_AGG=reduce`` uses one RCCL sum-reduce of the wires instead (the wire dtype's
+    arithmetic at every hop: fp16 for the default codec)."""
+
+    def __init__(self, transport, server=None, members=None, codec=None, wire=None, root_worker=True):
+        import os
+
         self.t = transport
         self.server = server
         self.members = members or []
+        self.root_worker = root_worker  # rank 0 contributes a gradient (colocated topology)
+        self.agg_mode = os.environ.get("PSX_SYNC_AGG", "gather")
+        self._gbufs = None
         self.codec = codec  # FetchCodec (parallel/codec.py); None = raw fp32 arena
         # weight-image fast path (parallel/codec.py WeightWire): this rank's worker-side wire
         # (None on a dedicated server rank); the server's own wire is kept by the apply
@@ -150,13 +161,25 @@ class SyncCollectiveChannel:
 
     def push(self, worker_id, grads, local_step, buffers=None):
         sparse = grads.dtype == torch.int32  # top-k payloads cannot be summed by a reduce: gather
-        gathered = self.t.gather_to_server(grads) if sparse else self.t.reduce_sum_to_server(grads)
+        world = getattr(self.t, "world_size", 1)
+        dense_gather = not sparse and self.agg_mode == "gather" and world > 1
+        if sparse:
+            gathered = self.t.gather_to_server(grads)
+        elif dense_gather:
+            if self.server is not None and self._gbufs is None:
+                self._gbufs = {r: torch.empty_like(grads) for r in range(1, world)}
+            self.t.gather_from_workers(grads, self._gbufs if self.server is not None else None)
+        else:
+            self.t.reduce_sum_to_server(grads)
         if buffers is not None:
             self.t.reduce_sum_to_server(buffers)
         if self.server is not None:
             steps = [local_step] * len(self.members)
             if sparse:
                 self.server.apply_gathered(gathered, self.members, steps, buffers_sum=buffers)
+            elif dense_gather:
+                srcs = ([grads] if self.root_worker else []) + [self._gbufs[r] for r in sorted(self._gbufs)]
+                self.server.apply_sources(srcs, self.members, steps, buffers_sum=buffers)
             else:
                 self.server.apply_reduced(grads, self.members, steps, buffers_sum=buffers)
             self.server.maybe_checkpoint()

@@ -423,3 +423,21 @@ def test_eval_workers_first_only_worker0_evaluates():
     assert len(accs[0]) == 1 and accs[1] == []
     res = run_local(tiny_cfg(mode="sync", workers=2), log=lambda *a, **k: None)
     assert all(len(w["all_accuracies_percent"]) == 1 for w in res["workers"])
+
+
+@pytest.mark.parametrize("topology", ["colocated", "dedicated"])
+def test_sync_round_fp32_aggregation(topology):
+    """gloo world 3: the server arena after one sync round equals the float64 average of the
+    decoded fp16 pushes to fp32 rounding (the workers' wires are gathered and summed in fp32,
+    not reduced in fp16)."""
+    port = _free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tests", "helpers", "sync_agg_rank.py"),
+           topology]
+    r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if "RESULT " in ln][0].split("RESULT ", 1)[1])
+    assert res["gs"] == 1
+    assert res["err"] < 1e-6, res  # fp32 rounding of the update only
+    assert res["err_fp16_sum"] > 10 * res["err"], res  # what an fp16 running sum would have cost

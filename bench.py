@@ -34,7 +34,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
 import psx  # noqa: E402,F401
 from psx.parallel.compute import HipCompute  # noqa: E402
@@ -126,9 +125,7 @@ class Run:
     def barrier_sync(self):
         torch.cuda.synchronize()
         if self.t is not None:
-            # async: the server thread drives RCCL p2p on the default group, so host barriers
-            # use the gloo control group
-            self.t.barrier() if self.async_dist else dist.barrier()
+            self.t.barrier()  # host barrier on the gloo control group
         torch.cuda.synchronize()
 
     def measure(self, steps, warmup):
@@ -145,12 +142,8 @@ class Run:
             host.append(time.perf_counter() - h0)
         self.barrier_sync()
         dt = time.perf_counter() - t0
-        if self.t is not None and self.async_dist:
-            dt = max(self.t.all_gather_object(dt))
-        elif self.t is not None:
-            tt = torch.tensor([dt], dtype=torch.float64, device=torch.cuda.current_device())
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            dt = float(tt.item())
+        if self.t is not None:
+            dt = max(self.t.all_gather_object(dt))  # the slowest rank's time (gloo control group)
         return dt, host
 
     def parallelism(self):

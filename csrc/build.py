@@ -101,6 +101,16 @@ def build(jobs: int = 8, debug: bool = False, verbose: bool = False) -> dict:
     if c_objs and _newer(c_objs, c_lib):
         _run([HIPCC, "-shared", "-fPIC", "-pthread", "-o", c_lib] + c_objs + ["-ldl", "-lrt"])
     libs["comm"] = c_lib
+
+    # TEST-ONLY: libpsx_fakecomm.so, an RCCL stand-in for several ranks on one GPU (see
+    # csrc/tests/fakecomm.hip); tests load it with PSX_RCCL_LIB + PSX_FAKECOMM_TEST=1
+    f_src = os.path.join(HERE, "tests", "fakecomm.hip")
+    f_lib = os.path.join(OUT, "testing", "libpsx_fakecomm.so")
+    if os.path.exists(f_src) and _newer([f_src], f_lib):
+        os.makedirs(os.path.dirname(f_lib), exist_ok=True)
+        _run([HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared", "-Wall", "-D__HIP_PLATFORM_AMD__",
+              "-I", "/opt/rocm/include"] + opt + [f_src, "-o", f_lib, "-lrt", "-pthread"])
+    libs["fakecomm"] = f_lib
     return libs
 
 

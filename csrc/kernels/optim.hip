@@ -113,15 +113,16 @@ __global__ __launch_bounds__(256) void sgd_apply_multi_kernel(float* __restrict_
 
 // vectorised fp16-wire form (no momentum / weight decay): 8 elements per lane, every source's
 // 16-byte chunk loaded before the fixed-order sum
+// (same arithmetic as sgd_apply_multi_kernel: d = sum * gscale, p -= lr * d)
 template <bool IMG>
 __global__ __launch_bounds__(256) void sgd_apply_multi_h8_kernel(float* __restrict__ p, SrcList srcs, size_t n,
-                                                                 float step, uint16_t* __restrict__ img) {
+                                                                 float lr, float gscale, uint16_t* __restrict__ img) {
   const size_t n8 = n >> 3;
   if (blockIdx.x == 0 && threadIdx.x < (n & 7)) {  // tail (n % 8 elements)
     const size_t i = (n8 << 3) + threadIdx.x;
     float s = 0.f;
     for (int k = 0; k < srcs.n; ++k) s += ld_grad(reinterpret_cast<const uint16_t*>(srcs.p[k]), i);
-    const float nv = p[i] - step * s;
+    const float nv = p[i] - lr * (s * gscale);
     p[i] = nv;
     if (IMG) img[i] = f2bf(nv);
   }
@@ -139,8 +140,8 @@ __global__ __launch_bounds__(256) void sgd_apply_multi_h8_kernel(float* __restri
     f32x4 p1 = reinterpret_cast<f32x4*>(p)[2 * i + 1];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      p0[j] -= step * s[j];
-      p1[j] -= step * s[4 + j];
+      p0[j] -= lr * (s[j] * gscale);
+      p1[j] -= lr * (s[4 + j] * gscale);
     }
     reinterpret_cast<f32x4*>(p)[2 * i] = p0;
     reinterpret_cast<f32x4*>(p)[2 * i + 1] = p1;
@@ -422,10 +423,10 @@ int psx_sgd_apply_multi(float* p, const void* const* srcs, int nsrc, float* buf,
   if (!mom && wd == 0.f && grad_fp16 && n >= 8 && aligned) {
     if (im)
       hipLaunchKernelGGL(sgd_apply_multi_h8_kernel<true>, dim3(grid_for(n / 8)), dim3(256), 0, st, p, sl, (size_t)n,
-                         lr * gscale, im);
+                         lr, gscale, im);
     else
       hipLaunchKernelGGL(sgd_apply_multi_h8_kernel<false>, dim3(grid_for(n / 8)), dim3(256), 0, st, p, sl, (size_t)n,
-                         lr * gscale, im);
+                         lr, gscale, im);
     return (int)hipGetLastError();
   }
   const int grid = grid_for(n);

@@ -207,6 +207,20 @@ class RcclTransport(DistTransport):
         return None
 
     # ---- sharded server (parallel/sharded.py)
+    def exchange_chunks(self, t, chunk: int, bufs):
+        """All-to-all of the wire chunks in one group of ncclSend/ncclRecv (every link busy at
+        once), on the caller's stream."""
+        lib = comm()
+        _check(lib.psx_comm_group_start(), "ncclGroupStart")
+        try:
+            for p in range(self.world_size):
+                if p != self.rank:
+                    self.comm.send(t[p * chunk:(p + 1) * chunk], p)
+                    self.comm.recv(bufs[p], p)
+        finally:
+            _check(lib.psx_comm_group_end(), "ncclGroupEnd")
+        return bufs
+
     def reduce_scatter_sum(self, t, out):
         self.comm.reduce_scatter_sum(t, out)
         return out

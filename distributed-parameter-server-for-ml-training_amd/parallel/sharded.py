@@ -6,11 +6,14 @@ src/parameter_server/server.py:95-96, SURVEY.md §2.4 "Sharded PS ... no"); SURV
 sharded-server variant as the xGMI-friendly stretch next to the rank-0 PS the north star fixes.
 Here the sync round is
 
-    push : reduce-scatter(sum) of the fp16 gradient wire — rank r receives the summed chunk r
-    apply: rank r runs the fused SGD (csrc/kernels/optim.hip) on params[lo_r:hi_r] only, writing
-           the bf16 image of that range in the same pass, and gathers the fp32 entries of its
-           range that a worker needs (BN affine, FC; rank 0 also the BN running buffers)
-    fetch: all-gather of the bf16 image chunks + all-gather of the fp32 chunks
+    push : all-to-all of the fp16 gradient wire chunks — rank r receives every rank's chunk r
+           (the bytes of a reduce-scatter, without its fp16 running sum)
+    apply: rank r runs the fused SGD (csrc/kernels/optim.hip sgd_apply_multi: the W chunks
+           decoded and summed in fp32 in rank order) on params[lo_r:hi_r] only, writing the
+           parameter image of that range (bf16 for the bf16 compute path, fp32 for fp32) and
+           gathers the fp32 entries of its range that a worker needs (BN affine, FC; rank 0 also
+           the BN running buffers)
+    fetch: all-gather of the image chunks + all-gather of the fp32 chunks
 
 so every link carries (world-1)/world of the payload in each direction and no rank serialises
 the whole update (ring reduce + broadcast through rank 0 in the default topology). Rank 0 keeps
@@ -56,20 +59,21 @@ class ShardPlan:
 
 
 class ShardedWire:
-    """The fetch payload of the sharded round: ``img`` = bf16 image of all params (padded to
-    world equal chunks, arena offsets), ``small`` = [world][S] fp32 remainder blocks."""
+    """The fetch payload of the sharded round: ``img`` = image of all params (padded to world
+    equal chunks, arena offsets; bf16 for the bf16 compute path, fp32 for fp32), ``small`` =
+    [world][S] fp32 remainder blocks."""
 
-    def __init__(self, plan: ShardPlan, device):
+    def __init__(self, plan: ShardPlan, device, img_dtype=torch.bfloat16):
         self.plan = plan
         self.device = torch.device(device)
-        self.img = torch.zeros(plan.padded, dtype=torch.bfloat16, device=self.device)
+        self.img = torch.zeros(plan.padded, dtype=img_dtype, device=self.device)
         self.small = torch.zeros(plan.world * plan.S, dtype=torch.float32, device=self.device)
         self.small_index = plan.dst.to(self.device)
         self.small_src = plan.src.to(self.device)
 
     @property
     def nbytes(self) -> int:
-        return self.img.numel() * 2 + self.small.numel() * 4
+        return self.img.numel() * self.img.element_size() + self.small.numel() * 4
 
     def publish_full(self, arena: torch.Tensor, rank: int | None = None):
         self.img[: self.plan.n].copy_(arena[: self.plan.n])
@@ -101,13 +105,17 @@ class ShardedSyncChannel:
         self.rank, self.world = transport.rank, transport.world_size
         self.members = members
         self.plan = ShardPlan(layout, self.world)
-        self.wire = ShardedWire(self.plan, device)
+        f32 = getattr(cfg, "dtype", "bf16") == "fp32"
+        self.wire = ShardedWire(self.plan, device, torch.float32 if f32 else torch.bfloat16)
         self.wire.publish_full(server.arena)  # every rank starts from the same replica
-        self.in_place = in_place  # the HIP engine reads the wire itself (use_wire)
+        # the bf16 HIP engine reads the wire's image itself (use_wire); the fp32 engine unpacks
+        # from its fp32 local arena, which the fetch fills from the fp32 image
+        self.in_place = in_place and not f32
         r = self.rank
         self.lo, self.hi = self.plan.lo[r], self.plan.hi[r]
         dt = torch.float16 if cfg.codec == "fp16" else torch.float32
-        self.gshard = torch.zeros(self.plan.chunk, dtype=dt, device=device)
+        # chunk r of every other rank's wire (all-to-all); this rank's own chunk stays in place
+        self.recv = {p: torch.zeros(self.plan.chunk, dtype=dt, device=device) for p in range(self.world) if p != r}
         server.wire = None  # this rank's image range is written by apply_shard, not server.apply
         self._gs = 0
 
@@ -137,7 +145,9 @@ class ShardedSyncChannel:
             raise RuntimeError("the sharded server takes dense gradients without --bn-sync")
         if grads.numel() < self.plan.padded:
             raise RuntimeError("gradient buffer not padded to the shard plan (bind_compute)")
-        self.t.reduce_scatter_sum(grads[: self.plan.padded], self.gshard)
+        c, r = self.plan.chunk, self.rank
+        self.t.exchange_chunks(grads[: self.plan.padded], c, self.recv)
+        srcs = [grads[r * c:(r + 1) * c] if p == r else self.recv[p] for p in range(self.world)]
         W = len(self.members)
         weight = 1.0 / W
         if self.rank == 0:
@@ -148,7 +158,7 @@ class ShardedSyncChannel:
             if res is None or not res.apply:
                 raise RuntimeError("sharded sync round did not complete at the barrier")
             weight = res.weight
-        self.apply_shard(weight)
+        self.apply_shard(weight, srcs)
         self._gs += 1
         return True
 
@@ -156,19 +166,26 @@ class ShardedSyncChannel:
         pass
 
     # ---- server side of this rank
-    def apply_shard(self, weight: float):
+    def apply_shard(self, weight: float, srcs: list):
+        """params[lo:hi] -= lr * weight * sum_r srcs[r] (fp32 sum in rank order), image range."""
         s = self.server
         n = self.hi - self.lo
         if n > 0:
+            bf16_img = self.wire.img.dtype == torch.bfloat16
             if s.device.type == "cuda":
                 from ..ops import kernels as K
 
                 buf = s.momentum_buf[self.lo:self.hi] if s.momentum_buf is not None else None
-                K.sgd_apply(s.params[self.lo:self.hi], self.gshard[:n], s.lr, gscale=weight, momentum=s.cfg.momentum,
-                            wd=s.cfg.weight_decay, buf=buf, first=s._mom_first, n=n,
-                            img=self.wire.img[self.lo:self.hi])
+                K.sgd_apply_multi(s.params[self.lo:self.hi], [x[:n] for x in srcs], s.lr, gscale=weight,
+                                  momentum=s.cfg.momentum, wd=s.cfg.weight_decay, buf=buf, first=s._mom_first, n=n,
+                                  img=self.wire.img[self.lo:self.hi] if bf16_img else None)
+                if not bf16_img:
+                    self.wire.img[self.lo:self.hi].copy_(s.params[self.lo:self.hi])
             else:
-                s.apply_range(self.gshard[:n], weight, self.lo, self.hi)
+                agg = torch.zeros(n, dtype=torch.float32, device=s.device)
+                for x in srcs:  # fixed order, fp32 accumulation
+                    agg.add_(x[:n].to(torch.float32))
+                s.apply_range(agg, weight, self.lo, self.hi)
                 self.wire.img[self.lo:self.hi].copy_(s.params[self.lo:self.hi])
         self.wire.publish_small(s.arena, self.rank)
         s.finish_round_apply()

@@ -55,6 +55,10 @@ class LocalTransport:
     def all_gather_into(self, buf, chunk: int):
         return buf
 
+    def exchange_chunks(self, t, chunk: int, bufs):
+        assert not bufs
+        return bufs
+
     def isend(self, t, dst):
         raise RuntimeError("LocalTransport has no peers")
 
@@ -79,7 +83,9 @@ class DistTransport:
     def __init__(self, backend: str | None = None, device=None, timeout_s: float = 600.0):
         if not dist.is_initialized():
             if backend is None:
-                backend = "nccl" if torch.cuda.is_available() else "gloo"
+                # PSX_DIST_BACKEND=gloo: the torch group on gloo even with GPUs (several ranks
+                # sharing one GPU in tests, where RCCL would refuse the duplicate device)
+                backend = os.environ.get("PSX_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
             kw = {}
             if backend == "nccl" and device is not None:
                 kw["device_id"] = torch.device(device)
@@ -132,6 +138,24 @@ class DistTransport:
             return buf
         dist.all_gather_into_tensor(buf[: chunk * self.world_size], mine)
         return buf
+
+    def exchange_chunks(self, t, chunk: int, bufs):
+        """All-to-all of equal chunks: rank r sends t[p*chunk:(p+1)*chunk] to every rank p != r
+        and receives rank p's chunk r into bufs[p] (sharded server push)."""
+        r = self.rank
+        works = []
+        for p in range(self.world_size):
+            if p == r:
+                continue
+            if p < r:  # deterministic pairing order on both ends
+                works.append(dist.irecv(bufs[p], src=p))
+                works.append(dist.isend(t[p * chunk:(p + 1) * chunk].contiguous(), dst=p))
+            else:
+                works.append(dist.isend(t[p * chunk:(p + 1) * chunk].contiguous(), dst=p))
+                works.append(dist.irecv(bufs[p], src=p))
+        for w in works:
+            w.wait()
+        return bufs
 
     def gather_to_server(self, t):
         """Equal-size tensors of every rank -> list on rank 0 (RCCL gather: point-to-point

@@ -1,0 +1,169 @@
+"""The multi-rank data plane executed for real on ONE MI355X.
+
+RCCL refuses two ranks on one device, so a one-GPU box cannot run NativeComm at world > 1. These
+tests load the test-only RCCL stand-in (csrc/tests/fakecomm.hip: the same C ABI, host-synchronous,
+HIP IPC + shared memory) through ``psx_comm_load`` (PSX_RCCL_LIB) and run 2-3 processes on the
+GPU: the native communicator (parallel/rccl.py NativeComm + csrc/comm/rccl_comm.cpp), the sync
+channels (gathered fp16 wires + fp32 aggregation, broadcast fetch, dedicated / co-located /
+sharded topologies) and bench.py itself — the code the 8-GPU run uses, minus RCCL's kernels.
+The torch control group runs on gloo (PSX_DIST_BACKEND=gloo).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FAKE = os.path.join(ROOT, "distributed-parameter-server-for-ml-training_amd", "_native", "testing",
+                    "libpsx_fakecomm.so")
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env(extra=None):
+    env = dict(os.environ, PYTHONPATH=ROOT, PSX_RCCL_LIB=FAKE, PSX_FAKECOMM_TEST="1", PSX_DIST_BACKEND="gloo",
+               PSX_FAKECOMM_TIMEOUT_S="60", OMP_NUM_THREADS="4")
+    env.pop("CUDA_VISIBLE_DEVICES", None)
+    env.update(extra or {})
+    return env
+
+
+def _torchrun(nproc, argv, timeout=300, extra=None):
+    port = _port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port)] + argv
+    r = subprocess.run(cmd, env=_env(extra), stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=timeout)
+    assert r.returncode == 0, r.stdout[-4000:]
+    return r.stdout
+
+
+def _json_lines(out, key):
+    return [json.loads(ln[ln.index("{"):]) for ln in out.splitlines() if key in ln and "{" in ln]
+
+
+def test_fake_comm_refuses_without_test_gate():
+    code = (f"import sys; sys.path.insert(0, {ROOT!r}); import torch, psx, ctypes as C; "
+            "from psx.ops._lib import comm; lib = comm(); "
+            f"assert lib.psx_comm_load({FAKE!r}.encode()) == 0; "
+            "b = C.create_string_buffer(lib.psx_comm_id_bytes()); assert lib.psx_comm_unique_id(b) == 0; "
+            "h = C.c_void_p(); print('RC', lib.psx_comm_init(b.raw, 1, 0, 0, C.byref(h)))")
+    env = _env()
+    env.pop("PSX_FAKECOMM_TEST")
+    r = subprocess.run([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True, timeout=120)
+    assert "RC 5" in r.stdout, r.stdout[-2000:]  # ncclInvalidUsage
+
+
+_OPS = r"""
+import json, os, sys
+sys.path.insert(0, {root!r})
+import torch
+import psx
+from psx.parallel.rccl import RcclTransport
+t = RcclTransport(device=torch.device("cuda", 0))
+r, w = t.rank, t.world_size
+res = {{}}
+g = torch.full((1 << 16,), float(r + 1), device="cuda").half()
+t.reduce_sum_to_server(g)
+if r == 0:
+    res["reduce"] = float(g[0]) == sum(range(1, w + 1))
+b = torch.full((1000,), float(r), device="cuda")
+if r == 0:
+    b.fill_(7.0)
+t.broadcast_from_server(b)
+res["bcast"] = bool((b == 7.0).all())
+x = torch.full((4096,), float(r + 1), device="cuda")
+bufs = {{p: torch.empty_like(x) for p in range(1, w)}} if r == 0 else None
+t.gather_from_workers(x, bufs)
+if r == 0:
+    res["gather"] = all(bool((bufs[p] == p + 1).all()) for p in range(1, w))
+c = 256
+y = torch.arange(w * c, device="cuda", dtype=torch.float32) + 1000 * r
+rb = {{p: torch.empty(c, device="cuda") for p in range(w) if p != r}}
+t.exchange_chunks(y, c, rb)
+res["alltoall"] = all(bool(torch.equal(rb[p], torch.arange(r * c, (r + 1) * c, device="cuda",
+                                                             dtype=torch.float32) + 1000 * p)) for p in rb)
+z = torch.full((w * 64,), float(r + 1), device="cuda")
+out = torch.empty(64, device="cuda")
+t.reduce_scatter_sum(z, out)
+res["reduce_scatter"] = bool((out == sum(range(1, w + 1))).all())
+ag = torch.zeros(w * 64, device="cuda")
+ag[r * 64:(r + 1) * 64] = r
+t.all_gather_into(ag, 64)
+res["all_gather"] = all(bool((ag[p * 64:(p + 1) * 64] == p).all()) for p in range(w))
+res["async_error"] = t.comm.async_error()
+t.close()
+print("RESULT " + json.dumps(res))
+"""
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_native_collectives_multirank(world, tmp_path):
+    script = tmp_path / "ops.py"
+    script.write_text(_OPS.format(root=ROOT))
+    out = _torchrun(world, [str(script)])
+    recs = _json_lines(out, "RESULT ")
+    assert len(recs) == world, out[-3000:]
+    for rec in recs:
+        assert all(v is True or v == 0 for v in rec.values()), rec
+    assert sum("reduce" in r and "gather" in r for r in recs) == 1  # rank 0's view
+
+
+@pytest.mark.parametrize("world,topology", [(2, "auto"), (3, "auto"), (3, "colocated"), (2, "sharded")])
+def test_bench_multirank(world, topology):
+    """bench.py itself at world 2-3 (fp32 headline path): dedicated (auto), co-located, sharded."""
+    out = _torchrun(world, [os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "3", "--warmup", "2",
+                            "--secondary", "none", "--topology", topology, "--train-samples", "2048"])
+    recs = _json_lines(out, '"metric"')
+    assert len(recs) == 1, out[-3000:]
+    rec = recs[0]
+    want = {"auto": "dedicated"}.get(topology, topology)
+    assert rec["n_gpus"] == world and rec["config"]["topology"] == want, rec
+    assert rec["config"]["workers"] == (world - 1 if want == "dedicated" else world)
+    assert rec["config"]["transport"] == "native RCCL (psx comm)"
+    assert rec["dtype"] == "fp32" and rec["value"] > 0 and rec["global_steps"] == 5, rec
+    assert rec["last_loss"] is None or 0.0 < rec["last_loss"] < 20.0
+
+
+_RUN = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+import psx
+from psx.parallel.runner import {fn}
+from psx.utils.config import PSConfig
+cfg = PSConfig(model="resnet18", batch_size=64, epochs=1, train_samples=1024, eval_every=0, verbose=0, lr=0.1,
+               max_steps=4, mode="sync", topology={topo!r}, workers={W}).validate()
+res = {fn}(cfg, log=lambda *a, **k: None)
+if "server" in res:
+    print("RESULT " + json.dumps([res["server"]["final_param_checksum"], res["server"]["global_steps_completed"]]))
+"""
+
+
+@pytest.mark.parametrize("world,topology", [(2, "colocated"), (3, "dedicated")])
+def test_distributed_sync_matches_loopback(world, topology, tmp_path):
+    """A whole sync PS run at world 2-3 over the native communicator ends in the same master state
+    as the single-process loopback with the same number of simulated workers (same shards, seeds
+    and fp32 aggregation order) — up to the run-to-run noise of the BN statistics."""
+    W = world - 1 if topology == "dedicated" else world
+    dist_py = tmp_path / "dist.py"
+    dist_py.write_text(_RUN.format(root=ROOT, fn="run_distributed", topo=topology, W=W))
+    out = _torchrun(world, [str(dist_py)])
+    got = [r for r in _json_lines(out, "RESULT ") if r]
+    loop_py = tmp_path / "loop.py"
+    loop_py.write_text(_RUN.format(root=ROOT, fn="run_local", topo="colocated", W=W))
+    r = subprocess.run([sys.executable, str(loop_py)], env=_env(), stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:]
+    ref = _json_lines(r.stdout, "RESULT ")[-1]
+    assert len(got) == 1 and got[0][1] == ref[1] == 4, (got, ref)
+    assert abs(got[0][0] - ref[0]) <= 2e-4 * abs(ref[0]), (got, ref)

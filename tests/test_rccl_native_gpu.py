@@ -103,7 +103,7 @@ import psx
 from psx.parallel.runner import run_distributed
 from psx.utils.config import PSConfig
 cfg = PSConfig(model="resnet18", batch_size=64, epochs=1, train_samples=2048, eval_every=1, test_samples=256,
-               verbose=0, lr=0.1, max_steps=6, mode="sync", use_graph={graph!r}).validate()
+               verbose=0, lr=0.1, max_steps=6, mode="sync", use_graph={graph!r}, dtype="bf16").validate()
 import psx.parallel.runner as R
 made = []
 _mk = R.make_sync_channel

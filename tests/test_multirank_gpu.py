@@ -48,7 +48,15 @@ def _torchrun(nproc, argv, timeout=300, extra=None):
 
 
 def _json_lines(out, key):
-    return [json.loads(ln[ln.index("{"):]) for ln in out.splitlines() if key in ln and "{" in ln]
+    recs = []
+    for ln in out.splitlines():
+        if key not in ln:
+            continue
+        if key == "RESULT ":
+            recs.append(json.loads(ln.split("RESULT ", 1)[1]))
+        elif "{" in ln:
+            recs.append(json.loads(ln[ln.index("{"):]))
+    return recs
 
 
 def test_fake_comm_refuses_without_test_gate():

@@ -10,6 +10,7 @@ The torch control group runs on gloo (PSX_DIST_BACKEND=gloo).
 """
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -48,15 +49,10 @@ def _torchrun(nproc, argv, timeout=300, extra=None):
 
 
 def _json_lines(out, key):
-    recs = []
-    for ln in out.splitlines():
-        if key not in ln:
-            continue
-        if key == "RESULT ":
-            recs.append(json.loads(ln.split("RESULT ", 1)[1]))
-        elif "{" in ln:
-            recs.append(json.loads(ln[ln.index("{"):]))
-    return recs
+    """RESULT records (flat dicts / lists; ranks' lines may interleave) or whole-line JSON."""
+    if key == "RESULT ":
+        return [json.loads(m.group(1)) for m in re.finditer(r"RESULT (\{[^{}]*\}|\[[^\[\]]*\])", out)]
+    return [json.loads(ln[ln.index("{"):]) for ln in out.splitlines() if key in ln and "{" in ln]
 
 
 def test_fake_comm_refuses_without_test_gate():

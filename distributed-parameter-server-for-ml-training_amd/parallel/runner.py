@@ -39,7 +39,8 @@ from .server import ParameterServer
 from .rccl import make_transport
 from .sharded import ShardedSyncChannel
 from .transport import LocalTransport, env_world
-from .worker import (AsyncChannel, InProcessChannel, LocalAsyncChannel, SyncCollectiveChannel, Worker)
+from .worker import (AsyncChannel, InProcessChannel, LocalAsyncChannel, SyncCollectiveChannel, Worker,
+                     rounds_to_batches)
 
 
 def _device_for(local_rank: int):
@@ -352,10 +353,11 @@ def _dedicated_sync_server(cfg, server, chan, steps, device, skip=0):
     else:
         zeros = torch.zeros(server.n, dtype=_wire_dtype(cfg), device=device)
     zbuf = torch.zeros(server.layout.buffer_numel, dtype=torch.float32, device=device) if cfg.bn_sync else None
-    done = skip
+    skip_b = rounds_to_batches(skip, steps, K)  # checkpointed rounds -> batches (window aligned)
+    done = skip_b
     for epoch in range(cfg.epochs):
         for b in range(steps):
-            if epoch * steps + b < skip:
+            if epoch * steps + b < skip_b:
                 continue
             if b % K == 0:
                 chan.fetch(None, None)

@@ -176,12 +176,16 @@ class ParameterServer:
         self.bytes_fetched += w.nbytes
         return w, gs
 
-    def push_gradients(self, worker_id: int, grads: torch.Tensor, local_step: int) -> bool:
+    def push_gradients(self, worker_id: int, grads: torch.Tensor, local_step: int, buffers=None) -> bool:
         """In-process push (single-process loopback runs). Sync: aggregate until the barrier
-        completes, then apply the average. Async: staleness check + weighted apply."""
+        completes, then apply the average. Async: staleness check + weighted apply.
+        ``buffers`` (--bn-sync): the worker's BN running statistics, counted only when the core
+        takes the push into the round (a duplicate / unknown / rejected push contributes nothing)."""
         self.bytes_pushed += grads[: self.n].numel() * grads.element_size()
         res = self.core.on_push(worker_id, local_step)
         self.last_push = res
+        if buffers is not None and (res.decision in (WAIT, APPLY) if self.cfg.mode == "sync" else res.accepted):
+            self.push_buffers(worker_id, buffers)
         if self.cfg.mode == "sync":
             if self.cfg.sync_semantics == "reference":
                 # reference: pending[worker_id] = grads (overwrites), average over the dict

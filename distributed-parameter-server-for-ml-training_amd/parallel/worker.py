@@ -32,6 +32,17 @@ from ..utils.data import EpochSampler, shard_range
 from . import control as CP
 
 
+def rounds_to_batches(rounds: int, steps_per_epoch: int, K: int) -> int:
+    """Batches a worker has consumed after ``rounds`` completed push rounds (restart recovery):
+    each epoch has ceil(steps/K) rounds (one per --sync-steps window; with --accumulate the last
+    window may be partial), and a checkpointed round ends a whole window, so the worker resumes
+    at the first batch of the next window."""
+    K = max(1, K)
+    per_epoch = max(1, -(-steps_per_epoch // K))
+    epochs, rem = divmod(max(0, rounds), per_epoch)
+    return epochs * steps_per_epoch + min(rem * K, steps_per_epoch)
+
+
 class InProcessChannel:
     """``wire``: a WeightWire (parallel/codec.py) the worker's step reads its conv weights from
     (ParameterServer.enable_weight_wire must be on). A worker WeightWire of its own receives one
@@ -67,9 +78,7 @@ class InProcessChannel:
         return gs
 
     def push(self, worker_id, grads, local_step, buffers=None):
-        if buffers is not None:
-            self.server.push_buffers(worker_id, buffers)
-        return self.server.push_gradients(worker_id, grads, local_step)
+        return self.server.push_gradients(worker_id, grads, local_step, buffers=buffers)
 
     def finished(self, worker_id):
         self.server.job_finished(worker_id, emit=self.emit_on_last)
@@ -386,15 +395,19 @@ class Worker:
             torch.cuda.synchronize()
 
     def run_training(self, skip_steps: int = 0):
-        """The reference training loop (worker.py:350-403). ``skip_steps`` fast-forwards past
-        rounds that a resumed server checkpoint already contains (restart recovery)."""
+        """The reference training loop (worker.py:350-403). ``skip_steps`` = push rounds that a
+        resumed server checkpoint already contains (restart recovery): the worker fast-forwards
+        past the batches of those rounds (rounds_to_batches) and keeps each epoch's absolute batch
+        index, so the --sync-steps windows (fetch / push points) stay where they were."""
         if self.sampler is None:
             self.setup_data()
         self.log(f"\n--- Starting distributed training for {self.num_epochs} epochs ---")
-        if skip_steps:
-            self.log(f"[Resume] worker {self.worker_id} skips {skip_steps} completed steps")
-        self.training_start_time = time.time()
         K = self.local_steps_per_sync
+        if skip_steps:
+            rounds = skip_steps
+            skip_steps = rounds_to_batches(rounds, len(self.sampler.epoch_indices(0)), K)
+            self.log(f"[Resume] worker {self.worker_id} skips {rounds} completed rounds ({skip_steps} batches)")
+        self.training_start_time = time.time()
         fi_worker, fi_step = _parse_fault(self.cfg.fault_inject)
         try:
             for epoch in range(self.num_epochs):
@@ -405,11 +418,11 @@ class Worker:
                     skip_steps -= len(batches)
                     self.local_step_counter += len(batches)
                     continue
-                if skip_steps:
-                    self.local_step_counter += skip_steps
-                    batches = batches[skip_steps:]
-                    skip_steps = 0
-                for batch_idx, idx in enumerate(batches):
+                start = skip_steps
+                self.local_step_counter += start
+                skip_steps = 0
+                for batch_idx in range(start, len(batches)):
+                    idx = batches[batch_idx]
                     if fi_worker == self.worker_id and self.local_step_counter == fi_step:
                         raise _InjectedFault(f"fault injected: worker {self.worker_id} at step {fi_step}")
                     if batch_idx % K == 0:

@@ -441,3 +441,39 @@ def test_sync_round_fp32_aggregation(topology):
     assert res["gs"] == 1
     assert res["err"] < 1e-6, res  # fp32 rounding of the update only
     assert res["err_fp16_sum"] > 10 * res["err"], res  # what an fp16 running sum would have cost
+
+
+def test_rounds_to_batches():
+    from psx.parallel.worker import rounds_to_batches
+
+    assert rounds_to_batches(0, 12, 2) == 0
+    assert rounds_to_batches(3, 12, 2) == 6            # windows of 2: round r ends at batch 2r
+    assert rounds_to_batches(7, 12, 2) == 12 + 2        # 6 rounds per epoch
+    assert rounds_to_batches(4, 13, 3) == 12            # ceil(13/3) = 5 rounds per epoch (last window partial)
+    assert rounds_to_batches(5, 13, 3) == 13            # epoch 1 fully done at its 5th round
+    assert rounds_to_batches(6, 13, 3) == 13 + 3
+    assert rounds_to_batches(5, 10, 1) == 5
+
+
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_fault_restart_with_sync_steps_odd_checkpoint(tmp_path, accumulate):
+    """--sync-steps 2 with a checkpoint every 3 rounds (odd): after the restart the workers skip
+    exactly the batches of the checkpointed rounds, keep their window alignment, and the job
+    ends with the fault-free number of rounds (no round re-run, no collective mismatch)."""
+    ck = tmp_path / "ck"
+    # the fault hits right after round 3: the window's first batch (reference rule, local step 5)
+    # or its last (--accumulate, local step 6)
+    fault = "kill_worker:1@6" if accumulate else "kill_worker:1@5"
+    args = ["--mode", "sync", "--epochs", "2", "--sync-steps", "2", "--ckpt-every", "3", "--ckpt-dir", str(ck),
+            "--resume", "latest", "--fault-inject", fault, "--verbose", "1"]
+    if accumulate:
+        args.append("--accumulate")
+    tiny = list(TINY)
+    for opt in ("--epochs", "--verbose"):
+        i = tiny.index(opt)
+        del tiny[i:i + 2]
+    recs, out = _spawn(3, args + tiny, max_restarts=1)
+    assert "fault injected" in out and "[Resume] restored global step 3" in out, out[-3000:]
+    steps = -(-(96 // 3) // 8)
+    srv = [r for r in recs if r["type"] == "SERVER_FINAL_METRICS"]
+    assert srv[-1]["global_steps_completed"] == 2 * -(-steps // 2)

@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
                                                             const float* __restrict__ mean2,
                                                             const float* __restrict__ invstd2, float* __restrict__ part,
                                                             int npix, int C, int pix_per_block, int fuse_fin,
-                                                            BnBwdFin fin1, BnBwdFin fin2) {
+                                                            BnBwdFin fin1, BnBwdFin fin2, DetRed det) {
   constexpr int NS = TWO ? 3 : 2;
   extern __shared__ __attribute__((aligned(16))) float sred[];  // [256][NS*8]
   const int cvec = C >> 3;
@@ -163,7 +163,17 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
     float acc = 0.f;
     for (int q = 0; q < tpp; ++q) acc += sred[(q * cvec + cgi) * (NS * 8) + sj];
     const int stat = sj >> 3, j = sj & 7;
-    atomicAdd(part + ((size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * NS + stat) * C + cgi * 8 + j, acc);
+    if (det.slab)
+      atomicAdd(det.slab + ((size_t)blockIdx.x * NS + stat) * C + cgi * 8 + j, acc);
+    else
+      atomicAdd(part + ((size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * NS + stat) * C + cgi * 8 + j, acc);
+  }
+  if (det.slab) {
+    if (det_finish(det, NS, C, part, gridDim.x, reinterpret_cast<unsigned char*>(sred)) && fuse_fin) {
+      bn_bwd_finalize_block<PSX_STAT_SLOTS>(part, NS, 1, fin1);
+      if (TWO) bn_bwd_finalize_block<PSX_STAT_SLOTS>(part, NS, 2, fin2);
+    }
+    return;
   }
   // in-launch finalize (bnfin.hpp): the last block computes the coefficients + dgamma/dbeta
   if (fuse_fin && last_block_arrive(fin1.counter, gridDim.x, reinterpret_cast<unsigned char*>(sred))) {
@@ -370,6 +380,29 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin_kernel(const T* __restri
   }
 }
 
+// ---- deterministic mode host state (bnfin.hpp DetRed)
+namespace {
+struct DetState {
+  float* slab = nullptr;
+  long slab_floats = 0;
+  unsigned* counters = nullptr;
+  int ncounters = 0;
+  int next = 0;
+};
+DetState g_det;
+}  // namespace
+
+bool det_enabled() { return g_det.slab != nullptr; }
+
+DetRed det_next(int rows, int NS, int C) {
+  DetRed d{nullptr, nullptr, 0};
+  if (!g_det.slab || (long)rows * NS * C > g_det.slab_floats) return d;
+  d.slab = g_det.slab;
+  d.counter = g_det.counters + (g_det.next++ % g_det.ncounters);
+  d.rows = rows;
+  return d;
+}
+
 }  // namespace psx
 
 using namespace psx;
@@ -391,6 +424,24 @@ static int ew_grid(size_t nvec) {
 }
 
 extern "C" {
+
+// Deterministic mode on (buf = a zeroed device buffer of `bytes`, >= 4 KiB: 64 launch counters +
+// the row slab) or off (buf = nullptr). Every later producer of BN sums (conv epilogues, split-K
+// epilogue, bn_bwd_reduce, the head) reduces through it (bnfin.hpp DetRed). Host state only:
+// set it before a HIP graph is captured.
+int psx_set_deterministic(void* buf, long bytes) {
+  if (!buf) {
+    g_det = DetState{};
+    return 0;
+  }
+  if (bytes < 4096) return -2;
+  g_det.counters = (unsigned*)buf;
+  g_det.ncounters = 64;
+  g_det.slab = (float*)((char*)buf + 256);
+  g_det.slab_floats = (bytes - 256) / 4;
+  g_det.next = 0;
+  return 0;
+}
 
 int psx_bn_finalize(const float* part, int T, int C, float count, const float* gamma, const float* beta, float eps,
                     float momentum, float* run_mean, float* run_var, float* scale, float* shift, float* save_mean,
@@ -450,16 +501,17 @@ int psx_bn_bwd_reduce(const void* g, const void* o, const void* y1, const float*
   if (!part) return PSX_STAT_SLOTS;
   const bool mask = o != nullptr, two = y2 != nullptr;
   const size_t lds = 256 * (two ? 3 : 2) * 8 * sizeof(float);
+  const DetRed det = det_next(T, two ? 3 : 2, C);
 #define PSX_BBR(M, TW)                                                                                         \
   do {                                                                                                         \
     if (f32)                                                                                                   \
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, M, TW>), dim3(T), dim3(256), lds, st, (const float*)g,   \
                          (const float*)o, (const float*)y1, mean1, invstd1, (const float*)y2, mean2, invstd2,  \
-                         part, npix, C, ppb, fuse, f1, f2);                                                    \
+                         part, npix, C, ppb, fuse, f1, f2, det);                                               \
     else                                                                                                       \
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<uint16_t, M, TW>), dim3(T), dim3(256), lds, st,                 \
                          (const uint16_t*)g, (const uint16_t*)o, (const uint16_t*)y1, mean1, invstd1,          \
-                         (const uint16_t*)y2, mean2, invstd2, part, npix, C, ppb, fuse, f1, f2);               \
+                         (const uint16_t*)y2, mean2, invstd2, part, npix, C, ppb, fuse, f1, f2, det);          \
   } while (0)
   if (mask && two) PSX_BBR(true, true);
   else if (mask) PSX_BBR(true, false);

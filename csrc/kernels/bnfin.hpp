@@ -64,6 +64,52 @@ PSX_DEV bool last_block_arrive(unsigned* counter, unsigned nblocks, unsigned cha
   return last;
 }
 
+// ---------------------------------------------------------------------------------------
+// Deterministic mode (psx_set_deterministic, bn.hip): a launch that produces per-channel sums
+// adds each workgroup's partial row into a row of its own of a scratch slab [rows][NS][C] —
+// exactly one add per location into zeros, so the value is exact whatever the order — and its
+// last-arriving workgroup sums the rows in a fixed order into slot row 0 of the usual
+// [PSX_STAT_SLOTS][NS][C] buffer (the other slot rows stay zero), then re-zeroes the slab and
+// its counter for the next launch. The consumers are unchanged and sum the slot rows in a fixed
+// order, so every BN statistic — and with it the whole step — is bit-reproducible. The slab
+// adds are memory-side float atomics (no release needed, as for the slots); the slab lines the
+// last workgroup reads were never cached by this launch, and kernel boundaries write back and
+// invalidate the non-coherent L2 lines of the previous launch's re-zeroing.
+struct DetRed {
+  float* slab;        // nullptr: deterministic mode off
+  unsigned* counter;  // zero at launch, re-zeroed by the last workgroup
+  int rows;
+};
+
+// every workgroup of the launch calls this (block-uniformly) after its slab adds; returns true
+// in the last-arriving workgroup (after the fixed-order reduction, so an in-launch finalize of
+// the same sums can follow)
+PSX_DEV bool det_finish(const DetRed& d, int NS, int C, float* part, unsigned nblocks, unsigned char* lds) {
+  if (!last_block_arrive(d.counter, nblocks, lds)) return false;
+  const size_t stride = (size_t)NS * C;
+  for (int j = threadIdx.x; j < NS * C; j += blockDim.x) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int r = 0;
+    for (; r + 3 < d.rows; r += 4) {
+      s0 += d.slab[(size_t)r * stride + j];
+      s1 += d.slab[(size_t)(r + 1) * stride + j];
+      s2 += d.slab[(size_t)(r + 2) * stride + j];
+      s3 += d.slab[(size_t)(r + 3) * stride + j];
+    }
+    for (; r < d.rows; ++r) s0 += d.slab[(size_t)r * stride + j];
+    part[j] = (s0 + s1) + (s2 + s3);
+    for (r = 0; r < d.rows; ++r) d.slab[(size_t)r * stride + j] = 0.f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(d.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+// host: the DetRed of the next producing launch (slab rows for `rows` x NS x C sums), or a
+// disabled one when deterministic mode is off / the slab is too small (bn.hip)
+DetRed det_next(int rows, int NS, int C);
+bool det_enabled();
+
 // part: [T][2][C] slot rows (sum, sum of squares). Same math as bn_finalize_kernel (bn.hip).
 // One thread per channel, all T slot loads issued back to back: the slot sums sit at the
 // memory side (float atomics bypass L2), so a per-channel-group LDS reduction would pay one

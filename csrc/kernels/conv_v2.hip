@@ -44,6 +44,7 @@ struct Conv2Args {
   const float* bsaved1;  // [2][OC] mean, invstd
   const float* bsaved2;
   int bns;
+  DetRed det;  // deterministic mode: the launch's row slab (bnfin.hpp)
 };
 
 PSX_DEV int kmaj2(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
@@ -124,7 +125,13 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   const int npix_c = MODE == 3 ? a.Nb * CH * CW : a.npix;
   if (MODE == 3) {
     nk = (nr * nsx) << (a.log2_icc - 3);
-    if (pix0 >= npix_c) return;  // whole workgroup: this class has fewer tiles
+    if (pix0 >= npix_c) {  // whole workgroup: this class has fewer tiles
+      if (!SPLIT && a.det.slab && (a.stats || a.bpart))  // it still arrives at the launch counter
+        if (det_finish(a.det, a.bpart ? a.bns : 2, a.OC, a.bpart ? a.bpart : a.stats, gridDim.x * gridDim.y, smem) &&
+            a.stats && a.fuse_fin)
+          bn_finalize_block<PSX_STAT_SLOTS>(a.stats, a.fin);
+      return;
+    }
   }
 
   f32x4 acc[MT][NT];
@@ -478,12 +485,18 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     }
     __syncthreads();
     const int nst = bwd ? a.bns : 2;
-    float* dst = (bwd ? a.bpart : a.stats) + (size_t)(pix_t & (PSX_STAT_SLOTS - 1)) * nst * a.OC;
+    float* dst = a.det.slab ? a.det.slab + (size_t)(pix_t + (MODE == 3 ? cls * a.n_pix_tiles : 0)) * nst * a.OC
+                            : (bwd ? a.bpart : a.stats) + (size_t)(pix_t & (PSX_STAT_SLOTS - 1)) * nst * a.OC;
     for (int j = tid; j < nst * BM; j += 256) {
       const int which = j / BM, row = j - which * BM;
       const float v = red[which * BM + row] + red[(3 + which) * BM + row] + red[(6 + which) * BM + row] +
                       red[(9 + which) * BM + row];
       atomicAdd(dst + which * a.OC + oc0 + row, v);
+    }
+    if (a.det.slab) {
+      if (det_finish(a.det, nst, a.OC, bwd ? a.bpart : a.stats, gridDim.x * gridDim.y, smem) && st && a.fuse_fin)
+        bn_finalize_block<PSX_STAT_SLOTS>(a.stats, a.fin);
+      return;
     }
     if (st && a.fuse_fin && last_block_arrive(a.fin.counter, gridDim.x, smem))
       bn_finalize_block<PSX_STAT_SLOTS>(a.stats, a.fin);
@@ -504,7 +517,8 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
                                                             const T* __restrict__ by1,
                                                             const T* __restrict__ by2,
                                                             const float* __restrict__ bsaved1,
-                                                            const float* __restrict__ bsaved2, int bns) {
+                                                            const float* __restrict__ bsaved2, int bns,
+                                                            DetRed det) {
   extern __shared__ __attribute__((aligned(16))) float sred[];  // [256][24]
   const int cvec = OC >> 3, tpp = 256 / cvec;
   const int cg = threadIdx.x % cvec, pr = threadIdx.x / cvec;
@@ -571,13 +585,20 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
     mine[16 + j] = st[2][j];
   }
   __syncthreads();
-  float* dst = (bwd ? bpart : stats) + (size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * nst * OC;
+  float* dst = det.slab ? det.slab + (size_t)blockIdx.x * nst * OC
+                        : (bwd ? bpart : stats) + (size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * nst * OC;
   for (int t = threadIdx.x; t < cvec * nst * 8; t += 256) {
     const int cgi = t / (nst * 8), sj = t - cgi * (nst * 8);
     float acc = 0.f;
     for (int q = 0; q < tpp; ++q) acc += sred[(q * cvec + cgi) * 24 + sj];
     const int which = sj >> 3, j = sj & 7;
     atomicAdd(dst + which * OC + cgi * 8 + j, acc);
+  }
+  if (det.slab) {
+    if (det_finish(det, nst, OC, bwd ? bpart : stats, gridDim.x, reinterpret_cast<unsigned char*>(sred)) && stats &&
+        fuse_fin)
+      bn_finalize_block<PSX_STAT_SLOTS>(stats, fin);
+    return;
   }
   if (!stats) return;
   if (fuse_fin && last_block_arrive(fin.counter, gridDim.x, reinterpret_cast<unsigned char*>(sred)))
@@ -628,11 +649,18 @@ Plan plan_for(int OC, int npix, int ksteps, bool f32 = false) {
   return p;
 }
 
+// deterministic mode: this launch's slab rows (one per pixel tile, per parity class for MODE 3)
+void with_det(Conv2Args& b, int rows) {
+  if (b.stats || b.bpart) b.det = det_next(rows, b.bpart ? b.bns : 2, b.OC);
+}
+
 template <typename T, int BM, int BN, int MODE, bool RES, bool SPLIT, int WGM = 2>
 int launch2(const Conv2Args& a, hipStream_t st) {
   const size_t lds = (size_t)3 * (BM + BN) * 128;
   dim3 grid(a.n_oc_tiles * a.n_pix_tiles, SPLIT ? a.splits : (MODE == 3 ? 4 : 1));
-  hipLaunchKernelGGL((conv2_kernel<T, BM, BN, MODE, RES, SPLIT, WGM>), grid, dim3(256), lds, st, a);
+  Conv2Args b = a;
+  if (!SPLIT) with_det(b, a.n_pix_tiles * (MODE == 3 ? 4 : 1));
+  hipLaunchKernelGGL((conv2_kernel<T, BM, BN, MODE, RES, SPLIT, WGM>), grid, dim3(256), lds, st, b);
   return (int)hipGetLastError();
 }
 
@@ -657,8 +685,10 @@ int dispatch2(const Plan& p, const Conv2Args& a, hipStream_t st) {
 template <typename T, int BM, int BN, int MODE, bool RES, int WGM, int TP = 1>
 int launch_tapr(const Conv2Args& a, hipStream_t st) {
   const size_t lds = (size_t)2 * (3 * BM * 128 + (TP == 2 ? BN + 8 : BN + 1) * 128);
+  Conv2Args b = a;
+  with_det(b, a.n_pix_tiles);
   hipLaunchKernelGGL((conv2_kernel<T, BM, BN, MODE, RES, false, WGM, TP>), dim3(a.n_oc_tiles * a.n_pix_tiles),
-                     dim3(256), lds, st, a);
+                     dim3(256), lds, st, b);
   return (int)hipGetLastError();
 }
 
@@ -707,14 +737,16 @@ int finish_split(const Conv2Args& a, hipStream_t st) {
   if (ppb < 8) ppb = 8;
   const int grid = (a.npix + ppb - 1) / ppb;
   const size_t lds = 256 * 24 * sizeof(float);
+  DetRed det{nullptr, nullptr, 0};
+  if (a.stats || a.bpart) det = det_next(grid, a.bpart ? a.bns : 2, a.OC);
   if (a.res)
     hipLaunchKernelGGL((conv_splitk_epilogue<T, true>), dim3(grid), dim3(256), lds, st, a.part, a.splits, a.npix,
                        a.OC, (T*)a.out, (const T*)a.res, a.stats, ppb, a.fuse_fin, a.fin, a.bpart, (const T*)a.bo,
-                       (const T*)a.by1, (const T*)a.by2, a.bsaved1, a.bsaved2, a.bns);
+                       (const T*)a.by1, (const T*)a.by2, a.bsaved1, a.bsaved2, a.bns, det);
   else
     hipLaunchKernelGGL((conv_splitk_epilogue<T, false>), dim3(grid), dim3(256), lds, st, a.part, a.splits, a.npix,
                        a.OC, (T*)a.out, (const T*)nullptr, a.stats, ppb, a.fuse_fin, a.fin, a.bpart, (const T*)a.bo,
-                       (const T*)a.by1, (const T*)a.by2, a.bsaved1, a.bsaved2, a.bns);
+                       (const T*)a.by1, (const T*)a.by2, a.bsaved1, a.bsaved2, a.bns, det);
   return (int)hipGetLastError();
 }
 

@@ -4,6 +4,7 @@
 // Replaces nn.AdaptiveAvgPool2d((1,1)), nn.Linear and nn.CrossEntropyLoss of the reference
 // (reference: src/parameter_server/server.py:56-57,73-75; src/workers/worker.py:133,342) and
 // the accuracy count of evaluate_model (worker.py:324-326).
+#include "bnfin.hpp"
 #include "common.hpp"
 
 namespace psx {
@@ -31,7 +32,7 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ act, in
                                                    const int* __restrict__ labels, float* __restrict__ pooled,
                                                    float* __restrict__ dlogits, T* __restrict__ dact,
                                                    float* __restrict__ loss, int* __restrict__ correct, float invB,
-                                                   HeadBnStats bs) {
+                                                   HeadBnStats bs, DetRed det) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
   float* sp = sh;      // [C]  pooled
   float* sl = sh + C;  // [K]  logits -> dlogits
@@ -142,13 +143,14 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ act, in
         x0 += d0 * (y0 - m0) * i0;
         x1 += d1 * (y1v - m1) * i1;
       }
-      float* dst = bs.part + (size_t)(b & (PSX_STAT_SLOTS - 1)) * 2 * C;
+      float* dst = det.slab ? det.slab + (size_t)b * 2 * C : bs.part + (size_t)(b & (PSX_STAT_SLOTS - 1)) * 2 * C;
       atomicAdd(dst + c, z0);
       atomicAdd(dst + c + 1, z1);
       atomicAdd(dst + C + c, x0);
       atomicAdd(dst + C + c + 1, x1);
     }
   }
+  if (det.slab) det_finish(det, 2, C, bs.part, gridDim.x, reinterpret_cast<unsigned char*>(sh));
 }
 
 // dW[k][c] = sum_b dlogits[b][k] * pooled[b][c]; db[k] = sum_b dlogits[b][k].
@@ -374,7 +376,7 @@ int head_fwd_bwd_t(const void* act, int B, int HW, int C, const float* fcw, cons
                        pooled, dlogits, (long)B * K);
     // logits: split-K over the C-long dot products (a 2048 x 1000 head at B = 128 is only 64
     // output tiles; 16 splits of 128 channels fill the chip)
-    const int ks = C >= 1024 ? 16 : 4;
+    const int ks = det_enabled() ? 1 : (C >= 1024 ? 16 : 4);  // deterministic mode: one add per logit
     hipLaunchKernelGGL((head_gemm_kernel<true, 0>), dim3((K + 63) / 64, (B + 31) / 32, ks), dim3(256), 0, st,
                        pooled, fcw, B, K, C, fcb, dlogits, (uint16_t*)nullptr, HW);
     hipLaunchKernelGGL(head_softmax_kernel, dim3(B), dim3(64), 0, st, dlogits, K, labels, loss, correct,
@@ -388,12 +390,13 @@ int head_fwd_bwd_t(const void* act, int B, int HW, int C, const float* fcw, cons
   if (K > 1024 || C % 16 || (C > 512 && C % 512)) return -2;
   const size_t lds = (size_t)(C + K + 64) * sizeof(float);
   const HeadBnStats bs = (bst && dact) ? *bst : HeadBnStats{};
+  const DetRed det = bs.part ? det_next(B, 2, C) : DetRed{nullptr, nullptr, 0};
   if (dact)
     hipLaunchKernelGGL((head_kernel<T, true>), dim3(B), dim3(256), lds, st, (const T*)act, HW, C, fcw, fcb, K,
-                       labels, pooled, dlogits, (T*)dact, loss, correct, 1.f / (float)B, bs);
+                       labels, pooled, dlogits, (T*)dact, loss, correct, 1.f / (float)B, bs, det);
   else
     hipLaunchKernelGGL((head_kernel<T, false>), dim3(B), dim3(256), lds, st, (const T*)act, HW, C, fcw, fcb, K,
-                       labels, pooled, dlogits, (T*)nullptr, loss, correct, 1.f / (float)B, bs);
+                       labels, pooled, dlogits, (T*)nullptr, loss, correct, 1.f / (float)B, bs, DetRed{});
   const int e = (int)hipGetLastError();
   return e ? -e : (bs.part ? 1 : 0);
 }

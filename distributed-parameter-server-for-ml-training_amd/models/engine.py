@@ -160,7 +160,7 @@ class HipResNetEngine:
 
     def __init__(self, model: torch.nn.Module, layout: ParamLayout, batch: int, device="cuda",
                  grad_dtype=torch.float16, in_hw=(32, 32), mean=CIFAR_MEAN, std=CIFAR_STD, bn_eps=1e-5,
-                 bn_momentum=0.1, seed=1234, dtype=torch.bfloat16):
+                 bn_momentum=0.1, seed=1234, dtype=torch.bfloat16, deterministic=None):
         if not torch.cuda.is_available():
             raise RuntimeError("HipResNetEngine needs an MI355X (torch.cuda / HIP device)")
         K.unpack_desc_size()  # fail loudly right here if the native library is missing
@@ -175,6 +175,11 @@ class HipResNetEngine:
             raise ValueError(f"engine dtype {dtype}: bfloat16 or float32")
         self.dtype = dtype
         self.f32 = dtype == torch.float32
+        # deterministic mode: every BN statistic reduced in a fixed order (no atomic-order
+        # dependence), so two runs of a step give bit-identical gradients (PSX_DETERMINISTIC=1)
+        if deterministic is None:
+            deterministic = os.environ.get("PSX_DETERMINISTIC", "0") == "1"
+        self.deterministic = bool(deterministic)
         self.mean, self.std = mean, std
         self.eps, self.mom = bn_eps, bn_momentum
         self.seed = seed
@@ -341,6 +346,16 @@ class HipResNetEngine:
             h_in = d["out"]
         self.final = h_in
         self.red = self._f32(red_off[0])
+        self.det_buf = None
+        if self.deterministic:
+            # row slab: the most rows x stat rows x channels any producer uses (split-K epilogue
+            # rows >= 8 pixels each, conv tiles >= 64 pixels, <= 512 bn_bwd_reduce blocks, B head rows)
+            need = 0
+            for cs in all_convs(sp):
+                oh, ow = cs.out_hw
+                need = max(need, (B * oh * ow // 8 + 64) * 3 * cs.cout, (B * cs.h * cs.w // 8 + 64) * 3 * cs.cp)
+            need = max(need, 3 * 1024 * max(b.convs[-1].cout for b in sp.blocks), B * 2 * sp.fc_in)
+            self.det_buf = torch.zeros(64 + need, dtype=torch.float32, device=self.dev)
         self.wpart = self._f32(max(1, max_wg))
         self.wpart_w = self._f32(max(1, self._plan_wpart(max_wp)))
         # head
@@ -619,6 +634,9 @@ class HipResNetEngine:
         self._zeroed = train
 
     def forward(self, arena: torch.Tensor, train: bool = True):
+        # the kernel library's deterministic-reduction state is process-wide host state: every
+        # step (and every captured graph) takes this engine's setting
+        K.set_deterministic(self.det_buf if self.deterministic else None)
         sp, B = self.spec, self.B
         st = sp.stem_conv
         zeroed, self._zeroed = self._zeroed, False

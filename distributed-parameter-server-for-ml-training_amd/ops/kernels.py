@@ -64,6 +64,23 @@ def conv_dgrad(dy, wd, dx, res, nb, h, w, ic_fwd, oc_fwd, k, stride, pad, kgd, c
 _ZERO_PAGES = {}
 
 
+_DET_BUF = None  # keeps the deterministic-mode scratch alive while the library points at it
+
+
+def set_deterministic(buf):
+    """Deterministic BN reductions (csrc/kernels/bnfin.hpp DetRed) through ``buf`` (a zeroed
+    device tensor of >= 4 KiB: 64 launch counters + the row slab), or off with None. Host state
+    of the kernel library: set it before capturing a HIP graph."""
+    global _DET_BUF
+    if buf is None:
+        check(kernels().psx_set_deterministic(None, 0), "set_deterministic")
+        _DET_BUF = None
+        return
+    assert buf.is_contiguous() and buf.is_cuda
+    check(kernels().psx_set_deterministic(ptr(buf), buf.numel() * buf.element_size()), "set_deterministic")
+    _DET_BUF = buf
+
+
 def is_f32(t) -> int:
     """1 when an activation / operand tensor is fp32 (the fp32 compute path), 0 for bf16."""
     if t.dtype == torch.float32:

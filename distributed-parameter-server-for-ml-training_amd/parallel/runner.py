@@ -94,7 +94,8 @@ def run_local(cfg, log=print) -> dict:
     for w in range(W):
         m = model if w == 0 else build_model(cfg.model, cfg.num_classes, seed=cfg.seed)
         comp = make_compute(m, layout, cfg.batch_size, device, cfg.model, _wire_dtype(cfg), seed=cfg.seed + w,
-                            use_graph=cfg.use_graph, dtype=cfg.dtype)
+                            use_graph=cfg.use_graph, dtype=cfg.dtype,
+                            deterministic=cfg.deterministic)
         wk = Worker(cfg, comp, make_local_channel(cfg, server, layout, device), train, test,
                     worker_name=f"{cfg.worker_name}-{w}", rank=0, log=log, requested_id=w,
                     steps_per_epoch=_common_steps(cfg, W, len(train)))
@@ -188,7 +189,8 @@ def run_distributed(cfg, log=print) -> dict:
     wk = None
     if is_worker:
         comp = make_compute(model, layout, cfg.batch_size, device, cfg.model, _wire_dtype(cfg),
-                            seed=cfg.seed + wid_of_rank[rank], use_graph=cfg.use_graph, dtype=cfg.dtype)
+                            seed=cfg.seed + wid_of_rank[rank], use_graph=cfg.use_graph, dtype=cfg.dtype,
+                            deterministic=cfg.deterministic)
     # restart recovery: a server that resumed from a checkpoint tells every rank how many
     # global steps are already done (sync: one round per step; async: spread over workers)
     done = t.broadcast_object(server.core.global_step if rank == 0 else None)

@@ -322,8 +322,13 @@ ncclResult_t ncclCommInitRank(ncclComm_t* out, int nranks, ncclUniqueId id, int 
 
 static ncclResult_t release(Comm* c, bool abort) {
   if (!c) return ncclSuccess;
-  if (abort) c->shm->aborted.store(1);
-  if (!abort) barrier(c);  // every rank is done reading the others' buffers
+  if (abort) {
+    // ncclCommAbort may come from another thread while this rank's collectives spin on the
+    // segment (the liveness watchdog): flag every rank and keep the mapping alive (leaked)
+    c->shm->aborted.store(1);
+    return ncclSuccess;
+  }
+  barrier(c);  // every rank is done reading the others' buffers
   for (auto& kv : c->mapped) hipIpcCloseMemHandle(kv.second);
   if (c->shm->left.fetch_add(1) + 1 == c->nranks) shm_unlink(c->name.c_str());
   munmap(c->shm, sizeof(Shm));

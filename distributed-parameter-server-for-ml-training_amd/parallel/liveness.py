@@ -1,0 +1,116 @@
+"""Liveness guard of the synchronous round.
+
+The reference's liveness is gRPC keepalive + registration retry (reference
+src/workers/worker.py:199-231, src/parameter_server/server.py:372-378): a dead peer surfaces as
+an RPC error. Over RCCL a stalled or hung rank instead leaves every other rank's collective
+waiting forever — nothing in the communicator times out. ``RoundWatchdog`` watches the round
+progress of one rank from a daemon thread:
+
+* the sync channel brackets the host part of every fetch / push (``begin`` / ``end``): a
+  blocking transport (gloo / torch.distributed, a host-synchronous communicator) stalls inside
+  it; the native RCCL push hands over a HIP event recorded right after its collectives (they
+  are stream-ordered, the host does not wait), completed when the device has finished them;
+* when no round completes within ``timeout_s`` while one is outstanding, the watchdog polls the
+  communicator's asynchronous error (ncclCommGetAsyncError), aborts it (ncclCommAbort — this is
+  what unblocks collectives stuck on a dead peer) and terminates the process with exit status 3
+  (``os._exit``: no re-exec). torchrun then tears the group down and restarts it; the server
+  resumes from its last checkpoint (--ckpt-every / --resume latest) and the workers skip the
+  rounds it contains (parallel/worker.py rounds_to_batches).
+
+``--round-timeout 0`` disables it.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import threading
+import time
+from collections import deque
+
+EXIT_STALLED = 3
+
+
+class RoundWatchdog:
+    def __init__(self, timeout_s: float, comm=None, name: str = "", poll_s: float = 0.5, on_expire=None):
+        self.timeout_s = float(timeout_s)
+        self.comm = comm  # parallel/rccl.py NativeComm (or None for torch.distributed / gloo)
+        self.name = name
+        self.poll_s = poll_s
+        self.on_expire = on_expire or self._abort_and_exit
+        self._lock = threading.Lock()
+        self._events = deque()   # HIP events of issued, not yet observed rounds
+        self._blocking = 0       # blocking round calls in progress
+        self._progress = time.monotonic()
+        self.rounds_done = 0
+        self.expired = False
+        self._stop = threading.Event()
+        self._thread = None
+        if self.timeout_s > 0:
+            self._thread = threading.Thread(target=self._run, name="psx-round-watchdog", daemon=True)
+            self._thread.start()
+
+    # ---- channel side
+    def begin(self):
+        """The host part of a fetch / push starts."""
+        with self._lock:
+            if not self._events and not self._blocking:
+                self._progress = time.monotonic()  # the clock starts with the first outstanding call
+            self._blocking += 1
+
+    def end(self, event=None):
+        """The host part returned; ``event``: recorded after stream-ordered collectives that the
+        device has yet to finish (None: the call itself completed them)."""
+        with self._lock:
+            self._blocking -= 1
+            if event is None:
+                self._progress = time.monotonic()
+                self.rounds_done += 1
+            else:
+                self._events.append(event)
+
+    # ---- watchdog thread
+    def _poll(self) -> bool:
+        """Retire completed rounds; True when the oldest outstanding one is overdue."""
+        with self._lock:
+            while self._events and self._events[0].query():
+                self._events.popleft()
+                self._progress = time.monotonic()
+                self.rounds_done += 1
+            pending = bool(self._events) or self._blocking > 0
+            return pending and time.monotonic() - self._progress > self.timeout_s
+
+    def _run(self):
+        while not self._stop.wait(self.poll_s):
+            try:
+                overdue = self._poll()
+            except Exception as e:  # noqa: BLE001 - a HIP error on query is itself a failed round
+                print(f"[psx watchdog{self.name}] round event query failed: {e}", file=sys.stderr, flush=True)
+                overdue = True
+            if overdue:
+                self.expired = True
+                self.on_expire(self)
+                return
+
+    def _abort_and_exit(self, _wd):
+        err = None
+        if self.comm is not None:
+            try:
+                err = self.comm.async_error()
+            except Exception:  # noqa: BLE001
+                pass
+        print(f"[psx watchdog{self.name}] no sync round completed for {self.timeout_s:.0f} s "
+              f"(rounds done {self.rounds_done}, communicator async error {err}): aborting the communicator "
+              f"and exiting with status {EXIT_STALLED} so the launcher restarts the group from the last "
+              "checkpoint", file=sys.stderr, flush=True)
+        if self.comm is not None:
+            try:
+                self.comm.destroy(abort=True)
+            except Exception:  # noqa: BLE001
+                pass
+        sys.stdout.flush()
+        os._exit(EXIT_STALLED)
+
+    def stop(self):
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=2 * self.poll_s + 1)

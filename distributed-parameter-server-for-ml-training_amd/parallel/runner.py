@@ -204,6 +204,10 @@ def run_distributed(cfg, log=print) -> dict:
         else:
             chan = make_sync_channel(cfg, t, server, W, layout, device, worker=is_worker)
         chan._gs = done  # non-server ranks track the global step locally
+        if cfg.round_timeout > 0 and world > 1 and hasattr(chan, "watchdog"):
+            from .liveness import RoundWatchdog
+
+            chan.watchdog = RoundWatchdog(cfg.round_timeout, comm=getattr(t, "comm", None), name=f" rank {rank}")
         if is_worker:
             wk = Worker(cfg, comp, chan, train, test, worker_name=names[rank], rank=rank, log=lg,
                         requested_id=wid_of_rank[rank], steps_per_epoch=steps)
@@ -218,6 +222,8 @@ def run_distributed(cfg, log=print) -> dict:
         wk = sess.worker
     if cfg.mode == "sync" and sharded:
         chan.gather_master()  # rank 0's arena = the full trained state (final metrics)
+    if cfg.mode == "sync" and getattr(chan, "watchdog", None) is not None:
+        chan.watchdog.stop()
     if device.type == "cuda":
         torch.cuda.synchronize()
     wall = time.time() - t0

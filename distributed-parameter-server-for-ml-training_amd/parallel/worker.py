@@ -102,11 +102,33 @@ class SyncCollectiveChannel:
         self.root_worker = root_worker  # rank 0 contributes a gradient (colocated topology)
         self.agg_mode = os.environ.get("PSX_SYNC_AGG", "gather")
         self._gbufs = None
+        self.watchdog = None  # parallel/liveness.py RoundWatchdog (run_distributed)
         self.codec = codec  # FetchCodec (parallel/codec.py); None = raw fp32 arena
         # weight-image fast path (parallel/codec.py WeightWire): this rank's worker-side wire
         # (None on a dedicated server rank); the server's own wire is kept by the apply
         self.image_wire = wire
         self.image = wire is not None or (server is not None and server.wire is not None)
+
+    def _native(self) -> bool:
+        return bool(getattr(self.t, "native", False))
+
+    def _guard(self, fn, *a, event=False):
+        """Run one half of a round under the liveness watchdog (parallel/liveness.py): the host
+        call is bracketed; with ``event`` (the native transport's push) completion is an event
+        recorded after its stream-ordered collectives."""
+        wd = self.watchdog
+        if wd is None:
+            return fn(*a)
+        wd.begin()
+        ev = None
+        try:
+            r = fn(*a)
+            if event:
+                ev = torch.cuda.Event()
+                ev.record()
+            return r
+        finally:
+            wd.end(ev)
 
     def register(self, name, requested_id=-1):
         # registrations of every rank are done by the runner on rank 0 (gathered names)
@@ -139,6 +161,9 @@ class SyncCollectiveChannel:
         return self._gs_after_fetch()
 
     def fetch(self, worker_id, local_arena):
+        return self._guard(self._fetch, worker_id, local_arena)
+
+    def _fetch(self, worker_id, local_arena):
         if self.image:
             return self._fetch_image()
         if self.server is not None:
@@ -169,6 +194,9 @@ class SyncCollectiveChannel:
         return self._gs
 
     def push(self, worker_id, grads, local_step, buffers=None):
+        return self._guard(self._push, worker_id, grads, local_step, buffers, event=self._native())
+
+    def _push(self, worker_id, grads, local_step, buffers=None):
         sparse = grads.dtype == torch.int32  # top-k payloads cannot be summed by a reduce: gather
         world = getattr(self.t, "world_size", 1)
         dense_gather = not sparse and self.agg_mode == "gather" and world > 1
@@ -408,7 +436,7 @@ class Worker:
             skip_steps = rounds_to_batches(rounds, len(self.sampler.epoch_indices(0)), K)
             self.log(f"[Resume] worker {self.worker_id} skips {rounds} completed rounds ({skip_steps} batches)")
         self.training_start_time = time.time()
-        fi_worker, fi_step = _parse_fault(self.cfg.fault_inject)
+        fi_kind, fi_worker, fi_step = _parse_fault(self.cfg.fault_inject)
         try:
             for epoch in range(self.num_epochs):
                 self._sync()
@@ -424,6 +452,13 @@ class Worker:
                 for batch_idx in range(start, len(batches)):
                     idx = batches[batch_idx]
                     if fi_worker == self.worker_id and self.local_step_counter == fi_step:
+                        if fi_kind == "hang_worker":  # alive but stalled: only a liveness guard notices
+                            import sys
+
+                            print(f"fault injected: worker {self.worker_id} hangs at step {fi_step}", file=sys.stderr,
+                                  flush=True)
+                            while True:
+                                time.sleep(3600)
                         raise _InjectedFault(f"fault injected: worker {self.worker_id} at step {fi_step}")
                     if batch_idx % K == 0:
                         with self.timer.span("fetch"):
@@ -497,13 +532,14 @@ class _InjectedFault(RuntimeError):
 
 
 def _parse_fault(spec: str):
-    """'kill_worker:K@S' -> (K, S); anything else -> (None, None). Only armed on the first
-    attempt of an elastic job (torchrun sets TORCHELASTIC_RESTART_COUNT), so a restarted job
-    resumes instead of failing again."""
+    """'kill_worker:K@S' (worker K raises at its step S) or 'hang_worker:K@S' (worker K stalls
+    forever at step S, process alive) -> (kind, K, S); anything else -> (None, None, None). Only
+    armed on the first attempt of an elastic job (torchrun sets TORCHELASTIC_RESTART_COUNT), so a
+    restarted job resumes instead of failing again."""
     import os
 
-    if not spec or not spec.startswith("kill_worker:") or int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")):
-        return None, None
-    body = spec.split(":", 1)[1]
-    k, s = body.split("@")
-    return int(k), int(s)
+    kind = spec.split(":", 1)[0] if spec else ""
+    if kind not in ("kill_worker", "hang_worker") or int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")):
+        return None, None, None
+    k, s = spec.split(":", 1)[1].split("@")
+    return kind, int(k), int(s)

@@ -87,7 +87,8 @@ class PSConfig:
     heartbeat_timeout: float = 60.0
     log_dir: str = ""
     use_graph: bool = True
-    fault_inject: str = ""         # e.g. "kill_worker:2@5" (worker 2 exits at its step 5)
+    fault_inject: str = ""         # "kill_worker:2@5" (worker 2 exits at its step 5) | "hang_worker:2@5" (stalls)
+    round_timeout: float = 300.0   # sync liveness guard: abort + exit 3 when no round completes (0: off)
     verbose: int = 1
     extra: dict = field(default_factory=dict)
 
@@ -179,7 +180,10 @@ def add_arguments(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     A("--heartbeat-timeout", type=float, default=None)
     A("--log-dir", default=None)
     A("--no-graph", dest="use_graph", action="store_false", default=None)
-    A("--fault-inject", default=None)
+    A("--fault-inject", default=None, help="kill_worker:K@S or hang_worker:K@S (first attempt only)")
+    A("--round-timeout", type=float, default=None,
+      help="sync rounds: seconds without a completed round before the communicator is aborted and the rank "
+           "exits (status 3) for a launcher restart from the last checkpoint; 0 disables")
     A("--verbose", type=int, default=None)
     return ap
 

@@ -171,3 +171,28 @@ def test_distributed_sync_matches_loopback(world, topology, tmp_path):
     ref = _json_lines(r.stdout, "RESULT ")[-1]
     assert len(got) == 1 and got[0][1] == ref[1] == 4, (got, ref)
     assert abs(got[0][0] - ref[0]) <= 2e-4 * abs(ref[0]), (got, ref)
+
+
+def test_native_hung_worker_watchdog_restart(tmp_path):
+    """Sync liveness guard on the native communicator: worker 1 stalls at its step 5 (alive);
+    rank 0's round watchdog aborts the communicator after --round-timeout and exits with status
+    3; torchrun restarts the group, the server resumes from its last checkpoint and the job
+    completes with the fault-free number of rounds."""
+    ck, logs = tmp_path / "ck", tmp_path / "logs"
+    port = _port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--max-restarts=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "scripts", "psx_train.py"),
+           "--mode", "sync", "--model", "resnet18", "--batch-size", "32", "--train-samples", "512", "--epochs", "2",
+           "--eval-every", "0", "--ckpt-every", "2", "--ckpt-dir", str(ck), "--resume", "latest",
+           "--fault-inject", "hang_worker:1@5", "--round-timeout", "15", "--verbose", "1", "--log-dir", str(logs)]
+    r = subprocess.run(cmd, env=_env({"PSX_FAKECOMM_TIMEOUT_S": "300"}), stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=600)
+    out = r.stdout
+    assert r.returncode == 0, out[-4000:]
+    assert "hangs at step 5" in out and "psx watchdog" in out and "[Resume] restored global step 4" in out, out[-4000:]
+    recs = []
+    for f in sorted(os.listdir(logs)):
+        with open(os.path.join(logs, f)) as fh:
+            recs += [json.loads(ln) for ln in fh if ln.strip()]
+    srv = [x for x in recs if x["type"] == "SERVER_FINAL_METRICS"]
+    assert srv and srv[-1]["global_steps_completed"] == 2 * (256 // 32)

@@ -477,3 +477,22 @@ def test_fault_restart_with_sync_steps_odd_checkpoint(tmp_path, accumulate):
     steps = -(-(96 // 3) // 8)
     srv = [r for r in recs if r["type"] == "SERVER_FINAL_METRICS"]
     assert srv[-1]["global_steps_completed"] == 2 * -(-steps // 2)
+
+
+def test_hung_worker_watchdog_restart(tmp_path):
+    """Liveness guard: worker 1 stalls (alive, no exit) at its step 5; the other ranks' round
+    watchdogs see no sync round complete for --round-timeout seconds, exit with status 3, torchrun
+    restarts the group and the job resumes from the last checkpoint to the fault-free number of
+    global steps."""
+    ck = tmp_path / "ck"
+    args = ["--mode", "sync", "--epochs", "2", "--ckpt-every", "2", "--ckpt-dir", str(ck), "--resume", "latest",
+            "--fault-inject", "hang_worker:1@5", "--round-timeout", "6", "--verbose", "1"]
+    tiny = list(TINY)
+    for opt in ("--epochs", "--verbose"):
+        i = tiny.index(opt)
+        del tiny[i:i + 2]
+    recs, out = _spawn(3, args + tiny, max_restarts=1, timeout=300)
+    assert "hangs at step 5" in out and "psx watchdog" in out and "[Resume] restored global step 4" in out, out[-3000:]
+    steps = -(-(96 // 3) // 8)
+    srv = [r for r in recs if r["type"] == "SERVER_FINAL_METRICS"]
+    assert srv[-1]["global_steps_completed"] == 2 * steps

@@ -99,7 +99,7 @@ class GraphRoundChannel(SyncCollectiveChannel):
         torch.cuda.current_stream().wait_stream(self.cstream)
 
     # ---------------------------------------------------------------- protocol
-    def fetch(self, worker_id, local_arena):
+    def _fetch(self, worker_id, local_arena):
         if self.server is not None:
             for w in self.members:
                 self.server.core.on_fetch(w)
@@ -113,7 +113,7 @@ class GraphRoundChannel(SyncCollectiveChannel):
             return self.server.core.global_step
         return self._gs_after_fetch()
 
-    def push(self, worker_id, grads, local_step, buffers=None):
+    def _push(self, worker_id, grads, local_step, buffers=None):
         """The round's device work ran inside the step graph; record it in the server core."""
         if self.server is not None:
             res = None

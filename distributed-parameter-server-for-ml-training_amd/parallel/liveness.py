@@ -114,3 +114,39 @@ class RoundWatchdog:
         self._stop.set()
         if self._thread is not None:
             self._thread.join(timeout=2 * self.poll_s + 1)
+
+
+class WatchedRounds:
+    """Mixin of the sync channels (SyncCollectiveChannel and its overlap / graph-round
+    subclasses, ShardedSyncChannel): ``fetch`` / ``push`` run the channel's ``_fetch`` /
+    ``_push`` under its ``watchdog`` (set by parallel/runner.py run_distributed; None = off)."""
+
+    watchdog = None
+
+    def _native(self) -> bool:
+        return bool(getattr(self.t, "native", False))
+
+    def _guard(self, fn, *a, event=False):
+        """Bracket the host call; with ``event`` (native transport push) completion is an event
+        recorded after its stream-ordered collectives."""
+        wd = self.watchdog
+        if wd is None:
+            return fn(*a)
+        wd.begin()
+        ev = None
+        try:
+            r = fn(*a)
+            if event:
+                import torch
+
+                ev = torch.cuda.Event()
+                ev.record()
+            return r
+        finally:
+            wd.end(ev)
+
+    def fetch(self, worker_id, local_arena):
+        return self._guard(self._fetch, worker_id, local_arena)
+
+    def push(self, worker_id, grads, local_step, buffers=None):
+        return self._guard(self._push, worker_id, grads, local_step, buffers, event=self._native())

@@ -197,7 +197,7 @@ class OverlapSyncChannel(SyncCollectiveChannel):
             self._finish_bucket(k - 1)
         self._streamed += 1
 
-    def push(self, worker_id, grads, local_step, buffers=None):
+    def _push(self, worker_id, grads, local_step, buffers=None):
         if self._streamed == 0:  # nothing streamed (dedicated server rank): issue every bucket now
             for k in range(len(self.buckets)):
                 self.push_bucket(k, grads)
@@ -254,7 +254,7 @@ class OverlapSyncChannel(SyncCollectiveChannel):
             self.wire.unpack_buffers(local_arena)  # parity: fetched running stats overwrite local ones
         return self._gs_after_fetch()
 
-    def fetch(self, worker_id, local_arena):
+    def _fetch(self, worker_id, local_arena):
         if not self._inflight:
             return self._full_fetch(local_arena)
         return self._complete(local_arena)

@@ -30,6 +30,7 @@ from __future__ import annotations
 import torch
 
 from .codec import small_index_of
+from .liveness import WatchedRounds
 
 
 class ShardPlan:
@@ -96,7 +97,7 @@ class ShardedWire:
         return local_arena
 
 
-class ShardedSyncChannel:
+class ShardedSyncChannel(WatchedRounds):
     """Sync rounds against the sharded server (see the module docstring). ``server`` is this
     rank's ParameterServer (its range only is updated); rank 0's also does the bookkeeping."""
 
@@ -129,7 +130,7 @@ class ShardedSyncChannel:
     def bind_compute(self, compute):
         compute.pad_grads(self.plan.padded)
 
-    def fetch(self, worker_id, local_arena):
+    def _fetch(self, worker_id, local_arena):
         if self.rank == 0:
             for w in self.members:
                 self.server.core.on_fetch(w)
@@ -140,7 +141,7 @@ class ShardedSyncChannel:
             self.wire.to_arena(local_arena)
         return self.server.core.global_step if self.rank == 0 else self._gs
 
-    def push(self, worker_id, grads, local_step, buffers=None):
+    def _push(self, worker_id, grads, local_step, buffers=None):
         if grads.dtype == torch.int32 or buffers is not None:
             raise RuntimeError("the sharded server takes dense gradients without --bn-sync")
         if grads.numel() < self.plan.padded:

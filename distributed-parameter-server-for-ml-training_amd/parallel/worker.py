@@ -30,6 +30,7 @@ import torch
 from ..utils import metrics as M
 from ..utils.data import EpochSampler, shard_range
 from . import control as CP
+from .liveness import WatchedRounds
 
 
 def rounds_to_batches(rounds: int, steps_per_epoch: int, K: int) -> int:
@@ -84,7 +85,7 @@ class InProcessChannel:
         self.server.job_finished(worker_id, emit=self.emit_on_last)
 
 
-class SyncCollectiveChannel:
+class SyncCollectiveChannel(WatchedRounds):
     """All ranks call push/fetch in lockstep. Rank 0 may or may not train (topology).
 
     Push (dense wire): the workers' wires are gathered to rank 0 and summed there in fp32 by the
@@ -102,33 +103,11 @@ class SyncCollectiveChannel:
         self.root_worker = root_worker  # rank 0 contributes a gradient (colocated topology)
         self.agg_mode = os.environ.get("PSX_SYNC_AGG", "gather")
         self._gbufs = None
-        self.watchdog = None  # parallel/liveness.py RoundWatchdog (run_distributed)
         self.codec = codec  # FetchCodec (parallel/codec.py); None = raw fp32 arena
         # weight-image fast path (parallel/codec.py WeightWire): this rank's worker-side wire
         # (None on a dedicated server rank); the server's own wire is kept by the apply
         self.image_wire = wire
         self.image = wire is not None or (server is not None and server.wire is not None)
-
-    def _native(self) -> bool:
-        return bool(getattr(self.t, "native", False))
-
-    def _guard(self, fn, *a, event=False):
-        """Run one half of a round under the liveness watchdog (parallel/liveness.py): the host
-        call is bracketed; with ``event`` (the native transport's push) completion is an event
-        recorded after its stream-ordered collectives."""
-        wd = self.watchdog
-        if wd is None:
-            return fn(*a)
-        wd.begin()
-        ev = None
-        try:
-            r = fn(*a)
-            if event:
-                ev = torch.cuda.Event()
-                ev.record()
-            return r
-        finally:
-            wd.end(ev)
 
     def register(self, name, requested_id=-1):
         # registrations of every rank are done by the runner on rank 0 (gathered names)
@@ -160,9 +139,6 @@ class SyncCollectiveChannel:
         self.t.broadcast_from_server(self.image_wire.buf)
         return self._gs_after_fetch()
 
-    def fetch(self, worker_id, local_arena):
-        return self._guard(self._fetch, worker_id, local_arena)
-
     def _fetch(self, worker_id, local_arena):
         if self.image:
             return self._fetch_image()
@@ -192,9 +168,6 @@ class SyncCollectiveChannel:
         # global step advances by exactly one per sync round; workers track it locally
         self._gs = getattr(self, "_gs", 0)
         return self._gs
-
-    def push(self, worker_id, grads, local_step, buffers=None):
-        return self._guard(self._push, worker_id, grads, local_step, buffers, event=self._native())
 
     def _push(self, worker_id, grads, local_step, buffers=None):
         sparse = grads.dtype == torch.int32  # top-k payloads cannot be summed by a reduce: gather

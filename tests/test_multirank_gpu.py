@@ -174,15 +174,16 @@ def test_distributed_sync_matches_loopback(world, topology, tmp_path):
 
 
 def test_native_hung_worker_watchdog_restart(tmp_path):
-    """Sync liveness guard on the native communicator: worker 1 stalls at its step 5 (alive);
-    rank 0's round watchdog aborts the communicator after --round-timeout and exits with status
-    3; torchrun restarts the group, the server resumes from its last checkpoint and the job
-    completes with the fault-free number of rounds."""
+    """Sync liveness guard on the native communicator (dedicated topology, world 3): worker 1
+    stalls at its step 5 (alive); the other ranks' round watchdogs abort their communicators
+    after --round-timeout and exit with status 3; torchrun restarts the group, the server resumes
+    from its last checkpoint and the job completes with the fault-free number of rounds."""
     ck, logs = tmp_path / "ck", tmp_path / "logs"
     port = _port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--max-restarts=1",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3", "--max-restarts=1",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "scripts", "psx_train.py"),
-           "--mode", "sync", "--model", "resnet18", "--batch-size", "32", "--train-samples", "512", "--epochs", "2",
+           "--mode", "sync", "--topology", "dedicated", "--model", "resnet18", "--batch-size", "32",
+           "--train-samples", "512", "--epochs", "2",
            "--eval-every", "0", "--ckpt-every", "2", "--ckpt-dir", str(ck), "--resume", "latest",
            "--fault-inject", "hang_worker:1@5", "--round-timeout", "15", "--verbose", "1", "--log-dir", str(logs)]
     r = subprocess.run(cmd, env=_env({"PSX_FAKECOMM_TIMEOUT_S": "300"}), stdout=subprocess.PIPE,

@@ -10,19 +10,26 @@
 //   decisions registration, staleness = global_step - local_step, reject above the bound,
 //             weight max(0.1, 1/(1+0.1 s)), heartbeat timeouts: the native core
 //             (csrc/runtime/ps_core.cpp), no Python in the loop.
-//   data      RCCL point-to-point on the psx communicator (csrc/comm/rccl_comm.cpp), all on one
-//             communication stream: a PUSH posts ncclRecv into the worker's gradient slot (RCCL
-//             has no any-source receive — the mailbox message names the peer); a FETCH sends a
-//             per-worker snapshot of the fetch payload (bf16 weight image + fp32 remainder).
+//   data      RCCL point-to-point (csrc/comm/rccl_comm.cpp), one communicator and one
+//             communication stream PER WORKER (a 2-rank communicator {server, worker}, see
+//             parallel/rccl.py RcclTransport.open_pairs): the pushes and fetches of different
+//             workers are independent streams of work, so 7 workers drive 7 xGMI links at once and
+//             no worker's transfer waits behind another's. A PUSH posts ncclRecv into the worker's
+//             gradient slot (RCCL has no any-source receive — the mailbox message names the peer);
+//             a FETCH sends a per-worker snapshot of the fetch payload (bf16conv: bf16 weight image
+//             + fp32 remainder; fp32: the whole fp32 arena, the reference's payload).
 //   updates   one update stream serializes every apply (the reference's param_lock): the fused
-//             SGD kernel waits on the slot's receive event, updates the fp32 master arena and
-//             rewrites the bf16 image in the same pass (csrc/kernels/optim.hip). Snapshots are
+//             SGD kernel (momentum / weight decay as the Python server) waits on the slot's receive
+//             event, updates the fp32 master arena and rewrites the bf16 image in the same pass
+//             (csrc/kernels/optim.hip); pushes complete in any order across workers. Snapshots are
 //             taken on the same stream, so a fetch never sees a half-applied update and a send
 //             in flight never races the next update (it reads its own snapshot).
 //   local     the co-located worker of rank 0 calls psx_loop_local_push / _fetch / _done; the
 //             loop thread serves them between mailbox messages, ordered on the update stream
 //             against the caller's stream by events.
 //
+// Checkpoints (--ckpt-every): after the apply that reaches a multiple of the period the loop
+// synchronises the update stream and calls back into the host (ParameterServer.maybe_checkpoint).
 // The loop ends when the expected number of workers finished (or were declared dead) and no
 // receive is pending, or on STOP. Kernels and runtime functions are bound by dlsym from the
 // already-loaded psx libraries (paths passed by the caller).
@@ -93,18 +100,24 @@ struct LocalReq {
 struct PsxLoopCfg {  // mirrored by parallel/native_loop.py (ctypes.Structure)
   void* mbox;
   void* core;
-  void* comm;
-  float* arena;         // fp32 master arena (params | buffers) on the device
-  const long* small_idx;  // device int64 arena indices of the fp32 remainder of the fetch payload
+  void* const* comms;      // worker id -> communicator of its data plane (host array [max_wid])
+  const int* comm_peer;    // worker id -> the worker's rank in that communicator
+  float* arena;            // fp32 master arena (params | buffers) on the device
+  const long* small_idx;   // device int64 arena indices of the fp32 remainder of the fetch payload
   const int* remote_rank;  // worker id -> transport rank (-1: not remote), host array [max_wid]
   long n_params, small_n, arena_numel;
-  float lr;
+  float lr, momentum, weight_decay;
   int device, grad_fp16, max_wid, expected;
+  int fetch_fp32;          // 1: fetch payload = whole fp32 arena; 0: bf16 image + fp32 remainder
+  int mom_first;           // momentum buffer not yet initialised (no update since start / resume)
+  float* mom_buf;          // device momentum buffer [n_params] (nullptr: plain SGD)
   double heartbeat_timeout, poll_s;
   // update stream: the co-located worker's compute stream when there is one (its pushes and
   // fetches are then plain stream order, as with a single stream), else a stream of the loop
   hipStream_t upd_stream;
   int own_upd_stream;
+  long long ckpt_every;
+  int (*ckpt_cb)(long long global_step);  // host checkpoint hook (nullptr: none)
 };
 
 struct PsxLoop {
@@ -117,11 +130,12 @@ struct PsxLoop {
   int err = 0;
   bool stopped = false;
   // device state
-  hipStream_t s_comm = nullptr, s_upd = nullptr;
+  hipStream_t s_upd = nullptr;
   uint16_t* img = nullptr;  // server bf16 image of the parameters (rewritten by every apply)
+  std::vector<hipStream_t> s_comm;  // per worker: communication stream
   std::vector<void*> slot;  // per worker: gradient receive buffer
   std::vector<uint16_t*> snap_img;
-  std::vector<float*> snap_small;
+  std::vector<float*> snap_small;  // fp32 remainder (bf16conv) or the whole arena (fp32 fetch)
   std::vector<hipEvent_t> sent;  // per worker: last snapshot send done (snapshot reusable)
   struct Pending {
     int wid;
@@ -139,21 +153,32 @@ size_t gbytes(const PsxLoop* L) { return (size_t)L->c.n_params * (L->c.grad_fp16
 
 int alloc_worker(PsxLoop* L, int w) {
   if (L->slot[w]) return 0;
+  if (!L->c.comms[w]) return -24;  // a remote request from a worker without a data-plane communicator
+  if (hipStreamCreateWithFlags(&L->s_comm[w], hipStreamNonBlocking) != hipSuccess) return -25;
   if (hipMalloc(&L->slot[w], gbytes(L)) != hipSuccess) return -20;
-  if (hipMalloc((void**)&L->snap_img[w], (size_t)L->c.n_params * 2) != hipSuccess) return -21;
-  if (hipMalloc((void**)&L->snap_small[w], (size_t)std::max(1L, L->c.small_n) * 4) != hipSuccess) return -22;
+  if (!L->c.fetch_fp32 && hipMalloc((void**)&L->snap_img[w], (size_t)L->c.n_params * 2) != hipSuccess) return -21;
+  const long nsmall = L->c.fetch_fp32 ? L->c.arena_numel : std::max(1L, L->c.small_n);
+  if (hipMalloc((void**)&L->snap_small[w], (size_t)nsmall * 4) != hipSuccess) return -22;
   if (hipEventCreateWithFlags(&L->sent[w], hipEventDisableTiming) != hipSuccess) return -23;
-  hipEventRecord(L->sent[w], L->s_comm);
+  hipEventRecord(L->sent[w], L->s_comm[w]);
   return 0;
 }
 
 // the fused SGD apply of one gradient with the core's weight, writing the bf16 image too
 int apply(PsxLoop* L, const void* g, float weight) {
   const double t0 = now_s();
-  const int e = L->rt.sgd_apply(L->c.arena, g, nullptr, L->c.n_params, L->c.lr, weight, 0.f, 0.f, 0, L->c.grad_fp16,
-                                L->img, L->s_upd);
+  const int e = L->rt.sgd_apply(L->c.arena, g, L->c.mom_buf, L->c.n_params, L->c.lr, weight, L->c.momentum,
+                                L->c.weight_decay, L->c.mom_first, L->c.grad_fp16, L->img, L->s_upd);
+  L->c.mom_first = 0;
   L->rt.ps_on_applied(L->c.core, now_s() - t0);
   ++L->applies;
+  if (!e && L->c.ckpt_cb && L->c.ckpt_every > 0) {
+    const long long gs = L->rt.ps_global_step(L->c.core);
+    if (gs % L->c.ckpt_every == 0) {
+      hipStreamSynchronize(L->s_upd);  // the checkpoint reads the arena from another stream
+      if (L->c.ckpt_cb(gs)) return -32;
+    }
+  }
   return e;
 }
 
@@ -162,16 +187,26 @@ int serve_fetch(PsxLoop* L, int w, int rank) {
   // snapshot on the update stream (after every apply so far), once the previous send of this
   // worker's snapshot has finished
   hipStreamWaitEvent(L->s_upd, L->sent[w], 0);
-  hipMemcpyAsync(L->snap_img[w], L->img, (size_t)L->c.n_params * 2, hipMemcpyDeviceToDevice, L->s_upd);
-  if (L->c.small_n) L->rt.gather_f32(L->c.arena, L->c.small_idx, L->c.small_n, L->snap_small[w], L->s_upd);
+  if (L->c.fetch_fp32) {
+    hipMemcpyAsync(L->snap_small[w], L->c.arena, (size_t)L->c.arena_numel * 4, hipMemcpyDeviceToDevice, L->s_upd);
+  } else {
+    hipMemcpyAsync(L->snap_img[w], L->img, (size_t)L->c.n_params * 2, hipMemcpyDeviceToDevice, L->s_upd);
+    if (L->c.small_n) L->rt.gather_f32(L->c.arena, L->c.small_idx, L->c.small_n, L->snap_small[w], L->s_upd);
+  }
   hipEvent_t ready;
   hipEventCreateWithFlags(&ready, hipEventDisableTiming);
   hipEventRecord(ready, L->s_upd);
-  hipStreamWaitEvent(L->s_comm, ready, 0);
+  hipStreamWaitEvent(L->s_comm[w], ready, 0);
   hipEventDestroy(ready);
-  int e = psx_comm_send(L->c.comm, L->snap_img[w], L->c.n_params, PSX_BF16, rank, L->s_comm);
-  if (!e && L->c.small_n) e = psx_comm_send(L->c.comm, L->snap_small[w], L->c.small_n, PSX_F32, rank, L->s_comm);
-  hipEventRecord(L->sent[w], L->s_comm);
+  void* comm = L->c.comms[w];
+  int e;
+  if (L->c.fetch_fp32) {
+    e = psx_comm_send(comm, L->snap_small[w], L->c.arena_numel, PSX_F32, rank, L->s_comm[w]);
+  } else {
+    e = psx_comm_send(comm, L->snap_img[w], L->c.n_params, PSX_BF16, rank, L->s_comm[w]);
+    if (!e && L->c.small_n) e = psx_comm_send(comm, L->snap_small[w], L->c.small_n, PSX_F32, rank, L->s_comm[w]);
+  }
+  hipEventRecord(L->sent[w], L->s_comm[w]);
   return e;
 }
 
@@ -183,21 +218,26 @@ int post_recv(PsxLoop* L, int w, int rank, long long local_step) {
   hipEvent_t upd;
   hipEventCreateWithFlags(&upd, hipEventDisableTiming);
   hipEventRecord(upd, L->s_upd);
-  hipStreamWaitEvent(L->s_comm, upd, 0);
+  hipStreamWaitEvent(L->s_comm[w], upd, 0);
   hipEventDestroy(upd);
-  const int e = psx_comm_recv(L->c.comm, L->slot[w], L->c.n_params, L->c.grad_fp16 ? PSX_F16 : PSX_F32, rank,
-                              L->s_comm);
+  const int e = psx_comm_recv(L->c.comms[w], L->slot[w], L->c.n_params, L->c.grad_fp16 ? PSX_F16 : PSX_F32, rank,
+                              L->s_comm[w]);
   hipEvent_t ev;
   hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-  hipEventRecord(ev, L->s_comm);
+  hipEventRecord(ev, L->s_comm[w]);
   L->pending.push_back({w, local_step, ev});
   return e;
 }
 
 void complete_pending(PsxLoop* L) {
-  while (!L->pending.empty()) {  // in arrival order (head-of-line on one comm stream anyway)
-    PsxLoop::Pending& p = L->pending.front();
-    if (hipEventQuery(p.ev) != hipSuccess) break;
+  // in completion order: every worker has its own stream, so a slow transfer does not hold back
+  // the others (each worker has at most one push in flight: it waits for the reply)
+  for (auto it = L->pending.begin(); it != L->pending.end();) {
+    PsxLoop::Pending& p = *it;
+    if (hipEventQuery(p.ev) != hipSuccess) {
+      ++it;
+      continue;
+    }
     float weight = 0.f;
     int ncontrib = 0;
     long long st = 0;
@@ -211,7 +251,7 @@ void complete_pending(PsxLoop* L) {
     L->rt.mbox_reply(L->c.mbox, L->c.remote_rank[p.wid], R_PUSHED, p.wid, accepted,
                      L->rt.ps_global_step(L->c.core), st);
     hipEventDestroy(p.ev);
-    L->pending.pop_front();
+    it = L->pending.erase(it);
   }
 }
 
@@ -271,7 +311,6 @@ void serve_local(PsxLoop* L) {
 
 void run(PsxLoop* L) {
   hipSetDevice(L->c.device);
-  hipStreamCreateWithFlags(&L->s_comm, hipStreamNonBlocking);
   if (L->c.own_upd_stream)
     hipStreamCreateWithFlags(&L->s_upd, hipStreamNonBlocking);
   else
@@ -282,6 +321,7 @@ void run(PsxLoop* L) {
   hipMalloc(&zero, gbytes(L));
   hipMemsetAsync(zero, 0, gbytes(L), L->s_upd);
   L->rt.sgd_apply(L->c.arena, zero, nullptr, L->c.n_params, 0.f, 1.f, 0.f, 0.f, 0, L->c.grad_fp16, L->img, L->s_upd);
+  // (lr 0, no momentum buffer: the state is untouched)
   hipStreamSynchronize(L->s_upd);
   hipFree(zero);
   double last_to = now_s();
@@ -299,10 +339,10 @@ void run(PsxLoop* L) {
         L->rt.mbox_reply(L->c.mbox, src, R_REGISTERED, id, L->c.expected, 0, 0);
       } else if (type == FETCH && known) {
         const long long gs = L->rt.ps_on_fetch(L->c.core, wid, now_s());
-        if (int e = serve_fetch(L, wid, L->c.remote_rank[wid])) L->err = e;
+        if (int e = serve_fetch(L, wid, L->c.comm_peer[wid])) L->err = e;
         L->rt.mbox_reply(L->c.mbox, L->c.remote_rank[wid], R_FETCHED, wid, 0, gs, 0);
       } else if (type == PUSH && known) {
-        if (int e = post_recv(L, wid, L->c.remote_rank[wid], m[4])) L->err = e;
+        if (int e = post_recv(L, wid, L->c.comm_peer[wid], m[4])) L->err = e;
       } else if (type == DONE && known) {
         L->rt.ps_job_finished(L->c.core, wid);
         ++L->finished;
@@ -323,7 +363,8 @@ void run(PsxLoop* L) {
     if (L->finished >= L->c.expected && L->pending.empty()) break;
     if (L->err) break;
   }
-  hipStreamSynchronize(L->s_comm);
+  for (hipStream_t s : L->s_comm)
+    if (s) hipStreamSynchronize(s);
   hipStreamSynchronize(L->s_upd);
   {
     std::lock_guard<std::mutex> lk(L->mu);
@@ -365,6 +406,7 @@ void* psx_loop_create(const PsxLoopCfg* cfg, const char* runtime_path, const cha
   }
   const int n = cfg->max_wid;
   L->slot.assign(n, nullptr);
+  L->s_comm.assign(n, nullptr);
   L->snap_img.assign(n, nullptr);
   L->snap_small.assign(n, nullptr);
   L->sent.assign(n, nullptr);
@@ -433,8 +475,9 @@ void psx_loop_destroy(void* h) {
     if (L->snap_small[w]) hipFree(L->snap_small[w]);
     if (L->sent[w]) hipEventDestroy(L->sent[w]);
   }
+  for (hipStream_t s : L->s_comm)
+    if (s) hipStreamDestroy(s);
   if (L->img) hipFree(L->img);
-  if (L->s_comm) hipStreamDestroy(L->s_comm);
   if (L->s_upd && L->c.own_upd_stream) hipStreamDestroy(L->s_upd);
   delete L;
 }

@@ -2,17 +2,19 @@
 
 The async server role of rank 0 — mailbox control, RCCL point-to-point receive of pushed
 gradients and send of fetch snapshots, staleness decisions, the fused SGD apply, heartbeat
-timeouts — runs in one C++ thread on two HIP streams (communication, update); see the C++ file
-for the ordering rules. Python only starts it, serves the co-located worker's calls through it,
-and joins it. This replaces ParameterServer.serve_async (the Python loop, kept for the CPU/gloo
-path and the configurations below) for MI355X jobs on the native RCCL transport.
+timeouts, checkpoint triggers — runs in one C++ thread on HIP streams (one communication stream
+and one 2-rank communicator per worker, one update stream); see the C++ file for the ordering
+rules. Python only starts it, serves the co-located worker's calls through it, writes the
+checkpoints it asks for, and joins it. It is THE async server of MI355X jobs on the native
+transport (PSX_NATIVE_LOOP=0 selects ParameterServer.serve_async, the Python loop, which stays
+the CPU/gloo path and serves the configurations below).
 
 Remote workers use ``NativeAsyncChannel``: control requests on the shared-memory mailbox as
-before, tensors by ncclSend/ncclRecv on the psx communicator (parallel/rccl.py), posted on a
-communication stream ordered after the worker's compute stream by events.
+before, tensors by ncclSend/ncclRecv on their pair communicator (parallel/rccl.py open_pairs),
+posted on a communication stream ordered after the worker's compute stream by events.
 
-Scope: dense fp16/fp32 gradients, plain SGD (momentum/weight decay 0 — the reference's server
-update, server.py:133), no --bn-sync, bf16conv fetch payload. Enabled with PSX_NATIVE_LOOP=1.
+Scope: dense fp16/fp32 gradients; SGD with the server's momentum / weight decay; fetch payload
+bf16conv or fp32; checkpoints. Not covered (Python loop): top-k payloads, --bn-sync.
 """
 from __future__ import annotations
 
@@ -30,12 +32,17 @@ from .worker import AsyncChannel
 vp, i32, i64, f32, f64 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_double
 
 
+CKPT_CB = C.CFUNCTYPE(i32, C.c_longlong)
+
+
 class LoopCfg(C.Structure):
     """csrc/server/event_loop.cpp PsxLoopCfg."""
-    _fields_ = [("mbox", vp), ("core", vp), ("comm", vp), ("arena", vp), ("small_idx", vp), ("remote_rank", vp),
-                ("n_params", i64), ("small_n", i64), ("arena_numel", i64), ("lr", f32), ("device", i32),
-                ("grad_fp16", i32), ("max_wid", i32), ("expected", i32), ("heartbeat_timeout", f64),
-                ("poll_s", f64), ("upd_stream", vp), ("own_upd_stream", i32)]
+    _fields_ = [("mbox", vp), ("core", vp), ("comms", vp), ("comm_peer", vp), ("arena", vp), ("small_idx", vp),
+                ("remote_rank", vp), ("n_params", i64), ("small_n", i64), ("arena_numel", i64), ("lr", f32),
+                ("momentum", f32), ("weight_decay", f32), ("device", i32), ("grad_fp16", i32), ("max_wid", i32),
+                ("expected", i32), ("fetch_fp32", i32), ("mom_first", i32), ("mom_buf", vp),
+                ("heartbeat_timeout", f64), ("poll_s", f64), ("upd_stream", vp), ("own_upd_stream", i32),
+                ("ckpt_every", C.c_longlong), ("ckpt_cb", CKPT_CB)]
 
 
 _SIGS = {
@@ -64,9 +71,9 @@ def _lib():
 
 
 def native_loop_enabled(cfg, transport) -> bool:
-    return (os.environ.get("PSX_NATIVE_LOOP", "0") == "1" and getattr(transport, "native", False)
-            and cfg.codec in ("fp16", "none") and not cfg.momentum and not cfg.weight_decay and not cfg.bn_sync
-            and cfg.fetch_codec == "bf16conv")
+    """Default for async jobs on the native transport (PSX_NATIVE_LOOP=0: the Python loop)."""
+    return (os.environ.get("PSX_NATIVE_LOOP", "1") == "1" and getattr(transport, "native", False)
+            and cfg.codec in ("fp16", "none") and not cfg.bn_sync)
 
 
 class NativeServerLoop:
@@ -74,24 +81,37 @@ class NativeServerLoop:
 
     def __init__(self, server, transport, mbox, rank_of_wid: dict, expected: int, poll_s: float = 0.0005,
                  update_stream: torch.cuda.Stream | None = None):
-        """update_stream: the co-located worker's compute stream (its pushes/fetches are then in
-        plain stream order with the loop's updates); None = the loop creates its own."""
+        """rank_of_wid: worker id -> transport rank of the remote workers (transport None: local
+        workers only). update_stream: the co-located worker's compute stream (its pushes/fetches
+        are then in plain stream order with the loop's updates); None = the loop creates its own."""
         self.server = server
         lay = server.layout
+        cfg = server.cfg
         self.small_idx = small_index_of(lay).to(server.device)
         max_wid = max([expected] + [w + 1 for w in rank_of_wid])
         self.remote = (C.c_int * max_wid)(*([-1] * max_wid))
+        self.comms = (vp * max_wid)()
+        self.peer = (C.c_int * max_wid)(*([-1] * max_wid))
         for w, r in rank_of_wid.items():
             self.remote[w] = r
+            c, p = transport.p2p(r)  # the worker's pair communicator (parallel/rccl.py open_pairs)
+            self.comms[w], self.peer[w] = c.h.value, p
         dev = server.device.index or 0
-        self.cfg = LoopCfg(mbox=mbox._h, core=server.core._h, comm=transport.comm.h.value,
+        mom = server.momentum_buf if cfg.momentum else None
+        self._ckpt = CKPT_CB(self._checkpoint)  # kept alive with the loop
+        self.cfg = LoopCfg(mbox=mbox._h if mbox is not None else None, core=server.core._h,
+                           comms=C.cast(self.comms, vp), comm_peer=C.cast(self.peer, vp),
                            arena=server.arena.data_ptr(), small_idx=self.small_idx.data_ptr(),
                            remote_rank=C.cast(self.remote, vp), n_params=lay.param_numel,
                            small_n=self.small_idx.numel(), arena_numel=lay.arena_numel, lr=float(server.lr),
-                           device=dev, grad_fp16=int(server.cfg.codec == "fp16"), max_wid=max_wid,
-                           expected=expected, heartbeat_timeout=float(server.cfg.heartbeat_timeout or 0.0),
-                           poll_s=poll_s, upd_stream=update_stream.cuda_stream if update_stream is not None else None,
-                           own_upd_stream=int(update_stream is None))
+                           momentum=float(cfg.momentum or 0.0), weight_decay=float(cfg.weight_decay or 0.0),
+                           device=dev, grad_fp16=int(cfg.codec == "fp16"), max_wid=max_wid, expected=expected,
+                           fetch_fp32=int(cfg.fetch_codec == "fp32"), mom_first=int(server._mom_first),
+                           mom_buf=mom.data_ptr() if mom is not None else None,
+                           heartbeat_timeout=float(cfg.heartbeat_timeout or 0.0), poll_s=poll_s,
+                           upd_stream=update_stream.cuda_stream if update_stream is not None else None,
+                           own_upd_stream=int(update_stream is None),
+                           ckpt_every=int(cfg.ckpt_every or 0) if cfg.ckpt_dir else 0, ckpt_cb=self._ckpt)
         kernels()  # both libraries are loaded (the loop binds their entry points by path)
         runtime()
         self.h = _lib().psx_loop_create(C.byref(self.cfg), os.path.join(NATIVE_DIR, "libpsx_runtime.so").encode(),
@@ -101,11 +121,25 @@ class NativeServerLoop:
         torch.cuda.synchronize(server.device)  # the arena is final before the loop reads it
         _lib().psx_loop_start(self.h)
 
+    def _checkpoint(self, global_step: int) -> int:
+        """Called on the loop thread once the update stream has finished the apply that reached
+        ``global_step`` (a multiple of --ckpt-every)."""
+        try:
+            with torch.cuda.device(self.server.device):
+                self.server.maybe_checkpoint()
+            return 0
+        except Exception as e:  # noqa: BLE001 - reported, the loop ends with an error
+            import sys
+
+            print(f"[psx native loop] checkpoint at step {global_step} failed: {e}", file=sys.stderr, flush=True)
+            return 1
+
     def join(self):
         if self.h is None:
             return 0
         rc = _lib().psx_loop_join(self.h)
         s = self.server
+        s._mom_first = s._mom_first and not int(_lib().psx_loop_applies(self.h))
         s.bytes_pushed = int(s.core.metrics().get("gradients_processed", 0)) * s.n * (2 if s.cfg.codec == "fp16" else 4)
         _lib().psx_loop_destroy(self.h)
         self.h = None
@@ -149,6 +183,7 @@ class NativeAsyncChannel(AsyncChannel):
     def __init__(self, transport, mbox, rank, codec):
         super().__init__(transport, mbox, rank, codec=codec)
         self.cs = torch.cuda.Stream(device=transport.device)
+        self.comm, self.server_peer = transport.p2p(0)  # the pair communicator with the server
 
     def _fork(self):
         self.cs.wait_stream(torch.cuda.current_stream())
@@ -157,8 +192,8 @@ class NativeAsyncChannel(AsyncChannel):
     def fetch(self, worker_id, local_arena):
         self.mbox.send(CP.Msg(CP.FETCH, self.rank, worker_id))
         with self._fork():
-            for b in self.codec.wire:  # bf16 image, then the fp32 remainder (server send order)
-                self.t.comm.recv(b, 0, stream=self.cs)
+            for b in self.codec.wire:  # bf16 image + fp32 remainder, or the fp32 arena (server send order)
+                self.comm.recv(b, self.server_peer, stream=self.cs)
         r = self.mbox.wait_reply(self.rank)
         torch.cuda.current_stream().wait_stream(self.cs)
         self.codec.unpack(local_arena)
@@ -169,7 +204,7 @@ class NativeAsyncChannel(AsyncChannel):
             raise RuntimeError("the native server loop does not take BN buffers (--bn-sync)")
         self.mbox.send(CP.Msg(CP.PUSH, self.rank, worker_id, 0, local_step))
         with self._fork():
-            self.t.comm.send(grads, 0, stream=self.cs)
+            self.comm.send(grads, self.server_peer, stream=self.cs)
         r = self.mbox.wait_reply(self.rank)
         torch.cuda.current_stream().wait_stream(self.cs)  # the gradient buffer is reusable
         self.last_staleness = r.d

@@ -1,13 +1,21 @@
-"""Native RCCL transport: the sync data plane issued straight onto the compute stream.
+"""Native RCCL transport: every bulk tensor of the PS protocol on psx's own communicators.
 
-``RcclTransport`` keeps DistTransport's torch.distributed groups for control (gloo: registration
-names, barriers, metrics) and for the async mode's point-to-point tensors, and moves the sync
-round's bulk tensors through psx's own RCCL communicator (csrc/comm/rccl_comm.cpp):
+``RcclTransport`` keeps DistTransport's torch.distributed group for host control only (gloo:
+registration names, barriers, metrics, the unique ids) and moves every bulk tensor through
+psx's RCCL communicators (csrc/comm/rccl_comm.cpp):
 
   reference RPC (src/communication/ps.proto:4-19)   here
-  PushGradrients (sync)   pickled fp16 dict         ncclReduce(sum -> rank 0) of the fp16 wire
+  PushGradrients (sync)   pickled fp16 dict         grouped ncclSend/ncclRecv gather of the wires
+                                                    to rank 0 (fp32 sum there), or ncclReduce
   FetchParameters (sync)  pickled fp32 state_dict   ncclBroadcast(rank 0) of the weight wire
   (top-k payloads)        -                         grouped ncclSend/ncclRecv gather to rank 0
+  PushGradrients (async)  pickled fp16 dict         ncclSend worker -> server on the pair's
+  FetchParameters (async) pickled fp32 state_dict   communicator / ncclSend server -> worker
+
+Async point-to-point runs on one 2-rank communicator per (server, worker) pair (``open_pairs``)
+with its own HIP stream on each side, so the transfers of different workers never queue behind
+each other: with 7 workers the server's 7 xGMI links carry 7 pushes at once (the reference's
+20-thread gRPC pool, server.py:380-383, serves concurrent RPCs).
 
 Each collective is enqueued on the caller's current HIP stream — the worker's compute stream —
 so a round needs no cross-stream event and no host wait (torch.distributed runs RCCL on an
@@ -89,11 +97,28 @@ class NativeComm:
         elif err:
             raise RcclError(err)
         uid = broadcast_object(uid)
+        self._init(uid, world, rank, device)
+
+    def _init(self, uid: bytes, world: int, rank: int, device):
         h = C.c_void_p()
         self.device = torch.device(device)
-        _check(lib.psx_comm_init(uid, world, rank, self.device.index or 0, C.byref(h)), "ncclCommInitRank")
+        _check(comm().psx_comm_init(uid, world, rank, self.device.index or 0, C.byref(h)), "ncclCommInitRank")
         self.h = h
         self.rank, self.world = rank, world
+
+    @classmethod
+    def from_id(cls, uid: bytes, world: int, rank: int, device) -> "NativeComm":
+        """A communicator over an id drawn by ``new_id`` (library already loaded)."""
+        c = cls.__new__(cls)
+        c._init(uid, world, rank, device)
+        return c
+
+    @staticmethod
+    def new_id() -> bytes:
+        lib = comm()
+        buf = C.create_string_buffer(lib.psx_comm_id_bytes())
+        _check(lib.psx_comm_unique_id(buf), "ncclGetUniqueId")
+        return buf.raw
 
     def reduce_sum(self, t: torch.Tensor, root: int = 0, stream=None):
         code, _ = _dt(t)
@@ -138,7 +163,7 @@ class NativeComm:
         _check(comm().psx_comm_recv(self.h, t.data_ptr(), t.numel(), code, peer, _stream(stream)), "ncclRecv")
 
     def async_error(self) -> int:
-        return comm().psx_comm_async_error(self.h)
+        return comm().psx_comm_async_error(self.h) if self.h else 0
 
     def destroy(self, abort: bool = False):
         if self.h:
@@ -172,6 +197,52 @@ class RcclTransport(DistTransport):
         self.comm = NativeComm(self.rank, self.world_size, self.device, self.broadcast_object,
                                self.all_gather_object)
         self._cstream = torch.cuda.Stream(device=self.device)
+        self._pairs = {}    # peer rank -> (communicator, peer's rank in it)
+        self._pstream = {}  # peer rank -> HIP stream of the async point-to-point with that peer
+
+    # ---- async mode point-to-point: one communicator + stream per (server, worker) pair
+    def open_pairs(self, peers=None):
+        """Collective over all ranks: a 2-rank communicator {0, r} for every rank r in ``peers``
+        (default: every rank > 0). Rank 0 draws the ids; the ranks initialise in rank order on
+        rank 0 (each worker only waits for its own pair). PSX_PAIR_COMMS=0 keeps everything on
+        the job communicator. World 2: the job communicator already is the pair."""
+        peers = sorted(peers) if peers is not None else list(range(1, self.world_size))
+        if os.environ.get("PSX_PAIR_COMMS", "1") == "0" or self.world_size <= 2:
+            return
+        ids = self.broadcast_object({r: NativeComm.new_id() for r in peers} if self.rank == 0 else None)
+        if self.rank == 0:
+            for r in peers:
+                self._pairs[r] = (NativeComm.from_id(ids[r], 2, 0, self.device), 1)
+        elif self.rank in ids:
+            self._pairs[0] = (NativeComm.from_id(ids[self.rank], 2, 1, self.device), 0)
+
+    def p2p(self, peer: int):
+        """(communicator, peer rank in it) carrying this rank's point-to-point with ``peer``."""
+        return self._pairs.get(peer, (self.comm, peer))
+
+    def _p2p_stream(self, peer: int):
+        s = self._pstream.get(peer)
+        if s is None:
+            s = self._pstream[peer] = torch.cuda.Stream(device=self.device)
+        return s
+
+    def _p2p(self, t, peer: int, send: bool):
+        c, p = self.p2p(peer)
+        s = self._p2p_stream(peer)
+        s.wait_stream(torch.cuda.current_stream())
+        (c.send if send else c.recv)(t, p, stream=s)
+        ev = torch.cuda.Event()
+        ev.record(s)
+        t.record_stream(s)
+        return NativeWork(ev)
+
+    def isend(self, t, dst: int):
+        """Non-blocking send on the pair's stream; ``completed`` / ``wait()`` joins the caller's
+        stream to it (the tensor must stay unmodified until then)."""
+        return self._p2p(t, dst, True)
+
+    def irecv(self, t, src: int):
+        return self._p2p(t, src, False)
 
     # ---- sync mode collectives: in stream order on the caller's stream
     def reduce_sum_to_server(self, t):
@@ -257,6 +328,9 @@ class RcclTransport(DistTransport):
         try:
             torch.cuda.synchronize(self.device)
         finally:
+            for c, _ in self._pairs.values():
+                c.destroy()
+            self._pairs = {}
             self.comm.destroy()
             super().close()
 

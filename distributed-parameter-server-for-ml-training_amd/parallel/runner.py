@@ -257,6 +257,8 @@ class AsyncSession:
         if rank != 0:
             self.mbox = CP.ShmMailbox(mbox_name, nreply=t.world_size, owner=False)
         remote = {w: r for w, r in rank_of_wid.items() if r != 0}
+        if getattr(t, "native", False):  # one communicator + stream per (server, worker) pair
+            t.open_pairs(sorted(remote.values()))
         self.worker, self.thread, self.hb, self.loop = None, None, None, None
         native = native_loop_enabled(cfg, t)  # the C++ server loop (parallel/native_loop.py)
         if rank == 0:

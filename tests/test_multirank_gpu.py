@@ -197,3 +197,36 @@ def test_native_hung_worker_watchdog_restart(tmp_path):
             recs += [json.loads(ln) for ln in fh if ln.strip()]
     srv = [x for x in recs if x["type"] == "SERVER_FINAL_METRICS"]
     assert srv and srv[-1]["global_steps_completed"] == 2 * (256 // 32)
+
+
+_ARUN = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+import psx
+from psx.parallel.runner import run_distributed
+from psx.utils.config import PSConfig
+cfg = PSConfig(model="resnet18", batch_size=64, epochs=1, train_samples=1024, eval_every=0, verbose=0, lr=0.05,
+               max_steps=4, mode="async", topology={topo!r}, heartbeat_timeout=0).validate()
+res = run_distributed(cfg, log=lambda *a, **k: None)
+if "server" in res:
+    s = res["server"]
+    print("RESULT " + json.dumps([s["global_steps_completed"], s["gradients_processed"], s["final_param_checksum"]]))
+"""
+
+
+@pytest.mark.parametrize("world,topology", [(2, "colocated"), (3, "dedicated"), (3, "colocated")])
+@pytest.mark.parametrize("native_loop", ["1", "0"])
+def test_async_remote_workers(world, topology, native_loop, tmp_path):
+    """Async mode at world 2-3: remote workers push / fetch over their pair communicators
+    (RcclTransport.open_pairs; world 2 reuses the job communicator) to the native event loop
+    (default) or the Python loop (PSX_NATIVE_LOOP=0, its point-to-point also on the native
+    communicators). Every push of every worker reaches the server and is processed."""
+    W = world - 1 if topology == "dedicated" else world
+    script = tmp_path / "arun.py"
+    script.write_text(_ARUN.format(root=ROOT, topo=topology))
+    out = _torchrun(world, [str(script)], extra={"PSX_NATIVE_LOOP": native_loop})
+    recs = [r for r in _json_lines(out, "RESULT ") if r]
+    assert len(recs) == 1, out[-3000:]
+    gs, processed, checksum = recs[0]
+    assert processed == W * 4 and 0 < gs <= W * 4, recs
+    assert checksum == checksum and abs(checksum) < 1e12

@@ -1,19 +1,27 @@
-"""Native async server event loop (csrc/server/event_loop.cpp, parallel/native_loop.py) on one
-MI355X, world size 1 in a subprocess: the co-located worker's path through a whole async run
-(loop start, registration, staleness decisions, fused apply + bf16 image, fetch copies in stream
-order, JobFinished, loop end), against the Python server loop.
+"""Native async server event loop (csrc/server/event_loop.cpp, parallel/native_loop.py) — the
+default async server on the native transport — against the Python loop
+(ParameterServer.serve_async, PSX_NATIVE_LOOP=0) on one MI355X:
 
-Not covered on a one-GPU box: the remote-worker path (mailbox PUSH/FETCH + ncclRecv/ncclSend to a
-peer rank). RCCL refuses two ranks on one device, and rank 0 cannot be its own peer either —
-self send/recv from two threads fails with "invalid usage" (RCCL wants both in one group call) —
-so that path stays opt-in (PSX_NATIVE_LOOP=1) until a multi-GPU run has exercised it.
+* a scripted push/fetch schedule of three workers (in-process, served through the loops' local
+  paths): the same accept/reject decisions, staleness values and histogram, global steps and a
+  bit-identical master arena, with plain SGD and with momentum + weight decay;
+* a whole co-located async run at world size 1 (registration, fused apply + bf16 image, fetch
+  copies in stream order, checkpoints requested by the loop, JobFinished, loop end).
+
+The remote-worker path (mailbox PUSH/FETCH + ncclRecv/ncclSend on per-worker pair
+communicators and streams) runs at world 2-3 in tests/test_multirank_gpu.py on the test-only
+communicator (RCCL refuses two ranks on one device).
 """
 import json
 import os
 import subprocess
 import sys
+import threading
+import queue
+import uuid
 
 import pytest
+import torch
 
 pytestmark = pytest.mark.gpu
 
@@ -30,25 +38,95 @@ def _run(code, port, extra_env=None, timeout=240):
     return json.loads(line[7:])
 
 
+# (kind, worker, local step): staleness bound 2 -> a mix of fresh, stale-accepted and rejected pushes
+SCHEDULE = [("p", 0, 0), ("p", 1, 0), ("p", 2, 0), ("f", 0, 0), ("p", 0, 3), ("p", 1, 0), ("p", 2, 3), ("f", 1, 0),
+            ("p", 1, 5), ("p", 0, 1), ("p", 2, 4), ("f", 2, 0), ("p", 2, 7), ("p", 0, 7), ("p", 1, 5), ("p", 1, 9)]
+
+
+def _drive(native: bool, momentum: float):
+    import psx  # noqa: F401
+    from psx.parallel import control as CP
+    from psx.parallel.native_loop import NativeLocalChannel, NativeServerLoop
+    from psx.parallel.runner import build_state
+    from psx.parallel.server import ParameterServer
+    from psx.parallel.worker import LocalAsyncChannel
+    from psx.utils.config import PSConfig
+
+    W = 3
+    cfg = PSConfig(model="resnet18", mode="async", workers=W, lr=0.05, staleness_bound=2, codec="fp16",
+                   momentum=momentum, weight_decay=5e-4 if momentum else 0.0, eval_every=0, verbose=0,
+                   heartbeat_timeout=0).validate()
+    _, lay, arena, counters = build_state(cfg)
+    srv = ParameterServer(cfg, lay, arena.clone(), counters, device="cuda", total_workers=W, log=lambda *a, **k: None)
+    for w in range(W):
+        srv.register_worker(f"w{w}", w)
+    mbox = CP.ShmMailbox(f"/psx_t{uuid.uuid4().hex[:10]}", nreply=1, owner=True)
+    gen = torch.Generator().manual_seed(7)
+    grads = [(torch.randn(srv.n, generator=gen) * 0.01).half().cuda() for _ in SCHEDULE]
+    local = torch.empty(lay.arena_numel, device="cuda")
+    trace = []
+    try:
+        if native:
+            loop = NativeServerLoop(srv, None, mbox, {}, W, update_stream=torch.cuda.current_stream())
+            ch = NativeLocalChannel(srv, loop)
+        else:
+            q = queue.Queue()
+            th = threading.Thread(target=srv.serve_async, args=(None, mbox, {}),
+                                  kwargs={"local_queue": q, "expected": W}, daemon=True)
+            th.start()
+            ch = LocalAsyncChannel(srv, q)
+        for i, (kind, w, ls) in enumerate(SCHEDULE):
+            if kind == "p":
+                trace.append(("p", bool(ch.push(w, grads[i], ls)), srv.core.global_step))
+            else:
+                trace.append(("f", ch.fetch(w, local)))
+        for w in range(W):
+            ch.finished(w)
+        if native:
+            loop.join()
+        else:
+            th.join(timeout=60)
+        torch.cuda.synchronize()
+    finally:
+        mbox.close()
+    return trace, srv.core.staleness_histogram(), srv.core.global_step, srv.arena.clone()
+
+
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+def test_scripted_schedule_matches_python_loop(momentum):
+    nat = _drive(True, momentum)
+    py = _drive(False, momentum)
+    assert nat[0] == py[0], (nat[0], py[0])
+    accepted = sum(1 for t in py[0] if t[0] == "p" and t[1])
+    assert 0 < accepted < sum(1 for t in SCHEDULE if t[0] == "p")  # the schedule rejects some pushes
+    assert nat[1] == py[1] and nat[2] == py[2] == accepted
+    assert torch.equal(nat[3], py[3])
+
+
 _ASYNC = r"""
-import json, sys
+import json, os, sys
 sys.path.insert(0, {root!r})
 import psx
 from psx.parallel.runner import run_distributed
 from psx.utils.config import PSConfig
 cfg = PSConfig(model="resnet18", batch_size=64, epochs=1, train_samples=2048, eval_every=0, verbose=0, lr=0.1,
-               max_steps=8, mode="async", dtype="bf16").validate()
+               max_steps=8, mode="async", dtype={dtype!r}, momentum={mom}, weight_decay={wd},
+               ckpt_every=4, ckpt_dir={ck!r}).validate()
 res = run_distributed(cfg, log=lambda *a, **k: None)
 s = res["server"]
 print("RESULT " + json.dumps([s["final_param_checksum"], s["global_steps_completed"], s["async_updates"],
-                             s["max_staleness_observed"]]))
+                             s["max_staleness_observed"], sorted(os.listdir({ck!r}))]))
 """
 
 
-def test_native_loop_colocated_run_matches_python_loop():
+@pytest.mark.parametrize("dtype,mom", [("bf16", 0.0), ("fp32", 0.9)])
+def test_native_loop_colocated_run_matches_python_loop(dtype, mom, tmp_path):
     out = {}
     for flag, port in (("1", 29661), ("0", 29662)):
-        out[flag] = _run(_ASYNC.format(root=ROOT), port, {"PSX_NATIVE_LOOP": flag})
-    (a, ga, ua, sa), (b, gb, ub, sb) = out["1"], out["0"]
+        ck = str(tmp_path / f"ck{flag}")
+        code = _ASYNC.format(root=ROOT, dtype=dtype, mom=mom, wd=5e-4 if mom else 0.0, ck=ck)
+        out[flag] = _run(code, port, {"PSX_NATIVE_LOOP": flag})
+    (a, ga, ua, sa, ca), (b, gb, ub, sb, cb) = out["1"], out["0"]
     assert ga == gb == 8 and ua == ub == 8 and sa == sb == 0, out
     assert abs(a - b) <= 2e-4 * max(abs(a), abs(b)), out
+    assert ca == cb and len(ca) >= 2, out  # checkpoints at steps 4 and 8 from both loops

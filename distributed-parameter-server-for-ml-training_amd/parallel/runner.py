@@ -71,10 +71,11 @@ def make_datasets(cfg, device, classes):
         train = DeviceDataset.cifar_binary(tr, max_records=cfg.train_samples, device=device)
         test = DeviceDataset.cifar_binary(te, max_records=cfg.test_samples, device=device) if os.path.exists(te) else None
         return train, test
-    train = DeviceDataset.synthetic(cfg.train_samples, h, classes, seed=cfg.seed, device=device)
+    gen = DeviceDataset.synthetic_hard if cfg.synthetic_kind == "hard" else DeviceDataset.synthetic
+    train = gen(cfg.train_samples, h, classes, seed=cfg.seed, device=device)
     test = None
     if cfg.eval_every and cfg.test_samples:
-        test = DeviceDataset.synthetic(cfg.test_samples, h, classes, seed=cfg.seed, device=device, offset=10_000_000)
+        test = gen(cfg.test_samples, h, classes, seed=cfg.seed, device=device, offset=10_000_000)
     return train, test
 
 

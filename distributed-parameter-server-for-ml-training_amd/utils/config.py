@@ -74,6 +74,7 @@ class PSConfig:
     overlap: bool = False
     bucket_mb: float = 4.0         # bucket target size in MiB of fp16 wire gradient
     synthetic: bool = True
+    synthetic_kind: str = "proto"  # proto: prototype + noise (learnable); hard: low contrast + 20% label noise
     data_dir: str = ""
     train_samples: int = 50000
     test_samples: int = 10000
@@ -122,6 +123,8 @@ class PSConfig:
             raise ValueError("--dtype fp32 computes with fp32 weights: --fetch-codec fp32")
         if self.bucket_mb <= 0:
             raise ValueError("--bucket-mb must be > 0")
+        if self.synthetic_kind not in ("proto", "hard"):
+            raise ValueError("--synthetic-kind must be proto or hard")
         if not (0.0 < self.topk_ratio <= 1.0):
             raise ValueError("--topk-ratio must be in (0, 1]")
         return self
@@ -166,6 +169,8 @@ def add_arguments(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     A("--no-overlap", dest="overlap", action="store_false", default=None)
     A("--bucket-mb", type=float, default=None, help="overlapped sync: gradient bucket size (MiB of fp16)")
     A("--synthetic", action="store_true", default=None)
+    A("--synthetic-kind", choices=["proto", "hard"], default=None,
+      help="synthetic data: proto (class prototype + noise) or hard (low contrast, 20%% label noise)")
     A("--data-dir", default=None, help="directory with cifar-100-binary/{train,test}.bin")
     A("--train-samples", type=int, default=None)
     A("--test-samples", type=int, default=None)

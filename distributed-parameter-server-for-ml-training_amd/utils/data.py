@@ -65,6 +65,13 @@ class DeviceDataset:
         return cls(imgs, labs)
 
     @classmethod
+    def synthetic_hard(cls, n: int, hw: int = 32, classes: int = 100, seed: int = 0, device="cuda", offset: int = 0,
+                       label_noise: float = 0.2):
+        """synthetic_hard_numpy, resident on ``device``."""
+        imgs, labs = synthetic_hard_numpy(n, hw, classes, seed, offset, label_noise)
+        return cls(torch.from_numpy(imgs).to(device), torch.from_numpy(labs).to(device))
+
+    @classmethod
     def cifar_binary(cls, path: str, label_bytes: int = 2, label_index: int = 1, max_records: int = 0,
                      device="cuda"):
         from ..ops._lib import runtime
@@ -82,6 +89,28 @@ class DeviceDataset:
         if got != n:
             raise IOError(f"{path}: read {got} of {n} records")
         return cls(torch.from_numpy(img).to(device), torch.from_numpy(lab).to(device))
+
+
+def synthetic_hard_numpy(n: int, hw: int = 32, classes: int = 100, seed: int = 0, offset: int = 0,
+                         label_noise: float = 0.2, chunk: int = 4096):
+    """Class-conditional noise with label noise (convergence studies, ``--synthetic-kind hard``):
+    low-contrast 4x4 class prototypes (128 + 12·N(0,1) per cell and channel) under per-pixel
+    Gaussian noise of std 64, and a fraction ``label_noise`` of the labels replaced by a uniformly
+    drawn class. Not trivially separable, and the label noise caps the attainable accuracy at
+    about 1 - label_noise·(1 - 1/classes). The prototypes depend on ``seed`` only, so the train
+    set (offset 0) and the test set (another offset) share them."""
+    protos = 128.0 + 12.0 * np.random.default_rng([seed, 7]).standard_normal((classes, 4, 4, 3))
+    up = np.repeat(np.repeat(protos, hw // 4, axis=1), hw // 4, axis=2).astype(np.float32)
+    rng = np.random.default_rng([seed, offset, 1])
+    labels = rng.integers(0, classes, size=n)
+    imgs = np.empty((n, hw, hw, 3), dtype=np.uint8)
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        x = up[labels[s:e]] + 64.0 * rng.standard_normal((e - s, hw, hw, 3), dtype=np.float32)
+        imgs[s:e] = np.clip(np.rint(x), 0, 255).astype(np.uint8)
+    noisy = rng.random(n) < label_noise
+    observed = np.where(noisy, rng.integers(0, classes, size=n), labels).astype(np.int32)
+    return imgs, observed
 
 
 def synthetic_numpy(n: int, hw: int = 32, classes: int = 100, seed: int = 0, offset: int = 0):

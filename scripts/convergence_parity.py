@@ -11,6 +11,11 @@
                       ParameterServer), fp32 HIP engine, fp16 gradient wire (the reference codec).
 * ``psx_fp32_wire32`` the same with the fp32 wire (--codec none).
 * ``psx_bf16``        the bf16 HIP engine (fast path), fp16 wire, bf16conv fetch.
+* ``psx_fp32_reference_bn`` psx_fp32 with the reference's BN semantics (no --bn-sync): same
+                      training curve, but the evaluation runs on never-learned running statistics.
+
+The psx runs other than the last push their BN running statistics with the gradient (--bn-sync;
+with W = 1 the server then holds the worker's statistics, as a single-process trainer does).
 
 All runs start from the same weights (except ``torch_fp32_init1``), see the same batches in the
 same order and the same augmented pixels (the torch runs call the psx augmentation kernel with
@@ -64,9 +69,13 @@ def batches_for(args):
     return out[: args.steps]
 
 
-def run_psx(args, train, test, dtype: str, codec: str):
+def run_psx(args, train, test, dtype: str, codec: str, bn_sync: bool = True):
+    """bn_sync: the worker pushes its BN running statistics with the gradient (W = 1: the server
+    keeps the worker's, as a single-process trainer does); without it the reference semantics
+    apply (every fetch resets them to the server's never-updated copy)."""
     cfg = PSConfig(model="resnet18", mode="sync", workers=1, lr=args.lr, batch_size=args.batch, epochs=10 ** 6,
-                   train_samples=args.train, eval_every=0, verbose=0, dtype=dtype, codec=codec).validate()
+                   train_samples=args.train, eval_every=0, verbose=0, dtype=dtype, codec=codec,
+                   bn_sync=bn_sync).validate()
     model, lay, arena, counters = build_state(cfg)
     srv = ParameterServer(cfg, lay, arena.clone(), counters, device=DEV, total_workers=1, log=_noop)
     comp = make_compute(model, lay, args.batch, DEV, "resnet18", _wire_dtype(cfg), seed=0, use_graph=True,
@@ -153,7 +162,11 @@ def run_w4(args, bn_sync: bool):
     cfg = PSConfig(model="resnet18", mode="sync", workers=4, lr=args.lr, batch_size=args.batch, epochs=epochs,
                    train_samples=args.train, test_samples=args.test, eval_every=epochs, verbose=0,
                    synthetic_kind="hard", bn_sync=bn_sync).validate()
-    res = run_local(cfg, log=_noop)
+    import contextlib
+    import io
+
+    with contextlib.redirect_stdout(io.StringIO()):  # METRICS_JSON lines of the loopback run
+        res = run_local(cfg, log=_noop)
     accs = [w["all_accuracies_percent"][-1] for w in res["workers"]]
     return {"global_steps": res["server"]["global_steps_completed"], "epochs": epochs,
             "worker_test_acc": accs, "last_loss": [w["last_loss"] for w in res["workers"]]}
@@ -186,7 +199,8 @@ def main():
                      ("torch_fp32_init1", lambda: run_torch(args, train, test, 1)),
                      ("psx_fp32", lambda: run_psx(args, train, test, "fp32", "fp16")),
                      ("psx_fp32_wire32", lambda: run_psx(args, train, test, "fp32", "none")),
-                     ("psx_bf16", lambda: run_psx(args, train, test, "bf16", "fp16"))):
+                     ("psx_bf16", lambda: run_psx(args, train, test, "bf16", "fp16")),
+                     ("psx_fp32_reference_bn", lambda: run_psx(args, train, test, "fp32", "fp16", bn_sync=False))):
         runs[name] = fn()
         r = runs[name]
         print(f"{name:18s} last-100 loss {np.mean(r['loss'][-100:]):.4f} test acc {r['test_acc']:.2f}% "
@@ -232,7 +246,7 @@ def main():
         for a in ax:
             a.grid(alpha=0.3)
             a.legend(fontsize=8)
-        fig.suptitle("ResNet-18, synthetic_hard (20% label noise), batch %d, lr %.3g, MI355X" % (args.batch, args.lr))
+        fig.suptitle(f"ResNet-18, synthetic_hard (20% label noise), batch {args.batch}, lr {args.lr:g}, MI355X")
         fig.tight_layout()
         fig.savefig(os.path.join(args.out, "convergence_parity.png"), dpi=110)
     except Exception as e:  # noqa: BLE001 - the JSON is the artifact; the figure is a convenience

@@ -603,9 +603,14 @@ int launch_w3(const Wgrad3Args& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// fp32 plan (wgrad2f_kernel): MFMA-bound, so the model is the f32 MFMA time of a stage
-// (BR*BC/4 cycles per wave at one wave per SIMD; co-resident workgroups share the SIMDs) per
-// round of workgroups + a per-workgroup prologue/epilogue + the split-K partial traffic.
+// fp32 plan (wgrad2f_kernel): workgroups run in rounds of 256 CUs x k co-resident workgroups
+// (k <= the LDS occupancy); a round's length is its workgroups' stages x the f32 MFMA time of a
+// stage (BR*BC/4 cycles per wave) x k / eff(k) — a lone wave per SIMD leaves every stage's DMA wait
+// and barrier exposed — plus ~1.5 us of prologue / partial-tile store, and the split-K partial
+// traffic (written here, read by the reduction) comes on top. Round quantisation dominates: the
+// 64-channel 32x32 layer takes 100 us at 84 splits (756 workgroups: one round at k = 3) and 131 us
+// at 86 (774: a second round for 6 workgroups). eff measured with scripts/dev/wgf_splits.py:
+// 64x64 0.55 / 0.65 / 0.72 at k = 1 / 2 / 3.
 WPlan wplanf(int OC, int Kg, int npix) {
   WPlan best{64, 64, 3, 1, 0};
   double best_t = 1e30;
@@ -617,19 +622,21 @@ WPlan wplanf(int OC, int Kg, int npix) {
       if (Kg % BR || OC % BC) continue;
       const int NS = 3;
       int occ = 163840 / (NS * 32 * (BR + BC) * 4);
-      if (occ > 4) occ = 4;
+      if (occ > 3) occ = 3;
       if (occ < 1) continue;
-      const int slots = wg_slots(occ);
+      const bool sq = BR == 64 && BC == 64;
       const long tiles = (long)(Kg / BR) * (OC / BC);
-      const double step_us = (double)(BR * BC) / 4.0 / 2100.0;  // at ~2.1 GHz under load
-      const int smax = steps / 8 > 0 ? steps / 8 : 1;
-      for (int sp = 1; sp <= smax && sp <= 128; ++sp) {
+      const double step_us = (double)(BR * BC) / 4.0 / 2100.0;  // one stage at full f32 MFMA rate
+      auto eff = [&](int k) { return sq ? (k <= 1 ? 0.55 : k == 2 ? 0.65 : 0.72) : (k <= 1 ? 0.60 : 0.68); };
+      for (int sp = 1; sp <= 256 && sp <= steps; ++sp) {
         const int sps = (steps + sp - 1) / sp;
         const int spl = (steps + sps - 1) / sps;
-        const long wgs = tiles * spl;
-        const long rounds = (wgs + slots - 1) / slots;
-        const double per_wg = sps * step_us * (double)(wgs < 256L * occ ? (wgs + 255) / 256 : occ) + 3.0;
-        const double t = rounds * per_wg + (spl > 1 ? spl * (double)OC * Kg * 8.0 / 5e6 : 0.0);
+        if (sp > 1 && spl != sp) continue;
+        const long wgs = tiles * spl, full = wgs / (256L * occ), rest = wgs - full * 256L * occ;
+        const int krest = (int)((rest + 255) / 256);
+        double t = full * (sps * step_us * occ / eff(occ) + 1.5);
+        if (rest) t += sps * step_us * krest / eff(krest) + 1.5;
+        if (spl > 1) t += spl * (double)OC * Kg * 6.0 / 6e6;  // reduction read + extra store
         if (t < best_t) {
           best_t = t;
           best = WPlan{BR, BC, NS, spl, sps};
@@ -681,6 +688,11 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
     WPlan p = wplanf(OC, Kg, a.npix);
     if (const char* e = getenv("PSX_WGF_BR")) p.BR = atoi(e);
     if (const char* e = getenv("PSX_WGF_BC")) p.BC = atoi(e);
+    if (const char* e = getenv("PSX_WGF_SPLITS"); e && atoi(e) > 0) {  // sweeps
+      const int steps = (a.npix + 31) / 32;
+      p.sps = (steps + atoi(e) - 1) / atoi(e);
+      p.splits = (steps + p.sps - 1) / p.sps;
+    }
     if (Kg % p.BR || OC % p.BC) return -2;
     a.n_k_tiles = Kg / p.BR;
     a.n_oc_tiles = OC / p.BC;

@@ -7,12 +7,28 @@
 //   send    { (i, fp16(acc[i])) : |acc[i]| > T } + enough |acc[i]| == T ties to make exactly k
 //   resid = acc - sent                       (incl. the fp16 rounding error of sent values)
 //
-// The select never leaves the device: three histogram passes over the magnitude bits
-// (11 + 11 + 9 bits, LDS histograms flushed with sparse global atomics), each followed by a
-// one-block "select" kernel that finds the bin holding the k-th element and refines the
-// (prefix, mask, k_remaining) state in HBM; a count / scan / write compaction then emits the
-// payload in index order (deterministic, no same-address atomics). No host round trip, so the
-// whole encode is stream-ordered and graph-capturable.
+// Two passes over the gradient, five launches, no host round trip (stream-ordered,
+// graph-capturable):
+//   A  (1024 workgroups, one contiguous chunk each) acc = resid + g in place and a 4096-bin LDS
+//      histogram of the top 12 magnitude bits (exponent + 4 mantissa bits); flushed to a global
+//      histogram with sparse atomics, and kept per workgroup as suffix sums;
+//   S  (one workgroup) the bin b0 holding the k-th largest; every chunk's count of elements above
+//      b0 ("sure") and inside it ("candidates") is two lookups in its suffix row: exclusive scans
+//      give each chunk its write bases;
+//   B  (1024 workgroups, same chunks) writes the sure entries to the payload in index order
+//      (workgroup-scan ranks; resid -= fp16 value), compacts the candidates (index, acc) in index
+//      order and histograms their remaining 19 bits: 1024 coarse bins (bits 18..9, LDS) and the
+//      full 2^19 fine bins (global atomics);
+//   Rc (256 workgroups over the candidates) every workgroup finds the exact threshold T from the
+//      two histograms (coarse bin, then its 512 fine bins) and counts its range's candidates
+//      above T and equal to T;
+//   Rw (same) appends its selected candidates in index order (base = prefix of the preceding
+//      ranges' counts; ties at T taken lowest index first), updates resid, clears the histograms
+//      and writes the header.
+// With error feedback the unsent mass piles up just below the threshold (10x the candidates of a
+// Gaussian), so the candidate stage is grid-parallel. Deterministic: positions come from ordered
+// scans, never from same-address atomics. The previous encoder made three full histogram passes
+// + count / scan / write (5 passes, 11 launches).
 //
 // Payload (int32 words): [count, kcap, n, 0 | idx[kcap] | fp16 val[kcap] (packed)]
 // Server side: dst[idx] += scale * val (decode into a dense fp32 buffer, or straight into the
@@ -21,258 +37,410 @@
 
 namespace psx {
 
-enum { TK_KREM = 0, TK_PREFIX = 1, TK_MASK = 2, TK_CNTGT = 3, TK_TIES = 4, TK_STATE_WORDS = 16 };
-constexpr int TK_HIST = 2048;
-
-template <int PASS>
-struct TkPass {
-  static constexpr int SHIFT = PASS == 0 ? 20 : (PASS == 1 ? 9 : 0);
-  static constexpr int NB = PASS == 2 ? 512 : 2048;
-};
+enum { TK_KREM = 0, TK_B0 = 1, TK_CNTGT = 2, TK_NC = 3, TK_T = 4, TK_NEED = 5, TK_STATE_WORDS = 16 };
+constexpr int TK_RB = 256;                 // workgroups of the candidate stage
+constexpr int TK_FINE = 1 << 19;           // fine bins: magnitude bits 18..0
+constexpr int TK_NB0 = 4096, TK_SH0 = 19;  // first-level bins: magnitude bits 30..19
+constexpr int TK_BLOCKS = 1024;            // chunks of passes A / B
+constexpr int TK_ROW = TK_NB0 + 1;         // per-chunk suffix row (entry 4096 = 0)
 
 PSX_DEV uint32_t mag_key(float a) { return __float_as_uint(a) & 0x7fffffffu; }
 
-__global__ __launch_bounds__(256) void topk_init_kernel(uint32_t* state, uint32_t* hist, int* payload, int k,
-                                                        int kcap, long n) {
-  for (int i = threadIdx.x; i < TK_HIST; i += 256) hist[i] = 0;
-  if (threadIdx.x < TK_STATE_WORDS) state[threadIdx.x] = threadIdx.x == TK_KREM ? (uint32_t)k : 0u;
-  if (threadIdx.x == 0) {
-    payload[0] = 0;
-    payload[1] = kcap;
-    payload[2] = (int)n;
-    payload[3] = 0;
-  }
-}
-
-// PASS 0 also forms acc = resid + g in place.
-template <int PASS, typename GT>
-__global__ __launch_bounds__(256) void topk_hist_kernel(const GT* __restrict__ g, float* __restrict__ resid, long n,
-                                                        const uint32_t* __restrict__ state, uint32_t* __restrict__ hist) {
-  using P = TkPass<PASS>;
-  __shared__ uint32_t lh[P::NB];
-  for (int i = threadIdx.x; i < P::NB; i += 256) lh[i] = 0;
-  __syncthreads();
-  const uint32_t prefix = state[TK_PREFIX], pmask = state[TK_MASK];
-  auto bump = [&](float a) {
-    const uint32_t key = mag_key(a);
-    if ((key & pmask) == prefix) atomicAdd(&lh[(key >> P::SHIFT) & (P::NB - 1)], 1u);
-  };
-  const long n4 = n >> 2;
-  const long stride = (long)gridDim.x * 256;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
-    f32x4 r = reinterpret_cast<const f32x4*>(resid)[i];
-    if (PASS == 0 && g != nullptr) {
-      if constexpr (sizeof(GT) == 2) {
-        const u32x2 h = reinterpret_cast<const u32x2*>(g)[i];
-        const _Float16* hp = reinterpret_cast<const _Float16*>(&h);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) r[e] += (float)hp[e];
-      } else {
-        const f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
-        r += gv;
-      }
-      reinterpret_cast<f32x4*>(resid)[i] = r;
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bump(r[e]);
-  }
-  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {  // scalar tail
-    const long i = (n4 << 2) + threadIdx.x;
-    float a = resid[i];
-    if (PASS == 0 && g != nullptr) {
-      if constexpr (sizeof(GT) == 2) a += (float)reinterpret_cast<const _Float16*>(g)[i];
-      else a += (float)g[i];
-      resid[i] = a;
-    }
-    bump(a);
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < P::NB; i += 256)
-    if (lh[i]) atomicAdd(&hist[i], lh[i]);
-}
-
-// One block: locate the bin (scanning from the largest magnitudes down) that holds the k-th
-// element, fold it into the prefix, and clear the histogram for the next pass.
-template <int PASS>
-__global__ __launch_bounds__(256) void topk_select_kernel(uint32_t* __restrict__ hist, uint32_t* __restrict__ state) {
-  using P = TkPass<PASS>;
-  constexpr int PER = P::NB / 256;
-  __shared__ uint32_t wtot[4];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  uint32_t c[PER];
-  uint32_t local = 0;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    c[j] = hist[P::NB - 1 - (t * PER + j)];  // thread 0 owns the highest bins
-    local += c[j];
-  }
-  const uint32_t krem = state[TK_KREM];
-  // block exclusive scan of `local` in thread order
-  uint32_t incl = local;
+// exclusive scan of v over the workgroup in thread order (NT threads); *total = the sum
+template <int NT>
+PSX_DEV uint32_t tk_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t incl = v;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t v = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += v;
+    const uint32_t t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
   }
-  if (lane == 63) wtot[w] = incl;
+  if (lane == 63) wsum[w] = incl;
   __syncthreads();
-  uint32_t above = incl - local;
-  for (int i = 0; i < w; ++i) above += wtot[i];
-  if (above < krem && above + local >= krem) {
+  uint32_t base = 0, tot = 0;
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      if (above + c[j] >= krem) {
-        const uint32_t b = (uint32_t)(P::NB - 1 - (t * PER + j));
-        state[TK_CNTGT] += above;
-        state[TK_KREM] = krem - above;
-        state[TK_PREFIX] |= b << P::SHIFT;
-        state[TK_MASK] |= (uint32_t)(P::NB - 1) << P::SHIFT;
+  for (int i = 0; i < NT / 64; ++i) {
+    const uint32_t x = wsum[i];
+    if (i < w) base += x;
+    tot += x;
+  }
+  __syncthreads();  // wsum reusable
+  *total = tot;
+  return base + incl - v;
+}
+
+PSX_DEV uint16_t tk_half(float a) {
+  return __builtin_bit_cast(uint16_t, (_Float16)fminf(fmaxf(a, -65504.f), 65504.f));
+}
+
+template <typename GT>
+PSX_DEV float tk_load_g(const GT* g, long i) {
+  if constexpr (sizeof(GT) == 2) return (float)reinterpret_cast<const _Float16*>(g)[i];
+  else return (float)g[i];
+}
+
+// Pass A: acc = resid + g (g may be null), 4096-bin histogram -> global + per-chunk suffix row.
+template <typename GT>
+__global__ __launch_bounds__(256) void tk_pass_a(const GT* __restrict__ g, float* __restrict__ resid, long n,
+                                                 long chunk, uint32_t* __restrict__ ghist,
+                                                 uint32_t* __restrict__ rows) {
+  __shared__ uint32_t lh2[2 * TK_NB0];  // two copies (waves 0-1 / 2-3): half the same-bin contention
+  __shared__ uint32_t wsum[4];
+  const int t = threadIdx.x;
+  for (int i = t; i < 2 * TK_NB0; i += 256) lh2[i] = 0;
+  __syncthreads();
+  uint32_t* const lh = lh2 + (t >> 7) * TK_NB0;
+  const long lo = (long)blockIdx.x * chunk;
+  const long hi = lo + chunk < n ? lo + chunk : n;
+  // 4 tiles of 1024 per iteration: their loads are all in flight before the first add / atomic
+  constexpr int U = 4;
+  long i = lo + 4 * t;
+  for (; i + (U - 1) * 1024 + 3 < hi; i += U * 1024) {
+    f32x4 r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = *reinterpret_cast<const f32x4*>(resid + i + u * 1024);
+    if (g != nullptr) {
+      if constexpr (sizeof(GT) == 2) {
+        u32x2 hv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) hv[u] = *reinterpret_cast<const u32x2*>(g + i + u * 1024);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const _Float16* hp = reinterpret_cast<const _Float16*>(&hv[u]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) r[u][e] += (float)hp[e];
+        }
+      } else {
+        f32x4 gv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) gv[u] = *reinterpret_cast<const f32x4*>(g + i + u * 1024);
+#pragma unroll
+        for (int u = 0; u < U; ++u) r[u] += gv[u];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) *reinterpret_cast<f32x4*>(resid + i + u * 1024) = r[u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) atomicAdd(&lh[mag_key(r[u][e]) >> TK_SH0], 1u);
+  }
+  for (; i < hi; i += 1024) {
+    if (i + 3 < hi) {
+      f32x4 r = *reinterpret_cast<const f32x4*>(resid + i);
+      if (g != nullptr) {
+        if constexpr (sizeof(GT) == 2) {
+          const u32x2 h = *reinterpret_cast<const u32x2*>(g + i);
+          const _Float16* hp = reinterpret_cast<const _Float16*>(&h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) r[e] += (float)hp[e];
+        } else {
+          r += *reinterpret_cast<const f32x4*>(g + i);
+        }
+        *reinterpret_cast<f32x4*>(resid + i) = r;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) atomicAdd(&lh[mag_key(r[e]) >> TK_SH0], 1u);
+    } else {
+      for (long j = i; j < hi; ++j) {
+        float a = resid[j];
+        if (g != nullptr) {
+          a += tk_load_g(g, j);
+          resid[j] = a;
+        }
+        atomicAdd(&lh[mag_key(a) >> TK_SH0], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < TK_NB0; i += 256) lh2[i] += lh2[TK_NB0 + i];
+  __syncthreads();
+  // suffix sums in descending bin order: thread t owns bins 4095 - 16 t - j (j < 16)
+  uint32_t c[16], local = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    c[j] = lh2[TK_NB0 - 1 - (16 * t + j)];
+    local += c[j];
+  }
+  uint32_t tot;
+  uint32_t above = tk_excl_scan<256>(local, wsum, &tot);
+  uint32_t* row = rows + (size_t)blockIdx.x * TK_ROW;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    above += c[j];
+    row[TK_NB0 - 1 - (16 * t + j)] = above;  // # elements of this chunk in bins >= bin
+  }
+  if (t == 0) row[TK_NB0] = 0;
+  for (int i = t; i < TK_NB0; i += 256)
+    if (lh2[i]) atomicAdd(&ghist[i], lh2[i]);
+}
+
+// S: one workgroup of 1024 threads. The bin b0 holding the k-th largest; per-chunk bases of the
+// sure entries and of the candidates; clears the global histogram for the next encode.
+__global__ __launch_bounds__(1024) void tk_select0(uint32_t* __restrict__ ghist, const uint32_t* __restrict__ rows,
+                                                   uint32_t* __restrict__ state, uint32_t* __restrict__ bases, int k) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t sb[2];
+  const int t = threadIdx.x;
+  uint32_t c[4], local = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    c[j] = ghist[TK_NB0 - 1 - (4 * t + j)];
+    local += c[j];
+  }
+  if (t == 0) sb[0] = sb[1] = 0;
+  uint32_t tot;
+  uint32_t above = tk_excl_scan<1024>(local, wsum, &tot);
+  const uint32_t kk = (uint32_t)k;
+  if (above < kk && above + local >= kk) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (above + c[j] >= kk) {
+        sb[0] = (uint32_t)(TK_NB0 - 1 - (4 * t + j));
+        sb[1] = above;
         break;
       }
       above += c[j];
     }
   }
-#pragma unroll
-  for (int j = 0; j < PER; ++j) hist[P::NB - 1 - (t * PER + j)] = 0;
-}
-
-// Deterministic two-phase compaction (no same-address atomics): block b owns the contiguous
-// chunk [b*chunk, (b+1)*chunk). Phase 1 counts its "greater" and "tie" elements, a one-block
-// scan turns the counts into bases, phase 2 writes the selected entries in index order:
-//   pos(i) = #gt(< i) + min(#eq(< i), ties_needed)
-constexpr int TK_BLOCKS = 1024;
-
-PSX_DEV void tk_flags(const float* resid, long i, long end, uint32_t T, bool& gt, bool& eq, float& a) {
-  const bool in = i < end;
-  a = in ? resid[i] : 0.f;
-  const uint32_t key = mag_key(a);
-  gt = in && key > T;
-  eq = in && key == T;
-}
-
-__global__ __launch_bounds__(256) void topk_count_kernel(const float* __restrict__ resid, long n, long chunk,
-                                                         const uint32_t* __restrict__ state,
-                                                         uint32_t* __restrict__ counts) {
-  __shared__ uint32_t red[2][4];
-  const uint32_t T = state[TK_PREFIX];
-  const long lo = (long)blockIdx.x * chunk;
-  const long hi = lo + chunk < n ? lo + chunk : n;
-  uint32_t cg = 0, ce = 0;
-  for (long base = lo; base < hi; base += 256) {
-    bool gt, eq;
-    float a;
-    tk_flags(resid, base + threadIdx.x, hi, T, gt, eq, a);
-    cg += (uint32_t)__popcll(__ballot(gt));
-    ce += (uint32_t)__popcll(__ballot(eq));
-  }
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    red[0][w] = cg;
-    red[1][w] = ce;
-  }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    counts[2 * blockIdx.x] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-    counts[2 * blockIdx.x + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  const uint32_t b0 = sb[0], cnt_gt = sb[1];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ghist[4 * t + j] = 0;
+  // chunk t: sure = bins > b0, candidates = bin b0
+  const uint32_t* row = rows + (size_t)t * TK_ROW;
+  const uint32_t sure = row[b0 + 1], cand = row[b0] - sure;
+  uint32_t ts, tc;
+  const uint32_t bs = tk_excl_scan<1024>(sure, wsum, &ts);
+  const uint32_t bc = tk_excl_scan<1024>(cand, wsum, &tc);
+  bases[2 * t] = bs;
+  bases[2 * t + 1] = bc;
+  if (t == 0) {
+    state[TK_KREM] = kk - cnt_gt;
+    state[TK_B0] = b0;
+    state[TK_CNTGT] = cnt_gt;
+    state[TK_NC] = tc;
   }
 }
 
-// One block of 256 threads, TK_BLOCKS/256 blocks' counts per thread: exclusive scans.
-__global__ __launch_bounds__(256) void topk_scan_kernel(const uint32_t* __restrict__ counts,
-                                                        uint32_t* __restrict__ bases) {
-  constexpr int PER = TK_BLOCKS / 256;
-  __shared__ uint32_t wt[2][4];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  uint32_t g[PER], e[PER], sg = 0, se = 0;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    g[j] = counts[2 * (t * PER + j)];
-    e[j] = counts[2 * (t * PER + j) + 1];
-    sg += g[j];
-    se += e[j];
-  }
-  uint32_t ig = sg, ie = se;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t vg = __shfl_up(ig, o, 64), ve = __shfl_up(ie, o, 64);
-    if (lane >= o) {
-      ig += vg;
-      ie += ve;
-    }
-  }
-  if (lane == 63) {
-    wt[0][w] = ig;
-    wt[1][w] = ie;
-  }
-  __syncthreads();
-  uint32_t bg = ig - sg, be = ie - se;
-  for (int i = 0; i < w; ++i) {
-    bg += wt[0][i];
-    be += wt[1][i];
-  }
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    bases[2 * (t * PER + j)] = bg;
-    bases[2 * (t * PER + j) + 1] = be;
-    bg += g[j];
-    be += e[j];
-  }
-}
-
-__global__ __launch_bounds__(256) void topk_write_kernel(float* __restrict__ resid, long n, long chunk,
-                                                         const uint32_t* __restrict__ state,
-                                                         const uint32_t* __restrict__ bases,
-                                                         int* __restrict__ payload, int kcap) {
-  __shared__ uint32_t wt[2][4];
-  const uint32_t T = state[TK_PREFIX];
-  const uint32_t need = state[TK_KREM];  // ties to take
+// B: sure entries -> payload (index order), candidates -> (cidx, cval) (index order) + their
+// coarse / fine histograms. Tiles of 1024 elements, 4 consecutive ones per thread (one 16-byte
+// load), ranks by a workgroup scan.
+__global__ __launch_bounds__(256) void tk_pass_b(float* __restrict__ resid, long n, long chunk,
+                                                 const uint32_t* __restrict__ state,
+                                                 const uint32_t* __restrict__ bases, int* __restrict__ payload,
+                                                 int kcap, int* __restrict__ cidx, float* __restrict__ cval,
+                                                 uint32_t* __restrict__ coarse, uint32_t* __restrict__ fine) {
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t lh[1024];
+  for (int i = threadIdx.x; i < 1024; i += 256) lh[i] = 0;
+  const uint32_t b0 = state[TK_B0];
   int* idx = payload + 4;
   uint16_t* val = reinterpret_cast<uint16_t*>(payload + 4 + kcap);
   const long lo = (long)blockIdx.x * chunk;
   const long hi = lo + chunk < n ? lo + chunk : n;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  uint32_t rg = bases[2 * blockIdx.x], re = bases[2 * blockIdx.x + 1];  // running #gt / #eq before tile
-  for (long base = lo; base < hi; base += 256) {
-    bool gt, eq;
-    float a;
-    const long i = base + threadIdx.x;
-    tk_flags(resid, i, hi, T, gt, eq, a);
-    const uint64_t mg = __ballot(gt), me = __ballot(eq);
-    __syncthreads();  // previous tile's wt reads are done
-    if (lane == 0) {
-      wt[0][w] = (uint32_t)__popcll(mg);
-      wt[1][w] = (uint32_t)__popcll(me);
+  uint32_t rs = bases[2 * blockIdx.x], rc = bases[2 * blockIdx.x + 1];
+  auto load4 = [&](long i0, float (&a)[4]) {
+    if (i0 + 3 < hi) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(resid + i0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] = v[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] = i0 + e < hi ? resid[i0 + e] : 0.f;
     }
-    __syncthreads();
-    uint32_t pg = rg, pe = re, tg = 0, te = 0;
+  };
+  float nx1[4], nx2[4];  // tiles t + 1 and t + 2 are in flight while tile t is ranked and written
+  load4(lo + 4 * threadIdx.x, nx1);
+  load4(lo + 1024 + 4 * threadIdx.x, nx2);
+  for (long base = lo; base < hi; base += 1024) {
+    const long i0 = base + 4 * threadIdx.x;
+    float a[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[e] = nx1[e];
+      nx1[e] = nx2[e];
+    }
+    if (base + 2048 < hi) load4(i0 + 2048, nx2);
+    uint32_t ns = 0, ncnd = 0, fs = 0, fc = 0;  // counts and per-element flags (bit e)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool in = i0 + e < hi;
+      const uint32_t bin = mag_key(a[e]) >> TK_SH0;
+      if (in && bin > b0) {
+        fs |= 1u << e;
+        ++ns;
+      } else if (in && bin == b0) {
+        fc |= 1u << e;
+        ++ncnd;
+      }
+    }
+    uint32_t tp;  // one scan of both counts packed (each <= 1024 per tile)
+    const uint32_t ex = tk_excl_scan<256>(ns | (ncnd << 16), wsum, &tp);
+    const uint32_t ts = tp & 0xffffu, tc = tp >> 16;
+    uint32_t ps = rs + (ex & 0xffffu), pc = rc + (ex >> 16);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long i = i0 + e;
+      if (fs >> e & 1u) {
+        if (ps < (uint32_t)kcap) {
+          const uint16_t h = tk_half(a[e]);
+          idx[ps] = (int)i;
+          val[ps] = h;
+          resid[i] = a[e] - (float)__builtin_bit_cast(_Float16, h);
+        }
+        ++ps;
+      } else if (fc >> e & 1u) {
+        const uint32_t key = mag_key(a[e]);
+        cidx[pc] = (int)i;
+        cval[pc] = a[e];
+        ++pc;
+        atomicAdd(&lh[(key >> 9) & 1023u], 1u);
+        atomicAdd(&fine[key & (TK_FINE - 1)], 1u);
+      }
+    }
+    rs += ts;
+    rc += tc;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 1024; i += 256)
+    if (lh[i]) atomicAdd(&coarse[i], lh[i]);
+}
+
+PSX_DEV void tk_crange(uint32_t nc, uint32_t& lo, uint32_t& hi) {
+  const uint32_t per = (nc + TK_RB - 1) / TK_RB;
+  lo = blockIdx.x * per;
+  hi = lo + per < nc ? lo + per : nc;
+  if (lo > hi) lo = hi;
+}
+
+// Rc: exact threshold (every workgroup, from the histograms) + this range's > T / == T counts.
+__global__ __launch_bounds__(256) void tk_refine_count(const float* __restrict__ cval, uint32_t* __restrict__ state,
+                                                       const uint32_t* __restrict__ coarse,
+                                                       const uint32_t* __restrict__ fine,
+                                                       uint32_t* __restrict__ counts) {
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t sb[4];
+  const int t = threadIdx.x;
+  const uint32_t nc = state[TK_NC], b0 = state[TK_B0];
+  const uint32_t krem = state[TK_KREM];
+  if (t == 0) sb[0] = sb[1] = sb[2] = sb[3] = 0;
+  // coarse bins, descending: thread t owns 1023 - 4t - j
+  uint32_t c[4], local = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    c[j] = coarse[1023 - (4 * t + j)];
+    local += c[j];
+  }
+  uint32_t tot;
+  uint32_t above = tk_excl_scan<256>(local, wsum, &tot);
+  if (above < krem && above + local >= krem) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (j < w) {
-        pg += wt[0][j];
-        pe += wt[1][j];
+      if (above + c[j] >= krem) {
+        sb[0] = 1023u - (4 * t + j);
+        sb[1] = above;
+        break;
       }
-      tg += wt[0][j];
-      te += wt[1][j];
+      above += c[j];
     }
-    pg += (uint32_t)__popcll(mg & lt);
-    pe += (uint32_t)__popcll(me & lt);
-    const bool sel = gt || (eq && pe < need);
-    if (sel) {
-      const uint32_t pos = pg + (pe < need ? pe : need);
-      if (pos < (uint32_t)kcap) {
-        const _Float16 h = (_Float16)fminf(fmaxf(a, -65504.f), 65504.f);
-        idx[pos] = (int)i;
-        val[pos] = __builtin_bit_cast(uint16_t, h);
-        resid[i] = a - (float)h;
-      }
-    }
-    rg += tg;
-    re += te;
   }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
-    const uint32_t total = rg + (re < need ? re : need);
-    payload[0] = (int)(total < (uint32_t)kcap ? total : (uint32_t)kcap);
+  __syncthreads();
+  const uint32_t b1 = sb[0], k1 = krem - sb[1];
+  // fine bins of coarse bin b1, descending: thread t owns 511 - 2t - j
+  uint32_t f[2];
+  local = 0;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    f[j] = fine[(b1 << 9) | (511u - (2 * t + j))];
+    local += f[j];
+  }
+  above = tk_excl_scan<256>(local, wsum, &tot);
+  if (above < k1 && above + local >= k1) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (above + f[j] >= k1) {
+        sb[2] = 511u - (2 * t + j);
+        sb[3] = above;
+        break;
+      }
+      above += f[j];
+    }
+  }
+  __syncthreads();
+  const uint32_t T = (b0 << TK_SH0) | (b1 << 9) | sb[2];
+  if (blockIdx.x == 0 && t == 0) {
+    state[TK_T] = T;
+    state[TK_NEED] = k1 - sb[3];  // ties at T to take (>= 1)
+  }
+  uint32_t lo, hi;
+  tk_crange(nc, lo, hi);
+  uint32_t ng = 0, ne = 0;
+  for (uint32_t i = lo + t; i < hi; i += 256) {
+    const uint32_t key = mag_key(cval[i]);
+    ng += key > T;
+    ne += key == T;
+  }
+  uint32_t tg, te;
+  tk_excl_scan<256>(ng, wsum, &tg);
+  tk_excl_scan<256>(ne, wsum, &te);
+  if (t == 0) {
+    counts[2 * blockIdx.x] = tg;
+    counts[2 * blockIdx.x + 1] = te;
+  }
+}
+
+// Rw: ordered append of the selected candidates of this range; clears the histograms.
+__global__ __launch_bounds__(256) void tk_refine_write(float* __restrict__ resid, const int* __restrict__ cidx,
+                                                       const float* __restrict__ cval,
+                                                       const uint32_t* __restrict__ state,
+                                                       const uint32_t* __restrict__ counts, int* __restrict__ payload,
+                                                       int kcap, long n, int k, uint32_t* __restrict__ coarse,
+                                                       uint32_t* __restrict__ fine) {
+  __shared__ uint32_t wsum[4];
+  const int t = threadIdx.x;
+  const uint32_t nc = state[TK_NC], T = state[TK_T], need = state[TK_NEED], cnt_gt = state[TK_CNTGT];
+  // bases: # > T and # == T in the preceding ranges (one value per thread, TK_RB == 256)
+  const bool prev = (uint32_t)t < blockIdx.x;
+  uint32_t sg, se;
+  tk_excl_scan<256>(prev ? counts[2 * t] : 0u, wsum, &sg);
+  tk_excl_scan<256>(prev ? counts[2 * t + 1] : 0u, wsum, &se);
+  uint32_t lo, hi;
+  tk_crange(nc, lo, hi);
+  // selected before this range = # > T + min(# == T, need) over the preceding ranges
+  uint32_t run_sel = sg + (se < need ? se : need), run_tie = se;
+  int* idx = payload + 4;
+  uint16_t* val = reinterpret_cast<uint16_t*>(payload + 4 + kcap);
+  for (uint32_t base = lo; base < hi; base += 256) {
+    const uint32_t i = base + t;
+    const bool in = i < hi;
+    const float a = in ? cval[i] : 0.f;
+    const uint32_t key = mag_key(a);
+    const bool gt = in && key > T, eq = in && key == T;
+    uint32_t teq, tsel;
+    const uint32_t tie = run_tie + tk_excl_scan<256>(eq ? 1u : 0u, wsum, &teq);
+    const bool sel = gt || (eq && tie < need);
+    const uint32_t pos = cnt_gt + run_sel + tk_excl_scan<256>(sel ? 1u : 0u, wsum, &tsel);
+    if (in) fine[key & (TK_FINE - 1)] = 0;  // this candidate's fine bin (read by Rc, done)
+    if (sel && pos < (uint32_t)kcap) {
+      const uint16_t hv = tk_half(a);
+      const int gi = cidx[i];
+      idx[pos] = gi;
+      val[pos] = hv;
+      resid[gi] = a - (float)__builtin_bit_cast(_Float16, hv);
+    }
+    run_sel += tsel;
+    run_tie += teq;
+  }
+  if (blockIdx.x == 0) {
+    for (int i = t; i < 1024; i += 256) coarse[i] = 0;
+    if (t == 0) {
+      payload[0] = k < kcap ? k : kcap;
+      payload[1] = kcap;
+      payload[2] = (int)n;
+      payload[3] = 0;
+    }
   }
 }
 
@@ -290,47 +458,51 @@ __global__ __launch_bounds__(256) void topk_decode_add_kernel(const int* __restr
 
 using namespace psx;
 
-static int tk_grid(long n) {
-  long b = (n / 4 + 255) / 256;
-  if (b > 1024) b = 1024;
-  return (int)(b < 1 ? 1 : b);
-}
+static long tk_chunk(long n) { return ((n + TK_BLOCKS - 1) / TK_BLOCKS + 1023) / 1024 * 1024; }
 
 extern "C" {
 
-int psx_topk_workspace_words() { return TK_HIST + TK_STATE_WORDS + 4 * TK_BLOCKS; }
+// int32 words of workspace for gradients of n elements (histogram, state, chunk bases, per-chunk
+// suffix rows, candidate buffers of n entries — never overflow, whatever the distribution —,
+// the candidates' coarse / fine histograms and the candidate stage's range counts).
+long psx_topk_workspace_words(long n) {
+  return (long)TK_NB0 + TK_STATE_WORDS + 2L * TK_BLOCKS + (long)TK_BLOCKS * TK_ROW + 2L * (((n > 0 ? n : 1) + 3) / 4 * 4) +
+         1024 + TK_FINE + 2L * TK_RB;
+}
 
 int psx_topk_payload_words(int kcap) { return 4 + kcap + (kcap + 1) / 2; }
 
 // g: fp16 (g_fp16=1) or fp32 gradient, or NULL (select from resid as is); resid: fp32 error
-// feedback buffer (updated in place); ws: psx_topk_workspace_words() uint32.
+// feedback buffer (updated in place); ws: psx_topk_workspace_words(n) uint32, zeroed once at
+// allocation (every encode leaves its histogram zeroed).
 int psx_topk_encode(const void* g, int g_fp16, float* resid, long n, int k, int kcap, int* payload, uint32_t* ws,
                     hipStream_t st) {
   if (k > kcap) k = kcap;
   if ((long)k > n) k = (int)n;
+  if (k < 1 || n < 1) return (int)hipErrorInvalidValue;
   if (((uintptr_t)resid & 15) || (g && ((uintptr_t)g & (g_fp16 ? 7 : 15)))) return (int)hipErrorInvalidValue;
   uint32_t* hist = ws;
-  uint32_t* state = ws + TK_HIST;
-  const int grid = tk_grid(n);
-  hipLaunchKernelGGL(topk_init_kernel, dim3(1), dim3(256), 0, st, state, hist, payload, k, kcap, n);
+  uint32_t* state = hist + TK_NB0;
+  uint32_t* bases = state + TK_STATE_WORDS;
+  uint32_t* rows = bases + 2 * TK_BLOCKS;
+  int* cidx = (int*)(rows + (size_t)TK_BLOCKS * TK_ROW);
+  float* cval = (float*)(cidx + (n + 3) / 4 * 4);
+  uint32_t* coarse = (uint32_t*)(cval + (n + 3) / 4 * 4);
+  uint32_t* fine = coarse + 1024;
+  uint32_t* rcounts = fine + TK_FINE;
+  const long chunk = tk_chunk(n);
   if (g_fp16)
-    hipLaunchKernelGGL((topk_hist_kernel<0, uint16_t>), dim3(grid), dim3(256), 0, st, (const uint16_t*)g, resid, n,
-                       state, hist);
+    hipLaunchKernelGGL((tk_pass_a<uint16_t>), dim3(TK_BLOCKS), dim3(256), 0, st, (const uint16_t*)g, resid, n, chunk,
+                       hist, rows);
   else
-    hipLaunchKernelGGL((topk_hist_kernel<0, float>), dim3(grid), dim3(256), 0, st, (const float*)g, resid, n, state,
-                       hist);
-  hipLaunchKernelGGL(topk_select_kernel<0>, dim3(1), dim3(256), 0, st, hist, state);
-  hipLaunchKernelGGL((topk_hist_kernel<1, float>), dim3(grid), dim3(256), 0, st, nullptr, resid, n, state, hist);
-  hipLaunchKernelGGL(topk_select_kernel<1>, dim3(1), dim3(256), 0, st, hist, state);
-  hipLaunchKernelGGL((topk_hist_kernel<2, float>), dim3(grid), dim3(256), 0, st, nullptr, resid, n, state, hist);
-  hipLaunchKernelGGL(topk_select_kernel<2>, dim3(1), dim3(256), 0, st, hist, state);
-  uint32_t* counts = state + TK_STATE_WORDS;
-  uint32_t* bases = counts + 2 * TK_BLOCKS;
-  const long chunk = ((n + TK_BLOCKS - 1) / TK_BLOCKS + 255) / 256 * 256;
-  hipLaunchKernelGGL(topk_count_kernel, dim3(TK_BLOCKS), dim3(256), 0, st, resid, n, chunk, state, counts);
-  hipLaunchKernelGGL(topk_scan_kernel, dim3(1), dim3(256), 0, st, counts, bases);
-  hipLaunchKernelGGL(topk_write_kernel, dim3(TK_BLOCKS), dim3(256), 0, st, resid, n, chunk, state, bases, payload,
-                     kcap);
+    hipLaunchKernelGGL((tk_pass_a<float>), dim3(TK_BLOCKS), dim3(256), 0, st, (const float*)g, resid, n, chunk, hist,
+                       rows);
+  hipLaunchKernelGGL(tk_select0, dim3(1), dim3(1024), 0, st, hist, rows, state, bases, k);
+  hipLaunchKernelGGL(tk_pass_b, dim3(TK_BLOCKS), dim3(256), 0, st, resid, n, chunk, state, bases, payload, kcap,
+                     cidx, cval, coarse, fine);
+  hipLaunchKernelGGL(tk_refine_count, dim3(TK_RB), dim3(256), 0, st, cval, state, coarse, fine, rcounts);
+  hipLaunchKernelGGL(tk_refine_write, dim3(TK_RB), dim3(256), 0, st, resid, cidx, cval, state, rcounts, payload, kcap,
+                     n, k, coarse, fine);
   return (int)hipGetLastError();
 }
 

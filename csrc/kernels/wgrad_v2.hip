@@ -337,6 +337,9 @@ __global__ __launch_bounds__(256) void wgrad2f_kernel(Wgrad2Args a) {
 // transposed-read address picks slot (pixel + s - 1), or the zero row when ow + s - 1 leaves
 // the image row; 64-pixel steps hold whole rows because W is a power of two <= 64. Staged
 // bytes per step stay ~16 KB while the MFMA work per step triples (wgrad2 is LDS-DMA bound).
+// G (general widths, e.g. ResNet-50's 56 / 28 / 14 / 7): a step takes PIX = 56 pixels — whole
+// rows of any W dividing 56 — in the 64-row tiles; rows 56..63 are zero on both operands (1/8 of
+// the MFMA work idle), pixel -> (oh, ow) by multiply-high division.
 struct Wgrad3Args {
   const uint16_t* x;
   const uint16_t* dy;
@@ -344,6 +347,8 @@ struct Wgrad3Args {
   const uint16_t* zero;  // (bf16 only)
   int H, W, log2w, IC, OC, Kg, npix;
   int n_c_tiles, n_oc_tiles, splits, steps_per_split;
+  int pix;               // pixels per step (G: 56)
+  FastDiv div_w, div_h;  // (G)
 };
 
 // wait until at most `ahead` later stage groups (PER DMA ops each) are still in flight
@@ -359,7 +364,7 @@ PSX_DEV void wait_ahead(int ahead) {
   }
 }
 
-template <int BC, int NS>
+template <int BC, int NS, bool G>
 __global__ __launch_bounds__(256) void wgrad3_kernel(Wgrad3Args a) {
   constexpr int DROWB = BC * 2, DCPR = DROWB / 16, DRPI = 64 / DCPR, LD = 64 / DRPI / 4;
   constexpr int XT = 65 * 128, DT = 64 * DROWB, STAGE = XT + DT;
@@ -375,8 +380,9 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(Wgrad3Args a) {
   const int oc_t = t % a.n_oc_tiles, rest = t / a.n_oc_tiles;
   const int c_t = rest % a.n_c_tiles, r = rest / a.n_c_tiles;
   const int c0 = c_t * 64, oc0 = oc_t * BC;
-  const int pbeg = split * a.steps_per_split * 64;
-  const int nsteps = min(a.steps_per_split, (a.npix - pbeg + 63) / 64);
+  const int PIX = G ? a.pix : 64;
+  const int pbeg = split * a.steps_per_split * PIX;
+  const int nsteps = min(a.steps_per_split, (a.npix - pbeg + PIX - 1) / PIX);
   const int W = a.W;
 
   // zero row (slot 64) of every stage; the DMA never writes it
@@ -402,19 +408,27 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(Wgrad3Args a) {
 
   auto issue = [&](int st, int stage) {
     unsigned char* base = smem + stage * STAGE;
-    const int p0 = pbeg + st * 64;
+    const int p0 = pbeg + st * PIX;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int pix = p0 + xrow[i];
-      const int ih = ((pix >> a.log2w) & (a.H - 1)) + r - 1;
+      int ih;
+      if constexpr (G) {
+        const int q = fdiv(pix, a.div_w);
+        ih = q - fdiv(q, a.div_h) * a.H + r - 1;
+      } else {
+        ih = ((pix >> a.log2w) & (a.H - 1)) + r - 1;
+      }
       const uint16_t* src = a.zero;
-      if (pix < a.npix && (unsigned)ih < (unsigned)a.H) src = a.x + ((long)pix + xshift) * a.IC + xcol[i];
+      if ((!G || xrow[i] < PIX) && pix < a.npix && (unsigned)ih < (unsigned)a.H)
+        src = a.x + ((long)pix + xshift) * a.IC + xcol[i];
       glds16(src, base + (i * 4 + wid) * 1024);
     }
 #pragma unroll
     for (int i = 0; i < LD; ++i) {
       const int pix = p0 + drow[i];
-      const uint16_t* src = pix < a.npix ? a.dy + (size_t)pix * a.OC + oc0 + dchunk[i] * 8 : a.zero;
+      const bool ok = (!G || drow[i] < PIX) && pix < a.npix;
+      const uint16_t* src = ok ? a.dy + (size_t)pix * a.OC + oc0 + dchunk[i] * 8 : a.zero;
       glds16(src, base + XT + (i * 4 + wid) * 1024);
     }
   };
@@ -427,11 +441,11 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(Wgrad3Args a) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int row = kk * 32 + h * 16 + 4 * g + q;
-      const int ow = row & (W - 1);
+      const int ow = G ? row - fdiv(row, a.div_w) * W : row & (W - 1);
 #pragma unroll
       for (int s = 0; s < 3; ++s) {
         const int iw = ow + s - 1;
-        const int slot = ((unsigned)iw < (unsigned)W) ? row + s - 1 : 64;
+        const int slot = ((!G || row < PIX) && (unsigned)iw < (unsigned)W) ? row + s - 1 : 64;
         soff[kk][h][s] = slot * 128 + ((4 * p & 7) << 1);
         sxr[kk][h][s] = ((slot >> 1) & 3) << 1;
       }
@@ -567,10 +581,10 @@ int launch_w2(const Wgrad2Args& a, hipStream_t st) {
 constexpr int wlds3(int BC, int NS) { return NS * (65 * 128 + 64 * BC * 2); }
 
 // wgrad3 plan, same model as wplan with wgrad3's per-step costs.
-WPlan wplan3(int OC, int IC, int Kg, int npix) {
+WPlan wplan3(int OC, int IC, int Kg, int npix, int pix = 64) {
   WPlan best{0, 64, 3, 1, 0};
   double best_t = 1e30;
-  const int steps = npix / 64;
+  const int steps = npix / pix;
   for (int cfg = 0; cfg < 4; ++cfg) {
     const int BC = cfg & 1 ? 128 : 64, NS = cfg & 2 ? 6 : 3;
     if (OC % BC) continue;
@@ -596,9 +610,9 @@ WPlan wplan3(int OC, int IC, int Kg, int npix) {
   return best;
 }
 
-template <int BC, int NS>
+template <int BC, int NS, bool G = false>
 int launch_w3(const Wgrad3Args& a, hipStream_t st) {
-  hipLaunchKernelGGL((wgrad3_kernel<BC, NS>), dim3(3 * a.n_c_tiles * a.n_oc_tiles * a.splits), dim3(256),
+  hipLaunchKernelGGL((wgrad3_kernel<BC, NS, G>), dim3(3 * a.n_c_tiles * a.n_oc_tiles * a.splits), dim3(256),
                      (size_t)wlds3(BC, NS), st, a);
   return (int)hipGetLastError();
 }
@@ -706,15 +720,19 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
     else e = launch_w2f<64, 64>(a, st);
     return e ? -e : p.splits;
   }
-  // 3x3 stride-1 layers with power-of-two rows: tap-reuse kernel (PSX_WG3=0 disables)
+  // 3x3 stride-1 layers, tap-reuse kernel (PSX_WG3=0 disables): power-of-two rows (64-pixel
+  // steps), or widths dividing 56 (ResNet-50: 56-pixel steps of whole rows, G)
   const char* w3env = getenv("PSX_WG3");
-  if (R == 3 && S == 3 && stride == 1 && pad == 1 && IC % 64 == 0 && (W & (W - 1)) == 0 && (H & (H - 1)) == 0 &&
-      W <= 64 && W >= 2 && a.npix % 64 == 0 && !(w3env && w3env[0] == '0')) {
-    WPlan p = wplan3(OC, IC, Kg, a.npix);
+  const bool w3ok = R == 3 && S == 3 && stride == 1 && pad == 1 && IC % 64 == 0 && !(w3env && w3env[0] == '0');
+  const bool pow2 = (W & (W - 1)) == 0 && (H & (H - 1)) == 0 && W <= 64 && W >= 2 && a.npix % 64 == 0;
+  const bool gen = !pow2 && W >= 2 && 56 % W == 0 && a.npix % 56 == 0;
+  if (w3ok && (pow2 || gen)) {
+    const int pix = pow2 ? 64 : 56;
+    WPlan p = wplan3(OC, IC, Kg, a.npix, pix);
     if (const char* e = getenv("PSX_WG_BC")) p.BC = atoi(e);
     if (const char* e = getenv("PSX_WG_NS")) p.NS = atoi(e) >= 6 ? 6 : 3;
     if (const char* e = getenv("PSX_WG_SPLITS")) {
-      const int steps = a.npix / 64;
+      const int steps = a.npix / pix;
       p.sps = (steps + atoi(e) - 1) / atoi(e);
       p.splits = (steps + p.sps - 1) / p.sps;
     }
@@ -724,8 +742,16 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
     b.x = (const uint16_t*)a.x; b.dy = (const uint16_t*)a.dy; b.part = part; b.zero = (const uint16_t*)a.zero;
     b.H = H; b.W = W; b.log2w = ilog2w(W); b.IC = IC; b.OC = OC; b.Kg = Kg; b.npix = a.npix;
     b.n_c_tiles = IC / 64; b.n_oc_tiles = OC / p.BC; b.splits = p.splits; b.steps_per_split = p.sps;
-    const int e = p.BC == 128 ? (p.NS == 6 ? launch_w3<128, 6>(b, st) : launch_w3<128, 3>(b, st))
-                              : (p.NS == 6 ? launch_w3<64, 6>(b, st) : launch_w3<64, 3>(b, st));
+    b.pix = pix;
+    b.div_w = make_fastdiv(W);
+    b.div_h = make_fastdiv(H);
+    int e;
+    if (pow2)
+      e = p.BC == 128 ? (p.NS == 6 ? launch_w3<128, 6>(b, st) : launch_w3<128, 3>(b, st))
+                      : (p.NS == 6 ? launch_w3<64, 6>(b, st) : launch_w3<64, 3>(b, st));
+    else
+      e = p.BC == 128 ? (p.NS == 6 ? launch_w3<128, 6, true>(b, st) : launch_w3<128, 3, true>(b, st))
+                      : (p.NS == 6 ? launch_w3<64, 6, true>(b, st) : launch_w3<64, 3, true>(b, st));
     return e ? -e : p.splits;
   }
   WPlan p = wplan(OC, Kg, a.npix);

@@ -74,7 +74,7 @@ _KERNEL_SIGS = {
     "psx_nchw_to_nhwc": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, vp]),
     "psx_maxpool3s2_fwd": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "psx_maxpool3s2_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp]),
-    "psx_topk_workspace_words": (i32, []),
+    "psx_topk_workspace_words": (i64, [i64]),
     "psx_topk_payload_words": (i32, [i32]),
     "psx_topk_encode": (i32, [vp, i32, vp, i64, i32, i32, vp, vp, vp]),
     "psx_topk_decode_add": (i32, [vp, vp, f32, i32, vp]),

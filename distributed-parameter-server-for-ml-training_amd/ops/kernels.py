@@ -343,8 +343,8 @@ def maxpool3s2_bwd(dy, arg, dx):
           "maxpool3s2_bwd")
 
 
-def topk_workspace_words() -> int:
-    return kernels().psx_topk_workspace_words()
+def topk_workspace_words(n: int) -> int:
+    return kernels().psx_topk_workspace_words(int(n))
 
 
 def topk_payload_words(kcap: int) -> int:

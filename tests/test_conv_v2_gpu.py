@@ -20,7 +20,8 @@ SHAPES += [(4, 3, 64, 224, 7, 2, 3), (8, 64, 64, 56, 1, 1, 0), (8, 64, 64, 56, 3
            (8, 128, 512, 28, 1, 1, 0), (8, 256, 512, 56, 1, 2, 0), (8, 512, 128, 28, 1, 1, 0),
            (8, 128, 128, 28, 3, 1, 1), (8, 256, 256, 28, 3, 2, 1), (8, 512, 1024, 28, 1, 2, 0),
            (8, 1024, 256, 14, 1, 1, 0), (8, 512, 512, 14, 3, 2, 1), (8, 1024, 2048, 14, 1, 2, 0),
-           (8, 2048, 512, 7, 1, 1, 0), (8, 512, 512, 7, 3, 1, 1), (8, 512, 2048, 7, 1, 1, 0)]
+           (8, 2048, 512, 7, 1, 1, 0), (8, 512, 512, 7, 3, 1, 1), (8, 512, 2048, 7, 1, 1, 0),
+           (8, 256, 256, 14, 3, 1, 1)]
 
 
 def _ws(nb, oh, ow, oc, kg):

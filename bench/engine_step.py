@@ -1,10 +1,11 @@
 """Single-GPU micro-benchmark of the worker training step.
 
 Compares (a) the psx HIP engine (eager launches), (b) the same step replayed from a HIP graph,
-and (c) a PyTorch-ROCm reference step (channels_last, bf16 autocast, MIOpen convs, autograd,
-SGD) on the same ResNet-18 / batch — the library baseline our kernels must beat.
+and (c) a PyTorch-ROCm reference step (channels_last, MIOpen convs, autograd, SGD; bf16 autocast
+for --dtype bf16, plain fp32 with TF32 off for --dtype fp32) on the same ResNet-18 / batch — the
+library baseline our kernels must beat.
 
-    python bench/engine_step.py --batch 128 --iters 50
+    python bench/engine_step.py --batch 128 --iters 50 [--dtype fp32]
 """
 import argparse
 import json
@@ -42,20 +43,24 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--no-torch", action="store_true")
     ap.add_argument("--only", default="")
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     a = ap.parse_args()
+    f32 = a.dtype == "fp32"
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
     B = a.batch
     torch.manual_seed(0)
     model = ResNet18(100)
     layout = ParamLayout.from_module(model)
     arena, _ = layout.pack(model)
     arena = arena.cuda()
-    eng = HipResNetEngine(model, layout, B)
+    eng = HipResNetEngine(model, layout, B, dtype=torch.float32 if f32 else torch.bfloat16)
     n = 50000
     imgs = torch.empty(n, 32, 32, 3, dtype=torch.uint8, device="cuda")
     labs = torch.empty(n, dtype=torch.int32, device="cuda")
     K.synth_gen(imgs, labs, n, 32, 32, 100, 1)
     eng.index.copy_(torch.randperm(n, device="cuda")[:B].to(torch.int32))
-    res = {"batch": B}
+    res = {"batch": B, "dtype": a.dtype}
 
     def step():
         eng.train_step(arena, imgs, labs)
@@ -83,14 +88,14 @@ def main():
 
         def tstep():
             opt.zero_grad(set_to_none=True)
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=not f32):
                 loss = F.cross_entropy(m(x), y)
             loss.backward()
             opt.step()
 
         t = timeit(tstep, a.iters)
-        res["torch_bf16_ms"] = t * 1e3
-        res["torch_bf16_img_s"] = B / t
+        res[f"torch_{a.dtype}_ms"] = t * 1e3
+        res[f"torch_{a.dtype}_img_s"] = B / t
     print(json.dumps(res))
 
 

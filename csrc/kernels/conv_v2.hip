@@ -696,7 +696,7 @@ int launch_tapr(const Conv2Args& a, hipStream_t st) {
 // pad 1, square power-of-two images whose rows tile BN exactly, 64-channel chunks; no split-K.
 // PSX_CV_TAPR=0 disables it, PSX_CV_TAPR_BN=64|128|256 forces the width (sweeps). Other widths
 // (and PSX_CV_TAPR_HALO=1, a test override) take the halo mode with 64-pixel tiles: returns -64.
-int tapr_bn(int R, int S, int stride, int pad, int H, int W, int IC, int OC, int npix) {
+int tapr_bn(int R, int S, int stride, int pad, int H, int W, int IC, int OC, int npix, bool f32 = false) {
   if (const char* e = getenv("PSX_CV_TAPR"))
     if (e[0] == '0') return 0;
   if (R != 3 || S != 3 || stride != 1 || pad != 1 || IC % 64 || OC % 64) return 0;
@@ -709,7 +709,12 @@ int tapr_bn(int R, int S, int stride, int pad, int H, int W, int IC, int OC, int
   // per CU) win or tie on every layer — 32x32x64: 27.3/20.9 vs generic 26.3/23.0; 16x16x128:
   // 18.7/15.8 vs 20.6/19.3; 8x8x256: 14.8/13.7 vs 25.5/23.4; 4x4x512: 20.5/19.2 vs 29.3/28.0
   // (generic = split-K + epilogue launch there); 128/256-pixel tiles (1 workgroup per CU) lose.
-  const int BN = force ? force : 64;
+  // fp32 (scripts/dev/f32_tapr_sweep.sh, us fwd/dgrad): 256-pixel tiles with 64x64 wave tiles (WGM 1)
+  // win while the grid still has >= 256 workgroups — 32x32x64: 95/94 vs 103/97, 16x16x128: 85/84
+  // vs 94/92 — and lose below (8x8x256: 148 vs 89); the f32 MFMA work per stage then hides the
+  // DMA wait at one workgroup per CU
+  int BN = force ? force : 64;
+  if (!force && f32 && npix % 256 == 0 && 256 % W == 0 && (long)(npix / 256) * (OC / 64) >= 256) BN = 256;
   if ((BN != 64 && BN != 128 && BN != 256) || BN % W || npix % BN) return 0;
   return BN;
 }
@@ -769,7 +774,7 @@ int conv_fwd2_t(Conv2Args& a, float* ws, hipStream_t st) {
   const int IC = a.IC, OC = a.OC, Kg = a.Kg;
   a.log2_icc = ilog2i(IC / kEPC<T>);
   if (OC % 64 || Kg % KS || IC % kEPC<T> || (IC & (IC - 1))) return -2;
-  if (const int tbn = tapr_bn(a.R, a.S, a.stride, a.pad, a.IH, a.IW, IC, OC, a.npix))
+  if (const int tbn = tapr_bn(a.R, a.S, a.stride, a.pad, a.IH, a.IW, IC, OC, a.npix, sizeof(T) == 4))
     return dispatch_tapr<T, 0, false>(tbn, a, st);
   const Plan p = plan_for(OC, a.npix, Kg / KS, sizeof(T) == 4);
   a.n_oc_tiles = OC / p.BM;
@@ -789,7 +794,7 @@ int conv_dgrad2_t(Conv2Args& a, float* ws, hipStream_t st) {
   a.log2_icc = ilog2i(OC_fwd / kEPC<T>);
   if (IC_fwd % 64 || Kg % KS || (OC_fwd & (OC_fwd - 1)) || OC_fwd % kEPC<T>) return -2;
   const bool res = a.res != nullptr;
-  if (const int tbn = tapr_bn(a.R, a.S, a.stride, a.pad, H, W, OC_fwd, IC_fwd, a.npix))
+  if (const int tbn = tapr_bn(a.R, a.S, a.stride, a.pad, H, W, OC_fwd, IC_fwd, a.npix, sizeof(T) == 4))
     return res ? dispatch_tapr<T, 1, true>(tbn, a, st) : dispatch_tapr<T, 1, false>(tbn, a, st);
   const Plan p = plan_for(IC_fwd, a.npix, Kg / KS, sizeof(T) == 4);
   a.n_oc_tiles = IC_fwd / p.BM;

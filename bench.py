@@ -59,8 +59,10 @@ class Run:
         self.cfg = cfg = PSConfig(mode=a.mode, staleness_bound=a.staleness_bound, model=a.model, batch_size=a.batch,
                                   train_samples=n_train, lr=0.1, sync_steps=1, epochs=1, eval_every=0, verbose=0,
                                   codec=a.codec, topk_ratio=a.topk_ratio, use_graph=not a.no_graph,
-                                  fetch_codec=a.fetch_codec, overlap=a.overlap, bucket_mb=a.bucket_mb,
+                                  fetch_codec=a.fetch_codec, bucket_mb=a.bucket_mb,
+                                  overlap={"auto": None, "on": True, "off": False}[a.overlap],
                                   topology=topology, dtype=dtype).validate()
+        cfg.resolve_overlap(world)
         model, layout, arena, counters = build_state(cfg)
         self.layout = layout
         wire = torch.float16 if a.codec == "fp16" else torch.float32  # topk encodes from fp32 grads
@@ -200,8 +202,9 @@ def main():
                     help="auto: fp32 for --dtype fp32, bf16conv for bf16. bf16conv: conv weights travel as the "
                          "bf16 bits the workers compute with, everything else fp32; fp32: the reference's full "
                          "fp32 state")
-    ap.add_argument("--overlap", action="store_true",
-                    help="stream gradient buckets (reduce/apply/broadcast) during the backward pass")
+    ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
+                    help="stream gradient buckets (gather/apply/broadcast) during the backward pass; auto: on "
+                         "with >= 2 ranks (sync, dense wire), off at N=1")
     ap.add_argument("--bucket-mb", type=float, default=4.0)
     ap.add_argument("--host-timing", action="store_true", help="report host-side issue time per step (stderr)")
     ap.add_argument("--mode", choices=["sync", "async"], default="sync",

@@ -156,14 +156,19 @@ class OverlapSyncChannel(SyncCollectiveChannel):
     """Sync-mode channel whose push is streamed bucket by bucket during the backward pass.
 
     Every rank issues the same collectives in the same order:
-    reduce(b0), reduce(b1), bcast(b0), reduce(b2), bcast(b1), ..., bcast(b_last),
+    push(b0), push(b1), bcast(b0), push(b2), bcast(b1), ..., bcast(b_last),
     [reduce(BN buffers), bcast(BN buffers)  -- --bn-sync only].
+    push(b) = the workers' wire slices gathered to rank 0 by point-to-point (default, every
+    worker on its own link) and summed there in fp32 in worker order by the range apply
+    (server.apply_range_sources) — the serial round's aggregation; PSX_SYNC_AGG=reduce: an RCCL
+    sum-reduce of the slice (wire-dtype arithmetic at every hop).
     """
 
     overlap = True
 
-    def __init__(self, transport, server=None, members=None, codec=None, buckets=None, device="cpu"):
-        super().__init__(transport, server, members, codec)
+    def __init__(self, transport, server=None, members=None, codec=None, buckets=None, device="cpu",
+                 root_worker=True):
+        super().__init__(transport, server, members, codec, root_worker=root_worker)
         if codec is None:
             raise ValueError("OverlapSyncChannel needs a FetchCodec (its kind selects the wire format)")
         self.buckets = buckets
@@ -182,17 +187,30 @@ class OverlapSyncChannel(SyncCollectiveChannel):
         w, grads = self._red.pop(k)
         b = self.buckets[k]
         if self.server is not None:
-            w.wait()  # compute stream waits for the (normally already finished) reduce
-            self.server.apply_range(grads[b.lo:b.hi], self._weight, b.lo, b.hi)
+            w.wait()  # compute stream waits for the (normally already finished) reduce / gather
+            if self._gather():
+                srcs = ([grads] if self.root_worker else []) + [self._gbufs[r] for r in sorted(self._gbufs)]
+                self.server.apply_range_sources(srcs, self._weight, b.lo, b.hi)
+            else:
+                self.server.apply_range(grads[b.lo:b.hi], self._weight, b.lo, b.hi)
             self.wire.pack(self.server.arena, k)
         else:
             self._works.append(w)
         self._works.append(self.t.broadcast_async(self.wire.segment(k)))
 
+    def _gather(self) -> bool:
+        return self.agg_mode == "gather" and getattr(self.t, "world_size", 1) > 1
+
     def push_bucket(self, k: int, grads: torch.Tensor):
         """Called right after backward segment k has been enqueued on the compute stream."""
         b = self.buckets[k]
-        self._red[k] = (self.t.reduce_async(grads[b.lo:b.hi]), grads)
+        if self._gather():
+            if self.server is not None and self._gbufs is None:
+                self._gbufs = {r: torch.empty_like(grads) for r in range(1, self.t.world_size)}
+            bufs = {r: g[b.lo:b.hi] for r, g in self._gbufs.items()} if self.server is not None else None
+            self._red[k] = (self.t.gather_async(grads[b.lo:b.hi], bufs), grads)
+        else:
+            self._red[k] = (self.t.reduce_async(grads[b.lo:b.hi]), grads)
         if k > 0:
             self._finish_bucket(k - 1)
         self._streamed += 1

@@ -313,6 +313,23 @@ class RcclTransport(DistTransport):
     def reduce_async(self, t):
         return self._on_comm_stream(lambda s: self.comm.reduce_sum(t, 0, stream=s))
 
+    def gather_async(self, t, bufs):
+        """gather_from_workers on the communication stream (one bucket of the overlapped round):
+        one group of ncclRecv on rank 0 (every worker's link at once) / one ncclSend."""
+        def fn(s):
+            lib = comm()
+            if self.rank != 0:
+                self.comm.send(t, 0, stream=s)
+                return
+            _check(lib.psx_comm_group_start(), "ncclGroupStart")
+            try:
+                for r, b in sorted(bufs.items()):
+                    self.comm.recv(b, r, stream=s)
+            finally:
+                _check(lib.psx_comm_group_end(), "ncclGroupEnd")
+
+        return self._on_comm_stream(fn)
+
     def broadcast_async(self, t):
         return self._on_comm_stream(lambda s: self.comm.broadcast(t, 0, stream=s))
 

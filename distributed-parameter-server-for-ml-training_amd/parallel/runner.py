@@ -85,6 +85,7 @@ def _common_steps(cfg, W, n):
 
 # ---------------------------------------------------------------------------- loopback
 def run_local(cfg, log=print) -> dict:
+    cfg.resolve_overlap(1)
     device = _device_for(0)
     W = cfg.workers
     model, layout, arena, counters = build_state(cfg)
@@ -162,6 +163,7 @@ def _interleave(cfg, workers, server, log):
 # ---------------------------------------------------------------------------- distributed
 def run_distributed(cfg, log=print) -> dict:
     rank, world, local = env_world()
+    cfg.resolve_overlap(world)
     device = _device_for(local)
     t = make_transport(device)
     dedicated = cfg.topology == "dedicated" and world > 1
@@ -326,7 +328,8 @@ def make_sync_channel(cfg, t, server, W, layout, device, worker: bool = True):
     codec = FetchCodec(layout, cfg.fetch_codec, device)
     if cfg.overlap and max(1, cfg.sync_steps) == 1 and cfg.codec != "topk":
         buckets = plan_buckets(layout, int(cfg.bucket_mb * (1 << 20)) // 2)
-        return OverlapSyncChannel(t, server, members=list(range(W)), codec=codec, buckets=buckets, device=device)
+        return OverlapSyncChannel(t, server, members=list(range(W)), codec=codec, buckets=buckets, device=device,
+                                  root_worker=server is None or worker)
     wire = None
     if weight_image_enabled(cfg) and torch.device(device).type == "cuda":
         if server is not None:

@@ -118,6 +118,23 @@ class ParameterServer:
             d = buf
         p.sub_(self.lr * d)
 
+    def apply_range_sources(self, srcs: list, weight: float, lo: int, hi: int):
+        """apply_range of the fp32 sum of several wires' [lo:hi] (fixed list order): one bucket
+        of an overlapped round whose wires were gathered (parallel/overlap.py)."""
+        if self.device.type == "cuda":
+            from ..ops import kernels as K
+
+            buf = self.momentum_buf[lo:hi] if self.momentum_buf is not None else None
+            img = self.wire.img[lo:hi] if self.wire is not None else None
+            K.sgd_apply_multi(self.params[lo:hi], [s[lo:hi] for s in srcs], self.lr, gscale=weight,
+                              momentum=self.cfg.momentum, wd=self.cfg.weight_decay, buf=buf, first=self._mom_first,
+                              n=hi - lo, img=img)
+            return
+        agg = torch.zeros(hi - lo, dtype=torch.float32, device=self.device)
+        for s in srcs:  # fixed order, fp32 accumulation
+            agg.add_(s[lo:hi].to(torch.float32))
+        self.apply_range(agg, weight, lo, hi)
+
     def finish_round_apply(self, dt: float = 0.0):
         self._mom_first = False
         self.core.on_applied(dt)  # host-side issue time (device work is stream-ordered)

@@ -59,6 +59,10 @@ class LocalTransport:
         assert not bufs
         return bufs
 
+    def gather_async(self, t, bufs):
+        assert not bufs
+        return _Works([])
+
     def isend(self, t, dst):
         raise RuntimeError("LocalTransport has no peers")
 
@@ -75,6 +79,21 @@ class LocalTransport:
 
     def close(self):
         pass
+
+
+class _Works:
+    """Several point-to-point works as one (wait = all)."""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        return True
+
+    def is_completed(self) -> bool:
+        return all(w.is_completed() for w in self.works)
 
 
 class DistTransport:
@@ -182,6 +201,12 @@ class DistTransport:
 
     # ---- bucketed (overlapped) sync round: non-blocking; RCCL runs on its own stream ordered
     # after the caller's stream at issue time, work.wait() orders the caller's stream after it
+    def gather_async(self, t, bufs):
+        """Non-blocking gather_from_workers (one bucket of the overlapped round)."""
+        if self.rank == 0:
+            return _Works([dist.irecv(b, src=r) for r, b in sorted(bufs.items())])
+        return _Works([dist.isend(t, dst=0)])
+
     def reduce_async(self, t):
         return dist.reduce(t, dst=0, op=dist.ReduceOp.SUM, async_op=True)
 

@@ -68,10 +68,11 @@ class PSConfig:
     # + fp32 for everything else (half the bytes); "fp32" = the reference's full fp32 state;
     # "auto" = fp32 for --dtype fp32, bf16conv for --dtype bf16.
     fetch_codec: str = "auto"
-    # sync rounds stream gradient buckets during the backward pass (parallel/overlap.py).
-    # Opt-in: at N=1 it costs ~0.25 ms/step of cross-queue waits (profiles/README.md), which is
-    # about the xGMI time it can hide at N=8; the serial round stays the default until measured.
-    overlap: bool = False
+    # sync rounds stream gradient buckets during the backward pass (parallel/overlap.py). None =
+    # auto: on with >= 2 ranks (the gather / apply / broadcast of the first buckets hides under
+    # the rest of the backward), off at N=1, where there is no transfer to hide and the
+    # per-bucket graphs cost ~0.2 ms/step (profiles/README.md). resolve_overlap() decides.
+    overlap: object = None
     bucket_mb: float = 4.0         # bucket target size in MiB of fp16 wire gradient
     synthetic: bool = True
     synthetic_kind: str = "proto"  # proto: prototype + noise (learnable); hard: low contrast + 20% label noise
@@ -106,7 +107,7 @@ class PSConfig:
             raise ValueError(f"--topology must be colocated, dedicated or sharded, got {self.topology!r}")
         if self.topology == "sharded":  # parallel/sharded.py scope
             if self.mode != "sync" or self.codec not in ("fp16", "none") or self.bn_sync or self.ckpt_every \
-                    or self.resume or max(1, self.sync_steps) != 1 or self.overlap:
+                    or self.resume or max(1, self.sync_steps) != 1 or self.overlap is True:
                 raise ValueError("--topology sharded: sync mode, dense fp16/fp32 gradients, one push per batch, "
                                  "no --bn-sync / --overlap / checkpoints")
         if self.sync_semantics not in ("barrier", "reference"):
@@ -128,6 +129,14 @@ class PSConfig:
         if not (0.0 < self.topk_ratio <= 1.0):
             raise ValueError("--topk-ratio must be in (0, 1]")
         return self
+
+    def resolve_overlap(self, world: int) -> bool:
+        """--overlap / --no-overlap, or auto: bucketed rounds when there are peers to exchange
+        with and the round qualifies (sync, one push per batch, dense wire, rank-0 server)."""
+        if self.overlap is None:
+            self.overlap = (world > 1 and self.mode == "sync" and max(1, self.sync_steps) == 1
+                            and self.codec != "topk" and self.topology != "sharded")
+        return bool(self.overlap)
 
     def to_json(self) -> str:
         return json.dumps(dataclasses.asdict(self), sort_keys=True)

@@ -327,15 +327,16 @@ def test_plan_buckets_resnet18():
 
 
 @pytest.mark.parametrize("extra", [[], ["--bucket-mb", "0.01"], ["--bucket-mb", "0.01", "--bn-sync"],
-                                   ["--bucket-mb", "0.01", "--fetch-codec", "fp32", "--topology", "dedicated"]])
+                                   ["--bucket-mb", "0.01", "--fetch-codec", "fp32", "--topology", "dedicated"],
+                                   ["--bucket-mb", "0.01", "--codec", "fp16", "--topology", "dedicated"]])
 def test_dist_sync_overlap_matches_serial(extra):
-    """The bucketed/overlapped round must give exactly the serial round's parameters."""
+    """The bucketed/overlapped round must give exactly the serial round's parameters: both gather
+    the wires to rank 0 and sum them in fp32 in worker order (per bucket range vs whole arena)."""
     outs = {}
     for ov in (True, False):
         d = os.path.join("/tmp", f"psx_ov_{os.getpid()}_{int(ov)}")
-        # fp32 wire: an fp16 reduce may round differently when the message is split differently
         args = (["--mode", "sync", "--codec", "none", "--ckpt-every", "1000", "--ckpt-dir", d] + TINY + extra
-                + (["--overlap"] if ov else []))
+                + (["--overlap"] if ov else ["--no-overlap"]))
         recs, _ = _spawn(3, args)
         srv = [r for r in recs if r["type"] == "SERVER_FINAL_METRICS"][0]
         outs[ov] = srv

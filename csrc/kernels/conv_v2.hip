@@ -82,12 +82,14 @@ PSX_DEV const T* gather_src(const Conv2Args& a, int nbase, int hb, int wb, bool 
 // TAPR (3x3 / stride 1 / pad 1, MODE 0 or 1, tiles of whole image rows): tap-reuse mainloop.
 // A macro step = (kernel row r, 64-channel chunk): the three weight tiles of taps (r, 0..2) and
 // ONE window X of the tile's BN pixels at (row r, centre column) are staged; pixel j of tap s
-// reads window slot j + d(s) (d = s - 1 forward, 1 - s dgrad: ih = oh + pad - r there) or a zero
-// row when its column leaves the image row. The im2col operand is staged once per kernel row
+// reads window slot j + d(s) (d = s - 1 forward, 1 - s dgrad: ih = oh + pad - r there); when its
+// column leaves the image row the fragment is zeroed in registers (a per-lane mask fixed for the
+// whole kernel: no zero row in LDS, so a 128-pixel stage fits two workgroups per CU). The im2col
+// operand is staged once per kernel row
 // instead of once per tap (1/3 of the L2->LDS bytes of the gathered operand); 2 LDS stages.
 // TAPR = 1: tiles of whole image rows (power-of-two widths); TAPR = 2 ("halo", any width, e.g.
 // ResNet-50's 56/28/14/7): the window also holds the pixel before and after the tile (slot k =
-// pixel pix0 - 1 + k), so a shift never leaves the staged rows; the zero row sits at slot BN + 2.
+// pixel pix0 - 1 + k), so a shift never leaves the staged rows; a zero row sits at slot BN + 2.
 //
 // T: activation / weight storage type (common.hpp kEPC/kKS): one k-step is a 128-byte row of
 // every operand = 64 bf16 or 32 fp32 channels; the staging below is written in 16-byte chunks
@@ -143,13 +145,11 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   if constexpr (TAPR) {
     static_assert(MODE == 0 || MODE == 1, "tap reuse: forward or stride-1 dgrad");
     constexpr bool HALO = TAPR == 2;
-    constexpr int XROWS = HALO ? BN + 8 : BN + 1, ZS = HALO ? BN + 2 : BN;  // window rows, zero slot
-    constexpr int XOFF = 3 * BM * 128, TST = XOFF + XROWS * 128;            // A0 A1 A2 | X
+    constexpr int XROWS = HALO ? BN + 8 : BN, ZS = BN + 2;  // window rows; the halo mode's zero slot
+    constexpr int XOFF = 3 * BM * 128, TST = XOFF + XROWS * 128;  // A0 A1 A2 | X
     const int nch = a.IC / KS, nmac = 3 * nch;
     const int W = a.OW, log2w = __builtin_ctz(W);
     const int lrow = lane >> 3, lpos = lane & 7;
-    if (!HALO && tid < 16)  // (the halo DMA writes zeros into slots BN+2.. of every stage itself)
-      *reinterpret_cast<uint4*>(smem + (tid >> 3) * TST + XOFF + BN * 128 + (tid & 7) * 16) = uint4{0u, 0u, 0u, 0u};
     const T* wsrc[LA];
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
@@ -195,6 +195,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     // per-lane B-fragment byte offsets of the three taps (tile starts on an image row)
     const int frow = lane & 15, fch = lane >> 4;
     int boff[NT][3];
+    bool keep[NT][3];  // (whole-row tiles) the tap's column is inside the image row
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
       const int prow = wn * (BN / WGN) + n * 16 + frow;
@@ -202,11 +203,13 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
 #pragma unroll
       for (int sx = 0; sx < 3; ++sx) {
         const int d = MODE == 0 ? sx - 1 : 1 - sx;
-        const int slot = (unsigned)(ow + d) < (unsigned)W ? prow + d + (HALO ? 1 : 0) : ZS;
+        const bool in = (unsigned)(ow + d) < (unsigned)W;
+        const int slot = in ? prow + d + (HALO ? 1 : 0) : (HALO ? ZS : prow);
+        keep[n][sx] = HALO || in;
         boff[n][sx] = slot * 128 + ((fch ^ ((slot >> 1) & 7)) << 4);
       }
     }
-    __syncthreads();  // zero rows written
+    if (HALO) __syncthreads();
     if (nmac > 0) issue_t(0, 0);
     for (int t = 0; t < nmac; ++t) {
       wait_vmcnt<0>();
@@ -225,7 +228,10 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
           for (int m = 0; m < MT; ++m)
             fa[m] = *reinterpret_cast<const u32x4*>(A + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
 #pragma unroll
-          for (int n = 0; n < NT; ++n) fb[n] = *reinterpret_cast<const u32x4*>(X + (boff[n][sx] ^ (kk << 6)));
+          for (int n = 0; n < NT; ++n) {
+            fb[n] = *reinterpret_cast<const u32x4*>(X + (boff[n][sx] ^ (kk << 6)));
+            if (!HALO && sx != 1 && !keep[n][sx]) fb[n] = u32x4{0u, 0u, 0u, 0u};
+          }
           mma_tiles<MT, NT, T>(acc, fa, fb);
         }
       }
@@ -394,7 +400,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     constexpr int TS = BM + 4;      // fp32 row stride of the staged tile (spreads the banks)
     constexpr int CPR = BM / 8;     // 8-channel groups per pixel row
     constexpr int RPP = 256 / CPR;  // pixel rows per pass
-    constexpr int LDSB = TAPR ? 2 * (3 * BM * 128 + (TAPR == 2 ? BN + 8 : BN + 1) * 128)
+    constexpr int LDSB = TAPR ? 2 * (3 * BM * 128 + (TAPR == 2 ? BN + 8 : BN) * 128)
                               : 3 * (BM + BN) * 128;  // launched
     static_assert(256 % CPR == 0 && BN * TS * 4 <= LDSB, "staged tile fits the mainloop LDS");
     float* Ts = reinterpret_cast<float*>(smem);
@@ -684,7 +690,7 @@ int dispatch2(const Plan& p, const Conv2Args& a, hipStream_t st) {
 
 template <typename T, int BM, int BN, int MODE, bool RES, int WGM, int TP = 1>
 int launch_tapr(const Conv2Args& a, hipStream_t st) {
-  const size_t lds = (size_t)2 * (3 * BM * 128 + (TP == 2 ? BN + 8 : BN + 1) * 128);
+  const size_t lds = (size_t)2 * (3 * BM * 128 + (TP == 2 ? BN + 8 : BN) * 128);
   Conv2Args b = a;
   with_det(b, a.n_pix_tiles);
   hipLaunchKernelGGL((conv2_kernel<T, BM, BN, MODE, RES, false, WGM, TP>), dim3(a.n_oc_tiles * a.n_pix_tiles),

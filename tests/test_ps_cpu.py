@@ -497,3 +497,18 @@ def test_hung_worker_watchdog_restart(tmp_path):
     steps = -(-(96 // 3) // 8)
     srv = [r for r in recs if r["type"] == "SERVER_FINAL_METRICS"]
     assert srv[-1]["global_steps_completed"] == 2 * steps
+
+
+def test_overlap_auto_resolution():
+    """--overlap auto (None): bucketed rounds with >= 2 ranks for dense sync rounds, never at N=1,
+    with top-k payloads, --sync-steps > 1 or the sharded server; explicit flags win."""
+    from psx.utils.config import PSConfig
+
+    assert PSConfig(mode="sync").validate().resolve_overlap(8) is True
+    assert PSConfig(mode="sync").validate().resolve_overlap(1) is False
+    assert PSConfig(mode="async").validate().resolve_overlap(8) is False
+    assert PSConfig(mode="sync", codec="topk").validate().resolve_overlap(8) is False
+    assert PSConfig(mode="sync", sync_steps=2).validate().resolve_overlap(8) is False
+    assert PSConfig(mode="sync", topology="sharded").validate().resolve_overlap(8) is False
+    assert PSConfig(mode="sync", overlap=False).validate().resolve_overlap(8) is False
+    assert PSConfig(mode="sync", overlap=True).validate().resolve_overlap(1) is True

@@ -508,6 +508,153 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(Wgrad3Args a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// wgrad3f: the fp32 tap-reuse weight gradient (3x3 / stride 1 / pad 1, power-of-two W <= 32).
+// Same decomposition as wgrad3 — one workgroup = kernel row r x 64 input channels x BC output
+// channels x a pixel range, its 192-row tile covering the taps s = 0, 1, 2 — on the exact-f32
+// v_mfma_f32_16x16x4_f32. A stage holds 32 pixels (whole image rows: W divides 32) of x shifted
+// by r - 1 rows and of dy; the A fragment of tap s is the x window read one slot left / in place /
+// one slot right (lane l: channel l & 15 of pixel 4k + (l >> 4) + s - 1). Slots that leave the
+// image row (ow + s - 1 outside [0, W)) are zeroed in registers from a per-lane bit mask over the
+// 8 k-steps, computed once. Compared with wgrad2f (64x64 tiles, one tap per row) the MFMA work
+// per staged byte triples: x is staged once per kernel row instead of once per tap. Rows are
+// 256 B (x) / 256-512 B (dy); the 16-byte chunk index is XOR-ed with bit 2 on odd slots (in the
+// DMA source address), so the two slots a 32-lane read group touches sit 16 banks apart. A
+// 256-byte guard row in front of every stage's x tile absorbs the masked slot -1 read.
+template <int BC, int NS>
+__global__ __launch_bounds__(256) void wgrad3f_kernel(Wgrad3Args a) {
+  constexpr int PS = 32;
+  constexpr int DROWB = BC * 4, DCPR = DROWB / 16, DRPI = 64 / DCPR;
+  constexpr int LX = PS / 4 / 4, LD = PS / DRPI / 4;  // DMA instructions per wave per stage
+  constexpr int GUARD = 256, XT = PS * 256, DT = PS * DROWB, STAGE = GUARD + XT + DT;
+  constexpr int NT = BC / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntile = 3 * a.n_c_tiles * a.n_oc_tiles;
+  const int bid = xcd_remap(blockIdx.x, ntile * a.splits);
+  const int split = bid / ntile, t = bid - split * ntile;
+  const int oc_t = t % a.n_oc_tiles, rest = t / a.n_oc_tiles;
+  const int c_t = rest % a.n_c_tiles, r = rest / a.n_c_tiles;
+  const int c0 = c_t * 64, oc0 = oc_t * BC;
+  const int pbeg = split * a.steps_per_split * PS;
+  const int nsteps = min(a.steps_per_split, (a.npix - pbeg) / PS);
+  const int W = a.W;
+  const float* const xg = (const float*)a.x;
+  const float* const dyg = (const float*)a.dy;
+  const float* const zero = (const float*)a.zero;
+
+  // ---- per-lane DMA state ----
+  int xrow[LX], xcol[LX];
+#pragma unroll
+  for (int i = 0; i < LX; ++i) {
+    const int row = (i * 4 + wid) * 4 + (lane >> 4);
+    xrow[i] = row;
+    xcol[i] = c0 + (((lane & 15) ^ ((row & 1) << 2)) << 2);
+  }
+  int drow[LD], dcol[LD];
+#pragma unroll
+  for (int i = 0; i < LD; ++i) {
+    const int row = (i * 4 + wid) * DRPI + lane / DCPR;
+    drow[i] = row;
+    dcol[i] = oc0 + (((lane % DCPR) ^ ((row & 1) << 2)) << 2);
+  }
+  const long xshift = (long)(r - 1) * W;
+
+  auto issue = [&](int st, int stage) {
+    unsigned char* base = smem + stage * STAGE + GUARD;
+    const int p0 = pbeg + st * PS;
+#pragma unroll
+    for (int i = 0; i < LX; ++i) {
+      const int pix = p0 + xrow[i];
+      const int ih = ((pix >> a.log2w) & (a.H - 1)) + r - 1;
+      const float* src = (unsigned)ih < (unsigned)a.H ? xg + ((long)pix + xshift) * a.IC + xcol[i] : zero;
+      glds16(src, base + (i * 4 + wid) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < LD; ++i) glds16(dyg + (size_t)(p0 + drow[i]) * a.OC + dcol[i], base + XT + (i * 4 + wid) * 1024);
+  };
+
+  // per-lane fragment offsets (relative to the k-step's first slot row) and tap masks
+  const int kq = lane >> 4, col = lane & 15;
+  int aoff[3][2], boff[NT];
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int c = wm * 32 + m * 16 + col;
+      aoff[s][m] = (kq + s - 1) * 256 + ((((c >> 2) ^ (((kq + s + 1) & 1) << 2)) << 4) + ((c & 3) << 2));
+    }
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int c = wn * (BC / 2) + n * 16 + col;
+    boff[n] = kq * DROWB + ((((c >> 2) ^ ((kq & 1) << 2)) << 4) + ((c & 3) << 2));
+  }
+  unsigned lmask = 0, rmask = 0;  // bit k: slot of tap 0 / tap 2 inside the image row at k-step k
+#pragma unroll
+  for (int k = 0; k < PS / 4; ++k) {
+    const int ow = (4 * k + kq) & (W - 1);
+    lmask |= (ow != 0 ? 1u : 0u) << k;
+    rmask |= (ow != W - 1 ? 1u : 0u) << k;
+  }
+
+  f32x4 acc[3][2][NT];
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) acc[s][m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < nsteps) issue(i, i);
+  int stage = 0;
+  for (int st = 0; st < nsteps; ++st) {
+    wait_ahead<LX + LD, NS - 2>(min(NS - 2, nsteps - 1 - st));
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (st + NS - 1 < nsteps) issue(st + NS - 1, stage == 0 ? NS - 1 : stage - 1);
+    const unsigned char* X = smem + stage * STAGE + GUARD;
+    const unsigned char* D = X + XT;
+#pragma unroll
+    for (int k = 0; k < PS / 4; ++k) {
+      float fa[3][2], fb[NT];
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const float v = *reinterpret_cast<const float*>(X + k * 1024 + aoff[s][m]);
+          fa[s][m] = s == 1 ? v : (((s == 0 ? lmask : rmask) >> k) & 1u) ? v : 0.f;
+        }
+#pragma unroll
+      for (int n = 0; n < NT; ++n) fb[n] = *reinterpret_cast<const float*>(D + k * 4 * DROWB + boff[n]);
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int n = 0; n < NT; ++n)
+            acc[s][m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[s][m], fb[n], acc[s][m][n], 0, 0, 0);
+    }
+    stage = stage == NS - 1 ? 0 : stage + 1;
+  }
+
+  float* part = a.part + (size_t)split * a.OC * a.Kg;
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const int k = (r * 3 + s) * a.IC + c0 + wm * 32 + m * 16 + 4 * (lane >> 4);
+        const int oc = oc0 + wn * (BC / 2) + n * 16 + (lane & 15);
+        *reinterpret_cast<f32x4*>(part + (size_t)oc * a.Kg + k) = acc[s][m][n];
+      }
+}
+
 }  // namespace psx
 
 using namespace psx;
@@ -660,6 +807,48 @@ WPlan wplanf(int OC, int Kg, int npix) {
   return best;
 }
 
+constexpr int wlds3f(int BC, int NS) { return NS * (256 + 32 * 256 + 32 * BC * 4); }
+
+// wgrad3f plan: the wplanf round model with the tap-reuse tile (192 x BC per workgroup, 3 x 64 x
+// BC x 32 MACs per stage). eff(k) as measured for the tap-reuse conv mainloops (64-66 % at 2-3
+// co-resident workgroups).
+WPlan wplan3f(int OC, int IC, int Kg, int npix) {
+  WPlan best{0, 64, 3, 1, 0};
+  double best_t = 1e30;
+  const int steps = npix / 32;
+  for (int BC = 64; BC <= 128; BC *= 2) {
+    if (OC % BC) continue;
+    const int NS = 3;
+    int occ = 163840 / wlds3f(BC, NS);
+    if (occ > 3) occ = 3;
+    const long tiles = 3L * (IC / 64) * (OC / BC);
+    const double step_us = 3.0 * 64 * BC / 4.0 / 2100.0;
+    auto eff = [&](int k) { return k <= 1 ? 0.55 : k == 2 ? 0.66 : 0.70; };
+    for (int sp = 1; sp <= 512 && sp <= steps; ++sp) {
+      const int sps = (steps + sp - 1) / sp;
+      const int spl = (steps + sps - 1) / sps;
+      if (sp > 1 && spl != sp) continue;
+      const long wgs = tiles * spl, full = wgs / (256L * occ), rest = wgs - full * 256L * occ;
+      const int krest = (int)((rest + 255) / 256);
+      double t = full * (sps * step_us * occ / eff(occ) + 1.5);
+      if (rest) t += sps * step_us * krest / eff(krest) + 1.5;
+      if (spl > 1) t += spl * (double)OC * Kg * 6.0 / 6e6;
+      if (t < best_t) {
+        best_t = t;
+        best = WPlan{0, BC, NS, spl, sps};
+      }
+    }
+  }
+  return best;
+}
+
+template <int BC>
+int launch_w3f(const Wgrad3Args& a, hipStream_t st) {
+  hipLaunchKernelGGL((wgrad3f_kernel<BC, 3>), dim3(3 * a.n_c_tiles * a.n_oc_tiles * a.splits), dim3(256),
+                     (size_t)wlds3f(BC, 3), st, a);
+  return (int)hipGetLastError();
+}
+
 template <int BR, int BC>
 int launch_w2f(const Wgrad2Args& a, hipStream_t st) {
   const size_t lds = (size_t)3 * 32 * (BR + BC) * 4;
@@ -696,6 +885,28 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
   a.div_ow = make_fastdiv(OW);
   a.div_s = make_fastdiv(S);
   if (OC % 64 || Kg % 64) return -2;
+  const char* w3env = getenv("PSX_WG3");
+  const bool w3ok = R == 3 && S == 3 && stride == 1 && pad == 1 && IC % 64 == 0 && !(w3env && w3env[0] == '0');
+  if (f32 && w3ok && (W & (W - 1)) == 0 && (H & (H - 1)) == 0 && W <= 32 && W >= 2 && a.npix % 32 == 0 &&
+      Kg == 9 * IC) {
+    // 3x3 stride-1 layers: fp32 tap-reuse kernel (PSX_WG3=0 disables)
+    WPlan p = wplan3f(OC, IC, Kg, a.npix);
+    if (const char* e = getenv("PSX_WG_BC")) p.BC = atoi(e);
+    if (const char* e = getenv("PSX_WGF_SPLITS"); e && atoi(e) > 0) {
+      const int steps = a.npix / 32;
+      p.sps = (steps + atoi(e) - 1) / atoi(e);
+      p.splits = (steps + p.sps - 1) / p.sps;
+    }
+    if (OC % p.BC) return -2;
+    if (!part) return p.splits;
+    Wgrad3Args b{};
+    b.x = (const uint16_t*)x; b.dy = (const uint16_t*)dy; b.part = part; b.zero = (const uint16_t*)zero;
+    b.H = H; b.W = W; b.log2w = ilog2w(W); b.IC = IC; b.OC = OC; b.Kg = Kg; b.npix = a.npix;
+    b.n_c_tiles = IC / 64; b.n_oc_tiles = OC / p.BC; b.splits = p.splits; b.steps_per_split = p.sps;
+    b.pix = 32;
+    const int e = p.BC == 128 ? launch_w3f<128>(b, st) : launch_w3f<64>(b, st);
+    return e ? -e : p.splits;
+  }
   if (f32) {
     a.log2_icc = ilog2w(IC / 4);
     if (IC % 4 || (IC & (IC - 1))) return -2;
@@ -722,8 +933,6 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
   }
   // 3x3 stride-1 layers, tap-reuse kernel (PSX_WG3=0 disables): power-of-two rows (64-pixel
   // steps), or widths dividing 56 (ResNet-50: 56-pixel steps of whole rows, G)
-  const char* w3env = getenv("PSX_WG3");
-  const bool w3ok = R == 3 && S == 3 && stride == 1 && pad == 1 && IC % 64 == 0 && !(w3env && w3env[0] == '0');
   const bool pow2 = (W & (W - 1)) == 0 && (H & (H - 1)) == 0 && W <= 64 && W >= 2 && a.npix % 64 == 0;
   const bool gen = !pow2 && W >= 2 && 56 % W == 0 && a.npix % 56 == 0;
   if (w3ok && (pow2 || gen)) {

@@ -44,6 +44,9 @@ struct Conv2Args {
   const float* bsaved1;  // [2][OC] mean, invstd
   const float* bsaved2;
   int bns;
+  // bmask: store dz = g*[o > 0] instead of g, so the BN-backward apply that consumes this output
+  // needs no ReLU-mask operand (one full activation read less per BN layer)
+  int bmask;
   DetRed det;  // deterministic mode: the launch's row slab (bnfin.hpp)
 };
 
@@ -447,7 +450,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] += rr[k];
       }
-      st8((T*)a.out + off, v);  // v = the stored values from here on
+      if (!bwd) st8((T*)a.out + off, v);  // v = the stored values from here on
       if (st) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -457,16 +460,26 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       }
       if (bwd) {
         float om[8], yv[8], y2v[8];
+        if constexpr (sizeof(T) == 2) {  // bf16: the stored (rounded) g feeds the sums
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[i] = bf2f(f2bf(v[i]));
+        }
         ld8((const T*)a.bo + off, om);
         ld8((const T*)a.by1 + off, yv);
         if (two) ld8((const T*)a.by2 + off, y2v);
+        float dzv[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const float dz = om[i] > 0.f ? v[i] : 0.f;
+          dzv[i] = dz;
           s1[i] += dz;
           s2[i] += dz * (yv[i] - bm1[i]) * bi1[i];
           if (two) s3[i] += dz * (y2v[i] - bm2[i]) * bi2[i];
         }
+        if (a.bmask)
+          st8((T*)a.out + off, dzv);
+        else
+          st8((T*)a.out + off, v);
       }
     }
     if (!st && !bwd) return;
@@ -524,7 +537,7 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
                                                             const T* __restrict__ by2,
                                                             const float* __restrict__ bsaved1,
                                                             const float* __restrict__ bsaved2, int bns,
-                                                            DetRed det) {
+                                                            int bmask, DetRed det) {
   extern __shared__ __attribute__((aligned(16))) float sred[];  // [256][24]
   const int cvec = OC >> 3, tpp = 256 / cvec;
   const int cg = threadIdx.x % cvec, pr = threadIdx.x / cvec;
@@ -561,7 +574,7 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += r[j];
     }
-    st8(out + off, v);  // v = the stored values from here on
+    if (!bwd) st8(out + off, v);  // v = the stored values from here on
     if (stats) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -570,16 +583,26 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
       }
     } else if (bwd) {
       float om[8], yv[8], y2v[8];
+      if constexpr (sizeof(T) == 2) {  // bf16: the stored (rounded) g feeds the sums
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = bf2f(f2bf(v[e]));
+      }
       ld8(bo + off, om);
       ld8(by1 + off, yv);
       if (two) ld8(by2 + off, y2v);
+      float dzv[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float dz = om[e] > 0.f ? v[e] : 0.f;
+        dzv[e] = dz;
         st[0][e] += dz;
         st[1][e] += dz * (yv[e] - m1[e]) * i1[e];
         if (two) st[2][e] += dz * (y2v[e] - m2[e]) * i2[e];
       }
+      if (bmask)
+        st8(out + off, dzv);
+      else
+        st8(out + off, v);
     }
   }
   if (!stats && !bwd) return;
@@ -753,11 +776,11 @@ int finish_split(const Conv2Args& a, hipStream_t st) {
   if (a.res)
     hipLaunchKernelGGL((conv_splitk_epilogue<T, true>), dim3(grid), dim3(256), lds, st, a.part, a.splits, a.npix,
                        a.OC, (T*)a.out, (const T*)a.res, a.stats, ppb, a.fuse_fin, a.fin, a.bpart, (const T*)a.bo,
-                       (const T*)a.by1, (const T*)a.by2, a.bsaved1, a.bsaved2, a.bns, det);
+                       (const T*)a.by1, (const T*)a.by2, a.bsaved1, a.bsaved2, a.bns, a.bmask, det);
   else
     hipLaunchKernelGGL((conv_splitk_epilogue<T, false>), dim3(grid), dim3(256), lds, st, a.part, a.splits, a.npix,
                        a.OC, (T*)a.out, (const T*)nullptr, a.stats, ppb, a.fuse_fin, a.fin, a.bpart, (const T*)a.bo,
-                       (const T*)a.by1, (const T*)a.by2, a.bsaved1, a.bsaved2, a.bns, det);
+                       (const T*)a.by1, (const T*)a.by2, a.bsaved1, a.bsaved2, a.bns, a.bmask, det);
   return (int)hipGetLastError();
 }
 
@@ -770,6 +793,7 @@ struct BwdStatsDesc {  // fused BN-backward reduction over the dgrad output (see
   const void* y2;
   const float* saved1;
   const float* saved2;
+  int mask_store;  // store dz = g*[o > 0] instead of g (Conv2Args::bmask)
 };
 
 namespace {
@@ -882,6 +906,7 @@ int psx_conv_dgrad2(const void* dy, const void* wd, void* dx, const void* res, c
     a.bsaved1 = bst->saved1;
     a.bsaved2 = bst->saved2;
     a.bns = bst->y2 ? 3 : 2;
+    a.bmask = bst->mask_store;
   }
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   a.in = dy;

@@ -204,6 +204,12 @@ class HipResNetEngine:
         self.fin_apply = not self.fuse_fin and os.environ.get("PSX_BNFIN_APPLY", "1") == "1"
         self.fuse_bnbwd = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNBWD", "1") == "1"
         self._prereduced = set()
+        # with the fused sums the dgrad epilogue already reads the ReLU mask operand o: it stores
+        # dz = g*[o > 0] instead of g (bwd_stats_desc mask_store), the BN-backward apply then runs
+        # without o (one activation read less per BN layer) and dz doubles as the identity
+        # shortcut's gradient (no dzout copy). PSX_MASK_STORE=0: off
+        self.mask_store = self.fuse_bnbwd and os.environ.get("PSX_MASK_STORE", "1") == "1"
+        self._premasked = set()
         # weight gradients (+ their batched reductions) on a side stream, a parallel branch of the
         # captured step graph next to the dgrad -> BN-backward chain: 1.837/1.841 vs 1.853/1.858
         # ms/step on the main stream (two A/B pairs, session 3); PSX_WGRAD_STREAM=0: main stream
@@ -534,19 +540,33 @@ class HipResNetEngine:
             if bn_next is not None and self.fuse_bnbwd:
                 bs, o, y, two = bn_next
                 st = self.bn[bs.name]
+                ms = self.mask_store
                 if two is None:
-                    bst = K.bwd_stats_desc(self._red(bs, "bwd"), o, y, st["saved"])
+                    bst = K.bwd_stats_desc(self._red(bs, "bwd"), o, y, st["saved"], mask_store=ms)
                 else:
                     bs2, y2 = two
-                    bst = K.bwd_stats_desc(self._red(bs, "bwd"), o, y, st["saved"], y2, self.bn[bs2.name]["saved"])
+                    bst = K.bwd_stats_desc(self._red(bs, "bwd"), o, y, st["saved"], y2, self.bn[bs2.name]["saved"],
+                                           mask_store=ms)
                 self._prereduced.add(bs.name)
+                if ms:
+                    self._premasked.add(bs.name)
             K.conv_dgrad2(dy, wd, dx, res, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
                           cs.kgd, bst=bst)
         else:
             K.conv_dgrad(dy, wd, dx, res, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kgd)
 
     def _bn_bwd(self, bs: BNSpec, arena, g, o, y, dx, npix, two=None, dzout=None):
-        """BN (+ReLU mask from o) backward; two = (bs2, y2, dx2) for a shared-dz second BN."""
+        """BN (+ReLU mask from o) backward; two = (bs2, y2, dx2) for a shared-dz second BN.
+        Returns the buffer that holds dz = g*[o > 0]: ``g`` itself when the producing dgrad stored
+        it masked (mask_store), else ``dzout`` (written here when given)."""
+        if bs.name in self._premasked:
+            self._premasked.discard(bs.name)
+            self._bn_bwd_body(bs, arena, g, None, y, dx, npix, two, None)
+            return g
+        self._bn_bwd_body(bs, arena, g, o, y, dx, npix, two, dzout)
+        return dzout
+
+    def _bn_bwd_body(self, bs: BNSpec, arena, g, o, y, dx, npix, two, dzout):
         st = self.bn[bs.name]
         part = self._red(bs, "bwd")
         fuse = self.fuse_fin
@@ -712,7 +732,7 @@ class HipResNetEngine:
             ds, dbn = b.down
             self._bn_bwd(b.bns[-1], arena, g, d["out"], d["y"][-1], d["dy"][-1], npix, two=(dbn, d["ys"], d["dys"]))
         else:
-            self._bn_bwd(b.bns[-1], arena, g, d["out"], d["y"][-1], d["dy"][-1], npix, dzout=d["dz"])
+            dz = self._bn_bwd(b.bns[-1], arena, g, d["out"], d["y"][-1], d["dy"][-1], npix, dzout=d["dz"])
         for i in range(L - 1, -1, -1):
             cs = b.convs[i]
             x_in = d["inp"] if i == 0 else d["a"][i - 1]
@@ -727,7 +747,7 @@ class HipResNetEngine:
                 self._dgrad(ds, d["dys"], d["dxs"])
                 self._dgrad(cs, d["dy"][0], d["gin"], res=d["dxs"], bn_next=self._bn_into(j))
             else:
-                self._dgrad(cs, d["dy"][0], d["gin"], res=d["dz"], bn_next=self._bn_into(j))
+                self._dgrad(cs, d["dy"][0], d["gin"], res=dz, bn_next=self._bn_into(j))
 
     def _bn_into(self, j: int):
         """The BN whose backward consumes block j's input gradient: the previous block's output

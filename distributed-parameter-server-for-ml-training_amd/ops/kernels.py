@@ -144,11 +144,13 @@ def conv_fwd2(x, wf, y, stats, ws, nb, h, w, ic, oc, k, stride, pad, kg, fin: Bn
 class BwdStatsDesc(C.Structure):
     """csrc/kernels/conv_v2.hip BwdStatsDesc: fused BN-backward reduction over a dgrad output."""
     _fields_ = [("part", C.c_void_p), ("o", C.c_void_p), ("y1", C.c_void_p), ("y2", C.c_void_p),
-                ("saved1", C.c_void_p), ("saved2", C.c_void_p)]
+                ("saved1", C.c_void_p), ("saved2", C.c_void_p), ("mask_store", C.c_int)]
 
 
-def bwd_stats_desc(part, o, y1, saved1, y2=None, saved2=None) -> BwdStatsDesc:
-    return BwdStatsDesc(ptr(part), ptr(o), ptr(y1), ptr(y2), ptr(saved1), ptr(saved2))
+def bwd_stats_desc(part, o, y1, saved1, y2=None, saved2=None, mask_store=False) -> BwdStatsDesc:
+    """``mask_store`` (dgrad only): the epilogue stores dz = g * [o > 0] instead of g, so the BN
+    backward apply reading it runs without the mask operand o."""
+    return BwdStatsDesc(ptr(part), ptr(o), ptr(y1), ptr(y2), ptr(saved1), ptr(saved2), int(bool(mask_store)))
 
 
 def conv_dgrad2(dy, wd, dx, res, ws, nb, h, w, ic_fwd, oc_fwd, k, stride, pad, kgd, bst: BwdStatsDesc | None = None):

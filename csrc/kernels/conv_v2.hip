@@ -18,6 +18,15 @@
 #include "bnfin.hpp"
 #include "pipeline.hpp"
 
+// fp32 register double buffer of the MFMA fragments (A/B builds: csrc/build.py --variant):
+// bit 0 the tap-reuse mainloop, bit 1 the generic one. Same-box A/B (fp32 layers, B=128, us
+// fwd/dgrad): tap reuse 32x32 102.2/96.7 -> 98.9/94.6, 8x8 89.7/87.9 -> 87.1/83.7, 4x4
+// 103.0/96.3 -> 92.9/89.5 (bench 5.15 -> 5.03 ms/step); the generic loop (stride 2, 1x1)
+// measured neutral to 4 % slower, so only bit 0 is on.
+#ifndef PSX_CONV_PF
+#define PSX_CONV_PF 1
+#endif
+
 namespace psx {
 
 struct Conv2Args {
@@ -212,30 +221,90 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
         boff[n][sx] = slot * 128 + ((fch ^ ((slot >> 1) & 7)) << 4);
       }
     }
-    if (HALO) __syncthreads();
-    if (nmac > 0) issue_t(0, 0);
-    for (int t = 0; t < nmac; ++t) {
-      wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (t + 1 < nmac) issue_t(t + 1, (t + 1) & 1);
-      const unsigned char* base = smem + (t & 1) * TST;
-      const unsigned char* X = base + XOFF;
-#pragma unroll
-      for (int sx = 0; sx < 3; ++sx) {
+    if constexpr (sizeof(T) == 4 && (PSX_CONV_PF & 1)) {
+      // Fragments are double-buffered in registers: a macro step is 6 sub-steps q = (tap sx = q/2,
+      // half kk = q%2), and the LDS reads of sub-step q+1 are issued before the MFMAs of q, so the
+      // read latency (one s_waitcnt lgkmcnt(0) in front of every sub-step's MFMAs before) hides
+      // behind them. At the last sub-step the stage boundary comes first — this wave's DMA of the
+      // next stage retired, its own reads of this stage retired (lgkmcnt), barrier, DMA of step t+2
+      // into the stage just drained, reads of the next stage's first sub-step — then its MFMAs.
+      auto load_frags = [&](const unsigned char* base, int q, u32x4(&fa)[MT], u32x4(&fb)[NT]) {
+        const int sx = q >> 1, kk = q & 1;
         const unsigned char* A = base + sx * BM * 128;
+        const unsigned char* X = base + XOFF;
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          u32x4 fa[MT], fb[NT];
+        for (int m = 0; m < MT; ++m)
+          fa[m] = *reinterpret_cast<const u32x4*>(A + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
 #pragma unroll
-          for (int m = 0; m < MT; ++m)
-            fa[m] = *reinterpret_cast<const u32x4*>(A + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
+        for (int n = 0; n < NT; ++n) fb[n] = *reinterpret_cast<const u32x4*>(X + (boff[n][sx] ^ (kk << 6)));
+      };
+      u32x4 fa0[MT], fb0[NT], fa1[MT], fb1[NT];
+      if (HALO) __syncthreads();
+      if (nmac > 0) {
+        issue_t(0, 0);
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (nmac > 1) issue_t(1, 1);
+        load_frags(smem, 0, fa0, fb0);
+      }
+      for (int t = 0; t < nmac; ++t) {
+        const unsigned char* base = smem + (t & 1) * TST;
+        auto sub = [&](auto qc, u32x4(&fa)[MT], u32x4(&fb)[NT], u32x4(&na)[MT], u32x4(&nb)[NT]) {
+          constexpr int q = decltype(qc)::value, sx = q >> 1;
+          if constexpr (q < 5) {
+            load_frags(base, q + 1, na, nb);
+          } else if (t + 1 < nmac) {
+            wait_vmcnt<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (t + 2 < nmac) issue_t(t + 2, t & 1);
+            load_frags(smem + ((t + 1) & 1) * TST, 0, na, nb);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (!HALO && sx != 1) {
 #pragma unroll
-          for (int n = 0; n < NT; ++n) {
-            fb[n] = *reinterpret_cast<const u32x4*>(X + (boff[n][sx] ^ (kk << 6)));
-            if (!HALO && sx != 1 && !keep[n][sx]) fb[n] = u32x4{0u, 0u, 0u, 0u};
+            for (int n = 0; n < NT; ++n)
+              if (!keep[n][sx]) fb[n] = u32x4{0u, 0u, 0u, 0u};
           }
           mma_tiles<MT, NT, T>(acc, fa, fb);
+        };
+        sub(std::integral_constant<int, 0>{}, fa0, fb0, fa1, fb1);
+        sub(std::integral_constant<int, 1>{}, fa1, fb1, fa0, fb0);
+        sub(std::integral_constant<int, 2>{}, fa0, fb0, fa1, fb1);
+        sub(std::integral_constant<int, 3>{}, fa1, fb1, fa0, fb0);
+        sub(std::integral_constant<int, 4>{}, fa0, fb0, fa1, fb1);
+        sub(std::integral_constant<int, 5>{}, fa1, fb1, fa0, fb0);
+      }
+    } else {
+      // bf16: 4 MFMAs of 16 cycles per sub-step are shorter than the read latency; the
+      // register double buffer measured neutral to 5 % slower there, so it keeps one fragment set
+      if (HALO) __syncthreads();
+      if (nmac > 0) issue_t(0, 0);
+      for (int t = 0; t < nmac; ++t) {
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (t + 1 < nmac) issue_t(t + 1, (t + 1) & 1);
+        const unsigned char* base = smem + (t & 1) * TST;
+        const unsigned char* X = base + XOFF;
+#pragma unroll
+        for (int sx = 0; sx < 3; ++sx) {
+          const unsigned char* A = base + sx * BM * 128;
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            u32x4 fa[MT], fb[NT];
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+              fa[m] = *reinterpret_cast<const u32x4*>(A + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+              fb[n] = *reinterpret_cast<const u32x4*>(X + (boff[n][sx] ^ (kk << 6)));
+              if (!HALO && sx != 1 && !keep[n][sx]) fb[n] = u32x4{0u, 0u, 0u, 0u};
+            }
+            mma_tiles<MT, NT, T>(acc, fa, fb);
+          }
         }
       }
     }
@@ -350,32 +419,74 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     }
   };
 
-  if (nk > 0) issue(0, 0);
-  if (nk > 1) issue(1, 1);
   const int frow = lane & 15, fch = lane >> 4;
-  int stage = 0;
-  for (int ks = 0; ks < nk; ++ks) {
-    if (ks + 1 < nk)
-      wait_vmcnt<LA + LB>();
-    else
-      wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (ks + 2 < nk) issue(ks + 2, stage == 0 ? 2 : stage - 1);
-    const unsigned char* A = smem + stage * STAGE;
+  auto load_frags = [&](int stg, int kk, u32x4(&fa)[MT], u32x4(&fb)[NT]) {
+    const unsigned char* A = smem + stg * STAGE;
     const unsigned char* B = A + BM * 128;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      u32x4 fa[MT], fb[NT];
+    for (int m = 0; m < MT; ++m)
+      fa[m] = *reinterpret_cast<const u32x4*>(A + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
-        fa[m] = *reinterpret_cast<const u32x4*>(A + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
-#pragma unroll
-      for (int n = 0; n < NT; ++n)
-        fb[n] = *reinterpret_cast<const u32x4*>(B + kmaj2(wn * (BN / WGN) + n * 16 + frow, kk * 4 + fch));
-      mma_tiles<MT, NT, T>(acc, fa, fb);
+    for (int n = 0; n < NT; ++n)
+      fb[n] = *reinterpret_cast<const u32x4*>(B + kmaj2(wn * (BN / WGN) + n * 16 + frow, kk * 4 + fch));
+  };
+  if (nk > 0) issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  if constexpr (sizeof(T) == 4 && (PSX_CONV_PF & 2)) {
+    // fp32: the fragments of the next half k-step are read before the MFMAs of the current one
+    // (register double buffer, as in the tap-reuse loop); the stage boundary — DMA of k-step
+    // ks+1 retired, this wave's reads of stage ks retired, barrier, DMA of ks+3 into stage ks —
+    // sits between the two halves of k-step ks.
+    u32x4 fa0[MT], fb0[NT], fa1[MT], fb1[NT];
+    if (nk > 0) {
+      if (nk > 1)
+        wait_vmcnt<LA + LB>();
+      else
+        wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (nk > 2) issue(2, 2);
+      load_frags(0, 0, fa0, fb0);
     }
-    stage = stage == 2 ? 0 : stage + 1;
+    int stage = 0;
+    for (int ks = 0; ks < nk; ++ks) {
+      const int nxt = stage == 2 ? 0 : stage + 1;
+      load_frags(stage, 1, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_tiles<MT, NT, T>(acc, fa0, fb0);
+      if (ks + 1 < nk) {
+        if (ks + 2 < nk)
+          wait_vmcnt<LA + LB>();
+        else
+          wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (ks + 3 < nk) issue(ks + 3, stage);
+        load_frags(nxt, 0, fa0, fb0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mma_tiles<MT, NT, T>(acc, fa1, fb1);
+      stage = nxt;
+    }
+  } else {
+    int stage = 0;
+    for (int ks = 0; ks < nk; ++ks) {
+      if (ks + 1 < nk)
+        wait_vmcnt<LA + LB>();
+      else
+        wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (ks + 2 < nk) issue(ks + 2, stage == 0 ? 2 : stage - 1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        u32x4 fa[MT], fb[NT];
+        load_frags(stage, kk, fa, fb);
+        mma_tiles<MT, NT, T>(acc, fa, fb);
+      }
+      stage = stage == 2 ? 0 : stage + 1;
+    }
   }
   }  // generic mainloop
 

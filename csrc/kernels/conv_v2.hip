@@ -26,6 +26,9 @@
 #ifndef PSX_CONV_PF
 #define PSX_CONV_PF 1
 #endif
+#ifndef PSX_TAPR_F32_128
+#define PSX_TAPR_F32_128 1
+#endif
 
 namespace psx {
 
@@ -855,6 +858,12 @@ int tapr_bn(int R, int S, int stride, int pad, int H, int W, int IC, int OC, int
   // DMA wait at one workgroup per CU
   int BN = force ? force : 64;
   if (!force && f32 && npix % 256 == 0 && 256 % W == 0 && (long)(npix / 256) * (OC / 64) >= 256) BN = 256;
+#if PSX_TAPR_F32_128
+  // fp32 with the register double buffer: 128-pixel tiles (two workgroups per CU, one's epilogue
+  // under the other's mainloop) where they fill two full rounds of the chip. Same-box A/B: 32x32x64
+  // 102.9/96.8 -> 99.2/94.0 us fwd/dgrad, 16x16 equal; bench 4.977 -> 4.936/4.946 ms/step
+  if (!force && f32 && npix % 128 == 0 && 128 % W == 0 && (long)(npix / 128) * (OC / 64) >= 512) BN = 128;
+#endif
   if ((BN != 64 && BN != 128 && BN != 256) || BN % W || npix % BN) return 0;
   return BN;
 }

@@ -51,7 +51,10 @@ print("RESULT " + json.dumps(res))
 
 
 def _run(code, port, extra_env=None, timeout=240):
-    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # PSX_COMM_SELF=1: issue the one-rank collectives through RCCL (they are skipped as identities
+    # otherwise), so this file exercises the RCCL call path
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               PSX_COMM_SELF="1")
     env.update(extra_env or {})
     r = subprocess.run([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                        timeout=timeout)

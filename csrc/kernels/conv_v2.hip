@@ -26,6 +26,16 @@
 #ifndef PSX_CONV_PF
 #define PSX_CONV_PF 1
 #endif
+// bf16: the same double buffer in the tap-reuse loop, and 256-pixel tiles (64x64 wave tiles)
+// where they keep >= 256 workgroups. Same-box A/B (bf16 layers, us fwd/dgrad): 32x32 30.9/23.0
+// -> 25.5/22.0, 16x16 22.9/19.4 -> 18.9/17.3, 4x4 23.5/22.0 -> 21.1/19.7; bench --dtype bf16
+// 1.858 -> 1.81-1.83 ms/step (the tiles alone: 1.838)
+#ifndef PSX_CONV_PF_BF16
+#define PSX_CONV_PF_BF16 1
+#endif
+#ifndef PSX_TAPR_BF16_256
+#define PSX_TAPR_BF16_256 1
+#endif
 #ifndef PSX_TAPR_F32_128
 #define PSX_TAPR_F32_128 1
 #endif
@@ -224,7 +234,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
         boff[n][sx] = slot * 128 + ((fch ^ ((slot >> 1) & 7)) << 4);
       }
     }
-    if constexpr (sizeof(T) == 4 && (PSX_CONV_PF & 1)) {
+    if constexpr ((sizeof(T) == 4 || PSX_CONV_PF_BF16) && (PSX_CONV_PF & 1)) {
       // Fragments are double-buffered in registers: a macro step is 6 sub-steps q = (tap sx = q/2,
       // half kk = q%2), and the LDS reads of sub-step q+1 are issued before the MFMAs of q, so the
       // read latency (one s_waitcnt lgkmcnt(0) in front of every sub-step's MFMAs before) hides
@@ -281,8 +291,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
         sub(std::integral_constant<int, 5>{}, fa1, fb1, fa0, fb0);
       }
     } else {
-      // bf16: 4 MFMAs of 16 cycles per sub-step are shorter than the read latency; the
-      // register double buffer measured neutral to 5 % slower there, so it keeps one fragment set
+      // single fragment set (PSX_CONV_PF_BF16=0 builds)
       if (HALO) __syncthreads();
       if (nmac > 0) issue_t(0, 0);
       for (int t = 0; t < nmac; ++t) {
@@ -857,7 +866,8 @@ int tapr_bn(int R, int S, int stride, int pad, int H, int W, int IC, int OC, int
   // vs 94/92 — and lose below (8x8x256: 148 vs 89); the f32 MFMA work per stage then hides the
   // DMA wait at one workgroup per CU
   int BN = force ? force : 64;
-  if (!force && f32 && npix % 256 == 0 && 256 % W == 0 && (long)(npix / 256) * (OC / 64) >= 256) BN = 256;
+  if (!force && (f32 || PSX_TAPR_BF16_256) && npix % 256 == 0 && 256 % W == 0 && (long)(npix / 256) * (OC / 64) >= 256)
+    BN = 256;
 #if PSX_TAPR_F32_128
   // fp32 with the register double buffer: 128-pixel tiles (two workgroups per CU, one's epilogue
   // under the other's mainloop) where they fill two full rounds of the chip. Same-box A/B: 32x32x64

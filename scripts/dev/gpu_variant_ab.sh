@@ -2,7 +2,8 @@
 # GPU-box helper: same-box A/B of kernel-library variants (csrc/build.py --variant NAME ...):
 # fp32 per-layer conv bench and the fp32 bench step for the default build and each variant.
 # Usage: bash scripts/dev/gpu_variant_ab.sh TAG VARIANT...   (VARIANT = a build name, or
-# env:NAME=VALUE to run the default build with that environment variable set)
+# env:NAME=VALUE to run the default build with that environment variable set); DTYPE=bf16 runs
+# the bf16 layer bench and bench.py --dtype bf16 instead
 set -o pipefail
 export TMPDIR=/tmp
 T=$1; shift
@@ -16,7 +17,11 @@ for v in default "$@" default; do
     env:*) export "${v#env:}" ;;
     *) export PSX_KERNELS_LIB=$PWD/$V/libpsx_kernels_$v.so ;;
   esac
-  MIOPEN=0 timeout -k 10 300 python bench/conv_layers_f32.py > $OUT/layers_$v.jsonl 2> $OUT/layers_$v.err || exit $?
-  timeout -k 10 200 python bench.py --steps 30 --warmup 5 --secondary none >> $OUT/bench_$v.log 2>&1 || exit $?
+  if [ "${DTYPE:-fp32}" = bf16 ]; then
+    timeout -k 10 300 python bench/conv_layers.py > $OUT/layers_$v.jsonl 2> $OUT/layers_$v.err || exit $?
+  else
+    MIOPEN=0 timeout -k 10 300 python bench/conv_layers_f32.py > $OUT/layers_$v.jsonl 2> $OUT/layers_$v.err || exit $?
+  fi
+  timeout -k 10 200 python bench.py --steps 30 --warmup 5 --secondary none --dtype ${DTYPE:-fp32} >> $OUT/bench_$v.log 2>&1 || exit $?
   case "$v" in env:*) unset "$(echo ${v#env:} | cut -d= -f1)" ;; esac
 done

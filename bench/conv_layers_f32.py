@@ -71,6 +71,27 @@ def main():
             r["wgrad_splits"] = spl
             r["wgrad_us"] = t_us(lambda: K.conv_wgrad2(xh, dy, part, B, hw, hw, cp, cout, k, s, p, kg))
             r["wreduce_us"] = t_us(lambda: K.wgrad_reduce(part, spl, cout, kg, cin, cp, k, 1.0, out.data_ptr(), True))
+        if k == 3 and s == 1 and cin >= 64 and K.wino_ok(hw, hw, cin, cout) and not only:
+            # Winograd F(4x4,3x3) (csrc/kernels/wino.hip): forward / data gradient per GEMM tile
+            # config, and the per-step weight transforms (forward + flipped)
+            u = torch.empty(36 * cout * cin, device="cuda")
+            ud = torch.empty(36 * cout * cin, device="cuda")
+            nv = max(K.wino_v_floats(B, hw, hw, cin), K.wino_v_floats(B, hw, hw, cout))
+            v1, v2 = torch.empty(nv, device="cuda"), torch.empty(nv, device="cuda")
+            xw = x.permute(0, 2, 3, 1).contiguous()
+            r["wino_wt_us"] = t_us(lambda: (K.wino_weights(w, u, cout, cin), K.wino_weights(w, ud, cout, cin, True)))
+            for cfg in range(4):
+                r[f"wino_fwd_c{cfg}_us"] = t_us(lambda: K.wino_conv(xw, u, y, None, stats, v1, v2, B, hw, hw, cin,
+                                                                    cout, cfg=cfg))
+                r[f"wino_dgrad_c{cfg}_us"] = t_us(lambda: K.wino_conv(dy, ud, dx, None, None, v2, v1, B, hw, hw, cout,
+                                                                      cin, cfg=cfg))
+            K.wino_conv(xw, u, y, None, stats, v1, v2, B, hw, hw, cin, cout)
+            q = K.wino_wgrad_q(B, hw, hw, cin, cout)
+            if q > 0:
+                wpart = torch.empty(36 * q * cout * cin, device="cuda")
+                gout = torch.empty(cout * cin * 9, dtype=torch.float16, device="cuda")
+                r["wino_wgrad_q"] = q
+                r["wino_wgrad_us"] = t_us(lambda: K.wino_wgrad(v1, dy, v2, wpart, gout, B, hw, hw, cin, cout))
         psx_us = sum(r.get(key, 0.0) for key in ("fwd_us", "dgrad_us", "wgrad_us", "wreduce_us"))
         tot["psx"] += cnt * psx_us
         if miopen:

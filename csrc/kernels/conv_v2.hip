@@ -1054,4 +1054,37 @@ int psx_conv_dgrad2(const void* dy, const void* wd, void* dx, const void* res, c
   return f32 ? conv_dgrad2_t<float>(a, ws, st) : conv_dgrad2_t<uint16_t>(a, ws, st);
 }
 
+// nb independent fp32 GEMMs P[b][M][N] = A[b] . B[:, b, :]^T with A [nb][M][Kd] (batch-major
+// rows) and B [N][nb][Kd], Kd a power of two >= 32, on the conv mainloop: an implicit GEMM over M
+// "pixels" whose nb "taps" are the batches — the operand is an image of nb rows x M columns
+// (R = nb, S = 1: tap b reads row b, i.e. A[b]) — split-K into nb slabs of Kd, so split s is
+// exactly batch s (the Winograd GEMMs, wino.hip). cfg: tile (0: 64x64, 1: 64x128, 2: 64x256 /
+// 1x4 waves, 3: 64x128 / 1x4 waves; N rows x M pixels).
+int psx_bgemm_f32(const float* A, const float* B, float* P, const void* zero, int M, int N, int Kd, int nb, int cfg,
+                  hipStream_t st) {
+  if (N % 64 || Kd < kKS<float> || (Kd & (Kd - 1)) || M < 1 || nb < 1) return -2;
+  Plan p{64, 64, nb, 2};
+  if (cfg == 1) p.BN = 128;
+  if (cfg == 2) { p.BN = 256; p.WGM = 1; }
+  if (cfg == 3) { p.BN = 128; p.WGM = 1; }
+  Conv2Args a{};
+  a.in = A;
+  a.w = B;
+  a.out = nullptr;
+  a.part = P;
+  a.zero = zero;
+  a.Nb = 1; a.IH = nb; a.IW = M; a.OH = 1; a.OW = M;
+  a.IC = Kd;
+  a.OC = N;
+  a.R = nb; a.S = 1; a.pad = 0; a.stride = 1;
+  a.Kg = nb * Kd;
+  a.log2_icc = ilog2i(Kd / kEPC<float>);
+  a.npix = M;
+  a.n_oc_tiles = N / 64;
+  a.n_pix_tiles = (M + p.BN - 1) / p.BN;
+  a.splits = nb;
+  a.kps = Kd / kKS<float>;
+  return nb > 1 ? dispatch2<float, 0, false>(p, a, st) : -2;
+}
+
 }  // extern "C"

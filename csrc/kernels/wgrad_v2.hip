@@ -867,6 +867,36 @@ int ilog2w(int v) {
 
 extern "C" {
 
+// Batched TN GEMMs part[b * q + j][K][C] = sum over tiles t in range j of D[b][t][:]^T . X[b][t][:]
+// with X [nb][T][C], D [nb][T][K] (the Winograd weight gradient, wino.hip): wgrad2f_kernel as a
+// 1x1 weight gradient over nb * T pixels whose split s = b * q + j covers T / q pixels of batch b.
+// T % (32 q) == 0; BR | C, BC | K (64 or 128); C a power of two.
+int psx_bgemm_tn_f32(const float* X, const float* D, float* part, const void* zero, int T, int C, int K, int nb, int q,
+                     int BR, int BC, hipStream_t st) {
+  if (q < 1 || T % (32 * q) || C % BR || K % BC || (C & (C - 1)) || (BR != 64 && BR != 128) || (BC != 64 && BC != 128))
+    return -2;
+  Wgrad2Args a{};
+  a.x = X;
+  a.dy = D;
+  a.part = part;
+  a.zero = zero;
+  a.IH = a.IW = 1; a.IC = C; a.OC = K; a.R = a.S = 1; a.pad = 0; a.stride = 1;
+  a.Kg = C;
+  a.log2_icc = ilog2w(C / 4);
+  a.npix = nb * T;
+  a.div_ohw = make_fastdiv(1);
+  a.div_ow = make_fastdiv(1);
+  a.div_s = make_fastdiv(1);
+  a.n_k_tiles = C / BR;
+  a.n_oc_tiles = K / BC;
+  a.splits = nb * q;
+  a.steps_per_split = T / q / 32;
+  if (BR == 128 && BC == 128) return launch_w2f<128, 128>(a, st);
+  if (BR == 128) return launch_w2f<128, 64>(a, st);
+  if (BC == 128) return launch_w2f<64, 128>(a, st);
+  return launch_w2f<64, 64>(a, st);
+}
+
 // Returns the split count (query with part == nullptr); partials need splits*OC*Kg floats.
 // f32: x / dy are fp32 (wgrad2f_kernel) instead of bf16.
 int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero, int Nb, int H, int W, int IC, int OC,

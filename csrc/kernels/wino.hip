@@ -1,0 +1,374 @@
+// fp32 Winograd F(4x4, 3x3) convolution for the small-image 3x3 / stride-1 / pad-1 layers
+// (ResNet-18 CIFAR stages 2-4: 16x16x128, 8x8x256 and 4x4x512, forward and data gradient).
+// Same-box per layer (B=128, us fwd / dgrad, direct -> Winograd incl. transforms): 16x16 85/82 ->
+// 54/54, 8x8 86/84 -> 44/44, 4x4 91/89 -> 46/45; 32x32x64 ties (98 vs 98: its transformed
+// operands, 75 MB each, make the transforms the cost), so it stays direct.
+//
+// Why: on those layers the direct implicit GEMM is MFMA-bound at fp32 (v_mfma_f32_16x16x4_f32,
+// 1/16 of the bf16 rate) while the activations are small (8.4 / 4.2 MB at B=128), so trading
+// multiplies for transform traffic pays: F(4x4,3x3) does 36 products per 16 outputs instead of
+// 144 (4x fewer MFMA flops) for ~2.25x the activation bytes in the transformed domain. The
+// arithmetic stays fp32 end to end (transforms, MFMA operands, fp32 accumulation): relative
+// error vs an fp64 reference ~3e-6 (direct fp32: ~2e-7) — the algorithm MIOpen / cuDNN pick for
+// fp32 3x3 convolutions. PSX_WINO=0 (engine) keeps the direct kernels.
+//
+// Layouts (T = N * (H/4) * (W/4) output tiles, tile t = (n, ti, tj)):
+//   V [36][T][C]   input tiles d (6x6 window at (4ti-1, 4tj-1), zero padded) -> B^T d B
+//   U [K][36][C]   weights g (3x3) -> G g G^T           (dgrad: U'[C][36][K] of rot180(g)^T)
+//   P [36][T][K]   36 independent GEMMs P[b] = V[b] . U[:, b, :]^T, run as ONE launch of the
+//                  conv_v2 LDS-DMA mainloop (an implicit GEMM over T pixels whose 36 "taps" are
+//                  the batches, split-K into 36 slabs of C = exactly the 36 batches; psx_bgemm_f32)
+//   y [N][H][W][K] A^T P A per tile (+ residual) and the BN partial sums of y (slot rows, as the
+//                  conv epilogue writes them)
+// Weight gradient (F(3x3,4x4) by transposition: dg = G^T [sum_t (A dy_t A^T) . V_t] G):
+//   D [36][T][K]   dy tiles -> A dy A^T
+//   M [36][K][C]   M[b] = D[b]^T . V[b]: 36 TN GEMMs reduced over the T tiles, ONE launch of the
+//                  fp32 weight-gradient mainloop (wgrad2f_kernel as a 1x1 wgrad over 36*T pixels
+//                  whose split s covers exactly batch s (x q tile ranges); psx_bgemm_tn_f32)
+//   dW [K][C][3][3] G^T M G straight into the gradient wire (fp16 codec or fp32)
+// Matrices (points 0, +-1, +-2, inf; checked against torch float64 in tests/test_wino_gpu.py):
+//   B^T = [4 0 -5 0 1 0; 0 -4 -4 1 1 0; 0 4 -4 -1 1 0; 0 -2 -1 2 1 0; 0 2 -1 -2 1 0; 0 4 0 -5 0 1]
+//   G   = [1/4 0 0; -1/6 -1/6 -1/6; -1/6 1/6 -1/6; 1/24 1/12 1/6; 1/24 -1/12 1/6; 0 0 1]
+//   A^T = [1 1 1 1 1 0; 0 1 -1 2 -2 0; 0 1 1 4 4 0; 0 1 -1 8 -8 1]
+#include <stdlib.h>
+
+#include "common.hpp"
+
+extern "C" int psx_bgemm_f32(const float* A, const float* B, float* P, const void* zero, int M, int N, int Kd, int nb,
+                             int cfg, hipStream_t st);
+extern "C" int psx_bgemm_tn_f32(const float* X, const float* D, float* part, const void* zero, int T, int C, int K,
+                                int nb, int q, int BR, int BC, hipStream_t st);
+
+namespace psx {
+
+PSX_DEV void wino_bt6(const float (&d)[6], float (&r)[6]) {
+  r[0] = 4.f * d[0] - 5.f * d[2] + d[4];
+  r[1] = -4.f * (d[1] + d[2]) + d[3] + d[4];
+  r[2] = 4.f * (d[1] - d[2]) - d[3] + d[4];
+  r[3] = 2.f * (d[3] - d[1]) - d[2] + d[4];
+  r[4] = 2.f * (d[1] - d[3]) - d[2] + d[4];
+  r[5] = 4.f * d[1] - 5.f * d[3] + d[5];
+}
+
+PSX_DEV void wino_at6(const float (&m)[6], float (&o)[4]) {
+  const float a = m[1] + m[2], b = m[1] - m[2], c = m[3] + m[4], d = m[3] - m[4];
+  o[0] = m[0] + a + c;
+  o[1] = b + 2.f * d;
+  o[2] = a + 4.f * c;
+  o[3] = b + 8.f * d + m[5];
+}
+
+// V[b][t][c]: one thread per (tile, channel); block = 64 channels x 4 tiles
+__global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ x, float* __restrict__ V, int T, int H,
+                                                      int W, int C) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int tw = W >> 2, tpi = (H >> 2) * tw;
+  for (int t = blockIdx.y * 4 + (threadIdx.x >> 6); t < T; t += 4 * gridDim.y) {
+    const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
+    const int h0 = 4 * ti - 1, w0 = 4 * tj - 1;
+    const float* xn = x + (size_t)n * H * W * C + c;
+    float d[6][6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {
+        const int h = h0 + r, w = w0 + s;
+        d[r][s] = ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) ? xn[((size_t)h * W + w) * C] : 0.f;
+      }
+    float e[6][6];  // e = B^T d (columns)
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      float col[6] = {d[0][s], d[1][s], d[2][s], d[3][s], d[4][s], d[5][s]}, r6[6];
+      wino_bt6(col, r6);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) e[r][s] = r6[r];
+    }
+    float* vt = V + (size_t)t * C + c;
+    const size_t bs = (size_t)T * C;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {  // rows: (B^T d) B
+      float r6[6];
+      wino_bt6(e[r], r6);
+#pragma unroll
+      for (int s = 0; s < 6; ++s) vt[(r * 6 + s) * bs] = r6[s];
+    }
+  }
+}
+
+__constant__ float kWinoG[6][3] = {{0.25f, 0.f, 0.f},
+                                   {-1.f / 6.f, -1.f / 6.f, -1.f / 6.f},
+                                   {-1.f / 6.f, 1.f / 6.f, -1.f / 6.f},
+                                   {1.f / 24.f, 1.f / 12.f, 1.f / 6.f},
+                                   {1.f / 24.f, -1.f / 12.f, 1.f / 6.f},
+                                   {0.f, 0.f, 1.f}};
+
+// U[row][b][col] = (G g G^T)[b], g = w[k][c] (fwd: row k, col c) or rot180(w[k][c]) (dgrad: row
+// c, col k). One thread per (row, col) pair — every weight read once — col fastest (each of its
+// 36 stores is a coalesced 256-byte wave row), 64-thread workgroups so a 128-channel layer still
+// spreads over 256 CUs. Measured alternatives (B=128 per-layer bench, fwd + flipped pair, 512
+// channels): a thread per (pair, output row) 45.6 us (6 scattered re-reads of every weight in the
+// flipped case), a thread per output element 225 us; this one 22.8 us.
+__global__ __launch_bounds__(64) void wino_w_kernel(const float* __restrict__ w, float* __restrict__ U, int K, int C,
+                                                    int flip) {
+  const int rows = flip ? C : K, cols = flip ? K : C;
+  const long i = (long)blockIdx.x * 64 + threadIdx.x;
+  if (i >= (long)rows * cols) return;
+  const int row = (int)(i / cols), col = (int)(i - (long)row * cols);
+  const int k = flip ? col : row, c = flip ? row : col;
+  const float* g = w + ((size_t)k * C + c) * 9;
+  float gg[3][3];
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) gg[p][q] = flip ? g[(2 - p) * 3 + (2 - q)] : g[p * 3 + q];
+  float* dst = U + (size_t)row * 36 * cols + col;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    float gr[3];  // (G g)[r][q]
+#pragma unroll
+    for (int q = 0; q < 3; ++q) gr[q] = kWinoG[r][0] * gg[0][q] + kWinoG[r][1] * gg[1][q] + kWinoG[r][2] * gg[2][q];
+#pragma unroll
+    for (int s = 0; s < 6; ++s)
+      dst[(size_t)(r * 6 + s) * cols] = kWinoG[s][0] * gr[0] + kWinoG[s][1] * gr[1] + kWinoG[s][2] * gr[2];
+  }
+}
+
+// y = A^T P A (+ res); BN partial sums (sum y, sum y^2) of the stored values into slot rows
+// stats[slot][2][K]. Block = 64 channels x 4 tiles; grid.y strides over the tiles.
+__global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__ P, float* __restrict__ y,
+                                                       const float* __restrict__ res, float* __restrict__ stats, int T,
+                                                       int H, int W, int K) {
+  __shared__ float red[2][4][64];
+  const int kl = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + kl;
+  const int tw = W >> 2, tpi = (H >> 2) * tw;
+  const size_t bstride = (size_t)T * K;
+  float s1 = 0.f, s2 = 0.f;
+  for (int t = blockIdx.y * 4 + ty; t < T; t += 4 * gridDim.y) {
+    const float* pt = P + (size_t)t * K + k;
+    float m[6][6];
+#pragma unroll
+    for (int b = 0; b < 36; ++b) m[b / 6][b % 6] = pt[b * bstride];
+    float e[4][6];  // e = A^T m (columns)
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      float col[6] = {m[0][s], m[1][s], m[2][s], m[3][s], m[4][s], m[5][s]}, o[4];
+      wino_at6(col, o);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) e[i][s] = o[i];
+    }
+    const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
+    const size_t base = (((size_t)n * H + 4 * ti) * W + 4 * tj) * K + k;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float o[4];
+      wino_at6(e[i], o);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t off = base + ((size_t)i * W + j) * K;
+        float v = o[j];
+        if (res) v += res[off];
+        y[off] = v;
+        s1 += v;
+        s2 += v * v;
+      }
+    }
+  }
+  if (!stats) return;
+  red[0][ty][kl] = s1;
+  red[1][ty][kl] = s2;
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const int which = threadIdx.x >> 6;
+    const float v = red[which][0][kl] + red[which][1][kl] + red[which][2][kl] + red[which][3][kl];
+    float* dst = stats + (size_t)(blockIdx.y & (PSX_STAT_SLOTS - 1)) * 2 * K + (size_t)which * K + k;
+    atomicAdd(dst, v);
+  }
+}
+
+// Weight gradient, dy side: DY[b][t][k] = (A dy_t A^T)[b] for the 4x4 output tile dy_t
+// (A = (A^T)^T, 6x4). Same thread layout as wino_in_kernel.
+PSX_DEV void wino_a4(const float (&y)[4], float (&r)[6]) {
+  const float e = y[0] + y[2], o = y[1] + y[3], e4 = y[0] + 4.f * y[2], o2 = 2.f * y[1] + 8.f * y[3];
+  r[0] = y[0];
+  r[1] = e + o;
+  r[2] = e - o;
+  r[3] = e4 + o2;
+  r[4] = e4 - o2;
+  r[5] = y[3];
+}
+
+__global__ __launch_bounds__(256) void wino_dy_kernel(const float* __restrict__ dy, float* __restrict__ D, int T, int H,
+                                                      int W, int K) {
+  const int k = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int tw = W >> 2, tpi = (H >> 2) * tw;
+  const size_t bs = (size_t)T * K;
+  for (int t = blockIdx.y * 4 + (threadIdx.x >> 6); t < T; t += 4 * gridDim.y) {
+    const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
+    const float* src = dy + (((size_t)n * H + 4 * ti) * W + 4 * tj) * K + k;
+    float e[6][4];  // e = A dy (columns)
+    {
+      float y[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[i][j] = src[((size_t)i * W + j) * K];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float col[4] = {y[0][j], y[1][j], y[2][j], y[3][j]}, r6[6];
+        wino_a4(col, r6);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) e[r][j] = r6[r];
+      }
+    }
+    float* dt = D + (size_t)t * K + k;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      float r6[6];
+      wino_a4(e[r], r6);
+#pragma unroll
+      for (int s = 0; s < 6; ++s) dt[(r * 6 + s) * bs] = r6[s];
+    }
+  }
+}
+
+// dW[k][c][3][3] = scale * G^T M G, M[b] = sum of the q partial slabs part[b * q + j][k][c]
+// (the batched TN GEMM's split of each batch over tile ranges). One thread per (k, c), c fastest;
+// OutT = uint16_t: the fp16 wire (reference codec), float: fp32 gradients. OIHW like
+// wgrad_reduce's output.
+PSX_DEV void wino_gt6(const float (&m)[6], float (&o)[3]) {
+  const float a = m[1] + m[2], b = m[1] - m[2], c = m[3] + m[4], d = m[3] - m[4];
+  o[0] = 0.25f * m[0] - a * (1.f / 6.f) + c * (1.f / 24.f);
+  o[1] = -b * (1.f / 6.f) + d * (1.f / 12.f);
+  o[2] = -a * (1.f / 6.f) + c * (1.f / 6.f) + m[5];
+}
+
+template <typename OutT>
+__global__ __launch_bounds__(256) void wino_wout_kernel(const float* __restrict__ part, OutT* __restrict__ out, int K,
+                                                        int C, int q, float scale) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)K * C) return;
+  const size_t slab = (size_t)K * C;
+  float m[6][6];
+#pragma unroll
+  for (int b = 0; b < 36; ++b) {
+    const float* p = part + (size_t)b * q * slab + i;
+    float v = p[0];
+    for (int j = 1; j < q; ++j) v += p[j * slab];
+    m[b / 6][b % 6] = v;
+  }
+  float e[3][6];  // e = G^T m (columns)
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    float col[6] = {m[0][s], m[1][s], m[2][s], m[3][s], m[4][s], m[5][s]}, o[3];
+    wino_gt6(col, o);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) e[r][s] = o[r];
+  }
+  OutT* dst = out + i * 9;  // i = k * C + c
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    float o[3];
+    wino_gt6(e[r], o);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const float v = o[s] * scale;
+      if constexpr (sizeof(OutT) == 2)
+        dst[r * 3 + s] = __builtin_bit_cast(uint16_t, (_Float16)v);
+      else
+        dst[r * 3 + s] = v;
+    }
+  }
+}
+
+int wino_tile_grid(int T) {
+  int gy = (T + 3) / 4;
+  return gy > 256 ? 256 : gy;
+}
+
+}  // namespace psx
+
+using namespace psx;
+
+extern "C" {
+
+// Floats of one Winograd conv's transformed operands: V = T*36*C (input tiles, kept per layer for
+// the weight gradient) and P = 36*T*K (GEMM output / dy tiles).
+long psx_wino_v_floats(int N, int H, int W, int C) { return (long)N * (H / 4) * (W / 4) * 36 * C; }
+
+long psx_wino_workspace(int N, int H, int W, int C, int K) {
+  return psx_wino_v_floats(N, H, W, C) + psx_wino_v_floats(N, H, W, K);
+}
+
+// 1 when psx_wino_conv handles this layer: 3x3 / stride 1 / pad 1, H, W multiples of 4,
+// channels powers of two >= 64 (transform blocks, the GEMM's per-batch channel decode).
+int psx_wino_ok(int H, int W, int C, int K) {
+  return H % 4 == 0 && W % 4 == 0 && C >= 64 && K >= 64 && !(C & (C - 1)) && !(K & (K - 1));
+}
+
+// fwd (flip = 0): U[K][36][C] from w [K][C][3][3]; dgrad (flip = 1): U[C][36][K] of rot180(w)^T.
+int psx_wino_weights(const float* w, float* U, int K, int C, int flip, hipStream_t st) {
+  const long n = (long)K * C;
+  hipLaunchKernelGGL(wino_w_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, w, U, K, C, flip);
+  return (int)hipGetLastError();
+}
+
+// y[N][H][W][K] = conv3x3(x[N][H][W][C]) (+ res) with the pre-transformed weights U [K][36][C];
+// stats (nullable): BN partial sums into slot rows [PSX_STAT_SLOTS][2][K] (pre-zeroed).
+// V: psx_wino_v_floats(C) (the transformed input, left there for psx_wino_wgrad), P: 36*T*K
+// floats. cfg: GEMM tile (psx_bgemm_f32).
+int psx_wino_conv(const float* x, const float* U, float* y, const float* res, float* stats, float* V, float* P,
+                  const void* zero, int N, int H, int W, int C, int K, int cfg, hipStream_t st) {
+  if (!psx_wino_ok(H, W, C, K)) return -2;
+  const int T = N * (H / 4) * (W / 4);
+  const int gy = wino_tile_grid(T);
+  hipLaunchKernelGGL(wino_in_kernel, dim3(C / 64, gy), dim3(256), 0, st, x, V, T, H, W, C);
+  int e = psx_bgemm_f32(V, U, P, zero, T, K, C, 36, cfg, st);
+  if (e) return e;
+  hipLaunchKernelGGL(wino_out_kernel, dim3(K / 64, gy), dim3(256), 0, st, P, y, res, stats, T, H, W, K);
+  return (int)hipGetLastError();
+}
+
+// Weight-gradient GEMM tile (BR = BC): 64 (3 workgroups per CU) unless PSX_WINO_WBR=128.
+static int wino_wtile(int C, int K) {
+  if (const char* e = getenv("PSX_WINO_WBR"); e && atoi(e) == 128 && C % 128 == 0 && K % 128 == 0) return 128;
+  return 64;
+}
+
+// Tile-range splits q of the weight-gradient GEMM: 36 * q * (C/BR) * (K/BC) workgroups, each
+// over T / q tiles (a multiple of 32): the smallest q reaching 512 workgroups while a split keeps
+// >= 256 tiles. 0 = not applicable.
+int psx_wino_wgrad_q(int N, int H, int W, int C, int K) {
+  const int T = N * (H / 4) * (W / 4);
+  if (!psx_wino_ok(H, W, C, K) || T % 32) return 0;
+  const int bt = wino_wtile(C, K);
+  int q = 1;
+  if (const char* e = getenv("PSX_WINO_WQ"); e && atoi(e) > 0) q = atoi(e);
+  else
+    while (36L * q * (C / bt) * (K / bt) < 512 && T % (32 * 2 * q) == 0 && T / (2 * q) >= 256) q *= 2;
+  return T % (32 * q) ? 0 : q;
+}
+
+// Weight gradient of psx_wino_conv: V = that call's transformed input, dy [N][H][W][K]; D: 36*T*K
+// floats of scratch, part: 36*q*K*C floats (q = psx_wino_wgrad_q). out: OIHW gradient, fp16
+// (out_fp16, the wire) or fp32, times scale.
+int psx_wino_wgrad(const float* V, const float* dy, float* D, float* part, void* out, int out_fp16, float scale,
+                   const void* zero, int N, int H, int W, int C, int K, hipStream_t st) {
+  const int q = psx_wino_wgrad_q(N, H, W, C, K);
+  if (q < 1) return -2;
+  const int T = N * (H / 4) * (W / 4);
+  hipLaunchKernelGGL(wino_dy_kernel, dim3(K / 64, wino_tile_grid(T)), dim3(256), 0, st, dy, D, T, H, W, K);
+  const int bt = wino_wtile(C, K);
+  int e = psx_bgemm_tn_f32(V, D, part, zero, T, C, K, 36, q, bt, bt, st);
+  if (e) return e;
+  const long n = (long)K * C;
+  if (out_fp16)
+    hipLaunchKernelGGL((wino_wout_kernel<uint16_t>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part,
+                       (uint16_t*)out, K, C, q, scale);
+  else
+    hipLaunchKernelGGL((wino_wout_kernel<float>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part,
+                       (float*)out, K, C, q, scale);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

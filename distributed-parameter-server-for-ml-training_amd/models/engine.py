@@ -364,6 +364,7 @@ class HipResNetEngine:
             self.det_buf = torch.zeros(64 + need, dtype=torch.float32, device=self.dev)
         self.wpart = self._f32(max(1, max_wg))
         self.wpart_w = self._f32(max(1, self._plan_wpart(max_wp)))
+        self._plan_wino()
         # head
         fh, fw = self.final.shape[1], self.final.shape[2]
         self.head_hw = fh * fw
@@ -374,6 +375,54 @@ class HipResNetEngine:
         self.dfinal = torch.empty_like(self.final)
         # gradient wire buffer (trainable-parameter prefix of the arena)
         self.grads = torch.zeros(self.layout.param_numel, dtype=self.grad_dtype, device=self.dev)
+
+    def _plan_wino(self):
+        """fp32 Winograd F(4x4,3x3) (csrc/kernels/wino.hip) for the 3x3 / stride-1 layers on small
+        images (H, W <= PSX_WINO_MAXHW, default 16: ResNet-18 CIFAR stages 2-4): forward, data
+        gradient and (PSX_WINO_WGRAD=1, default) weight gradient. Per layer: the transformed
+        forward weights U [cout][36][cin] and data-gradient weights U' [cin][36][cout] (rebuilt by
+        unpack() every step) and the transformed input V [36][T][cin] the forward leaves for the
+        weight gradient. Not in deterministic mode (its BN sums are slot atomics) and not for
+        bf16. PSX_WINO=0: direct kernels everywhere."""
+        self.wino_layers = {}
+        self.wino_wgrad = set()
+        if not self.f32 or self.deterministic or os.environ.get("PSX_WINO", "1") == "0":
+            return
+        maxhw = int(os.environ.get("PSX_WINO_MAXHW", "16"))
+        wg = os.environ.get("PSX_WINO_WGRAD", "1") == "1"
+        B = self.B
+        s_main = s_d = s_part = 0
+        for cs in all_convs(self.spec):
+            if (cs.k != 3 or cs.stride != 1 or cs.pad != 1 or cs.cp != cs.cin or cs.h > maxhw or cs.w > maxhw
+                    or not K.wino_ok(cs.h, cs.w, cs.cp, cs.cout)):
+                continue
+            uf = self._f32(36 * cs.cout * cs.cp)
+            ud = self._f32(36 * cs.cout * cs.cp) if cs.need_dgrad else None
+            v = self._f32(K.wino_v_floats(B, cs.h, cs.w, cs.cp))
+            self.wino_layers[cs.name] = (uf, ud, v)
+            vk, vc = K.wino_v_floats(B, cs.h, cs.w, cs.cout), K.wino_v_floats(B, cs.h, cs.w, cs.cp)
+            s_main = max(s_main, vk, vc)
+            q = K.wino_wgrad_q(B, cs.h, cs.w, cs.cp, cs.cout) if wg else 0
+            if q > 0:
+                self.wino_wgrad.add(cs.name)
+                s_d = max(s_d, vk)
+                s_part = max(s_part, 36 * q * cs.cout * cs.cp)
+        # main-stream scratch (forward GEMM output; data-gradient input tiles + GEMM output) and
+        # the weight-gradient side stream's own (dy tiles, GEMM partials)
+        self.wino_s1 = self._f32(max(1, s_main))
+        self.wino_s2 = self._f32(max(1, s_main))
+        self.wino_wd = self._f32(max(1, s_d))
+        self.wino_wpart = self._f32(max(1, s_part))
+
+    def _wino_unpack(self, arena):
+        for cs in all_convs(self.spec):
+            u = self.wino_layers.get(cs.name)
+            if u is None:
+                continue
+            w = self._aview(arena, f"{cs.name}.weight")
+            K.wino_weights(w, u[0], cs.cout, cs.cp)
+            if u[1] is not None:
+                K.wino_weights(w, u[1], cs.cout, cs.cp, flip=True)
 
     # ------------------------------------------------------------------ helpers
     def _gptr(self, name: str) -> int:
@@ -419,6 +468,14 @@ class HipResNetEngine:
         wf = self.wbuf[cs.wf_off:cs.wf_off + cs.cout * cs.kg]
         stats = self._red(bs, "fwd") if train else None
         fin = self._fin_fwd(bs, arena, npix) if (train and self.fuse_fin) else None
+        wl = self.wino_layers.get(cs.name)
+        if wl is not None:
+            K.wino_conv(x, wl[0], y, None, stats, wl[2], self.wino_s1, self.B, cs.h, cs.w, cs.cp, cs.cout)
+            if not train:
+                self._bn_eval(bs, arena)
+            elif not self._fold:  # no in-launch finalize on this path
+                self._bn_train(bs, arena, self.nslots, npix)
+            return
         if self.conv_impl == 2:
             K.conv_fwd2(x, wf, y, stats, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
                         cs.kg, fin=fin)
@@ -512,6 +569,10 @@ class HipResNetEngine:
                     self._wgrad_now(cs, x, dy)
 
     def _wgrad_now(self, cs: ConvSpec, x, dy):
+        if cs.name in self.wino_wgrad:  # straight into the wire: no split partials to reduce
+            K.wino_wgrad(self.wino_layers[cs.name][2], dy, self.wino_wd, self.wino_wpart,
+                         self.layout.grad_view(self.grads, f"{cs.name}.weight"), self.B, cs.h, cs.w, cs.cp, cs.cout)
+            return
         part = self.wpart_w[cs.wp_off:cs.wp_off + cs.wp]
         if self.conv_impl == 2:
             K.conv_wgrad2(x, dy, part, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
@@ -534,6 +595,10 @@ class HipResNetEngine:
     def _dgrad(self, cs: ConvSpec, dy, dx, res=None, bn_next=None):
         """bn_next = (BNSpec, o, y, two|None): the BN whose backward consumes dx; with conv v2 its
         reduction (sum dz, sum dz*xhat) is produced by the dgrad epilogue (PSX_FUSE_BNBWD)."""
+        wl = self.wino_layers.get(cs.name)
+        if wl is not None:  # no fused BN-backward sums here: that BN runs its own reduction pass
+            K.wino_conv(dy, wl[1], dx, res, None, self.wino_s1, self.wino_s2, self.B, cs.h, cs.w, cs.cout, cs.cp)
+            return
         wd = self.wbuf[cs.wd_off:cs.wd_off + cs.cp * cs.kgd]
         if self.conv_impl == 2:
             bst = None
@@ -620,6 +685,8 @@ class HipResNetEngine:
             return
         src = self.wsrc if self.wsrc is not None else arena
         K.param_unpack_tiles(src, self.descs, self.ndesc, self.ntiles, self.wbuf, scatter=self.small_scatter)
+        if self.wino_layers:
+            self._wino_unpack(arena)
 
     small_scatter = None
     _zeroed = False       # red zeroed by this step's augment launch (consumed by forward)

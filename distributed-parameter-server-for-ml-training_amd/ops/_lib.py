@@ -50,6 +50,15 @@ _KERNEL_SIGS = {
     "psx_conv_wgrad2": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
     "psx_conv_fwd2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp]),
     "psx_conv_dgrad2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp]),
+    "psx_bgemm_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
+    "psx_wino_workspace": (i64, [i32, i32, i32, i32, i32]),
+    "psx_wino_ok": (i32, [i32, i32, i32, i32]),
+    "psx_wino_weights": (i32, [vp, vp, i32, i32, i32, vp]),
+    "psx_wino_conv": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
+    "psx_wino_v_floats": (i64, [i32, i32, i32, i32]),
+    "psx_wino_wgrad_q": (i32, [i32, i32, i32, i32, i32]),
+    "psx_wino_wgrad": (i32, [vp, vp, vp, vp, vp, i32, f32, vp, i32, i32, i32, i32, i32, vp]),
+    "psx_bgemm_tn_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
     "psx_bn_finalize": (i32, [vp, i32, i32, f32, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp]),
     "psx_bn_eval_affine": (i32, [i32, vp, vp, vp, vp, f32, vp, vp, vp]),
     "psx_bn_apply": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),

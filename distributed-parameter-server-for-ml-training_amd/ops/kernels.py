@@ -161,6 +161,77 @@ def conv_dgrad2(dy, wd, dx, res, ws, nb, h, w, ic_fwd, oc_fwd, k, stride, pad, k
                                     C.byref(bst) if bst is not None else None, is_f32(dy), stream_ptr()), "conv_dgrad2")
 
 
+def bgemm_f32(a, b, p, m, n, kd, nb, cfg=0):
+    """nb batched fp32 GEMMs p[i] = a[i] @ b[:, i, :].T (a [nb][m][kd], b [n][nb][kd], p [nb][m][n];
+    kd a power of two >= 32) on the conv_v2 mainloop (csrc/kernels/conv_v2.hip psx_bgemm_f32)."""
+    assert a.dtype == b.dtype == p.dtype == torch.float32
+    assert a.numel() >= m * nb * kd and b.numel() >= n * nb * kd and p.numel() >= nb * m * n
+    check(kernels().psx_bgemm_f32(ptr(a), ptr(b), ptr(p), ptr(zero_page(a.device)), m, n, kd, nb, cfg, stream_ptr()),
+          "bgemm_f32")
+
+
+def bgemm_tn_f32(x, d, part, t, c, k, nb, q=1, br=64, bc=64):
+    """Batched TN GEMMs part[i * q + j] = d[i, range j].T @ x[i, range j] (x [nb][t][c],
+    d [nb][t][k], part [nb*q][k][c]) on the fp32 weight-gradient mainloop (wgrad_v2.hip)."""
+    assert x.dtype == d.dtype == part.dtype == torch.float32
+    assert x.numel() >= nb * t * c and d.numel() >= nb * t * k and part.numel() >= nb * q * k * c
+    check(kernels().psx_bgemm_tn_f32(ptr(x), ptr(d), ptr(part), ptr(zero_page(x.device)), t, c, k, nb, q, br, bc,
+                                     stream_ptr()), "bgemm_tn_f32")
+
+
+def wino_ok(h, w, c, k) -> bool:
+    return bool(kernels().psx_wino_ok(h, w, c, k))
+
+
+def wino_v_floats(nb, h, w, c) -> int:
+    """Floats of a layer's transformed operand [36][T][c] (T = nb * h/4 * w/4 tiles)."""
+    return int(kernels().psx_wino_v_floats(nb, h, w, c))
+
+
+def wino_workspace_floats(nb, h, w, c, k) -> int:
+    return int(kernels().psx_wino_workspace(nb, h, w, c, k))
+
+
+def wino_wgrad_q(nb, h, w, c, k) -> int:
+    """Tile-range splits of the Winograd weight-gradient GEMM (0: not applicable)."""
+    return int(kernels().psx_wino_wgrad_q(nb, h, w, c, k))
+
+
+WINO_CFG = int(os.environ.get("PSX_WINO_CFG", "0"))
+
+
+def wino_weights(w_oihw, u, k, c, flip=False):
+    """Winograd F(4x4,3x3) weight transform (csrc/kernels/wino.hip): forward U[k][36][c] from the
+    fp32 OIHW weights, or (flip) the data-gradient operand U[c][36][k] of rot180(w)^T."""
+    assert w_oihw.dtype == torch.float32 and w_oihw.numel() == k * c * 9 and u.numel() >= 36 * k * c
+    check(kernels().psx_wino_weights(ptr(w_oihw), ptr(u), k, c, int(bool(flip)), stream_ptr()), "wino_weights")
+
+
+def wino_conv(x, u, y, res, stats, v, p, nb, h, w, c, k, cfg=None):
+    """fp32 3x3/s1/p1 conv y = conv(x) (+ res) via Winograd F(4x4,3x3) with pre-transformed
+    weights u (wino_weights); stats: BN slot sums of y (pre-zeroed) or None. v (>= wino_v_floats
+    of c) receives the transformed input (kept for wino_wgrad), p (>= wino_v_floats of k) is
+    scratch."""
+    assert x.dtype == torch.float32 and y.dtype == torch.float32
+    assert x.numel() == nb * h * w * c and y.numel() == nb * h * w * k and u.numel() >= 36 * k * c
+    assert v.numel() >= wino_v_floats(nb, h, w, c) and p.numel() >= wino_v_floats(nb, h, w, k)
+    assert res is None or res.numel() == y.numel()
+    check(kernels().psx_wino_conv(ptr(x), ptr(u), ptr(y), ptr(res), ptr(stats), ptr(v), ptr(p), ptr(zero_page(x.device)),
+                                  nb, h, w, c, k, WINO_CFG if cfg is None else cfg, stream_ptr()), "wino_conv")
+
+
+def wino_wgrad(v, dy, d, part, out, nb, h, w, c, k, scale=1.0):
+    """Weight gradient of a wino_conv layer from its transformed input v and dy [nb][h][w][k]:
+    out (OIHW, fp16 wire or fp32) = scale * dW. d: >= wino_v_floats(k) scratch, part:
+    36 * q * k * c floats (q = wino_wgrad_q)."""
+    q = wino_wgrad_q(nb, h, w, c, k)
+    assert q > 0 and dy.dtype == torch.float32 and dy.numel() == nb * h * w * k
+    assert d.numel() >= wino_v_floats(nb, h, w, k) and part.numel() >= 36 * q * k * c
+    assert out.dtype in (torch.float16, torch.float32) and out.numel() >= k * c * 9
+    check(kernels().psx_wino_wgrad(ptr(v), ptr(dy), ptr(d), ptr(part), ptr(out), int(out.dtype == torch.float16),
+                                   float(scale), ptr(zero_page(dy.device)), nb, h, w, c, k, stream_ptr()), "wino_wgrad")
+
+
 def conv_wgrad2_splits(nb, h, w, ic, oc, k, stride, pad, kg, f32=False) -> int:
     n = kernels().psx_conv_wgrad2(None, None, None, None, nb, h, w, ic, oc, k, k, stride, pad, kg, int(bool(f32)), None)
     if n <= 0:

@@ -145,7 +145,9 @@ class SyncCollectiveChannel(WatchedRounds):
         if self.server is not None:
             for w in self.members:
                 self.server.core.on_fetch(w)
-            if self.codec is None:
+            if self.codec is None or self.codec.kind == "fp32":
+                # the fp32 payload IS the arena: broadcast it in place (no wire copy; the next
+                # apply is stream-ordered after this round's fetch)
                 self.t.broadcast_from_server(self.server.arena)
                 nbytes = self.server.arena.numel() * 4
             else:
@@ -156,8 +158,8 @@ class SyncCollectiveChannel(WatchedRounds):
             if local_arena is not None and local_arena.data_ptr() != self.server.arena.data_ptr():
                 local_arena.copy_(self.server.arena)
             return self.server.core.global_step
-        if self.codec is None:
-            self.t.broadcast_from_server(local_arena)
+        if self.codec is None or self.codec.kind == "fp32":
+            self.t.broadcast_from_server(local_arena)  # received straight into the local arena
         else:
             for buf in self.codec.wire:
                 self.t.broadcast_from_server(buf)

@@ -91,8 +91,8 @@ def test_wino_dgrad(nb, h, c, k):
     assert _rel(dx, _nhwc(ref)) < TOL
 
 
-@pytest.mark.parametrize("nb,h,c,k,fp16", [(4, 8, 128, 256, False), (8, 4, 512, 512, False), (32, 16, 128, 128, True),
-                                           (2, 4, 64, 64, False)])
+@pytest.mark.parametrize("nb,h,c,k,fp16", [(32, 8, 128, 256, False), (32, 4, 512, 512, False), (32, 16, 128, 128, True),
+                                           (64, 4, 64, 64, False)])
 def test_wino_wgrad(nb, h, c, k, fp16):
     """dW of y = conv3x3(x) from the forward's transformed input V and dy: F(3x3,4x4) by
     transposition, dg = G^T [sum_t (A dy_t A^T) . V_t] G, written as OIHW fp32 or the fp16 wire."""

@@ -243,47 +243,67 @@ PSX_DEV void wino_gt6(const float (&m)[6], float (&o)[3]) {
   o[2] = -a * (1.f / 6.f) + c * (1.f / 6.f) + m[5];
 }
 
-template <typename OutT>
+template <typename OutT, int Q>
 __global__ __launch_bounds__(256) void wino_wout_kernel(const float* __restrict__ part, OutT* __restrict__ out, int K,
                                                         int C, int q, float scale) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long)K * C) return;
+  __shared__ float stage[256 * 9];
+  const long i0 = (long)blockIdx.x * 256, n = (long)K * C;
+  const long i = i0 + threadIdx.x;
+  const int qq = Q > 0 ? Q : q;
   const size_t slab = (size_t)K * C;
-  float m[6][6];
+  float o9[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (i < n) {
+    float m[6][6];
 #pragma unroll
-  for (int b = 0; b < 36; ++b) {
-    const float* p = part + (size_t)b * q * slab + i;
-    float v = p[0];
-    for (int j = 1; j < q; ++j) v += p[j * slab];
-    m[b / 6][b % 6] = v;
-  }
-  float e[3][6];  // e = G^T m (columns)
+    for (int b = 0; b < 36; ++b) {
+      const float* p = part + (size_t)b * qq * slab + i;
+      float v = p[0];
+      if constexpr (Q > 0) {
 #pragma unroll
-  for (int s = 0; s < 6; ++s) {
-    float col[6] = {m[0][s], m[1][s], m[2][s], m[3][s], m[4][s], m[5][s]}, o[3];
-    wino_gt6(col, o);
-#pragma unroll
-    for (int r = 0; r < 3; ++r) e[r][s] = o[r];
-  }
-  OutT* dst = out + i * 9;  // i = k * C + c
-#pragma unroll
-  for (int r = 0; r < 3; ++r) {
-    float o[3];
-    wino_gt6(e[r], o);
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const float v = o[s] * scale;
-      if constexpr (sizeof(OutT) == 2)
-        dst[r * 3 + s] = __builtin_bit_cast(uint16_t, (_Float16)v);
-      else
-        dst[r * 3 + s] = v;
+        for (int j = 1; j < Q; ++j) v += p[j * slab];
+      } else {
+        for (int j = 1; j < qq; ++j) v += p[j * slab];
+      }
+      m[b / 6][b % 6] = v;
     }
+    float e[3][6];  // e = G^T m (columns)
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      float col[6] = {m[0][s], m[1][s], m[2][s], m[3][s], m[4][s], m[5][s]}, o[3];
+      wino_gt6(col, o);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) e[r][s] = o[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      float o[3];
+      wino_gt6(e[r], o);
+#pragma unroll
+      for (int s = 0; s < 3; ++s) o9[r * 3 + s] = o[s] * scale;
+    }
+  }
+  // the workgroup's 256 (k, c) pairs own one contiguous run of 256 * 9 outputs (i = k * C + c):
+  // staged in LDS, stored by consecutive threads (the direct 9-strided stores split every wave
+  // store into 18-byte pieces)
+#pragma unroll
+  for (int j = 0; j < 9; ++j) stage[threadIdx.x * 9 + j] = o9[j];
+  __syncthreads();
+  const long lim = (n - i0 < 256 ? n - i0 : 256) * 9;
+  OutT* dst = out + i0 * 9;
+  for (int j = threadIdx.x; j < lim; j += 256) {
+    const float v = stage[j];
+    if constexpr (sizeof(OutT) == 2)
+      dst[j] = __builtin_bit_cast(uint16_t, (_Float16)v);
+    else
+      dst[j] = v;
   }
 }
 
+// grid.y of the transform kernels: 4 tiles per workgroup, one per wave (a 256-row cap starved
+// the 4x4 / 8x8 layers: 256 workgroups of 1-2 tiles per thread, ~2x their byte time)
 int wino_tile_grid(int T) {
   int gy = (T + 3) / 4;
-  return gy > 256 ? 256 : gy;
+  return gy > 16384 ? 16384 : gy;
 }
 
 }  // namespace psx
@@ -336,8 +356,9 @@ static int wino_wtile(int C, int K) {
 }
 
 // Tile-range splits q of the weight-gradient GEMM: 36 * q * (C/BR) * (K/BC) workgroups, each
-// over T / q tiles (a multiple of 32): the smallest q reaching 512 workgroups while a split keeps
-// >= 256 tiles. 0 = not applicable.
+// over T / q tiles (a multiple of 32): the smallest q reaching 1024 workgroups while a split keeps
+// >= 256 tiles, at most 4. Same-box sweep (B=128, us, q = 1 / 2 / 4 / 8): 8x8x256 48 / 43 / - / 107,
+// 16x16x128 - / 62 / 52 / 106, 4x4x512 45 / 52 / - / -. 0 = not applicable.
 int psx_wino_wgrad_q(int N, int H, int W, int C, int K) {
   const int T = N * (H / 4) * (W / 4);
   if (!psx_wino_ok(H, W, C, K) || T % 32) return 0;
@@ -345,7 +366,7 @@ int psx_wino_wgrad_q(int N, int H, int W, int C, int K) {
   int q = 1;
   if (const char* e = getenv("PSX_WINO_WQ"); e && atoi(e) > 0) q = atoi(e);
   else
-    while (36L * q * (C / bt) * (K / bt) < 512 && T % (32 * 2 * q) == 0 && T / (2 * q) >= 256) q *= 2;
+    while (36L * q * (C / bt) * (K / bt) < 1024 && q < 4 && T % (32 * 2 * q) == 0 && T / (2 * q) >= 256) q *= 2;
   return T % (32 * q) ? 0 : q;
 }
 
@@ -362,12 +383,20 @@ int psx_wino_wgrad(const float* V, const float* dy, float* D, float* part, void*
   int e = psx_bgemm_tn_f32(V, D, part, zero, T, C, K, 36, q, bt, bt, st);
   if (e) return e;
   const long n = (long)K * C;
-  if (out_fp16)
-    hipLaunchKernelGGL((wino_wout_kernel<uint16_t>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part,
-                       (uint16_t*)out, K, C, q, scale);
-  else
-    hipLaunchKernelGGL((wino_wout_kernel<float>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part,
-                       (float*)out, K, C, q, scale);
+  const dim3 grid((unsigned)((n + 255) / 256));
+#define PSX_WOUT(OT, QV) hipLaunchKernelGGL((wino_wout_kernel<OT, QV>), grid, dim3(256), 0, st, part, (OT*)out, K, C, q, scale)
+  if (out_fp16) {
+    if (q == 1) PSX_WOUT(uint16_t, 1);
+    else if (q == 2) PSX_WOUT(uint16_t, 2);
+    else if (q == 4) PSX_WOUT(uint16_t, 4);
+    else PSX_WOUT(uint16_t, 0);
+  } else {
+    if (q == 1) PSX_WOUT(float, 1);
+    else if (q == 2) PSX_WOUT(float, 2);
+    else if (q == 4) PSX_WOUT(float, 4);
+    else PSX_WOUT(float, 0);
+  }
+#undef PSX_WOUT
   return (int)hipGetLastError();
 }
 

@@ -377,38 +377,42 @@ class HipResNetEngine:
         self.grads = torch.zeros(self.layout.param_numel, dtype=self.grad_dtype, device=self.dev)
 
     def _plan_wino(self):
-        """fp32 Winograd F(4x4,3x3) (csrc/kernels/wino.hip) for the 3x3 / stride-1 layers on small
-        images (H, W <= PSX_WINO_MAXHW, default 16: ResNet-18 CIFAR stages 2-4): forward, data
-        gradient and (PSX_WINO_WGRAD=1, default) weight gradient. Per layer: the transformed
-        forward weights U [cout][36][cin] and data-gradient weights U' [cin][36][cout] (rebuilt by
-        unpack() every step) and the transformed input V [36][T][cin] the forward leaves for the
-        weight gradient. Not in deterministic mode (its BN sums are slot atomics) and not for
+        """fp32 Winograd F(4x4,3x3) (csrc/kernels/wino.hip) for the 3x3 / stride-1 layers: forward
+        and data gradient on images up to PSX_WINO_MAXHW (default 32: every 3x3 stride-1 layer of
+        ResNet-18 CIFAR), weight gradient (PSX_WINO_WGRAD=1, default) up to PSX_WINO_WGRAD_MAXHW
+        (default 16: on 32x32 the direct tap-reuse kernel is faster, 101 vs 129 us). Same-box
+        per-layer A/B in profiles/r2s4_wino_*.jsonl. Per layer: the transformed forward weights
+        U [cout][36][cin] and data-gradient weights U' [cin][36][cout] (rebuilt by unpack() every
+        step) and, where the weight gradient is Winograd, the transformed input V [36][T][cin] the
+        forward leaves for it. Not in deterministic mode (its BN sums are slot atomics) and not for
         bf16. PSX_WINO=0: direct kernels everywhere."""
         self.wino_layers = {}
         self.wino_wgrad = set()
         if not self.f32 or self.deterministic or os.environ.get("PSX_WINO", "1") == "0":
             return
-        maxhw = int(os.environ.get("PSX_WINO_MAXHW", "16"))
+        maxhw = int(os.environ.get("PSX_WINO_MAXHW", "32"))
         wg = os.environ.get("PSX_WINO_WGRAD", "1") == "1"
+        wg_maxhw = int(os.environ.get("PSX_WINO_WGRAD_MAXHW", "32"))
         B = self.B
         s_main = s_d = s_part = 0
         for cs in all_convs(self.spec):
             if (cs.k != 3 or cs.stride != 1 or cs.pad != 1 or cs.cp != cs.cin or cs.h > maxhw or cs.w > maxhw
                     or not K.wino_ok(cs.h, cs.w, cs.cp, cs.cout)):
                 continue
-            uf = self._f32(36 * cs.cout * cs.cp)
-            ud = self._f32(36 * cs.cout * cs.cp) if cs.need_dgrad else None
-            v = self._f32(K.wino_v_floats(B, cs.h, cs.w, cs.cp))
-            self.wino_layers[cs.name] = (uf, ud, v)
             vk, vc = K.wino_v_floats(B, cs.h, cs.w, cs.cout), K.wino_v_floats(B, cs.h, cs.w, cs.cp)
             s_main = max(s_main, vk, vc)
-            q = K.wino_wgrad_q(B, cs.h, cs.w, cs.cp, cs.cout) if wg else 0
+            q = K.wino_wgrad_q(B, cs.h, cs.w, cs.cp, cs.cout) if wg and max(cs.h, cs.w) <= wg_maxhw else 0
+            uf = self._f32(36 * cs.cout * cs.cp)
+            ud = self._f32(36 * cs.cout * cs.cp) if cs.need_dgrad else None
+            v = self._f32(vc) if q > 0 else None  # None: the forward's V goes to scratch
+            self.wino_layers[cs.name] = (uf, ud, v)
             if q > 0:
                 self.wino_wgrad.add(cs.name)
                 s_d = max(s_d, vk)
                 s_part = max(s_part, 36 * q * cs.cout * cs.cp)
-        # main-stream scratch (forward GEMM output; data-gradient input tiles + GEMM output) and
-        # the weight-gradient side stream's own (dy tiles, GEMM partials)
+        # main-stream scratch (forward V of layers without a Winograd weight gradient / GEMM output;
+        # data-gradient input tiles + GEMM output) and the weight-gradient side stream's own (dy
+        # tiles, GEMM partials)
         self.wino_s1 = self._f32(max(1, s_main))
         self.wino_s2 = self._f32(max(1, s_main))
         self.wino_wd = self._f32(max(1, s_d))
@@ -470,7 +474,8 @@ class HipResNetEngine:
         fin = self._fin_fwd(bs, arena, npix) if (train and self.fuse_fin) else None
         wl = self.wino_layers.get(cs.name)
         if wl is not None:
-            K.wino_conv(x, wl[0], y, None, stats, wl[2], self.wino_s1, self.B, cs.h, cs.w, cs.cp, cs.cout)
+            v = wl[2] if wl[2] is not None else self.wino_s2
+            K.wino_conv(x, wl[0], y, None, stats, v, self.wino_s1, self.B, cs.h, cs.w, cs.cp, cs.cout)
             if not train:
                 self._bn_eval(bs, arena)
             elif not self._fold:  # no in-launch finalize on this path

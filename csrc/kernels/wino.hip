@@ -133,17 +133,88 @@ __global__ __launch_bounds__(64) void wino_w_kernel(const float* __restrict__ w,
   }
 }
 
-// y = A^T P A (+ res); BN partial sums (sum y, sum y^2) of the stored values into slot rows
-// stats[slot][2][K]. Block = 64 channels x 4 tiles; grid.y strides over the tiles.
+// All layers' weight transforms of a step in one launch: descriptor j covers pairs
+// [p0_j, p0_{j+1}) of layer j's (row, col) grid (the per-layer launches were ~6 us each, mostly
+// launch and tail latency: 26 per ResNet-18 step).
+struct WinoWDesc {
+  const float* w;
+  float* U;
+  int K, C, flip, pad_;
+  long p0;
+};
+constexpr int kWinoWMax = 40;
+struct WinoWBatch {
+  WinoWDesc d[kWinoWMax];
+  int n;
+  long total;
+};
+
+__global__ __launch_bounds__(64) void wino_w_multi_kernel(WinoWBatch bt) {
+  const long i = (long)blockIdx.x * 64 + threadIdx.x;
+  if (i >= bt.total) return;
+  int j = 0;
+  while (j + 1 < bt.n && i >= bt.d[j + 1].p0) ++j;
+  const WinoWDesc& d = bt.d[j];
+  const int flip = d.flip, K = d.K, C = d.C;
+  const int rows = flip ? C : K, cols = flip ? K : C;
+  const long li = i - d.p0;
+  const int row = (int)(li / cols), col = (int)(li - (long)row * cols);
+  (void)rows;
+  const int k = flip ? col : row, c = flip ? row : col;
+  const float* g = d.w + ((size_t)k * C + c) * 9;
+  float gg[3][3];
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) gg[p][q] = flip ? g[(2 - p) * 3 + (2 - q)] : g[p * 3 + q];
+  float* dst = d.U + (size_t)row * 36 * cols + col;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    float gr[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) gr[q] = kWinoG[r][0] * gg[0][q] + kWinoG[r][1] * gg[1][q] + kWinoG[r][2] * gg[2][q];
+#pragma unroll
+    for (int s = 0; s < 6; ++s)
+      dst[(size_t)(r * 6 + s) * cols] = kWinoG[s][0] * gr[0] + kWinoG[s][1] * gr[1] + kWinoG[s][2] * gr[2];
+  }
+}
+
+// Fused BN-backward sums over a data-gradient output (the layout of conv_v2.hip BwdStatsDesc):
+// dz = g * [o > 0], slot rows [PSX_STAT_SLOTS][bns][K] of sum dz, sum dz * xhat1 (, * xhat2);
+// mask_store: store dz instead of g.
+struct WinoBwdStats {
+  float* part;
+  const float* o;
+  const float* y1;
+  const float* y2;
+  const float* saved1;  // [2][K] mean, invstd
+  const float* saved2;
+  int mask_store;
+};
+
+// y = A^T P A (+ res); forward: BN partial sums (sum y, sum y^2) of the stored values into slot
+// rows stats[slot][2][K]; data gradient (bs.part): the BN-backward sums of the consumer BN
+// instead (what the direct dgrad epilogue fuses). Block = 64 channels x 4 tiles, one tile per
+// wave.
 __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__ P, float* __restrict__ y,
                                                        const float* __restrict__ res, float* __restrict__ stats, int T,
-                                                       int H, int W, int K) {
-  __shared__ float red[2][4][64];
+                                                       int H, int W, int K, WinoBwdStats bs) {
+  __shared__ float red[3][4][64];
   const int kl = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + kl;
   const int tw = W >> 2, tpi = (H >> 2) * tw;
   const size_t bstride = (size_t)T * K;
-  float s1 = 0.f, s2 = 0.f;
+  const bool bwd = bs.part != nullptr, two = bs.y2 != nullptr;
+  float m1 = 0.f, i1 = 0.f, m2 = 0.f, i2 = 0.f;
+  if (bwd) {
+    m1 = bs.saved1[k];
+    i1 = bs.saved1[K + k];
+    if (two) {
+      m2 = bs.saved2[k];
+      i2 = bs.saved2[K + k];
+    }
+  }
+  float s1 = 0.f, s2 = 0.f, s3 = 0.f;
   for (int t = blockIdx.y * 4 + ty; t < T; t += 4 * gridDim.y) {
     const float* pt = P + (size_t)t * K + k;
     float m[6][6];
@@ -168,21 +239,31 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
         const size_t off = base + ((size_t)i * W + j) * K;
         float v = o[j];
         if (res) v += res[off];
-        y[off] = v;
-        s1 += v;
-        s2 += v * v;
+        if (bwd) {
+          const float dz = bs.o[off] > 0.f ? v : 0.f;
+          s1 += dz;
+          s2 += dz * (bs.y1[off] - m1) * i1;
+          if (two) s3 += dz * (bs.y2[off] - m2) * i2;
+          y[off] = bs.mask_store ? dz : v;
+        } else {
+          y[off] = v;
+          s1 += v;
+          s2 += v * v;
+        }
       }
     }
   }
-  if (!stats) return;
+  float* dst = bwd ? bs.part : stats;
+  if (!dst) return;
+  const int nst = bwd ? (two ? 3 : 2) : 2;
   red[0][ty][kl] = s1;
   red[1][ty][kl] = s2;
+  red[2][ty][kl] = s3;
   __syncthreads();
-  if (threadIdx.x < 128) {
+  if (threadIdx.x < 64 * nst) {
     const int which = threadIdx.x >> 6;
     const float v = red[which][0][kl] + red[which][1][kl] + red[which][2][kl] + red[which][3][kl];
-    float* dst = stats + (size_t)(blockIdx.y & (PSX_STAT_SLOTS - 1)) * 2 * K + (size_t)which * K + k;
-    atomicAdd(dst, v);
+    atomicAdd(dst + (size_t)(blockIdx.y & (PSX_STAT_SLOTS - 1)) * nst * K + (size_t)which * K + k, v);
   }
 }
 
@@ -333,19 +414,41 @@ int psx_wino_weights(const float* w, float* U, int K, int C, int flip, hipStream
   return (int)hipGetLastError();
 }
 
+// n (<= 40) weight transforms in one launch: w[j] OIHW [K[j]][C[j]][3][3] -> U[j] (flip[j] as in
+// psx_wino_weights).
+int psx_wino_weights_multi(const float* const* w, float* const* U, const int* K, const int* C, const int* flip, int n,
+                           hipStream_t st) {
+  if (n < 1 || n > kWinoWMax) return -2;
+  WinoWBatch b{};
+  long p = 0;
+  for (int j = 0; j < n; ++j) {
+    b.d[j] = WinoWDesc{w[j], U[j], K[j], C[j], flip[j], 0, p};
+    p += (long)K[j] * C[j];
+  }
+  b.n = n;
+  b.total = p;
+  hipLaunchKernelGGL(wino_w_multi_kernel, dim3((unsigned)((p + 63) / 64)), dim3(64), 0, st, b);
+  return (int)hipGetLastError();
+}
+
 // y[N][H][W][K] = conv3x3(x[N][H][W][C]) (+ res) with the pre-transformed weights U [K][36][C];
-// stats (nullable): BN partial sums into slot rows [PSX_STAT_SLOTS][2][K] (pre-zeroed).
+// stats (nullable): BN partial sums into slot rows [PSX_STAT_SLOTS][2][K] (pre-zeroed); bst
+// (nullable, data gradient): the consumer BN's backward sums instead (conv_v2 BwdStatsDesc).
 // V: psx_wino_v_floats(C) (the transformed input, left there for psx_wino_wgrad), P: 36*T*K
 // floats. cfg: GEMM tile (psx_bgemm_f32).
 int psx_wino_conv(const float* x, const float* U, float* y, const float* res, float* stats, float* V, float* P,
-                  const void* zero, int N, int H, int W, int C, int K, int cfg, hipStream_t st) {
+                  const void* zero, int N, int H, int W, int C, int K, int cfg, const WinoBwdStats* bst,
+                  hipStream_t st) {
   if (!psx_wino_ok(H, W, C, K)) return -2;
   const int T = N * (H / 4) * (W / 4);
   const int gy = wino_tile_grid(T);
   hipLaunchKernelGGL(wino_in_kernel, dim3(C / 64, gy), dim3(256), 0, st, x, V, T, H, W, C);
   int e = psx_bgemm_f32(V, U, P, zero, T, K, C, 36, cfg, st);
   if (e) return e;
-  hipLaunchKernelGGL(wino_out_kernel, dim3(K / 64, gy), dim3(256), 0, st, P, y, res, stats, T, H, W, K);
+  WinoBwdStats bs{};
+  if (bst) bs = *bst;
+  hipLaunchKernelGGL(wino_out_kernel, dim3(K / 64, gy), dim3(256), 0, st, P, y, res, bst ? nullptr : stats, T, H, W,
+                     K, bs);
   return (int)hipGetLastError();
 }
 

@@ -419,14 +419,21 @@ class HipResNetEngine:
         self.wino_wpart = self._f32(max(1, s_part))
 
     def _wino_unpack(self, arena):
-        for cs in all_convs(self.spec):
-            u = self.wino_layers.get(cs.name)
-            if u is None:
-                continue
-            w = self._aview(arena, f"{cs.name}.weight")
-            K.wino_weights(w, u[0], cs.cout, cs.cp)
-            if u[1] is not None:
-                K.wino_weights(w, u[1], cs.cout, cs.cp, flip=True)
+        """Every Winograd layer's forward and data-gradient weight transforms, one launch."""
+        key = arena.data_ptr()
+        if getattr(self, "_wino_wb_key", None) != key:
+            items = []
+            for cs in all_convs(self.spec):
+                u = self.wino_layers.get(cs.name)
+                if u is None:
+                    continue
+                w = self._aview(arena, f"{cs.name}.weight")
+                items.append((w, u[0], cs.cout, cs.cp, False))
+                if u[1] is not None:
+                    items.append((w, u[1], cs.cout, cs.cp, True))
+            self._wino_wb = K.WinoWeightBatch(items)
+            self._wino_wb_key = key
+        self._wino_wb()
 
     # ------------------------------------------------------------------ helpers
     def _gptr(self, name: str) -> int:
@@ -601,29 +608,31 @@ class HipResNetEngine:
         """bn_next = (BNSpec, o, y, two|None): the BN whose backward consumes dx; with conv v2 its
         reduction (sum dz, sum dz*xhat) is produced by the dgrad epilogue (PSX_FUSE_BNBWD)."""
         wl = self.wino_layers.get(cs.name)
-        if wl is not None:  # no fused BN-backward sums here: that BN runs its own reduction pass
-            K.wino_conv(dy, wl[1], dx, res, None, self.wino_s1, self.wino_s2, self.B, cs.h, cs.w, cs.cout, cs.cp)
+        if self.conv_impl != 2:
+            wd = self.wbuf[cs.wd_off:cs.wd_off + cs.cp * cs.kgd]
+            K.conv_dgrad(dy, wd, dx, res, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kgd)
+            return
+        bst = None
+        if bn_next is not None and self.fuse_bnbwd:
+            bs, o, y, two = bn_next
+            st = self.bn[bs.name]
+            ms = self.mask_store
+            if two is None:
+                bst = K.bwd_stats_desc(self._red(bs, "bwd"), o, y, st["saved"], mask_store=ms)
+            else:
+                bs2, y2 = two
+                bst = K.bwd_stats_desc(self._red(bs, "bwd"), o, y, st["saved"], y2, self.bn[bs2.name]["saved"],
+                                       mask_store=ms)
+            self._prereduced.add(bs.name)
+            if ms:
+                self._premasked.add(bs.name)
+        if wl is not None:  # Winograd: the output transform produces the same fused sums
+            K.wino_conv(dy, wl[1], dx, res, None, self.wino_s1, self.wino_s2, self.B, cs.h, cs.w, cs.cout, cs.cp,
+                        bst=bst)
             return
         wd = self.wbuf[cs.wd_off:cs.wd_off + cs.cp * cs.kgd]
-        if self.conv_impl == 2:
-            bst = None
-            if bn_next is not None and self.fuse_bnbwd:
-                bs, o, y, two = bn_next
-                st = self.bn[bs.name]
-                ms = self.mask_store
-                if two is None:
-                    bst = K.bwd_stats_desc(self._red(bs, "bwd"), o, y, st["saved"], mask_store=ms)
-                else:
-                    bs2, y2 = two
-                    bst = K.bwd_stats_desc(self._red(bs, "bwd"), o, y, st["saved"], y2, self.bn[bs2.name]["saved"],
-                                           mask_store=ms)
-                self._prereduced.add(bs.name)
-                if ms:
-                    self._premasked.add(bs.name)
-            K.conv_dgrad2(dy, wd, dx, res, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
-                          cs.kgd, bst=bst)
-        else:
-            K.conv_dgrad(dy, wd, dx, res, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kgd)
+        K.conv_dgrad2(dy, wd, dx, res, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
+                      cs.kgd, bst=bst)
 
     def _bn_bwd(self, bs: BNSpec, arena, g, o, y, dx, npix, two=None, dzout=None):
         """BN (+ReLU mask from o) backward; two = (bs2, y2, dx2) for a shared-dz second BN.

@@ -207,17 +207,41 @@ def wino_weights(w_oihw, u, k, c, flip=False):
     check(kernels().psx_wino_weights(ptr(w_oihw), ptr(u), k, c, int(bool(flip)), stream_ptr()), "wino_weights")
 
 
-def wino_conv(x, u, y, res, stats, v, p, nb, h, w, c, k, cfg=None):
+class WinoWeightBatch:
+    """Every Winograd weight transform of a step as ONE launch (wino.hip psx_wino_weights_multi):
+    items = [(w_oihw, u, k, c, flip)], pointers fixed at construction (<= 40 items)."""
+
+    def __init__(self, items):
+        n = len(items)
+        assert 1 <= n <= 40
+        for w, u, k, c, _ in items:
+            assert w.dtype == torch.float32 and w.numel() == k * c * 9 and u.numel() >= 36 * k * c
+        self.n = n
+        self.keep = [(w, u) for w, u, *_ in items]
+        self.w = (C.c_void_p * n)(*[ptr(w) for w, *_ in items])
+        self.u = (C.c_void_p * n)(*[ptr(u) for _, u, *_ in items])
+        self.k = (C.c_int * n)(*[int(it[2]) for it in items])
+        self.c = (C.c_int * n)(*[int(it[3]) for it in items])
+        self.flip = (C.c_int * n)(*[int(bool(it[4])) for it in items])
+
+    def __call__(self):
+        check(kernels().psx_wino_weights_multi(self.w, self.u, self.k, self.c, self.flip, self.n, stream_ptr()),
+              "wino_weights_multi")
+
+
+def wino_conv(x, u, y, res, stats, v, p, nb, h, w, c, k, cfg=None, bst: "BwdStatsDesc | None" = None):
     """fp32 3x3/s1/p1 conv y = conv(x) (+ res) via Winograd F(4x4,3x3) with pre-transformed
-    weights u (wino_weights); stats: BN slot sums of y (pre-zeroed) or None. v (>= wino_v_floats
-    of c) receives the transformed input (kept for wino_wgrad), p (>= wino_v_floats of k) is
-    scratch."""
+    weights u (wino_weights); stats: BN slot sums of y (pre-zeroed) or None; bst (data gradient,
+    bwd_stats_desc): the consumer BN's backward sums (and the masked store) instead. v (>=
+    wino_v_floats of c) receives the transformed input (kept for wino_wgrad), p (>= wino_v_floats
+    of k) is scratch."""
     assert x.dtype == torch.float32 and y.dtype == torch.float32
     assert x.numel() == nb * h * w * c and y.numel() == nb * h * w * k and u.numel() >= 36 * k * c
     assert v.numel() >= wino_v_floats(nb, h, w, c) and p.numel() >= wino_v_floats(nb, h, w, k)
     assert res is None or res.numel() == y.numel()
     check(kernels().psx_wino_conv(ptr(x), ptr(u), ptr(y), ptr(res), ptr(stats), ptr(v), ptr(p), ptr(zero_page(x.device)),
-                                  nb, h, w, c, k, WINO_CFG if cfg is None else cfg, stream_ptr()), "wino_conv")
+                                  nb, h, w, c, k, WINO_CFG if cfg is None else cfg,
+                                  C.byref(bst) if bst is not None else None, stream_ptr()), "wino_conv")
 
 
 def wino_wgrad(v, dy, d, part, out, nb, h, w, c, k, scale=1.0):

@@ -159,3 +159,57 @@ def test_engine_step_wino_vs_direct(monkeypatch):
     assert max(errs)[0] < 2e-2, max(errs)
     assert sorted(errs)[len(errs) // 2][0] < 1e-2, sorted(errs)
     assert torch.isfinite(g1[:n]).all()
+
+
+def test_wino_weights_multi_matches_single():
+    """All of a step's weight transforms in one launch == the per-layer transforms, bit for bit."""
+    torch.manual_seed(5)
+    shapes = [(64, 64), (128, 64), (256, 512)]
+    items, ref = [], []
+    for k, c in shapes:
+        w = torch.randn(k, c, 3, 3, device=DEV)
+        for flip in (False, True):
+            u = torch.full((36 * k * c,), float("nan"), device=DEV)
+            r = torch.empty(36 * k * c, device=DEV)
+            K.wino_weights(w, r, k, c, flip=flip)
+            items.append((w, u, k, c, flip))
+            ref.append(r)
+    K.WinoWeightBatch(items)()
+    torch.cuda.synchronize()
+    for (_, u, *_), r in zip(items, ref):
+        assert torch.equal(u, r)
+
+
+@pytest.mark.parametrize("two,mask_store,res", [(False, False, False), (True, True, True), (False, True, False)])
+def test_wino_dgrad_fused_bn_bwd_sums(two, mask_store, res):
+    """Data gradient with the consumer BN's backward sums fused into the output transform (what
+    the direct dgrad epilogue does): slot sums of dz = g*[o>0], dz*xhat1 (, dz*xhat2); the stored
+    output is dz with mask_store, else g."""
+    torch.manual_seed(11)
+    nb, h, c, k = 32, 8, 128, 256
+    w = torch.randn(k, c, 3, 3, device=DEV) * (2.0 / (9 * c)) ** 0.5
+    dy = torch.randn(nb, h, h, k, device=DEV)
+    r = torch.randn(nb, h, h, c, device=DEV) if res else None
+    o = torch.randn(nb, h, h, c, device=DEV)
+    y1, y2 = torch.randn(nb, h, h, c, device=DEV), torch.randn(nb, h, h, c, device=DEV)
+    saved1 = torch.stack([torch.randn(c, device=DEV), torch.rand(c, device=DEV) + 0.5])
+    saved2 = torch.stack([torch.randn(c, device=DEV), torch.rand(c, device=DEV) + 0.5])
+    part = torch.zeros(K.STAT_SLOTS, 3 if two else 2, c, device=DEV)
+    bst = K.bwd_stats_desc(part, o, y1, saved1, y2 if two else None, saved2 if two else None, mask_store=mask_store)
+    u = torch.empty(36 * k * c, device=DEV)
+    K.wino_weights(w, u, k, c, flip=True)
+    dx = torch.empty(nb, h, h, c, device=DEV)
+    v = torch.empty(K.wino_v_floats(nb, h, h, k), device=DEV)
+    p = torch.empty(K.wino_v_floats(nb, h, h, c), device=DEV)
+    K.wino_conv(dy, u, dx, r, None, v, p, nb, h, h, k, c, bst=bst)
+    torch.cuda.synchronize()
+    g = torch.nn.grad.conv2d_input((nb, c, h, h), w.double(), dy.double().permute(0, 3, 1, 2), padding=1)
+    g = g.permute(0, 2, 3, 1) + (r.double() if res else 0)
+    dz = torch.where(o.double() > 0, g, torch.zeros_like(g))
+    assert _rel(dx, dz if mask_store else g) < TOL
+    s = part.double().sum(0)
+    sums = [dz.sum((0, 1, 2)), (dz * (y1.double() - saved1[0].double()) * saved1[1].double()).sum((0, 1, 2))]
+    if two:
+        sums.append((dz * (y2.double() - saved2[0].double()) * saved2[1].double()).sum((0, 1, 2)))
+    for i, ref in enumerate(sums):
+        assert _rel(s[i], ref) < 1e-4, i

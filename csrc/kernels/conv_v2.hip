@@ -70,6 +70,29 @@ struct Conv2Args {
   // needs no ReLU-mask operand (one full activation read less per BN layer)
   int bmask;
   DetRed det;  // deterministic mode: the launch's row slab (bnfin.hpp)
+  int wH, wW;  // WOUT: the output image (Winograd tiles t = (n, ti, tj) of 4x4 pixels)
+};
+
+// Winograd F(4x4,3x3) output-transform coefficients: y[i][j] = sum_b kWinoAT2[b][4 i + j] P[b],
+// b = 6 r + s, kWinoAT2[b][4 i + j] = A^T[i][r] A^T[j][s] (wino.hip has the matrices)
+__constant__ float kWinoAT2[36][16] = {
+#define PSX_AT(i, r) ((r) == 0 ? ((i) == 0 ? 1.f : 0.f) : (r) == 5 ? ((i) == 3 ? 1.f : 0.f) : \
+                      (float)(((r) == 1 ? 1 : (r) == 2 ? ((i) & 1 ? -1 : 1) : (r) == 3 ? (1 << (i)) : (((i) & 1) ? -(1 << (i)) : (1 << (i))))))
+#define PSX_ROW(b) {PSX_AT(0, (b) / 6) * PSX_AT(0, (b) % 6), PSX_AT(0, (b) / 6) * PSX_AT(1, (b) % 6), \
+                     PSX_AT(0, (b) / 6) * PSX_AT(2, (b) % 6), PSX_AT(0, (b) / 6) * PSX_AT(3, (b) % 6), \
+                     PSX_AT(1, (b) / 6) * PSX_AT(0, (b) % 6), PSX_AT(1, (b) / 6) * PSX_AT(1, (b) % 6), \
+                     PSX_AT(1, (b) / 6) * PSX_AT(2, (b) % 6), PSX_AT(1, (b) / 6) * PSX_AT(3, (b) % 6), \
+                     PSX_AT(2, (b) / 6) * PSX_AT(0, (b) % 6), PSX_AT(2, (b) / 6) * PSX_AT(1, (b) % 6), \
+                     PSX_AT(2, (b) / 6) * PSX_AT(2, (b) % 6), PSX_AT(2, (b) / 6) * PSX_AT(3, (b) % 6), \
+                     PSX_AT(3, (b) / 6) * PSX_AT(0, (b) % 6), PSX_AT(3, (b) / 6) * PSX_AT(1, (b) % 6), \
+                     PSX_AT(3, (b) / 6) * PSX_AT(2, (b) % 6), PSX_AT(3, (b) / 6) * PSX_AT(3, (b) % 6)}
+    PSX_ROW(0),  PSX_ROW(1),  PSX_ROW(2),  PSX_ROW(3),  PSX_ROW(4),  PSX_ROW(5),  PSX_ROW(6),  PSX_ROW(7),
+    PSX_ROW(8),  PSX_ROW(9),  PSX_ROW(10), PSX_ROW(11), PSX_ROW(12), PSX_ROW(13), PSX_ROW(14), PSX_ROW(15),
+    PSX_ROW(16), PSX_ROW(17), PSX_ROW(18), PSX_ROW(19), PSX_ROW(20), PSX_ROW(21), PSX_ROW(22), PSX_ROW(23),
+    PSX_ROW(24), PSX_ROW(25), PSX_ROW(26), PSX_ROW(27), PSX_ROW(28), PSX_ROW(29), PSX_ROW(30), PSX_ROW(31),
+    PSX_ROW(32), PSX_ROW(33), PSX_ROW(34), PSX_ROW(35)
+#undef PSX_ROW
+#undef PSX_AT
 };
 
 PSX_DEV int kmaj2(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
@@ -119,7 +142,12 @@ PSX_DEV const T* gather_src(const Conv2Args& a, int nbase, int hb, int wb, bool 
 // T: activation / weight storage type (common.hpp kEPC/kKS): one k-step is a 128-byte row of
 // every operand = 64 bf16 or 32 fp32 channels; the staging below is written in 16-byte chunks
 // and bytes, so only the element strides (EPC per chunk, KS per k-step) depend on T.
-template <typename T, int BM, int BN, int MODE, bool HAS_RES, bool SPLIT, int WGM = 2, int TAPR = 0>
+// WOUT (fp32 Winograd, wino.hip): the GEMM over all 36 batches of a layer (R = 36 "taps", Kg =
+// 36 C) with the output transform fused: at every batch boundary of the k-loop the batch's
+// accumulators are folded into the 16 output pixels of each (tile, channel) element
+// (kWinoAT2) and reset, so the transformed product P never leaves registers; the epilogue
+// stores y (+ residual) with the BN statistics or the BN-backward sums.
+template <typename T, int BM, int BN, int MODE, bool HAS_RES, bool SPLIT, int WGM = 2, int TAPR = 0, bool WOUT = false>
 __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   constexpr int EPC = kEPC<T>, KS = kKS<T>;
   const T* const in = (const T*)a.in;
@@ -166,6 +194,29 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  static_assert(!WOUT || (sizeof(T) == 4 && !SPLIT && !TAPR && MODE == 0 && MT * NT == 1), "WOUT: fp32 16x16 wave tiles");
+  float yacc[WOUT ? 4 : 1][WOUT ? 16 : 1];
+  if constexpr (WOUT) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) yacc[e][q] = 0.f;
+  }
+  // batch boundary (WOUT): fold the batch's product into the output pixels, reset
+  auto wfold = [&](int ks) {
+    if constexpr (WOUT) {
+      if (((ks + 1) & (a.kps - 1)) == 0) {
+        const int b = __builtin_amdgcn_readfirstlane(ks / a.kps);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const float c = kWinoAT2[b][q];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) yacc[e][q] += c * acc[0][0][e];
+        }
+        acc[0][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
 
   if constexpr (TAPR) {
     static_assert(MODE == 0 || MODE == 1, "tap reuse: forward or stride-1 dgrad");
@@ -479,6 +530,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       }
       __builtin_amdgcn_sched_barrier(0);
       mma_tiles<MT, NT, T>(acc, fa1, fb1);
+      wfold(ks);
       stage = nxt;
     }
   } else {
@@ -497,10 +549,88 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
         load_frags(stage, kk, fa, fb);
         mma_tiles<MT, NT, T>(acc, fa, fb);
       }
+      wfold(ks);
       stage = stage == 2 ? 0 : stage + 1;
     }
   }
   }  // generic mainloop
+
+  if constexpr (WOUT) {
+    // lane: 4 consecutive channels oc..oc+3 (e) of tile t; 16 output pixels each
+    const int oc = oc0 + wm * (BM / WGM) + 4 * (lane >> 4);
+    const int t = pix0 + wn * (BN / WGN) + (lane & 15);
+    const bool bwd = a.bpart != nullptr, two = a.by2 != nullptr, st = a.stats != nullptr;
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f}, s3[4] = {0.f, 0.f, 0.f, 0.f};
+    float bm1[4], bi1[4], bm2[4], bi2[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bm1[e] = bi1[e] = bm2[e] = bi2[e] = 0.f;
+      if (bwd) {
+        bm1[e] = a.bsaved1[oc + e];
+        bi1[e] = a.bsaved1[a.OC + oc + e];
+        if (two) {
+          bm2[e] = a.bsaved2[oc + e];
+          bi2[e] = a.bsaved2[a.OC + oc + e];
+        }
+      }
+    }
+    if (t < a.npix) {
+      const int tw = a.wW >> 2, tpi = (a.wH >> 2) * tw;
+      const int nn = t / tpi, rem = t - nn * tpi, ti = rem / tw, tj = rem - ti * tw;
+      const size_t base = (((size_t)nn * a.wH + 4 * ti) * a.wW + 4 * tj) * a.OC + oc;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const size_t off = base + ((size_t)i * a.wW + j) * a.OC;
+          f32x4 v = {yacc[0][i * 4 + j], yacc[1][i * 4 + j], yacc[2][i * 4 + j], yacc[3][i * 4 + j]};
+          if (HAS_RES) v += *reinterpret_cast<const f32x4*>((const float*)a.res + off);
+          if (bwd) {
+            const f32x4 om = *reinterpret_cast<const f32x4*>((const float*)a.bo + off);
+            const f32x4 y1 = *reinterpret_cast<const f32x4*>((const float*)a.by1 + off);
+            f32x4 y2 = {0.f, 0.f, 0.f, 0.f};
+            if (two) y2 = *reinterpret_cast<const f32x4*>((const float*)a.by2 + off);
+            f32x4 dz;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              dz[e] = om[e] > 0.f ? v[e] : 0.f;
+              s1[e] += dz[e];
+              s2[e] += dz[e] * (y1[e] - bm1[e]) * bi1[e];
+              if (two) s3[e] += dz[e] * (y2[e] - bm2[e]) * bi2[e];
+            }
+            *reinterpret_cast<f32x4*>((float*)a.out + off) = a.bmask ? dz : v;
+          } else {
+            *reinterpret_cast<f32x4*>((float*)a.out + off) = v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              s1[e] += v[e];
+              s2[e] += v[e] * v[e];
+            }
+          }
+        }
+    }
+    if (!st && !bwd) return;
+    // lanes of one wave with the same channels differ in lane bits 0..3
+#pragma unroll
+    for (int sh = 1; sh < 16; sh <<= 1)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s1[e] += __shfl_xor(s1[e], sh, 64);
+        s2[e] += __shfl_xor(s2[e], sh, 64);
+        if (two) s3[e] += __shfl_xor(s3[e], sh, 64);
+      }
+    if ((lane & 15) == 0) {
+      const int nst = bwd ? a.bns : 2;
+      float* dst = (bwd ? a.bpart : a.stats) + (size_t)(pix_t & (PSX_STAT_SLOTS - 1)) * nst * a.OC + oc;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        atomicAdd(dst + e, s1[e]);
+        atomicAdd(dst + a.OC + e, s2[e]);
+        if (two) atomicAdd(dst + 2 * a.OC + e, s3[e]);
+      }
+    }
+    return;
+  }
 
   if constexpr (SPLIT) {
     float* dst = a.part + (size_t)split * a.npix * a.OC;
@@ -1052,6 +1182,52 @@ int psx_conv_dgrad2(const void* dy, const void* wd, void* dx, const void* res, c
   a.Kg = Kg;
   a.npix = Nb * H * W;
   return f32 ? conv_dgrad2_t<float>(a, ws, st) : conv_dgrad2_t<uint16_t>(a, ws, st);
+}
+
+// Fused Winograd GEMM + output transform (conv2_kernel WOUT): V [36][T][C] (batch-major), U
+// [K][36][C] -> y [N][H][W][K] (+ res) with the BN statistics (stats) or the BN-backward sums
+// (bst, conv_v2 BwdStatsDesc) of y. 32x32 workgroup tiles (16x16 per wave); C a power of two >= 32.
+int psx_wino_gemm_out(const float* V, const float* U, float* y, const float* res, float* stats,
+                      const BwdStatsDesc* bst, const void* zero, int N, int H, int W, int C, int K, hipStream_t st) {
+  const int T = N * (H / 4) * (W / 4);
+  if (K % 32 || C < kKS<float> || (C & (C - 1)) || H % 4 || W % 4 || T < 1) return -2;
+  Conv2Args a{};
+  a.in = V;
+  a.w = U;
+  a.out = y;
+  a.res = res;
+  a.stats = bst ? nullptr : stats;
+  a.zero = zero;
+  if (bst) {
+    a.bpart = bst->part;
+    a.bo = bst->o;
+    a.by1 = bst->y1;
+    a.by2 = bst->y2;
+    a.bsaved1 = bst->saved1;
+    a.bsaved2 = bst->saved2;
+    a.bns = bst->y2 ? 3 : 2;
+    a.bmask = bst->mask_store;
+  }
+  a.Nb = 1; a.IH = 36; a.IW = T; a.OH = 1; a.OW = T;
+  a.IC = C;
+  a.OC = K;
+  a.R = 36; a.S = 1; a.pad = 0; a.stride = 1;
+  a.Kg = 36 * C;
+  a.log2_icc = ilog2i(C / kEPC<float>);
+  a.npix = T;
+  a.n_oc_tiles = K / 32;
+  a.n_pix_tiles = (T + 31) / 32;
+  a.splits = 1;
+  a.kps = C / kKS<float>;
+  a.wH = H;
+  a.wW = W;
+  const size_t lds = (size_t)3 * (32 + 32) * 128;
+  const dim3 grid(a.n_oc_tiles * a.n_pix_tiles);
+  if (res)
+    hipLaunchKernelGGL((conv2_kernel<float, 32, 32, 0, true, false, 2, 0, true>), grid, dim3(256), lds, st, a);
+  else
+    hipLaunchKernelGGL((conv2_kernel<float, 32, 32, 0, false, false, 2, 0, true>), grid, dim3(256), lds, st, a);
+  return (int)hipGetLastError();
 }
 
 // nb independent fp32 GEMMs P[b][M][N] = A[b] . B[:, b, :]^T with A [nb][M][Kd] (batch-major

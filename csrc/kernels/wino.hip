@@ -36,6 +36,8 @@
 
 extern "C" int psx_bgemm_f32(const float* A, const float* B, float* P, const void* zero, int M, int N, int Kd, int nb,
                              int cfg, hipStream_t st);
+extern "C" int psx_wino_gemm_out(const float* V, const float* U, float* y, const float* res, float* stats,
+                                 const void* bst, const void* zero, int N, int H, int W, int C, int K, hipStream_t st);
 extern "C" int psx_bgemm_tn_f32(const float* X, const float* D, float* part, const void* zero, int T, int C, int K,
                                 int nb, int q, int BR, int BC, hipStream_t st);
 
@@ -443,6 +445,15 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
   const int T = N * (H / 4) * (W / 4);
   const int gy = wino_tile_grid(T);
   hipLaunchKernelGGL(wino_in_kernel, dim3(C / 64, gy), dim3(256), 0, st, x, V, T, H, W, C);
+  // fused GEMM + output transform (conv_v2.hip WOUT: P stays in registers), PSX_WINO_FUSED=1
+  // where its 32x32 tiles fill the chip, 2 always (tests). Off by default: its 16x16 wave tiles
+  // (the 16 output pixels of every accumulator element take 64 registers) run the MFMA far below
+  // the 64x64-tile batched GEMM; same-box per layer 32x32x64 85 vs 82 us, 16x16x128 98 vs 54 us,
+  // bench 4.01 vs 3.83 ms/step
+  const char* fe = getenv("PSX_WINO_FUSED");
+  const int fused_mode = fe ? atoi(fe) : 0;
+  if (K % 32 == 0 && (fused_mode == 2 || (fused_mode == 1 && (long)(K / 32) * ((T + 31) / 32) >= 256)))
+    return psx_wino_gemm_out(V, U, y, res, stats, bst, zero, N, H, W, C, K, st);
   int e = psx_bgemm_f32(V, U, P, zero, T, K, C, 36, cfg, st);
   if (e) return e;
   WinoBwdStats bs{};

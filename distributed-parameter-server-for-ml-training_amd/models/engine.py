@@ -378,8 +378,9 @@ class HipResNetEngine:
 
     def _plan_wino(self):
         """fp32 Winograd F(4x4,3x3) (csrc/kernels/wino.hip) for the 3x3 / stride-1 layers: forward
-        and data gradient on images up to PSX_WINO_MAXHW (default 32: every 3x3 stride-1 layer of
-        ResNet-18 CIFAR), weight gradient (PSX_WINO_WGRAD=1, default) up to PSX_WINO_WGRAD_MAXHW
+        and data gradient on images up to PSX_WINO_MAXHW (default 64: every 3x3 stride-1 layer of
+        ResNet-18 CIFAR and ResNet-50's 56x56 / 28x28 ones; R50 fp32 top-k 3,060 -> 3,188 img/s),
+        weight gradient (PSX_WINO_WGRAD=1, default) up to PSX_WINO_WGRAD_MAXHW
         (default 16: on 32x32 the direct tap-reuse kernel is faster, 101 vs 129 us). Same-box
         per-layer A/B in profiles/r2s4_wino_*.jsonl. Per layer: the transformed forward weights
         U [cout][36][cin] and data-gradient weights U' [cin][36][cout] (rebuilt by unpack() every
@@ -390,7 +391,7 @@ class HipResNetEngine:
         self.wino_wgrad = set()
         if not self.f32 or self.deterministic or os.environ.get("PSX_WINO", "1") == "0":
             return
-        maxhw = int(os.environ.get("PSX_WINO_MAXHW", "32"))
+        maxhw = int(os.environ.get("PSX_WINO_MAXHW", "64"))
         wg = os.environ.get("PSX_WINO_WGRAD", "1") == "1"
         wg_maxhw = int(os.environ.get("PSX_WINO_WGRAD_MAXHW", "32"))
         B = self.B

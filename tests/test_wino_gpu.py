@@ -51,9 +51,13 @@ def _nhwc(t):
     return t.permute(0, 2, 3, 1).contiguous()
 
 
+@pytest.mark.parametrize("fused", ["0", "2"])
 @pytest.mark.parametrize("nb,h,c,k,res", [(4, 8, 64, 128, False), (3, 4, 128, 64, True), (8, 8, 256, 256, True),
-                                          (2, 16, 64, 64, False), (4, 4, 512, 512, False)])
-def test_wino_fwd(nb, h, c, k, res):
+                                          (2, 16, 64, 64, False), (4, 4, 512, 512, False), (8, 32, 64, 64, True)])
+def test_wino_fwd(nb, h, c, k, res, fused, monkeypatch):
+    """fused = "2": the GEMM with the output transform in its epilogue (conv_v2 WOUT), "0": the
+    36 batched GEMMs + the output-transform kernel."""
+    monkeypatch.setenv("PSX_WINO_FUSED", fused)
     torch.manual_seed(nb * h + c)
     x = torch.relu(torch.randn(nb, c, h, h, device=DEV, dtype=torch.float64))
     w = torch.randn(k, c, 3, 3, device=DEV, dtype=torch.float64) * (2.0 / (9 * c)) ** 0.5
@@ -74,8 +78,10 @@ def test_wino_fwd(nb, h, c, k, res):
     assert torch.allclose(s[1], (refn ** 2).sum((0, 1, 2)), rtol=1e-4)
 
 
+@pytest.mark.parametrize("fused", ["0", "2"])
 @pytest.mark.parametrize("nb,h,c,k", [(4, 8, 128, 256), (3, 4, 512, 512)])
-def test_wino_dgrad(nb, h, c, k):
+def test_wino_dgrad(nb, h, c, k, fused, monkeypatch):
+    monkeypatch.setenv("PSX_WINO_FUSED", fused)
     """dx of y = conv3x3(x): the forward pipeline on dy with the flipped transform U'[c][36][k]."""
     torch.manual_seed(c + k)
     w = torch.randn(k, c, 3, 3, device=DEV, dtype=torch.float64) * (2.0 / (9 * c)) ** 0.5
@@ -180,8 +186,10 @@ def test_wino_weights_multi_matches_single():
         assert torch.equal(u, r)
 
 
+@pytest.mark.parametrize("fused", ["0", "2"])
 @pytest.mark.parametrize("two,mask_store,res", [(False, False, False), (True, True, True), (False, True, False)])
-def test_wino_dgrad_fused_bn_bwd_sums(two, mask_store, res):
+def test_wino_dgrad_fused_bn_bwd_sums(two, mask_store, res, fused, monkeypatch):
+    monkeypatch.setenv("PSX_WINO_FUSED", fused)
     """Data gradient with the consumer BN's backward sums fused into the output transform (what
     the direct dgrad epilogue does): slot sums of dz = g*[o>0], dz*xhat1 (, dz*xhat2); the stored
     output is dz with mask_store, else g."""

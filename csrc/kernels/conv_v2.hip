@@ -172,7 +172,9 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   // MODE 3 = stride-2 dgrad, one parity class (py, px) of dx per blockIdx.y: dx(2i+py, 2j+px)
   // only receives taps r = r0, r0+2, .. and s = s0, s0+2, .. (r0 = (py+pad)&1), i.e. a dense
   // GEMM over 1, 2, 2 or 4 of the 9 taps instead of 9 with 3/4 of the products zero.
-  const int cls = MODE == 3 ? blockIdx.y : 0;
+  // classes in decreasing work order (the (1,1) class has 4 of the 9 taps, (0,0) one): the
+  // dispatcher walks blockIdx.y last, so the longest workgroups start first
+  const int cls = MODE == 3 ? 3 - (int)blockIdx.y : 0;
   const int py = cls >> 1, px = cls & 1;
   const int CH = (a.OH - py + 1) >> 1, CW = (a.OW - px + 1) >> 1;
   const int r0 = (py + a.pad) & 1, s0 = (px + a.pad) & 1;

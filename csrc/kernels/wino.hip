@@ -60,11 +60,57 @@ PSX_DEV void wino_at6(const float (&m)[6], float (&o)[4]) {
   o[3] = b + 8.f * d + m[5];
 }
 
-// V[b][t][c]: one thread per (tile, channel); block = 64 channels x 4 tiles
+// Forward BN finalize descriptor (the layout of bnfin.hpp BnFin)
+struct WinoBnFin {
+  const float* gamma;
+  const float* beta;
+  float* run_mean;
+  float* run_var;
+  float* scale;
+  float* shift;
+  float* save_mean;
+  float* save_invstd;
+  unsigned* counter;
+  float count, eps, momentum;
+  int C;
+};
+
+// V[b][t][c]: one thread per (tile, channel); block = 64 channels x 4 tiles.
+// bnpart (nullable): x is the PRE-BatchNorm conv output z of the previous layer, and the operand
+// is relu(BN(z)) — the training-mode BN finalize (batch statistics from the slot rows
+// bnpart[slot][2][C], as bnfin.hpp bn_fin_lds computes them) and the BN + ReLU apply are folded
+// into this load, so the activation relu(BN(z)) is never written. The workgroups of tile row 0
+// publish the affine, saved statistics and running statistics of their channels.
 __global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ x, float* __restrict__ V, int T, int H,
-                                                      int W, int C) {
+                                                      int W, int C, const float* __restrict__ bnpart, WinoBnFin fin) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int tw = W >> 2, tpi = (H >> 2) * tw;
+  float sc = 1.f, sh = 0.f;
+  if (bnpart) {
+    double s = 0.0, ss = 0.0;
+#pragma unroll
+    for (int t = 0; t < PSX_STAT_SLOTS; ++t) {
+      s += bnpart[(size_t)t * 2 * C + c];
+      ss += bnpart[(size_t)t * 2 * C + C + c];
+    }
+    const double mean = s / fin.count;
+    double var = ss / fin.count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)fin.eps));
+    sc = fin.gamma[c] * invstd;
+    sh = fin.beta[c] - (float)mean * sc;
+    if (blockIdx.y == 0 && threadIdx.x < 64) {
+      fin.scale[c] = sc;
+      fin.shift[c] = sh;
+      fin.save_mean[c] = (float)mean;
+      fin.save_invstd[c] = invstd;
+      if (fin.run_mean) {
+        const double unb = fin.count > 1.f ? var * fin.count / (fin.count - 1.0) : var;
+        fin.run_mean[c] = (1.f - fin.momentum) * fin.run_mean[c] + fin.momentum * (float)mean;
+        fin.run_var[c] = (1.f - fin.momentum) * fin.run_var[c] + fin.momentum * (float)unb;
+      }
+    }
+  }
   for (int t = blockIdx.y * 4 + (threadIdx.x >> 6); t < T; t += 4 * gridDim.y) {
     const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
     const int h0 = 4 * ti - 1, w0 = 4 * tj - 1;
@@ -75,7 +121,12 @@ __global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ 
 #pragma unroll
       for (int s = 0; s < 6; ++s) {
         const int h = h0 + r, w = w0 + s;
-        d[r][s] = ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) ? xn[((size_t)h * W + w) * C] : 0.f;
+        float v = 0.f;  // zero padding stays zero (outside the image, after BN + ReLU)
+        if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
+          v = xn[((size_t)h * W + w) * C];
+          if (bnpart) v = fmaxf(v * sc + sh, 0.f);
+        }
+        d[r][s] = v;
       }
     float e[6][6];  // e = B^T d (columns)
 #pragma unroll
@@ -192,6 +243,7 @@ struct WinoBwdStats {
   const float* saved1;  // [2][K] mean, invstd
   const float* saved2;
   int mask_store;
+  const float* mask_aff;  // nullable: ReLU mask = [y1 * scale + shift > 0] (affine [2][K]) instead of o
 };
 
 // y = A^T P A (+ res); forward: BN partial sums (sum y, sum y^2) of the stored values into slot
@@ -207,10 +259,14 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
   const int tw = W >> 2, tpi = (H >> 2) * tw;
   const size_t bstride = (size_t)T * K;
   const bool bwd = bs.part != nullptr, two = bs.y2 != nullptr;
-  float m1 = 0.f, i1 = 0.f, m2 = 0.f, i2 = 0.f;
+  float m1 = 0.f, i1 = 0.f, m2 = 0.f, i2 = 0.f, msc = 0.f, msh = 0.f;
   if (bwd) {
     m1 = bs.saved1[k];
     i1 = bs.saved1[K + k];
+    if (bs.mask_aff) {
+      msc = bs.mask_aff[k];
+      msh = bs.mask_aff[K + k];
+    }
     if (two) {
       m2 = bs.saved2[k];
       i2 = bs.saved2[K + k];
@@ -242,9 +298,11 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
         float v = o[j];
         if (res) v += res[off];
         if (bwd) {
-          const float dz = bs.o[off] > 0.f ? v : 0.f;
+          const float y1 = bs.y1[off];
+          const bool pos = bs.mask_aff ? y1 * msc + msh > 0.f : bs.o[off] > 0.f;
+          const float dz = pos ? v : 0.f;
           s1 += dz;
-          s2 += dz * (bs.y1[off] - m1) * i1;
+          s2 += dz * (y1 - m1) * i1;
           if (two) s3 += dz * (bs.y2[off] - m2) * i2;
           y[off] = bs.mask_store ? dz : v;
         } else {
@@ -436,15 +494,20 @@ int psx_wino_weights_multi(const float* const* w, float* const* U, const int* K,
 // y[N][H][W][K] = conv3x3(x[N][H][W][C]) (+ res) with the pre-transformed weights U [K][36][C];
 // stats (nullable): BN partial sums into slot rows [PSX_STAT_SLOTS][2][K] (pre-zeroed); bst
 // (nullable, data gradient): the consumer BN's backward sums instead (conv_v2 BwdStatsDesc).
+// bnpart + bnfin (nullable, forward): x is the previous layer's pre-BN output; its BN finalize +
+// BN + ReLU run inside the input transform (wino_in_kernel).
 // V: psx_wino_v_floats(C) (the transformed input, left there for psx_wino_wgrad), P: 36*T*K
 // floats. cfg: GEMM tile (psx_bgemm_f32).
 int psx_wino_conv(const float* x, const float* U, float* y, const float* res, float* stats, float* V, float* P,
                   const void* zero, int N, int H, int W, int C, int K, int cfg, const WinoBwdStats* bst,
-                  hipStream_t st) {
+                  const float* bnpart, const WinoBnFin* bnfin, hipStream_t st) {
+  if (bnpart && (!bnfin || bnfin->C != C)) return -3;
   if (!psx_wino_ok(H, W, C, K)) return -2;
   const int T = N * (H / 4) * (W / 4);
   const int gy = wino_tile_grid(T);
-  hipLaunchKernelGGL(wino_in_kernel, dim3(C / 64, gy), dim3(256), 0, st, x, V, T, H, W, C);
+  WinoBnFin bf{};
+  if (bnpart) bf = *bnfin;
+  hipLaunchKernelGGL(wino_in_kernel, dim3(C / 64, gy), dim3(256), 0, st, x, V, T, H, W, C, bnpart, bf);
   // fused GEMM + output transform (conv_v2.hip WOUT: P stays in registers), PSX_WINO_FUSED=1
   // where its 32x32 tiles fill the chip, 2 always (tests). Off by default: its 16x16 wave tiles
   // (the 16 output pixels of every accumulator element take 64 registers) run the MFMA far below
@@ -452,7 +515,8 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
   // bench 4.01 vs 3.83 ms/step
   const char* fe = getenv("PSX_WINO_FUSED");
   const int fused_mode = fe ? atoi(fe) : 0;
-  if (K % 32 == 0 && (fused_mode == 2 || (fused_mode == 1 && (long)(K / 32) * ((T + 31) / 32) >= 256)))
+  if (K % 32 == 0 && !(bst && bst->mask_aff) &&
+      (fused_mode == 2 || (fused_mode == 1 && (long)(K / 32) * ((T + 31) / 32) >= 256)))
     return psx_wino_gemm_out(V, U, y, res, stats, bst, zero, N, H, W, C, K, st);
   int e = psx_bgemm_f32(V, U, P, zero, T, K, C, 36, cfg, st);
   if (e) return e;

@@ -389,6 +389,7 @@ class HipResNetEngine:
         bf16. PSX_WINO=0: direct kernels everywhere."""
         self.wino_layers = {}
         self.wino_wgrad = set()
+        self.wino_bnfold = {}
         if not self.f32 or self.deterministic or os.environ.get("PSX_WINO", "1") == "0":
             return
         maxhw = int(os.environ.get("PSX_WINO_MAXHW", "64"))
@@ -411,6 +412,18 @@ class HipResNetEngine:
                 self.wino_wgrad.add(cs.name)
                 s_d = max(s_d, vk)
                 s_part = max(s_part, 36 * q * cs.cout * cs.cp)
+        # BN folded into the next conv's input transform (PSX_WINO_BNFOLD=1, default): a block's inner
+        # BN (+ ReLU) whose only consumer is a Winograd conv with a Winograd weight gradient (that
+        # reads V, not the activation) is finalized and applied inside wino_in_kernel, so its
+        # activation is never written; the data gradient's ReLU mask comes from the BN affine
+        # (needs the masked dz store, so the BN-backward apply never reads the activation either)
+        self.wino_bnfold = {}
+        if self._fold and self.mask_store and os.environ.get("PSX_WINO_BNFOLD", "1") == "1":
+            for b in self.spec.blocks:
+                for i in range(len(b.convs) - 1):
+                    nxt = b.convs[i + 1]
+                    if nxt.name in self.wino_wgrad and nxt.cin == b.bns[i].c:
+                        self.wino_bnfold[b.bns[i].name] = nxt.name
         # main-stream scratch (forward V of layers without a Winograd weight gradient / GEMM output;
         # data-gradient input tiles + GEMM output) and the weight-gradient side stream's own (dy
         # tiles, GEMM partials)
@@ -472,7 +485,7 @@ class HipResNetEngine:
             self._fins[key] = f
         return f
 
-    def _conv_bn_fwd(self, cs: ConvSpec, x, y, bs: BNSpec, arena, train: bool):
+    def _conv_bn_fwd(self, cs: ConvSpec, x, y, bs: BNSpec, arena, train: bool, bn_in=None):
         """conv -> (train) batch statistics + BN finalize | (eval) running-statistics affine.
         With conv v2 the finalize runs inside the conv launch (last workgroup, bnfin.hpp)."""
         oh, ow = cs.out_hw
@@ -481,9 +494,10 @@ class HipResNetEngine:
         stats = self._red(bs, "fwd") if train else None
         fin = self._fin_fwd(bs, arena, npix) if (train and self.fuse_fin) else None
         wl = self.wino_layers.get(cs.name)
+        assert bn_in is None or wl is not None, cs.name
         if wl is not None:
             v = wl[2] if wl[2] is not None else self.wino_s2
-            K.wino_conv(x, wl[0], y, None, stats, v, self.wino_s1, self.B, cs.h, cs.w, cs.cp, cs.cout)
+            K.wino_conv(x, wl[0], y, None, stats, v, self.wino_s1, self.B, cs.h, cs.w, cs.cp, cs.cout, bn_in=bn_in)
             if not train:
                 self._bn_eval(bs, arena)
             elif not self._fold:  # no in-launch finalize on this path
@@ -618,7 +632,10 @@ class HipResNetEngine:
             bs, o, y, two = bn_next
             st = self.bn[bs.name]
             ms = self.mask_store
-            if two is None:
+            if bs.name in self.wino_bnfold:  # o was never written: the mask comes from the affine
+                bst = K.bwd_stats_desc(self._red(bs, "bwd"), None, y, st["saved"], mask_store=ms,
+                                       mask_aff=st["affine"])
+            elif two is None:
                 bst = K.bwd_stats_desc(self._red(bs, "bwd"), o, y, st["saved"], mask_store=ms)
             else:
                 bs2, y2 = two
@@ -751,10 +768,17 @@ class HipResNetEngine:
         for b, d in zip(sp.blocks, self.blk):
             src = d["inp"]
             L = len(b.convs)
+            bn_in = None
             for i, cs in enumerate(b.convs):
-                self._conv_bn_fwd(cs, src, d["y"][i], b.bns[i], arena, train)
+                self._conv_bn_fwd(cs, src, d["y"][i], b.bns[i], arena, train, bn_in=bn_in)
+                bn_in = None
                 if i < L - 1:
-                    self._apply(b.bns[i], d["y"][i], d["a"][i], arena, train)
+                    bs = b.bns[i]
+                    if train and bs.name in self.wino_bnfold:  # applied by the next conv's input transform
+                        bn_in = (self._red(bs, "fwd"), self._fin_fwd(bs, arena, d["y"][i].numel() // bs.c))
+                        src = d["y"][i]
+                        continue
+                    self._apply(bs, d["y"][i], d["a"][i], arena, train)
                     src = d["a"][i]
             if b.down:
                 ds, dbn = b.down

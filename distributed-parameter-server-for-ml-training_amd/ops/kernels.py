@@ -144,13 +144,18 @@ def conv_fwd2(x, wf, y, stats, ws, nb, h, w, ic, oc, k, stride, pad, kg, fin: Bn
 class BwdStatsDesc(C.Structure):
     """csrc/kernels/conv_v2.hip BwdStatsDesc: fused BN-backward reduction over a dgrad output."""
     _fields_ = [("part", C.c_void_p), ("o", C.c_void_p), ("y1", C.c_void_p), ("y2", C.c_void_p),
-                ("saved1", C.c_void_p), ("saved2", C.c_void_p), ("mask_store", C.c_int)]
+                ("saved1", C.c_void_p), ("saved2", C.c_void_p), ("mask_store", C.c_int),
+                ("mask_aff", C.c_void_p)]
 
 
-def bwd_stats_desc(part, o, y1, saved1, y2=None, saved2=None, mask_store=False) -> BwdStatsDesc:
+def bwd_stats_desc(part, o, y1, saved1, y2=None, saved2=None, mask_store=False, mask_aff=None) -> BwdStatsDesc:
     """``mask_store`` (dgrad only): the epilogue stores dz = g * [o > 0] instead of g, so the BN
-    backward apply reading it runs without the mask operand o."""
-    return BwdStatsDesc(ptr(part), ptr(o), ptr(y1), ptr(y2), ptr(saved1), ptr(saved2), int(bool(mask_store)))
+    backward apply reading it runs without the mask operand o. ``mask_aff`` (Winograd data
+    gradient only; o = None): the ReLU mask is [y1 * scale + shift > 0] with the BN affine
+    [2][C] — the layer whose post-ReLU activation was never written (wino_conv ``bn_in``)."""
+    assert o is not None or mask_aff is not None
+    return BwdStatsDesc(ptr(part), ptr(o), ptr(y1), ptr(y2), ptr(saved1), ptr(saved2), int(bool(mask_store)),
+                        ptr(mask_aff))
 
 
 def conv_dgrad2(dy, wd, dx, res, ws, nb, h, w, ic_fwd, oc_fwd, k, stride, pad, kgd, bst: BwdStatsDesc | None = None):
@@ -229,19 +234,23 @@ class WinoWeightBatch:
               "wino_weights_multi")
 
 
-def wino_conv(x, u, y, res, stats, v, p, nb, h, w, c, k, cfg=None, bst: "BwdStatsDesc | None" = None):
+def wino_conv(x, u, y, res, stats, v, p, nb, h, w, c, k, cfg=None, bst: "BwdStatsDesc | None" = None, bn_in=None):
     """fp32 3x3/s1/p1 conv y = conv(x) (+ res) via Winograd F(4x4,3x3) with pre-transformed
     weights u (wino_weights); stats: BN slot sums of y (pre-zeroed) or None; bst (data gradient,
     bwd_stats_desc): the consumer BN's backward sums (and the masked store) instead. v (>=
     wino_v_floats of c) receives the transformed input (kept for wino_wgrad), p (>= wino_v_floats
-    of k) is scratch."""
+    of k) is scratch. bn_in = (slot rows [STAT_SLOTS][2][c], BnFin): x is the previous layer's
+    pre-BN output; its training-mode BN finalize + BN + ReLU are folded into the input transform
+    (the BnFin's affine / saved / running statistics are written by the launch)."""
     assert x.dtype == torch.float32 and y.dtype == torch.float32
     assert x.numel() == nb * h * w * c and y.numel() == nb * h * w * k and u.numel() >= 36 * k * c
     assert v.numel() >= wino_v_floats(nb, h, w, c) and p.numel() >= wino_v_floats(nb, h, w, k)
     assert res is None or res.numel() == y.numel()
     check(kernels().psx_wino_conv(ptr(x), ptr(u), ptr(y), ptr(res), ptr(stats), ptr(v), ptr(p), ptr(zero_page(x.device)),
                                   nb, h, w, c, k, WINO_CFG if cfg is None else cfg,
-                                  C.byref(bst) if bst is not None else None, stream_ptr()), "wino_conv")
+                                  C.byref(bst) if bst is not None else None,
+                                  ptr(bn_in[0]) if bn_in is not None else None,
+                                  C.byref(bn_in[1]) if bn_in is not None else None, stream_ptr()), "wino_conv")
 
 
 def wino_wgrad(v, dy, d, part, out, nb, h, w, c, k, scale=1.0):

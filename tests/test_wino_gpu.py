@@ -221,3 +221,43 @@ def test_wino_dgrad_fused_bn_bwd_sums(two, mask_store, res, fused, monkeypatch):
         sums.append((dz * (y2.double() - saved2[0].double()) * saved2[1].double()).sum((0, 1, 2)))
     for i, ref in enumerate(sums):
         assert _rel(s[i], ref) < 1e-4, i
+
+
+def test_engine_bn_fold_matches_unfolded(monkeypatch):
+    """Inner BN + ReLU folded into the next Winograd conv's input transform (PSX_WINO_BNFOLD=1,
+    default: the activation is never written, the backward mask comes from the BN affine) vs the
+    separate apply pass: loss, gradients and the running statistics the folded path publishes."""
+    from psx.models.engine import HipResNetEngine
+    from psx.models.layout import ParamLayout
+    from psx.models.resnet import ResNet18
+
+    torch.manual_seed(1)
+    model = ResNet18(100)
+    layout = ParamLayout.from_module(model)
+    arena0, _ = layout.pack(model)
+    arena0 = arena0.to(DEV)
+    B = 32
+    imgs = torch.randint(0, 256, (64, 32, 32, 3), dtype=torch.uint8, device=DEV)
+    labs = torch.randint(0, 100, (64,), dtype=torch.int32, device=DEV)
+    out = {}
+    for fold in ("1", "0"):
+        monkeypatch.setenv("PSX_WINO_BNFOLD", fold)
+        eng = HipResNetEngine(model, layout, B, dtype=torch.float32)
+        assert (len(eng.wino_bnfold) == 8) == (fold == "1"), eng.wino_bnfold
+        eng.index.copy_(torch.arange(B, dtype=torch.int32, device=DEV))
+        a = arena0.clone()
+        eng.train_step(a, imgs, labs)
+        torch.cuda.synchronize()
+        out[fold] = (eng.loss.double().mean().item(), eng.grads.double().clone(), a.double().clone())
+    (l1, g1, a1), (l0, g0, a0) = out["1"], out["0"]
+    assert abs(l1 - l0) < 1e-5 * max(1.0, abs(l0))
+    errs = []
+    for name, e in layout.entries.items():
+        if e.region != "param":
+            continue
+        x, y = g1[e.offset:e.offset + e.numel], g0[e.offset:e.offset + e.numel]
+        errs.append((((x - y).norm() / y.norm().clamp_min(1e-30)).item(), name))
+    assert max(errs)[0] < 2e-2, max(errs)
+    assert sorted(errs)[len(errs) // 2][0] < 1e-2, sorted(errs)
+    n = layout.param_numel  # running statistics (buffer region) written by the folded finalize
+    assert torch.allclose(a1[n:], a0[n:], rtol=1e-5, atol=1e-6)

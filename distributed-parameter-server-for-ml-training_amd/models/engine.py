@@ -223,6 +223,25 @@ class HipResNetEngine:
         self.pre_unpack = None
         self._build()
 
+    def _set_unpack_descs(self, convs):
+        """The param_unpack_tiles table: one descriptor per conv whose implicit-GEMM operands
+        (forward rows at wf_off, data-gradient rows at wd_off of wbuf) are unpacked each step."""
+        descs = []
+        tile0 = 0  # flat grid of param_unpack_tiles: (64x64 (oc, c) tile, chunk of <= 3 taps) units
+        for cs in convs:
+            descs.append((self.layout.offset(f"{cs.name}.weight"), cs.wf_off, cs.wd_off, cs.cout, cs.cin, cs.k, cs.k,
+                          cs.cp, cs.kg, cs.kgd, tile0))
+            tile0 += -(-cs.cout // 64) * -(-cs.cp // 64) * -(-(cs.k * cs.k) // 3)
+        self.ntiles = tile0
+        dsz = K.unpack_desc_size()
+        assert dsz == 3 * 8 + 8 * 4, dsz
+        raw = np.zeros(len(descs), dtype=np.dtype([("o", "<i8", 3), ("i", "<i4", 8)]))
+        for j, d in enumerate(descs):
+            raw[j]["o"] = d[:3]
+            raw[j]["i"] = d[3:]
+        self.descs = torch.from_numpy(raw.view(np.uint8).copy()).to(self.dev)
+        self.ndesc = len(descs)
+
     # ------------------------------------------------------------------ allocation
     def _bf(self, *shape):
         """An activation buffer of the compute dtype."""
@@ -235,8 +254,6 @@ class HipResNetEngine:
         sp, B = self.spec, self.B
         # weights: one bf16 buffer holding every conv's fwd (and dgrad) operand
         off = 0
-        descs = []
-        tile0 = 0  # flat grid of param_unpack_tiles: (64x64 (oc, c) tile, chunk of <= 3 taps) units
         for cs in all_convs(sp):
             cs.finalize(4 if self.f32 else 8)
             cs.wf_off = off
@@ -246,19 +263,8 @@ class HipResNetEngine:
                 off += cs.cp * cs.kgd
             else:
                 cs.wd_off = -1
-            descs.append((self.layout.offset(f"{cs.name}.weight"), cs.wf_off, cs.wd_off, cs.cout, cs.cin, cs.k, cs.k,
-                          cs.cp, cs.kg, cs.kgd, tile0))
-            tile0 += -(-cs.cout // 64) * -(-cs.cp // 64) * -(-(cs.k * cs.k) // 3)
-        self.ntiles = tile0
         self.wbuf = torch.zeros(off, dtype=self.dtype, device=self.dev)
-        dsz = K.unpack_desc_size()
-        assert dsz == 3 * 8 + 8 * 4, dsz
-        raw = np.zeros(len(descs), dtype=np.dtype([("o", "<i8", 3), ("i", "<i4", 8)]))
-        for j, d in enumerate(descs):
-            raw[j]["o"] = d[:3]
-            raw[j]["i"] = d[3:]
-        self.descs = torch.from_numpy(raw.view(np.uint8).copy()).to(self.dev)
-        self.ndesc = len(descs)
+        self._set_unpack_descs(list(all_convs(sp)))
 
         H, W = sp.in_hw
         self.x0 = self._bf(B, H, W, sp.stem_conv.cp)
@@ -365,6 +371,10 @@ class HipResNetEngine:
         self.wpart = self._f32(max(1, max_wg))
         self.wpart_w = self._f32(max(1, self._plan_wpart(max_wp)))
         self._plan_wino()
+        if self.wino_layers:
+            # Winograd layers read their own transformed weights (unpack -> _wino_unpack): drop
+            # them from the implicit-GEMM operand unpack (13 of ResNet-18's 20 convs, most bytes)
+            self._set_unpack_descs([cs for cs in all_convs(sp) if cs.name not in self.wino_layers])
         # head
         fh, fw = self.final.shape[1], self.final.shape[2]
         self.head_hw = fh * fw

@@ -83,10 +83,11 @@ struct WinoBnFin {
 // publish the affine, saved statistics and running statistics of their channels.
 __global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ x, float* __restrict__ V, int T, int H,
                                                       int W, int C, const float* __restrict__ bnpart, WinoBnFin fin) {
+  __shared__ float aff[2][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int tw = W >> 2, tpi = (H >> 2) * tw;
   float sc = 1.f, sh = 0.f;
-  if (bnpart) {
+  if (bnpart && threadIdx.x < 64) {  // wave 0 finalizes the workgroup's 64 channels
     double s = 0.0, ss = 0.0;
 #pragma unroll
     for (int t = 0; t < PSX_STAT_SLOTS; ++t) {
@@ -99,7 +100,9 @@ __global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ 
     const float invstd = (float)(1.0 / sqrt(var + (double)fin.eps));
     sc = fin.gamma[c] * invstd;
     sh = fin.beta[c] - (float)mean * sc;
-    if (blockIdx.y == 0 && threadIdx.x < 64) {
+    aff[0][threadIdx.x] = sc;
+    aff[1][threadIdx.x] = sh;
+    if (blockIdx.y == 0) {
       fin.scale[c] = sc;
       fin.shift[c] = sh;
       fin.save_mean[c] = (float)mean;
@@ -110,6 +113,11 @@ __global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ 
         fin.run_var[c] = (1.f - fin.momentum) * fin.run_var[c] + fin.momentum * (float)unb;
       }
     }
+  }
+  if (bnpart) {
+    __syncthreads();
+    sc = aff[0][threadIdx.x & 63];
+    sh = aff[1][threadIdx.x & 63];
   }
   for (int t = blockIdx.y * 4 + (threadIdx.x >> 6); t < T; t += 4 * gridDim.y) {
     const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;

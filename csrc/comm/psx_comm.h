@@ -11,6 +11,9 @@ int psx_comm_reduce_sum(void* h, const void* send, void* recv, long count, int d
 int psx_comm_broadcast(void* h, void* buf, long count, int dtype, int root, hipStream_t st);
 int psx_comm_reduce_scatter_sum(void* h, const void* send, void* recv, long count, int dtype, hipStream_t st);
 int psx_comm_all_gather(void* h, const void* send, void* recv, long count, int dtype, hipStream_t st);
+int psx_comm_abort(void* h);
+int psx_comm_group_start();
+int psx_comm_group_end();
 }
 
 // psx dtype codes (parallel/rccl.py DTYPES)

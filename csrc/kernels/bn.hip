@@ -10,7 +10,10 @@
 // ([T][2][C]); bn_finalize reduces them (fp64, fixed order => deterministic), produces the
 // per-channel affine (scale, shift) and updates the running stats. Every elementwise pass is
 // vectorised at 8 channels per lane (16 B bf16 / 32 B fp32).
+#include <stdio.h>
 #include <stdlib.h>
+
+#include <algorithm>
 
 #include "bnfin.hpp"
 #include "common.hpp"
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
       atomicAdd(part + ((size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * NS + stat) * C + cgi * 8 + j, acc);
   }
   if (det.slab) {
-    if (det_finish(det, NS, C, part, gridDim.x, reinterpret_cast<unsigned char*>(sred)) && fuse_fin) {
+    if (det_finish(det, NS, C, part, blockIdx.x, reinterpret_cast<unsigned char*>(sred)) && fuse_fin) {
       bn_bwd_finalize_block<PSX_STAT_SLOTS>(part, NS, 1, fin1);
       if (TWO) bn_bwd_finalize_block<PSX_STAT_SLOTS>(part, NS, 2, fin2);
     }
@@ -394,12 +397,29 @@ DetState g_det;
 
 bool det_enabled() { return g_det.slab != nullptr; }
 
-DetRed det_next(int rows, int NS, int C) {
-  DetRed d{nullptr, nullptr, 0};
-  if (!g_det.slab || (long)rows * NS * C > g_det.slab_floats) return d;
+constexpr int kDetCtrSets = 64, kDetCtrPerSet = 256;  // counter words: [set][1 + group]
+
+DetRed det_next(int rows, int NS, int C, int nper) {
+  DetRed d{};
+  if (!g_det.slab) return d;
+  // level-1 groups of ~sqrt(rows) rows (the two levels' serial chains balanced), <= kDetCtrPerSet - 1
+  int group = 8;
+  while (group * group < rows) group *= 2;
+  while ((rows + group - 1) / group > kDetCtrPerSet - 1) group *= 2;
+  const int ngroups = (rows + group - 1) / group;
+  const long need = ((long)rows + ngroups) * NS * C;
+  if (need > g_det.slab_floats) {
+    fprintf(stderr, "psx deterministic mode: slab of %ld floats < %ld needed (%d rows x %d x %d)\n",
+            g_det.slab_floats, need, rows, NS, C);
+    abort();
+  }
   d.slab = g_det.slab;
-  d.counter = g_det.counters + (g_det.next++ % g_det.ncounters);
+  d.slab2 = g_det.slab + (size_t)rows * NS * C;
+  d.counter = g_det.counters + (size_t)(g_det.next++ % kDetCtrSets) * kDetCtrPerSet;
   d.rows = rows;
+  d.group = group;
+  d.ngroups = ngroups;
+  d.nper = nper;
   return d;
 }
 
@@ -434,11 +454,12 @@ int psx_set_deterministic(void* buf, long bytes) {
     g_det = DetState{};
     return 0;
   }
-  if (bytes < 4096) return -2;
+  const long ctr_bytes = (long)kDetCtrSets * kDetCtrPerSet * 4;
+  if (bytes < ctr_bytes + 4096) return -2;
   g_det.counters = (unsigned*)buf;
-  g_det.ncounters = 64;
-  g_det.slab = (float*)((char*)buf + 256);
-  g_det.slab_floats = (bytes - 256) / 4;
+  g_det.ncounters = kDetCtrSets;
+  g_det.slab = (float*)((char*)buf + ctr_bytes);
+  g_det.slab_floats = (bytes - ctr_bytes) / 4;
   g_det.next = 0;
   return 0;
 }

@@ -67,47 +67,91 @@ PSX_DEV bool last_block_arrive(unsigned* counter, unsigned nblocks, unsigned cha
 // ---------------------------------------------------------------------------------------
 // Deterministic mode (psx_set_deterministic, bn.hip): a launch that produces per-channel sums
 // adds each workgroup's partial row into a row of its own of a scratch slab [rows][NS][C] —
-// exactly one add per location into zeros, so the value is exact whatever the order — and its
-// last-arriving workgroup sums the rows in a fixed order into slot row 0 of the usual
-// [PSX_STAT_SLOTS][NS][C] buffer (the other slot rows stay zero), then re-zeroes the slab and
-// its counter for the next launch. The consumers are unchanged and sum the slot rows in a fixed
-// order, so every BN statistic — and with it the whole step — is bit-reproducible. The slab
-// adds are memory-side float atomics (no release needed, as for the slots); the slab lines the
-// last workgroup reads were never cached by this launch, and kernel boundaries write back and
-// invalidate the non-coherent L2 lines of the previous launch's re-zeroing.
+// exactly one add per location into zeros, so the value is exact whatever the order. The rows
+// are then summed in a fixed order by a two-level tree:
+//   level 1: rows are grouped `group` at a time; the workgroup arriving last among a group's
+//            writers (`nper` per row: e.g. the channel tiles of a conv) sums the group's rows in
+//            row order into row g of a second slab [ngroups][NS][C] (again one add per location)
+//            and re-zeroes the group's rows and counter;
+//   level 2: the last group reducer sums the ngroups rows in order into slot row 0 of the usual
+//            [PSX_STAT_SLOTS][NS][C] buffer (the other slot rows stay zero), re-zeroes the second
+//            slab and the launch counter.
+// Groups of ~sqrt(rows) rows keep both levels short (the one-level form, one workgroup reading
+// every row, read up to 1 MB from one CU per launch; both levels are latency-bound chains of
+// dependent loads, det_rows). The consumers are
+// unchanged and sum the slot rows in a fixed order, so every BN statistic — and with it the
+// whole step — is bit-reproducible. All payload adds are memory-side float atomics (no release
+// needed, as for the slots); the slab lines a reducer reads were never cached by this launch,
+// and kernel boundaries write back and invalidate the non-coherent L2 lines of the previous
+// launch's re-zeroing.
 struct DetRed {
   float* slab;        // nullptr: deterministic mode off
-  unsigned* counter;  // zero at launch, re-zeroed by the last workgroup
-  int rows;
+  float* slab2;       // level-2 rows [ngroups][NS][C]
+  unsigned* counter;  // [0]: level 2, [1 + g]: group g; zero at launch, re-zeroed by the reducers
+  int rows, group, ngroups, nper;
 };
 
-// every workgroup of the launch calls this (block-uniformly) after its slab adds; returns true
-// in the last-arriving workgroup (after the fixed-order reduction, so an in-launch finalize of
-// the same sums can follow)
-PSX_DEV bool det_finish(const DetRed& d, int NS, int C, float* part, unsigned nblocks, unsigned char* lds) {
-  if (!last_block_arrive(d.counter, nblocks, lds)) return false;
-  const size_t stride = (size_t)NS * C;
-  for (int j = threadIdx.x; j < NS * C; j += blockDim.x) {
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int r = 0;
-    for (; r + 3 < d.rows; r += 4) {
-      s0 += d.slab[(size_t)r * stride + j];
-      s1 += d.slab[(size_t)(r + 1) * stride + j];
-      s2 += d.slab[(size_t)(r + 2) * stride + j];
-      s3 += d.slab[(size_t)(r + 3) * stride + j];
+// Fixed-order sum of rows [r0, r1) of a [rows][n] slab into dst[j] (j < n), by the whole block:
+// value j is summed by `lanes` = max(1, 256 / n) threads over interleaved row subsets (8 loads in
+// flight each: the reduction is latency-bound), combined through LDS in lane order. Every value's
+// sum has the same association for a given (r0, r1, n), whatever the launch's timing.
+// add = true: dst receives one atomic add (onto zero: exact); else a plain store. Re-zeroes the rows.
+PSX_DEV void det_rows(float* slab, int r0, int r1, int n, float* dst, bool add, float* scratch) {
+  const int lanes = n >= 256 ? 1 : 256 / n;
+  for (int jb = 0; jb < n; jb += 256) {
+    const int t = threadIdx.x, k = lanes > 1 ? t / n : 0, j = jb + (lanes > 1 ? t % n : t);
+    float acc = 0.f;
+    if (k < lanes && j < n) {
+      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      int r = r0 + k;
+      for (; r + 7 * lanes < r1; r += 8 * lanes) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] += slab[(size_t)(r + u * lanes) * n + j];
+      }
+      for (int u = 0; r < r1; r += lanes, ++u) a[u & 7] += slab[(size_t)r * n + j];
+      acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+      for (r = r0 + k; r < r1; r += lanes) slab[(size_t)r * n + j] = 0.f;
     }
-    for (; r < d.rows; ++r) s0 += d.slab[(size_t)r * stride + j];
-    part[j] = (s0 + s1) + (s2 + s3);
-    for (r = 0; r < d.rows; ++r) d.slab[(size_t)r * stride + j] = 0.f;
+    if (lanes > 1) {
+      __syncthreads();
+      if (k < lanes && j < n) scratch[k * n + (j - jb)] = acc;
+      __syncthreads();
+      if (t < n) {
+        float v = 0.f;
+        for (int q = 0; q < lanes; ++q) v += scratch[q * n + t];
+        if (add) atomicAdd(dst + t, v);
+        else dst[t] = v;
+      }
+    } else if (j < n) {
+      if (add) atomicAdd(dst + j, acc);
+      else dst[j] = acc;
+    }
   }
+}
+
+// every workgroup of the launch calls this (block-uniformly) after its slab adds into row `row`;
+// returns true in the last-arriving workgroup (after the fixed-order reduction, so an in-launch
+// finalize of the same sums can follow). lds: >= 16 + 1024 bytes of the caller's LDS.
+PSX_DEV bool det_finish(const DetRed& d, int NS, int C, float* part, int row, unsigned char* lds) {
+  const int g = row / d.group;
+  const int r0 = g * d.group, r1 = min(d.rows, r0 + d.group);
+  if (!last_block_arrive(d.counter + 1 + g, (unsigned)(d.nper * (r1 - r0)), lds)) return false;
+  float* scratch = reinterpret_cast<float*>(lds + 16);
+  const int n = NS * C;
+  det_rows(d.slab, r0, r1, n, d.slab2 + (size_t)g * n, true, scratch);
+  if (threadIdx.x == 0) __hip_atomic_store(d.counter + 1 + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!last_block_arrive(d.counter, (unsigned)d.ngroups, lds)) return false;
+  det_rows(d.slab2, 0, d.ngroups, n, part, false, scratch);
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(d.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
 
-// host: the DetRed of the next producing launch (slab rows for `rows` x NS x C sums), or a
-// disabled one when deterministic mode is off / the slab is too small (bn.hip)
-DetRed det_next(int rows, int NS, int C);
+// host: the DetRed of the next producing launch (slab rows for `rows` x NS x C sums, `nper`
+// writer workgroups per row). Deterministic mode off: a disabled one. The slab too small for
+// the launch is a hard error (bn.hip det_next aborts): a silent fall back to the atomic slots
+// would break bit-reproducibility unnoticed.
+DetRed det_next(int rows, int NS, int C, int nper = 1);
 bool det_enabled();
 
 // part: [T][2][C] slot rows (sum, sum of squares). Same math as bn_finalize_kernel (bn.hip).

@@ -184,7 +184,8 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     nk = (nr * nsx) << (a.log2_icc - 3);
     if (pix0 >= npix_c) {  // whole workgroup: this class has fewer tiles
       if (!SPLIT && a.det.slab && (a.stats || a.bpart))  // it still arrives at the launch counter
-        if (det_finish(a.det, a.bpart ? a.bns : 2, a.OC, a.bpart ? a.bpart : a.stats, gridDim.x * gridDim.y, smem) &&
+        if (det_finish(a.det, a.bpart ? a.bns : 2, a.OC, a.bpart ? a.bpart : a.stats, pix_t + cls * a.n_pix_tiles,
+                       smem) &&
             a.stats && a.fuse_fin)
           bn_finalize_block<PSX_STAT_SLOTS>(a.stats, a.fin);
       return;
@@ -768,7 +769,8 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       atomicAdd(dst + which * a.OC + oc0 + row, v);
     }
     if (a.det.slab) {
-      if (det_finish(a.det, nst, a.OC, bwd ? a.bpart : a.stats, gridDim.x * gridDim.y, smem) && st && a.fuse_fin)
+      if (det_finish(a.det, nst, a.OC, bwd ? a.bpart : a.stats, pix_t + (MODE == 3 ? cls * a.n_pix_tiles : 0), smem) &&
+          st && a.fuse_fin)
         bn_finalize_block<PSX_STAT_SLOTS>(a.stats, a.fin);
       return;
     }
@@ -879,7 +881,7 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
     atomicAdd(dst + which * OC + cgi * 8 + j, acc);
   }
   if (det.slab) {
-    if (det_finish(det, nst, OC, bwd ? bpart : stats, gridDim.x, reinterpret_cast<unsigned char*>(sred)) && stats &&
+    if (det_finish(det, nst, OC, bwd ? bpart : stats, blockIdx.x, reinterpret_cast<unsigned char*>(sred)) && stats &&
         fuse_fin)
       bn_finalize_block<PSX_STAT_SLOTS>(stats, fin);
     return;
@@ -935,7 +937,7 @@ Plan plan_for(int OC, int npix, int ksteps, bool f32 = false) {
 
 // deterministic mode: this launch's slab rows (one per pixel tile, per parity class for MODE 3)
 void with_det(Conv2Args& b, int rows) {
-  if (b.stats || b.bpart) b.det = det_next(rows, b.bpart ? b.bns : 2, b.OC);
+  if (b.stats || b.bpart) b.det = det_next(rows, b.bpart ? b.bns : 2, b.OC, b.n_oc_tiles);
 }
 
 template <typename T, int BM, int BN, int MODE, bool RES, bool SPLIT, int WGM = 2>
@@ -1033,7 +1035,7 @@ int finish_split(const Conv2Args& a, hipStream_t st) {
   if (ppb < 8) ppb = 8;
   const int grid = (a.npix + ppb - 1) / ppb;
   const size_t lds = 256 * 24 * sizeof(float);
-  DetRed det{nullptr, nullptr, 0};
+  DetRed det{};
   if (a.stats || a.bpart) det = det_next(grid, a.bpart ? a.bns : 2, a.OC);
   if (a.res)
     hipLaunchKernelGGL((conv_splitk_epilogue<T, true>), dim3(grid), dim3(256), lds, st, a.part, a.splits, a.npix,
@@ -1225,6 +1227,7 @@ int psx_wino_gemm_out(const float* V, const float* U, float* y, const float* res
   a.wW = W;
   const size_t lds = (size_t)3 * (32 + 32) * 128;
   const dim3 grid(a.n_oc_tiles * a.n_pix_tiles);
+  with_det(a, a.n_pix_tiles);
   if (res)
     hipLaunchKernelGGL((conv2_kernel<float, 32, 32, 0, true, false, 2, 0, true>), grid, dim3(256), lds, st, a);
   else

@@ -5,6 +5,8 @@
 // (reference: src/parameter_server/server.py:56-57,73-75; src/workers/worker.py:133,342) and
 // the accuracy count of evaluate_model (worker.py:324-326).
 #include "bnfin.hpp"
+#include <algorithm>
+
 #include "common.hpp"
 
 namespace psx {
@@ -150,7 +152,7 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ act, in
       atomicAdd(dst + C + c + 1, x1);
     }
   }
-  if (det.slab) det_finish(det, 2, C, bs.part, gridDim.x, reinterpret_cast<unsigned char*>(sh));
+  if (det.slab) det_finish(det, 2, C, bs.part, blockIdx.x, reinterpret_cast<unsigned char*>(sh));
 }
 
 // dW[k][c] = sum_b dlogits[b][k] * pooled[b][c]; db[k] = sum_b dlogits[b][k].
@@ -388,9 +390,10 @@ int head_fwd_bwd_t(const void* act, int B, int HW, int C, const float* fcw, cons
     return e ? -e : 0;
   }
   if (K > 1024 || C % 16 || (C > 512 && C % 512)) return -2;
-  const size_t lds = (size_t)(C + K + 64) * sizeof(float);
+  // >= 16 + 1024 bytes: the deterministic-mode reduction's flag + scratch (bnfin.hpp det_finish)
+  const size_t lds = std::max<size_t>((size_t)(C + K + 64) * sizeof(float), 1040);
   const HeadBnStats bs = (bst && dact) ? *bst : HeadBnStats{};
-  const DetRed det = bs.part ? det_next(B, 2, C) : DetRed{nullptr, nullptr, 0};
+  const DetRed det = bs.part ? det_next(B, 2, C) : DetRed{};
   if (dact)
     hipLaunchKernelGGL((head_kernel<T, true>), dim3(B), dim3(256), lds, st, (const T*)act, HW, C, fcw, fcb, K,
                        labels, pooled, dlogits, (T*)dact, loss, correct, 1.f / (float)B, bs, det);

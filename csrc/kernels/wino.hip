@@ -32,6 +32,7 @@
 //   A^T = [1 1 1 1 1 0; 0 1 -1 2 -2 0; 0 1 1 4 4 0; 0 1 -1 8 -8 1]
 #include <stdlib.h>
 
+#include "bnfin.hpp"
 #include "common.hpp"
 
 extern "C" int psx_bgemm_f32(const float* A, const float* B, float* P, const void* zero, int M, int N, int Kd, int nb,
@@ -258,9 +259,11 @@ struct WinoBwdStats {
 // rows stats[slot][2][K]; data gradient (bs.part): the BN-backward sums of the consumer BN
 // instead (what the direct dgrad epilogue fuses). Block = 64 channels x 4 tiles, one tile per
 // wave.
+// Deterministic mode (det.slab): each workgroup's sums go to slab row blockIdx.y and the launch
+// reduces the rows in a fixed order (bnfin.hpp det_finish) into slot row 0.
 __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__ P, float* __restrict__ y,
                                                        const float* __restrict__ res, float* __restrict__ stats, int T,
-                                                       int H, int W, int K, WinoBwdStats bs) {
+                                                       int H, int W, int K, WinoBwdStats bs, DetRed det) {
   __shared__ float red[3][4][64];
   const int kl = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + kl;
@@ -328,10 +331,16 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
   red[1][ty][kl] = s2;
   red[2][ty][kl] = s3;
   __syncthreads();
+  float* row = det.slab ? det.slab + (size_t)blockIdx.y * nst * K
+                        : dst + (size_t)(blockIdx.y & (PSX_STAT_SLOTS - 1)) * nst * K;
   if (threadIdx.x < 64 * nst) {
     const int which = threadIdx.x >> 6;
     const float v = red[which][0][kl] + red[which][1][kl] + red[which][2][kl] + red[which][3][kl];
-    atomicAdd(dst + (size_t)(blockIdx.y & (PSX_STAT_SLOTS - 1)) * nst * K + (size_t)which * K + k, v);
+    atomicAdd(row + (size_t)which * K + k, v);
+  }
+  if (det.slab) {
+    __syncthreads();  // red[] is reused as the hand-off flag
+    det_finish(det, nst, K, dst, blockIdx.y, reinterpret_cast<unsigned char*>(&red[0][0][0]));
   }
 }
 
@@ -530,8 +539,10 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
   if (e) return e;
   WinoBwdStats bs{};
   if (bst) bs = *bst;
+  DetRed det{};
+  if (bst || stats) det = det_next(gy, bst ? (bst->y2 ? 3 : 2) : 2, K, K / 64);
   hipLaunchKernelGGL(wino_out_kernel, dim3(K / 64, gy), dim3(256), 0, st, P, y, res, bst ? nullptr : stats, T, H, W,
-                     K, bs);
+                     K, bs, det);
   return (int)hipGetLastError();
 }
 

@@ -29,10 +29,28 @@
 //             against the caller's stream by events.
 //
 // Checkpoints (--ckpt-every): after the apply that reaches a multiple of the period the loop
-// synchronises the update stream and calls back into the host (ParameterServer.maybe_checkpoint).
-// The loop ends when the expected number of workers finished (or were declared dead) and no
-// receive is pending, or on STOP. Kernels and runtime functions are bound by dlsym from the
-// already-loaded psx libraries (paths passed by the caller).
+// waits for that apply (an event on the update stream) and calls back into the host
+// (ParameterServer.maybe_checkpoint). The loop thread runs in relaxed stream-capture mode, so
+// neither that wait nor its other runtime calls invalidate a HIP graph the co-located worker
+// captures on another thread.
+//
+// Failures (the reference tolerates leaving / failing workers: JobFinished server.py:306-318,
+// keepalive :375-377). A remote worker is dropped when
+//   * its heartbeats stop (--heartbeat-timeout, the native core's timeouts),
+//   * one of its transfers is still in flight --transfer-timeout s after it was posted,
+//   * it sends no request for --stall-timeout s (alive but stalled: heartbeats alone never
+//     notice a hung training loop),
+//   * a transfer on its communicator fails.
+// Dropping w aborts its pair communicator when a receive or snapshot send is in flight
+// (ncclCommAbort: what unblocks RCCL kernels waiting on a dead peer), discards its pending
+// receive, marks it dead in the core (the wait-for-N barrier and the end-of-job count go on
+// without it) and answers its later requests with R_DROPPED. The other workers keep being
+// served; SERVER_FINAL_METRICS reports dead_workers.
+//
+// The loop ends when the expected number of workers finished or were dropped and no receive is
+// pending, or on STOP. Every HIP runtime call is checked (a failure ends the loop with an
+// error). Kernels and runtime functions are bound by dlsym from the already-loaded psx
+// libraries (paths passed by the caller).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -51,7 +69,7 @@ namespace {
 
 // mailbox message types (parallel/control.py)
 enum { HELLO = 1, PUSH = 2, FETCH = 3, DONE = 4, HEARTBEAT = 5, STOP = 6 };
-enum { R_REGISTERED = 11, R_PUSHED = 12, R_FETCHED = 13, R_ACK = 14 };
+enum { R_REGISTERED = 11, R_PUSHED = 12, R_FETCHED = 13, R_ACK = 14, R_DROPPED = 15 };
 enum { PSX_APPLY = 1 };
 
 struct Rt {  // libpsx_runtime.so + libpsx_kernels.so entry points
@@ -63,6 +81,7 @@ struct Rt {  // libpsx_runtime.so + libpsx_kernels.so entry points
   int (*ps_on_push)(void*, int, long long, double, float*, int*, long long*);
   void (*ps_on_applied)(void*, double);
   int (*ps_job_finished)(void*, int);
+  int (*ps_mark_dead)(void*, int);
   int (*ps_check_timeouts)(void*, double, double, int*, int);
   long long (*ps_global_step)(void*);
   int (*sgd_apply)(float*, const void*, float*, long, float, float, float, float, int, int, void*, hipStream_t);
@@ -118,6 +137,9 @@ struct PsxLoopCfg {  // mirrored by parallel/native_loop.py (ctypes.Structure)
   int own_upd_stream;
   long long ckpt_every;
   int (*ckpt_cb)(long long global_step);  // host checkpoint hook (nullptr: none)
+  const int* comm_owned;   // worker id -> 1: comms[w] is w's own pair communicator (abortable)
+  double transfer_timeout;  // s, 0 = off: a receive / snapshot send in flight longer drops the worker
+  double stall_timeout;     // s, 0 = off: a remote worker without any request that long is dropped
 };
 
 struct PsxLoop {
@@ -137,12 +159,22 @@ struct PsxLoop {
   std::vector<uint16_t*> snap_img;
   std::vector<float*> snap_small;  // fp32 remainder (bf16conv) or the whole arena (fp32 fetch)
   std::vector<hipEvent_t> sent;  // per worker: last snapshot send done (snapshot reusable)
+  std::vector<double> sent_t;    // per worker: when that send was posted
   struct Pending {
     int wid;
     long long local_step;
     hipEvent_t ev;
+    double t_post;
   };
   std::deque<Pending> pending;
+  struct WState {
+    bool seen = false;      // registered through the mailbox (a remote worker)
+    bool finished = false;  // counted towards `expected` (DONE or dropped)
+    bool dead = false;      // dropped
+    bool aborted = false;   // its pair communicator was aborted
+    double last_req = 0;
+  };
+  std::vector<WState> ws;
   int finished = 0;
   long long applies = 0;
 };
@@ -150,6 +182,25 @@ struct PsxLoop {
 namespace {
 
 size_t gbytes(const PsxLoop* L) { return (size_t)L->c.n_params * (L->c.grad_fp16 ? 2 : 4); }
+
+// HIP runtime calls of the loop: a failure is recorded (first one wins) and ends the loop
+#define PSX_HIP(L, call)                                                                          \
+  do {                                                                                            \
+    const hipError_t e_ = (call);                                                                 \
+    if (e_ != hipSuccess) {                                                                       \
+      fprintf(stderr, "psx event loop: %s failed: %s\n", #call, hipGetErrorString(e_));           \
+      if (!(L)->err) (L)->err = -50;                                                              \
+    }                                                                                             \
+  } while (0)
+
+// a is ordered after everything enqueued on b so far (a transient event)
+void stream_after(PsxLoop* L, hipStream_t a, hipStream_t b) {
+  hipEvent_t ev;
+  PSX_HIP(L, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  PSX_HIP(L, hipEventRecord(ev, b));
+  PSX_HIP(L, hipStreamWaitEvent(a, ev, 0));
+  PSX_HIP(L, hipEventDestroy(ev));
+}
 
 int alloc_worker(PsxLoop* L, int w) {
   if (L->slot[w]) return 0;
@@ -160,11 +211,12 @@ int alloc_worker(PsxLoop* L, int w) {
   const long nsmall = L->c.fetch_fp32 ? L->c.arena_numel : std::max(1L, L->c.small_n);
   if (hipMalloc((void**)&L->snap_small[w], (size_t)nsmall * 4) != hipSuccess) return -22;
   if (hipEventCreateWithFlags(&L->sent[w], hipEventDisableTiming) != hipSuccess) return -23;
-  hipEventRecord(L->sent[w], L->s_comm[w]);
+  if (hipEventRecord(L->sent[w], L->s_comm[w]) != hipSuccess) return -23;
   return 0;
 }
 
-// the fused SGD apply of one gradient with the core's weight, writing the bf16 image too
+// the fused SGD apply of one gradient with the core's weight (+ the bf16 image of the updated
+// state when the fetch payload carries it; the fp32 fetch never reads one)
 int apply(PsxLoop* L, const void* g, float weight) {
   const double t0 = now_s();
   const int e = L->rt.sgd_apply(L->c.arena, g, L->c.mom_buf, L->c.n_params, L->c.lr, weight, L->c.momentum,
@@ -175,29 +227,66 @@ int apply(PsxLoop* L, const void* g, float weight) {
   if (!e && L->c.ckpt_cb && L->c.ckpt_every > 0) {
     const long long gs = L->rt.ps_global_step(L->c.core);
     if (gs % L->c.ckpt_every == 0) {
-      hipStreamSynchronize(L->s_upd);  // the checkpoint reads the arena from another stream
+      // the checkpoint reads the arena from another stream: wait for this apply only (an event,
+      // not a stream synchronize)
+      hipEvent_t ev;
+      PSX_HIP(L, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      PSX_HIP(L, hipEventRecord(ev, L->s_upd));
+      PSX_HIP(L, hipEventSynchronize(ev));
+      PSX_HIP(L, hipEventDestroy(ev));
       if (L->c.ckpt_cb(gs)) return -32;
     }
   }
   return e;
 }
 
+bool in_flight(PsxLoop* L, int w) {
+  for (const auto& p : L->pending)
+    if (p.wid == w) return true;
+  return L->sent[w] && hipEventQuery(L->sent[w]) == hipErrorNotReady;
+}
+
+// Drop worker w (see the header): abort its pair communicator if a transfer is in flight, discard
+// its pending receive, mark it dead in the core, count it as finished.
+void drop_worker(PsxLoop* L, int w, const char* why, bool core_marked = false) {
+  PsxLoop::WState& s = L->ws[w];
+  if (s.dead) return;
+  s.dead = true;
+  const bool busy = in_flight(L, w);
+  fprintf(stderr, "[psx native loop] worker %d %s: dropped%s; serving the others\n", w, why,
+          busy && L->c.comm_owned && L->c.comm_owned[w] ? " (pair communicator aborted)" : "");
+  if (busy && L->c.comm_owned && L->c.comm_owned[w] && L->c.comms[w]) {
+    psx_comm_abort(L->c.comms[w]);  // RCCL kernels waiting on the dead peer exit
+    s.aborted = true;
+  }
+  for (auto it = L->pending.begin(); it != L->pending.end();) {
+    if (it->wid == w) {
+      hipEventDestroy(it->ev);  // never waited on: the update stream does not depend on it
+      it = L->pending.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  if (!core_marked) L->rt.ps_mark_dead(L->c.core, w);
+  if (!s.finished) {
+    s.finished = true;
+    ++L->finished;
+  }
+}
+
 int serve_fetch(PsxLoop* L, int w, int rank) {
   if (int e = alloc_worker(L, w)) return e;
   // snapshot on the update stream (after every apply so far), once the previous send of this
   // worker's snapshot has finished
-  hipStreamWaitEvent(L->s_upd, L->sent[w], 0);
+  PSX_HIP(L, hipStreamWaitEvent(L->s_upd, L->sent[w], 0));
   if (L->c.fetch_fp32) {
-    hipMemcpyAsync(L->snap_small[w], L->c.arena, (size_t)L->c.arena_numel * 4, hipMemcpyDeviceToDevice, L->s_upd);
+    PSX_HIP(L, hipMemcpyAsync(L->snap_small[w], L->c.arena, (size_t)L->c.arena_numel * 4, hipMemcpyDeviceToDevice,
+                              L->s_upd));
   } else {
-    hipMemcpyAsync(L->snap_img[w], L->img, (size_t)L->c.n_params * 2, hipMemcpyDeviceToDevice, L->s_upd);
+    PSX_HIP(L, hipMemcpyAsync(L->snap_img[w], L->img, (size_t)L->c.n_params * 2, hipMemcpyDeviceToDevice, L->s_upd));
     if (L->c.small_n) L->rt.gather_f32(L->c.arena, L->c.small_idx, L->c.small_n, L->snap_small[w], L->s_upd);
   }
-  hipEvent_t ready;
-  hipEventCreateWithFlags(&ready, hipEventDisableTiming);
-  hipEventRecord(ready, L->s_upd);
-  hipStreamWaitEvent(L->s_comm[w], ready, 0);
-  hipEventDestroy(ready);
+  stream_after(L, L->s_comm[w], L->s_upd);
   void* comm = L->c.comms[w];
   int e;
   if (L->c.fetch_fp32) {
@@ -206,7 +295,8 @@ int serve_fetch(PsxLoop* L, int w, int rank) {
     e = psx_comm_send(comm, L->snap_img[w], L->c.n_params, PSX_BF16, rank, L->s_comm[w]);
     if (!e && L->c.small_n) e = psx_comm_send(comm, L->snap_small[w], L->c.small_n, PSX_F32, rank, L->s_comm[w]);
   }
-  hipEventRecord(L->sent[w], L->s_comm[w]);
+  PSX_HIP(L, hipEventRecord(L->sent[w], L->s_comm[w]));
+  L->sent_t[w] = now_s();
   return e;
 }
 
@@ -215,18 +305,38 @@ int post_recv(PsxLoop* L, int w, int rank, long long local_step) {
   // the slot is free: its previous gradient was applied on s_upd before this worker could push
   // again (the worker waits for the reply, which follows the apply's enqueue) -> order the
   // receive after the update stream
-  hipEvent_t upd;
-  hipEventCreateWithFlags(&upd, hipEventDisableTiming);
-  hipEventRecord(upd, L->s_upd);
-  hipStreamWaitEvent(L->s_comm[w], upd, 0);
-  hipEventDestroy(upd);
+  stream_after(L, L->s_comm[w], L->s_upd);
   const int e = psx_comm_recv(L->c.comms[w], L->slot[w], L->c.n_params, L->c.grad_fp16 ? PSX_F16 : PSX_F32, rank,
                               L->s_comm[w]);
+  if (e) return e;
   hipEvent_t ev;
-  hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-  hipEventRecord(ev, L->s_comm[w]);
-  L->pending.push_back({w, local_step, ev});
-  return e;
+  PSX_HIP(L, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  PSX_HIP(L, hipEventRecord(ev, L->s_comm[w]));
+  L->pending.push_back({w, local_step, ev, now_s()});
+  return 0;
+}
+
+// deadlines of in-flight transfers and silent workers
+void check_deadlines(PsxLoop* L, double t) {
+  if (L->c.transfer_timeout > 0) {
+    for (size_t i = 0; i < L->pending.size(); ++i) {
+      const PsxLoop::Pending p = L->pending[i];
+      if (t - p.t_post > L->c.transfer_timeout && hipEventQuery(p.ev) == hipErrorNotReady) {
+        drop_worker(L, p.wid, "gradient receive overdue (--transfer-timeout)");
+        i = (size_t)-1;  // the deque changed: rescan
+      }
+    }
+    for (int w = 0; w < L->c.max_wid; ++w)
+      if (!L->ws[w].dead && L->sent[w] && t - L->sent_t[w] > L->c.transfer_timeout &&
+          hipEventQuery(L->sent[w]) == hipErrorNotReady)
+        drop_worker(L, w, "snapshot send overdue (--transfer-timeout)");
+  }
+  if (L->c.stall_timeout > 0)
+    for (int w = 0; w < L->c.max_wid; ++w) {
+      const PsxLoop::WState& s = L->ws[w];
+      if (s.seen && !s.finished && t - s.last_req > L->c.stall_timeout)
+        drop_worker(L, w, "sent no request (--stall-timeout)");
+    }
 }
 
 void complete_pending(PsxLoop* L) {
@@ -234,9 +344,15 @@ void complete_pending(PsxLoop* L) {
   // the others (each worker has at most one push in flight: it waits for the reply)
   for (auto it = L->pending.begin(); it != L->pending.end();) {
     PsxLoop::Pending& p = *it;
-    if (hipEventQuery(p.ev) != hipSuccess) {
+    const hipError_t q = hipEventQuery(p.ev);
+    if (q == hipErrorNotReady) {
       ++it;
       continue;
+    }
+    if (q != hipSuccess) {
+      fprintf(stderr, "psx event loop: receive event of worker %d: %s\n", p.wid, hipGetErrorString(q));
+      if (!L->err) L->err = -50;
+      return;
     }
     float weight = 0.f;
     int ncontrib = 0;
@@ -244,13 +360,13 @@ void complete_pending(PsxLoop* L) {
     const int d = L->rt.ps_on_push(L->c.core, p.wid, p.local_step, now_s(), &weight, &ncontrib, &st);
     int accepted = 0;
     if (d == PSX_APPLY) {
-      hipStreamWaitEvent(L->s_upd, p.ev, 0);
+      PSX_HIP(L, hipStreamWaitEvent(L->s_upd, p.ev, 0));
       if (apply(L, L->slot[p.wid], weight)) L->err = -30;
       accepted = 1;
     }
     L->rt.mbox_reply(L->c.mbox, L->c.remote_rank[p.wid], R_PUSHED, p.wid, accepted,
                      L->rt.ps_global_step(L->c.core), st);
-    hipEventDestroy(p.ev);
+    PSX_HIP(L, hipEventDestroy(p.ev));
     it = L->pending.erase(it);
   }
 }
@@ -262,8 +378,6 @@ void serve_local(PsxLoop* L) {
     q.swap(L->local);
   }
   for (LocalReq* r : q) {
-    hipEvent_t ev;
-    hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (r->kind == 0) {  // push: the caller's gradient is ready at this point of its stream
       float weight = 0.f;
       int ncontrib = 0;
@@ -271,36 +385,27 @@ void serve_local(PsxLoop* L) {
       const int d = L->rt.ps_on_push(L->c.core, r->wid, r->local_step, now_s(), &weight, &ncontrib, &st);
       const bool same = r->stream == L->s_upd;
       if (d == PSX_APPLY) {
-        if (!same) {
-          hipEventRecord(ev, r->stream);
-          hipStreamWaitEvent(L->s_upd, ev, 0);
-        }
+        if (!same) stream_after(L, L->s_upd, r->stream);
         if (apply(L, r->grads, weight)) L->err = -31;
         r->accepted = 1;
       }
       r->staleness = st;
       r->global_step = L->rt.ps_global_step(L->c.core);
-      if (!same) {  // the caller's stream waits: its gradient buffer is free again
-        hipEventRecord(ev, L->s_upd);
-        hipStreamWaitEvent(r->stream, ev, 0);
-      }
+      if (!same) stream_after(L, r->stream, L->s_upd);  // the caller's gradient buffer is free again
     } else if (r->kind == 1) {  // fetch: fp32 arena copy, ordered after every apply so far
       r->global_step = L->rt.ps_on_fetch(L->c.core, r->wid, now_s());
       const bool same = r->stream == L->s_upd;
-      if (!same) {
-        hipEventRecord(ev, r->stream);
-        hipStreamWaitEvent(L->s_upd, ev, 0);
-      }
-      hipMemcpyAsync(r->dst, L->c.arena, (size_t)L->c.arena_numel * 4, hipMemcpyDeviceToDevice, L->s_upd);
-      if (!same) {
-        hipEventRecord(ev, L->s_upd);
-        hipStreamWaitEvent(r->stream, ev, 0);
-      }
+      if (!same) stream_after(L, L->s_upd, r->stream);
+      PSX_HIP(L, hipMemcpyAsync(r->dst, L->c.arena, (size_t)L->c.arena_numel * 4, hipMemcpyDeviceToDevice,
+                                L->s_upd));
+      if (!same) stream_after(L, r->stream, L->s_upd);
     } else {
       L->rt.ps_job_finished(L->c.core, r->wid);
-      ++L->finished;
+      if (!L->ws[r->wid].finished) {
+        L->ws[r->wid].finished = true;
+        ++L->finished;
+      }
     }
-    hipEventDestroy(ev);
     {
       std::lock_guard<std::mutex> lk(L->mu);
       r->done = true;
@@ -310,45 +415,78 @@ void serve_local(PsxLoop* L) {
 }
 
 void run(PsxLoop* L) {
-  hipSetDevice(L->c.device);
+  PSX_HIP(L, hipSetDevice(L->c.device));
+  // relaxed capture mode: this thread's runtime calls (event waits, allocations, the checkpoint
+  // callback's copies) never invalidate a graph capture of the co-located worker's thread
+  hipStreamCaptureMode cm = hipStreamCaptureModeRelaxed;
+  PSX_HIP(L, hipThreadExchangeStreamCaptureMode(&cm));
   if (L->c.own_upd_stream)
-    hipStreamCreateWithFlags(&L->s_upd, hipStreamNonBlocking);
+    PSX_HIP(L, hipStreamCreateWithFlags(&L->s_upd, hipStreamNonBlocking));
   else
     L->s_upd = L->c.upd_stream;
-  // initial bf16 image of the state: an lr-0 apply of a zero gradient writes bf16(p) exactly
-  void* zero = nullptr;
-  hipMalloc((void**)&L->img, (size_t)L->c.n_params * 2);
-  hipMalloc(&zero, gbytes(L));
-  hipMemsetAsync(zero, 0, gbytes(L), L->s_upd);
-  L->rt.sgd_apply(L->c.arena, zero, nullptr, L->c.n_params, 0.f, 1.f, 0.f, 0.f, 0, L->c.grad_fp16, L->img, L->s_upd);
-  // (lr 0, no momentum buffer: the state is untouched)
-  hipStreamSynchronize(L->s_upd);
-  hipFree(zero);
+  if (!L->c.fetch_fp32) {
+    // initial bf16 image of the state: an lr-0 apply of a zero gradient writes bf16(p) exactly
+    // (lr 0, no momentum buffer: the state is untouched). The fp32 fetch has no image.
+    void* zero = nullptr;
+    PSX_HIP(L, hipMalloc((void**)&L->img, (size_t)L->c.n_params * 2));
+    PSX_HIP(L, hipMalloc(&zero, gbytes(L)));
+    PSX_HIP(L, hipMemsetAsync(zero, 0, gbytes(L), L->s_upd));
+    if (!L->err && L->rt.sgd_apply(L->c.arena, zero, nullptr, L->c.n_params, 0.f, 1.f, 0.f, 0.f, 0, L->c.grad_fp16,
+                                   L->img, L->s_upd))
+      L->err = -33;
+    PSX_HIP(L, hipStreamSynchronize(L->s_upd));
+    PSX_HIP(L, hipFree(zero));
+  }
   double last_to = now_s();
   std::vector<int> dead(L->c.max_wid + 1);
   long long m[6];
-  for (;;) {
+  bool need_drain = false;  // a long iteration happened: drain the mailbox before any timeout check
+  while (!L->err) {
+    const double t_iter = now_s();
     const int got = L->rt.mbox_recv(L->c.mbox, m, L->c.poll_s);
     if (got > 0) {
       const int type = (int)m[0], src = (int)m[1], wid = (int)m[2];
       const bool known = wid >= 0 && wid < L->c.max_wid;
-      if (type == HELLO) {
+      const double t = now_s();
+      if (known && type != HEARTBEAT) L->ws[wid].last_req = t;
+      if (type == HELLO && known && L->ws[wid].dead) {
+        L->rt.mbox_reply(L->c.mbox, src, R_DROPPED, wid, 0, 0, 0);  // a dropped id does not come back
+      } else if (type == HELLO) {
         char name[32];
         snprintf(name, sizeof name, "rank%d", src);
-        const int id = L->rt.ps_register(L->c.core, name, wid, now_s());
+        const int id = L->rt.ps_register(L->c.core, name, wid, t);
+        if (id >= 0 && id < L->c.max_wid) {
+          L->ws[id].seen = true;
+          L->ws[id].last_req = t;
+        }
         L->rt.mbox_reply(L->c.mbox, src, R_REGISTERED, id, L->c.expected, 0, 0);
+      } else if (known && L->ws[wid].dead && type != HEARTBEAT) {
+        // a dropped worker (e.g. one that stalled past --stall-timeout and woke up): no transfer
+        // is posted for it any more; DONE is acknowledged, everything else refused
+        L->rt.mbox_reply(L->c.mbox, L->c.remote_rank[wid], type == DONE ? R_ACK : R_DROPPED, wid, 0,
+                         L->rt.ps_global_step(L->c.core), 0);
       } else if (type == FETCH && known) {
-        const long long gs = L->rt.ps_on_fetch(L->c.core, wid, now_s());
-        if (int e = serve_fetch(L, wid, L->c.comm_peer[wid])) L->err = e;
-        L->rt.mbox_reply(L->c.mbox, L->c.remote_rank[wid], R_FETCHED, wid, 0, gs, 0);
+        const long long gs = L->rt.ps_on_fetch(L->c.core, wid, t);
+        if (int e = serve_fetch(L, wid, L->c.comm_peer[wid])) {
+          drop_worker(L, wid, "snapshot send failed");
+          L->rt.mbox_reply(L->c.mbox, L->c.remote_rank[wid], R_DROPPED, wid, e, gs, 0);
+        } else {
+          L->rt.mbox_reply(L->c.mbox, L->c.remote_rank[wid], R_FETCHED, wid, 0, gs, 0);
+        }
       } else if (type == PUSH && known) {
-        if (int e = post_recv(L, wid, L->c.comm_peer[wid], m[4])) L->err = e;
+        if (int e = post_recv(L, wid, L->c.comm_peer[wid], m[4])) {
+          drop_worker(L, wid, "gradient receive failed");
+          L->rt.mbox_reply(L->c.mbox, L->c.remote_rank[wid], R_DROPPED, wid, e, L->rt.ps_global_step(L->c.core), 0);
+        }
       } else if (type == DONE && known) {
         L->rt.ps_job_finished(L->c.core, wid);
-        ++L->finished;
+        if (!L->ws[wid].finished) {
+          L->ws[wid].finished = true;
+          ++L->finished;
+        }
         L->rt.mbox_reply(L->c.mbox, L->c.remote_rank[wid], R_ACK, wid, 0, 0, 0);
       } else if (type == HEARTBEAT && known) {
-        L->rt.ps_heartbeat(L->c.core, wid, now_s());
+        L->rt.ps_heartbeat(L->c.core, wid, t);
       } else if (type == STOP) {
         break;
       }
@@ -356,16 +494,26 @@ void run(PsxLoop* L) {
     complete_pending(L);
     serve_local(L);
     const double t = now_s();
-    if (L->c.heartbeat_timeout > 0 && t - last_to > 1.0) {
+    // after a long iteration (a blocking transfer call) the live workers' queued heartbeats and
+    // requests are seen first: no timeout check until the mailbox has been drained once
+    if (t - t_iter > 0.5) need_drain = true;
+    if (got <= 0) need_drain = false;
+    if (!need_drain && t - last_to > 0.25) {
       last_to = t;
-      L->finished += L->rt.ps_check_timeouts(L->c.core, t, L->c.heartbeat_timeout, dead.data(), L->c.max_wid);
+      if (L->c.heartbeat_timeout > 0) {
+        const int n = L->rt.ps_check_timeouts(L->c.core, t, L->c.heartbeat_timeout, dead.data(), L->c.max_wid);
+        for (int i = 0; i < n && i < L->c.max_wid; ++i)
+          if (dead[i] >= 0 && dead[i] < L->c.max_wid) drop_worker(L, dead[i], "missed heartbeats", true);
+      }
+      check_deadlines(L, t);
     }
     if (L->finished >= L->c.expected && L->pending.empty()) break;
-    if (L->err) break;
   }
-  for (hipStream_t s : L->s_comm)
-    if (s) hipStreamSynchronize(s);
-  hipStreamSynchronize(L->s_upd);
+  // drain: the communication streams of live workers (a dropped worker's stream may hold a
+  // transfer its aborted communicator never completes), then the update stream
+  for (size_t w = 0; w < L->s_comm.size(); ++w)
+    if (L->s_comm[w] && !L->ws[w].dead) PSX_HIP(L, hipStreamSynchronize(L->s_comm[w]));
+  PSX_HIP(L, hipStreamSynchronize(L->s_upd));
   {
     std::lock_guard<std::mutex> lk(L->mu);
     L->stopped = true;
@@ -396,7 +544,7 @@ void* psx_loop_create(const PsxLoopCfg* cfg, const char* runtime_path, const cha
                   bind(rt, "psx_ps_register", &r.ps_register) && bind(rt, "psx_ps_heartbeat", &r.ps_heartbeat) &&
                   bind(rt, "psx_ps_on_fetch", &r.ps_on_fetch) && bind(rt, "psx_ps_on_push", &r.ps_on_push) &&
                   bind(rt, "psx_ps_on_applied", &r.ps_on_applied) &&
-                  bind(rt, "psx_ps_job_finished", &r.ps_job_finished) &&
+                  bind(rt, "psx_ps_job_finished", &r.ps_job_finished) && bind(rt, "psx_ps_mark_dead", &r.ps_mark_dead) &&
                   bind(rt, "psx_ps_check_timeouts", &r.ps_check_timeouts) &&
                   bind(rt, "psx_ps_global_step", &r.ps_global_step) && bind(kn, "psx_sgd_apply", &r.sgd_apply) &&
                   bind(kn, "psx_gather_f32", &r.gather_f32);
@@ -410,6 +558,8 @@ void* psx_loop_create(const PsxLoopCfg* cfg, const char* runtime_path, const cha
   L->snap_img.assign(n, nullptr);
   L->snap_small.assign(n, nullptr);
   L->sent.assign(n, nullptr);
+  L->sent_t.assign(n, 0.0);
+  L->ws.assign(n, PsxLoop::WState{});
   return L;
 }
 
@@ -427,6 +577,22 @@ int psx_loop_join(void* h) {
 }
 
 long long psx_loop_applies(void* h) { return ((PsxLoop*)h)->applies; }
+
+// After join: the dropped workers (ids into out[cap]) and, per id, whether their pair
+// communicator was aborted by the loop (aborted[cap], nullable: the caller must not destroy it).
+int psx_loop_dropped(void* h, int* out, int* aborted, int cap) {
+  PsxLoop* L = (PsxLoop*)h;
+  int n = 0;
+  for (size_t w = 0; w < L->ws.size(); ++w)
+    if (L->ws[w].dead) {
+      if (n < cap) {
+        out[n] = (int)w;
+        if (aborted) aborted[n] = L->ws[w].aborted ? 1 : 0;
+      }
+      ++n;
+    }
+  return n;
+}
 
 static int local_call(PsxLoop* L, LocalReq* r) {
   {
@@ -470,13 +636,20 @@ void psx_loop_destroy(void* h) {
   if (!L) return;
   if (L->th.joinable()) L->th.join();
   for (size_t w = 0; w < L->slot.size(); ++w) {
+    if (L->ws[w].dead && L->s_comm[w] && hipStreamQuery(L->s_comm[w]) == hipErrorNotReady) {
+      // a dropped worker's transfer never completed: keep its buffers (a late kernel may still
+      // touch them) rather than free memory under it
+      fprintf(stderr, "[psx native loop] worker %d: transfer still pending at teardown; buffers kept\n", (int)w);
+      continue;
+    }
     if (L->slot[w]) hipFree(L->slot[w]);
     if (L->snap_img[w]) hipFree(L->snap_img[w]);
     if (L->snap_small[w]) hipFree(L->snap_small[w]);
     if (L->sent[w]) hipEventDestroy(L->sent[w]);
   }
-  for (hipStream_t s : L->s_comm)
-    if (s) hipStreamDestroy(s);
+  for (size_t w = 0; w < L->s_comm.size(); ++w)
+    if (L->s_comm[w] && !(L->ws[w].dead && hipStreamQuery(L->s_comm[w]) == hipErrorNotReady))
+      hipStreamDestroy(L->s_comm[w]);
   if (L->img) hipFree(L->img);
   if (L->s_upd && L->c.own_upd_stream) hipStreamDestroy(L->s_upd);
   delete L;

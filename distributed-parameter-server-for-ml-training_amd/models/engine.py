@@ -367,7 +367,8 @@ class HipResNetEngine:
                 oh, ow = cs.out_hw
                 need = max(need, (B * oh * ow // 8 + 64) * 3 * cs.cout, (B * cs.h * cs.w // 8 + 64) * 3 * cs.cp)
             need = max(need, 3 * 1024 * max(b.convs[-1].cout for b in sp.blocks), B * 2 * sp.fc_in)
-            self.det_buf = torch.zeros(64 + need, dtype=torch.float32, device=self.dev)
+            # [64 x 256 launch counters | level-1 rows | level-2 group rows] (bnfin.hpp DetRed)
+            self.det_buf = torch.zeros(16384 + 2 * need, dtype=torch.float32, device=self.dev)
         self.wpart = self._f32(max(1, max_wg))
         self.wpart_w = self._f32(max(1, self._plan_wpart(max_wp)))
         self._plan_wino()
@@ -395,12 +396,13 @@ class HipResNetEngine:
         per-layer A/B in profiles/r2s4_wino_*.jsonl. Per layer: the transformed forward weights
         U [cout][36][cin] and data-gradient weights U' [cin][36][cout] (rebuilt by unpack() every
         step) and, where the weight gradient is Winograd, the transformed input V [36][T][cin] the
-        forward leaves for it. Not in deterministic mode (its BN sums are slot atomics) and not for
-        bf16. PSX_WINO=0: direct kernels everywhere."""
+        forward leaves for it. In deterministic mode its BN sums take the fixed-order reduction
+        like every other producer (wino_out_kernel + bnfin.hpp DetRed). Not for bf16. PSX_WINO=0:
+        direct kernels everywhere."""
         self.wino_layers = {}
         self.wino_wgrad = set()
         self.wino_bnfold = {}
-        if not self.f32 or self.deterministic or os.environ.get("PSX_WINO", "1") == "0":
+        if not self.f32 or os.environ.get("PSX_WINO", "1") == "0":
             return
         maxhw = int(os.environ.get("PSX_WINO_MAXHW", "64"))
         wg = os.environ.get("PSX_WINO_WGRAD", "1") == "1"

@@ -25,10 +25,15 @@ from ..ops._lib import runtime
 # request types (worker -> server)
 HELLO, PUSH, FETCH, DONE, HEARTBEAT, STOP = 1, 2, 3, 4, 5, 6
 # reply types (server -> worker)
-R_REGISTERED, R_PUSHED, R_FETCHED, R_ACK = 11, 12, 13, 14
+R_REGISTERED, R_PUSHED, R_FETCHED, R_ACK, R_DROPPED = 11, 12, 13, 14, 15
 
 NAMES = {HELLO: "HELLO", PUSH: "PUSH", FETCH: "FETCH", DONE: "DONE", HEARTBEAT: "HEARTBEAT", STOP: "STOP",
-         R_REGISTERED: "REGISTERED", R_PUSHED: "PUSHED", R_FETCHED: "FETCHED", R_ACK: "ACK"}
+         R_REGISTERED: "REGISTERED", R_PUSHED: "PUSHED", R_FETCHED: "FETCHED", R_ACK: "ACK", R_DROPPED: "DROPPED"}
+
+
+class WorkerDropped(RuntimeError):
+    """The server declared this worker dead (missed heartbeats, an overdue transfer, a stall) and
+    refuses its requests (R_DROPPED): the worker ends its training loop."""
 
 
 class Msg(tuple):

@@ -127,8 +127,9 @@ class WatchedRounds:
         return bool(getattr(self.t, "native", False))
 
     def _guard(self, fn, *a, event=False):
-        """Bracket the host call; with ``event`` (native transport push) completion is an event
-        recorded after its stream-ordered collectives."""
+        """Bracket the host call; with ``event`` (native transport: the collectives are
+        stream-ordered, the host does not wait for them) completion is ``_round_event()``, an
+        event that completes only when the device has finished the call's collectives."""
         wd = self.watchdog
         if wd is None:
             return fn(*a)
@@ -137,16 +138,25 @@ class WatchedRounds:
         try:
             r = fn(*a)
             if event:
-                import torch
-
-                ev = torch.cuda.Event()
-                ev.record()
+                ev = self._round_event()
             return r
         finally:
             wd.end(ev)
 
+    def _round_event(self):
+        """Event after the last collective the call issued: by default they are all on the
+        current (compute) stream; channels that issue them on a communication stream the compute
+        stream does not wait for (OverlapSyncChannel) record it there."""
+        import torch
+
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev
+
     def fetch(self, worker_id, local_arena):
-        return self._guard(self._fetch, worker_id, local_arena)
+        # native transport: the broadcast is stream-ordered too (ADVICE r2: a fetch stuck on a dead
+        # peer must not count as a finished round)
+        return self._guard(self._fetch, worker_id, local_arena, event=self._native())
 
     def push(self, worker_id, grads, local_step, buffers=None):
         return self._guard(self._push, worker_id, grads, local_step, buffers, event=self._native())

@@ -42,7 +42,8 @@ class LoopCfg(C.Structure):
                 ("momentum", f32), ("weight_decay", f32), ("device", i32), ("grad_fp16", i32), ("max_wid", i32),
                 ("expected", i32), ("fetch_fp32", i32), ("mom_first", i32), ("mom_buf", vp),
                 ("heartbeat_timeout", f64), ("poll_s", f64), ("upd_stream", vp), ("own_upd_stream", i32),
-                ("ckpt_every", C.c_longlong), ("ckpt_cb", CKPT_CB)]
+                ("ckpt_every", C.c_longlong), ("ckpt_cb", CKPT_CB), ("comm_owned", vp), ("transfer_timeout", f64),
+                ("stall_timeout", f64)]
 
 
 _SIGS = {
@@ -51,6 +52,7 @@ _SIGS = {
     "psx_loop_start": (i32, [vp]),
     "psx_loop_join": (i32, [vp]),
     "psx_loop_applies": (C.c_longlong, [vp]),
+    "psx_loop_dropped": (i32, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), i32]),
     "psx_loop_local_push": (i32, [vp, i32, vp, C.c_longlong, vp, C.POINTER(C.c_longlong)]),
     "psx_loop_local_fetch": (C.c_longlong, [vp, i32, vp, vp]),
     "psx_loop_local_done": (i32, [vp, i32]),
@@ -85,17 +87,27 @@ class NativeServerLoop:
         workers only). update_stream: the co-located worker's compute stream (its pushes/fetches
         are then in plain stream order with the loop's updates); None = the loop creates its own."""
         self.server = server
+        self.t = transport
+        self.rank_of_wid = dict(rank_of_wid)
         lay = server.layout
         cfg = server.cfg
         self.small_idx = small_index_of(lay).to(server.device)
         max_wid = max([expected] + [w + 1 for w in rank_of_wid])
+        self.max_wid = max_wid
         self.remote = (C.c_int * max_wid)(*([-1] * max_wid))
         self.comms = (vp * max_wid)()
         self.peer = (C.c_int * max_wid)(*([-1] * max_wid))
+        # 1: the worker's communicator is its own 2-rank pair (abortable when it is dropped);
+        # 0: a shared one (PSX_PAIR_COMMS=0), never aborted by the loop
+        self.owned = (C.c_int * max_wid)(*([0] * max_wid))
+        pairs = getattr(transport, "_pairs", {}) if transport is not None else {}
         for w, r in rank_of_wid.items():
             self.remote[w] = r
             c, p = transport.p2p(r)  # the worker's pair communicator (parallel/rccl.py open_pairs)
             self.comms[w], self.peer[w] = c.h.value, p
+            self.owned[w] = int(r in pairs)
+        self.dropped = []          # [(worker id, pair communicator aborted)] after join
+        self.dropped_ranks = []
         dev = server.device.index or 0
         mom = server.momentum_buf if cfg.momentum else None
         self._ckpt = CKPT_CB(self._checkpoint)  # kept alive with the loop
@@ -111,7 +123,9 @@ class NativeServerLoop:
                            heartbeat_timeout=float(cfg.heartbeat_timeout or 0.0), poll_s=poll_s,
                            upd_stream=update_stream.cuda_stream if update_stream is not None else None,
                            own_upd_stream=int(update_stream is None),
-                           ckpt_every=int(cfg.ckpt_every or 0) if cfg.ckpt_dir else 0, ckpt_cb=self._ckpt)
+                           ckpt_every=int(cfg.ckpt_every or 0) if cfg.ckpt_dir else 0, ckpt_cb=self._ckpt,
+                           comm_owned=C.cast(self.owned, vp), transfer_timeout=float(cfg.transfer_timeout or 0.0),
+                           stall_timeout=float(cfg.stall_timeout or 0.0))
         kernels()  # both libraries are loaded (the loop binds their entry points by path)
         runtime()
         self.h = _lib().psx_loop_create(C.byref(self.cfg), os.path.join(NATIVE_DIR, "libpsx_runtime.so").encode(),
@@ -138,6 +152,17 @@ class NativeServerLoop:
         if self.h is None:
             return 0
         rc = _lib().psx_loop_join(self.h)
+        ids, ab = (C.c_int * self.max_wid)(), (C.c_int * self.max_wid)()
+        n = _lib().psx_loop_dropped(self.h, ids, ab, self.max_wid)
+        self.dropped = [(int(ids[i]), bool(ab[i])) for i in range(min(n, self.max_wid))]
+        for w, aborted in self.dropped:
+            r = self.rank_of_wid.get(w)
+            if r is None:
+                continue
+            self.dropped_ranks.append(r)
+            if aborted:  # ncclCommAbort freed it: the transport must not destroy it again
+                self.t.p2p(r)[0].h = None
+        self.server.dropped_workers = sorted(w for w, _ in self.dropped)
         s = self.server
         s._mom_first = s._mom_first and not int(_lib().psx_loop_applies(self.h))
         s.bytes_pushed = int(s.core.metrics().get("gradients_processed", 0)) * s.n * (2 if s.cfg.codec == "fp16" else 4)
@@ -189,12 +214,26 @@ class NativeAsyncChannel(AsyncChannel):
         self.cs.wait_stream(torch.cuda.current_stream())
         return torch.cuda.stream(self.cs)
 
+    crash_in_push = False  # --fault-inject crash_in_push (Worker.run_training)
+
+    def _dropped(self, r):
+        """R_DROPPED: the server no longer serves this worker. The transfer this call posted has
+        no partner any more: abort the pair communicator (that is what ends a posted RCCL kernel)
+        and end the training loop."""
+        if r.type != CP.R_DROPPED:
+            return
+        pairs = getattr(self.t, "_pairs", {})
+        if 0 in pairs and self.comm.h:
+            self.comm.destroy(abort=True)
+        raise CP.WorkerDropped(f"worker rank {self.rank}: dropped by the parameter server")
+
     def fetch(self, worker_id, local_arena):
         self.mbox.send(CP.Msg(CP.FETCH, self.rank, worker_id))
         with self._fork():
             for b in self.codec.wire:  # bf16 image + fp32 remainder, or the fp32 arena (server send order)
                 self.comm.recv(b, self.server_peer, stream=self.cs)
         r = self.mbox.wait_reply(self.rank)
+        self._dropped(r)
         torch.cuda.current_stream().wait_stream(self.cs)
         self.codec.unpack(local_arena)
         return r.c
@@ -203,9 +242,15 @@ class NativeAsyncChannel(AsyncChannel):
         if buffers is not None:
             raise RuntimeError("the native server loop does not take BN buffers (--bn-sync)")
         self.mbox.send(CP.Msg(CP.PUSH, self.rank, worker_id, 0, local_step))
+        if self.crash_in_push:  # the server has posted its receive; this process dies before sending
+            import sys
+
+            print(f"fault injected: worker rank {self.rank} crashes inside a push", file=sys.stderr, flush=True)
+            os._exit(17)
         with self._fork():
             self.comm.send(grads, self.server_peer, stream=self.cs)
         r = self.mbox.wait_reply(self.rank)
+        self._dropped(r)
         torch.cuda.current_stream().wait_stream(self.cs)  # the gradient buffer is reusable
         self.last_staleness = r.d
         return bool(r.b)

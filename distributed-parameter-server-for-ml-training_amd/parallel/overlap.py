@@ -277,6 +277,13 @@ class OverlapSyncChannel(SyncCollectiveChannel):
             return self._full_fetch(local_arena)
         return self._complete(local_arena)
 
+    def _round_event(self):
+        """The round's gathers / broadcasts run on the transport's communication stream, which
+        the compute stream only waits for at the next fetch: the watchdog event is the last
+        outstanding work's (recorded on that stream after every collective of the round)."""
+        ev = getattr(self._works[-1], "event", None) if self._works else None
+        return ev if isinstance(ev, torch.cuda.Event) else super()._round_event()
+
     def drain(self):
         """Finish an in-flight round without consuming it (end of training)."""
         for w in self._works:

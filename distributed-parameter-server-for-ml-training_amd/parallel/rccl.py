@@ -215,9 +215,10 @@ class RcclTransport(DistTransport):
         """Collective over all ranks: a 2-rank communicator {0, r} for every rank r in ``peers``
         (default: every rank > 0). Rank 0 draws the ids; the ranks initialise in rank order on
         rank 0 (each worker only waits for its own pair). PSX_PAIR_COMMS=0 keeps everything on
-        the job communicator. World 2: the job communicator already is the pair."""
+        the job communicator. World 2 gets its own pair as well: the async server aborts a dropped
+        worker's pair communicator, which must never be the job communicator."""
         peers = sorted(peers) if peers is not None else list(range(1, self.world_size))
-        if os.environ.get("PSX_PAIR_COMMS", "1") == "0" or self.world_size <= 2:
+        if os.environ.get("PSX_PAIR_COMMS", "1") == "0" or self.world_size < 2:
             return
         ids = self.broadcast_object({r: NativeComm.new_id() for r in peers} if self.rank == 0 else None)
         if self.rank == 0:
@@ -352,13 +353,16 @@ class RcclTransport(DistTransport):
         return super().completed(work)
 
     def close(self):
+        """With dead ranks (``degraded``) their pair communicators and the job communicator are
+        aborted, not destroyed: a destroy waits for peers that will never come."""
         try:
             torch.cuda.synchronize(self.device)
         finally:
-            for c, _ in self._pairs.values():
-                c.destroy()
+            dead = set(self.degraded)
+            for peer, (c, _) in self._pairs.items():
+                c.destroy(abort=peer in dead or (self.rank in dead))
             self._pairs = {}
-            self.comm.destroy()
+            self.comm.destroy(abort=bool(dead))
             super().close()
 
 

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import os
 import queue
+import sys
 import threading
 import time
 import uuid
@@ -233,9 +234,11 @@ def run_distributed(cfg, log=print) -> dict:
     imgs = t.all_gather_object(wk.images if wk is not None else 0)
     result = {"worker": getattr(wk, "final_metrics", None)}
     if rank == 0:
-        extra = {"images_per_second": round(sum(imgs) / wall, 2) if wall > 0 else 0.0, "gpus": world,
+        extra = {"images_per_second": round(sum(i for i in imgs if i) / wall, 2) if wall > 0 else 0.0, "gpus": world,
                  "topology": cfg.topology if world > 1 or sharded else "colocated"}
-        server.images_processed = sum(imgs)
+        if getattr(server, "dropped_workers", None):
+            extra["dropped_workers"] = list(server.dropped_workers)
+        server.images_processed = sum(i for i in imgs if i)
         result["server"] = server.final_metrics(emit=True, extra=extra)
     t.close()
     return result
@@ -254,7 +257,10 @@ class AsyncSession:
         wid_of_rank = {r: i for i, r in enumerate(worker_ranks)}
         rank_of_wid = {i: r for r, i in wid_of_rank.items()}
         self.t, self.rank = t, rank
+        self.dropped_ranks = []    # rank 0: the worker ranks the native loop dropped
+        self.self_dropped = False  # this worker was dropped by the server
         mbox_name = t.broadcast_object(f"/psx_{uuid.uuid4().hex[:12]}" if rank == 0 else None)
+        self.tag = mbox_name.strip("/")
         self.mbox = CP.ShmMailbox(mbox_name, nreply=t.world_size, owner=True) if rank == 0 else None
         t.barrier()
         if rank != 0:
@@ -295,6 +301,9 @@ class AsyncSession:
         try:
             if self.worker is not None:
                 self.worker.run_training(skip_steps=skip_steps)
+        except CP.WorkerDropped as e:  # the server declared this worker dead: end cleanly
+            self.self_dropped = True
+            print(f"[psx] {e}", file=sys.stderr, flush=True)
         finally:
             self._stop()
 
@@ -314,12 +323,31 @@ class AsyncSession:
             self.thread.join()
             self.thread = None
         if self.loop is not None:
-            self.loop.join()
-            self.loop = None
+            try:
+                self.loop.join()
+            finally:
+                self.dropped_ranks = list(self.loop.dropped_ranks)
+                self.loop = None
 
     def close(self):
+        """End of the async job. Rank 0 publishes the ranks its loop dropped; with none, a normal
+        barrier; otherwise the transport continues among the live ranks (DistTransport.degrade)."""
+        dead = self._end_state()
+        if dead:
+            self.t.degrade(dead, self.tag)
         self.t.barrier()
         self.mbox.close()
+
+    def _end_state(self):
+        import json
+
+        if not getattr(self.t, "is_distributed", False) or self.t.world_size < 2:
+            return []
+        st = self.t._store()
+        key = f"psx/{self.tag}/end"
+        if self.rank == 0:
+            st.set(key, json.dumps(sorted(self.dropped_ranks)))
+        return json.loads(st.get(key))
 
 
 def make_sync_channel(cfg, t, server, W, layout, device, worker: bool = True):

@@ -232,26 +232,78 @@ class DistTransport:
             return True
         return False
 
+    # ---- degraded mode: the job goes on without ranks the async server dropped
+    degraded = ()
+
+    def degrade(self, dead, tag: str):
+        """Ranks ``dead`` (async workers the server dropped: crashed, hung) will never join another
+        collective: from here on the host control operations run among the live ranks on the
+        rendezvous store (a gloo / RCCL collective would wait for the dead ranks forever), and
+        close() aborts communicators instead of destroying them."""
+        self.degraded = tuple(sorted(set(int(r) for r in dead)))
+        self._dtag, self._dseq = tag, 0
+
+    def _live(self):
+        return [r for r in range(self.world_size) if r not in self.degraded]
+
+    @staticmethod
+    def _store():
+        from torch.distributed import distributed_c10d as c10d
+
+        return c10d._get_default_store()
+
+    def _dkey(self, what: str) -> str:
+        self._dseq += 1
+        return f"psx/{self._dtag}/{what}{self._dseq}"
+
+    def _store_gather(self, obj):
+        import pickle
+
+        key, st = self._dkey("obj"), self._store()
+        st.set(f"{key}/{self.rank}", pickle.dumps(obj))
+        if self.rank in self.degraded:
+            return [obj if r == self.rank else None for r in range(self.world_size)]
+        live = self._live()
+        st.wait([f"{key}/{r}" for r in live])
+        return [pickle.loads(st.get(f"{key}/{r}")) if r in live else None for r in range(self.world_size)]
+
     # ---- host control
     def barrier(self):
+        if self.degraded:
+            self._store_gather(None)  # every live rank's key present = everyone arrived
+            return
         dist.barrier(group=self.ctrl)
 
     def all_gather_object(self, obj):
+        if self.degraded:
+            return self._store_gather(obj)
         out = [None] * self.world_size
         dist.all_gather_object(out, obj, group=self.ctrl)
         return out
 
     def broadcast_object(self, obj):
+        if self.degraded:
+            return self._store_gather(obj if self.rank == 0 else None)[0]
         lst = [obj]
         dist.broadcast_object_list(lst, src=0, group=self.ctrl)
         return lst[0]
 
     def close(self):
         if dist.is_initialized():
-            try:
-                dist.barrier(group=self.ctrl)
-            except Exception:
-                pass
+            if self.degraded:
+                # the store lives in rank 0's process: rank 0 leaves last (the others only check in)
+                key, st = self._dkey("close"), self._store()
+                try:
+                    st.set(f"{key}/{self.rank}", b"1")
+                    if self.rank == 0:
+                        st.wait([f"{key}/{r}" for r in self._live() if r != 0])
+                except Exception:
+                    pass
+            else:
+                try:
+                    dist.barrier(group=self.ctrl)
+                except Exception:
+                    pass
             dist.destroy_process_group()
 
 

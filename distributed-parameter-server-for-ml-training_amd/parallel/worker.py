@@ -411,7 +411,7 @@ class Worker:
             skip_steps = rounds_to_batches(rounds, len(self.sampler.epoch_indices(0)), K)
             self.log(f"[Resume] worker {self.worker_id} skips {rounds} completed rounds ({skip_steps} batches)")
         self.training_start_time = time.time()
-        fi_kind, fi_worker, fi_step = _parse_fault(self.cfg.fault_inject)
+        fi_kind, fi_worker, fi_step, fi_secs = _parse_fault(self.cfg.fault_inject)
         try:
             for epoch in range(self.num_epochs):
                 self._sync()
@@ -430,11 +430,25 @@ class Worker:
                         if fi_kind == "hang_worker":  # alive but stalled: only a liveness guard notices
                             import sys
 
-                            print(f"fault injected: worker {self.worker_id} hangs at step {fi_step}", file=sys.stderr,
-                                  flush=True)
-                            while True:
-                                time.sleep(3600)
-                        raise _InjectedFault(f"fault injected: worker {self.worker_id} at step {fi_step}")
+                            print(f"fault injected: worker {self.worker_id} hangs at step {fi_step}"
+                                  + (f" for {fi_secs:g} s" if fi_secs else ""), file=sys.stderr, flush=True)
+                            t_end = time.time() + (fi_secs or float("inf"))
+                            while time.time() < t_end:
+                                time.sleep(min(3600.0, max(0.0, t_end - time.time())))
+                        elif fi_kind == "crash_in_push":  # the channel dies after posting this step's PUSH
+                            self.channel.crash_in_push = True
+                        elif self.cfg.mode == "async":
+                            # an async worker's process dies between requests: no JobFinished, its
+                            # heartbeats stop (the server's timeout drops it; sync mode raises
+                            # instead, for the launcher's restart path)
+                            import os
+                            import sys
+
+                            print(f"fault injected: worker {self.worker_id} process exits at step {fi_step}",
+                                  file=sys.stderr, flush=True)
+                            os._exit(17)
+                        else:
+                            raise _InjectedFault(f"fault injected: worker {self.worker_id} at step {fi_step}")
                     if batch_idx % K == 0:
                         with self.timer.span("fetch"):
                             self.fetch_parameters()
@@ -507,14 +521,18 @@ class _InjectedFault(RuntimeError):
 
 
 def _parse_fault(spec: str):
-    """'kill_worker:K@S' (worker K raises at its step S) or 'hang_worker:K@S' (worker K stalls
-    forever at step S, process alive) -> (kind, K, S); anything else -> (None, None, None). Only
-    armed on the first attempt of an elastic job (torchrun sets TORCHELASTIC_RESTART_COUNT), so a
-    restarted job resumes instead of failing again."""
+    """'kill_worker:K@S' (worker K raises at its step S), 'hang_worker:K@S[:secs]' (worker K stalls
+    at step S, process alive — forever, or for secs seconds) or 'crash_in_push:K@S' (async: worker
+    K's process exits inside its step-S push, after the PUSH request, before sending the gradient)
+    -> (kind, K, S, secs); anything else -> (None, None, None, None). Only armed on the first
+    attempt of an elastic job (torchrun sets TORCHELASTIC_RESTART_COUNT), so a restarted job
+    resumes instead of failing again."""
     import os
 
     kind = spec.split(":", 1)[0] if spec else ""
-    if kind not in ("kill_worker", "hang_worker") or int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")):
-        return None, None, None
-    k, s = spec.split(":", 1)[1].split("@")
-    return kind, int(k), int(s)
+    if kind not in ("kill_worker", "hang_worker", "crash_in_push") or \
+            int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")):
+        return None, None, None, None
+    k, rest = spec.split(":", 1)[1].split("@")
+    s, _, secs = rest.partition(":")
+    return kind, int(k), int(s), float(secs) if secs else None

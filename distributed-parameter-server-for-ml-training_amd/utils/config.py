@@ -89,7 +89,11 @@ class PSConfig:
     heartbeat_timeout: float = 60.0
     log_dir: str = ""
     use_graph: bool = True
-    fault_inject: str = ""         # "kill_worker:2@5" (worker 2 exits at its step 5) | "hang_worker:2@5" (stalls)
+    # "kill_worker:2@5" (worker 2 raises at its step 5) | "hang_worker:2@5[:secs]" (stalls, forever or secs)
+    # | "crash_in_push:2@5" (async: worker 2's process dies inside its step-5 push, after the PUSH request)
+    fault_inject: str = ""
+    transfer_timeout: float = 300.0  # async native loop: drop a worker whose transfer is in flight longer (0: off)
+    stall_timeout: float = 0.0       # async native loop: drop a worker silent (no request) that long (0: off)
     round_timeout: float = 300.0   # sync liveness guard: abort + exit 3 when no round completes (0: off)
     verbose: int = 1
     extra: dict = field(default_factory=dict)
@@ -114,6 +118,8 @@ class PSConfig:
             raise ValueError("--sync-semantics must be barrier or reference")
         if self.staleness_bound < 0:
             raise ValueError("--staleness-bound must be >= 0")
+        if self.transfer_timeout < 0 or self.stall_timeout < 0:
+            raise ValueError("--transfer-timeout / --stall-timeout must be >= 0")
         if self.dtype not in ("fp32", "bf16"):
             raise ValueError(f"--dtype must be fp32 or bf16, got {self.dtype!r}")
         if self.fetch_codec == "auto":
@@ -121,7 +127,9 @@ class PSConfig:
         if self.fetch_codec not in ("bf16conv", "fp32"):
             raise ValueError("--fetch-codec must be bf16conv or fp32")
         if self.dtype == "fp32" and self.fetch_codec != "fp32":
-            raise ValueError("--dtype fp32 computes with fp32 weights: --fetch-codec fp32")
+            raise ValueError("--fetch-codec bf16conv ships bf16 conv weights, which only the bf16 engine consumes: "
+                             "add --dtype bf16 (the default since round 2 is --dtype fp32, the reference's "
+                             "precision, whose fetch payload is the fp32 state)")
         if self.bucket_mb <= 0:
             raise ValueError("--bucket-mb must be > 0")
         if self.synthetic_kind not in ("proto", "hard"):
@@ -194,7 +202,14 @@ def add_arguments(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     A("--heartbeat-timeout", type=float, default=None)
     A("--log-dir", default=None)
     A("--no-graph", dest="use_graph", action="store_false", default=None)
-    A("--fault-inject", default=None, help="kill_worker:K@S or hang_worker:K@S (first attempt only)")
+    A("--fault-inject", default=None,
+      help="kill_worker:K@S, hang_worker:K@S[:secs] or crash_in_push:K@S (first attempt only)")
+    A("--transfer-timeout", type=float, default=None,
+      help="async server: seconds a gradient receive / snapshot send may stay in flight before the worker is "
+           "dropped (its pair communicator aborted); 0 disables")
+    A("--stall-timeout", type=float, default=None,
+      help="async server: seconds a worker may send no request before it is dropped (catches a hung training "
+           "loop whose heartbeat thread still runs); 0 disables")
     A("--round-timeout", type=float, default=None,
       help="sync rounds: seconds without a completed round before the communicator is aborted and the rank "
            "exits (status 3) for a launcher restart from the last checkpoint; 0 disables")

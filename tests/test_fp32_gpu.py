@@ -258,7 +258,7 @@ def test_engine_step_f32_matches_torch_fp64():
     layout = ParamLayout.from_module(model)
     arena, _ = layout.pack(model)
     arena = arena.to(DEV)
-    eng = HipResNetEngine(model, layout, B, grad_dtype=torch.float32, dtype=torch.float32)
+    eng = HipResNetEngine(model, layout, B, grad_dtype=torch.float32, dtype=torch.float32, deterministic=True)
     x = torch.randn(B, 3, 32, 32, device=DEV)
     y = torch.randint(0, 100, (B,), device=DEV)
     eng.unpack(arena)
@@ -288,14 +288,18 @@ def test_engine_step_f32_matches_torch_fp64():
         rows.append((name, err, err32))
     for name, err, err32 in rows:
         print(f"{name:32s} engine {err:.2e}  torch-fp32 {err32:.2e}")
-    # At random init BN-normalised backward passes amplify rounding-order differences (the BN
-    # statistics use fp32 atomics): run to run the engine's own gradients move by ~3e-3 and torch's
-    # fp32 autograd sits at ~2e-3 from fp64 (scripts/dev/fp32_noise_probe.py). The bar: that noise
-    # level per tensor, and the head (no BN amplification) tight.
+    # At random init BN-normalised backward passes amplify fp32 rounding: a forward value that
+    # lands on the other side of a ReLU flips its mask, and a BN bias gradient (a sum of dz with
+    # heavy cancellation) moves by far more than the rounding. torch's own fp32 autograd sits at
+    # 0.7-3.6e-3 from fp64 per tensor; the engine (deterministic, so this is one fixed measurement,
+    # not a noise sample: 1.9-5.4e-3 below layer4.1, median 3.9e-3, with Winograd's ~3e-6 forward
+    # rounding) gets the same amplification from its forward rounding; torch's own number moves
+    # from run to run (MIOpen's algorithm choice: conv1.weight 3.1e-3 in one run, 8.4e-4 in the
+    # next). Bars: per tensor below 1e-2, median below 5e-3, the head (no BN amplification) tight.
     for name, err, err32 in rows:
-        assert err < 2e-2, (name, err, err32)
+        assert err < 1e-2, (name, err, err32)
     errs = sorted(r[1] for r in rows)
-    assert errs[len(errs) // 2] < 1e-2, errs
+    assert errs[len(errs) // 2] < 5e-3, errs
     assert dict((r[0], r[1]) for r in rows)["fc.weight"] < 1e-5
     sd = ref.state_dict()
     for name in ("bn1.running_mean", "layer2.0.bn1.running_var", "layer4.1.bn2.running_mean"):

@@ -111,7 +111,7 @@ from psx.parallel.runner import run_distributed
 from psx.utils.config import PSConfig
 cfg = PSConfig(model="resnet18", batch_size=64, epochs=1, train_samples=2048, eval_every=0, verbose=0, lr=0.1,
                max_steps=8, mode="async", dtype={dtype!r}, momentum={mom}, weight_decay={wd},
-               ckpt_every=4, ckpt_dir={ck!r}).validate()
+               ckpt_every=4, ckpt_dir={ck!r}, deterministic=True).validate()
 res = run_distributed(cfg, log=lambda *a, **k: None)
 s = res["server"]
 print("RESULT " + json.dumps([s["final_param_checksum"], s["global_steps_completed"], s["async_updates"],
@@ -121,6 +121,10 @@ print("RESULT " + json.dumps([s["final_param_checksum"], s["global_steps_complet
 
 @pytest.mark.parametrize("dtype,mom", [("bf16", 0.0), ("fp32", 0.9)])
 def test_native_loop_colocated_run_matches_python_loop(dtype, mom, tmp_path):
+    """Both loops run the same co-located job in deterministic mode (fixed-order BN reductions,
+    Winograd included): the master state must agree bit for bit. (Round 2 compared two
+    non-deterministic runs at 2e-4 and flaked: 8 steps at lr 0.1 / momentum 0.9 amplify the
+    atomic-order noise of the BN statistics past that bar.)"""
     out = {}
     for flag, port in (("1", 29661), ("0", 29662)):
         ck = str(tmp_path / f"ck{flag}")
@@ -128,5 +132,5 @@ def test_native_loop_colocated_run_matches_python_loop(dtype, mom, tmp_path):
         out[flag] = _run(code, port, {"PSX_NATIVE_LOOP": flag})
     (a, ga, ua, sa, ca), (b, gb, ub, sb, cb) = out["1"], out["0"]
     assert ga == gb == 8 and ua == ub == 8 and sa == sb == 0, out
-    assert abs(a - b) <= 2e-4 * max(abs(a), abs(b)), out
+    assert a == b, out  # bit-identical arenas give identical checksums
     assert ca == cb and len(ca) >= 2, out  # checkpoints at steps 4 and 8 from both loops

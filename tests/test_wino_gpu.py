@@ -14,6 +14,15 @@ from psx.ops import kernels as K  # noqa: E402
 DEV = "cuda"
 TOL = 1e-4
 
+# Winograd-on vs Winograd-off whole step, both deterministic (test_engine_step_wino_vs_direct).
+# Measured: median 7.4e-3, worst 1.0e-2 (a BN bias). Not a kernel error: each layer agrees with
+# fp64 to ~3e-6 (the per-layer tests above); the random-init network's BN-normalised backward
+# amplifies that forward rounding through ReLU-mask flips (test_fp32_gpu.py: torch's own fp32
+# autograd is 0.7-3.6e-3 from fp64 on the same kind of step). Deterministic on both sides, so
+# these are fixed numbers, not a noise sample.
+WINO_STEP_MAX = 2e-2
+WINO_STEP_MEDIAN = 1e-2
+
 
 def _rel(a, b):
     a, b = a.double(), b.double()
@@ -124,8 +133,10 @@ def test_wino_wgrad(nb, h, c, k, fp16):
 
 
 def test_engine_step_wino_vs_direct(monkeypatch):
-    """One fp32 ResNet-18 step with the Winograd layers (default) and with PSX_WINO=0: the loss and
-    every gradient agree to fp32 tolerance, and the Winograd engine really routed layers to it."""
+    """One fp32 ResNet-18 step with the Winograd layers (default) and with PSX_WINO=0, both in
+    deterministic mode (fixed-order BN reductions, so the only difference left is the algorithm):
+    the loss and every gradient agree to fp32 tolerance, and the Winograd engine really routed
+    layers to it."""
     from psx.models.engine import HipResNetEngine
     from psx.models.layout import ParamLayout
     from psx.models.resnet import ResNet18
@@ -141,7 +152,7 @@ def test_engine_step_wino_vs_direct(monkeypatch):
     out = {}
     for wino in ("1", "0"):
         monkeypatch.setenv("PSX_WINO", wino)
-        eng = HipResNetEngine(model, layout, B, dtype=torch.float32)
+        eng = HipResNetEngine(model, layout, B, dtype=torch.float32, deterministic=True)
         assert (len(eng.wino_layers) > 0) == (wino == "1")
         eng.index.copy_(torch.arange(B, dtype=torch.int32, device=DEV))
         a = arena.clone()
@@ -149,11 +160,10 @@ def test_engine_step_wino_vs_direct(monkeypatch):
         torch.cuda.synchronize()
         out[wino] = (eng.loss.double().mean().item(), eng.grads.double().clone())
     (l1, g1), (l0, g0) = out["1"], out["0"]
-    assert abs(l1 - l0) < 1e-4 * max(1.0, abs(l0))
+    assert abs(l1 - l0) < 1e-5 * max(1.0, abs(l0))  # the forward itself: Winograd rounding only
     n = layout.param_numel
-    # the bar of test_fp32_gpu.py's whole-step test: at random init the BN-normalised backward
-    # amplifies rounding differences (a flipped ReLU mask moves a BN bias gradient by ~1e-2 of its
-    # norm; the engine's own run-to-run spread is ~3e-3), so per tensor < 2e-2, median < 1e-2.
+    # deterministic on both sides: what is left is Winograd's own rounding (~3e-6 per conv vs
+    # fp64, direct ~2e-7), amplified by the BN-normalised backward of a random-init network.
     # Accuracy against float64 autograd with the Winograd layers on (the default) is
     # test_fp32_gpu.py::test_engine_step_f32_matches_torch_fp64
     errs = []
@@ -162,8 +172,10 @@ def test_engine_step_wino_vs_direct(monkeypatch):
             continue
         a, b = g1[e.offset:e.offset + e.numel], g0[e.offset:e.offset + e.numel]
         errs.append((((a - b).norm() / b.norm().clamp_min(1e-30)).item(), name))
-    assert max(errs)[0] < 2e-2, max(errs)
-    assert sorted(errs)[len(errs) // 2][0] < 1e-2, sorted(errs)
+    errs.sort()
+    print("wino vs direct: median %.2e, worst %s" % (errs[len(errs) // 2][0], errs[-3:]))
+    assert errs[-1][0] < WINO_STEP_MAX, errs[-3:]
+    assert errs[len(errs) // 2][0] < WINO_STEP_MEDIAN, errs
     assert torch.isfinite(g1[:n]).all()
 
 
@@ -242,7 +254,7 @@ def test_engine_bn_fold_matches_unfolded(monkeypatch):
     out = {}
     for fold in ("1", "0"):
         monkeypatch.setenv("PSX_WINO_BNFOLD", fold)
-        eng = HipResNetEngine(model, layout, B, dtype=torch.float32)
+        eng = HipResNetEngine(model, layout, B, dtype=torch.float32, deterministic=True)
         assert (len(eng.wino_bnfold) == 8) == (fold == "1"), eng.wino_bnfold
         eng.index.copy_(torch.arange(B, dtype=torch.int32, device=DEV))
         a = arena0.clone()
@@ -250,14 +262,10 @@ def test_engine_bn_fold_matches_unfolded(monkeypatch):
         torch.cuda.synchronize()
         out[fold] = (eng.loss.double().mean().item(), eng.grads.double().clone(), a.double().clone())
     (l1, g1, a1), (l0, g0, a0) = out["1"], out["0"]
-    assert abs(l1 - l0) < 1e-5 * max(1.0, abs(l0))
-    errs = []
-    for name, e in layout.entries.items():
-        if e.region != "param":
-            continue
-        x, y = g1[e.offset:e.offset + e.numel], g0[e.offset:e.offset + e.numel]
-        errs.append((((x - y).norm() / y.norm().clamp_min(1e-30)).item(), name))
-    assert max(errs)[0] < 2e-2, max(errs)
-    assert sorted(errs)[len(errs) // 2][0] < 1e-2, sorted(errs)
-    n = layout.param_numel  # running statistics (buffer region) written by the folded finalize
-    assert torch.allclose(a1[n:], a0[n:], rtol=1e-5, atol=1e-6)
+    # deterministic mode: the fold computes the same affine from the same fixed-order sums and
+    # applies the same BN + ReLU, only inside another kernel: loss and gradients bit for bit. The
+    # running statistics the folded finalize publishes may differ by an ulp (the compiler
+    # contracts the momentum update into FMAs differently in the two kernels).
+    assert l1 == l0
+    assert torch.equal(g1, g0)
+    assert torch.allclose(a1, a0, rtol=1e-6, atol=1e-7)

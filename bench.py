@@ -41,6 +41,7 @@ from psx.parallel.runner import (AsyncSession, build_state, make_datasets, make_
                                  make_sync_channel)
 from psx.parallel.server import ParameterServer  # noqa: E402
 from psx.parallel.sharded import ShardedSyncChannel  # noqa: E402
+from psx.parallel.native_sync import NativeSyncServer, native_sync_enabled  # noqa: E402
 from psx.parallel.rccl import make_transport  # noqa: E402
 from psx.parallel.transport import env_world  # noqa: E402
 from psx.parallel.worker import Worker  # noqa: E402
@@ -99,11 +100,16 @@ class Run:
                 self.wk = Worker(cfg, comp, self.chan, train, None, worker_name=f"worker-{wid}", rank=rank, log=quiet,
                                  requested_id=wid)
                 self.wk.connect_to_server()
+        self.native = None
         if self.wk is not None:
             self.wk.setup_data()
             self.batches = self.wk.sampler.epoch_indices(0)
         elif self.sess is not None:
             pass  # dedicated async server rank: its event-loop thread does the work
+        elif native_sync_enabled(cfg, t, self.chan, self.server, rank):
+            # dedicated sync server rank: every round of a run in one native call (no Python per
+            # round; csrc/server/sync_loop.cpp)
+            self.native = NativeSyncServer(self.server, t, self.chan)
         elif a.codec == "topk":
             from psx.parallel.topk import empty_payload
 
@@ -133,15 +139,22 @@ class Run:
     def measure(self, steps, warmup):
         """Untimed warmup, then exactly ``steps`` timed steps; returns (max seconds over ranks,
         host issue times of this rank)."""
-        for i in range(warmup):
-            self.step(i)
-        self.barrier_sync()
-        host = []
-        t0 = time.perf_counter()
-        for i in range(steps):
-            h0 = time.perf_counter()
-            self.step(warmup + i)
-            host.append(time.perf_counter() - h0)
+        if self.native is not None:  # the native server rank runs its rounds in one call each
+            self.native.run(warmup)
+            self.barrier_sync()
+            t0 = time.perf_counter()
+            self.native.run(steps)
+            host = [(time.perf_counter() - t0) / max(1, steps)] * steps
+        else:
+            for i in range(warmup):
+                self.step(i)
+            self.barrier_sync()
+            host = []
+            t0 = time.perf_counter()
+            for i in range(steps):
+                h0 = time.perf_counter()
+                self.step(warmup + i)
+                host.append(time.perf_counter() - h0)
         self.barrier_sync()
         dt = time.perf_counter() - t0
         if self.t is not None:
@@ -158,6 +171,8 @@ class Run:
         agg = os.environ.get("PSX_SYNC_AGG", "gather")
         push = ("RCCL send/recv gather of the fp16 wires to rank 0 + fp32 aggregation" if agg == "gather" else
                 "RCCL reduce(grads)")
+        if self.native is not None:
+            push += " (server rounds in native code)"
         return (f"{a.mode}-PS: rank0 = parameter server{' only' if self.dedicated else ' + worker 0'}, {W} "
                 f"data-parallel worker(s); " + (f"{push} + RCCL broadcast(params) over xGMI" if a.mode == "sync" else
                                                  "shm mailbox control + RCCL send/recv over xGMI"))
@@ -170,6 +185,8 @@ class Run:
         return "colocated" if self.t is not None else "loopback"
 
     def close(self):
+        if self.native is not None:
+            self.native.close()
         if self.sess is not None:
             self.sess.finish()
             self.sess.close()

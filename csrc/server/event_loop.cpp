@@ -219,6 +219,9 @@ int alloc_worker(PsxLoop* L, int w) {
 // state when the fetch payload carries it; the fp32 fetch never reads one)
 int apply(PsxLoop* L, const void* g, float weight) {
   const double t0 = now_s();
+  // the kernel wrappers report hipGetLastError(): clear what an earlier hipEventQuery (a
+  // hipErrorNotReady of a transfer still in flight) left in this thread's error slot
+  (void)hipGetLastError();
   const int e = L->rt.sgd_apply(L->c.arena, g, L->c.mom_buf, L->c.n_params, L->c.lr, weight, L->c.momentum,
                                 L->c.weight_decay, L->c.mom_first, L->c.grad_fp16, L->img, L->s_upd);
   L->c.mom_first = 0;
@@ -284,7 +287,9 @@ int serve_fetch(PsxLoop* L, int w, int rank) {
                               L->s_upd));
   } else {
     PSX_HIP(L, hipMemcpyAsync(L->snap_img[w], L->img, (size_t)L->c.n_params * 2, hipMemcpyDeviceToDevice, L->s_upd));
-    if (L->c.small_n) L->rt.gather_f32(L->c.arena, L->c.small_idx, L->c.small_n, L->snap_small[w], L->s_upd);
+    (void)hipGetLastError();  // see apply()
+    if (L->c.small_n && L->rt.gather_f32(L->c.arena, L->c.small_idx, L->c.small_n, L->snap_small[w], L->s_upd))
+      return -26;
   }
   stream_after(L, L->s_comm[w], L->s_upd);
   void* comm = L->c.comms[w];
@@ -431,6 +436,7 @@ void run(PsxLoop* L) {
     PSX_HIP(L, hipMalloc((void**)&L->img, (size_t)L->c.n_params * 2));
     PSX_HIP(L, hipMalloc(&zero, gbytes(L)));
     PSX_HIP(L, hipMemsetAsync(zero, 0, gbytes(L), L->s_upd));
+    (void)hipGetLastError();
     if (!L->err && L->rt.sgd_apply(L->c.arena, zero, nullptr, L->c.n_params, 0.f, 1.f, 0.f, 0.f, 0, L->c.grad_fp16,
                                    L->img, L->s_upd))
       L->err = -33;

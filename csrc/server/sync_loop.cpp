@@ -1,0 +1,359 @@
+// Native synchronous parameter-server rounds of the dedicated server rank (rank 0 of the
+// 1 server + N-1 workers layout), on HIP streams.
+//
+// The reference's sync handler counts pushes under a lock and applies the average when the
+// last worker's gradient arrives (reference: src/parameter_server/server.py:264-288, :145-169,
+// :126-143); its workers then fetch the new state (:213-230). Here the server rank runs every
+// round of the job inside ONE native call — no Python per round — issuing exactly the
+// collective sequence the workers' sync channels issue (parallel/worker.py
+// SyncCollectiveChannel, parallel/overlap.py OverlapSyncChannel):
+//
+//   serial round     fetch: broadcast of the fp32 arena (or of the WeightWire: bf16 image of the
+//                    parameters + fp32 remainder, republished from the arena);
+//                    push:  one group of ncclRecv, one per worker rank (every worker on its own
+//                    xGMI link) -> sgd_apply_multi: the W wires decoded and summed in fp32 in
+//                    worker order, p -= lr * sum / W (+ momentum / weight decay, + the image)
+//   overlapped round per gradient bucket k (backward order): gather(k) on the communication
+//                    stream; the apply of bucket k on the update stream once its gather is done,
+//                    written straight into the bucket's fetch-wire segment (fp32: the arena slice
+//                    itself is broadcast; bf16conv: the apply writes the bf16 image into the
+//                    segment and the fp32 entries are gathered after it), then broadcast(k) on
+//                    the communication stream — gather(k+1) is already queued ahead of it, as on
+//                    the workers. The first round starts with one broadcast of the whole wire.
+//
+// The native core (csrc/runtime/ps_core.cpp) records every round: on_fetch / on_push per member
+// (the wait-for-N barrier completes on the last), on_applied. Checkpoints (--ckpt-every) call
+// back into the host after an event wait on the round's apply. At most two rounds are in flight
+// on the device (the host waits for round r-2's completion event), and the number of rounds
+// whose device work has completed is published for the liveness watchdog
+// (parallel/liveness.py RoundWatchdog polls psx_sync_progress). Every HIP call is checked.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <time.h>
+
+#include <atomic>
+#include <deque>
+#include <vector>
+
+#include "psx_comm.h"
+
+namespace {
+
+enum { PSX_APPLY_ = 1 };
+
+struct SyncRt {
+  long long (*ps_on_fetch)(void*, int, double);
+  int (*ps_on_push)(void*, int, long long, double, float*, int*, long long*);
+  void (*ps_on_applied)(void*, double);
+  long long (*ps_global_step)(void*);
+  int (*sgd_apply_multi)(float*, const void* const*, int, float*, long, float, float, float, float, int, int, void*,
+                         hipStream_t);
+  int (*gather_f32)(const float*, const long*, long, float*, hipStream_t);
+};
+
+template <typename F>
+bool bindf(void* lib, const char* name, F* fn) {
+  *fn = reinterpret_cast<F>(dlsym(lib, name));
+  if (!*fn) fprintf(stderr, "psx sync loop: missing symbol %s\n", name);
+  return *fn != nullptr;
+}
+
+double now_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+}  // namespace
+
+// One gradient bucket of the overlapped round (mirrors parallel/overlap.py Bucket + BucketWire).
+struct PsxSyncBucket {
+  long lo, hi;          // parameter range [lo, hi)
+  void* seg;            // its fetch-wire segment (device)
+  long seg_bytes;       // bytes broadcast (the workers' segment size)
+  const long* small;    // bf16conv: device arena indices of the fp32 entries (nullptr: fp32 kind)
+  long nsmall;
+  float* seg_small;     // bf16conv: where they go in the segment
+};
+
+struct PsxSyncCfg {  // mirrored by parallel/native_sync.py (ctypes.Structure)
+  void* comm;           // the job communicator (rank 0 = this server)
+  void* core;
+  float* arena;         // fp32 master arena (params | buffers)
+  long n_params, arena_numel;
+  int nworkers;         // worker ranks 1..nworkers (dedicated topology: world = nworkers + 1)
+  const int* members;   // worker ids of the round, in core order [nworkers]
+  void* const* gbufs;   // per worker rank 1..nworkers: its gathered gradient wire [nworkers]
+  int grad_fp16;
+  float lr, momentum, weight_decay;
+  float* mom_buf;
+  int mom_first;
+  // fetch payload of the serial round: 0 = the fp32 arena (broadcast in place); 1 = WeightWire
+  int image;
+  void* wire_buf;       // WeightWire: [bf16 image | fp32 remainder] (device)
+  long wire_bytes;
+  uint16_t* wire_img;   // its image part (the apply writes it)
+  const long* small_idx;  // its remainder's arena indices
+  long small_n;
+  float* wire_small;
+  // overlapped round (nbuckets > 0): buckets in backward order, the first round's whole-wire
+  // broadcast, the BN-buffer segment
+  int nbuckets;
+  const PsxSyncBucket* buckets;
+  void* full_wire;
+  long full_wire_bytes;
+  int primed;           // the first round's full fetch already happened (resume of a channel)
+  hipStream_t upd_stream;   // compute / update stream of the server rank
+  hipStream_t comm_stream;  // the overlapped round's communication stream
+  long long ckpt_every;
+  int (*ckpt_cb)(long long global_step);
+};
+
+struct PsxSync {
+  PsxSyncCfg c;
+  SyncRt rt;
+  std::atomic<long long> issued{0}, done{0};
+  std::deque<hipEvent_t> inflight;
+  int err = 0;
+};
+
+namespace {
+
+#define PSX_SHIP(S, call)                                                                        \
+  do {                                                                                           \
+    const hipError_t e_ = (call);                                                                \
+    if (e_ != hipSuccess) {                                                                      \
+      fprintf(stderr, "psx sync loop: %s failed: %s\n", #call, hipGetErrorString(e_));            \
+      if (!(S)->err) (S)->err = -50;                                                             \
+    }                                                                                            \
+  } while (0)
+
+#define PSX_SCOMM(S, call)                                                                       \
+  do {                                                                                           \
+    const int e_ = (call);                                                                       \
+    if (e_ && !(S)->err) {                                                                       \
+      fprintf(stderr, "psx sync loop: %s failed (%d)\n", #call, e_);                             \
+      (S)->err = -60;                                                                            \
+    }                                                                                            \
+  } while (0)
+
+void after(PsxSync* S, hipStream_t a, hipStream_t b) {
+  hipEvent_t ev;
+  PSX_SHIP(S, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  PSX_SHIP(S, hipEventRecord(ev, b));
+  PSX_SHIP(S, hipStreamWaitEvent(a, ev, 0));
+  PSX_SHIP(S, hipEventDestroy(ev));
+}
+
+// rounds whose device work finished (host-side bookkeeping of the in-flight events)
+void retire(PsxSync* S, size_t keep) {
+  while (S->inflight.size() > keep) {
+    hipEvent_t ev = S->inflight.front();
+    PSX_SHIP(S, hipEventSynchronize(ev));
+    PSX_SHIP(S, hipEventDestroy(ev));
+    S->inflight.pop_front();
+    S->done.fetch_add(1);
+  }
+  while (!S->inflight.empty() && hipEventQuery(S->inflight.front()) == hipSuccess) {
+    PSX_SHIP(S, hipEventDestroy(S->inflight.front()));
+    S->inflight.pop_front();
+    S->done.fetch_add(1);
+  }
+}
+
+void gather(PsxSync* S, long lo, long n, hipStream_t st) {
+  const int dt = S->c.grad_fp16 ? PSX_F16 : PSX_F32;
+  const size_t es = S->c.grad_fp16 ? 2 : 4;
+  PSX_SCOMM(S, psx_comm_group_start());
+  for (int r = 1; r <= S->c.nworkers; ++r)
+    PSX_SCOMM(S, psx_comm_recv(S->c.comm, (char*)S->c.gbufs[r - 1] + lo * es, n, dt, r, st));
+  PSX_SCOMM(S, psx_comm_group_end());
+}
+
+// p[lo:hi] -= lr * sum_k g_k[lo:hi] / W (+ momentum / wd), image (nullable) of the range
+void apply_range(PsxSync* S, long lo, long hi, void* img, hipStream_t st) {
+  const size_t es = S->c.grad_fp16 ? 2 : 4;
+  std::vector<const void*> srcs(S->c.nworkers);
+  for (int k = 0; k < S->c.nworkers; ++k) srcs[k] = (const char*)S->c.gbufs[k] + lo * es;
+  // the kernel wrappers report hipGetLastError(): clear a hipErrorNotReady of an earlier
+  // hipEventQuery (retire) from this thread's error slot
+  (void)hipGetLastError();
+  if (S->rt.sgd_apply_multi(S->c.arena + lo, srcs.data(), S->c.nworkers, S->c.mom_buf ? S->c.mom_buf + lo : nullptr,
+                            hi - lo, S->c.lr, 1.f / (float)S->c.nworkers, S->c.momentum, S->c.weight_decay,
+                            S->c.mom_first, S->c.grad_fp16, img, st) &&
+      !S->err)
+    S->err = -61;
+}
+
+// the core's bookkeeping of one completed round (every member pushed, the barrier completes on
+// the last) + the checkpoint hook
+void record_round(PsxSync* S, double t0) {
+  float w = 0.f;
+  int nc = 0;
+  long long st = 0;
+  int d = 0;
+  const long long gs = S->rt.ps_global_step(S->c.core);
+  for (int k = 0; k < S->c.nworkers; ++k) d = S->rt.ps_on_push(S->c.core, S->c.members[k], gs, now_s(), &w, &nc, &st);
+  if (d != PSX_APPLY_ && !S->err) {
+    fprintf(stderr, "psx sync loop: the round did not complete on the core (decision %d)\n", d);
+    S->err = -62;
+  }
+  S->rt.ps_on_applied(S->c.core, now_s() - t0);
+  S->c.mom_first = 0;
+  const long long g2 = S->rt.ps_global_step(S->c.core);
+  if (S->c.ckpt_cb && S->c.ckpt_every > 0 && g2 % S->c.ckpt_every == 0) {
+    hipEvent_t ev;  // the apply of this round, not the whole stream
+    PSX_SHIP(S, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    PSX_SHIP(S, hipEventRecord(ev, S->c.upd_stream));
+    PSX_SHIP(S, hipEventSynchronize(ev));
+    PSX_SHIP(S, hipEventDestroy(ev));
+    if (S->c.ckpt_cb(g2) && !S->err) S->err = -63;
+  }
+}
+
+void fetch_bookkeeping(PsxSync* S) {
+  for (int k = 0; k < S->c.nworkers; ++k) S->rt.ps_on_fetch(S->c.core, S->c.members[k], now_s());
+}
+
+void serial_round(PsxSync* S) {
+  hipStream_t st = S->c.upd_stream;
+  const double t0 = now_s();
+  fetch_bookkeeping(S);
+  if (S->c.image) {
+    (void)hipGetLastError();
+    if (S->c.small_n && S->rt.gather_f32(S->c.arena, S->c.small_idx, S->c.small_n, S->c.wire_small, st) && !S->err)
+      S->err = -64;
+    PSX_SCOMM(S, psx_comm_broadcast(S->c.comm, S->c.wire_buf, S->c.wire_bytes, PSX_U8, 0, st));
+  } else {
+    PSX_SCOMM(S, psx_comm_broadcast(S->c.comm, S->c.arena, S->c.arena_numel, PSX_F32, 0, st));
+  }
+  gather(S, 0, S->c.n_params, st);
+  apply_range(S, 0, S->c.n_params, S->c.image ? S->c.wire_img : nullptr, st);
+  record_round(S, t0);
+}
+
+void overlap_round(PsxSync* S) {
+  hipStream_t cs = S->c.comm_stream, us = S->c.upd_stream;
+  const double t0 = now_s();
+  fetch_bookkeeping(S);
+  if (!S->c.primed) {  // first round: the whole wire (every segment + the BN buffers), packed by the host
+    after(S, cs, us);
+    PSX_SCOMM(S, psx_comm_broadcast(S->c.comm, S->c.full_wire, S->c.full_wire_bytes, PSX_U8, 0, cs));
+    S->c.primed = 1;
+  }
+  std::vector<hipEvent_t> got(S->c.nbuckets);
+  auto issue_gather = [&](int k) {
+    const PsxSyncBucket& b = S->c.buckets[k];
+    after(S, cs, us);  // the previous apply of this range (and the wire pack) before new data lands
+    gather(S, b.lo, b.hi - b.lo, cs);
+    PSX_SHIP(S, hipEventCreateWithFlags(&got[k], hipEventDisableTiming));
+    PSX_SHIP(S, hipEventRecord(got[k], cs));
+  };
+  auto finish = [&](int k) {  // apply (+ segment pack) on the update stream, broadcast on cs
+    const PsxSyncBucket& b = S->c.buckets[k];
+    PSX_SHIP(S, hipStreamWaitEvent(us, got[k], 0));
+    PSX_SHIP(S, hipEventDestroy(got[k]));
+    if (b.small) {  // bf16conv segment: the apply writes the bf16 image, then the fp32 entries
+      apply_range(S, b.lo, b.hi, b.seg, us);
+      (void)hipGetLastError();
+      if (b.nsmall && S->rt.gather_f32(S->c.arena, b.small, b.nsmall, b.seg_small, us) && !S->err) S->err = -64;
+      after(S, cs, us);
+      PSX_SCOMM(S, psx_comm_broadcast(S->c.comm, b.seg, b.seg_bytes, PSX_U8, 0, cs));
+    } else {  // fp32 segment = the arena slice itself, broadcast in place
+      apply_range(S, b.lo, b.hi, nullptr, us);
+      after(S, cs, us);
+      PSX_SCOMM(S, psx_comm_broadcast(S->c.comm, S->c.arena + b.lo, b.seg_bytes, PSX_U8, 0, cs));
+    }
+  };
+  for (int k = 0; k < S->c.nbuckets; ++k) {
+    issue_gather(k);
+    if (k > 0) finish(k - 1);
+  }
+  finish(S->c.nbuckets - 1);
+  after(S, us, cs);  // the round ends when its broadcasts are done (next round's applies after them)
+  record_round(S, t0);
+}
+
+}  // namespace
+
+extern "C" {
+
+int psx_sync_cfg_size() { return (int)sizeof(PsxSyncCfg); }
+int psx_sync_bucket_size() { return (int)sizeof(PsxSyncBucket); }
+
+void* psx_sync_create(const PsxSyncCfg* cfg, const char* runtime_path, const char* kernels_path) {
+  void* rt = dlopen(runtime_path, RTLD_NOW | RTLD_NOLOAD);
+  if (!rt) rt = dlopen(runtime_path, RTLD_NOW);
+  void* kn = dlopen(kernels_path, RTLD_NOW | RTLD_NOLOAD);
+  if (!kn) kn = dlopen(kernels_path, RTLD_NOW);
+  if (!rt || !kn) {
+    fprintf(stderr, "psx_sync_create: %s\n", dlerror());
+    return nullptr;
+  }
+  if (cfg->nworkers < 1 || cfg->nworkers > 32 || !cfg->comm ||
+      (cfg->nbuckets > 0 && (!cfg->buckets || !cfg->comm_stream || !cfg->full_wire))) {
+    fprintf(stderr, "psx_sync_create: invalid configuration\n");
+    return nullptr;
+  }
+  PsxSync* S = new PsxSync();
+  S->c = *cfg;
+  SyncRt& r = S->rt;
+  const bool ok = bindf(rt, "psx_ps_on_fetch", &r.ps_on_fetch) && bindf(rt, "psx_ps_on_push", &r.ps_on_push) &&
+                  bindf(rt, "psx_ps_on_applied", &r.ps_on_applied) &&
+                  bindf(rt, "psx_ps_global_step", &r.ps_global_step) &&
+                  bindf(kn, "psx_sgd_apply_multi", &r.sgd_apply_multi) && bindf(kn, "psx_gather_f32", &r.gather_f32);
+  if (!ok) {
+    delete S;
+    return nullptr;
+  }
+  return S;
+}
+
+// Runs `rounds` sync rounds (blocking the calling thread; ctypes releases the GIL) and returns
+// 0 or the first error. The device work of the last round may still be in flight on return
+// (psx_sync_drain waits for it).
+int psx_sync_run(void* h, long long rounds) {
+  PsxSync* S = (PsxSync*)h;
+  hipStreamCaptureMode cm = hipStreamCaptureModeRelaxed;
+  PSX_SHIP(S, hipThreadExchangeStreamCaptureMode(&cm));
+  for (long long r = 0; r < rounds && !S->err; ++r) {
+    if (S->c.nbuckets > 0)
+      overlap_round(S);
+    else
+      serial_round(S);
+    hipEvent_t ev;
+    PSX_SHIP(S, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    PSX_SHIP(S, hipEventRecord(ev, S->c.upd_stream));
+    S->inflight.push_back(ev);
+    S->issued.fetch_add(1);
+    retire(S, 2);  // at most two rounds in flight on the device
+  }
+  return S->err;
+}
+
+int psx_sync_drain(void* h) {
+  PsxSync* S = (PsxSync*)h;
+  retire(S, 0);
+  return S->err;
+}
+
+// [rounds issued, rounds whose device work completed] (the liveness watchdog's progress)
+void psx_sync_progress(void* h, long long* out) {
+  PsxSync* S = (PsxSync*)h;
+  out[0] = S->issued.load();
+  out[1] = S->done.load();
+}
+
+int psx_sync_mom_first(void* h) { return ((PsxSync*)h)->c.mom_first; }
+int psx_sync_primed(void* h) { return ((PsxSync*)h)->c.primed; }
+
+void psx_sync_destroy(void* h) {
+  PsxSync* S = (PsxSync*)h;
+  if (!S) return;
+  for (hipEvent_t ev : S->inflight) hipEventDestroy(ev);
+  delete S;
+}
+
+}  // extern "C"

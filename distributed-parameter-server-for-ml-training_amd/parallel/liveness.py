@@ -44,6 +44,8 @@ class RoundWatchdog:
         self.rounds_done = 0
         self.expired = False
         self._stop = threading.Event()
+        self._follow = None       # native run: progress_fn() -> (rounds issued, rounds completed)
+        self._follow_done = -1
         self._thread = None
         if self.timeout_s > 0:
             self._thread = threading.Thread(target=self._run, name="psx-round-watchdog", daemon=True)
@@ -68,10 +70,26 @@ class RoundWatchdog:
             else:
                 self._events.append(event)
 
+    def follow(self, progress_fn):
+        """Watch a native run of rounds (parallel/native_sync.py) instead of bracketed calls:
+        ``progress_fn() -> (issued, completed)``; None ends it. While it is set, the watchdog
+        expires when the completed count does not move for ``timeout_s``."""
+        with self._lock:
+            self._follow = progress_fn
+            self._follow_done = -1
+            self._progress = time.monotonic()
+
     # ---- watchdog thread
     def _poll(self) -> bool:
         """Retire completed rounds; True when the oldest outstanding one is overdue."""
         with self._lock:
+            if self._follow is not None:
+                _, done = self._follow()
+                if done != self._follow_done:
+                    self._follow_done = done
+                    self._progress = time.monotonic()
+                    self.rounds_done = done
+                return time.monotonic() - self._progress > self.timeout_s
             while self._events and self._events[0].query():
                 self._events.popleft()
                 self._progress = time.monotonic()

@@ -218,7 +218,7 @@ def run_distributed(cfg, log=print) -> dict:
             wk.connect_to_server()
             wk.run_training(skip_steps=done)
         else:
-            _dedicated_sync_server(cfg, server, chan, steps, device, skip=done)
+            _dedicated_sync_server(cfg, server, chan, steps, device, skip=done, t=t)
     else:
         sess = AsyncSession(cfg, t, rank, worker_ranks, server, comp if is_worker else None, train, test, names, lg)
         sess.run_training(skip_steps=done // max(1, W))
@@ -384,10 +384,39 @@ def make_local_channel(cfg, server, layout, device, emit_on_last: bool = False):
     return InProcessChannel(server, emit_on_last=emit_on_last, wire=wire)
 
 
-def _dedicated_sync_server(cfg, server, chan, steps, device, skip=0):
-    """Rank 0 of the dedicated topology: takes part in every round's collectives with a zero
-    gradient contribution and applies the averaged update."""
+def _sync_rounds(cfg, steps, skip_b):
+    """Rounds a worker runs (fetch + push every K-th batch of an epoch, --max-steps) from its
+    batch ``skip_b`` on: the dedicated server takes part in exactly these."""
     K = max(1, cfg.sync_steps)
+    rounds, done = 0, skip_b
+    for epoch in range(cfg.epochs):
+        for b in range(steps):
+            if epoch * steps + b < skip_b:
+                continue
+            if b % K == 0:
+                rounds += 1
+            done += 1
+            if cfg.max_steps and done >= cfg.max_steps:
+                return rounds
+    return rounds
+
+
+def _dedicated_sync_server(cfg, server, chan, steps, device, skip=0, t=None):
+    """Rank 0 of the dedicated topology: takes part in every round's collectives with a zero
+    gradient contribution and applies the averaged update — all rounds in one native call
+    (parallel/native_sync.py) on the native transport, else per round in Python."""
+    K = max(1, cfg.sync_steps)
+    from .native_sync import NativeSyncServer, native_sync_enabled
+
+    if t is not None and native_sync_enabled(cfg, t, chan, server, getattr(t, "rank", 0)):
+        srv = NativeSyncServer(server, t, chan)
+        try:
+            srv.run(_sync_rounds(cfg, steps, rounds_to_batches(skip, steps, K)), watchdog=chan.watchdog)
+        finally:
+            srv.close()
+        if hasattr(chan, "drain"):
+            chan.drain()
+        return
     if cfg.codec == "topk":
         from .topk import empty_payload
 

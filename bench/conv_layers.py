@@ -1,4 +1,4 @@
-"""Per-layer conv kernel timing (ResNet-18 CIFAR shapes, batch 128): v1 vs v2 fwd/dgrad, wgrad,
+"""Per-layer conv kernel timing (ResNet-18 CIFAR shapes, batch 128): fwd / dgrad / wgrad (+ reduce)
 and MIOpen (torch channels_last bf16) for reference. Prints one JSON line per layer."""
 import json
 import os
@@ -49,20 +49,10 @@ def main():
         ws = torch.empty(max(n1, n2, 4) // 4, device="cuda")
         flops = 2.0 * B * oh * oh * cout * cin * k * k
         r = {"shape": [cin, cout, hw, k, s], "gflop": round(flops / 1e9, 3)}
-        r["fwd_v1_us"] = t_us(lambda: K.conv_fwd(xh, wf, y, stats, B, hw, hw, cp, cout, k, s, p, kg))
         r["fwd_v2_us"] = t_us(lambda: K.conv_fwd2(xh, wf, y, stats, ws, B, hw, hw, cp, cout, k, s, p, kg))
         if cin != 3:
-            r["dgrad_v1_us"] = t_us(lambda: K.conv_dgrad(dy, wd, dx, None, B, hw, hw, cp, cout, k, s, p, kgd))
             r["dgrad_v2_us"] = t_us(lambda: K.conv_dgrad2(dy, wd, dx, None, ws, B, hw, hw, cp, cout, k, s, p, kgd))
-        spl = K.conv_wgrad_splits(B, hw, hw, cp, cout, k, s, p, kg)
-        part = torch.empty(spl * cout * kg, device="cuda")
         out16 = torch.empty(cout * cin * k * k, dtype=torch.float16, device="cuda")
-
-        def wg():
-            K.conv_wgrad(xh, dy, part, B, hw, hw, cp, cout, k, s, p, kg, spl)
-            K.wgrad_reduce(part, spl, cout, kg, cin, cp, k, 1.0, out16.data_ptr(), True)
-
-        r["wgrad_us"] = t_us(wg)
         spl2 = K.conv_wgrad2_splits(B, hw, hw, cp, cout, k, s, p, kg)
         part2 = torch.empty(spl2 * cout * kg, device="cuda")
 

@@ -561,9 +561,13 @@ int psx_wino_wgrad_q(int N, int H, int W, int C, int K) {
   if (!psx_wino_ok(H, W, C, K) || T % 32) return 0;
   const int bt = wino_wtile(C, K);
   int q = 1;
+  static const int qmax = [] {
+    const char* e = getenv("PSX_WINO_WQ_MAX");
+    return e && atoi(e) > 0 ? atoi(e) : 4;
+  }();
   if (const char* e = getenv("PSX_WINO_WQ"); e && atoi(e) > 0) q = atoi(e);
   else
-    while (36L * q * (C / bt) * (K / bt) < 1024 && q < 4 && T % (32 * 2 * q) == 0 && T / (2 * q) >= 256) q *= 2;
+    while (36L * q * (C / bt) * (K / bt) < 1024 && q < qmax && T % (32 * 2 * q) == 0 && T / (2 * q) >= 256) q *= 2;
   return T % (32 * q) ? 0 : q;
 }
 

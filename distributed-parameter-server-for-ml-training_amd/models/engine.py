@@ -186,13 +186,8 @@ class HipResNetEngine:
         self.graph = None
         self.graphs = None
         self.segments = None  # backward split points (set_segments), None = one segment
-        # conv kernel generation: 2 = LDS-DMA pipelined + split-K (default), 1 = register-staged
-        # (bf16 only)
-        self.conv_impl = int(os.environ.get("PSX_CONV_IMPL", "2"))
-        if self.f32 and self.conv_impl != 2:
-            raise ValueError("the fp32 path runs on the v2 conv kernels (PSX_CONV_IMPL=2)")
         # BN finalize inside the producing launch (csrc/kernels/bnfin.hpp); 0 = separate kernels
-        self.fuse_fin = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNFIN", "0") == "1"
+        self.fuse_fin = os.environ.get("PSX_FUSE_BNFIN", "0") == "1"
         # BN-backward sums from the dgrad epilogue (skips the separate bn_bwd_reduce pass where a
         # dgrad produces the BN's input gradient): neutral with 32 stat slots + separate finalize
         # (2.215 vs 2.217 ms/step), a small win with 8 slots + folded finalize (1.996/2.000 vs
@@ -202,7 +197,7 @@ class HipResNetEngine:
         # launches per step. With 32 slot rows it measured slower (2.18 vs 2.10 ms/step); with 8
         # rows (csrc/kernels/common.hpp) it wins: 1.999 vs 2.019 ms/step. PSX_BNFIN_APPLY=0: off
         self.fin_apply = not self.fuse_fin and os.environ.get("PSX_BNFIN_APPLY", "1") == "1"
-        self.fuse_bnbwd = self.conv_impl == 2 and os.environ.get("PSX_FUSE_BNBWD", "1") == "1"
+        self.fuse_bnbwd = os.environ.get("PSX_FUSE_BNBWD", "1") == "1"
         self._prereduced = set()
         # with the fused sums the dgrad epilogue already reads the ReLU mask operand o: it stores
         # dz = g*[o > 0] instead of g (bwd_stats_desc mask_store), the BN-backward apply then runs
@@ -310,12 +305,9 @@ class HipResNetEngine:
 
         def track(cs: ConvSpec):
             # fp32 scratch: wgrad split-K partials (own buffer: wgrad may run on a side stream)
-            # and conv v2 split-K slabs (stream-ordered on the main stream)
+            # and conv split-K slabs (stream-ordered on the main stream)
             nonlocal max_wg, max_wp
-            if self.conv_impl == 2:
-                s = K.conv_wgrad2_splits(B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg, self.f32)
-            else:
-                s = K.conv_wgrad_splits(B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
+            s = K.conv_wgrad2_splits(B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg, self.f32)
             cs.splits = s
             oh, ow = cs.out_hw
             cs.wp = s * cs.cout * cs.kg  # fp32 partials of this layer (offset wp_off: _plan_wpart)
@@ -515,12 +507,8 @@ class HipResNetEngine:
             elif not self._fold:  # no in-launch finalize on this path
                 self._bn_train(bs, arena, self.nslots, npix)
             return
-        if self.conv_impl == 2:
-            K.conv_fwd2(x, wf, y, stats, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
-                        cs.kg, fin=fin)
-        else:
-            K.conv_fwd(x, wf, y, stats, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg,
-                       K.pick_tile(cs.cout, npix))
+        K.conv_fwd2(x, wf, y, stats, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
+                    cs.kg, fin=fin)
         if not train:
             self._bn_eval(bs, arena)
         elif fin is None and not self._fold:
@@ -613,10 +601,7 @@ class HipResNetEngine:
                          self.layout.grad_view(self.grads, f"{cs.name}.weight"), self.B, cs.h, cs.w, cs.cp, cs.cout)
             return
         part = self.wpart_w[cs.wp_off:cs.wp_off + cs.wp]
-        if self.conv_impl == 2:
-            K.conv_wgrad2(x, dy, part, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
-        else:
-            K.conv_wgrad(x, dy, part, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg, cs.splits)
+        K.conv_wgrad2(x, dy, part, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
         item = (part, cs.splits, cs.cout, cs.kg, cs.cin, cs.cp, cs.k, self._gptr(f"{cs.name}.weight"))
         if self._wr_batch is not None and K.wgrad_reduce_batchable(cs.cp, cs.k):
             self._wr_batch.append(item)  # reduced with the block's other layers (_flush_reduces)
@@ -635,10 +620,6 @@ class HipResNetEngine:
         """bn_next = (BNSpec, o, y, two|None): the BN whose backward consumes dx; with conv v2 its
         reduction (sum dz, sum dz*xhat) is produced by the dgrad epilogue (PSX_FUSE_BNBWD)."""
         wl = self.wino_layers.get(cs.name)
-        if self.conv_impl != 2:
-            wd = self.wbuf[cs.wd_off:cs.wd_off + cs.cp * cs.kgd]
-            K.conv_dgrad(dy, wd, dx, res, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kgd)
-            return
         bst = None
         if bn_next is not None and self.fuse_bnbwd:
             bs, o, y, two = bn_next

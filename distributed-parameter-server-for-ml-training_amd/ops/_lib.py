@@ -41,9 +41,6 @@ class HipError(RuntimeError):
 
 # name -> (restype, [argtypes])
 _KERNEL_SIGS = {
-    "psx_conv_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
-    "psx_conv_dgrad": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
-    "psx_conv_wgrad": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
     "psx_wgrad_reduce": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, f32, vp, i32, vp]),
     "psx_wgrad_reduce_batch": (i32, [i32, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, vp]),
     "psx_conv2_workspace": (i64, [i32, i32, i32, i32, i32, i32]),

@@ -17,48 +17,11 @@ import torch
 
 from ._lib import check, kernels, ptr, stream_ptr
 
-# conv tile configurations (must match csrc/kernels/conv_gemm.hip dispatch_tile)
-TILE_CFGS = {0: (64, 128), 1: (128, 128), 2: (64, 64), 3: (128, 64)}
-
-
-def pick_tile(oc: int, npix: int) -> int:
-    """Output-channel x pixel tile for conv fwd/dgrad: fill >= 256 CUs with >= 1-2 waves of tiles."""
-    if oc % 128 == 0 and (oc // 128) * -(-npix // 128) >= 512:
-        return 1
-    if (oc // 64) * -(-npix // 128) >= 256:
-        return 0
-    if oc % 128 == 0 and (oc // 128) * -(-npix // 64) >= 256:
-        return 3
-    return 2
-
-
 def conv_out_hw(h: int, w: int, k: int, stride: int, pad: int):
     return (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
 
 
 STAT_SLOTS = 8  # PSX_STAT_SLOTS in csrc/kernels/common.hpp
-
-
-def conv_fwd_ntiles(oc: int, npix: int, cfg: int) -> int:
-    """Rows of the BN-statistics slab the conv epilogue accumulates into (pre-zeroed)."""
-    return STAT_SLOTS
-
-
-def conv_fwd(x, wf, y, stats, nb, h, w, ic, oc, k, stride, pad, kg, cfg=None):
-    p, q = conv_out_hw(h, w, k, stride, pad)
-    if cfg is None:
-        cfg = pick_tile(oc, nb * p * q)
-    nt = C.c_int(0)
-    check(kernels().psx_conv_fwd(ptr(x), ptr(wf), ptr(y), ptr(stats), nb, h, w, ic, oc, k, k, stride, pad, kg, cfg,
-                                 C.byref(nt), stream_ptr()), "conv_fwd")
-    return nt.value
-
-
-def conv_dgrad(dy, wd, dx, res, nb, h, w, ic_fwd, oc_fwd, k, stride, pad, kgd, cfg=None):
-    if cfg is None:
-        cfg = pick_tile(ic_fwd, nb * h * w)
-    check(kernels().psx_conv_dgrad(ptr(dy), ptr(wd), ptr(dx), ptr(res), nb, h, w, ic_fwd, oc_fwd, k, k, stride, pad,
-                                   kgd, cfg, stream_ptr()), "conv_dgrad")
 
 
 _ZERO_PAGES = {}
@@ -278,21 +241,6 @@ def conv_wgrad2(x, dy, part, nb, h, w, ic, oc, k, stride, pad, kg) -> int:
                                   stride, pad, kg, is_f32(x), stream_ptr())
     if n <= 0:
         raise RuntimeError(f"conv_wgrad2 failed ({n})")
-    return n
-
-
-def conv_wgrad_splits(nb, h, w, ic, oc, k, stride, pad, kg, splits=0) -> int:
-    n = kernels().psx_conv_wgrad(None, None, None, nb, h, w, ic, oc, k, k, stride, pad, kg, splits, None)
-    if n <= 0:
-        raise RuntimeError(f"conv_wgrad split query failed ({n})")
-    return n
-
-
-def conv_wgrad(x, dy, part, nb, h, w, ic, oc, k, stride, pad, kg, splits) -> int:
-    n = kernels().psx_conv_wgrad(ptr(x), ptr(dy), ptr(part), nb, h, w, ic, oc, k, k, stride, pad, kg, splits,
-                                 stream_ptr())
-    if n <= 0:
-        raise RuntimeError(f"conv_wgrad failed ({n})")
     return n
 
 

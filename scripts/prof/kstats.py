@@ -1,7 +1,7 @@
 """Per-kernel summary from a rocprofv3 kernel trace, restricted to the last N steps
 (steps delimited by a marker kernel), grouped by kernel template.
 
-usage: python scripts/dev/kstats.py run_kernel_trace.csv|run_results.db [--steps 20] [--marker augment]
+usage: python scripts/prof/kstats.py run_kernel_trace.csv|run_results.db [--steps 20] [--marker augment]
 (rocprofv3 writes a rocpd SQLite database by default, a CSV with --output-format csv)
 """
 import argparse

@@ -68,48 +68,6 @@ R18_SHAPES = [
 
 
 @pytest.mark.parametrize("shape", R18_SHAPES)
-def test_conv_fwd_and_stats(shape):
-    torch.manual_seed(0)
-    n, cin, cout, hw, k, s, p = shape
-    x = torch.randn(n, cin, hw, hw, device=DEV).to(torch.bfloat16).float()
-    w = (torch.randn(cout, cin, k, k, device=DEV) / (cin * k * k) ** 0.5).to(torch.bfloat16).float()
-    wf, wd, cp, kg, kgd = make_operands(w)
-    xh = to_nhwc(x, cp)
-    oh = (hw + 2 * p - k) // s + 1
-    y = torch.empty(n, oh, oh, cout, dtype=torch.bfloat16, device=DEV)
-    npix = n * oh * oh
-    for cfg in (0, 1, 2, 3):
-        if K.TILE_CFGS[cfg][0] > cout or cout % K.TILE_CFGS[cfg][0]:
-            continue
-        T = K.conv_fwd_ntiles(cout, npix, cfg)
-        stats = torch.zeros(T, 2, cout, device=DEV)
-        K.conv_fwd(xh, wf, y, stats, n, hw, hw, cp, cout, k, s, p, kg, cfg)
-        ref = F.conv2d(x, w, stride=s, padding=p).permute(0, 2, 3, 1)
-        assert _rel(y, ref) < 1e-2, (shape, cfg)
-        yq = y.float().reshape(-1, cout)
-        assert torch.allclose(stats[:, 0].sum(0), yq.sum(0), rtol=1e-3, atol=1e-2), (shape, cfg)
-        assert torch.allclose(stats[:, 1].sum(0), (yq * yq).sum(0), rtol=1e-3, atol=1e-2), (shape, cfg)
-
-
-@pytest.mark.parametrize("shape", [s for s in R18_SHAPES if s[1] != 3])
-def test_conv_dgrad(shape):
-    torch.manual_seed(1)
-    n, cin, cout, hw, k, s, p = shape
-    w = (torch.randn(cout, cin, k, k, device=DEV) / (cin * k * k) ** 0.5).to(torch.bfloat16).float()
-    wf, wd, cp, kg, kgd = make_operands(w)
-    oh = (hw + 2 * p - k) // s + 1
-    dy = torch.randn(n, cout, oh, oh, device=DEV).to(torch.bfloat16).float()
-    ref = torch.nn.grad.conv2d_input((n, cin, hw, hw), w, dy, stride=s, padding=p).permute(0, 2, 3, 1)
-    dx = torch.empty(n, hw, hw, cp, dtype=torch.bfloat16, device=DEV)
-    K.conv_dgrad(to_nhwc(dy, cout), wd, dx, None, n, hw, hw, cp, cout, k, s, p, kgd)
-    assert _rel(dx[..., :cin], ref) < 1e-2, shape
-    # residual-add epilogue
-    res = torch.randn(n, hw, hw, cp, device=DEV).to(torch.bfloat16)
-    K.conv_dgrad(to_nhwc(dy, cout), wd, dx, res, n, hw, hw, cp, cout, k, s, p, kgd)
-    assert _rel(dx[..., :cin], ref + res[..., :cin].float()) < 1e-2, shape
-
-
-@pytest.mark.parametrize("shape", R18_SHAPES)
 def test_conv_wgrad(shape):
     torch.manual_seed(2)
     n, cin, cout, hw, k, s, p = shape
@@ -119,9 +77,11 @@ def test_conv_wgrad(shape):
     ref = torch.nn.grad.conv2d_weight(x, (cout, cin, k, k), dy, stride=s, padding=p)
     cp = _pow2(cin)
     kg = -(-(k * k * cp) // 64) * 64
-    splits = K.conv_wgrad_splits(n, hw, hw, cp, cout, k, s, p, kg)
+    # the split slabs of the weight-gradient mainloop (conv v2, tests/test_conv_v2_gpu.py for the
+    # kernel itself) through both reductions: fp32 and the fp16 wire
+    splits = K.conv_wgrad2_splits(n, hw, hw, cp, cout, k, s, p, kg)
     part = torch.zeros(splits * cout * kg, device=DEV)
-    got = K.conv_wgrad(to_nhwc(x, cp), to_nhwc(dy, cout), part, n, hw, hw, cp, cout, k, s, p, kg, splits)
+    got = K.conv_wgrad2(to_nhwc(x, cp), to_nhwc(dy, cout), part, n, hw, hw, cp, cout, k, s, p, kg)
     assert got == splits
     out = torch.zeros(cout * cin * k * k, device=DEV)
     K.wgrad_reduce(part, splits, cout, kg, cin, cp, k, 1.0, out.data_ptr(), False)

@@ -1,4 +1,4 @@
-"""Batched weight-gradient reduction (csrc/kernels/conv_gemm.hip wgrad_reduce2_batch_kernel):
+"""Batched weight-gradient reduction (csrc/kernels/wgrad_reduce.hip wgrad_reduce2_batch_kernel):
 one launch reducing several layers' split-K partials gives bit-identical OIHW gradients to one
 wgrad_reduce launch per layer, for fp16 and fp32 outputs; and an engine step with the batched
 reduction produces the same gradients as with per-layer reductions (up to the fp32-atomic BN

@@ -26,7 +26,9 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
                                                           float* __restrict__ run_mean, float* __restrict__ run_var,
                                                           float* __restrict__ scale, float* __restrict__ shift,
                                                           float* __restrict__ save_mean,
-                                                          float* __restrict__ save_invstd) {
+                                                          float* __restrict__ save_invstd,
+                                                          const float* __restrict__ sshift,
+                                                          float* __restrict__ sshift_next) {
   // 8 slot groups x 32 channels per block (T slot rows read with 8-way parallelism)
   __shared__ double red[2][8][32];
   const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
@@ -48,15 +50,15 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
       s += red[0][g][cl];
       ss += red[1][g][cl];
     }
-    const double mean = s / count;
-    double var = ss / count - mean * mean;
-    if (var < 0.0) var = 0.0;
+    double mean, var;  // shifted sums (bnfin.hpp BnFin::sshift)
+    bn_moments(s, ss, count, sshift ? sshift[c] : 0.f, mean, var);
     const float invstd = (float)(1.0 / sqrt(var + (double)eps));
     const float sc = gamma[c] * invstd;
     scale[c] = sc;
     shift[c] = beta[c] - (float)mean * sc;
     save_mean[c] = (float)mean;
     save_invstd[c] = invstd;
+    if (sshift_next) sshift_next[c] = (float)mean;
     if (run_mean) {
       const double unb = count > 1.f ? var * count / (count - 1.0) : var;
       run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
@@ -466,9 +468,9 @@ int psx_set_deterministic(void* buf, long bytes) {
 
 int psx_bn_finalize(const float* part, int T, int C, float count, const float* gamma, const float* beta, float eps,
                     float momentum, float* run_mean, float* run_var, float* scale, float* shift, float* save_mean,
-                    float* save_invstd, hipStream_t st) {
+                    float* save_invstd, const float* sshift, float* sshift_next, hipStream_t st) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, st, part, T, C, count, gamma, beta, eps,
-                     momentum, run_mean, run_var, scale, shift, save_mean, save_invstd);
+                     momentum, run_mean, run_var, scale, shift, save_mean, save_invstd, sshift, sshift_next);
   return (int)hipGetLastError();
 }
 

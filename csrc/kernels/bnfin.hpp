@@ -29,7 +29,21 @@ struct BnFin {  // forward: batch statistics -> affine (+ running statistics)
   unsigned* counter;
   float count, eps, momentum;
   int C;
+  // Shifted sums (nullable = 0): the producer summed (x - k_c) and (x - k_c)^2 with k = sshift,
+  // the previous step's batch mean, so the variance E[(x-k)^2] - E[x-k]^2 never cancels two
+  // large numbers (|mean| >> std); the finalize writes this batch's mean to sshift_next, which
+  // becomes the next step's sshift (engine.py: copied by the next step's first launch).
+  const float* sshift;
+  float* sshift_next;
 };
+
+// batch moments from the (shifted) sums: mean = k + s/n, var = ss/n - (s/n)^2 (biased)
+PSX_DEV void bn_moments(double s, double ss, float count, float k, double& mean, double& var) {
+  const double m1 = s / count;
+  mean = (double)k + m1;
+  var = ss / count - m1 * m1;
+  if (var < 0.0) var = 0.0;
+}
 
 struct BnBwdFin {  // backward: sum(dz), sum(dz*xhat) -> coefficients + dgamma/dbeta
   const float* gamma;
@@ -173,15 +187,15 @@ PSX_DEV void bn_finalize_block(const float* part, const BnFin& f) {
       s += v1[t];
       ss += v2[t];
     }
-    const double mean = s / f.count;
-    double var = ss / f.count - mean * mean;
-    if (var < 0.0) var = 0.0;
+    double mean, var;
+    bn_moments(s, ss, f.count, f.sshift ? f.sshift[c] : 0.f, mean, var);
     const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
     const float sc = f.gamma[c] * invstd;
     f.scale[c] = sc;
     f.shift[c] = f.beta[c] - (float)mean * sc;
     f.save_mean[c] = (float)mean;
     f.save_invstd[c] = invstd;
+    if (f.sshift_next) f.sshift_next[c] = (float)mean;
     if (f.run_mean) {
       const double unb = f.count > 1.f ? var * f.count / (f.count - 1.0) : var;
       f.run_mean[c] = (1.f - f.momentum) * f.run_mean[c] + f.momentum * (float)mean;
@@ -291,10 +305,8 @@ template <int T>
 PSX_DEV void bn_fin_lds(const float* part, const BnFin& f, float* sc, float* sh, double* red, float* scratch) {
   slot_reduce2<T>(part, 2, 0, 1, f.C, red, scratch);
   for (int c = threadIdx.x; c < f.C; c += 256) {
-    const double s = red[c], ss = red[f.C + c];
-    const double mean = s / f.count;
-    double var = ss / f.count - mean * mean;
-    if (var < 0.0) var = 0.0;
+    double mean, var;
+    bn_moments(red[c], red[f.C + c], f.count, f.sshift ? f.sshift[c] : 0.f, mean, var);
     const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
     const float scv = f.gamma[c] * invstd, shv = f.beta[c] - (float)mean * scv;
     sc[c] = scv;
@@ -304,6 +316,7 @@ PSX_DEV void bn_fin_lds(const float* part, const BnFin& f, float* sc, float* sh,
       f.shift[c] = shv;
       f.save_mean[c] = (float)mean;
       f.save_invstd[c] = invstd;
+      if (f.sshift_next) f.sshift_next[c] = (float)mean;
       if (f.run_mean) {
         const double unb = f.count > 1.f ? var * f.count / (f.count - 1.0) : var;
         f.run_mean[c] = (1.f - f.momentum) * f.run_mean[c] + f.momentum * (float)mean;

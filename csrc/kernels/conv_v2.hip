@@ -71,6 +71,9 @@ struct Conv2Args {
   int bmask;
   DetRed det;  // deterministic mode: the launch's row slab (bnfin.hpp)
   int wH, wW;  // WOUT: the output image (Winograd tiles t = (n, ti, tj) of 4x4 pixels)
+  // forward statistics: per-channel shift k subtracted before summing (nullable = 0; bnfin.hpp
+  // BnFin::sshift): the slots hold sum(y - k), sum((y - k)^2)
+  const float* sshift;
 };
 
 // Winograd F(4x4,3x3) output-transform coefficients: y[i][j] = sum_b kWinoAT2[b][4 i + j] P[b],
@@ -564,10 +567,11 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     const int t = pix0 + wn * (BN / WGN) + (lane & 15);
     const bool bwd = a.bpart != nullptr, two = a.by2 != nullptr, st = a.stats != nullptr;
     float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f}, s3[4] = {0.f, 0.f, 0.f, 0.f};
-    float bm1[4], bi1[4], bm2[4], bi2[4];
+    float bm1[4], bi1[4], bm2[4], bi2[4], ksh[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       bm1[e] = bi1[e] = bm2[e] = bi2[e] = 0.f;
+      ksh[e] = (st && a.sshift) ? a.sshift[oc + e] : 0.f;
       if (bwd) {
         bm1[e] = a.bsaved1[oc + e];
         bi1[e] = a.bsaved1[a.OC + oc + e];
@@ -606,8 +610,9 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
             *reinterpret_cast<f32x4*>((float*)a.out + off) = v;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              s1[e] += v[e];
-              s2[e] += v[e] * v[e];
+              const float d = v[e] - ksh[e];
+              s1[e] += d;
+              s2[e] += d * d;
             }
           }
         }
@@ -674,11 +679,12 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     __syncthreads();
     const bool bwd = a.bpart != nullptr, two = a.by2 != nullptr, st = a.stats != nullptr;
     const int cc = tid % CPR, ch0 = oc0 + cc * 8;
-    float s1[8], s2[8], s3[8], bm1[8], bi1[8], bm2[8], bi2[8];
+    float s1[8], s2[8], s3[8], bm1[8], bi1[8], bm2[8], bi2[8], ksh[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       s1[i] = s2[i] = s3[i] = 0.f;
       bm1[i] = bi1[i] = bm2[i] = bi2[i] = 0.f;
+      ksh[i] = (st && a.sshift) ? a.sshift[ch0 + i] : 0.f;
       if (bwd) {
         bm1[i] = a.bsaved1[ch0 + i];
         bi1[i] = a.bsaved1[a.OC + ch0 + i];
@@ -710,8 +716,9 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       if (st) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          s1[k] += v[k];
-          s2[k] += v[k] * v[k];
+          const float d = v[k] - ksh[k];
+          s1[k] += d;
+          s2[k] += d * d;
         }
       }
       if (bwd) {
@@ -794,7 +801,7 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
                                                             const T* __restrict__ by2,
                                                             const float* __restrict__ bsaved1,
                                                             const float* __restrict__ bsaved2, int bns,
-                                                            int bmask, DetRed det) {
+                                                            int bmask, DetRed det, const float* __restrict__ sshift) {
   extern __shared__ __attribute__((aligned(16))) float sred[];  // [256][24]
   const int cvec = OC >> 3, tpp = 256 / cvec;
   const int cg = threadIdx.x % cvec, pr = threadIdx.x / cvec;
@@ -802,10 +809,11 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
   // per-thread partial sums: fwd stats (sum, sumsq) or fused BN-backward (dz, dz*xh1, dz*xh2)
   const bool bwd = bpart != nullptr, two = by2 != nullptr;
   const int nst = bwd ? bns : 2;
-  float st[3][8], m1[8], i1[8], m2[8], i2[8];
+  float st[3][8], m1[8], i1[8], m2[8], i2[8], ksh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     st[0][j] = st[1][j] = st[2][j] = 0.f;
+    ksh[j] = (stats && sshift) ? sshift[cg * 8 + j] : 0.f;
     if (bwd) {
       m1[j] = bsaved1[cg * 8 + j];
       i1[j] = bsaved1[OC + cg * 8 + j];
@@ -835,8 +843,9 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
     if (stats) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        st[0][j] += v[j];
-        st[1][j] += v[j] * v[j];
+        const float d = v[j] - ksh[j];
+        st[0][j] += d;
+        st[1][j] += d * d;
       }
     } else if (bwd) {
       float om[8], yv[8], y2v[8];
@@ -1040,11 +1049,11 @@ int finish_split(const Conv2Args& a, hipStream_t st) {
   if (a.res)
     hipLaunchKernelGGL((conv_splitk_epilogue<T, true>), dim3(grid), dim3(256), lds, st, a.part, a.splits, a.npix,
                        a.OC, (T*)a.out, (const T*)a.res, a.stats, ppb, a.fuse_fin, a.fin, a.bpart, (const T*)a.bo,
-                       (const T*)a.by1, (const T*)a.by2, a.bsaved1, a.bsaved2, a.bns, a.bmask, det);
+                       (const T*)a.by1, (const T*)a.by2, a.bsaved1, a.bsaved2, a.bns, a.bmask, det, a.sshift);
   else
     hipLaunchKernelGGL((conv_splitk_epilogue<T, false>), dim3(grid), dim3(256), lds, st, a.part, a.splits, a.npix,
                        a.OC, (T*)a.out, (const T*)nullptr, a.stats, ppb, a.fuse_fin, a.fin, a.bpart, (const T*)a.bo,
-                       (const T*)a.by1, (const T*)a.by2, a.bsaved1, a.bsaved2, a.bns, a.bmask, det);
+                       (const T*)a.by1, (const T*)a.by2, a.bsaved1, a.bsaved2, a.bns, a.bmask, det, a.sshift);
   return (int)hipGetLastError();
 }
 
@@ -1133,10 +1142,12 @@ long psx_conv2_workspace(int Nb, int OH, int OW, int OC, int Kg, int f32) {
 // fin (nullable, needs stats): the BN layer fed by this conv is finalized by the kernel's last
 // workgroup (bnfin.hpp) instead of a separate psx_bn_finalize launch.
 // f32: x, wf, y are fp32 (the reference's precision) instead of bf16.
+// sshift (nullable): per-channel shift of the BN statistics (Conv2Args::sshift)
 int psx_conv_fwd2(const void* x, const void* wf, void* y, float* stats, const void* zero, float* ws, int Nb, int H,
                   int W, int IC, int OC, int R, int S, int stride, int pad, int Kg, const BnFin* fin, int f32,
-                  hipStream_t st) {
+                  const float* sshift, hipStream_t st) {
   Conv2Args a{};
+  a.sshift = sshift;
   if (fin && stats) {
     if (fin->C != OC) return -10;
     a.fuse_fin = 1;
@@ -1192,7 +1203,8 @@ int psx_conv_dgrad2(const void* dy, const void* wd, void* dx, const void* res, c
 // [K][36][C] -> y [N][H][W][K] (+ res) with the BN statistics (stats) or the BN-backward sums
 // (bst, conv_v2 BwdStatsDesc) of y. 32x32 workgroup tiles (16x16 per wave); C a power of two >= 32.
 int psx_wino_gemm_out(const float* V, const float* U, float* y, const float* res, float* stats,
-                      const BwdStatsDesc* bst, const void* zero, int N, int H, int W, int C, int K, hipStream_t st) {
+                      const BwdStatsDesc* bst, const void* zero, int N, int H, int W, int C, int K,
+                      const float* sshift, hipStream_t st) {
   const int T = N * (H / 4) * (W / 4);
   if (K % 32 || C < kKS<float> || (C & (C - 1)) || H % 4 || W % 4 || T < 1) return -2;
   Conv2Args a{};
@@ -1201,6 +1213,7 @@ int psx_wino_gemm_out(const float* V, const float* U, float* y, const float* res
   a.out = y;
   a.res = res;
   a.stats = bst ? nullptr : stats;
+  a.sshift = sshift;
   a.zero = zero;
   if (bst) {
     a.bpart = bst->part;

@@ -65,12 +65,16 @@ struct AugArgs {
   long nzero0;      // slots and accuracy counter: two fewer launches per step)
   uint32_t* zero1;
   long nzero1;
+  const uint32_t* copy_src;  // optional word copy of the same launch: the BN statistic shifts
+  uint32_t* copy_dst;        // (bnfin.hpp BnFin::sshift) the previous step's finalizes wrote
+  long ncopy;
 };
 
 __global__ __launch_bounds__(256) void augment_kernel(AugArgs a) {
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < a.nzero0; i += stride) a.zero0[i] = 0u;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < a.nzero1; i += stride) a.zero1[i] = 0u;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < a.ncopy; i += stride) a.copy_dst[i] = a.copy_src[i];
   const long total = (long)a.B * a.H * a.W;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int b = (int)(i / (a.H * a.W));
@@ -143,8 +147,12 @@ int psx_synth_gen(void* img, int* labels, int N, int H, int W, int classes, unsi
 
 int psx_augment(const void* img, const int* labels, const int* index, void* out, int* out_labels, int B, int H, int W,
                 int pad, unsigned seed, const unsigned* step, int train, const float* mean3, const float* std3,
-                void* zero0, long nzero0, void* zero1, long nzero1, int f32, hipStream_t st) {
+                void* zero0, long nzero0, void* zero1, long nzero1, const void* copy_src, void* copy_dst, long ncopy,
+                int f32, hipStream_t st) {
   AugArgs a{};
+  a.copy_src = (const uint32_t*)copy_src;
+  a.copy_dst = (uint32_t*)copy_dst;
+  a.ncopy = copy_src && copy_dst ? ncopy : 0;
   a.zero0 = (uint32_t*)zero0;
   a.nzero0 = zero0 ? nzero0 : 0;
   a.zero1 = (uint32_t*)zero1;

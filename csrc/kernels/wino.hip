@@ -38,7 +38,8 @@
 extern "C" int psx_bgemm_f32(const float* A, const float* B, float* P, const void* zero, int M, int N, int Kd, int nb,
                              int cfg, hipStream_t st);
 extern "C" int psx_wino_gemm_out(const float* V, const float* U, float* y, const float* res, float* stats,
-                                 const void* bst, const void* zero, int N, int H, int W, int C, int K, hipStream_t st);
+                                 const void* bst, const void* zero, int N, int H, int W, int C, int K,
+                                 const float* sshift, hipStream_t st);
 extern "C" int psx_bgemm_tn_f32(const float* X, const float* D, float* part, const void* zero, int T, int C, int K,
                                 int nb, int q, int BR, int BC, hipStream_t st);
 
@@ -74,6 +75,8 @@ struct WinoBnFin {
   unsigned* counter;
   float count, eps, momentum;
   int C;
+  const float* sshift;  // shifted sums (bnfin.hpp BnFin::sshift)
+  float* sshift_next;
 };
 
 // V[b][t][c]: one thread per (tile, channel); block = 64 channels x 4 tiles.
@@ -95,9 +98,8 @@ __global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ 
       s += bnpart[(size_t)t * 2 * C + c];
       ss += bnpart[(size_t)t * 2 * C + C + c];
     }
-    const double mean = s / fin.count;
-    double var = ss / fin.count - mean * mean;
-    if (var < 0.0) var = 0.0;
+    double mean, var;
+    bn_moments(s, ss, fin.count, fin.sshift ? fin.sshift[c] : 0.f, mean, var);
     const float invstd = (float)(1.0 / sqrt(var + (double)fin.eps));
     sc = fin.gamma[c] * invstd;
     sh = fin.beta[c] - (float)mean * sc;
@@ -108,6 +110,7 @@ __global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ 
       fin.shift[c] = sh;
       fin.save_mean[c] = (float)mean;
       fin.save_invstd[c] = invstd;
+      if (fin.sshift_next) fin.sshift_next[c] = (float)mean;
       if (fin.run_mean) {
         const double unb = fin.count > 1.f ? var * fin.count / (fin.count - 1.0) : var;
         fin.run_mean[c] = (1.f - fin.momentum) * fin.run_mean[c] + fin.momentum * (float)mean;
@@ -263,7 +266,8 @@ struct WinoBwdStats {
 // reduces the rows in a fixed order (bnfin.hpp det_finish) into slot row 0.
 __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__ P, float* __restrict__ y,
                                                        const float* __restrict__ res, float* __restrict__ stats, int T,
-                                                       int H, int W, int K, WinoBwdStats bs, DetRed det) {
+                                                       int H, int W, int K, WinoBwdStats bs, DetRed det,
+                                                       const float* __restrict__ sshift) {
   __shared__ float red[3][4][64];
   const int kl = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + kl;
@@ -284,6 +288,7 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
     }
   }
   float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  const float kshift = (!bwd && sshift) ? sshift[k] : 0.f;  // forward statistics: shifted sums
   for (int t = blockIdx.y * 4 + ty; t < T; t += 4 * gridDim.y) {
     const float* pt = P + (size_t)t * K + k;
     float m[6][6];
@@ -318,8 +323,9 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
           y[off] = bs.mask_store ? dz : v;
         } else {
           y[off] = v;
-          s1 += v;
-          s2 += v * v;
+          const float d = v - kshift;
+          s1 += d;
+          s2 += d * d;
         }
       }
     }
@@ -517,7 +523,7 @@ int psx_wino_weights_multi(const float* const* w, float* const* U, const int* K,
 // floats. cfg: GEMM tile (psx_bgemm_f32).
 int psx_wino_conv(const float* x, const float* U, float* y, const float* res, float* stats, float* V, float* P,
                   const void* zero, int N, int H, int W, int C, int K, int cfg, const WinoBwdStats* bst,
-                  const float* bnpart, const WinoBnFin* bnfin, hipStream_t st) {
+                  const float* bnpart, const WinoBnFin* bnfin, const float* sshift, hipStream_t st) {
   if (bnpart && (!bnfin || bnfin->C != C)) return -3;
   if (!psx_wino_ok(H, W, C, K)) return -2;
   const int T = N * (H / 4) * (W / 4);
@@ -534,7 +540,7 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
   const int fused_mode = fe ? atoi(fe) : 0;
   if (K % 32 == 0 && !(bst && bst->mask_aff) &&
       (fused_mode == 2 || (fused_mode == 1 && (long)(K / 32) * ((T + 31) / 32) >= 256)))
-    return psx_wino_gemm_out(V, U, y, res, stats, bst, zero, N, H, W, C, K, st);
+    return psx_wino_gemm_out(V, U, y, res, stats, bst, zero, N, H, W, C, K, sshift, st);
   int e = psx_bgemm_f32(V, U, P, zero, T, K, C, 36, cfg, st);
   if (e) return e;
   WinoBwdStats bs{};
@@ -542,7 +548,7 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
   DetRed det{};
   if (bst || stats) det = det_next(gy, bst ? (bst->y2 ? 3 : 2) : 2, K, K / 64);
   hipLaunchKernelGGL(wino_out_kernel, dim3(K / 64, gy), dim3(256), 0, st, P, y, res, bst ? nullptr : stats, T, H, W,
-                     K, bs, det);
+                     K, bs, det, sshift);
   return (int)hipGetLastError();
 }
 

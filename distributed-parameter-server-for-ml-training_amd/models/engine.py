@@ -276,6 +276,15 @@ class HipResNetEngine:
         # fp32 atomics into PSX_STAT_SLOTS slot rows per BN layer; all slot rows live in one
         # buffer that is zeroed once at the start of every step (one memset node in the graph).
         self.nslots = K.bn_bwd_reduce_T(1, 64)
+        # BN statistic shifts (csrc/kernels/bnfin.hpp BnFin::sshift): the forward statistics are
+        # sums of (y - k) and (y - k)^2 with k = the layer's previous batch mean, so the variance
+        # never cancels two large numbers when |mean| >> std. Row 0 = this step's k (read-only
+        # during the step), row 1 = the batch means the finalizes write; the next training step's
+        # augment launch copies row 1 -> row 0. Zero at the first step (plain sums).
+        nshift = sp.stem_bn.c + sum(bs.c for b in sp.blocks for bs in b.bns) + \
+            sum(b.down[1].c for b in sp.blocks if b.down)
+        self.bn_shift = torch.zeros(2, nshift, dtype=torch.float32, device=self.dev)
+        shift_off = [0]
         # the first CTR words of the slot buffer are the in-launch finalize counters (two per BN
         # layer: forward, backward; csrc/kernels/bnfin.hpp) — zeroed with the slots every step
         nbn = 1 + sum(len(b.bns) + (1 if b.down else 0) for b in sp.blocks)
@@ -288,9 +297,12 @@ class HipResNetEngine:
             bwd = fwd + self.nslots * 2 * bs.c
             red_off[0] = bwd + self.nslots * 3 * bs.c
             nctr[0] += 2
+            so = shift_off[0]
+            shift_off[0] += bs.c
             self.bn[bs.name] = dict(affine=self._f32(2, bs.c), saved=self._f32(2, bs.c), coef=self._f32(3, bs.c),
                                     c=bs.c, fwd=(fwd, self.nslots * 2 * bs.c), bwd=(bwd, self.nslots * 3 * bs.c),
-                                    ctr=nctr[0] - 2)
+                                    ctr=nctr[0] - 2, sshift=self.bn_shift[0, so:so + bs.c],
+                                    sshift_next=self.bn_shift[1, so:so + bs.c])
 
         # activation / gradient buffers
         st = sp.stem_conv
@@ -474,7 +486,8 @@ class HipResNetEngine:
             st = self.bn[bs.name]
             f = K.bn_fin(self._aview(arena, f"{bs.name}.weight"), self._aview(arena, f"{bs.name}.bias"),
                          self._aview(arena, f"{bs.name}.running_mean"), self._aview(arena, f"{bs.name}.running_var"),
-                         st["affine"], st["saved"], self._ctr(bs, 0), count, self.eps, self.mom, bs.c)
+                         st["affine"], st["saved"], self._ctr(bs, 0), count, self.eps, self.mom, bs.c,
+                         sshift=st["sshift"], sshift_next=st["sshift_next"])
             self._fins[key] = f
         return f
 
@@ -499,16 +512,18 @@ class HipResNetEngine:
         fin = self._fin_fwd(bs, arena, npix) if (train and self.fuse_fin) else None
         wl = self.wino_layers.get(cs.name)
         assert bn_in is None or wl is not None, cs.name
+        sshift = self.bn[bs.name]["sshift"] if train else None
         if wl is not None:
             v = wl[2] if wl[2] is not None else self.wino_s2
-            K.wino_conv(x, wl[0], y, None, stats, v, self.wino_s1, self.B, cs.h, cs.w, cs.cp, cs.cout, bn_in=bn_in)
+            K.wino_conv(x, wl[0], y, None, stats, v, self.wino_s1, self.B, cs.h, cs.w, cs.cp, cs.cout, bn_in=bn_in,
+                        sshift=sshift)
             if not train:
                 self._bn_eval(bs, arena)
             elif not self._fold:  # no in-launch finalize on this path
                 self._bn_train(bs, arena, self.nslots, npix)
             return
         K.conv_fwd2(x, wf, y, stats, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
-                    cs.kg, fin=fin)
+                    cs.kg, fin=fin, sshift=sshift)
         if not train:
             self._bn_eval(bs, arena)
         elif fin is None and not self._fold:
@@ -538,7 +553,7 @@ class HipResNetEngine:
         K.bn_finalize(self._red(bs, "fwd"), T, bs.c, count, self._aview(arena, f"{bs.name}.weight"),
                       self._aview(arena, f"{bs.name}.bias"), self.eps, self.mom,
                       self._aview(arena, f"{bs.name}.running_mean"), self._aview(arena, f"{bs.name}.running_var"),
-                      st["affine"], st["saved"])
+                      st["affine"], st["saved"], sshift=st["sshift"], sshift_next=st["sshift_next"])
 
     def _bn_eval(self, bs: BNSpec, arena):
         st = self.bn[bs.name]
@@ -742,7 +757,8 @@ class HipResNetEngine:
         zero = (self.red, self.correct) if train else None
         self._zeroed_head = train
         K.augment(images_u8, labels_all, self.index, self.x0, self.labels, self.B, H, W, 4, self.seed, self.step_dev,
-                  train, self.mean, self.std, zero=zero)
+                  train, self.mean, self.std, zero=zero,
+                  copy=(self.bn_shift[1], self.bn_shift[0]) if train else None)
         self._zeroed = train
 
     def forward(self, arena: torch.Tensor, train: bool = True):
@@ -754,6 +770,7 @@ class HipResNetEngine:
         zeroed, self._zeroed = self._zeroed, False
         if train and not zeroed:
             self.red.zero_()
+            self.bn_shift[0].copy_(self.bn_shift[1])  # this step's statistic shifts (see _build)
         self._conv_bn_fwd(st, self.x0, self.y0, sp.stem_bn, arena, train)
         self._apply(sp.stem_bn, self.y0, self.a0, arena, train)
         if sp.maxpool:
@@ -931,16 +948,23 @@ class HipResNetEngine:
             if on_segment is not None:
                 on_segment(si)
 
+    def reset_stat_shift(self):
+        """Forget the BN statistic shifts (the previous batch means, see _build): the next step
+        sums plainly, as the first step of a fresh engine does."""
+        self.bn_shift.zero_()
+
     # ------------------------------------------------------------------ graphs
     def capture(self, arena, images_u8, labels_all, unpack=True, warmup=2):
         """Capture the step into HIP graphs (one per backward segment, all sharing one memory
         pool); replay with ``step_graph()``."""
+        shift = self.bn_shift.clone()  # the warm-up steps' batch means must not become the first replay's shifts
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self.train_step(arena, images_u8, labels_all, unpack)
         torch.cuda.current_stream().wait_stream(s)
+        self.bn_shift.copy_(shift)
         graphs = []
         for fn in self._segment_fns(arena, images_u8, labels_all, unpack):
             g = torch.cuda.CUDAGraph()

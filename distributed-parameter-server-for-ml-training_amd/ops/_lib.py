@@ -45,19 +45,20 @@ _KERNEL_SIGS = {
     "psx_wgrad_reduce_batch": (i32, [i32, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, vp]),
     "psx_conv2_workspace": (i64, [i32, i32, i32, i32, i32, i32]),
     "psx_conv_wgrad2": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
-    "psx_conv_fwd2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp]),
+    "psx_conv_fwd2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp,
+                            vp]),
     "psx_conv_dgrad2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp]),
     "psx_bgemm_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "psx_wino_workspace": (i64, [i32, i32, i32, i32, i32]),
     "psx_wino_ok": (i32, [i32, i32, i32, i32]),
     "psx_wino_weights": (i32, [vp, vp, i32, i32, i32, vp]),
     "psx_wino_weights_multi": (i32, [vp, vp, vp, vp, vp, i32, vp]),
-    "psx_wino_conv": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
+    "psx_wino_conv": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp]),
     "psx_wino_v_floats": (i64, [i32, i32, i32, i32]),
     "psx_wino_wgrad_q": (i32, [i32, i32, i32, i32, i32]),
     "psx_wino_wgrad": (i32, [vp, vp, vp, vp, vp, i32, f32, vp, i32, i32, i32, i32, i32, vp]),
     "psx_bgemm_tn_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
-    "psx_bn_finalize": (i32, [vp, i32, i32, f32, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp]),
+    "psx_bn_finalize": (i32, [vp, i32, i32, f32, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "psx_bn_eval_affine": (i32, [i32, vp, vp, vp, vp, f32, vp, vp, vp]),
     "psx_bn_apply": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
     "psx_bn_bwd_reduce": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp, i32, vp]),
@@ -77,7 +78,8 @@ _KERNEL_SIGS = {
     "psx_param_unpack_tiles": (i32, [vp, i32, vp, i32, i32, vp, vp, vp, i64, vp, i32, vp, i32, vp]),
     "psx_unpack_desc_size": (i32, []),
     "psx_synth_gen": (i32, [vp, vp, i32, i32, i32, i32, u32, u32, vp]),
-    "psx_augment": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, u32, vp, i32, vp, vp, vp, i64, vp, i64, i32, vp]),
+    "psx_augment": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, u32, vp, i32, vp, vp, vp, i64, vp, i64, vp, vp, i64,
+                          i32, vp]),
     "psx_nchw_to_nhwc": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, vp]),
     "psx_maxpool3s2_fwd": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "psx_maxpool3s2_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp]),

@@ -72,7 +72,7 @@ class BnFin(C.Structure):
     _fields_ = [("gamma", C.c_void_p), ("beta", C.c_void_p), ("run_mean", C.c_void_p), ("run_var", C.c_void_p),
                 ("scale", C.c_void_p), ("shift", C.c_void_p), ("save_mean", C.c_void_p),
                 ("save_invstd", C.c_void_p), ("counter", C.c_void_p), ("count", C.c_float), ("eps", C.c_float),
-                ("momentum", C.c_float), ("C", C.c_int)]
+                ("momentum", C.c_float), ("C", C.c_int), ("sshift", C.c_void_p), ("sshift_next", C.c_void_p)]
 
 
 class BnBwdFin(C.Structure):
@@ -82,11 +82,14 @@ class BnBwdFin(C.Structure):
                 ("gscale", C.c_float), ("C", C.c_int), ("grad_fp16", C.c_int)]
 
 
-def bn_fin(gamma, beta, run_mean, run_var, affine, saved, counter_ptr, count, eps, momentum, c) -> BnFin:
-    """affine: [2, C] (scale, shift); saved: [2, C] (mean, invstd)."""
+def bn_fin(gamma, beta, run_mean, run_var, affine, saved, counter_ptr, count, eps, momentum, c, sshift=None,
+           sshift_next=None) -> BnFin:
+    """affine: [2, C] (scale, shift); saved: [2, C] (mean, invstd). sshift / sshift_next [C]
+    (optional): the statistics are shifted sums around sshift (what the producers were given);
+    the finalize writes the batch mean to sshift_next (csrc/kernels/bnfin.hpp BnFin)."""
     a, sv = ptr(affine), ptr(saved)
     return BnFin(ptr(gamma), ptr(beta), ptr(run_mean), ptr(run_var), a, a + 4 * c, sv, sv + 4 * c, counter_ptr,
-                 float(count), float(eps), float(momentum), int(c))
+                 float(count), float(eps), float(momentum), int(c), ptr(sshift), ptr(sshift_next))
 
 
 def bn_bwd_fin(gamma, saved, coef, dgamma_ptr, dbeta_ptr, counter_ptr, count, gscale, c, grad_fp16) -> BnBwdFin:
@@ -95,13 +98,14 @@ def bn_bwd_fin(gamma, saved, coef, dgamma_ptr, dbeta_ptr, counter_ptr, count, gs
                     float(gscale), int(c), int(grad_fp16))
 
 
-def conv_fwd2(x, wf, y, stats, ws, nb, h, w, ic, oc, k, stride, pad, kg, fin: BnFin | None = None):
+def conv_fwd2(x, wf, y, stats, ws, nb, h, w, ic, oc, k, stride, pad, kg, fin: BnFin | None = None, sshift=None):
     """LDS-DMA pipelined implicit-GEMM conv (csrc/kernels/conv_v2.hip); ws: fp32 split-K
     workspace of >= conv2_workspace_bytes(...) bytes (or None when that is 0). With ``fin`` the
-    kernel's last workgroup also finalizes the BN layer its statistics feed (bnfin.hpp)."""
+    kernel's last workgroup also finalizes the BN layer its statistics feed (bnfin.hpp).
+    sshift [oc] (optional): the BN statistics are sums of (y - sshift) and (y - sshift)^2."""
     check(kernels().psx_conv_fwd2(ptr(x), ptr(wf), ptr(y), ptr(stats), ptr(zero_page(x.device)), ptr(ws), nb, h, w,
                                   ic, oc, k, k, stride, pad, kg, C.byref(fin) if fin is not None else None,
-                                  is_f32(x), stream_ptr()), "conv_fwd2")
+                                  is_f32(x), ptr(sshift), stream_ptr()), "conv_fwd2")
 
 
 class BwdStatsDesc(C.Structure):
@@ -197,7 +201,8 @@ class WinoWeightBatch:
               "wino_weights_multi")
 
 
-def wino_conv(x, u, y, res, stats, v, p, nb, h, w, c, k, cfg=None, bst: "BwdStatsDesc | None" = None, bn_in=None):
+def wino_conv(x, u, y, res, stats, v, p, nb, h, w, c, k, cfg=None, bst: "BwdStatsDesc | None" = None, bn_in=None,
+              sshift=None):
     """fp32 3x3/s1/p1 conv y = conv(x) (+ res) via Winograd F(4x4,3x3) with pre-transformed
     weights u (wino_weights); stats: BN slot sums of y (pre-zeroed) or None; bst (data gradient,
     bwd_stats_desc): the consumer BN's backward sums (and the masked store) instead. v (>=
@@ -213,7 +218,8 @@ def wino_conv(x, u, y, res, stats, v, p, nb, h, w, c, k, cfg=None, bst: "BwdStat
                                   nb, h, w, c, k, WINO_CFG if cfg is None else cfg,
                                   C.byref(bst) if bst is not None else None,
                                   ptr(bn_in[0]) if bn_in is not None else None,
-                                  C.byref(bn_in[1]) if bn_in is not None else None, stream_ptr()), "wino_conv")
+                                  C.byref(bn_in[1]) if bn_in is not None else None, ptr(sshift), stream_ptr()),
+          "wino_conv")
 
 
 def wino_wgrad(v, dy, d, part, out, nb, h, w, c, k, scale=1.0):
@@ -273,11 +279,13 @@ def wgrad_reduce_batch(items, scale, out_fp16: bool):
           "wgrad_reduce_batch")
 
 
-def bn_finalize(part, T, c, count, gamma, beta, eps, momentum, run_mean, run_var, affine, saved):
-    """affine: [2, C] (scale, shift); saved: [2, C] (mean, invstd)."""
+def bn_finalize(part, T, c, count, gamma, beta, eps, momentum, run_mean, run_var, affine, saved, sshift=None,
+                sshift_next=None):
+    """affine: [2, C] (scale, shift); saved: [2, C] (mean, invstd); sshift / sshift_next: as bn_fin."""
     check(kernels().psx_bn_finalize(ptr(part), T, c, float(count), ptr(gamma), ptr(beta), float(eps),
                                     float(momentum), ptr(run_mean), ptr(run_var), ptr(affine), ptr(affine) + 4 * c,
-                                    ptr(saved), ptr(saved) + 4 * c, stream_ptr()), "bn_finalize")
+                                    ptr(saved), ptr(saved) + 4 * c, ptr(sshift), ptr(sshift_next), stream_ptr()),
+          "bn_finalize")
 
 
 def bn_eval_affine(c, gamma, beta, rm, rv, eps, affine):
@@ -473,15 +481,23 @@ def synth_gen(img, labels, n, h, w, classes, seed, offset=0):
 _F3 = C.c_float * 3
 
 
-def augment(img, labels, index, out, out_labels, b, h, w, pad, seed, step_dev, train, mean, std, zero=None):
-    """zero: up to two contiguous tensors of 32-bit elements zeroed by the same launch."""
+def augment(img, labels, index, out, out_labels, b, h, w, pad, seed, step_dev, train, mean, std, zero=None,
+            copy=None):
+    """zero: up to two contiguous tensors of 32-bit elements zeroed by the same launch; copy:
+    (src, dst) 32-bit tensors of equal size copied by it (the BN statistic shifts)."""
     zs = []
     for t in zero or ():
         assert t.is_contiguous() and t.element_size() == 4 and t.device == out.device
         zs += [ptr(t), t.numel()]
     zs += [None, 0] * (2 - len(zs) // 2)
+    cp = [None, None, 0]
+    if copy is not None:
+        src, dst = copy
+        assert src.numel() == dst.numel() and src.element_size() == dst.element_size() == 4
+        assert src.is_contiguous() and dst.is_contiguous()
+        cp = [ptr(src), ptr(dst), src.numel()]
     check(kernels().psx_augment(ptr(img), ptr(labels), ptr(index), ptr(out), ptr(out_labels), b, h, w, pad,
-                                seed & 0xFFFFFFFF, ptr(step_dev), int(train), _F3(*mean), _F3(*std), *zs,
+                                seed & 0xFFFFFFFF, ptr(step_dev), int(train), _F3(*mean), _F3(*std), *zs, *cp,
                                 is_f32(out), stream_ptr()), "augment")
 
 

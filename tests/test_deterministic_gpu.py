@@ -35,12 +35,14 @@ def test_two_runs_and_graph_replay_bit_identical(dtype):
     outs = []
     for _ in range(2):
         a = arena.clone()
+        eng.reset_stat_shift()  # engine state besides the arena: the BN statistic shifts
         eng.train_step(a, imgs, labs)
         torch.cuda.synchronize()
         outs.append((eng.grads.clone(), a.clone()))
     assert torch.equal(outs[0][0], outs[1][0])  # gradients
     assert torch.equal(outs[0][1], outs[1][1])  # running statistics in the local arena
     a = arena.clone()
+    eng.reset_stat_shift()
     eng.capture(a, imgs, labs, warmup=1)
     a.copy_(arena)
     eng.step_graph()
@@ -67,6 +69,7 @@ def test_side_stream_and_segments_bit_identical(monkeypatch):
         grads.append(eng.grads.clone())
     assert torch.equal(grads[0], grads[1])
     a = arena.clone()
+    side.reset_stat_shift()
     side.capture(a, imgs, labs, warmup=1)
     a.copy_(arena)
     side.step_graph()
@@ -74,6 +77,7 @@ def test_side_stream_and_segments_bit_identical(monkeypatch):
     assert torch.equal(side.grads, grads[0])
     side.set_segments([b.keys for b in plan_buckets(lay, 2 << 20)])
     a = arena.clone()
+    side.reset_stat_shift()
     side.capture(a, imgs, labs, warmup=1)
     a.copy_(arena)
     seen = []

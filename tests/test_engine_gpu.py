@@ -136,8 +136,10 @@ def test_fused_bn_finalize_matches_separate_kernels(setup, mode):
             c = bs.c
             fin = [f for k, f in eng._fins.items() if k[0] == "f" and k[1] == bs.name][0]
             aff, sav = torch.empty_like(st["affine"]), torch.empty_like(st["saved"])
+            # the slot sums are shifted by the step's statistic shift (engine.py bn_shift)
             K.bn_finalize(eng._red(bs, "fwd"), K.STAT_SLOTS, c, fin.count, layout.view(a, f"{bs.name}.weight"),
-                          layout.view(a, f"{bs.name}.bias"), eng.eps, eng.mom, None, None, aff, sav)
+                          layout.view(a, f"{bs.name}.bias"), eng.eps, eng.mom, None, None, aff, sav,
+                          sshift=st["sshift"])
             bf = [f for k, f in eng._fins.items() if k[0] == "b" and k[1] == bs.name][0]
             coef = torch.empty_like(st["coef"])
             dg = torch.empty(c, dtype=torch.float32, device=DEV)

@@ -314,3 +314,40 @@ def test_engine_step_f32_matches_torch_fp64(wino, monkeypatch):
     for name in ("bn1.running_mean", "layer2.0.bn1.running_var", "layer4.1.bn2.running_mean"):
         assert torch.allclose(layout.view(arena, name).double(), sd[name], rtol=1e-5, atol=1e-6), name
     print(f"fp32 engine vs fp64 autograd: worst per-tensor relative gradient error {max(r[1] for r in rows):.2e}")
+
+
+@pytest.mark.parametrize("f32", [True, False])
+def test_bn_statistics_large_mean_shifted_sums(f32):
+    """BN variance from one-pass sums cancels when |mean| >> std. The conv
+    epilogue sums (y - k) and (y - k)^2 around a per-channel shift k (the engine passes the
+    previous batch mean) and the finalize recombines: the saved mean / invstd and the running
+    variance of a conv output with mean 100 and std 1 per channel match float64 to ~1e-6, where
+    the plain sums (k = 0) lose about three digits of the variance."""
+    torch.manual_seed(3)
+    B, hw, c = 64, 16, 64
+    dt = torch.float32 if f32 else torch.bfloat16
+    x = (100.0 + torch.randn(B, hw, hw, c, device=DEV) * (1.0 + torch.rand(c, device=DEV))).to(dt)
+    w = torch.eye(c, device=DEV).to(dt).contiguous()  # 1x1 conv = identity: y = x
+    y = torch.empty(B, hw, hw, c, dtype=dt, device=DEV)
+    ref = x.double().reshape(-1, c)
+    mean_ref, var_ref = ref.mean(0), ref.var(0, unbiased=False)
+    errs = {}
+    for name, k in (("plain", None), ("shifted", (mean_ref + 0.3 * var_ref.sqrt()).float())):
+        stats = torch.zeros(K.STAT_SLOTS, 2, c, device=DEV)
+        K.conv_fwd2(x, w, y, stats, None, B, hw, hw, c, c, 1, 1, 0, 64, sshift=k)
+        gamma, beta = torch.ones(c, device=DEV), torch.zeros(c, device=DEV)
+        rm, rv = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+        aff, saved = torch.empty(2, c, device=DEV), torch.empty(2, c, device=DEV)
+        nxt = torch.zeros(c, device=DEV)
+        K.bn_finalize(stats, K.STAT_SLOTS, c, B * hw * hw, gamma, beta, 1e-5, 0.1, rm, rv, aff, saved, sshift=k,
+                      sshift_next=nxt)
+        torch.cuda.synchronize()
+        var = 1.0 / saved[1].double() ** 2 - 1e-5
+        errs[name] = (((saved[0].double() - mean_ref).abs().max() / var_ref.sqrt().max()).item(),
+                      ((var - var_ref).abs() / var_ref).max().item())
+        assert torch.allclose(nxt.double(), mean_ref, rtol=1e-6, atol=1e-4)
+        unb = var_ref * (B * hw * hw) / (B * hw * hw - 1)
+        if k is not None:
+            assert ((rv.double() - (0.9 + 0.1 * unb)).abs() / unb).max().item() < 1e-5
+    print("bn statistics mean / variance error:", errs)
+    assert errs["shifted"][0] < 1e-5 and errs["shifted"][1] < 2e-5, errs

@@ -335,3 +335,102 @@ def test_native_sync_server_matches_python(dt, fc, mom, rounds, tmp_path):
             assert len(rec) == 1 and rec[0][1] == 5, out[-3000:]
             sums[(ov, native)] = rec[0][0]
     assert len(set(sums.values())) == 1, sums
+
+
+_SCRIPTED = r"""
+import hashlib, json, os, sys, threading, uuid
+sys.path.insert(0, {root!r})
+import torch
+import psx
+from psx.parallel import control as CP
+from psx.parallel.codec import FetchCodec
+from psx.parallel.native_loop import NativeAsyncChannel, NativeServerLoop
+from psx.parallel.rccl import make_transport
+from psx.parallel.runner import build_state
+from psx.parallel.server import ParameterServer
+from psx.parallel.worker import AsyncChannel
+from psx.utils.config import PSConfig
+
+native = os.environ["PSX_NATIVE_LOOP"] == "1"
+torch.cuda.set_device(0)
+dev = torch.device("cuda", 0)
+t = make_transport(dev)
+rank, world = t.rank, t.world_size
+W = world - 1
+cfg = PSConfig(model="resnet18", mode="async", workers=W, lr=0.05, staleness_bound=2, codec="fp16",
+               momentum={mom}, weight_decay={wd}, eval_every=0, verbose=0, heartbeat_timeout=0,
+               fetch_codec="fp32").validate()
+_, lay, arena, counters = build_state(cfg)
+name = t.broadcast_object("/psx_s" + uuid.uuid4().hex[:10] if rank == 0 else None)
+mbox = CP.ShmMailbox(name, nreply=world, owner=True) if rank == 0 else None
+t.barrier()
+if rank != 0:
+    mbox = CP.ShmMailbox(name, nreply=world, owner=False)
+t.open_pairs(list(range(1, world)))
+store = t._store()
+SCHED = {sched!r}
+if rank == 0:
+    srv = ParameterServer(cfg, lay, arena.to(dev), counters, device=dev, total_workers=W, log=lambda *a, **k: None)
+    remote = {{w: w + 1 for w in range(W)}}
+    if native:
+        loop = NativeServerLoop(srv, t, mbox, remote, W)
+        loop.join()
+    else:
+        th = threading.Thread(target=srv.serve_async, args=(t, mbox, remote), kwargs={{"expected": W}}, daemon=True)
+        th.start()
+        th.join()
+    torch.cuda.synchronize()
+    h = hashlib.sha256(srv.arena.cpu().numpy().tobytes()).hexdigest()[:16]
+    hist = ",".join(str(v) for v in srv.core.staleness_histogram())
+    print("RESULT " + json.dumps([srv.core.global_step, hist, h]), flush=True)
+else:
+    wid = rank - 1
+    ch = (NativeAsyncChannel if native else AsyncChannel)(t, mbox, rank, codec=FetchCodec(lay, "fp32", dev))
+    ch.register(f"w{{wid}}", wid)
+    local = torch.empty(lay.arena_numel, device=dev)
+    gen = torch.Generator().manual_seed(100 + wid)
+    dec = []
+    for i, (w, kind, ls) in enumerate(SCHED):
+        if w != wid:
+            continue
+        if i:
+            store.wait([f"psx_turn{{i}}"])  # the previous action of the schedule has been answered
+        if kind == "p":
+            g = (torch.randn(lay.param_numel, generator=gen) * 0.01).half().to(dev)
+            dec.append(int(ch.push(wid, g, ls)))
+        else:
+            ch.fetch(wid, local)
+        torch.cuda.synchronize()
+        store.set(f"psx_turn{{i + 1}}", b"1")
+    ch.finished(wid)
+    print("RESULT " + json.dumps([wid, ",".join(map(str, dec))]), flush=True)
+t.barrier()
+mbox.close()
+t.close()
+"""
+
+# (worker, kind, local step): staleness bound 2 -> fresh, stale-accepted (weighted) and rejected
+# pushes of two remote workers interleaved
+SCHED_REMOTE = [(0, "f", 0), (1, "f", 0), (0, "p", 0), (1, "p", 0), (0, "p", 0), (1, "f", 0), (1, "p", 3),
+                (0, "p", 1), (0, "f", 0), (0, "p", 4), (1, "p", 2), (1, "p", 5), (0, "p", 6), (1, "f", 0)]
+
+
+@pytest.mark.parametrize("mom", [0.0, 0.9])
+def test_async_scripted_remote_native_matches_python(mom, tmp_path):
+    """two REMOTE workers (world 3, their own processes, pair communicators) push
+    and fetch in a scripted global order (each action waits for the previous one's reply): the
+    native event loop and the Python loop give the same accept/reject decision per push, the
+    same staleness histogram and global step, and a bit-identical master arena."""
+    res = {}
+    for native in ("1", "0"):
+        p = tmp_path / f"sched{native}.py"
+        p.write_text(_SCRIPTED.format(root=ROOT, sched=SCHED_REMOTE, mom=mom, wd=5e-4 if mom else 0.0))
+        out = _torchrun(3, [str(p)], extra={"PSX_NATIVE_LOOP": native})
+        recs = _json_lines(out, "RESULT ")
+        assert len(recs) == 3, out[-3000:]
+        res[native] = sorted(map(tuple, recs), key=str)
+    assert res["1"] == res["0"], res
+    server = [r for r in res["1"] if len(r) == 3][0]
+    decisions = "".join(r[1] for r in res["1"] if len(r) == 2)
+    assert "0" in decisions and "1" in decisions, res  # some pushes rejected, some applied
+    assert server[0] == decisions.count("1"), res

@@ -321,8 +321,13 @@ def main():
     run.close()
     if rank == 0 and a.mode == "async":
         sm = run.server.final_metrics()
+        # average / max_staleness_observed follow the reference (each worker's LAST push,
+        # server.py:300); the histogram and mean_staleness_all cover every push of the run
         rec["async_staleness"] = {k: sm.get(k) for k in ("average_gradient_staleness", "max_staleness_observed",
-                                                         "rejected_pushes", "staleness_histogram")}
+                                                         "mean_staleness_all", "async_updates", "rejected_pushes",
+                                                         "staleness_histogram")}
+        hist = sm.get("staleness_histogram") or []
+        rec["async_staleness"]["max_staleness_accepted"] = max((i for i, n in enumerate(hist) if n), default=0)
         rec["global_steps"] = run.server.core.global_step
 
     # secondary numbers (same transport): bf16 compute at N=1, the co-located topology at N>=2

@@ -2,6 +2,7 @@
 (steps delimited by a marker kernel), grouped by kernel template.
 
 usage: python scripts/prof/kstats.py run_kernel_trace.csv|run_results.db [--steps 20] [--marker augment]
+       [--grid REGEX]  (kernels matching REGEX split per launch grid, CSV input: one line per layer shape)
 (rocprofv3 writes a rocpd SQLite database by default, a CSV with --output-format csv)
 """
 import argparse
@@ -11,6 +12,8 @@ import re
 
 
 def short(n):
+    if " grid=(" in n:
+        return n[:100]
     n = re.sub(r"\(.*$", "", n) if not n.startswith("void ") else re.sub(r"\((?![^<]*>).*$", "", n[5:])
     return n[:80]
 
@@ -20,6 +23,7 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--marker", default="augment")
+    ap.add_argument("--grid", default=None)
     a = ap.parse_args()
     rows = []
     if a.csv.endswith(".db"):
@@ -29,7 +33,10 @@ def main():
     else:
         with open(a.csv) as f:
             for r in csv.DictReader(f):
-                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+                n = r["Kernel_Name"]
+                if a.grid and re.search(a.grid, n):
+                    n = f"{short(n)} grid=({r.get('Grid_Size_X')},{r.get('Grid_Size_Y')},{r.get('Grid_Size_Z')})"
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), n))
     rows.sort()
     marks = [s for s, _, n in rows if a.marker in n]
     lo, hi = marks[-a.steps - 1], marks[-1]
@@ -42,9 +49,9 @@ def main():
     busy = sum(v[1] for v in tot.values())
     wall = hi - lo
     print(f"{a.steps} steps: wall {wall / a.steps / 1e3:.1f} us/step, kernel time {busy / a.steps / 1e3:.1f} us/step")
-    print(f"{'kernel':80s} {'calls/step':>10s} {'us/step':>9s} {'%':>6s}")
+    print(f"{'kernel':100s} {'calls/step':>10s} {'us/step':>9s} {'%':>6s}")
     for k, (c, t) in sorted(tot.items(), key=lambda kv: -kv[1][1]):
-        print(f"{k:80s} {c / a.steps:10.1f} {t / a.steps / 1e3:9.1f} {100 * t / busy:6.1f}")
+        print(f"{k:100s} {c / a.steps:10.1f} {t / a.steps / 1e3:9.1f} {100 * t / busy:6.1f}")
 
 
 if __name__ == "__main__":

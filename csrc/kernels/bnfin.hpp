@@ -113,9 +113,11 @@ struct DetRed {
 PSX_DEV void det_rows(float* slab, int r0, int r1, int n, float* dst, bool add, float* scratch) {
   const int lanes = n >= 256 ? 1 : 256 / n;
   for (int jb = 0; jb < n; jb += 256) {
+    // the first 256 threads do the work (blocks of 384, wino.hip's split transforms, call it too)
     const int t = threadIdx.x, k = lanes > 1 ? t / n : 0, j = jb + (lanes > 1 ? t % n : t);
+    const bool act = t < 256;
     float acc = 0.f;
-    if (k < lanes && j < n) {
+    if (act && k < lanes && j < n) {
       float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       int r = r0 + k;
       for (; r + 7 * lanes < r1; r += 8 * lanes) {
@@ -128,7 +130,7 @@ PSX_DEV void det_rows(float* slab, int r0, int r1, int n, float* dst, bool add, 
     }
     if (lanes > 1) {
       __syncthreads();
-      if (k < lanes && j < n) scratch[k * n + (j - jb)] = acc;
+      if (act && k < lanes && j < n) scratch[k * n + (j - jb)] = acc;
       __syncthreads();
       if (t < n) {
         float v = 0.f;
@@ -136,7 +138,7 @@ PSX_DEV void det_rows(float* slab, int r0, int r1, int n, float* dst, bool add, 
         if (add) atomicAdd(dst + t, v);
         else dst[t] = v;
       }
-    } else if (j < n) {
+    } else if (act && j < n) {
       if (add) atomicAdd(dst + j, acc);
       else dst[j] = acc;
     }

@@ -36,6 +36,10 @@
 #ifndef PSX_TAPR_BF16_256
 #define PSX_TAPR_BF16_256 1
 #endif
+// WOUT (fused Winograd GEMM + output transform): the register double buffer of the generic loop
+#ifndef PSX_WOUT_PF
+#define PSX_WOUT_PF 1
+#endif
 #ifndef PSX_TAPR_F32_128
 #define PSX_TAPR_F32_128 1
 #endif
@@ -74,29 +78,15 @@ struct Conv2Args {
   // forward statistics: per-channel shift k subtracted before summing (nullable = 0; bnfin.hpp
   // BnFin::sshift): the slots hold sum(y - k), sum((y - k)^2)
   const float* sshift;
+  // WOUT backward: ReLU mask = [y1 * scale + shift > 0] from this affine [2][OC] (nullable: from bo)
+  const float* bmaff;
 };
 
-// Winograd F(4x4,3x3) output-transform coefficients: y[i][j] = sum_b kWinoAT2[b][4 i + j] P[b],
-// b = 6 r + s, kWinoAT2[b][4 i + j] = A^T[i][r] A^T[j][s] (wino.hip has the matrices)
-__constant__ float kWinoAT2[36][16] = {
-#define PSX_AT(i, r) ((r) == 0 ? ((i) == 0 ? 1.f : 0.f) : (r) == 5 ? ((i) == 3 ? 1.f : 0.f) : \
-                      (float)(((r) == 1 ? 1 : (r) == 2 ? ((i) & 1 ? -1 : 1) : (r) == 3 ? (1 << (i)) : (((i) & 1) ? -(1 << (i)) : (1 << (i))))))
-#define PSX_ROW(b) {PSX_AT(0, (b) / 6) * PSX_AT(0, (b) % 6), PSX_AT(0, (b) / 6) * PSX_AT(1, (b) % 6), \
-                     PSX_AT(0, (b) / 6) * PSX_AT(2, (b) % 6), PSX_AT(0, (b) / 6) * PSX_AT(3, (b) % 6), \
-                     PSX_AT(1, (b) / 6) * PSX_AT(0, (b) % 6), PSX_AT(1, (b) / 6) * PSX_AT(1, (b) % 6), \
-                     PSX_AT(1, (b) / 6) * PSX_AT(2, (b) % 6), PSX_AT(1, (b) / 6) * PSX_AT(3, (b) % 6), \
-                     PSX_AT(2, (b) / 6) * PSX_AT(0, (b) % 6), PSX_AT(2, (b) / 6) * PSX_AT(1, (b) % 6), \
-                     PSX_AT(2, (b) / 6) * PSX_AT(2, (b) % 6), PSX_AT(2, (b) / 6) * PSX_AT(3, (b) % 6), \
-                     PSX_AT(3, (b) / 6) * PSX_AT(0, (b) % 6), PSX_AT(3, (b) / 6) * PSX_AT(1, (b) % 6), \
-                     PSX_AT(3, (b) / 6) * PSX_AT(2, (b) % 6), PSX_AT(3, (b) / 6) * PSX_AT(3, (b) % 6)}
-    PSX_ROW(0),  PSX_ROW(1),  PSX_ROW(2),  PSX_ROW(3),  PSX_ROW(4),  PSX_ROW(5),  PSX_ROW(6),  PSX_ROW(7),
-    PSX_ROW(8),  PSX_ROW(9),  PSX_ROW(10), PSX_ROW(11), PSX_ROW(12), PSX_ROW(13), PSX_ROW(14), PSX_ROW(15),
-    PSX_ROW(16), PSX_ROW(17), PSX_ROW(18), PSX_ROW(19), PSX_ROW(20), PSX_ROW(21), PSX_ROW(22), PSX_ROW(23),
-    PSX_ROW(24), PSX_ROW(25), PSX_ROW(26), PSX_ROW(27), PSX_ROW(28), PSX_ROW(29), PSX_ROW(30), PSX_ROW(31),
-    PSX_ROW(32), PSX_ROW(33), PSX_ROW(34), PSX_ROW(35)
-#undef PSX_ROW
-#undef PSX_AT
-};
+// Winograd F(4x4,3x3) output transform A^T (wino.hip has the matrices): y = A^T P A
+__constant__ float kWinoAT[4][6] = {{1.f, 1.f, 1.f, 1.f, 1.f, 0.f},
+                                    {0.f, 1.f, -1.f, 2.f, -2.f, 0.f},
+                                    {0.f, 1.f, 1.f, 4.f, 4.f, 0.f},
+                                    {0.f, 1.f, -1.f, 8.f, -8.f, 1.f}};
 
 PSX_DEV int kmaj2(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
@@ -148,7 +138,7 @@ PSX_DEV const T* gather_src(const Conv2Args& a, int nbase, int hb, int wb, bool 
 // WOUT (fp32 Winograd, wino.hip): the GEMM over all 36 batches of a layer (R = 36 "taps", Kg =
 // 36 C) with the output transform fused: at every batch boundary of the k-loop the batch's
 // accumulators are folded into the 16 output pixels of each (tile, channel) element
-// (kWinoAT2) and reset, so the transformed product P never leaves registers; the epilogue
+// (two-stage, kWinoAT) and reset, so the transformed product P never leaves registers; the epilogue
 // stores y (+ residual) with the BN statistics or the BN-backward sums.
 template <typename T, int BM, int BN, int MODE, bool HAS_RES, bool SPLIT, int WGM = 2, int TAPR = 0, bool WOUT = false>
 __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
@@ -200,26 +190,59 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  static_assert(!WOUT || (sizeof(T) == 4 && !SPLIT && !TAPR && MODE == 0 && MT * NT == 1), "WOUT: fp32 16x16 wave tiles");
-  float yacc[WOUT ? 4 : 1][WOUT ? 16 : 1];
+  static_assert(!WOUT || (sizeof(T) == 4 && !SPLIT && !TAPR && MODE == 0 && MT * NT <= 2),
+                "WOUT: fp32, at most two 16x16 MFMA tiles per wave");
+  // WOUT: y[i][j] = sum_r A^T[i][r] Q_r[j], Q_r[j] = sum_s A^T[j][s] P[6 r + s], accumulated in two
+  // stages — per batch b = 6 r + s the 4 values Q_r += A^T[:, s] P_b, per finished row r the 16
+  // outputs y += A^T[:, r] Q_r — 6.7 instead of 16 FMAs per accumulator element and batch
+  constexpr int WT = WOUT ? MT * NT : 1;
+  float yacc[WT][4][WOUT ? 16 : 1];
+  float qacc[WT][4][WOUT ? 4 : 1];
   if constexpr (WOUT) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
+    for (int w = 0; w < WT; ++w)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) yacc[e][q] = 0.f;
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) yacc[w][e][q] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) qacc[w][e][j] = 0.f;
+      }
   }
-  // batch boundary (WOUT): fold the batch's product into the output pixels, reset
+  // batch boundary (WOUT): fold the batch's product into the row accumulators, reset
   auto wfold = [&](int ks) {
     if constexpr (WOUT) {
       if (((ks + 1) & (a.kps - 1)) == 0) {
         const int b = __builtin_amdgcn_readfirstlane(ks / a.kps);
+        const int r = b / 6, sc = b - 6 * r;
+        float cs[4];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const float c = kWinoAT2[b][q];
+        for (int j = 0; j < 4; ++j) cs[j] = kWinoAT[j][sc];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) yacc[e][q] += c * acc[0][0][e];
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int n = 0; n < NT; ++n) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) qacc[m * NT + n][e][j] += cs[j] * acc[m][n][e];
+            acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+          }
+        if (sc == 5) {
+          float cr[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) cr[i] = kWinoAT[i][r];
+#pragma unroll
+          for (int w = 0; w < WT; ++w)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) yacc[w][e][i * 4 + j] += cr[i] * qacc[w][e][j];
+                qacc[w][e][j] = 0.f;
+              }
         }
-        acc[0][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
       }
     }
   };
@@ -501,7 +524,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   };
   if (nk > 0) issue(0, 0);
   if (nk > 1) issue(1, 1);
-  if constexpr (sizeof(T) == 4 && (PSX_CONV_PF & 2)) {
+  if constexpr (sizeof(T) == 4 && ((PSX_CONV_PF & 2) || (WOUT && PSX_WOUT_PF))) {
     // fp32: the fragments of the next half k-step are read before the MFMAs of the current one
     // (register double buffer, as in the tap-reuse loop); the stage boundary — DMA of k-step
     // ks+1 retired, this wave's reads of stage ks retired, barrier, DMA of ks+3 into stage ks —
@@ -562,81 +585,117 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   }  // generic mainloop
 
   if constexpr (WOUT) {
-    // lane: 4 consecutive channels oc..oc+3 (e) of tile t; 16 output pixels each
-    const int oc = oc0 + wm * (BM / WGM) + 4 * (lane >> 4);
-    const int t = pix0 + wn * (BN / WGN) + (lane & 15);
-    const bool bwd = a.bpart != nullptr, two = a.by2 != nullptr, st = a.stats != nullptr;
-    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f}, s3[4] = {0.f, 0.f, 0.f, 0.f};
-    float bm1[4], bi1[4], bm2[4], bi2[4], ksh[4];
+    // lane: 4 consecutive channels oc..oc+3 (e) of tile t per wave tile (m, n); 16 output pixels
+    const bool bwd = a.bpart != nullptr, two = a.by2 != nullptr, st = a.stats != nullptr, maff = a.bmaff != nullptr;
+    float s1[MT][4], s2[MT][4], s3[MT][4], bm1[MT][4], bi1[MT][4], bm2[MT][4], bi2[MT][4], ksh[MT][4], msc[MT][4],
+        msh[MT][4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      bm1[e] = bi1[e] = bm2[e] = bi2[e] = 0.f;
-      ksh[e] = (st && a.sshift) ? a.sshift[oc + e] : 0.f;
-      if (bwd) {
-        bm1[e] = a.bsaved1[oc + e];
-        bi1[e] = a.bsaved1[a.OC + oc + e];
-        if (two) {
-          bm2[e] = a.bsaved2[oc + e];
-          bi2[e] = a.bsaved2[a.OC + oc + e];
+    for (int m = 0; m < MT; ++m) {
+      const int oc = oc0 + wm * (BM / WGM) + m * 16 + 4 * (lane >> 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s1[m][e] = s2[m][e] = s3[m][e] = 0.f;
+        bm1[m][e] = bi1[m][e] = bm2[m][e] = bi2[m][e] = msc[m][e] = msh[m][e] = 0.f;
+        ksh[m][e] = (st && a.sshift) ? a.sshift[oc + e] : 0.f;
+        if (bwd) {
+          bm1[m][e] = a.bsaved1[oc + e];
+          bi1[m][e] = a.bsaved1[a.OC + oc + e];
+          if (two) {
+            bm2[m][e] = a.bsaved2[oc + e];
+            bi2[m][e] = a.bsaved2[a.OC + oc + e];
+          }
+          if (maff) {
+            msc[m][e] = a.bmaff[oc + e];
+            msh[m][e] = a.bmaff[a.OC + oc + e];
+          }
         }
       }
     }
-    if (t < a.npix) {
-      const int tw = a.wW >> 2, tpi = (a.wH >> 2) * tw;
+    const int tw = a.wW >> 2, tpi = (a.wH >> 2) * tw;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const int t = pix0 + wn * (BN / WGN) + n * 16 + (lane & 15);
+      if (t >= a.npix) continue;
       const int nn = t / tpi, rem = t - nn * tpi, ti = rem / tw, tj = rem - ti * tw;
-      const size_t base = (((size_t)nn * a.wH + 4 * ti) * a.wW + 4 * tj) * a.OC + oc;
+      const size_t tbase = (((size_t)nn * a.wH + 4 * ti) * a.wW + 4 * tj) * a.OC;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int m = 0; m < MT; ++m) {
+        const size_t base = tbase + oc0 + wm * (BM / WGM) + m * 16 + 4 * (lane >> 4);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const size_t off = base + ((size_t)i * a.wW + j) * a.OC;
-          f32x4 v = {yacc[0][i * 4 + j], yacc[1][i * 4 + j], yacc[2][i * 4 + j], yacc[3][i * 4 + j]};
-          if (HAS_RES) v += *reinterpret_cast<const f32x4*>((const float*)a.res + off);
-          if (bwd) {
-            const f32x4 om = *reinterpret_cast<const f32x4*>((const float*)a.bo + off);
-            const f32x4 y1 = *reinterpret_cast<const f32x4*>((const float*)a.by1 + off);
-            f32x4 y2 = {0.f, 0.f, 0.f, 0.f};
-            if (two) y2 = *reinterpret_cast<const f32x4*>((const float*)a.by2 + off);
-            f32x4 dz;
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              dz[e] = om[e] > 0.f ? v[e] : 0.f;
-              s1[e] += dz[e];
-              s2[e] += dz[e] * (y1[e] - bm1[e]) * bi1[e];
-              if (two) s3[e] += dz[e] * (y2[e] - bm2[e]) * bi2[e];
-            }
-            *reinterpret_cast<f32x4*>((float*)a.out + off) = a.bmask ? dz : v;
-          } else {
-            *reinterpret_cast<f32x4*>((float*)a.out + off) = v;
+          for (int j = 0; j < 4; ++j) {
+            const size_t off = base + ((size_t)i * a.wW + j) * a.OC;
+            const float(&ya)[4][16] = yacc[m * NT + n];
+            f32x4 v = {ya[0][i * 4 + j], ya[1][i * 4 + j], ya[2][i * 4 + j], ya[3][i * 4 + j]};
+            if (HAS_RES) v += *reinterpret_cast<const f32x4*>((const float*)a.res + off);
+            if (bwd) {
+              const f32x4 y1 = *reinterpret_cast<const f32x4*>((const float*)a.by1 + off);
+              f32x4 om = y1, y2 = {0.f, 0.f, 0.f, 0.f};
+              if (!maff) om = *reinterpret_cast<const f32x4*>((const float*)a.bo + off);
+              if (two) y2 = *reinterpret_cast<const f32x4*>((const float*)a.by2 + off);
+              f32x4 dz;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float d = v[e] - ksh[e];
-              s1[e] += d;
-              s2[e] += d * d;
+              for (int e = 0; e < 4; ++e) {
+                const bool pos = maff ? y1[e] * msc[m][e] + msh[m][e] > 0.f : om[e] > 0.f;
+                dz[e] = pos ? v[e] : 0.f;
+                s1[m][e] += dz[e];
+                s2[m][e] += dz[e] * (y1[e] - bm1[m][e]) * bi1[m][e];
+                if (two) s3[m][e] += dz[e] * (y2[e] - bm2[m][e]) * bi2[m][e];
+              }
+              *reinterpret_cast<f32x4*>((float*)a.out + off) = a.bmask ? dz : v;
+            } else {
+              *reinterpret_cast<f32x4*>((float*)a.out + off) = v;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float d = v[e] - ksh[m][e];
+                s1[m][e] += d;
+                s2[m][e] += d * d;
+              }
             }
           }
-        }
+      }
     }
     if (!st && !bwd) return;
     // lanes of one wave with the same channels differ in lane bits 0..3
 #pragma unroll
     for (int sh = 1; sh < 16; sh <<= 1)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        s1[e] += __shfl_xor(s1[e], sh, 64);
-        s2[e] += __shfl_xor(s2[e], sh, 64);
-        if (two) s3[e] += __shfl_xor(s3[e], sh, 64);
-      }
-    if ((lane & 15) == 0) {
-      const int nst = bwd ? a.bns : 2;
-      float* dst = (bwd ? a.bpart : a.stats) + (size_t)(pix_t & (PSX_STAT_SLOTS - 1)) * nst * a.OC + oc;
+      for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        atomicAdd(dst + e, s1[e]);
-        atomicAdd(dst + a.OC + e, s2[e]);
-        if (two) atomicAdd(dst + 2 * a.OC + e, s3[e]);
-      }
+        for (int e = 0; e < 4; ++e) {
+          s1[m][e] += __shfl_xor(s1[m][e], sh, 64);
+          s2[m][e] += __shfl_xor(s2[m][e], sh, 64);
+          if (two) s3[m][e] += __shfl_xor(s3[m][e], sh, 64);
+        }
+    // one atomic per (statistic, channel) and workgroup: the WGN pixel-slice waves of a channel
+    // range meet in LDS (a deterministic-mode slab row then has a single writer per element)
+    float* red = reinterpret_cast<float*>(smem);  // [WGN][3][BM]
+    __syncthreads();  // every wave is done with the mainloop's LDS
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = wm * (BM / WGM) + m * 16 + 4 * (lane >> 4) + e;
+          red[(wn * 3 + 0) * BM + row] = s1[m][e];
+          red[(wn * 3 + 1) * BM + row] = s2[m][e];
+          red[(wn * 3 + 2) * BM + row] = s3[m][e];
+        }
     }
+    __syncthreads();
+    const int nst = bwd ? a.bns : 2;
+    float* const sdst = bwd ? a.bpart : a.stats;
+    float* dst = a.det.slab ? a.det.slab + (size_t)pix_t * nst * a.OC
+                            : sdst + (size_t)(pix_t & (PSX_STAT_SLOTS - 1)) * nst * a.OC;
+    for (int j = tid; j < nst * BM; j += 256) {
+      const int which = j / BM, row = j - which * BM;
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < WGN; ++q) v += red[(q * 3 + which) * BM + row];
+      atomicAdd(dst + which * a.OC + oc0 + row, v);
+    }
+    if (a.det.slab) det_finish(a.det, nst, a.OC, sdst, pix_t, smem);
     return;
   }
 
@@ -1203,10 +1262,10 @@ int psx_conv_dgrad2(const void* dy, const void* wd, void* dx, const void* res, c
 // [K][36][C] -> y [N][H][W][K] (+ res) with the BN statistics (stats) or the BN-backward sums
 // (bst, conv_v2 BwdStatsDesc) of y. 32x32 workgroup tiles (16x16 per wave); C a power of two >= 32.
 int psx_wino_gemm_out(const float* V, const float* U, float* y, const float* res, float* stats,
-                      const BwdStatsDesc* bst, const void* zero, int N, int H, int W, int C, int K,
-                      const float* sshift, hipStream_t st) {
+                      const BwdStatsDesc* bst, const float* mask_aff, const void* zero, int N, int H, int W, int C,
+                      int K, const float* sshift, int bm, hipStream_t st) {
   const int T = N * (H / 4) * (W / 4);
-  if (K % 32 || C < kKS<float> || (C & (C - 1)) || H % 4 || W % 4 || T < 1) return -2;
+  if (K % bm || (bm != 32 && bm != 64) || C < kKS<float> || (C & (C - 1)) || H % 4 || W % 4 || T < 1) return -2;
   Conv2Args a{};
   a.in = V;
   a.w = U;
@@ -1224,6 +1283,7 @@ int psx_wino_gemm_out(const float* V, const float* U, float* y, const float* res
     a.bsaved2 = bst->saved2;
     a.bns = bst->y2 ? 3 : 2;
     a.bmask = bst->mask_store;
+    a.bmaff = mask_aff;
   }
   a.Nb = 1; a.IH = 36; a.IW = T; a.OH = 1; a.OW = T;
   a.IC = C;
@@ -1232,19 +1292,26 @@ int psx_wino_gemm_out(const float* V, const float* U, float* y, const float* res
   a.Kg = 36 * C;
   a.log2_icc = ilog2i(C / kEPC<float>);
   a.npix = T;
-  a.n_oc_tiles = K / 32;
+  a.n_oc_tiles = K / bm;
   a.n_pix_tiles = (T + 31) / 32;
   a.splits = 1;
   a.kps = C / kKS<float>;
   a.wH = H;
   a.wW = W;
-  const size_t lds = (size_t)3 * (32 + 32) * 128;
+  const size_t lds = (size_t)3 * (bm + 32) * 128;
   const dim3 grid(a.n_oc_tiles * a.n_pix_tiles);
   with_det(a, a.n_pix_tiles);
-  if (res)
+  // bm = 64: 32 x 16 wave tiles (two MFMA tiles per wave), bm = 32: 16 x 16
+  if (bm == 64) {
+    if (res)
+      hipLaunchKernelGGL((conv2_kernel<float, 64, 32, 0, true, false, 2, 0, true>), grid, dim3(256), lds, st, a);
+    else
+      hipLaunchKernelGGL((conv2_kernel<float, 64, 32, 0, false, false, 2, 0, true>), grid, dim3(256), lds, st, a);
+  } else if (res) {
     hipLaunchKernelGGL((conv2_kernel<float, 32, 32, 0, true, false, 2, 0, true>), grid, dim3(256), lds, st, a);
-  else
+  } else {
     hipLaunchKernelGGL((conv2_kernel<float, 32, 32, 0, false, false, 2, 0, true>), grid, dim3(256), lds, st, a);
+  }
   return (int)hipGetLastError();
 }
 

@@ -38,8 +38,8 @@
 extern "C" int psx_bgemm_f32(const float* A, const float* B, float* P, const void* zero, int M, int N, int Kd, int nb,
                              int cfg, hipStream_t st);
 extern "C" int psx_wino_gemm_out(const float* V, const float* U, float* y, const float* res, float* stats,
-                                 const void* bst, const void* zero, int N, int H, int W, int C, int K,
-                                 const float* sshift, hipStream_t st);
+                                 const void* bst, const float* mask_aff, const void* zero, int N, int H, int W, int C,
+                                 int K, const float* sshift, int bm, hipStream_t st);
 extern "C" int psx_bgemm_tn_f32(const float* X, const float* D, float* part, const void* zero, int T, int C, int K,
                                 int nb, int q, int BR, int BC, hipStream_t st);
 
@@ -60,6 +60,13 @@ PSX_DEV void wino_at6(const float (&m)[6], float (&o)[4]) {
   o[1] = b + 2.f * d;
   o[2] = a + 4.f * c;
   o[3] = b + 8.f * d + m[5];
+}
+
+PSX_DEV void wino_gt6(const float (&m)[6], float (&o)[3]) {
+  const float a = m[1] + m[2], b = m[1] - m[2], c = m[3] + m[4], d = m[3] - m[4];
+  o[0] = 0.25f * m[0] - a * (1.f / 6.f) + c * (1.f / 24.f);
+  o[1] = -b * (1.f / 6.f) + d * (1.f / 12.f);
+  o[2] = -a * (1.f / 6.f) + c * (1.f / 6.f) + m[5];
 }
 
 // Forward BN finalize descriptor (the layout of bnfin.hpp BnFin)
@@ -127,18 +134,30 @@ __global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ 
     const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
     const int h0 = 4 * ti - 1, w0 = 4 * tj - 1;
     const float* xn = x + (size_t)n * H * W * C + c;
+    // all 36 loads unconditional (a padding position reads pixel (0, 0) of the image and is
+    // zeroed after): per-element guarded loads made the compiler wait for every load before the
+    // next (36 serialized round trips; 4x4x512 layer 11.8 us for a 2.5 us byte time)
     float d[6][6];
+    unsigned okr = 0, okc = 0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      okr |= (unsigned)((unsigned)(h0 + r) < (unsigned)H) << r;
+      okc |= (unsigned)((unsigned)(w0 + r) < (unsigned)W) << r;
+    }
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll
       for (int s = 0; s < 6; ++s) {
-        const int h = h0 + r, w = w0 + s;
-        float v = 0.f;  // zero padding stays zero (outside the image, after BN + ReLU)
-        if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
-          v = xn[((size_t)h * W + w) * C];
-          if (bnpart) v = fmaxf(v * sc + sh, 0.f);
-        }
-        d[r][s] = v;
+        const bool ok = (okr >> r) & (okc >> s) & 1u;
+        d[r][s] = xn[ok ? ((size_t)(h0 + r) * W + (w0 + s)) * C : 0];
+      }
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {
+        const bool ok = (okr >> r) & (okc >> s) & 1u;
+        const float v = bnpart ? fmaxf(d[r][s] * sc + sh, 0.f) : d[r][s];
+        d[r][s] = ok ? v : 0.f;  // zero padding stays zero (outside the image, after BN + ReLU)
       }
     float e[6][6];  // e = B^T d (columns)
 #pragma unroll
@@ -264,6 +283,7 @@ struct WinoBwdStats {
 // wave.
 // Deterministic mode (det.slab): each workgroup's sums go to slab row blockIdx.y and the launch
 // reduces the rows in a fixed order (bnfin.hpp det_finish) into slot row 0.
+template <bool RES, bool BWD, bool MAFF, bool TWO>
 __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__ P, float* __restrict__ y,
                                                        const float* __restrict__ res, float* __restrict__ stats, int T,
                                                        int H, int W, int K, WinoBwdStats bs, DetRed det,
@@ -273,16 +293,16 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
   const int k = blockIdx.x * 64 + kl;
   const int tw = W >> 2, tpi = (H >> 2) * tw;
   const size_t bstride = (size_t)T * K;
-  const bool bwd = bs.part != nullptr, two = bs.y2 != nullptr;
+  constexpr bool bwd = BWD, two = BWD && TWO;
   float m1 = 0.f, i1 = 0.f, m2 = 0.f, i2 = 0.f, msc = 0.f, msh = 0.f;
-  if (bwd) {
+  if constexpr (bwd) {
     m1 = bs.saved1[k];
     i1 = bs.saved1[K + k];
-    if (bs.mask_aff) {
+    if constexpr (MAFF) {
       msc = bs.mask_aff[k];
       msh = bs.mask_aff[K + k];
     }
-    if (two) {
+    if constexpr (two) {
       m2 = bs.saved2[k];
       i2 = bs.saved2[K + k];
     }
@@ -291,35 +311,52 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
   const float kshift = (!bwd && sshift) ? sshift[k] : 0.f;  // forward statistics: shifted sums
   for (int t = blockIdx.y * 4 + ty; t < T; t += 4 * gridDim.y) {
     const float* pt = P + (size_t)t * K + k;
-    float m[6][6];
+    const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
+    const size_t base = (((size_t)n * H + 4 * ti) * W + 4 * tj) * K + k;
+    // every load of the tile issued up front (the variant is a template, so no per-element
+    // branch splits them into dependent round trips)
+    float m[6][6], rv[16], y1v[16], ov[16], y2v[16];
 #pragma unroll
     for (int b = 0; b < 36; ++b) m[b / 6][b % 6] = pt[b * bstride];
-    float e[4][6];  // e = A^T m (columns)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const size_t off = base + ((size_t)(e >> 2) * W + (e & 3)) * K;
+      if constexpr (RES) rv[e] = res[off];
+      if constexpr (bwd) {
+        y1v[e] = bs.y1[off];
+        if constexpr (!MAFF) ov[e] = bs.o[off];
+        if constexpr (two) y2v[e] = bs.y2[off];
+      }
+    }
+    float e6[4][6];  // A^T m (columns)
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
       float col[6] = {m[0][s], m[1][s], m[2][s], m[3][s], m[4][s], m[5][s]}, o[4];
       wino_at6(col, o);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) e[i][s] = o[i];
+      for (int i = 0; i < 4; ++i) e6[i][s] = o[i];
     }
-    const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
-    const size_t base = (((size_t)n * H + 4 * ti) * W + 4 * tj) * K + k;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float o[4];
-      wino_at6(e[i], o);
+      wino_at6(e6[i], o);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
+        const int e = i * 4 + j;
         const size_t off = base + ((size_t)i * W + j) * K;
         float v = o[j];
-        if (res) v += res[off];
-        if (bwd) {
-          const float y1 = bs.y1[off];
-          const bool pos = bs.mask_aff ? y1 * msc + msh > 0.f : bs.o[off] > 0.f;
+        if constexpr (RES) v += rv[e];
+        if constexpr (bwd) {
+          const float y1 = y1v[e];
+          bool pos;
+          if constexpr (MAFF)
+            pos = y1 * msc + msh > 0.f;
+          else
+            pos = ov[e] > 0.f;
           const float dz = pos ? v : 0.f;
           s1 += dz;
           s2 += dz * (y1 - m1) * i1;
-          if (two) s3 += dz * (bs.y2[off] - m2) * i2;
+          if constexpr (two) s3 += dz * (y2v[e] - m2) * i2;
           y[off] = bs.mask_store ? dz : v;
         } else {
           y[off] = v;
@@ -396,16 +433,325 @@ __global__ __launch_bounds__(256) void wino_dy_kernel(const float* __restrict__ 
   }
 }
 
+// ---- Split transforms: one tile per 6-wave workgroup iteration, one transform row per wave ----
+// The kernels above give every thread a whole tile (36 loads + 36 stores of one (tile, channel)):
+// on the 4x4 / 8x8 layers that is 1-4 waves per CU, each one long dependent chain, and the
+// launch runs at 2-4x its byte time. Here a workgroup = 64 channels x 6 waves takes a tile per
+// iteration: wave r loads row r of the tile (6 loads), applies the row transform, hands the 6
+// results over LDS (double-buffered: one barrier per tile), and wave s then applies the column
+// transform to column s and stores it (6 stores). 6x the waves, 1/6 of the chain per wave, the
+// next tile's row prefetched behind the current tile's transform.
+constexpr int kXfWaves = 6;
+
+// grid.y of the split kernels: ~8 workgroups per CU over the channel blocks, at most a tile each
+int wino_xf_grid(int T, int cblocks) {
+  int gy = 2048 / cblocks;
+  if (gy < 1) gy = 1;
+  return gy > T ? T : gy;
+}
+
+// V = B^T d B (wino_in_kernel, split): bnpart / fin as there
+__global__ __launch_bounds__(384) void wino_in_xf_kernel(const float* __restrict__ x, float* __restrict__ V, int T,
+                                                         int H, int W, int C, const float* __restrict__ bnpart,
+                                                         WinoBnFin fin) {
+  __shared__ float xf[2][6][6][64];
+  __shared__ float aff[2][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int tw = W >> 2, tpi = (H >> 2) * tw;
+  const size_t bs = (size_t)T * C;
+  auto load = [&](int t, float (&d)[6], unsigned& okc, bool& okr) {
+    const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
+    const int h = 4 * ti - 1 + wv, w0 = 4 * tj - 1;
+    okr = (unsigned)h < (unsigned)H;
+    okc = 0;
+    const float* xr = x + ((size_t)n * H + (okr ? h : 0)) * W * C + c;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const bool ok = (unsigned)(w0 + s) < (unsigned)W;
+      okc |= (unsigned)ok << s;
+      d[s] = xr[(size_t)(ok ? w0 + s : 0) * C];  // unconditional (zeroed below when padding)
+    }
+  };
+  int t = blockIdx.y;
+  float d[6];
+  unsigned okc = 0;
+  bool okr = false;
+  if (t < T) load(t, d, okc, okr);
+  float sc = 1.f, sh = 0.f;
+  if (bnpart) {
+    if (wv == 0) {  // BN finalize of the workgroup's 64 channels (wino_in_kernel)
+      double s = 0.0, ss = 0.0;
+#pragma unroll
+      for (int q = 0; q < PSX_STAT_SLOTS; ++q) {
+        s += bnpart[(size_t)q * 2 * C + c];
+        ss += bnpart[(size_t)q * 2 * C + C + c];
+      }
+      double mean, var;
+      bn_moments(s, ss, fin.count, fin.sshift ? fin.sshift[c] : 0.f, mean, var);
+      const float invstd = (float)(1.0 / sqrt(var + (double)fin.eps));
+      const float a = fin.gamma[c] * invstd, b = fin.beta[c] - (float)mean * a;
+      aff[0][lane] = a;
+      aff[1][lane] = b;
+      if (blockIdx.y == 0) {
+        fin.scale[c] = a;
+        fin.shift[c] = b;
+        fin.save_mean[c] = (float)mean;
+        fin.save_invstd[c] = invstd;
+        if (fin.sshift_next) fin.sshift_next[c] = (float)mean;
+        if (fin.run_mean) {
+          const double unb = fin.count > 1.f ? var * fin.count / (fin.count - 1.0) : var;
+          fin.run_mean[c] = (1.f - fin.momentum) * fin.run_mean[c] + fin.momentum * (float)mean;
+          fin.run_var[c] = (1.f - fin.momentum) * fin.run_var[c] + fin.momentum * (float)unb;
+        }
+      }
+    }
+    __syncthreads();
+    sc = aff[0][lane];
+    sh = aff[1][lane];
+  }
+  for (int p = 0; t < T; t += gridDim.y, p ^= 1) {
+    float cur[6];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const float v = bnpart ? fmaxf(d[s] * sc + sh, 0.f) : d[s];
+      cur[s] = (okr && ((okc >> s) & 1u)) ? v : 0.f;  // zero padding stays zero after BN + ReLU
+    }
+    const int tn = t + gridDim.y;
+    if (tn < T) load(tn, d, okc, okr);
+    float e[6];  // row wv of d B
+    wino_bt6(cur, e);
+#pragma unroll
+    for (int s = 0; s < 6; ++s) xf[p][wv][s][lane] = e[s];
+    __syncthreads();
+    float col[6], o[6];  // column wv of (d B): B^T applied
+#pragma unroll
+    for (int r = 0; r < 6; ++r) col[r] = xf[p][r][wv][lane];
+    wino_bt6(col, o);
+    float* vt = V + (size_t)t * C + c;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) vt[(r * 6 + wv) * bs] = o[r];
+  }
+}
+
+// D = A dy A^T (wino_dy_kernel, split): waves 0-3 load the 4 rows of the dy tile
+__global__ __launch_bounds__(384) void wino_dy_xf_kernel(const float* __restrict__ dy, float* __restrict__ D, int T,
+                                                         int H, int W, int K) {
+  __shared__ float xf[2][4][6][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;
+  const int tw = W >> 2, tpi = (H >> 2) * tw;
+  const size_t bs = (size_t)T * K;
+  auto load = [&](int t, float (&y)[4]) {
+    const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
+    const float* src = dy + (((size_t)n * H + 4 * ti + wv) * W + 4 * tj) * K + k;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = src[(size_t)j * K];
+  };
+  int t = blockIdx.y;
+  float y[4];
+  if (t < T && wv < 4) load(t, y);
+  for (int p = 0; t < T; t += gridDim.y, p ^= 1) {
+    if (wv < 4) {
+      float cur[4] = {y[0], y[1], y[2], y[3]}, e[6];
+      const int tn = t + gridDim.y;
+      if (tn < T) load(tn, y);
+      wino_a4(cur, e);  // row wv of dy A^T
+#pragma unroll
+      for (int s = 0; s < 6; ++s) xf[p][wv][s][lane] = e[s];
+    }
+    __syncthreads();
+    float col[4] = {xf[p][0][wv][lane], xf[p][1][wv][lane], xf[p][2][wv][lane], xf[p][3][wv][lane]}, o[6];
+    wino_a4(col, o);
+    float* dt = D + (size_t)t * K + k;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) dt[(r * 6 + wv) * bs] = o[r];
+  }
+}
+
+// y = A^T P A (wino_out_kernel, split): wave r loads row r of the 6x6 tile and applies A^T to
+// it; waves 0-3 then each finish output column j (pixels (i, j), i = 0..3) with its epilogue.
+template <bool RES, bool BWD, bool MAFF, bool TWO>
+__global__ __launch_bounds__(384) void wino_out_xf_kernel(const float* __restrict__ P, float* __restrict__ y,
+                                                          const float* __restrict__ res, float* __restrict__ stats,
+                                                          int T, int H, int W, int K, WinoBwdStats bs, DetRed det,
+                                                          const float* __restrict__ sshift) {
+  __shared__ float xf[2][6][4][64];
+  __shared__ float red[3][4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;
+  const int tw = W >> 2, tpi = (H >> 2) * tw;
+  const size_t bstride = (size_t)T * K;
+  constexpr bool bwd = BWD, two = BWD && TWO;
+  float m1 = 0.f, i1 = 0.f, m2 = 0.f, i2 = 0.f, msc = 0.f, msh = 0.f;
+  if constexpr (bwd) {
+    m1 = bs.saved1[k];
+    i1 = bs.saved1[K + k];
+    if constexpr (MAFF) {
+      msc = bs.mask_aff[k];
+      msh = bs.mask_aff[K + k];
+    }
+    if constexpr (two) {
+      m2 = bs.saved2[k];
+      i2 = bs.saved2[K + k];
+    }
+  }
+  const float kshift = (!bwd && sshift) ? sshift[k] : 0.f;  // forward statistics: shifted sums
+  float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  auto load = [&](int t, float (&m)[6]) {
+    const float* pt = P + (size_t)t * K + k + (size_t)(wv * 6) * bstride;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) m[s] = pt[s * bstride];
+  };
+  int t = blockIdx.y;
+  float m[6];
+  if (t < T) load(t, m);
+  for (int p = 0; t < T; t += gridDim.y, p ^= 1) {
+    {
+      float cur[6] = {m[0], m[1], m[2], m[3], m[4], m[5]}, q[4];
+      const int tn = t + gridDim.y;
+      if (tn < T) load(tn, m);
+      wino_at6(cur, q);  // row wv of P A
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xf[p][wv][j][lane] = q[j];
+    }
+    const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
+    const size_t base = (((size_t)n * H + 4 * ti) * W + 4 * tj + wv) * K + k;  // pixel (0, wv)
+    float rv[4], y1v[4], ov[4], y2v[4];
+    if (wv < 4) {  // the epilogue's operands, issued before the barrier
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const size_t off = base + (size_t)i * W * K;
+        if constexpr (RES) rv[i] = res[off];
+        if constexpr (bwd) {
+          y1v[i] = bs.y1[off];
+          if constexpr (!MAFF) ov[i] = bs.o[off];
+          if constexpr (two) y2v[i] = bs.y2[off];
+        }
+      }
+    }
+    __syncthreads();
+    if (wv < 4) {
+      float col[6], o[4];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) col[r] = xf[p][r][wv][lane];
+      wino_at6(col, o);  // output column wv: A^T applied
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const size_t off = base + (size_t)i * W * K;
+        float v = o[i];
+        if constexpr (RES) v += rv[i];
+        if constexpr (bwd) {
+          const float y1 = y1v[i];
+          bool pos;
+          if constexpr (MAFF)
+            pos = y1 * msc + msh > 0.f;
+          else
+            pos = ov[i] > 0.f;
+          const float dz = pos ? v : 0.f;
+          s1 += dz;
+          s2 += dz * (y1 - m1) * i1;
+          if constexpr (two) s3 += dz * (y2v[i] - m2) * i2;
+          y[off] = bs.mask_store ? dz : v;
+        } else {
+          y[off] = v;
+          const float dd = v - kshift;
+          s1 += dd;
+          s2 += dd * dd;
+        }
+      }
+    }
+  }
+  float* dst = bwd ? bs.part : stats;
+  if (!dst) return;
+  const int nst = bwd ? (two ? 3 : 2) : 2;
+  if (wv < 4) {
+    red[0][wv][lane] = s1;
+    red[1][wv][lane] = s2;
+    red[2][wv][lane] = s3;
+  }
+  __syncthreads();
+  float* row = det.slab ? det.slab + (size_t)blockIdx.y * nst * K
+                        : dst + (size_t)(blockIdx.y & (PSX_STAT_SLOTS - 1)) * nst * K;
+  if (threadIdx.x < 64 * nst) {
+    const int which = threadIdx.x >> 6;
+    const float v = red[which][0][lane] + red[which][1][lane] + red[which][2][lane] + red[which][3][lane];
+    atomicAdd(row + (size_t)which * K + k, v);
+  }
+  if (det.slab) {
+    __syncthreads();  // red[] is reused as the hand-off flag
+    det_finish(det, nst, K, dst, blockIdx.y, reinterpret_cast<unsigned char*>(&red[0][0][0]));
+  }
+}
+
+// dW = scale * G^T M G (wino_wout_kernel, split): a workgroup = 64 (k, c) pairs x 6 waves; wave r
+// sums the q partial slabs of row r of M (6 q loads in flight, unrolled for Q > 0) and applies G
+// along the row, waves 0-2 then take column j of the result through LDS, and the workgroup's
+// 64 x 9 outputs leave as one contiguous run. The one-thread-per-pair kernel issued 36 q
+// loads per thread from (K C / 256) workgroups: 16 for a 64 x 64 layer, a latency chain
+// (q = 8 with its runtime loop: +50 us).
+template <typename OutT, int Q>
+__global__ __launch_bounds__(384) void wino_wout_xf_kernel(const float* __restrict__ part, OutT* __restrict__ out,
+                                                           int K, int C, int q, float scale) {
+  __shared__ float mg[6][3][64];
+  __shared__ float stage[64 * 9];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long i0 = (long)blockIdx.x * 64, n = (long)K * C;
+  const long i = i0 + lane;
+  const int qq = Q > 0 ? Q : q;
+  const size_t slab = (size_t)K * C;
+  if (i < n) {
+    float m6[6], o[3];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const float* p = part + (size_t)(wv * 6 + s) * qq * slab + i;
+      float v = p[0];
+      if constexpr (Q > 0) {
+#pragma unroll
+        for (int j = 1; j < Q; ++j) v += p[j * slab];
+      } else {
+        for (int j = 1; j < qq; ++j) v += p[j * slab];
+      }
+      m6[s] = v;
+    }
+    wino_gt6(m6, o);  // row wv of M G
+#pragma unroll
+    for (int j = 0; j < 3; ++j) mg[wv][j][lane] = o[j];
+  }
+  __syncthreads();
+  if (wv < 3 && i < n) {
+    float col[6], o[3];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) col[r] = mg[r][wv][lane];
+    wino_gt6(col, o);  // column wv of G^T (M G)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) stage[lane * 9 + p * 3 + wv] = o[p] * scale;
+  }
+  __syncthreads();
+  const long lim = (n - i0 < 64 ? n - i0 : 64) * 9;
+  OutT* dst = out + i0 * 9;
+  for (int j = threadIdx.x; j < lim; j += 384) {
+    const float v = stage[j];
+    if constexpr (sizeof(OutT) == 2)
+      dst[j] = __builtin_bit_cast(uint16_t, (_Float16)v);
+    else
+      dst[j] = v;
+  }
+}
+
+// PSX_WINO_XF=0: the whole-tile-per-thread transforms (A/B)
+static bool wino_xf_on() {
+  static const bool on = [] {
+    const char* e = getenv("PSX_WINO_XF");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 // dW[k][c][3][3] = scale * G^T M G, M[b] = sum of the q partial slabs part[b * q + j][k][c]
 // (the batched TN GEMM's split of each batch over tile ranges). One thread per (k, c), c fastest;
 // OutT = uint16_t: the fp16 wire (reference codec), float: fp32 gradients. OIHW like
 // wgrad_reduce's output.
-PSX_DEV void wino_gt6(const float (&m)[6], float (&o)[3]) {
-  const float a = m[1] + m[2], b = m[1] - m[2], c = m[3] + m[4], d = m[3] - m[4];
-  o[0] = 0.25f * m[0] - a * (1.f / 6.f) + c * (1.f / 24.f);
-  o[1] = -b * (1.f / 6.f) + d * (1.f / 12.f);
-  o[2] = -a * (1.f / 6.f) + c * (1.f / 6.f) + m[5];
-}
 
 template <typename OutT, int Q>
 __global__ __launch_bounds__(256) void wino_wout_kernel(const float* __restrict__ part, OutT* __restrict__ out, int K,
@@ -530,25 +876,65 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
   const int gy = wino_tile_grid(T);
   WinoBnFin bf{};
   if (bnpart) bf = *bnfin;
-  hipLaunchKernelGGL(wino_in_kernel, dim3(C / 64, gy), dim3(256), 0, st, x, V, T, H, W, C, bnpart, bf);
-  // fused GEMM + output transform (conv_v2.hip WOUT: P stays in registers), PSX_WINO_FUSED=1
-  // where its 32x32 tiles fill the chip, 2 always (tests). Off by default: its 16x16 wave tiles
-  // (the 16 output pixels of every accumulator element take 64 registers) run the MFMA far below
-  // the 64x64-tile batched GEMM; same-box per layer 32x32x64 85 vs 82 us, 16x16x128 98 vs 54 us,
-  // bench 4.01 vs 3.83 ms/step
+  if (wino_xf_on())
+    hipLaunchKernelGGL(wino_in_xf_kernel, dim3(C / 64, wino_xf_grid(T, C / 64)), dim3(64 * kXfWaves), 0, st, x, V, T,
+                       H, W, C, bnpart, bf);
+  else
+    hipLaunchKernelGGL(wino_in_kernel, dim3(C / 64, gy), dim3(256), 0, st, x, V, T, H, W, C, bnpart, bf);
+  // fused GEMM + output transform (conv_v2.hip WOUT: P stays in registers, so the 36 x T x K
+  // product never round-trips HBM). PSX_WINO_FUSED = 0 off, 1 where its 64 x 32 workgroup tiles
+  // (32 x 16 wave tiles) give >= PSX_WINO_FUSED_MINWG (default 256) workgroups, 2 always (tests).
+  // (read per call: the tests switch it inside one process; graph capture runs this once)
   const char* fe = getenv("PSX_WINO_FUSED");
   const int fused_mode = fe ? atoi(fe) : 0;
-  if (K % 32 == 0 && !(bst && bst->mask_aff) &&
-      (fused_mode == 2 || (fused_mode == 1 && (long)(K / 32) * ((T + 31) / 32) >= 256)))
-    return psx_wino_gemm_out(V, U, y, res, stats, bst, zero, N, H, W, C, K, sshift, st);
+  const char* fm = getenv("PSX_WINO_FUSED_MINWG");
+  const long fused_minwg = fm && atol(fm) > 0 ? atol(fm) : 256L;
+  if (fused_mode && K % 32 == 0) {
+    const int bm = K % 64 == 0 ? 64 : 32;
+    if (fused_mode == 2 || (bm == 64 && (long)(K / 64) * ((T + 31) / 32) >= fused_minwg)) {
+      const WinoBwdStats* b = bst;
+      struct {
+        float* part;
+        const void* o;
+        const void* y1;
+        const void* y2;
+        const float* saved1;
+        const float* saved2;
+        int mask_store;
+      } d{};  // conv_v2.hip BwdStatsDesc
+      if (b) d = {b->part, b->o, b->y1, b->y2, b->saved1, b->saved2, b->mask_store};
+      return psx_wino_gemm_out(V, U, y, res, stats, b ? &d : nullptr, b ? b->mask_aff : nullptr, zero, N, H, W, C, K,
+                               sshift, bm, st);
+    }
+  }
   int e = psx_bgemm_f32(V, U, P, zero, T, K, C, 36, cfg, st);
   if (e) return e;
   WinoBwdStats bs{};
   if (bst) bs = *bst;
+  const bool xf = wino_xf_on();
+  const int gyo = xf ? wino_xf_grid(T, K / 64) : gy;
   DetRed det{};
-  if (bst || stats) det = det_next(gy, bst ? (bst->y2 ? 3 : 2) : 2, K, K / 64);
-  hipLaunchKernelGGL(wino_out_kernel, dim3(K / 64, gy), dim3(256), 0, st, P, y, res, bst ? nullptr : stats, T, H, W,
-                     K, bs, det, sshift);
+  if (bst || stats) det = det_next(gyo, bst ? (bst->y2 ? 3 : 2) : 2, K, K / 64);
+  using OutK = void (*)(const float*, float*, const float*, float*, int, int, int, int, WinoBwdStats, DetRed,
+                       const float*);
+  // [res][variant]: forward, backward (ReLU mask from o / from the affine) x (one / two BN sums)
+  static const OutK kOut[2][5] = {
+      {wino_out_kernel<false, false, false, false>, wino_out_kernel<false, true, false, false>,
+       wino_out_kernel<false, true, false, true>, wino_out_kernel<false, true, true, false>,
+       wino_out_kernel<false, true, true, true>},
+      {wino_out_kernel<true, false, false, false>, wino_out_kernel<true, true, false, false>,
+       wino_out_kernel<true, true, false, true>, wino_out_kernel<true, true, true, false>,
+       wino_out_kernel<true, true, true, true>}};
+  static const OutK kOutXf[2][5] = {
+      {wino_out_xf_kernel<false, false, false, false>, wino_out_xf_kernel<false, true, false, false>,
+       wino_out_xf_kernel<false, true, false, true>, wino_out_xf_kernel<false, true, true, false>,
+       wino_out_xf_kernel<false, true, true, true>},
+      {wino_out_xf_kernel<true, false, false, false>, wino_out_xf_kernel<true, true, false, false>,
+       wino_out_xf_kernel<true, true, false, true>, wino_out_xf_kernel<true, true, true, false>,
+       wino_out_xf_kernel<true, true, true, true>}};
+  const int var = bst ? 1 + 2 * (bs.mask_aff != nullptr) + (bs.y2 != nullptr) : 0;
+  hipLaunchKernelGGL((xf ? kOutXf : kOut)[res != nullptr][var], dim3(K / 64, gyo), dim3(xf ? 64 * kXfWaves : 256), 0,
+                     st, P, y, res, bst ? nullptr : stats, T, H, W, K, bs, det, sshift);
   return (int)hipGetLastError();
 }
 
@@ -560,8 +946,10 @@ static int wino_wtile(int C, int K) {
 
 // Tile-range splits q of the weight-gradient GEMM: 36 * q * (C/BR) * (K/BC) workgroups, each
 // over T / q tiles (a multiple of 32): the smallest q reaching 1024 workgroups while a split keeps
-// >= 256 tiles, at most 4. Same-box sweep (B=128, us, q = 1 / 2 / 4 / 8): 8x8x256 48 / 43 / - / 107,
-// 16x16x128 - / 62 / 52 / 106, 4x4x512 45 / 52 / - / -. 0 = not applicable.
+// >= 256 tiles, at most 8 (PSX_WINO_WQ_MAX). Same-box sweep with the split output transform (B=128,
+// us incl. dy transform, q = 1 / 2 / 4 / 8 / 16): 32x32x64 244 / 134 / 79 / 69 / 83, 16x16x128
+// 72 / 62 / 51 / 48 / 69, 8x8x256 51 / 46 / 47 / 55 / 81, 4x4x512 47 / 54 / 75 (bench/wino_fused_ab.py).
+// 0 = not applicable.
 int psx_wino_wgrad_q(int N, int H, int W, int C, int K) {
   const int T = N * (H / 4) * (W / 4);
   if (!psx_wino_ok(H, W, C, K) || T % 32) return 0;
@@ -569,7 +957,7 @@ int psx_wino_wgrad_q(int N, int H, int W, int C, int K) {
   int q = 1;
   static const int qmax = [] {
     const char* e = getenv("PSX_WINO_WQ_MAX");
-    return e && atoi(e) > 0 ? atoi(e) : 4;
+    return e && atoi(e) > 0 ? atoi(e) : 8;
   }();
   if (const char* e = getenv("PSX_WINO_WQ"); e && atoi(e) > 0) q = atoi(e);
   else
@@ -585,12 +973,36 @@ int psx_wino_wgrad(const float* V, const float* dy, float* D, float* part, void*
   const int q = psx_wino_wgrad_q(N, H, W, C, K);
   if (q < 1) return -2;
   const int T = N * (H / 4) * (W / 4);
-  hipLaunchKernelGGL(wino_dy_kernel, dim3(K / 64, wino_tile_grid(T)), dim3(256), 0, st, dy, D, T, H, W, K);
+  if (wino_xf_on())
+    hipLaunchKernelGGL(wino_dy_xf_kernel, dim3(K / 64, wino_xf_grid(T, K / 64)), dim3(64 * kXfWaves), 0, st, dy, D, T,
+                       H, W, K);
+  else
+    hipLaunchKernelGGL(wino_dy_kernel, dim3(K / 64, wino_tile_grid(T)), dim3(256), 0, st, dy, D, T, H, W, K);
   const int bt = wino_wtile(C, K);
   int e = psx_bgemm_tn_f32(V, D, part, zero, T, C, K, 36, q, bt, bt, st);
   if (e) return e;
   const long n = (long)K * C;
   const dim3 grid((unsigned)((n + 255) / 256));
+  if (wino_xf_on()) {
+    const dim3 gx((unsigned)((n + 63) / 64));
+#define PSX_WOUT(OT, QV) \
+  hipLaunchKernelGGL((wino_wout_xf_kernel<OT, QV>), gx, dim3(64 * kXfWaves), 0, st, part, (OT*)out, K, C, q, scale)
+    if (out_fp16) {
+      if (q == 1) PSX_WOUT(uint16_t, 1);
+      else if (q == 2) PSX_WOUT(uint16_t, 2);
+      else if (q == 4) PSX_WOUT(uint16_t, 4);
+      else if (q == 8) PSX_WOUT(uint16_t, 8);
+      else PSX_WOUT(uint16_t, 0);
+    } else {
+      if (q == 1) PSX_WOUT(float, 1);
+      else if (q == 2) PSX_WOUT(float, 2);
+      else if (q == 4) PSX_WOUT(float, 4);
+      else if (q == 8) PSX_WOUT(float, 8);
+      else PSX_WOUT(float, 0);
+    }
+#undef PSX_WOUT
+    return (int)hipGetLastError();
+  }
 #define PSX_WOUT(OT, QV) hipLaunchKernelGGL((wino_wout_kernel<OT, QV>), grid, dim3(256), 0, st, part, (OT*)out, K, C, q, scale)
   if (out_fp16) {
     if (q == 1) PSX_WOUT(uint16_t, 1);

@@ -34,6 +34,7 @@
 
 #include "bnfin.hpp"
 #include "common.hpp"
+#include "wino.hpp"
 
 extern "C" int psx_bgemm_f32(const float* A, const float* B, float* P, const void* zero, int M, int N, int Kd, int nb,
                              int cfg, hipStream_t st);
@@ -44,47 +45,6 @@ extern "C" int psx_bgemm_tn_f32(const float* X, const float* D, float* part, con
                                 int nb, int q, int BR, int BC, hipStream_t st);
 
 namespace psx {
-
-PSX_DEV void wino_bt6(const float (&d)[6], float (&r)[6]) {
-  r[0] = 4.f * d[0] - 5.f * d[2] + d[4];
-  r[1] = -4.f * (d[1] + d[2]) + d[3] + d[4];
-  r[2] = 4.f * (d[1] - d[2]) - d[3] + d[4];
-  r[3] = 2.f * (d[3] - d[1]) - d[2] + d[4];
-  r[4] = 2.f * (d[1] - d[3]) - d[2] + d[4];
-  r[5] = 4.f * d[1] - 5.f * d[3] + d[5];
-}
-
-PSX_DEV void wino_at6(const float (&m)[6], float (&o)[4]) {
-  const float a = m[1] + m[2], b = m[1] - m[2], c = m[3] + m[4], d = m[3] - m[4];
-  o[0] = m[0] + a + c;
-  o[1] = b + 2.f * d;
-  o[2] = a + 4.f * c;
-  o[3] = b + 8.f * d + m[5];
-}
-
-PSX_DEV void wino_gt6(const float (&m)[6], float (&o)[3]) {
-  const float a = m[1] + m[2], b = m[1] - m[2], c = m[3] + m[4], d = m[3] - m[4];
-  o[0] = 0.25f * m[0] - a * (1.f / 6.f) + c * (1.f / 24.f);
-  o[1] = -b * (1.f / 6.f) + d * (1.f / 12.f);
-  o[2] = -a * (1.f / 6.f) + c * (1.f / 6.f) + m[5];
-}
-
-// Forward BN finalize descriptor (the layout of bnfin.hpp BnFin)
-struct WinoBnFin {
-  const float* gamma;
-  const float* beta;
-  float* run_mean;
-  float* run_var;
-  float* scale;
-  float* shift;
-  float* save_mean;
-  float* save_invstd;
-  unsigned* counter;
-  float count, eps, momentum;
-  int C;
-  const float* sshift;  // shifted sums (bnfin.hpp BnFin::sshift)
-  float* sshift_next;
-};
 
 // V[b][t][c]: one thread per (tile, channel); block = 64 channels x 4 tiles.
 // bnpart (nullable): x is the PRE-BatchNorm conv output z of the previous layer, and the operand
@@ -223,7 +183,7 @@ __global__ __launch_bounds__(64) void wino_w_kernel(const float* __restrict__ w,
 struct WinoWDesc {
   const float* w;
   float* U;
-  int K, C, flip, pad_;
+  int K, C, flip, layout;
   long p0;
 };
 constexpr int kWinoWMax = 40;
@@ -251,31 +211,29 @@ __global__ __launch_bounds__(64) void wino_w_multi_kernel(WinoWBatch bt) {
   for (int p = 0; p < 3; ++p)
 #pragma unroll
     for (int q = 0; q < 3; ++q) gg[p][q] = flip ? g[(2 - p) * 3 + (2 - q)] : g[p * 3 + q];
-  float* dst = d.U + (size_t)row * 36 * cols + col;
+  // layout 0: U[row][36][col] (the batched GEMM's operand); 1: the fused kernel's MFMA B-operand
+  // order (wino_fused.hip): [row/16][col/4][slot 10][lane = (col%4)*16 + row%16][4], slot 5h + i
+  // (i < 4) = points 18h + 4i .. +3, slot 5h + 4 = points 18h + 16, 18h + 17 and two zeros
+  float* dst = d.layout ? d.U + ((size_t)(row >> 4) * (cols >> 2) + (col >> 2)) * 2560 + ((col & 3) * 16 + (row & 15)) * 4
+                        : d.U + (size_t)row * 36 * cols + col;
+  if (d.layout) {
+    dst[4 * 256 + 2] = dst[4 * 256 + 3] = 0.f;
+    dst[9 * 256 + 2] = dst[9 * 256 + 3] = 0.f;
+  }
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     float gr[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) gr[q] = kWinoG[r][0] * gg[0][q] + kWinoG[r][1] * gg[1][q] + kWinoG[r][2] * gg[2][q];
 #pragma unroll
-    for (int s = 0; s < 6; ++s)
-      dst[(size_t)(r * 6 + s) * cols] = kWinoG[s][0] * gr[0] + kWinoG[s][1] * gr[1] + kWinoG[s][2] * gr[2];
+    for (int s = 0; s < 6; ++s) {
+      const int b = r * 6 + s;
+      const int hb = b >= 18, m = b - 18 * hb;  // layout 1: half, local point
+      dst[d.layout ? (size_t)(5 * hb + (m >> 2)) * 256 + (m & 3) : (size_t)b * cols] =
+          kWinoG[s][0] * gr[0] + kWinoG[s][1] * gr[1] + kWinoG[s][2] * gr[2];
+    }
   }
 }
-
-// Fused BN-backward sums over a data-gradient output (the layout of conv_v2.hip BwdStatsDesc):
-// dz = g * [o > 0], slot rows [PSX_STAT_SLOTS][bns][K] of sum dz, sum dz * xhat1 (, * xhat2);
-// mask_store: store dz instead of g.
-struct WinoBwdStats {
-  float* part;
-  const float* o;
-  const float* y1;
-  const float* y2;
-  const float* saved1;  // [2][K] mean, invstd
-  const float* saved2;
-  int mask_store;
-  const float* mask_aff;  // nullable: ReLU mask = [y1 * scale + shift > 0] (affine [2][K]) instead of o
-};
 
 // y = A^T P A (+ res); forward: BN partial sums (sum y, sum y^2) of the stored values into slot
 // rows stats[slot][2][K]; data gradient (bs.part): the BN-backward sums of the consumer BN
@@ -845,13 +803,17 @@ int psx_wino_weights(const float* w, float* U, int K, int C, int flip, hipStream
 
 // n (<= 40) weight transforms in one launch: w[j] OIHW [K[j]][C[j]][3][3] -> U[j] (flip[j] as in
 // psx_wino_weights).
+// layout (nullable): per item 1 = the fused kernel's operand order (rows and columns multiples of
+// 16 and 4).
 int psx_wino_weights_multi(const float* const* w, float* const* U, const int* K, const int* C, const int* flip, int n,
-                           hipStream_t st) {
+                           const int* layout, hipStream_t st) {
   if (n < 1 || n > kWinoWMax) return -2;
   WinoWBatch b{};
   long p = 0;
   for (int j = 0; j < n; ++j) {
-    b.d[j] = WinoWDesc{w[j], U[j], K[j], C[j], flip[j], 0, p};
+    const int lay = layout ? layout[j] : 0;
+    if (lay && ((flip[j] ? C[j] : K[j]) % 16 || (flip[j] ? K[j] : C[j]) % 4)) return -3;
+    b.d[j] = WinoWDesc{w[j], U[j], K[j], C[j], flip[j], lay, p};
     p += (long)K[j] * C[j];
   }
   b.n = n;

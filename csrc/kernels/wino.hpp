@@ -1,0 +1,64 @@
+// Shared pieces of the fp32 Winograd F(4x4,3x3) kernels (wino.hip: separate transforms + batched
+// GEMMs; wino_fused.hip: transforms fused into the GEMM). Matrices in wino.hip's header comment.
+#pragma once
+#include "bnfin.hpp"
+#include "common.hpp"
+
+namespace psx {
+
+PSX_DEV void wino_bt6(const float (&d)[6], float (&r)[6]) {
+  r[0] = 4.f * d[0] - 5.f * d[2] + d[4];
+  r[1] = -4.f * (d[1] + d[2]) + d[3] + d[4];
+  r[2] = 4.f * (d[1] - d[2]) - d[3] + d[4];
+  r[3] = 2.f * (d[3] - d[1]) - d[2] + d[4];
+  r[4] = 2.f * (d[1] - d[3]) - d[2] + d[4];
+  r[5] = 4.f * d[1] - 5.f * d[3] + d[5];
+}
+
+PSX_DEV void wino_at6(const float (&m)[6], float (&o)[4]) {
+  const float a = m[1] + m[2], b = m[1] - m[2], c = m[3] + m[4], d = m[3] - m[4];
+  o[0] = m[0] + a + c;
+  o[1] = b + 2.f * d;
+  o[2] = a + 4.f * c;
+  o[3] = b + 8.f * d + m[5];
+}
+
+PSX_DEV void wino_gt6(const float (&m)[6], float (&o)[3]) {
+  const float a = m[1] + m[2], b = m[1] - m[2], c = m[3] + m[4], d = m[3] - m[4];
+  o[0] = 0.25f * m[0] - a * (1.f / 6.f) + c * (1.f / 24.f);
+  o[1] = -b * (1.f / 6.f) + d * (1.f / 12.f);
+  o[2] = -a * (1.f / 6.f) + c * (1.f / 6.f) + m[5];
+}
+
+// Forward BN finalize descriptor (the layout of bnfin.hpp BnFin)
+struct WinoBnFin {
+  const float* gamma;
+  const float* beta;
+  float* run_mean;
+  float* run_var;
+  float* scale;
+  float* shift;
+  float* save_mean;
+  float* save_invstd;
+  unsigned* counter;
+  float count, eps, momentum;
+  int C;
+  const float* sshift;  // shifted sums (bnfin.hpp BnFin::sshift)
+  float* sshift_next;
+};
+
+// Fused BN-backward sums over a data-gradient output (the layout of conv_v2.hip BwdStatsDesc):
+// dz = g * [o > 0], slot rows [PSX_STAT_SLOTS][bns][K] of sum dz, sum dz * xhat1 (, * xhat2);
+// mask_store: store dz instead of g.
+struct WinoBwdStats {
+  float* part;
+  const float* o;
+  const float* y1;
+  const float* y2;
+  const float* saved1;  // [2][K] mean, invstd
+  const float* saved2;
+  int mask_store;
+  const float* mask_aff;  // nullable: ReLU mask = [y1 * scale + shift > 0] (affine [2][K]) instead of o
+};
+
+}  // namespace psx

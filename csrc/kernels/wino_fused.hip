@@ -1,0 +1,442 @@
+// fp32 Winograd F(4x4,3x3) conv with both transforms fused into the GEMM: ONE launch per conv, the
+// transformed input V and the 36 GEMM outputs P never reach HBM (wino.hip runs input transform ->
+// 36 batched GEMMs -> output transform as three launches, V and P 2.25x the activation each way:
+// on the 32x32x64 layer ~300 MB of the ~370 MB a conv moves, 100 us per call).
+//
+// Workgroup = 16 Winograd tiles x 64 output channels, 4 waves; wave w owns output channels
+// [16w, 16w + 16) of the block and accumulates all 36 Winograd points of its 16 x 16 (tile,
+// channel) block in registers: acc[b] is one v_mfma_f32_16x16x4_f32 tile (4 floats per lane,
+// 144 accumulator registers), so lane l ends holding M_b[tile 4(l>>4)+i][channel l&15] for every b
+// and i — all 36 points of 4 (tile, channel) pairs, exactly what the output transform A^T M A of
+// those pairs needs, in the epilogue, in registers.
+//
+// The reduction runs over C in groups of 16 channels = 4 MFMA k-steps. Per group each wave
+// transforms ONE k-step of the block's 16 tiles (lane = (tile l&15, channel l>>4): the 6x6 patch
+// through buffer loads with clamped rows / columns, the optional folded BN + ReLU of the previous
+// layer, zero padding, B^T d B in registers) and writes its 36 values into the LDS group buffer in
+// the MFMA A-operand order (four points per ds_write_b128); after one barrier every wave runs the
+// group's 4 x 36 MFMAs reading A from LDS (ds_read_b128 = four points) and B (the transformed
+// weights, pre-laid out in the B-operand order by the weight transform, layout 1) straight from
+// L2 with buffer_load_dwordx4, prefetched one k-step ahead. The next group's patch loads are in
+// flight during the MFMAs; the group buffer is double-buffered (one barrier per group). 73.7 KB of
+// LDS and <= 256 registers: two workgroups per CU.
+//
+// Epilogues (same contract as wino.hip wino_out_kernel): forward (+ residual) with BN slot sums of
+// y (shifted), or data gradient with the consumer BN's backward sums (ReLU mask from o or from the
+// affine, one or two BNs) and the masked store; deterministic mode through the slab (DetRed).
+// V (nullable): the forward also stores the transformed input [36][T][C] for the Winograd weight
+// gradient (wino.hip psx_wino_wgrad), from the registers that fed LDS.
+#include "bnfin.hpp"
+#include "common.hpp"
+#include "wino.hpp"
+
+// diagnostics (A/B builds only, wrong results): bit 1 no B loads, 2 no patch loads, 4 no transform
+// VALU, 8 no V stores
+#ifndef PSX_WF_PROBE
+#define PSX_WF_PROBE 0
+#endif
+// A operands read one point quad ahead of their MFMAs
+#ifndef PSX_WF_APF
+#define PSX_WF_APF 0
+#endif
+
+namespace psx {
+
+PSX_DEV void mfma_f32_16x16x4(f32x4& acc, float a, float b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+}
+
+constexpr int kWfT = 16;  // tiles per workgroup (the MFMA's 16 rows)
+constexpr int kWfK = 64;  // output channels per workgroup (4 waves x 16)
+
+struct WinoFusedArgs {
+  const float* x;  // [N][H][W][C]
+  const float* U;  // transformed weights, layout 1 (wino.hip wino_w_multi_kernel)
+  float* y;        // [N][H][W][K]
+  const float* res;
+  float* stats;
+  float* V;  // nullable: [36][T][C]
+  const float* bnpart;
+  const float* sshift;
+  int H, W, C, K, T, nkb;
+  int xbytes, ubytes, vbytes;
+};
+
+template <int GG, bool RES, bool BWD, bool MAFF, bool TWO>
+__global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, WinoBnFin fin, WinoBwdStats bs,
+                                                            DetRed det) {
+  // [buffer][k-step][slot][lane]: slot 5h + i (i < 4) = points 18h + 4i .. +3, slot 5h + 4 = points
+  // 18h + 16, 18h + 17 (+ 2 unused floats)
+  __shared__ f32x4 vb[2][4][10][64];
+  __shared__ float aff[2][256];
+  __shared__ float red[3][4][16];
+  const int l = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int kq = w & 3, h = w >> 2;  // channel quarter, Winograd point half
+  const int id = xcd_remap(blockIdx.x, gridDim.x);  // a tile block's channel blocks on one XCD
+  const int tb = id / a.nkb, kb = id - tb * a.nkb;
+  const int H = a.H, W = a.W, C = a.C, K = a.K;
+  const int tw = W >> 2, tpi = (H >> 2) * tw;
+  const bool bnin = a.bnpart != nullptr;
+  // the transform applies max(x * aff0 + aff1, lo) unconditionally (one branch-free group body):
+  // identity (1, 0, -inf) without a folded BN
+  const float lo = bnin ? 0.f : -__builtin_inff();
+  if (!bnin) {
+    for (int c = threadIdx.x; c < C; c += 512) {
+      aff[0][c] = 1.f;
+      aff[1][c] = 0.f;
+    }
+  } else {  // BN finalize of the input channels (wino.hip wino_in_kernel), all C of them
+    for (int c = threadIdx.x; c < C; c += 512) {
+      double s = 0.0, ss = 0.0;
+#pragma unroll
+      for (int q = 0; q < PSX_STAT_SLOTS; ++q) {
+        s += a.bnpart[(size_t)q * 2 * C + c];
+        ss += a.bnpart[(size_t)q * 2 * C + C + c];
+      }
+      double mean, var;
+      bn_moments(s, ss, fin.count, fin.sshift ? fin.sshift[c] : 0.f, mean, var);
+      const float invstd = (float)(1.0 / sqrt(var + (double)fin.eps));
+      const float sc = fin.gamma[c] * invstd, sh = fin.beta[c] - (float)mean * sc;
+      aff[0][c] = sc;
+      aff[1][c] = sh;
+      if (id == 0) {
+        fin.scale[c] = sc;
+        fin.shift[c] = sh;
+        fin.save_mean[c] = (float)mean;
+        fin.save_invstd[c] = invstd;
+        if (fin.sshift_next) fin.sshift_next[c] = (float)mean;
+        if (fin.run_mean) {
+          const double unb = fin.count > 1.f ? var * fin.count / (fin.count - 1.0) : var;
+          fin.run_mean[c] = (1.f - fin.momentum) * fin.run_mean[c] + fin.momentum * (float)mean;
+          fin.run_var[c] = (1.f - fin.momentum) * fin.run_var[c] + fin.momentum * (float)unb;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- transform role (waves 0-3, wave kq = k-step kq of a group): lane = (tile l&15, channel l>>4)
+  const int tl = l & 15, cl = l >> 4;
+  const int t = tb * kWfT + tl;
+  int rowoff[6], coloff[6];
+  unsigned okr = 0, okc = 0;
+  {
+    const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const int hh = 4 * ti - 1 + r, wc = 4 * tj - 1 + r;
+      const bool oh = (unsigned)hh < (unsigned)H, ow = (unsigned)wc < (unsigned)W;
+      okr |= (unsigned)oh << r;
+      okc |= (unsigned)ow << r;
+      // clamped in-image row / column: a padding position loads a real pixel, zeroed below
+      rowoff[r] = (((n * H + (oh ? hh : (hh < 0 ? 0 : H - 1))) * W) * C + cl) * 4;
+      coloff[r] = (ow ? wc : (wc < 0 ? 0 : W - 1)) * C * 4;
+    }
+  }
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x), 0, a.xbytes, 0x00020000);
+  const auto ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U), 0, a.ubytes, 0x00020000);
+  const int S4 = C >> 2;  // MFMA k-steps
+  // B operand of wave (kq, h): k-step s at ubase + s * 10 KB, its slots 5h .. 5h + 4
+  const int ubase = ((kb * 4 + kq) * S4 * 10 + h * 5) * 1024;
+  constexpr int G = GG;  // 16-channel groups (C / 16): the group loop is fully unrolled
+  // V side output through a buffer descriptor: stores of the pipeline's one dummy transform (past
+  // the last group) go to a zero-record descriptor and are dropped
+  const auto vr = __builtin_amdgcn_make_buffer_rsrc(a.V, 0, a.V ? a.vbytes : 0, 0x00020000);
+  const auto vnull = __builtin_amdgcn_make_buffer_rsrc(a.V, 0, 0, 0x00020000);
+  const int voff = (t * C + cl) * 4;
+
+  float d[36];
+  auto load_patch = [&](int g) {
+    const int so = (g * 16 + 4 * kq) * 4;
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int s = 0; s < 6; ++s)
+        d[r * 6 + s] = (PSX_WF_PROBE & 2) ? (float)(rowoff[r] + coloff[s] + so)
+                                          : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, rowoff[r] + coloff[s], so, 0));
+  };
+  auto xform = [&](int g, int p, bool real) {
+    const int ch0 = g * 16 + 4 * kq;  // wave-uniform
+    const float sc = aff[0][ch0 + cl], sh = aff[1][ch0 + cl];
+    float e[36];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {
+        const float v = fmaxf(d[r * 6 + s] * sc + sh, lo);
+        e[r * 6 + s] = ((okr >> r) & (okc >> s) & 1u) ? v : 0.f;  // zero padding stays zero after BN + ReLU
+      }
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {  // columns: B^T d
+      float col[6] = {e[s], e[6 + s], e[12 + s], e[18 + s], e[24 + s], e[30 + s]}, o[6];
+      wino_bt6(col, o);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) e[r * 6 + s] = o[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {  // rows: (B^T d) B
+      float row[6] = {e[r * 6], e[r * 6 + 1], e[r * 6 + 2], e[r * 6 + 3], e[r * 6 + 4], e[r * 6 + 5]}, o[6];
+      wino_bt6(row, o);
+#pragma unroll
+      for (int s = 0; s < 6; ++s) e[r * 6 + s] = o[s];
+    }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = 18 * hh + 4 * i;
+        vb[p][kq][5 * hh + i][l] = (f32x4){e[b], e[b + 1], e[b + 2], e[b + 3]};
+      }
+      vb[p][kq][5 * hh + 4][l] = (f32x4){e[18 * hh + 16], e[18 * hh + 17], 0.f, 0.f};
+    }
+    const auto rs = real ? vr : vnull;  // no V output: vr has zero records too
+    if constexpr ((PSX_WF_PROBE & 8) == 0)
+#pragma unroll
+    for (int b = 0; b < 36; ++b)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e[b]), rs, voff, (b * a.T * C + ch0) * 4, 0);
+  };
+
+  // acc[m]: local point m = 0..17 of this wave's half (point 18h + m)
+  f32x4 acc[18];
+#pragma unroll
+  for (int m = 0; m < 18; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 ub[4];
+  float2 uh;
+  auto load_u = [&](int s) {
+    const int so = ubase + s * 10 * 1024;
+    if constexpr ((PSX_WF_PROBE & 1) != 0) {  // diagnostic: B from registers
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ub[i] = (f32x4){(float)so, 1.f, 2.f, (float)i};
+      uh = make_float2((float)so, 1.f);
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      ub[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ur, l * 16 + i * 1024, so, 0));
+    uh = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(ur, l * 16 + 4 * 1024, so, 0));
+  };
+  load_u(0);
+  if (h == 0) {
+    load_patch(0);
+    xform(0, 0, true);
+    load_patch(G > 1 ? 1 : 0);
+  }
+  __syncthreads();
+  // Per group g: waves 0-3 first transform group g + 1 (patch loaded during the previous group)
+  // into the other buffer and issue the patch loads of g + 2, while waves 4-7 — the other wave on
+  // each SIMD — already run their MFMAs of g; then waves 0-3 run theirs. The MFMA pipe sees 72 + 72
+  // MFMAs per SIMD and group with the transform in between hidden. The group past the last is a
+  // dummy (clamped loads, dropped V stores, its LDS image never read).
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int p = g & 1;
+    if (h == 0) {
+      xform(g + 1, p ^ 1, g + 1 < G);
+      load_patch(g + 2 < G ? g + 2 : G - 1);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int s = g * 4 + q;
+      const f32x4 a0 = vb[p][q][5 * h][l], a1 = vb[p][q][5 * h + 1][l], a2 = vb[p][q][5 * h + 2][l],
+                  a3 = vb[p][q][5 * h + 3][l];
+      const float2 a4 = *reinterpret_cast<const float2*>(&vb[p][q][5 * h + 4][l]);
+      const f32x4 u0 = ub[0], u1 = ub[1], u2 = ub[2], u3 = ub[3];
+      const float2 u4 = uh;
+      load_u(s + 1 < S4 ? s + 1 : s);  // the next k-step's B (the last re-loads itself)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        mfma_f32_16x16x4(acc[j], a0[j], u0[j]);
+        mfma_f32_16x16x4(acc[4 + j], a1[j], u1[j]);
+        mfma_f32_16x16x4(acc[8 + j], a2[j], u2[j]);
+        mfma_f32_16x16x4(acc[12 + j], a3[j], u3[j]);
+      }
+      mfma_f32_16x16x4(acc[16], a4.x, u4.x);
+      mfma_f32_16x16x4(acc[17], a4.y, u4.y);
+    }
+    __syncthreads();
+  }
+
+
+  // ---- epilogue. Lane l holds M_b[tile 4(l>>4)+i][channel l&15] for this half's points b = 18h +
+  // m (rows 3h .. 3h + 2 of the 6x6), i = 0..3. Per tile: Z = (M rows) A (row pass, 3 x 4), then
+  // this half's share of y = A^T M A: Y_h[r][j] = sum_rr A^T[r][3h + rr] Z[rr][j]. Wave h keeps
+  // tiles 2h, 2h + 1, hands the other two's partials to its partner (kq, 1 - h) through LDS
+  // (the group buffers are free) and finishes its two tiles with the partner's partials.
+  // A^T columns 3h .. 3h + 2 (rows r = 0..3): h = 0: [1 1 1; 0 1 -1; 0 1 1; 0 1 -1],
+  // h = 1: [1 1 0; 2 -2 0; 4 4 0; 8 -8 1]
+  float at[4][3];
+  {
+    const float c0[4][3] = {{1.f, 1.f, 1.f}, {0.f, 1.f, -1.f}, {0.f, 1.f, 1.f}, {0.f, 1.f, -1.f}};
+    const float c1[4][3] = {{1.f, 1.f, 0.f}, {2.f, -2.f, 0.f}, {4.f, 4.f, 0.f}, {8.f, -8.f, 1.f}};
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int rr = 0; rr < 3; ++rr) at[r][rr] = h ? c1[r][rr] : c0[r][rr];
+  }
+  float yp[4][16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float z[3][4];
+#pragma unroll
+    for (int rr = 0; rr < 3; ++rr) {
+      float row[6] = {acc[6 * rr][i], acc[6 * rr + 1][i], acc[6 * rr + 2][i],
+                      acc[6 * rr + 3][i], acc[6 * rr + 4][i], acc[6 * rr + 5][i]};
+      wino_at6(row, z[rr]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) yp[i][r * 4 + j] = at[r][0] * z[0][j] + at[r][1] * z[1][j] + at[r][2] * z[2][j];
+  }
+  // hand-off: xb[kq][h][e][lane], e = 0..31 (the partner's two tiles x 16 pixels)
+  float* xb = reinterpret_cast<float*>(&vb[0][0][0][0]);
+  float* mine = xb + ((size_t)(kq * 2 + h) * 32) * 64 + l;
+  float* theirs = xb + ((size_t)(kq * 2 + (1 - h)) * 32) * 64 + l;
+#pragma unroll
+  for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) mine[(ii * 16 + e) * 64] = h ? yp[ii][e] : yp[2 + ii][e];
+  __syncthreads();
+  float yv[2][16];
+#pragma unroll
+  for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) yv[ii][e] = (h ? yp[2 + ii][e] : yp[ii][e]) + theirs[(ii * 16 + e) * 64];
+
+  const int k = kb * kWfK + kq * 16 + (l & 15);
+  constexpr bool bwd = BWD, two = BWD && TWO;
+  float m1 = 0.f, i1 = 0.f, m2 = 0.f, i2 = 0.f, msc = 0.f, msh = 0.f;
+  if constexpr (bwd) {
+    m1 = bs.saved1[k];
+    i1 = bs.saved1[K + k];
+    if constexpr (MAFF) {
+      msc = bs.mask_aff[k];
+      msh = bs.mask_aff[K + k];
+    }
+    if constexpr (two) {
+      m2 = bs.saved2[k];
+      i2 = bs.saved2[K + k];
+    }
+  }
+  const float kshift = (!bwd && a.sshift) ? a.sshift[k] : 0.f;  // forward statistics: shifted sums
+  float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+  for (int ii = 0; ii < 2; ++ii) {
+    const int tt = tb * kWfT + 4 * (l >> 4) + 2 * h + ii;
+    const int n = tt / tpi, rem = tt - n * tpi, ti = rem / tw, tj = rem - ti * tw;
+    const size_t base = (((size_t)n * H + 4 * ti) * W + 4 * tj) * K + k;
+    float rv[16], y1v[16], ov[16], y2v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const size_t off = base + ((size_t)(e >> 2) * W + (e & 3)) * K;
+      if constexpr (RES) rv[e] = a.res[off];
+      if constexpr (bwd) {
+        y1v[e] = bs.y1[off];
+        if constexpr (!MAFF) ov[e] = bs.o[off];
+        if constexpr (two) y2v[e] = bs.y2[off];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const size_t off = base + ((size_t)(e >> 2) * W + (e & 3)) * K;
+      float v = yv[ii][e];
+      if constexpr (RES) v += rv[e];
+      if constexpr (bwd) {
+        const float y1 = y1v[e];
+        bool pos;
+        if constexpr (MAFF)
+          pos = y1 * msc + msh > 0.f;
+        else
+          pos = ov[e] > 0.f;
+        const float dz = pos ? v : 0.f;
+        s1 += dz;
+        s2 += dz * (y1 - m1) * i1;
+        if constexpr (two) s3 += dz * (y2v[e] - m2) * i2;
+        a.y[off] = bs.mask_store ? dz : v;
+      } else {
+        a.y[off] = v;
+        const float dd = v - kshift;
+        s1 += dd;
+        s2 += dd * dd;
+      }
+    }
+  }
+  float* dst = bwd ? bs.part : a.stats;
+  if (!dst) return;
+  const int nst = bwd ? (two ? 3 : 2) : 2;
+  // lanes l, l^16, l^32, l^48 hold the same channel; then the wave pair (kq, 0 / 1) through LDS
+  s1 += __shfl_xor(s1, 16, 64);
+  s1 += __shfl_xor(s1, 32, 64);
+  s2 += __shfl_xor(s2, 16, 64);
+  s2 += __shfl_xor(s2, 32, 64);
+  if constexpr (two) {
+    s3 += __shfl_xor(s3, 16, 64);
+    s3 += __shfl_xor(s3, 32, 64);
+  }
+  if (h == 1 && l < 16) {
+    red[0][kq][l] = s1;
+    red[1][kq][l] = s2;
+    red[2][kq][l] = s3;
+  }
+  __syncthreads();
+  // deterministic mode: slab row tb, each element written by exactly one lane of one workgroup
+  float* row = det.slab ? det.slab + (size_t)tb * nst * K : dst + (size_t)(tb & (PSX_STAT_SLOTS - 1)) * nst * K;
+  if (h == 0 && l < 16) {
+    atomicAdd(row + k, s1 + red[0][kq][l]);
+    atomicAdd(row + K + k, s2 + red[1][kq][l]);
+    if constexpr (two) atomicAdd(row + 2 * K + k, s3 + red[2][kq][l]);
+  }
+  if (det.slab) {
+    __syncthreads();  // vb is the hand-off scratch
+    det_finish(det, nst, K, dst, tb, reinterpret_cast<unsigned char*>(&vb[0][0][0][0]));
+  }
+}
+
+}  // namespace psx
+
+using namespace psx;
+
+extern "C" {
+
+// 1 when psx_wino_fused handles the layer: the Winograd conditions (wino.hip psx_wino_ok), whole
+// 16-tile blocks, 64-channel output blocks, 64 or 128 input channels (the fully unrolled group
+// loop is instantiated for 4 and 8 groups) and 32-bit byte offsets.
+int psx_wino_fused_ok(int N, int H, int W, int C, int K) {
+  if (H % 4 || W % 4 || (C != 64 && C != 128) || K % kWfK) return 0;  // instantiated: 4 / 8 groups
+  const long T = (long)N * (H / 4) * (W / 4);
+  return T % kWfT == 0 && (long)N * H * W * (long)(C > K ? C : K) * 4 < (1L << 31) && 40L * C * K * 4 < (1L << 31) &&
+         36L * T * C < (1L << 31);
+}
+
+// y[N][H][W][K] = conv3x3(x[N][H][W][C]) (+ res) from the layout-1 transformed weights Uf; the rest
+// as psx_wino_conv (wino.hip). V (nullable): the transformed input [36][T][C] for psx_wino_wgrad.
+int psx_wino_fused(const float* x, const float* Uf, float* y, const float* res, float* stats, float* V, int N, int H,
+                   int W, int C, int K, const WinoBwdStats* bst, const float* bnpart, const WinoBnFin* bnfin,
+                   const float* sshift, hipStream_t st) {
+  if (!psx_wino_fused_ok(N, H, W, C, K)) return -2;
+  if (bnpart && (!bnfin || bnfin->C != C)) return -3;
+  const int T = N * (H / 4) * (W / 4);
+  WinoFusedArgs a{x, Uf, y, res, bst ? nullptr : stats, V, bnpart, sshift, H, W, C, K, T, K / kWfK,
+                  (int)((long)N * H * W * C * 4), (int)(40L * C * K * 4), (int)(36L * T * C * 4)};
+  WinoBnFin bf{};
+  if (bnpart) bf = *bnfin;
+  WinoBwdStats bs{};
+  if (bst) bs = *bst;
+  const int rows = T / kWfT;
+  DetRed det{};
+  if (bst || stats) det = det_next(rows, bst ? (bst->y2 ? 3 : 2) : 2, K, K / kWfK);
+  using FK = void (*)(WinoFusedArgs, WinoBnFin, WinoBwdStats, DetRed);
+#define PSX_WF_ROW(G, R)                                                                                     \
+  {wino_fused_kernel<G, R, false, false, false>, wino_fused_kernel<G, R, true, false, false>,                 \
+   wino_fused_kernel<G, R, true, false, true>, wino_fused_kernel<G, R, true, true, false>,                    \
+   wino_fused_kernel<G, R, true, true, true>}
+  // [C / 16 == 8][res][variant]: forward, backward (ReLU mask from o / from the affine) x (one / two BN sums)
+  static const FK kF[2][2][5] = {{PSX_WF_ROW(4, false), PSX_WF_ROW(4, true)}, {PSX_WF_ROW(8, false), PSX_WF_ROW(8, true)}};
+#undef PSX_WF_ROW
+  const int var = bst ? 1 + 2 * (bs.mask_aff != nullptr) + (bs.y2 != nullptr) : 0;
+  hipLaunchKernelGGL(kF[C == 128][res != nullptr][var], dim3((unsigned)(rows * (K / kWfK))), dim3(512), 0, st, a, bf, bs, det);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -402,12 +402,18 @@ class HipResNetEngine:
         step) and, where the weight gradient is Winograd, the transformed input V [36][T][cin] the
         forward leaves for it. In deterministic mode its BN sums take the fixed-order reduction
         like every other producer (wino_out_kernel + bnfin.hpp DetRed). Not for bf16. PSX_WINO=0:
-        direct kernels everywhere."""
+        direct kernels everywhere. Layers with 64 / 128 input channels (ResNet-18's 32x32 and 16x16
+        stages) run forward and data gradient as ONE fused launch each (wino_fused.hip: the
+        transforms inside the GEMM, V / P never in HBM) with PSX_WINO_FUSE=1 (off by default until it beats
+        the three-launch path: bench/wino_fused_ab.py).
+        The fused forward still writes V where the Winograd weight gradient reads it."""
         self.wino_layers = {}
         self.wino_wgrad = set()
         self.wino_bnfold = {}
+        self.wino_fused = {}
         if not self.f32 or os.environ.get("PSX_WINO", "1") == "0":
             return
+        fuse = os.environ.get("PSX_WINO_FUSE", "0") == "1"
         maxhw = int(os.environ.get("PSX_WINO_MAXHW", "64"))
         wg = os.environ.get("PSX_WINO_WGRAD", "1") == "1"
         wg_maxhw = int(os.environ.get("PSX_WINO_WGRAD_MAXHW", "32"))
@@ -420,8 +426,12 @@ class HipResNetEngine:
             vk, vc = K.wino_v_floats(B, cs.h, cs.w, cs.cout), K.wino_v_floats(B, cs.h, cs.w, cs.cp)
             s_main = max(s_main, vk, vc)
             q = K.wino_wgrad_q(B, cs.h, cs.w, cs.cp, cs.cout) if wg and max(cs.h, cs.w) <= wg_maxhw else 0
-            uf = self._f32(36 * cs.cout * cs.cp)
-            ud = self._f32(36 * cs.cout * cs.cp) if cs.need_dgrad else None
+            # fused single-launch kernel (wino_fused.hip) where it applies, per direction
+            ff = fuse and K.wino_fused_ok(B, cs.h, cs.w, cs.cp, cs.cout)
+            fd = fuse and cs.need_dgrad and K.wino_fused_ok(B, cs.h, cs.w, cs.cout, cs.cp)
+            self.wino_fused[cs.name] = (ff, fd)
+            uf = self._f32((40 if ff else 36) * cs.cout * cs.cp)
+            ud = self._f32((40 if fd else 36) * cs.cout * cs.cp) if cs.need_dgrad else None
             v = self._f32(vc) if q > 0 else None  # None: the forward's V goes to scratch
             self.wino_layers[cs.name] = (uf, ud, v)
             if q > 0:
@@ -458,9 +468,10 @@ class HipResNetEngine:
                 if u is None:
                     continue
                 w = self._aview(arena, f"{cs.name}.weight")
-                items.append((w, u[0], cs.cout, cs.cp, False))
+                ff, fd = self.wino_fused[cs.name]
+                items.append((w, u[0], cs.cout, cs.cp, False, int(ff)))
                 if u[1] is not None:
-                    items.append((w, u[1], cs.cout, cs.cp, True))
+                    items.append((w, u[1], cs.cout, cs.cp, True, int(fd)))
             self._wino_wb = K.WinoWeightBatch(items)
             self._wino_wb_key = key
         self._wino_wb()
@@ -514,9 +525,13 @@ class HipResNetEngine:
         assert bn_in is None or wl is not None, cs.name
         sshift = self.bn[bs.name]["sshift"] if train else None
         if wl is not None:
-            v = wl[2] if wl[2] is not None else self.wino_s2
-            K.wino_conv(x, wl[0], y, None, stats, v, self.wino_s1, self.B, cs.h, cs.w, cs.cp, cs.cout, bn_in=bn_in,
-                        sshift=sshift)
+            if self.wino_fused[cs.name][0]:
+                K.wino_fused(x, wl[0], y, None, stats, wl[2], self.B, cs.h, cs.w, cs.cp, cs.cout, bn_in=bn_in,
+                             sshift=sshift)
+            else:
+                v = wl[2] if wl[2] is not None else self.wino_s2
+                K.wino_conv(x, wl[0], y, None, stats, v, self.wino_s1, self.B, cs.h, cs.w, cs.cp, cs.cout,
+                            bn_in=bn_in, sshift=sshift)
             if not train:
                 self._bn_eval(bs, arena)
             elif not self._fold:  # no in-launch finalize on this path
@@ -653,8 +668,11 @@ class HipResNetEngine:
             if ms:
                 self._premasked.add(bs.name)
         if wl is not None:  # Winograd: the output transform produces the same fused sums
-            K.wino_conv(dy, wl[1], dx, res, None, self.wino_s1, self.wino_s2, self.B, cs.h, cs.w, cs.cout, cs.cp,
-                        bst=bst)
+            if self.wino_fused[cs.name][1]:
+                K.wino_fused(dy, wl[1], dx, res, None, None, self.B, cs.h, cs.w, cs.cout, cs.cp, bst=bst)
+            else:
+                K.wino_conv(dy, wl[1], dx, res, None, self.wino_s1, self.wino_s2, self.B, cs.h, cs.w, cs.cout,
+                            cs.cp, bst=bst)
             return
         wd = self.wbuf[cs.wd_off:cs.wd_off + cs.cp * cs.kgd]
         K.conv_dgrad2(dy, wd, dx, res, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,

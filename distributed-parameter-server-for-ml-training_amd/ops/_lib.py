@@ -52,7 +52,9 @@ _KERNEL_SIGS = {
     "psx_wino_workspace": (i64, [i32, i32, i32, i32, i32]),
     "psx_wino_ok": (i32, [i32, i32, i32, i32]),
     "psx_wino_weights": (i32, [vp, vp, i32, i32, i32, vp]),
-    "psx_wino_weights_multi": (i32, [vp, vp, vp, vp, vp, i32, vp]),
+    "psx_wino_weights_multi": (i32, [vp, vp, vp, vp, vp, i32, vp, vp]),
+    "psx_wino_fused_ok": (i32, [i32, i32, i32, i32, i32]),
+    "psx_wino_fused": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp]),
     "psx_wino_conv": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp]),
     "psx_wino_v_floats": (i64, [i32, i32, i32, i32]),
     "psx_wino_wgrad_q": (i32, [i32, i32, i32, i32, i32]),

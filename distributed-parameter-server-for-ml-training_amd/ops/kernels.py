@@ -181,24 +181,49 @@ def wino_weights(w_oihw, u, k, c, flip=False):
 
 class WinoWeightBatch:
     """Every Winograd weight transform of a step as ONE launch (wino.hip psx_wino_weights_multi):
-    items = [(w_oihw, u, k, c, flip)], pointers fixed at construction (<= 40 items)."""
+    items = [(w_oihw, u, k, c, flip[, layout])], pointers fixed at construction (<= 40 items).
+    layout 1: the fused kernel's operand order (wino_fused; 40 * k * c floats)."""
 
     def __init__(self, items):
         n = len(items)
         assert 1 <= n <= 40
-        for w, u, k, c, _ in items:
-            assert w.dtype == torch.float32 and w.numel() == k * c * 9 and u.numel() >= 36 * k * c
+        for w, u, k, c, *rest in items:
+            lay = rest[1] if len(rest) > 1 else 0
+            assert w.dtype == torch.float32 and w.numel() == k * c * 9 and u.numel() >= (40 if lay else 36) * k * c
         self.n = n
-        self.keep = [(w, u) for w, u, *_ in items]
-        self.w = (C.c_void_p * n)(*[ptr(w) for w, *_ in items])
-        self.u = (C.c_void_p * n)(*[ptr(u) for _, u, *_ in items])
+        self.keep = [(it[0], it[1]) for it in items]
+        self.w = (C.c_void_p * n)(*[ptr(it[0]) for it in items])
+        self.u = (C.c_void_p * n)(*[ptr(it[1]) for it in items])
         self.k = (C.c_int * n)(*[int(it[2]) for it in items])
         self.c = (C.c_int * n)(*[int(it[3]) for it in items])
         self.flip = (C.c_int * n)(*[int(bool(it[4])) for it in items])
+        self.layout = (C.c_int * n)(*[int(it[5]) if len(it) > 5 else 0 for it in items])
 
     def __call__(self):
-        check(kernels().psx_wino_weights_multi(self.w, self.u, self.k, self.c, self.flip, self.n, stream_ptr()),
-              "wino_weights_multi")
+        check(kernels().psx_wino_weights_multi(self.w, self.u, self.k, self.c, self.flip, self.n, self.layout,
+                                               stream_ptr()), "wino_weights_multi")
+
+
+def wino_fused_ok(nb, h, w, c, k) -> bool:
+    """psx_wino_fused handles this layer (csrc/kernels/wino_fused.hip: 64 or 128 input channels,
+    output channels a multiple of 64, whole 16-tile blocks)."""
+    return bool(kernels().psx_wino_fused_ok(nb, h, w, c, k))
+
+
+def wino_fused(x, uf, y, res, stats, v, nb, h, w, c, k, bst: "BwdStatsDesc | None" = None, bn_in=None, sshift=None):
+    """wino_conv in ONE launch (csrc/kernels/wino_fused.hip: input transform, 36 GEMMs and output
+    transform fused; V / P never reach HBM). uf: the transformed weights in layout 1
+    (WinoWeightBatch item layout=1, 40 * k * c floats); v (nullable): receives the transformed input [36][T][c] for
+    wino_wgrad. The other arguments as wino_conv."""
+    assert x.dtype == torch.float32 and y.dtype == torch.float32
+    assert x.numel() == nb * h * w * c and y.numel() == nb * h * w * k and uf.numel() >= 40 * k * c
+    assert v is None or v.numel() >= wino_v_floats(nb, h, w, c)
+    assert res is None or res.numel() == y.numel()
+    check(kernels().psx_wino_fused(ptr(x), ptr(uf), ptr(y), ptr(res), ptr(stats), ptr(v), nb, h, w, c, k,
+                                   C.byref(bst) if bst is not None else None,
+                                   ptr(bn_in[0]) if bn_in is not None else None,
+                                   C.byref(bn_in[1]) if bn_in is not None else None, ptr(sshift), stream_ptr()),
+          "wino_fused")
 
 
 def wino_conv(x, u, y, res, stats, v, p, nb, h, w, c, k, cfg=None, bst: "BwdStatsDesc | None" = None, bn_in=None,

@@ -1,31 +1,36 @@
 // fp32 Winograd F(4x4,3x3) conv with both transforms fused into the GEMM: ONE launch per conv, the
 // transformed input V and the 36 GEMM outputs P never reach HBM (wino.hip runs input transform ->
 // 36 batched GEMMs -> output transform as three launches, V and P 2.25x the activation each way:
-// on the 32x32x64 layer ~300 MB of the ~370 MB a conv moves, 100 us per call).
+// on the 32x32x64 layer ~300 MB of the ~370 MB a conv moves).
 //
-// Workgroup = 16 Winograd tiles x 64 output channels, 4 waves; wave w owns output channels
-// [16w, 16w + 16) of the block and accumulates all 36 Winograd points of its 16 x 16 (tile,
-// channel) block in registers: acc[b] is one v_mfma_f32_16x16x4_f32 tile (4 floats per lane,
-// 144 accumulator registers), so lane l ends holding M_b[tile 4(l>>4)+i][channel l&15] for every b
-// and i — all 36 points of 4 (tile, channel) pairs, exactly what the output transform A^T M A of
-// those pairs needs, in the epilogue, in registers.
+// Workgroup = 16 Winograd tiles x 64 output channels, 8 waves (two per SIMD, <= 256 registers,
+// 84 KB LDS: one workgroup per CU). Wave w = (kq = w & 3, h = w >> 2) owns output channels
+// [16 kq, 16 kq + 16) of the block and Winograd points 18h .. 18h + 17 (rows 3h .. 3h + 2 of the
+// 6x6): acc[m] is one v_mfma_f32_16x16x4_f32 tile per point (72 accumulator registers), so lane l
+// ends holding M_b[tile 4(l>>4)+i][channel l&15] for its 18 points and i = 0..3. 144 per wave (all
+// 36 points, one wave per SIMD) ran the same speed: the transform and the MFMAs serialise; here
+// waves 0-3 transform while waves 4-7 multiply.
 //
-// The reduction runs over C in groups of 16 channels = 4 MFMA k-steps. Per group each wave
-// transforms ONE k-step of the block's 16 tiles (lane = (tile l&15, channel l>>4): the 6x6 patch
-// through buffer loads with clamped rows / columns, the optional folded BN + ReLU of the previous
-// layer, zero padding, B^T d B in registers) and writes its 36 values into the LDS group buffer in
-// the MFMA A-operand order (four points per ds_write_b128); after one barrier every wave runs the
-// group's 4 x 36 MFMAs reading A from LDS (ds_read_b128 = four points) and B (the transformed
-// weights, pre-laid out in the B-operand order by the weight transform, layout 1) straight from
-// L2 with buffer_load_dwordx4, prefetched one k-step ahead. The next group's patch loads are in
-// flight during the MFMAs; the group buffer is double-buffered (one barrier per group). 73.7 KB of
-// LDS and <= 256 registers: two workgroups per CU.
+// The reduction runs over C in groups of 16 channels = 4 MFMA k-steps. Per group waves 0-3
+// transform the block's 16 tiles x 16 channels (lane = (tile 4 kq + (l>>4), channel l&15): each of
+// the 36 patch loads is 4 runs of 64 contiguous bytes — one (tile, channel) per lane with 16 tiles
+// per instruction measured 87 vs 63 us on 32x32x64; clamped rows / columns through buffer loads,
+// the optional folded BN + ReLU of the previous layer, zero padding, B^T d B in registers) and
+// write the 36 values into the LDS group buffer in the MFMA A-operand order (slots of four points,
+// ds_write_b128). After one barrier per group every wave runs its 4 x 18 MFMAs, A from LDS
+// (4 ds_read_b128 + 1 ds_read_b64 per k-step), B (the transformed weights, laid out in the
+// B-operand order by the weight transform, layout 1) straight from L2 by buffer loads prefetched
+// one k-step ahead. Waves 0-3 transform group g + 1 first (patch loaded during group g - 1) while
+// waves 4-7 already multiply group g; the group buffer is double-buffered. The group loop is fully
+// unrolled (4 or 8 groups: 64 / 128 input channels), which also keeps hipcc from copying the
+// loop-carried accumulators between register files every group.
 //
-// Epilogues (same contract as wino.hip wino_out_kernel): forward (+ residual) with BN slot sums of
-// y (shifted), or data gradient with the consumer BN's backward sums (ReLU mask from o or from the
-// affine, one or two BNs) and the masked store; deterministic mode through the slab (DetRed).
-// V (nullable): the forward also stores the transformed input [36][T][C] for the Winograd weight
-// gradient (wino.hip psx_wino_wgrad), from the registers that fed LDS.
+// Epilogue: per tile the row pass Z = (M rows) A of the wave's 3 rows, its share of y = A^T M A,
+// the partner wave's share of two of the four tiles through LDS, then (same contract as wino.hip
+// wino_out_kernel) forward (+ residual) with BN slot sums of y (shifted), or data gradient with the
+// consumer BN's backward sums (ReLU mask from o or from the affine, one or two BNs) and the masked
+// store; deterministic mode through the slab (DetRed). V (nullable): the forward also stores the
+// transformed input [36][T][C] for the Winograd weight gradient (wino.hip psx_wino_wgrad).
 #include "bnfin.hpp"
 #include "common.hpp"
 #include "wino.hpp"
@@ -117,8 +122,12 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
   __syncthreads();
 
   // ---- transform role (waves 0-3, wave kq = k-step kq of a group): lane = (tile l&15, channel l>>4)
-  const int tl = l & 15, cl = l >> 4;
+  // (tiles 4 kq .. 4 kq + 3 x the group's 16 channels: a patch load is 4 runs of 64 contiguous
+  // bytes; the value for (tile tl, channel cl) goes to A-operand lane (cl & 3) * 16 + tl of k-step
+  // cl >> 2)
+  const int tl = 4 * kq + (l >> 4), cl = l & 15;
   const int t = tb * kWfT + tl;
+  const int la = (cl & 3) * 16 + tl, qa = cl >> 2;
   int rowoff[6], coloff[6];
   unsigned okr = 0, okc = 0;
   {
@@ -148,7 +157,7 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
 
   float d[36];
   auto load_patch = [&](int g) {
-    const int so = (g * 16 + 4 * kq) * 4;
+    const int so = g * 16 * 4;
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll
@@ -157,7 +166,7 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
                                           : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, rowoff[r] + coloff[s], so, 0));
   };
   auto xform = [&](int g, int p, bool real) {
-    const int ch0 = g * 16 + 4 * kq;  // wave-uniform
+    const int ch0 = g * 16;  // wave-uniform
     const float sc = aff[0][ch0 + cl], sh = aff[1][ch0 + cl];
     float e[36];
 #pragma unroll
@@ -186,12 +195,12 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int b = 18 * hh + 4 * i;
-        vb[p][kq][5 * hh + i][l] = (f32x4){e[b], e[b + 1], e[b + 2], e[b + 3]};
+        vb[p][qa][5 * hh + i][la] = (f32x4){e[b], e[b + 1], e[b + 2], e[b + 3]};
       }
-      vb[p][kq][5 * hh + 4][l] = (f32x4){e[18 * hh + 16], e[18 * hh + 17], 0.f, 0.f};
+      vb[p][qa][5 * hh + 4][la] = (f32x4){e[18 * hh + 16], e[18 * hh + 17], 0.f, 0.f};
     }
-    const auto rs = real ? vr : vnull;  // no V output: vr has zero records too
-    if constexpr ((PSX_WF_PROBE & 8) == 0)
+    const auto rs = real ? vr : vnull;
+    if ((PSX_WF_PROBE & 8) == 0 && a.V)  // the stores cost ~4 us on 32x32x64 even when dropped
 #pragma unroll
     for (int b = 0; b < 36; ++b)
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e[b]), rs, voff, (b * a.T * C + ch0) * 4, 0);

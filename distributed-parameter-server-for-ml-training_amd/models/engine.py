@@ -404,8 +404,8 @@ class HipResNetEngine:
         like every other producer (wino_out_kernel + bnfin.hpp DetRed). Not for bf16. PSX_WINO=0:
         direct kernels everywhere. Layers with 64 / 128 input channels (ResNet-18's 32x32 and 16x16
         stages) run forward and data gradient as ONE fused launch each (wino_fused.hip: the
-        transforms inside the GEMM, V / P never in HBM) with PSX_WINO_FUSE=1 (off by default until it beats
-        the three-launch path: bench/wino_fused_ab.py).
+        transforms inside the GEMM, V / P never in HBM; PSX_WINO_FUSE=0: the three-launch path;
+        bench/wino_fused_ab.py: 32x32x64 fwd / dgrad 80 / 95 -> 58 / 63 us, 16x16x128 59 / 62 -> 50 / 51).
         The fused forward still writes V where the Winograd weight gradient reads it."""
         self.wino_layers = {}
         self.wino_wgrad = set()
@@ -413,7 +413,7 @@ class HipResNetEngine:
         self.wino_fused = {}
         if not self.f32 or os.environ.get("PSX_WINO", "1") == "0":
             return
-        fuse = os.environ.get("PSX_WINO_FUSE", "0") == "1"
+        fuse = os.environ.get("PSX_WINO_FUSE", "1") == "1"
         maxhw = int(os.environ.get("PSX_WINO_MAXHW", "64"))
         wg = os.environ.get("PSX_WINO_WGRAD", "1") == "1"
         wg_maxhw = int(os.environ.get("PSX_WINO_WGRAD_MAXHW", "32"))

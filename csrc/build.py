@@ -46,6 +46,12 @@ def _run(cmd):
     return r.stdout
 
 
+# per-source extra flags. wino_fused.hip: no SLP vectorization — packed f32 VALU (v_pk_add /
+# v_pk_fma) in the transform that runs beside the other wave's MFMAs measured slower (32x32x64
+# forward 52.2 -> 50.7 us without it; MI355X_MICROARCH.md: packed f32 beside MFMAs is an anti-lever)
+FILE_FLAGS = {"wino_fused.hip": ["-fno-slp-vectorize"]}
+
+
 def build(jobs: int = 8, debug: bool = False, verbose: bool = False) -> dict:
     os.makedirs(OUT, exist_ok=True)
     os.makedirs(OBJ, exist_ok=True)
@@ -63,7 +69,7 @@ def build(jobs: int = 8, debug: bool = False, verbose: bool = False) -> dict:
     for s in k_srcs:
         o = os.path.join(OBJ, os.path.basename(s) + ".o")
         if _newer([s] + k_hdrs, o):
-            jobs_list.append([HIPCC] + hip_flags + ["-c", s, "-o", o])
+            jobs_list.append([HIPCC] + hip_flags + FILE_FLAGS.get(os.path.basename(s), []) + ["-c", s, "-o", o])
     for s in r_srcs:
         o = os.path.join(OBJ, os.path.basename(s) + ".o")
         if _newer([s] + r_hdrs, o):
@@ -123,8 +129,9 @@ def build_variant(name: str, defines: list[str], jobs: int = 8) -> str:
     os.makedirs(vobj, exist_ok=True)
     k_srcs = sorted(glob.glob(os.path.join(HERE, "kernels", "*.hip")))
     flags = [f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-O3", "-munsafe-fp-atomics", "-I",
-             os.path.join(HERE, "kernels")] + [f"-D{d}" for d in defines]
-    cmds = [[HIPCC] + flags + ["-c", s_, "-o", os.path.join(vobj, os.path.basename(s_) + ".o")] for s_ in k_srcs]
+             os.path.join(HERE, "kernels")] + [d if d.startswith("-") else f"-D{d}" for d in defines]
+    cmds = [[HIPCC] + flags + FILE_FLAGS.get(os.path.basename(s_), []) +
+            ["-c", s_, "-o", os.path.join(vobj, os.path.basename(s_) + ".o")] for s_ in k_srcs]
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         list(ex.map(_run, cmds))
     lib = os.path.join(vout, f"libpsx_kernels_{name}.so")

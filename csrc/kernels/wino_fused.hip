@@ -36,13 +36,17 @@
 #include "wino.hpp"
 
 // diagnostics (A/B builds only, wrong results): bit 1 no B loads, 2 no patch loads, 4 no transform
-// VALU, 8 no V stores
+// VALU, 8 no V stores, 16 no A reads from LDS, 32 no transform at all (VALU + LDS writes)
 #ifndef PSX_WF_PROBE
 #define PSX_WF_PROBE 0
 #endif
-// A operands read one point quad ahead of their MFMAs
-#ifndef PSX_WF_APF
-#define PSX_WF_APF 0
+// bit 1: B operands loaded two k-steps ahead (else one); bit 2: the next k-step's A operands read
+// before this k-step's MFMAs (inside a group)
+#ifndef PSX_WF_PF
+#define PSX_WF_PF 0
+#endif
+#ifndef PSX_WF_SWZ
+#define PSX_WF_SWZ 1
 #endif
 
 namespace psx {
@@ -64,7 +68,7 @@ struct WinoFusedArgs {
   const float* bnpart;
   const float* sshift;
   int H, W, C, K, T, nkb;
-  int xbytes, ubytes, vbytes;
+  int xbytes, ubytes, vbytes, ybytes;
 };
 
 template <int GG, bool RES, bool BWD, bool MAFF, bool TWO>
@@ -155,6 +159,11 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
   const auto vnull = __builtin_amdgcn_make_buffer_rsrc(a.V, 0, 0, 0x00020000);
   const int voff = (t * C + cl) * 4;
 
+  // LDS image unit of (k-step q, A-operand lane u): XOR-swizzled within the k-step's 1 KB slot
+  // block so the transform's ds_write_b128 (16 lanes of one tile = 16 channels scatter over the 4
+  // k-steps and 4 lane groups) hit 16 different bank groups instead of one; the MFMA reads stay a
+  // permutation of one contiguous 1 KB block (conflict-free)
+  auto swz = [](int q, int u) { return PSX_WF_SWZ ? (u ^ ((((u >> 4) << 2) + q) & 15)) : u; };
   float d[36];
   auto load_patch = [&](int g) {
     const int so = g * 16 * 4;
@@ -166,6 +175,7 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
                                           : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, rowoff[r] + coloff[s], so, 0));
   };
   auto xform = [&](int g, int p, bool real) {
+    if constexpr ((PSX_WF_PROBE & 32) != 0) return;
     const int ch0 = g * 16;  // wave-uniform
     const float sc = aff[0][ch0 + cl], sh = aff[1][ch0 + cl];
     float e[36];
@@ -195,9 +205,9 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int b = 18 * hh + 4 * i;
-        vb[p][qa][5 * hh + i][la] = (f32x4){e[b], e[b + 1], e[b + 2], e[b + 3]};
+        vb[p][qa][5 * hh + i][swz(qa, la)] = (f32x4){e[b], e[b + 1], e[b + 2], e[b + 3]};
       }
-      vb[p][qa][5 * hh + 4][la] = (f32x4){e[18 * hh + 16], e[18 * hh + 17], 0.f, 0.f};
+      vb[p][qa][5 * hh + 4][swz(qa, la)] = (f32x4){e[18 * hh + 16], e[18 * hh + 17], 0.f, 0.f};
     }
     const auto rs = real ? vr : vnull;
     if ((PSX_WF_PROBE & 8) == 0 && a.V)  // the stores cost ~4 us on 32x32x64 even when dropped
@@ -210,22 +220,24 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
   f32x4 acc[18];
 #pragma unroll
   for (int m = 0; m < 18; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  f32x4 ub[4];
-  float2 uh;
-  auto load_u = [&](int s) {
+  constexpr int UD = (PSX_WF_PF & 1) ? 2 : 1;  // B prefetch distance (k-steps)
+  f32x4 ub[UD][4];
+  float2 uh[UD];
+  auto load_u = [&](int s, int slot) {
     const int so = ubase + s * 10 * 1024;
     if constexpr ((PSX_WF_PROBE & 1) != 0) {  // diagnostic: B from registers
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ub[i] = (f32x4){(float)so, 1.f, 2.f, (float)i};
-      uh = make_float2((float)so, 1.f);
+      for (int i = 0; i < 4; ++i) ub[slot][i] = (f32x4){(float)so, 1.f, 2.f, (float)i};
+      uh[slot] = make_float2((float)so, 1.f);
       return;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      ub[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ur, l * 16 + i * 1024, so, 0));
-    uh = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(ur, l * 16 + 4 * 1024, so, 0));
+      ub[slot][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ur, l * 16 + i * 1024, so, 0));
+    uh[slot] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(ur, l * 16 + 4 * 1024, so, 0));
   };
-  load_u(0);
+#pragma unroll
+  for (int i = 0; i < UD; ++i) load_u(i < S4 ? i : S4 - 1, i);
   if (h == 0) {
     load_patch(0);
     xform(0, 0, true);
@@ -237,6 +249,19 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
   // each SIMD — already run their MFMAs of g; then waves 0-3 run theirs. The MFMA pipe sees 72 + 72
   // MFMAs per SIMD and group with the transform in between hidden. The group past the last is a
   // dummy (clamped loads, dropped V stores, its LDS image never read).
+  f32x4 an[4];
+  float2 ah;
+  auto load_a = [&](int p, int q) {
+    if constexpr ((PSX_WF_PROBE & 16) != 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) an[i] = (f32x4){(float)p, (float)q, (float)i, 1.f};
+      ah = make_float2((float)q, 2.f);
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) an[i] = vb[p][q][5 * h + i][swz(q, l)];
+    ah = *reinterpret_cast<const float2*>(&vb[p][q][5 * h + 4][swz(q, l)]);
+  };
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const int p = g & 1;
@@ -244,15 +269,19 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
       xform(g + 1, p ^ 1, g + 1 < G);
       load_patch(g + 2 < G ? g + 2 : G - 1);
     }
+    if constexpr ((PSX_WF_PF & 2) != 0) load_a(p, 0);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int s = g * 4 + q;
-      const f32x4 a0 = vb[p][q][5 * h][l], a1 = vb[p][q][5 * h + 1][l], a2 = vb[p][q][5 * h + 2][l],
-                  a3 = vb[p][q][5 * h + 3][l];
-      const float2 a4 = *reinterpret_cast<const float2*>(&vb[p][q][5 * h + 4][l]);
-      const f32x4 u0 = ub[0], u1 = ub[1], u2 = ub[2], u3 = ub[3];
-      const float2 u4 = uh;
-      load_u(s + 1 < S4 ? s + 1 : s);  // the next k-step's B (the last re-loads itself)
+      if constexpr ((PSX_WF_PF & 2) == 0) load_a(p, q);
+      const f32x4 a0 = an[0], a1 = an[1], a2 = an[2], a3 = an[3];
+      const float2 a4 = ah;
+      if constexpr ((PSX_WF_PF & 2) != 0)
+        if (q < 3) load_a(p, q + 1);
+      const int us = s % UD;
+      const f32x4 u0 = ub[us][0], u1 = ub[us][1], u2 = ub[us][2], u3 = ub[us][3];
+      const float2 u4 = uh[us];
+      load_u(s + UD < S4 ? s + UD : S4 - 1, us);  // UD k-steps ahead (past the end: re-loads the last)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         mfma_f32_16x16x4(acc[j], a0[j], u0[j]);
@@ -265,7 +294,6 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
     }
     __syncthreads();
   }
-
 
   // ---- epilogue. Lane l holds M_b[tile 4(l>>4)+i][channel l&15] for this half's points b = 18h +
   // m (rows 3h .. 3h + 2 of the 6x6), i = 0..3. Per tile: Z = (M rows) A (row pass, 3 x 4), then
@@ -298,20 +326,38 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
 #pragma unroll
       for (int j = 0; j < 4; ++j) yp[i][r * 4 + j] = at[r][0] * z[0][j] + at[r][1] * z[1][j] + at[r][2] * z[2][j];
   }
-  // hand-off: xb[kq][h][e][lane], e = 0..31 (the partner's two tiles x 16 pixels)
+  // hand-off: xb[kq][h][lane][36] (32 used: the partner's two tiles x 16 pixels; the 144-byte lane
+  // stride keeps the b128 accesses conflict-free), h uniform: no per-value selects
   float* xb = reinterpret_cast<float*>(&vb[0][0][0][0]);
-  float* mine = xb + ((size_t)(kq * 2 + h) * 32) * 64 + l;
-  float* theirs = xb + ((size_t)(kq * 2 + (1 - h)) * 32) * 64 + l;
-#pragma unroll
-  for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) mine[(ii * 16 + e) * 64] = h ? yp[ii][e] : yp[2 + ii][e];
-  __syncthreads();
+  float* mine = xb + ((size_t)(kq * 2 + h) * 64 + l) * 36;
+  const float* theirs = xb + ((size_t)(kq * 2 + (1 - h)) * 64 + l) * 36;
   float yv[2][16];
+  if (h) {
 #pragma unroll
-  for (int ii = 0; ii < 2; ++ii)
+    for (int e = 0; e < 32; e += 4)
+      *reinterpret_cast<f32x4*>(mine + e) =
+          (f32x4){yp[e >> 4][e & 15], yp[e >> 4][(e & 15) + 1], yp[e >> 4][(e & 15) + 2], yp[e >> 4][(e & 15) + 3]};
 #pragma unroll
-    for (int e = 0; e < 16; ++e) yv[ii][e] = (h ? yp[2 + ii][e] : yp[ii][e]) + theirs[(ii * 16 + e) * 64];
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) yv[ii][e] = yp[2 + ii][e];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 32; e += 4)
+      *reinterpret_cast<f32x4*>(mine + e) = (f32x4){yp[2 + (e >> 4)][e & 15], yp[2 + (e >> 4)][(e & 15) + 1],
+                                                    yp[2 + (e >> 4)][(e & 15) + 2], yp[2 + (e >> 4)][(e & 15) + 3]};
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) yv[ii][e] = yp[ii][e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 32; e += 4) {
+    const f32x4 t4 = *reinterpret_cast<const f32x4*>(theirs + e);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) yv[e >> 4][(e & 15) + j] += t4[j];
+  }
 
   const int k = kb * kWfK + kq * 16 + (l & 15);
   constexpr bool bwd = BWD, two = BWD && TWO;
@@ -329,26 +375,36 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
     }
   }
   const float kshift = (!bwd && a.sshift) ? a.sshift[k] : 0.f;  // forward statistics: shifted sums
+  // the output-sized tensors through buffer descriptors: 32-bit lane offsets, the pixel step in
+  // the (uniform) soffset
+  const int ybytes = a.ybytes;
+  const auto yr = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, ybytes, 0x00020000);
+  const auto rr_ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.res), 0, RES ? ybytes : 0, 0x00020000);
+  const auto y1r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bs.y1), 0, bwd ? ybytes : 0, 0x00020000);
+  const auto orr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bs.o), 0, (bwd && !MAFF) ? ybytes : 0,
+                                                     0x00020000);
+  const auto y2r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bs.y2), 0, two ? ybytes : 0, 0x00020000);
+  const bool mstore = bwd && bs.mask_store;
   float s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
   for (int ii = 0; ii < 2; ++ii) {
     const int tt = tb * kWfT + 4 * (l >> 4) + 2 * h + ii;
     const int n = tt / tpi, rem = tt - n * tpi, ti = rem / tw, tj = rem - ti * tw;
-    const size_t base = (((size_t)n * H + 4 * ti) * W + 4 * tj) * K + k;
+    const int base = ((((n * H + 4 * ti) * W + 4 * tj) * K) + k) * 4;
     float rv[16], y1v[16], ov[16], y2v[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const size_t off = base + ((size_t)(e >> 2) * W + (e & 3)) * K;
-      if constexpr (RES) rv[e] = a.res[off];
+      const int so = ((e >> 2) * W + (e & 3)) * K * 4;
+      if constexpr (RES) rv[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr_, base, so, 0));
       if constexpr (bwd) {
-        y1v[e] = bs.y1[off];
-        if constexpr (!MAFF) ov[e] = bs.o[off];
-        if constexpr (two) y2v[e] = bs.y2[off];
+        y1v[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(y1r, base, so, 0));
+        if constexpr (!MAFF) ov[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(orr, base, so, 0));
+        if constexpr (two) y2v[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(y2r, base, so, 0));
       }
     }
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const size_t off = base + ((size_t)(e >> 2) * W + (e & 3)) * K;
+      const int so = ((e >> 2) * W + (e & 3)) * K * 4;
       float v = yv[ii][e];
       if constexpr (RES) v += rv[e];
       if constexpr (bwd) {
@@ -362,9 +418,9 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
         s1 += dz;
         s2 += dz * (y1 - m1) * i1;
         if constexpr (two) s3 += dz * (y2v[e] - m2) * i2;
-        a.y[off] = bs.mask_store ? dz : v;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mstore ? dz : v), yr, base, so, 0);
       } else {
-        a.y[off] = v;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), yr, base, so, 0);
         const float dd = v - kshift;
         s1 += dd;
         s2 += dd * dd;
@@ -427,7 +483,8 @@ int psx_wino_fused(const float* x, const float* Uf, float* y, const float* res, 
   if (bnpart && (!bnfin || bnfin->C != C)) return -3;
   const int T = N * (H / 4) * (W / 4);
   WinoFusedArgs a{x, Uf, y, res, bst ? nullptr : stats, V, bnpart, sshift, H, W, C, K, T, K / kWfK,
-                  (int)((long)N * H * W * C * 4), (int)(40L * C * K * 4), (int)(36L * T * C * 4)};
+                  (int)((long)N * H * W * C * 4), (int)(40L * C * K * 4), (int)(36L * T * C * 4),
+                  (int)((long)N * H * W * K * 4)};
   WinoBnFin bf{};
   if (bnpart) bf = *bnfin;
   WinoBwdStats bs{};

@@ -146,6 +146,19 @@ __constant__ float kWinoG[6][3] = {{0.25f, 0.f, 0.f},
                                    {1.f / 24.f, -1.f / 12.f, 1.f / 6.f},
                                    {0.f, 0.f, 1.f}};
 
+// the 36 transformed weights (G g G^T) of one 3x3 kernel, rounding pinned by explicit FMAs so
+// every transform kernel produces the same bits
+PSX_DEV void wino_g36(const float (&gg)[3][3], float (&v)[36]) {
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    float gr[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) gr[q] = fmaf(kWinoG[r][0], gg[0][q], fmaf(kWinoG[r][1], gg[1][q], kWinoG[r][2] * gg[2][q]));
+#pragma unroll
+    for (int s = 0; s < 6; ++s) v[r * 6 + s] = fmaf(kWinoG[s][0], gr[0], fmaf(kWinoG[s][1], gr[1], kWinoG[s][2] * gr[2]));
+  }
+}
+
 // U[row][b][col] = (G g G^T)[b], g = w[k][c] (fwd: row k, col c) or rot180(w[k][c]) (dgrad: row
 // c, col k). One thread per (row, col) pair — every weight read once — col fastest (each of its
 // 36 stores is a coalesced 256-byte wave row), 64-thread workgroups so a 128-channel layer still
@@ -166,15 +179,10 @@ __global__ __launch_bounds__(64) void wino_w_kernel(const float* __restrict__ w,
 #pragma unroll
     for (int q = 0; q < 3; ++q) gg[p][q] = flip ? g[(2 - p) * 3 + (2 - q)] : g[p * 3 + q];
   float* dst = U + (size_t)row * 36 * cols + col;
+  float v[36];
+  wino_g36(gg, v);
 #pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    float gr[3];  // (G g)[r][q]
-#pragma unroll
-    for (int q = 0; q < 3; ++q) gr[q] = kWinoG[r][0] * gg[0][q] + kWinoG[r][1] * gg[1][q] + kWinoG[r][2] * gg[2][q];
-#pragma unroll
-    for (int s = 0; s < 6; ++s)
-      dst[(size_t)(r * 6 + s) * cols] = kWinoG[s][0] * gr[0] + kWinoG[s][1] * gr[1] + kWinoG[s][2] * gr[2];
-  }
+  for (int b = 0; b < 36; ++b) dst[(size_t)b * cols] = v[b];
 }
 
 // All layers' weight transforms of a step in one launch: descriptor j covers pairs
@@ -200,10 +208,25 @@ __global__ __launch_bounds__(64) void wino_w_multi_kernel(WinoWBatch bt) {
   while (j + 1 < bt.n && i >= bt.d[j + 1].p0) ++j;
   const WinoWDesc& d = bt.d[j];
   const int flip = d.flip, K = d.K, C = d.C;
-  const int rows = flip ? C : K, cols = flip ? K : C;
+  const int cols = flip ? K : C;
   const long li = i - d.p0;
-  const int row = (int)(li / cols), col = (int)(li - (long)row * cols);
-  (void)rows;
+  // layout 0: U[row][36][col] (the batched GEMM's operand), thread = (row, col), col fastest;
+  // 1: the fused kernel's MFMA B-operand order (wino_fused.hip): [row/16][col/4][slot 10][lane =
+  // (col%4)*16 + row%16][4], slot 5h + i (i < 4) = points 18h + 4i .. +3, slot 5h + 4 = points
+  // 18h + 16, 18h + 17 and two zeros; thread = destination lane, so each slot is one coalesced
+  // 16-byte store per thread (the (row, col) order scattered every store: 90 us per step)
+  int row, col;
+  if (d.layout) {
+    const int ln = (int)(li & 63);
+    const long blk = li >> 6;
+    const int cq = cols >> 2;
+    const int rg = (int)(blk / cq), cs = (int)(blk - (long)rg * cq);
+    row = rg * 16 + (ln & 15);
+    col = cs * 4 + (ln >> 4);
+  } else {
+    row = (int)(li / cols);
+    col = (int)(li - (long)row * cols);
+  }
   const int k = flip ? col : row, c = flip ? row : col;
   const float* g = d.w + ((size_t)k * C + c) * 9;
   float gg[3][3];
@@ -211,27 +234,23 @@ __global__ __launch_bounds__(64) void wino_w_multi_kernel(WinoWBatch bt) {
   for (int p = 0; p < 3; ++p)
 #pragma unroll
     for (int q = 0; q < 3; ++q) gg[p][q] = flip ? g[(2 - p) * 3 + (2 - q)] : g[p * 3 + q];
-  // layout 0: U[row][36][col] (the batched GEMM's operand); 1: the fused kernel's MFMA B-operand
-  // order (wino_fused.hip): [row/16][col/4][slot 10][lane = (col%4)*16 + row%16][4], slot 5h + i
-  // (i < 4) = points 18h + 4i .. +3, slot 5h + 4 = points 18h + 16, 18h + 17 and two zeros
-  float* dst = d.layout ? d.U + ((size_t)(row >> 4) * (cols >> 2) + (col >> 2)) * 2560 + ((col & 3) * 16 + (row & 15)) * 4
-                        : d.U + (size_t)row * 36 * cols + col;
+  float v[36];
+  wino_g36(gg, v);
   if (d.layout) {
-    dst[4 * 256 + 2] = dst[4 * 256 + 3] = 0.f;
-    dst[9 * 256 + 2] = dst[9 * 256 + 3] = 0.f;
-  }
+    f32x4* dst = reinterpret_cast<f32x4*>(d.U) + (li >> 6) * 640 + (li & 63);
 #pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    float gr[3];
+    for (int hb = 0; hb < 2; ++hb) {
 #pragma unroll
-    for (int q = 0; q < 3; ++q) gr[q] = kWinoG[r][0] * gg[0][q] + kWinoG[r][1] * gg[1][q] + kWinoG[r][2] * gg[2][q];
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const int b = r * 6 + s;
-      const int hb = b >= 18, m = b - 18 * hb;  // layout 1: half, local point
-      dst[d.layout ? (size_t)(5 * hb + (m >> 2)) * 256 + (m & 3) : (size_t)b * cols] =
-          kWinoG[s][0] * gr[0] + kWinoG[s][1] * gr[1] + kWinoG[s][2] * gr[2];
+      for (int q = 0; q < 4; ++q) {
+        const int b = 18 * hb + 4 * q;
+        dst[(5 * hb + q) * 64] = (f32x4){v[b], v[b + 1], v[b + 2], v[b + 3]};
+      }
+      dst[(5 * hb + 4) * 64] = (f32x4){v[18 * hb + 16], v[18 * hb + 17], 0.f, 0.f};
     }
+  } else {
+    float* dst = d.U + (size_t)row * 36 * cols + col;
+#pragma unroll
+    for (int b = 0; b < 36; ++b) dst[(size_t)b * cols] = v[b];
   }
 }
 

@@ -512,18 +512,42 @@ __global__ __launch_bounds__(384) void wino_in_xf_kernel(const float* __restrict
 }
 
 // D = A dy A^T (wino_dy_kernel, split): waves 0-3 load the 4 rows of the dy tile
+// ybn / bpart (nullable): dy is the BN backward k1 dz + k2 ybn + k3 of dz (the dy argument) —
+// the BN-backward apply folded in (wino.hpp wino_bwd_coef: the same coefficients and rounding as
+// the fused data gradient that consumes the same dy)
 __global__ __launch_bounds__(384) void wino_dy_xf_kernel(const float* __restrict__ dy, float* __restrict__ D, int T,
-                                                         int H, int W, int K) {
+                                                         int H, int W, int K, const float* __restrict__ ybn,
+                                                         const float* __restrict__ bpart, BnBwdFin bfin) {
   __shared__ float xf[2][4][6][64];
+  __shared__ float kc[3][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + lane;
   const int tw = W >> 2, tpi = (H >> 2) * tw;
   const size_t bs = (size_t)T * K;
+  float k1 = 1.f, k2 = 0.f, k3 = 0.f;
+  if (bpart) {
+    if (wv == 0) {
+      double sdz, sxh;
+      wino_bwd_coef(bpart, bfin, k, k1, k2, k3, sdz, sxh);
+      kc[0][lane] = k1;
+      kc[1][lane] = k2;
+      kc[2][lane] = k3;
+    }
+    __syncthreads();
+    k1 = kc[0][lane];
+    k2 = kc[1][lane];
+    k3 = kc[2][lane];
+  }
   auto load = [&](int t, float (&y)[4]) {
     const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
-    const float* src = dy + (((size_t)n * H + 4 * ti + wv) * W + 4 * tj) * K + k;
+    const size_t off = (((size_t)n * H + 4 * ti + wv) * W + 4 * tj) * K + k;
+    const float* src = dy + off;
 #pragma unroll
     for (int j = 0; j < 4; ++j) y[j] = src[(size_t)j * K];
+    if (bpart) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[j] = wino_bwd_apply(y[j], ybn[off + (size_t)j * K], k1, k2, k3);
+    }
   };
   int t = blockIdx.y;
   float y[4];
@@ -949,14 +973,21 @@ int psx_wino_wgrad_q(int N, int H, int W, int C, int K) {
 // Weight gradient of psx_wino_conv: V = that call's transformed input, dy [N][H][W][K]; D: 36*T*K
 // floats of scratch, part: 36*q*K*C floats (q = psx_wino_wgrad_q). out: OIHW gradient, fp16
 // (out_fp16, the wire) or fp32, times scale.
+// ybn / bpart / bbfin (nullable): dy is dz of a BN whose backward apply is folded into the dy
+// transform (wino_dy_xf_kernel); the fused data gradient of the same layer publishes that BN's
+// coefficients and dgamma / dbeta.
 int psx_wino_wgrad(const float* V, const float* dy, float* D, float* part, void* out, int out_fp16, float scale,
-                   const void* zero, int N, int H, int W, int C, int K, hipStream_t st) {
+                   const void* zero, int N, int H, int W, int C, int K, const float* ybn, const float* bpart,
+                   const BnBwdFin* bbfin, hipStream_t st) {
   const int q = psx_wino_wgrad_q(N, H, W, C, K);
   if (q < 1) return -2;
+  if (bpart && (!ybn || !bbfin || bbfin->C != K)) return -3;
   const int T = N * (H / 4) * (W / 4);
-  if (wino_xf_on())
+  BnBwdFin bb{};
+  if (bpart) bb = *bbfin;
+  if (wino_xf_on() || bpart)
     hipLaunchKernelGGL(wino_dy_xf_kernel, dim3(K / 64, wino_xf_grid(T, K / 64)), dim3(64 * kXfWaves), 0, st, dy, D, T,
-                       H, W, K);
+                       H, W, K, ybn, bpart, bb);
   else
     hipLaunchKernelGGL(wino_dy_kernel, dim3(K / 64, wino_tile_grid(T)), dim3(256), 0, st, dy, D, T, H, W, K);
   const int bt = wino_wtile(C, K);

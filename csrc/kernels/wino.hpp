@@ -61,4 +61,30 @@ struct WinoBwdStats {
   const float* mask_aff;  // nullable: ReLU mask = [y1 * scale + shift > 0] (affine [2][K]) instead of o
 };
 
+
+// BN-backward fold into a consumer's operand loads (wino_fused.hip data gradient, wino.hip dy
+// transform): the coefficients of channel c from the consumer-producing dgrad's slot rows
+// part[PSX_STAT_SLOTS][2][C] (row 0 sum dz, row 1 sum dz*xhat; fixed slot order, double), as
+// bnfin.hpp bn_bwd_fin_lds: dx = k1 dz + k2 y + k3. Both consumers call this, so they read the
+// same bits.
+PSX_DEV void wino_bwd_coef(const float* part, const BnBwdFin& f, int c, float& k1, float& k2, float& k3, double& sdz,
+                           double& sxh) {
+  const int C = f.C;
+  sdz = 0.0;
+  sxh = 0.0;
+#pragma unroll
+  for (int q = 0; q < PSX_STAT_SLOTS; ++q) {
+    sdz += part[(size_t)q * 2 * C + c];
+    sxh += part[(size_t)q * 2 * C + C + c];
+  }
+  const float mdz = (float)(sdz / f.count), mxh = (float)(sxh / f.count);
+  const float is = f.invstd[c], gm = f.gamma[c];
+  k1 = gm * is;
+  k2 = -gm * is * is * mxh;
+  k3 = -gm * is * mdz + gm * is * is * f.mean[c] * mxh;
+}
+
+// the folded operand: dx = k1 dz + k2 y + k3 (one rounding order for every consumer)
+PSX_DEV float wino_bwd_apply(float dz, float y, float k1, float k2, float k3) { return fmaf(k1, dz, fmaf(k2, y, k3)); }
+
 }  // namespace psx

@@ -67,17 +67,19 @@ struct WinoFusedArgs {
   float* V;  // nullable: [36][T][C]
   const float* bnpart;
   const float* sshift;
+  const float* ybn;    // BN-backward fold (data gradient): the BN's forward input y (nullable)
+  const float* bpart;  // its backward slot sums [PSX_STAT_SLOTS][2][C]
   int H, W, C, K, T, nkb;
   int xbytes, ubytes, vbytes, ybytes;
 };
 
 template <int GG, bool RES, bool BWD, bool MAFF, bool TWO>
 __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, WinoBnFin fin, WinoBwdStats bs,
-                                                            DetRed det) {
+                                                            DetRed det, BnBwdFin bfin) {
   // [buffer][k-step][slot][lane]: slot 5h + i (i < 4) = points 18h + 4i .. +3, slot 5h + 4 = points
   // 18h + 16, 18h + 17 (+ 2 unused floats)
   __shared__ f32x4 vb[2][4][10][64];
-  __shared__ float aff[2][256];
+  __shared__ float aff[3][256];
   __shared__ float red[3][4][16];
   const int l = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -87,10 +89,35 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
   const int H = a.H, W = a.W, C = a.C, K = a.K;
   const int tw = W >> 2, tpi = (H >> 2) * tw;
   const bool bnin = a.bnpart != nullptr;
+  // BN-backward fold (data gradient whose input dy = BNbwd(dz, y) was never written): x is dz,
+  // the operand is k1 dz + k2 y + k3 with the coefficients finalized here from the slot sums
+  const bool bwdin = a.bpart != nullptr;
   // the transform applies max(x * aff0 + aff1, lo) unconditionally (one branch-free group body):
   // identity (1, 0, -inf) without a folded BN
   const float lo = bnin ? 0.f : -__builtin_inff();
-  if (!bnin) {
+  if (bwdin) {
+    for (int c = threadIdx.x; c < C; c += 512) {
+      float k1, k2, k3;
+      double sdz, sxh;
+      wino_bwd_coef(a.bpart, bfin, c, k1, k2, k3, sdz, sxh);
+      aff[0][c] = k1;
+      aff[1][c] = k3;
+      aff[2][c] = k2;
+      if (id == 0) {  // one workgroup publishes the coefficients and dgamma / dbeta (the wire)
+        bfin.coef[c] = k1;
+        bfin.coef[C + c] = k2;
+        bfin.coef[2 * C + c] = k3;
+        const float dg = (float)sxh * bfin.gscale, db = (float)sdz * bfin.gscale;
+        if (bfin.grad_fp16) {
+          reinterpret_cast<uint16_t*>(bfin.dgamma)[c] = __builtin_bit_cast(uint16_t, (_Float16)dg);
+          reinterpret_cast<uint16_t*>(bfin.dbeta)[c] = __builtin_bit_cast(uint16_t, (_Float16)db);
+        } else {
+          reinterpret_cast<float*>(bfin.dgamma)[c] = dg;
+          reinterpret_cast<float*>(bfin.dbeta)[c] = db;
+        }
+      }
+    }
+  } else if (!bnin) {
     for (int c = threadIdx.x; c < C; c += 512) {
       aff[0][c] = 1.f;
       aff[1][c] = 0.f;
@@ -148,6 +175,7 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
     }
   }
   const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x), 0, a.xbytes, 0x00020000);
+  const auto ybr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.ybn), 0, bwdin ? a.xbytes : 0, 0x00020000);
   const auto ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U), 0, a.ubytes, 0x00020000);
   const int S4 = C >> 2;  // MFMA k-steps
   // B operand of wave (kq, h): k-step s at ubase + s * 10 KB, its slots 5h .. 5h + 4
@@ -164,7 +192,7 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
   // k-steps and 4 lane groups) hit 16 different bank groups instead of one; the MFMA reads stay a
   // permutation of one contiguous 1 KB block (conflict-free)
   auto swz = [](int q, int u) { return PSX_WF_SWZ ? (u ^ ((((u >> 4) << 2) + q) & 15)) : u; };
-  float d[36];
+  float d[36], yb[36];
   auto load_patch = [&](int g) {
     const int so = g * 16 * 4;
 #pragma unroll
@@ -173,17 +201,31 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
       for (int s = 0; s < 6; ++s)
         d[r * 6 + s] = (PSX_WF_PROBE & 2) ? (float)(rowoff[r] + coloff[s] + so)
                                           : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, rowoff[r] + coloff[s], so, 0));
+    if (bwdin) {
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int s = 0; s < 6; ++s)
+          yb[r * 6 + s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ybr, rowoff[r] + coloff[s], so, 0));
+    }
   };
   auto xform = [&](int g, int p, bool real) {
     if constexpr ((PSX_WF_PROBE & 32) != 0) return;
     const int ch0 = g * 16;  // wave-uniform
     const float sc = aff[0][ch0 + cl], sh = aff[1][ch0 + cl];
     float e[36];
+    if (bwdin) {  // dy = k1 dz + k2 y + k3 (k2 in aff[2]), padding stays zero
+      const float k2 = aff[2][ch0 + cl];
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int s = 0; s < 6; ++s) d[r * 6 + s] = wino_bwd_apply(d[r * 6 + s], yb[r * 6 + s], sc, k2, sh);
+    }
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll
       for (int s = 0; s < 6; ++s) {
-        const float v = fmaxf(d[r * 6 + s] * sc + sh, lo);
+        const float v = bwdin ? d[r * 6 + s] : fmaxf(d[r * 6 + s] * sc + sh, lo);
         e[r * 6 + s] = ((okr >> r) & (okc >> s) & 1u) ? v : 0.f;  // zero padding stays zero after BN + ReLU
       }
 #pragma unroll
@@ -476,13 +518,19 @@ int psx_wino_fused_ok(int N, int H, int W, int C, int K) {
 
 // y[N][H][W][K] = conv3x3(x[N][H][W][C]) (+ res) from the layout-1 transformed weights Uf; the rest
 // as psx_wino_conv (wino.hip). V (nullable): the transformed input [36][T][C] for psx_wino_wgrad.
+// ybn / bpart / bbfin (nullable, data gradient): x is dz and the operand is the BN backward
+// k1 dz + k2 ybn + k3 of the BN whose backward sums are bpart (the BN-backward apply folded in;
+// the launch publishes the coefficients and dgamma / dbeta, bnfin.hpp BnBwdFin).
 int psx_wino_fused(const float* x, const float* Uf, float* y, const float* res, float* stats, float* V, int N, int H,
                    int W, int C, int K, const WinoBwdStats* bst, const float* bnpart, const WinoBnFin* bnfin,
-                   const float* sshift, hipStream_t st) {
+                   const float* sshift, const float* ybn, const float* bpart, const BnBwdFin* bbfin,
+                   hipStream_t st) {
   if (!psx_wino_fused_ok(N, H, W, C, K)) return -2;
   if (bnpart && (!bnfin || bnfin->C != C)) return -3;
+  if (bpart && (!bbfin || bbfin->C != C || !ybn || bnpart)) return -3;
   const int T = N * (H / 4) * (W / 4);
-  WinoFusedArgs a{x, Uf, y, res, bst ? nullptr : stats, V, bnpart, sshift, H, W, C, K, T, K / kWfK,
+  WinoFusedArgs a{x, Uf, y, res, bst ? nullptr : stats, V, bnpart, sshift, bpart ? ybn : nullptr, bpart, H, W, C, K, T,
+                  K / kWfK,
                   (int)((long)N * H * W * C * 4), (int)(40L * C * K * 4), (int)(36L * T * C * 4),
                   (int)((long)N * H * W * K * 4)};
   WinoBnFin bf{};
@@ -492,7 +540,9 @@ int psx_wino_fused(const float* x, const float* Uf, float* y, const float* res, 
   const int rows = T / kWfT;
   DetRed det{};
   if (bst || stats) det = det_next(rows, bst ? (bst->y2 ? 3 : 2) : 2, K, K / kWfK);
-  using FK = void (*)(WinoFusedArgs, WinoBnFin, WinoBwdStats, DetRed);
+  using FK = void (*)(WinoFusedArgs, WinoBnFin, WinoBwdStats, DetRed, BnBwdFin);
+  BnBwdFin bb{};
+  if (bpart) bb = *bbfin;
 #define PSX_WF_ROW(G, R)                                                                                     \
   {wino_fused_kernel<G, R, false, false, false>, wino_fused_kernel<G, R, true, false, false>,                 \
    wino_fused_kernel<G, R, true, false, true>, wino_fused_kernel<G, R, true, true, false>,                    \
@@ -501,7 +551,7 @@ int psx_wino_fused(const float* x, const float* Uf, float* y, const float* res, 
   static const FK kF[2][2][5] = {{PSX_WF_ROW(4, false), PSX_WF_ROW(4, true)}, {PSX_WF_ROW(8, false), PSX_WF_ROW(8, true)}};
 #undef PSX_WF_ROW
   const int var = bst ? 1 + 2 * (bs.mask_aff != nullptr) + (bs.y2 != nullptr) : 0;
-  hipLaunchKernelGGL(kF[C == 128][res != nullptr][var], dim3((unsigned)(rows * (K / kWfK))), dim3(512), 0, st, a, bf, bs, det);
+  hipLaunchKernelGGL(kF[C == 128][res != nullptr][var], dim3((unsigned)(rows * (K / kWfK))), dim3(512), 0, st, a, bf, bs, det, bb);
   return (int)hipGetLastError();
 }
 

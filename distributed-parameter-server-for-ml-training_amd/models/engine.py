@@ -204,6 +204,9 @@ class HipResNetEngine:
         # without o (one activation read less per BN layer) and dz doubles as the identity
         # shortcut's gradient (no dzout copy). PSX_MASK_STORE=0: off
         self.mask_store = self.fuse_bnbwd and os.environ.get("PSX_MASK_STORE", "1") == "1"
+        # BN-backward applies folded into the fused Winograd data gradient + dy transform (_bn_bwd_to)
+        self.bwd_fold = self.mask_store and os.environ.get("PSX_WINO_BWDFOLD", "1") == "1"
+        self._bwd_fold = {}
         self._premasked = set()
         # weight gradients (+ their batched reductions) on a side stream, a parallel branch of the
         # captured step graph next to the dgrad -> BN-backward chain: 1.837/1.841 vs 1.853/1.858
@@ -640,24 +643,27 @@ class HipResNetEngine:
         return need
 
     def _wgrad(self, cs: ConvSpec, x, dy):
+        fold = self._bwd_fold.get(cs.name)
         if self._wg_batch is not None:  # deferred: issued together at the end of the unit
-            self._wg_batch.append((cs, x, dy))
+            self._wg_batch.append((cs, x, dy, fold))
             return
         with self._side():
-            self._wgrad_now(cs, x, dy)
+            self._wgrad_now(cs, x, dy, fold)
 
     def _flush_wgrads(self):
         batch, self._wg_batch = self._wg_batch, None
         if batch:
             with self._side():
-                for cs, x, dy in batch:
-                    self._wgrad_now(cs, x, dy)
+                for cs, x, dy, fold in batch:
+                    self._wgrad_now(cs, x, dy, fold)
 
-    def _wgrad_now(self, cs: ConvSpec, x, dy):
+    def _wgrad_now(self, cs: ConvSpec, x, dy, fold=None):
         if cs.name in self.wino_wgrad:  # straight into the wire: no split partials to reduce
             K.wino_wgrad(self.wino_layers[cs.name][2], dy, self.wino_wd, self.wino_wpart,
-                         self.layout.grad_view(self.grads, f"{cs.name}.weight"), self.B, cs.h, cs.w, cs.cp, cs.cout)
+                         self.layout.grad_view(self.grads, f"{cs.name}.weight"), self.B, cs.h, cs.w, cs.cp, cs.cout,
+                         bwd_in=fold)
             return
+        assert fold is None, cs.name
         part = self.wpart_w[cs.wp_off:cs.wp_off + cs.wp]
         K.conv_wgrad2(x, dy, part, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad, cs.kg)
         item = (part, cs.splits, cs.cout, cs.kg, cs.cin, cs.cp, cs.k, self._gptr(f"{cs.name}.weight"))
@@ -697,7 +703,8 @@ class HipResNetEngine:
                 self._premasked.add(bs.name)
         if wl is not None:  # Winograd: the output transform produces the same fused sums
             if self.wino_fused[cs.name][1]:
-                K.wino_fused(dy, wl[1], dx, res, None, None, self.B, cs.h, cs.w, cs.cout, cs.cp, bst=bst)
+                K.wino_fused(dy, wl[1], dx, res, None, None, self.B, cs.h, cs.w, cs.cout, cs.cp, bst=bst,
+                             bwd_in=self._bwd_fold.get(cs.name))
             else:
                 K.wino_conv(dy, wl[1], dx, res, None, self.wino_s1, self.wino_s2, self.B, cs.h, cs.w, cs.cout,
                             cs.cp, bst=bst)
@@ -705,6 +712,24 @@ class HipResNetEngine:
         wd = self.wbuf[cs.wd_off:cs.wd_off + cs.cp * cs.kgd]
         K.conv_dgrad2(dy, wd, dx, res, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
                       cs.kgd, bst=bst)
+
+    def _bn_bwd_to(self, cs: ConvSpec, bs: BNSpec, arena, g, o, y, dx, npix, dzout=None):
+        """The backward of BN bs whose output gradient feeds only conv cs's data and weight
+        gradients. Returns (dz, dy): dz as _bn_bwd returns it, dy the buffer cs's gradients read.
+        Folded (PSX_WINO_BWDFOLD=1, default: cs has the fused Winograd data gradient and a Winograd
+        weight gradient, g is already the masked dz and its sums came from the producing dgrad's
+        epilogue): no apply pass — dy = k1 dz + k2 y + k3 is formed inside both consumers'
+        operand loads (wino_fused.hip, wino.hip dy transform), and the fused data gradient
+        publishes the coefficients and dgamma / dbeta."""
+        ok = (self.bwd_fold and self._fold and bs.name in self._premasked and bs.name in self._prereduced
+              and cs.name in self.wino_wgrad and self.wino_fused.get(cs.name, (False, False))[1])
+        if not ok:
+            dz = self._bn_bwd(bs, arena, g, o, y, dx, npix, dzout=dzout)
+            return dz, dx
+        self._premasked.discard(bs.name)
+        self._prereduced.discard(bs.name)
+        self._bwd_fold[cs.name] = (y, self._red(bs, "bwd"), self._fin_bwd(bs, arena, npix))
+        return g, g
 
     def _bn_bwd(self, bs: BNSpec, arena, g, o, y, dx, npix, two=None, dzout=None):
         """BN (+ReLU mask from o) backward; two = (bs2, y2, dx2) for a shared-dz second BN.
@@ -864,6 +889,7 @@ class HipResNetEngine:
             self._prereduced.add(last.name)
 
     def _bwd_fc(self, arena):
+        self._bwd_fold = {}  # the first backward unit: this step's folds are recorded afresh
         sp = self.spec
         with self._side():
             K.head_wgrad(self.dlogits, self.pooled, self.B, sp.classes, sp.fc_in, self._gptr(f"{sp.fc}.weight"),
@@ -890,26 +916,28 @@ class HipResNetEngine:
         last = b.convs[-1]
         oh, ow = last.out_hw
         npix = B * oh * ow
+        dys = list(d["dy"])  # the buffers each conv's gradients read (dz where a BN apply is folded)
         if b.down:
             ds, dbn = b.down
             self._bn_bwd(b.bns[-1], arena, g, d["out"], d["y"][-1], d["dy"][-1], npix, two=(dbn, d["ys"], d["dys"]))
         else:
-            dz = self._bn_bwd(b.bns[-1], arena, g, d["out"], d["y"][-1], d["dy"][-1], npix, dzout=d["dz"])
+            dz, dys[-1] = self._bn_bwd_to(b.convs[-1], b.bns[-1], arena, g, d["out"], d["y"][-1], d["dy"][-1], npix,
+                                          dzout=d["dz"])
         for i in range(L - 1, -1, -1):
             cs = b.convs[i]
             x_in = d["inp"] if i == 0 else d["a"][i - 1]
-            self._wgrad(cs, x_in, d["dy"][i])
+            self._wgrad(cs, x_in, dys[i])
             if i > 0:
-                self._dgrad(cs, d["dy"][i], d["da"][i - 1], bn_next=(b.bns[i - 1], d["a"][i - 1], d["y"][i - 1], None))
-                self._bn_bwd(b.bns[i - 1], arena, d["da"][i - 1], d["a"][i - 1], d["y"][i - 1], d["dy"][i - 1],
-                             B * cs.h * cs.w)
+                self._dgrad(cs, dys[i], d["da"][i - 1], bn_next=(b.bns[i - 1], d["a"][i - 1], d["y"][i - 1], None))
+                _, dys[i - 1] = self._bn_bwd_to(b.convs[i - 1], b.bns[i - 1], arena, d["da"][i - 1], d["a"][i - 1],
+                                                d["y"][i - 1], d["dy"][i - 1], B * cs.h * cs.w)
             elif b.down:
                 ds, dbn = b.down
                 self._wgrad(ds, d["inp"], d["dys"])
                 self._dgrad(ds, d["dys"], d["dxs"])
-                self._dgrad(cs, d["dy"][0], d["gin"], res=d["dxs"], bn_next=self._bn_into(j))
+                self._dgrad(cs, dys[0], d["gin"], res=d["dxs"], bn_next=self._bn_into(j))
             else:
-                self._dgrad(cs, d["dy"][0], d["gin"], res=dz, bn_next=self._bn_into(j))
+                self._dgrad(cs, dys[0], d["gin"], res=dz, bn_next=self._bn_into(j))
 
     def _bn_into(self, j: int):
         """The BN whose backward consumes block j's input gradient: the previous block's output

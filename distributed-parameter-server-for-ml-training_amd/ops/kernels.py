@@ -210,11 +210,15 @@ def wino_fused_ok(nb, h, w, c, k) -> bool:
     return bool(kernels().psx_wino_fused_ok(nb, h, w, c, k))
 
 
-def wino_fused(x, uf, y, res, stats, v, nb, h, w, c, k, bst: "BwdStatsDesc | None" = None, bn_in=None, sshift=None):
+def wino_fused(x, uf, y, res, stats, v, nb, h, w, c, k, bst: "BwdStatsDesc | None" = None, bn_in=None, sshift=None,
+               bwd_in=None):
     """wino_conv in ONE launch (csrc/kernels/wino_fused.hip: input transform, 36 GEMMs and output
     transform fused; V / P never reach HBM). uf: the transformed weights in layout 1
     (WinoWeightBatch item layout=1, 40 * k * c floats); v (nullable): receives the transformed input [36][T][c] for
-    wino_wgrad. The other arguments as wino_conv."""
+    wino_wgrad. The other arguments as wino_conv. bwd_in = (y, part, BnBwdFin) (data gradient):
+    x is dz of a BN whose backward apply is folded into the operand loads, dy = k1 dz + k2 y + k3
+    from the slot sums ``part`` [STAT_SLOTS][2][c]; the launch writes the BnBwdFin's coefficients
+    and dgamma / dbeta."""
     assert x.dtype == torch.float32 and y.dtype == torch.float32
     assert x.numel() == nb * h * w * c and y.numel() == nb * h * w * k and uf.numel() >= 40 * k * c
     assert v is None or v.numel() >= wino_v_floats(nb, h, w, c)
@@ -222,7 +226,10 @@ def wino_fused(x, uf, y, res, stats, v, nb, h, w, c, k, bst: "BwdStatsDesc | Non
     check(kernels().psx_wino_fused(ptr(x), ptr(uf), ptr(y), ptr(res), ptr(stats), ptr(v), nb, h, w, c, k,
                                    C.byref(bst) if bst is not None else None,
                                    ptr(bn_in[0]) if bn_in is not None else None,
-                                   C.byref(bn_in[1]) if bn_in is not None else None, ptr(sshift), stream_ptr()),
+                                   C.byref(bn_in[1]) if bn_in is not None else None, ptr(sshift),
+                                   ptr(bwd_in[0]) if bwd_in is not None else None,
+                                   ptr(bwd_in[1]) if bwd_in is not None else None,
+                                   C.byref(bwd_in[2]) if bwd_in is not None else None, stream_ptr()),
           "wino_fused")
 
 
@@ -247,16 +254,21 @@ def wino_conv(x, u, y, res, stats, v, p, nb, h, w, c, k, cfg=None, bst: "BwdStat
           "wino_conv")
 
 
-def wino_wgrad(v, dy, d, part, out, nb, h, w, c, k, scale=1.0):
+def wino_wgrad(v, dy, d, part, out, nb, h, w, c, k, scale=1.0, bwd_in=None):
     """Weight gradient of a wino_conv layer from its transformed input v and dy [nb][h][w][k]:
     out (OIHW, fp16 wire or fp32) = scale * dW. d: >= wino_v_floats(k) scratch, part:
-    36 * q * k * c floats (q = wino_wgrad_q)."""
+    36 * q * k * c floats (q = wino_wgrad_q). bwd_in = (y, part, BnBwdFin): dy is dz of a BN whose
+    backward apply is folded into the dy transform (as wino_fused's bwd_in; this launch writes
+    nothing of the BnBwdFin)."""
     q = wino_wgrad_q(nb, h, w, c, k)
     assert q > 0 and dy.dtype == torch.float32 and dy.numel() == nb * h * w * k
     assert d.numel() >= wino_v_floats(nb, h, w, k) and part.numel() >= 36 * q * k * c
     assert out.dtype in (torch.float16, torch.float32) and out.numel() >= k * c * 9
     check(kernels().psx_wino_wgrad(ptr(v), ptr(dy), ptr(d), ptr(part), ptr(out), int(out.dtype == torch.float16),
-                                   float(scale), ptr(zero_page(dy.device)), nb, h, w, c, k, stream_ptr()), "wino_wgrad")
+                                   float(scale), ptr(zero_page(dy.device)), nb, h, w, c, k,
+                                   ptr(bwd_in[0]) if bwd_in is not None else None,
+                                   ptr(bwd_in[1]) if bwd_in is not None else None,
+                                   C.byref(bwd_in[2]) if bwd_in is not None else None, stream_ptr()), "wino_wgrad")
 
 
 def conv_wgrad2_splits(nb, h, w, ic, oc, k, stride, pad, kg, f32=False) -> int:

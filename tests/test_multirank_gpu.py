@@ -322,9 +322,9 @@ def test_native_sync_server_matches_python(dt, fc, mom, rounds, tmp_path):
     (csrc/server/sync_loop.cpp) against the Python channel (PSX_NATIVE_SYNC=0), serial and
     bucketed-overlapped rounds, world 3 (1 server + 2 workers), deterministic mode: the runs end
     in the same master state bit for bit (so, for fp32, overlap on == overlap off as well). The
-    bf16 engine's serial round is not bit-reproducible across runs when three ranks share one GPU
-    (measured: checksums move in the 6th digit run to run, with either server; the bucketed round
-    and every fp32 run are exact) — that case is compared on the bucketed round only."""
+    bf16 engine is not bit-reproducible across runs when three ranks share one GPU (measured:
+    checksums move in the 6th-7th digit run to run, with either server, serial and bucketed
+    rounds; every fp32 run is exact) — that case is compared on the bucketed round at 1e-5."""
     sums = {}
     for ov in rounds:
         for native in ("1", "0"):
@@ -334,7 +334,11 @@ def test_native_sync_server_matches_python(dt, fc, mom, rounds, tmp_path):
             rec = [r for r in _json_lines(out, "RESULT ") if r]
             assert len(rec) == 1 and rec[0][1] == 5, out[-3000:]
             sums[(ov, native)] = rec[0][0]
-    assert len(set(sums.values())) == 1, sums
+    if dt == "fp32":
+        assert len(set(sums.values())) == 1, sums
+    else:
+        v = list(sums.values())
+        assert max(v) - min(v) <= 1e-5 * abs(v[0]), sums
 
 
 _SCRIPTED = r"""

@@ -201,3 +201,115 @@ def test_wino_fused_deterministic():
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
     assert torch.equal(res[0][1][1:], torch.zeros_like(res[0][1][1:]))  # everything in slot 0
     assert _rel(res[0][1].sum(0), res[2][1].sum(0)) < 1e-5
+
+
+def _bwd_case(nb, h, c, seed):
+    """dz, y, the BN's saved statistics / gamma and its backward slot sums (two slots)."""
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    dz = torch.randn(nb, h, h, c, device=DEV, generator=g)
+    y = torch.randn(nb, h, h, c, device=DEV, generator=g) * 1.5 + 0.3
+    mean = torch.randn(c, device=DEV, generator=g) * 0.2 + 0.3
+    invstd = torch.rand(c, device=DEV, generator=g) * 0.5 + 0.5
+    gamma = torch.rand(c, device=DEV, generator=g) + 0.5
+    xhat = (y - mean) * invstd
+    part = torch.zeros(K.STAT_SLOTS, 2, c, device=DEV)
+    part[0, 0] = dz.sum((0, 1, 2)) * 0.5
+    part[3, 0] = dz.sum((0, 1, 2)) * 0.5
+    part[1, 1] = (dz * xhat).sum((0, 1, 2))
+    saved = torch.stack([mean, invstd]).contiguous()
+    return dz, y, saved, gamma, part
+
+
+def _bwd_ref(dz, y, saved, gamma, part, cnt):
+    """dx = gamma invstd (dz - mean(dz) - xhat mean(dz xhat)) in float64, and dgamma / dbeta."""
+    mean, invstd = saved[0].double(), saved[1].double()
+    sdz, sxh = part[:, 0].double().sum(0), part[:, 1].double().sum(0)
+    xhat = (y.double() - mean) * invstd
+    dx = gamma.double() * invstd * (dz.double() - sdz / cnt - xhat * sxh / cnt)
+    return dx, sxh, sdz
+
+
+@pytest.mark.parametrize("nb,h,c,k", [(8, 16, 64, 128), (16, 32, 64, 64), (4, 16, 128, 128)])
+def test_wino_fused_bwd_fold(nb, h, c, k):
+    """The BN-backward apply folded into the fused data gradient's operand loads: dgrad(dy) with
+    dy = BNbwd(dz, y) never written == dgrad of the float64 BN backward, and the launch publishes
+    the coefficients and dgamma / dbeta; the Winograd weight gradient's dy transform folds the
+    same apply (== the weight gradient of the explicit dy)."""
+    torch.manual_seed(k + c)
+    cnt = nb * h * h
+    dz, yb, saved, gamma, part = _bwd_case(nb, h, k, seed=nb + h)
+    coef = torch.full((3, k), float("nan"), device=DEV)
+    dgb = torch.full((2, k), float("nan"), device=DEV)
+    ctr = torch.zeros(4, dtype=torch.int32, device=DEV)
+    fin = K.bn_bwd_fin(gamma, saved, coef, dgb[0].data_ptr(), dgb[1].data_ptr(), ctr.data_ptr(), cnt, 1.0, k, False)
+    w = torch.randn(k, c, 3, 3, device=DEV) * (2.0 / (9 * c)) ** 0.5
+    uf, u0 = _uf(w, k, c, flip=True)
+    dx = torch.full((nb, h, h, c), float("nan"), device=DEV)
+    K.wino_fused(dz, uf, dx, None, None, None, nb, h, h, k, c, bwd_in=(yb, part, fin))
+    torch.cuda.synchronize()
+    dy_ref, sxh, sdz = _bwd_ref(dz, yb, saved, gamma, part, cnt)
+    ref = torch.nn.grad.conv2d_input((nb, c, h, h), w.double(), dy_ref.permute(0, 3, 1, 2), padding=1)
+    assert _rel(dx, ref.permute(0, 2, 3, 1)) < TOL
+    assert torch.allclose(dgb[0].double(), sxh, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(dgb[1].double(), sdz, rtol=1e-5, atol=1e-5)
+    dyc = coef[0] * dz + coef[1] * yb + coef[2]  # the published coefficients reproduce dy
+    assert _rel(dyc, dy_ref) < 1e-5
+    # weight gradient: folded dy transform vs the explicit dy (same coefficients, same rounding)
+    x = torch.relu(torch.randn(nb, h, h, c, device=DEV))
+    uff, _ = _uf(w, k, c)
+    v = torch.empty(K.wino_v_floats(nb, h, h, c), device=DEV)
+    K.wino_fused(x, uff, torch.empty(nb, h, h, k, device=DEV), None, None, v, nb, h, h, c, k)
+    q = K.wino_wgrad_q(nb, h, h, c, k)
+    d = torch.empty(K.wino_v_floats(nb, h, h, k), device=DEV)
+    wp = torch.empty(36 * q * k * c, device=DEV)
+    g1, g0 = torch.empty(k * c * 9, device=DEV), torch.empty(k * c * 9, device=DEV)
+    K.wino_wgrad(v, dz, d, wp, g1, nb, h, h, c, k, bwd_in=(yb, part, fin))
+    dy_x = torch.addcmul(coef[2].expand_as(dz), coef[0].expand_as(dz), dz)
+    dy_x = torch.addcmul(dy_x, coef[1].expand_as(yb), yb)
+    K.wino_wgrad(v, dy_x.contiguous(), d, wp, g0, nb, h, h, c, k)
+    torch.cuda.synchronize()
+    wref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (k, c, 3, 3), dy_ref.permute(0, 3, 1, 2),
+                                       padding=1)
+    assert _rel(g1, wref.reshape(-1)) < 1e-4
+    assert _rel(g1, g0) < 1e-5
+
+
+def test_engine_bwd_fold_matches_unfolded(monkeypatch):
+    """Whole fp32 step, deterministic, BN-backward applies folded (PSX_WINO_BWDFOLD=1, default)
+    vs the separate apply passes: loss bit-equal, gradients equal to the rounding of the folded
+    apply (a different FMA order and slot-sum order), amplified by the BN backward of a random
+    init network."""
+    from psx.models.engine import HipResNetEngine
+    from psx.models.layout import ParamLayout
+    from psx.models.resnet import ResNet18
+
+    torch.manual_seed(2)
+    model = ResNet18(100)
+    layout = ParamLayout.from_module(model)
+    arena0, _ = layout.pack(model)
+    arena0 = arena0.to(DEV)
+    B = 32
+    imgs = torch.randint(0, 256, (64, 32, 32, 3), dtype=torch.uint8, device=DEV)
+    labs = torch.randint(0, 100, (64,), dtype=torch.int32, device=DEV)
+    out = {}
+    for fold in ("1", "0"):
+        monkeypatch.setenv("PSX_WINO_BWDFOLD", fold)
+        eng = HipResNetEngine(model, layout, B, dtype=torch.float32, deterministic=True)
+        eng.index.copy_(torch.arange(B, dtype=torch.int32, device=DEV))
+        a = arena0.clone()
+        eng.train_step(a, imgs, labs)
+        torch.cuda.synchronize()
+        assert bool(eng._bwd_fold) == (fold == "1"), eng._bwd_fold.keys()
+        out[fold] = (eng.loss.double().mean().item(), eng.grads.double().clone())
+    (l1, g1), (l0, g0) = out["1"], out["0"]
+    assert l1 == l0  # the forward is untouched
+    errs = []
+    for name, e in layout.entries.items():
+        if e.region != "param":
+            continue
+        a, b = g1[e.offset:e.offset + e.numel], g0[e.offset:e.offset + e.numel]
+        errs.append((((a - b).norm() / b.norm().clamp_min(1e-30)).item(), name))
+    errs.sort()
+    print("bwd fold vs apply: median %.2e, worst %s" % (errs[len(errs) // 2][0], errs[-3:]))
+    assert errs[-1][0] < 1e-2, errs[-3:]
+    assert errs[len(errs) // 2][0] < 1e-3, errs

@@ -460,6 +460,12 @@ class HipResNetEngine:
         self.wino_s2 = self._f32(max(1, s_main))
         self.wino_wd = self._f32(max(1, s_d))
         self.wino_wpart = self._f32(max(1, s_part))
+        # the first block's first conv's weight gradient runs on the compute stream, concurrently
+        # with the side stream's (_bwd_stem): its own scratch
+        self.tail_split = (self.wg_stream is not None and os.environ.get("PSX_TAIL_SPLIT", "1") == "1"
+                           and bool(self.spec.blocks) and self.spec.blocks[0].convs[0].name in self.wino_wgrad)
+        self.wino_wd2 = self._f32(max(1, s_d)) if self.tail_split else None
+        self.wino_wpart2 = self._f32(max(1, s_part)) if self.tail_split else None
 
     def _wino_unpack(self, arena):
         """Every Winograd layer's forward and data-gradient weight transforms: the first stage's
@@ -657,9 +663,10 @@ class HipResNetEngine:
                 for cs, x, dy, fold in batch:
                     self._wgrad_now(cs, x, dy, fold)
 
-    def _wgrad_now(self, cs: ConvSpec, x, dy, fold=None):
+    def _wgrad_now(self, cs: ConvSpec, x, dy, fold=None, scratch=None):
         if cs.name in self.wino_wgrad:  # straight into the wire: no split partials to reduce
-            K.wino_wgrad(self.wino_layers[cs.name][2], dy, self.wino_wd, self.wino_wpart,
+            wd, wpart = scratch if scratch is not None else (self.wino_wd, self.wino_wpart)
+            K.wino_wgrad(self.wino_layers[cs.name][2], dy, wd, wpart,
                          self.layout.grad_view(self.grads, f"{cs.name}.weight"), self.B, cs.h, cs.w, cs.cp, cs.cout,
                          bwd_in=fold)
             return
@@ -905,8 +912,29 @@ class HipResNetEngine:
         try:
             self._bwd_block_body(arena, j)
         finally:
+            if j == 0 and self._split_tail() and self._wg_batch:
+                # the step's tail: this weight gradient runs on the compute stream after the stem's
+                # BN backward (_bwd_stem), concurrently with the side stream's, instead of after it
+                first = self.spec.blocks[0].convs[0].name
+                keep = [it for it in self._wg_batch if it[0].name != first]
+                self._tail_wgrad = [it for it in self._wg_batch if it[0].name == first] or None
+                self._wg_batch = keep
             self._flush_wgrads()
             self._flush_reduces()
+
+    _tail_wgrad = None
+    tail_split = False
+    wino_wd2 = wino_wpart2 = None
+
+    def _split_tail(self) -> bool:
+        """Only when block 0 and the stem end in the same backward segment (a gradient bucket is
+        pushed when its segment ends)."""
+        if not self.tail_split:
+            return False
+        if self.segments is None:
+            return True
+        key = ".".join(self.spec.blocks[0].convs[0].name.split(".")[:2])
+        return any(key in g and "stem" in g for g in self.segments)
 
     def _bwd_block_body(self, arena, j: int):
         sp, B = self.spec, self.B
@@ -960,6 +988,9 @@ class HipResNetEngine:
             g = self.g0
         self._bn_bwd(sp.stem_bn, arena, g, self.a0, self.y0, self.dy0, B * p * q)
         self._wgrad(st, self.x0, self.dy0)
+        tail, self._tail_wgrad = self._tail_wgrad, None
+        for cs, x, dy, fold in tail or ():
+            self._wgrad_now(cs, x, dy, fold, scratch=(self.wino_wd2, self.wino_wpart2))
 
     def backward_units(self, arena):
         """The backward pass as (unit key, thunk) in execution order. Unit keys name the

@@ -1,3 +1,4 @@
+# kernel-trace profile of the bf16 step
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT

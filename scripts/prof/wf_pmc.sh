@@ -1,3 +1,4 @@
+# PMC counters of one fused Winograd launch shape (scripts/prof/wf_one.py), three passes within the per-block slot limits
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT

@@ -1,3 +1,5 @@
+# fused Winograd kernel: GPU tests + per-layer A/B (bench/wino_fused_ab.py); WF_VARIANTS="a b" also tests and times
+# _native/variants/libpsx_kernels_<v>.so builds (csrc/build.py build_variant)
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_wino_fused_gpu.py -q -x --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/wf_t.log 2>&1 || { tail -30 gpurun_out/wf_t.log; exit 1; }

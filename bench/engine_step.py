@@ -5,7 +5,10 @@ and (c) a PyTorch-ROCm reference step (channels_last, MIOpen convs, autograd, SG
 for --dtype bf16, plain fp32 with TF32 off for --dtype fp32) on the same ResNet-18 / batch — the
 library baseline our kernels must beat.
 
-    python bench/engine_step.py --batch 128 --iters 50 [--dtype fp32]
+    python bench/engine_step.py --batch 128 --iters 50 [--dtype fp32] [--model resnet50]
+
+--model resnet50: the ImageNet-shaped ResNet-50 (224x224, 1000 classes; BASELINE config 5's
+model) on the same terms.
 """
 import argparse
 import json
@@ -22,7 +25,7 @@ import torch.nn.functional as F  # noqa: E402
 import psx  # noqa: E402,F401
 from psx.models.engine import HipResNetEngine  # noqa: E402
 from psx.models.layout import ParamLayout  # noqa: E402
-from psx.models.resnet import ResNet18  # noqa: E402
+from psx.models.resnet import ResNet18, ResNet50  # noqa: E402
 from psx.ops import kernels as K  # noqa: E402
 
 
@@ -44,23 +47,31 @@ def main():
     ap.add_argument("--no-torch", action="store_true")
     ap.add_argument("--only", default="")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--model", choices=["resnet18", "resnet50"], default="resnet18")
     a = ap.parse_args()
+    r50 = a.model == "resnet50"
+    mk = (lambda: ResNet50(1000)) if r50 else (lambda: ResNet18(100))
+    hw, ncls = (224, 1000) if r50 else (32, 100)
     f32 = a.dtype == "fp32"
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False
     B = a.batch
     torch.manual_seed(0)
-    model = ResNet18(100)
+    model = mk()
     layout = ParamLayout.from_module(model)
     arena, _ = layout.pack(model)
     arena = arena.cuda()
-    eng = HipResNetEngine(model, layout, B, dtype=torch.float32 if f32 else torch.bfloat16)
-    n = 50000
-    imgs = torch.empty(n, 32, 32, 3, dtype=torch.uint8, device="cuda")
+    kw = {}
+    if r50:  # ImageNet-shaped input and normalisation, as parallel/compute.py builds it
+        from psx.models.engine import IMAGENET_MEAN, IMAGENET_STD
+        kw = dict(in_hw=(hw, hw), mean=IMAGENET_MEAN, std=IMAGENET_STD)
+    eng = HipResNetEngine(model, layout, B, dtype=torch.float32 if f32 else torch.bfloat16, **kw)
+    n = 1024 if r50 else 50000
+    imgs = torch.empty(n, hw, hw, 3, dtype=torch.uint8, device="cuda")
     labs = torch.empty(n, dtype=torch.int32, device="cuda")
-    K.synth_gen(imgs, labs, n, 32, 32, 100, 1)
+    K.synth_gen(imgs, labs, n, hw, hw, ncls, 1)
     eng.index.copy_(torch.randperm(n, device="cuda")[:B].to(torch.int32))
-    res = {"batch": B, "dtype": a.dtype}
+    res = {"model": a.model, "batch": B, "dtype": a.dtype}
 
     def step():
         eng.train_step(arena, imgs, labs)
@@ -81,10 +92,10 @@ def main():
         res["hip_graph_ms"] = t * 1e3
         res["hip_graph_img_s"] = B / t
     if not a.no_torch and a.only in ("", "torch"):
-        m = ResNet18(100).cuda().to(memory_format=torch.channels_last)
+        m = mk().cuda().to(memory_format=torch.channels_last)
         opt = torch.optim.SGD(m.parameters(), lr=0.1)
-        x = torch.randn(B, 3, 32, 32, device="cuda").to(memory_format=torch.channels_last)
-        y = torch.randint(0, 100, (B,), device="cuda")
+        x = torch.randn(B, 3, hw, hw, device="cuda").to(memory_format=torch.channels_last)
+        y = torch.randint(0, ncls, (B,), device="cuda")
 
         def tstep():
             opt.zero_grad(set_to_none=True)

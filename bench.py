@@ -23,6 +23,12 @@ random-init.
 Secondary numbers (``"secondary"`` in the JSON line, each measured after the headline with the
 same transport, ``--secondary none`` skips them): the bf16 compute path (N = 1) and the
 co-located topology (N >= 2).
+
+Liveness at N >= 2: every rank runs a RoundWatchdog (parallel/liveness.py) over its sync rounds
+(``--round-timeout``, default 120 s): a rank whose round does not complete in time prints what was
+outstanding (the collective, the native server's issued / completed rounds) and the fallback
+switches, aborts its communicator and exits with status 3 — a hang never rides to the launcher's
+timeout. The JSON reports the ranks the RCCL communicator saw (``rccl_ranks``, ncclCommCount).
 """
 import argparse
 import json
@@ -37,6 +43,7 @@ import torch  # noqa: E402
 
 import psx  # noqa: E402,F401
 from psx.parallel.compute import HipCompute  # noqa: E402
+from psx.parallel.liveness import RoundWatchdog  # noqa: E402
 from psx.parallel.runner import (AsyncSession, build_state, make_datasets, make_local_channel,  # noqa: E402
                                  make_sync_channel)
 from psx.parallel.server import ParameterServer  # noqa: E402
@@ -48,6 +55,9 @@ from psx.parallel.worker import Worker  # noqa: E402
 from psx.utils.config import PSConfig  # noqa: E402
 
 BASELINE_SYNC_IMG_S = 82.7  # sync PS, 4 workers, measured (experiment_results/sync_4workers.json)
+FALLBACK_HINT = ("; fallbacks to try: PSX_PAIR_COMMS=0 (async point-to-point on the job communicator), "
+                 "PSX_SYNC_AGG=reduce (ncclReduce instead of the send/recv gather), --overlap off (serial "
+                 "rounds), PSX_NATIVE_SYNC=0 (Python server rounds), PSX_TRANSPORT=torch (torch.distributed)")
 
 
 class Run:
@@ -101,6 +111,14 @@ class Run:
                                  requested_id=wid)
                 self.wk.connect_to_server()
         self.native = None
+        self.watchdog = None
+        if t is not None and world > 1 and a.round_timeout > 0 and not async_dist:
+            self.watchdog = RoundWatchdog(a.round_timeout, comm=getattr(t, "comm", None), name=f" rank {rank}",
+                                          hint=FALLBACK_HINT)
+            if hasattr(self.chan, "watchdog"):
+                self.chan.watchdog = self.watchdog
+        stall = a.stall_rank.split("@") if a.stall_rank else None
+        self.stall_at = int(stall[1]) if stall and int(stall[0]) == rank else -1
         if self.wk is not None:
             self.wk.setup_data()
             self.batches = self.wk.sampler.epoch_indices(0)
@@ -118,6 +136,10 @@ class Run:
             self.zeros = torch.zeros(layout.param_numel, dtype=wire, device=device)
 
     def step(self, i):
+        if i == self.stall_at:  # test hook (--stall-rank): this rank stops taking part in rounds
+            print(f"[bench] rank {self.rank} stalls at step {i} (--stall-rank)", file=sys.stderr, flush=True)
+            while True:
+                time.sleep(3600)
         if self.wk is not None:
             self.wk.fetch_parameters()
             self.wk.train_local_batch(self.batches[i % len(self.batches)])
@@ -131,20 +153,27 @@ class Run:
             self.chan.push(None, self.zeros, self.server.core.global_step)
 
     def barrier_sync(self):
-        torch.cuda.synchronize()
-        if self.t is not None:
-            self.t.barrier()  # host barrier on the gloo control group
-        torch.cuda.synchronize()
+        wd = self.watchdog
+        if wd is not None:
+            wd.begin("barrier + device synchronize between warmup and timed steps")
+        try:
+            torch.cuda.synchronize()
+            if self.t is not None:
+                self.t.barrier()  # host barrier on the gloo control group
+            torch.cuda.synchronize()
+        finally:
+            if wd is not None:
+                wd.end()
 
     def measure(self, steps, warmup):
         """Untimed warmup, then exactly ``steps`` timed steps; returns (max seconds over ranks,
         host issue times of this rank)."""
         if self.native is not None:  # the native server rank runs its rounds in one call each
-            self.native.run(warmup)
+            self.native.run(warmup, watchdog=self.watchdog)
             self.barrier_sync()
             t0 = time.perf_counter()
-            self.native.run(steps)
-            host = [(time.perf_counter() - t0) / max(1, steps)] * steps
+            self.native.run(steps, watchdog=self.watchdog)
+            host = None  # no per-step host issue: every round was issued by one native call
         else:
             for i in range(warmup):
                 self.step(i)
@@ -185,6 +214,9 @@ class Run:
         return "colocated" if self.t is not None else "loopback"
 
     def close(self):
+        if self.watchdog is not None:
+            self.watchdog.stop()
+            self.watchdog = None
         if self.native is not None:
             self.native.close()
         if self.sess is not None:
@@ -230,6 +262,10 @@ def main():
     ap.add_argument("--secondary", choices=["auto", "none"], default="auto",
                     help="auto: after the headline also time the bf16 compute path (N=1) or the co-located "
                          "topology (N>=2), reported under 'secondary'")
+    ap.add_argument("--round-timeout", type=float, default=120.0,
+                    help="N>=2: a rank whose sync round does not complete within this many seconds reports the "
+                         "outstanding collective, aborts its communicator and exits with status 3 (0: off)")
+    ap.add_argument("--stall-rank", default="", help=argparse.SUPPRESS)  # test hook "RANK@STEP"
     a = ap.parse_args()
 
     rank, world, local = env_world()
@@ -306,13 +342,15 @@ def main():
                 "workers": W,
                 "transport": (("native RCCL (psx comm)" if getattr(t, "native", False) else "torch.distributed")
                               if t is not None else "in-process"),
+                "rccl_ranks": t.comm.count() if getattr(t, "native", False) else None,
+                "pair_communicators": len(getattr(t, "_pairs", {}) or {}) if t is not None else 0,
                 "hip_graph": cfg.use_graph,
             },
             "global_steps": run.server.core.global_step,
             "last_loss": round(loss, 4) if loss is not None else None,
             "baseline_img_s": BASELINE_SYNC_IMG_S if r18 else None,
         }
-    if a.host_timing:
+    if a.host_timing and host:
         wait = getattr(run.wk.compute, "host_wait_s", 0.0) if run.wk is not None else 0.0
         print(json.dumps({"rank": rank, "host_issue_ms_per_step": round(1e3 * sum(host) / len(host), 4),
                           "host_issue_ms_max": round(1e3 * max(host), 4),

@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <unordered_map>
 
 namespace {
 
@@ -40,10 +41,20 @@ struct Api {
   decltype(&ncclGroupStart) group_start = nullptr;
   decltype(&ncclGroupEnd) group_end = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
+  decltype(&ncclCommCount) comm_count = nullptr;  // optional
 };
 
 Api g_api;
 std::mutex g_enqueue;  // RCCL communicators are not safe for concurrent enqueue from several threads
+
+// Registry of the communicators this process created. ncclCommAbort frees the communicator, and
+// the liveness watchdog calls it from its own thread while the training thread (or the native
+// sync loop) may be about to enqueue on it: once a handle is aborted or destroyed every later
+// call on it returns kAborted instead of touching freed memory. The registry has its own mutex
+// (never g_enqueue: an enqueue stuck inside RCCL on a dead peer holds that one, and the abort is
+// exactly what must get through to unblock it).
+std::mutex g_live_mu;
+std::unordered_map<void*, int> g_live;  // 1 = live, 0 = aborted / destroyed
 
 // psx dtype codes (parallel/rccl.py DTYPES) -> RCCL
 bool to_nccl(int code, ncclDataType_t* out) {
@@ -65,6 +76,18 @@ bool sym(void* lib, const char* name, F* fn) {
 
 constexpr int kNotLoaded = -1000;
 constexpr int kBadDtype = -1001;
+constexpr int kAborted = -1002;
+
+bool live(void* h) {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  auto it = g_live.find(h);
+  return h && it != g_live.end() && it->second == 1;
+}
+
+void retire_handle(void* h) {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  g_live[h] = 0;
+}
 
 }  // namespace
 
@@ -88,6 +111,7 @@ int psx_comm_load(const char* path) {
             sym(lib, "ncclSend", &a.send) && sym(lib, "ncclRecv", &a.recv) &&
             sym(lib, "ncclGroupStart", &a.group_start) && sym(lib, "ncclGroupEnd", &a.group_end) &&
             sym(lib, "ncclGetErrorString", &a.error_string);
+  sym(lib, "ncclCommCount", &a.comm_count);  // optional (not in every stand-in)
   if (!ok) {
     fprintf(stderr, "psx_comm_load: missing RCCL symbol in %s\n", path ? path : "librccl.so");
     return -2;
@@ -115,14 +139,38 @@ int psx_comm_init(const char* id_bytes, int nranks, int rank, int device, void**
   ncclComm_t comm = nullptr;
   const ncclResult_t r = g_api.comm_init_rank(&comm, nranks, id, rank);
   *out = r == ncclSuccess ? (void*)comm : nullptr;
+  if (r == ncclSuccess) {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    g_live[(void*)comm] = 1;
+  }
   return (int)r;
 }
 
-int psx_comm_destroy(void* h) { return g_api.lib && h ? (int)g_api.comm_destroy((ncclComm_t)h) : 0; }
-int psx_comm_abort(void* h) { return g_api.lib && h ? (int)g_api.comm_abort((ncclComm_t)h) : 0; }
+int psx_comm_destroy(void* h) {
+  if (!g_api.lib || !live(h)) return 0;
+  retire_handle(h);
+  return (int)g_api.comm_destroy((ncclComm_t)h);
+}
+
+// Safe from any thread, also while another thread is blocked inside RCCL on this communicator;
+// a second abort / destroy of the same handle is a no-op.
+int psx_comm_abort(void* h) {
+  if (!g_api.lib || !live(h)) return 0;
+  retire_handle(h);
+  return (int)g_api.comm_abort((ncclComm_t)h);
+}
+
+// number of ranks of the communicator as RCCL reports it (ncclCommCount)
+int psx_comm_count(void* h, int* n) {
+  if (!g_api.lib) return kNotLoaded;
+  if (!live(h)) return kAborted;
+  if (!g_api.comm_count) return -3;
+  return (int)g_api.comm_count((ncclComm_t)h, n);
+}
 
 int psx_comm_async_error(void* h) {
-  if (!g_api.lib || !h) return kNotLoaded;
+  if (!g_api.lib) return kNotLoaded;
+  if (!live(h)) return kAborted;
   ncclResult_t e = ncclSuccess;
   const ncclResult_t r = g_api.async_error((ncclComm_t)h, &e);
   return r != ncclSuccess ? (int)r : (int)e;
@@ -131,12 +179,14 @@ int psx_comm_async_error(void* h) {
 const char* psx_comm_error_string(int code) {
   if (code == kNotLoaded) return "RCCL not loaded (psx_comm_load)";
   if (code == kBadDtype) return "unsupported dtype code";
+  if (code == kAborted) return "communicator aborted or destroyed (liveness watchdog / recovery)";
   return g_api.lib ? g_api.error_string((ncclResult_t)code) : "RCCL not loaded";
 }
 
 // sum-reduce `count` elements of `send` into `recv` on `root` (recv may alias send)
 int psx_comm_reduce_sum(void* h, const void* send, void* recv, long count, int dtype, int root, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
+  if (!live(h)) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
@@ -145,6 +195,7 @@ int psx_comm_reduce_sum(void* h, const void* send, void* recv, long count, int d
 
 int psx_comm_all_reduce_sum(void* h, const void* send, void* recv, long count, int dtype, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
+  if (!live(h)) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
@@ -155,6 +206,7 @@ int psx_comm_all_reduce_sum(void* h, const void* send, void* recv, long count, i
 // send[r*count, (r+1)*count) in recv (recv may be send + r*count: in place).
 int psx_comm_reduce_scatter_sum(void* h, const void* send, void* recv, long count, int dtype, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
+  if (!live(h)) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
@@ -164,6 +216,7 @@ int psx_comm_reduce_scatter_sum(void* h, const void* send, void* recv, long coun
 // rank r's `count` elements land at recv + r*count on every rank (send == recv + r*count: in place)
 int psx_comm_all_gather(void* h, const void* send, void* recv, long count, int dtype, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
+  if (!live(h)) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
@@ -172,6 +225,7 @@ int psx_comm_all_gather(void* h, const void* send, void* recv, long count, int d
 
 int psx_comm_broadcast(void* h, void* buf, long count, int dtype, int root, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
+  if (!live(h)) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
@@ -180,6 +234,7 @@ int psx_comm_broadcast(void* h, void* buf, long count, int dtype, int root, hipS
 
 int psx_comm_send(void* h, const void* buf, long count, int dtype, int peer, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
+  if (!live(h)) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
@@ -188,6 +243,7 @@ int psx_comm_send(void* h, const void* buf, long count, int dtype, int peer, hip
 
 int psx_comm_recv(void* h, void* buf, long count, int dtype, int peer, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
+  if (!live(h)) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
@@ -202,6 +258,7 @@ int psx_comm_group_end() { return g_api.lib ? (int)g_api.group_end() : kNotLoade
 int psx_comm_gather(void* h, const void* send, void* recv, long count, int dtype, int elem_bytes, int root,
                     int rank, int nranks, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
+  if (!live(h)) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);

@@ -195,17 +195,27 @@ int psx_ps_round_members(void* h, int* out, int cap) {
   return n;
 }
 
+static void record_update_time(PsCore* c, double seconds) {
+  if (c->update_times.size() < 100) {
+    c->update_times.push_back(seconds);
+  } else {
+    c->update_times[c->ut_pos] = seconds;
+    c->ut_pos = (c->ut_pos + 1) % 100;
+  }
+}
+
 void psx_ps_on_applied(void* h, double update_seconds) {
   PsCore* c = P(h);
   std::lock_guard<std::mutex> g(c->mu);
   c->global_step++;
   c->total_updates++;
-  if (c->update_times.size() < 100) {
-    c->update_times.push_back(update_seconds);
-  } else {
-    c->update_times[c->ut_pos] = update_seconds;
-    c->ut_pos = (c->ut_pos + 1) % 100;
-  }
+  if (update_seconds >= 0) record_update_time(c, update_seconds);
+}
+
+void psx_ps_record_update_time(void* h, double update_seconds) {
+  PsCore* c = P(h);
+  std::lock_guard<std::mutex> g(c->mu);
+  if (update_seconds >= 0) record_update_time(c, update_seconds);
 }
 
 int psx_ps_job_finished(void* h, int wid) {

@@ -39,7 +39,11 @@ int psx_ps_on_push(void* h, int wid, int64_t local_step, double now, float* weig
                    int64_t* staleness);
 // Sync: list of worker ids contributing to the completed round (valid after PSX_APPLY).
 int psx_ps_round_members(void* h, int* out, int cap);
+// update_seconds < 0: the update's time is reported later (psx_ps_record_update_time), e.g. once
+// the device events bracketing the apply kernel have completed
 void psx_ps_on_applied(void* h, double update_seconds);
+// one sample of the average_update_time_seconds ring (reference: server.py:128,140-141)
+void psx_ps_record_update_time(void* h, double update_seconds);
 int psx_ps_job_finished(void* h, int wid);  // returns 1 when no active workers remain
 int psx_ps_mark_dead(void* h, int wid);     // returns 1 if a pending sync round became complete
 int psx_ps_check_timeouts(void* h, double now, double timeout, int* dead, int cap);

@@ -80,6 +80,7 @@ struct Rt {  // libpsx_runtime.so + libpsx_kernels.so entry points
   long long (*ps_on_fetch)(void*, int, double);
   int (*ps_on_push)(void*, int, long long, double, float*, int*, long long*);
   void (*ps_on_applied)(void*, double);
+  void (*ps_record_update_time)(void*, double);
   int (*ps_job_finished)(void*, int);
   int (*ps_mark_dead)(void*, int);
   int (*ps_check_timeouts)(void*, double, double, int*, int);
@@ -177,6 +178,16 @@ struct PsxLoop {
   std::vector<WState> ws;
   int finished = 0;
   long long applies = 0;
+  // events created once: an ordering ring (a wait enqueued on a stream captures the record at
+  // call time, so the event is re-recordable right after) and timing pairs around the applies,
+  // whose DEVICE time feeds average_update_time_seconds (reference server.py:128,140-141) when
+  // they complete
+  enum { NORDER = 16 };
+  hipEvent_t order[NORDER] = {};
+  int order_pos = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> tfree;   // timing pairs available
+  std::deque<std::pair<hipEvent_t, hipEvent_t>> tbusy;    // recorded, not yet read
+  hipEvent_t ckpt_ev = nullptr;
 };
 
 namespace {
@@ -193,13 +204,30 @@ size_t gbytes(const PsxLoop* L) { return (size_t)L->c.n_params * (L->c.grad_fp16
     }                                                                                             \
   } while (0)
 
-// a is ordered after everything enqueued on b so far (a transient event)
+// a is ordered after everything enqueued on b so far (an event of the ordering ring)
 void stream_after(PsxLoop* L, hipStream_t a, hipStream_t b) {
-  hipEvent_t ev;
-  PSX_HIP(L, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  if (!L->order[L->order_pos]) PSX_HIP(L, hipEventCreateWithFlags(&L->order[L->order_pos], hipEventDisableTiming));
+  hipEvent_t ev = L->order[L->order_pos];
+  L->order_pos = (L->order_pos + 1) % PsxLoop::NORDER;
   PSX_HIP(L, hipEventRecord(ev, b));
   PSX_HIP(L, hipStreamWaitEvent(a, ev, 0));
-  PSX_HIP(L, hipEventDestroy(ev));
+}
+
+// completed apply timings -> the core's update-time statistics (block: wait for all)
+void read_timings(PsxLoop* L, bool block) {
+  while (!L->tbusy.empty()) {
+    auto p = L->tbusy.front();
+    if (block) {
+      PSX_HIP(L, hipEventSynchronize(p.second));
+    } else if (hipEventQuery(p.second) != hipSuccess) {
+      break;  // in order on the update stream: later pairs are not done either
+    }
+    float ms = 0.f;
+    PSX_HIP(L, hipEventElapsedTime(&ms, p.first, p.second));
+    L->rt.ps_record_update_time(L->c.core, 1e-3 * (double)ms);
+    L->tbusy.pop_front();
+    L->tfree.push_back(p);
+  }
 }
 
 int alloc_worker(PsxLoop* L, int w) {
@@ -218,25 +246,34 @@ int alloc_worker(PsxLoop* L, int w) {
 // the fused SGD apply of one gradient with the core's weight (+ the bf16 image of the updated
 // state when the fetch payload carries it; the fp32 fetch never reads one)
 int apply(PsxLoop* L, const void* g, float weight) {
-  const double t0 = now_s();
+  read_timings(L, false);
+  std::pair<hipEvent_t, hipEvent_t> tp{nullptr, nullptr};
+  if (!L->tfree.empty()) {
+    tp = L->tfree.back();
+    L->tfree.pop_back();
+  } else {
+    PSX_HIP(L, hipEventCreate(&tp.first));
+    PSX_HIP(L, hipEventCreate(&tp.second));
+  }
+  PSX_HIP(L, hipEventRecord(tp.first, L->s_upd));
   // the kernel wrappers report hipGetLastError(): clear what an earlier hipEventQuery (a
   // hipErrorNotReady of a transfer still in flight) left in this thread's error slot
   (void)hipGetLastError();
   const int e = L->rt.sgd_apply(L->c.arena, g, L->c.mom_buf, L->c.n_params, L->c.lr, weight, L->c.momentum,
                                 L->c.weight_decay, L->c.mom_first, L->c.grad_fp16, L->img, L->s_upd);
+  PSX_HIP(L, hipEventRecord(tp.second, L->s_upd));
+  L->tbusy.push_back(tp);
   L->c.mom_first = 0;
-  L->rt.ps_on_applied(L->c.core, now_s() - t0);
+  L->rt.ps_on_applied(L->c.core, -1.0);  // device time recorded when the pair completes
   ++L->applies;
   if (!e && L->c.ckpt_cb && L->c.ckpt_every > 0) {
     const long long gs = L->rt.ps_global_step(L->c.core);
     if (gs % L->c.ckpt_every == 0) {
       // the checkpoint reads the arena from another stream: wait for this apply only (an event,
       // not a stream synchronize)
-      hipEvent_t ev;
-      PSX_HIP(L, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-      PSX_HIP(L, hipEventRecord(ev, L->s_upd));
-      PSX_HIP(L, hipEventSynchronize(ev));
-      PSX_HIP(L, hipEventDestroy(ev));
+      if (!L->ckpt_ev) PSX_HIP(L, hipEventCreateWithFlags(&L->ckpt_ev, hipEventDisableTiming));
+      PSX_HIP(L, hipEventRecord(L->ckpt_ev, L->s_upd));
+      PSX_HIP(L, hipEventSynchronize(L->ckpt_ev));
       if (L->c.ckpt_cb(gs)) return -32;
     }
   }
@@ -520,6 +557,7 @@ void run(PsxLoop* L) {
   for (size_t w = 0; w < L->s_comm.size(); ++w)
     if (L->s_comm[w] && !L->ws[w].dead) PSX_HIP(L, hipStreamSynchronize(L->s_comm[w]));
   PSX_HIP(L, hipStreamSynchronize(L->s_upd));
+  read_timings(L, true);
   {
     std::lock_guard<std::mutex> lk(L->mu);
     L->stopped = true;
@@ -550,6 +588,7 @@ void* psx_loop_create(const PsxLoopCfg* cfg, const char* runtime_path, const cha
                   bind(rt, "psx_ps_register", &r.ps_register) && bind(rt, "psx_ps_heartbeat", &r.ps_heartbeat) &&
                   bind(rt, "psx_ps_on_fetch", &r.ps_on_fetch) && bind(rt, "psx_ps_on_push", &r.ps_on_push) &&
                   bind(rt, "psx_ps_on_applied", &r.ps_on_applied) &&
+                  bind(rt, "psx_ps_record_update_time", &r.ps_record_update_time) &&
                   bind(rt, "psx_ps_job_finished", &r.ps_job_finished) && bind(rt, "psx_ps_mark_dead", &r.ps_mark_dead) &&
                   bind(rt, "psx_ps_check_timeouts", &r.ps_check_timeouts) &&
                   bind(rt, "psx_ps_global_step", &r.ps_global_step) && bind(kn, "psx_sgd_apply", &r.sgd_apply) &&
@@ -658,6 +697,17 @@ void psx_loop_destroy(void* h) {
       hipStreamDestroy(L->s_comm[w]);
   if (L->img) hipFree(L->img);
   if (L->s_upd && L->c.own_upd_stream) hipStreamDestroy(L->s_upd);
+  for (hipEvent_t ev : L->order)
+    if (ev) hipEventDestroy(ev);
+  for (auto& p : L->tfree) {
+    hipEventDestroy(p.first);
+    hipEventDestroy(p.second);
+  }
+  for (auto& p : L->tbusy) {  // the loop drained the update stream: these are complete
+    hipEventDestroy(p.first);
+    hipEventDestroy(p.second);
+  }
+  if (L->ckpt_ev) hipEventDestroy(L->ckpt_ev);
   delete L;
 }
 

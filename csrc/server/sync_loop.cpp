@@ -27,12 +27,20 @@
 // on the device (the host waits for round r-2's completion event), and the number of rounds
 // whose device work has completed is published for the liveness watchdog
 // (parallel/liveness.py RoundWatchdog polls psx_sync_progress). Every HIP call is checked.
+//
+// Events are created once per loop, not per call: a ring of ordering events (a wait enqueued on
+// a stream captures the event's record at call time, so an event is re-recordable right after),
+// one receive event per bucket, and per in-flight round slot its completion event plus a timing
+// pair around every apply range. The update time the core reports
+// (average_update_time_seconds, reference server.py:128,140-141) is the DEVICE time of the
+// round's apply kernels, read when the round retires — not the host's launch time.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
 #include <time.h>
 
+#include <algorithm>
 #include <atomic>
 #include <deque>
 #include <vector>
@@ -47,6 +55,7 @@ struct SyncRt {
   long long (*ps_on_fetch)(void*, int, double);
   int (*ps_on_push)(void*, int, long long, double, float*, int*, long long*);
   void (*ps_on_applied)(void*, double);
+  void (*ps_record_update_time)(void*, double);
   long long (*ps_global_step)(void*);
   int (*sgd_apply_multi)(float*, const void* const*, int, float*, long, float, float, float, float, int, int, void*,
                          hipStream_t);
@@ -111,11 +120,25 @@ struct PsxSyncCfg {  // mirrored by parallel/native_sync.py (ctypes.Structure)
   int (*ckpt_cb)(long long global_step);
 };
 
+// one round in flight: its completion event and the timing events around its apply ranges
+struct PsxSyncSlot {
+  hipEvent_t done = nullptr;
+  std::vector<hipEvent_t> t0, t1;  // [max(1, nbuckets)]
+  int nt = 0;                      // ranges timed this round
+};
+
 struct PsxSync {
   PsxSyncCfg c;
   SyncRt rt;
   std::atomic<long long> issued{0}, done{0};
-  std::deque<hipEvent_t> inflight;
+  enum { NSLOT = 3, NORDER = 16 };  // at most two rounds in flight + the one being issued
+  PsxSyncSlot slot[NSLOT];
+  int cur = 0;                 // slot of the round being issued
+  std::deque<int> inflight;    // slots of issued rounds not yet retired
+  hipEvent_t order[NORDER] = {};
+  int order_pos = 0;
+  std::vector<hipEvent_t> got;  // per bucket: its gather landed (comm stream)
+  hipEvent_t ckpt_ev = nullptr;
   int err = 0;
 };
 
@@ -139,27 +162,41 @@ namespace {
     }                                                                                            \
   } while (0)
 
+// stream a waits for everything enqueued on b so far (an event of the ordering ring)
 void after(PsxSync* S, hipStream_t a, hipStream_t b) {
-  hipEvent_t ev;
-  PSX_SHIP(S, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  hipEvent_t ev = S->order[S->order_pos];
+  S->order_pos = (S->order_pos + 1) % PsxSync::NORDER;
   PSX_SHIP(S, hipEventRecord(ev, b));
   PSX_SHIP(S, hipStreamWaitEvent(a, ev, 0));
-  PSX_SHIP(S, hipEventDestroy(ev));
 }
 
-// rounds whose device work finished (host-side bookkeeping of the in-flight events)
+// the round of slot k finished on the device: its apply time (sum of its timed ranges) goes
+// to the core's update-time statistics
+void retire_slot(PsxSync* S, int k) {
+  PsxSyncSlot& sl = S->slot[k];
+  double sec = 0;
+  for (int i = 0; i < sl.nt; ++i) {
+    float ms = 0.f;
+    PSX_SHIP(S, hipEventElapsedTime(&ms, sl.t0[i], sl.t1[i]));
+    sec += 1e-3 * (double)ms;
+  }
+  if (sl.nt) S->rt.ps_record_update_time(S->c.core, sec);
+  sl.nt = 0;
+  S->done.fetch_add(1);
+}
+
+// rounds whose device work finished (host-side bookkeeping of the in-flight slots)
 void retire(PsxSync* S, size_t keep) {
   while (S->inflight.size() > keep) {
-    hipEvent_t ev = S->inflight.front();
-    PSX_SHIP(S, hipEventSynchronize(ev));
-    PSX_SHIP(S, hipEventDestroy(ev));
+    const int k = S->inflight.front();
+    PSX_SHIP(S, hipEventSynchronize(S->slot[k].done));
     S->inflight.pop_front();
-    S->done.fetch_add(1);
+    retire_slot(S, k);
   }
-  while (!S->inflight.empty() && hipEventQuery(S->inflight.front()) == hipSuccess) {
-    PSX_SHIP(S, hipEventDestroy(S->inflight.front()));
+  while (!S->inflight.empty() && hipEventQuery(S->slot[S->inflight.front()].done) == hipSuccess) {
+    const int k = S->inflight.front();
     S->inflight.pop_front();
-    S->done.fetch_add(1);
+    retire_slot(S, k);
   }
 }
 
@@ -177,6 +214,9 @@ void apply_range(PsxSync* S, long lo, long hi, void* img, hipStream_t st) {
   const size_t es = S->c.grad_fp16 ? 2 : 4;
   std::vector<const void*> srcs(S->c.nworkers);
   for (int k = 0; k < S->c.nworkers; ++k) srcs[k] = (const char*)S->c.gbufs[k] + lo * es;
+  PsxSyncSlot& sl = S->slot[S->cur];
+  const bool timed = sl.nt < (int)sl.t0.size();
+  if (timed) PSX_SHIP(S, hipEventRecord(sl.t0[sl.nt], st));
   // the kernel wrappers report hipGetLastError(): clear a hipErrorNotReady of an earlier
   // hipEventQuery (retire) from this thread's error slot
   (void)hipGetLastError();
@@ -185,11 +225,12 @@ void apply_range(PsxSync* S, long lo, long hi, void* img, hipStream_t st) {
                             S->c.mom_first, S->c.grad_fp16, img, st) &&
       !S->err)
     S->err = -61;
+  if (timed) PSX_SHIP(S, hipEventRecord(sl.t1[sl.nt++], st));
 }
 
 // the core's bookkeeping of one completed round (every member pushed, the barrier completes on
 // the last) + the checkpoint hook
-void record_round(PsxSync* S, double t0) {
+void record_round(PsxSync* S) {
   float w = 0.f;
   int nc = 0;
   long long st = 0;
@@ -200,15 +241,13 @@ void record_round(PsxSync* S, double t0) {
     fprintf(stderr, "psx sync loop: the round did not complete on the core (decision %d)\n", d);
     S->err = -62;
   }
-  S->rt.ps_on_applied(S->c.core, now_s() - t0);
+  S->rt.ps_on_applied(S->c.core, -1.0);  // the apply's device time follows when the round retires
   S->c.mom_first = 0;
   const long long g2 = S->rt.ps_global_step(S->c.core);
   if (S->c.ckpt_cb && S->c.ckpt_every > 0 && g2 % S->c.ckpt_every == 0) {
-    hipEvent_t ev;  // the apply of this round, not the whole stream
-    PSX_SHIP(S, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    PSX_SHIP(S, hipEventRecord(ev, S->c.upd_stream));
-    PSX_SHIP(S, hipEventSynchronize(ev));
-    PSX_SHIP(S, hipEventDestroy(ev));
+    // the apply of this round, not the whole stream
+    PSX_SHIP(S, hipEventRecord(S->ckpt_ev, S->c.upd_stream));
+    PSX_SHIP(S, hipEventSynchronize(S->ckpt_ev));
     if (S->c.ckpt_cb(g2) && !S->err) S->err = -63;
   }
 }
@@ -219,7 +258,6 @@ void fetch_bookkeeping(PsxSync* S) {
 
 void serial_round(PsxSync* S) {
   hipStream_t st = S->c.upd_stream;
-  const double t0 = now_s();
   fetch_bookkeeping(S);
   if (S->c.image) {
     (void)hipGetLastError();
@@ -231,30 +269,27 @@ void serial_round(PsxSync* S) {
   }
   gather(S, 0, S->c.n_params, st);
   apply_range(S, 0, S->c.n_params, S->c.image ? S->c.wire_img : nullptr, st);
-  record_round(S, t0);
+  record_round(S);
 }
 
 void overlap_round(PsxSync* S) {
   hipStream_t cs = S->c.comm_stream, us = S->c.upd_stream;
-  const double t0 = now_s();
   fetch_bookkeeping(S);
   if (!S->c.primed) {  // first round: the whole wire (every segment + the BN buffers), packed by the host
     after(S, cs, us);
     PSX_SCOMM(S, psx_comm_broadcast(S->c.comm, S->c.full_wire, S->c.full_wire_bytes, PSX_U8, 0, cs));
     S->c.primed = 1;
   }
-  std::vector<hipEvent_t> got(S->c.nbuckets);
+  std::vector<hipEvent_t>& got = S->got;
   auto issue_gather = [&](int k) {
     const PsxSyncBucket& b = S->c.buckets[k];
     after(S, cs, us);  // the previous apply of this range (and the wire pack) before new data lands
     gather(S, b.lo, b.hi - b.lo, cs);
-    PSX_SHIP(S, hipEventCreateWithFlags(&got[k], hipEventDisableTiming));
     PSX_SHIP(S, hipEventRecord(got[k], cs));
   };
   auto finish = [&](int k) {  // apply (+ segment pack) on the update stream, broadcast on cs
     const PsxSyncBucket& b = S->c.buckets[k];
     PSX_SHIP(S, hipStreamWaitEvent(us, got[k], 0));
-    PSX_SHIP(S, hipEventDestroy(got[k]));
     if (b.small) {  // bf16conv segment: the apply writes the bf16 image, then the fp32 entries
       apply_range(S, b.lo, b.hi, b.seg, us);
       (void)hipGetLastError();
@@ -273,12 +308,14 @@ void overlap_round(PsxSync* S) {
   }
   finish(S->c.nbuckets - 1);
   after(S, us, cs);  // the round ends when its broadcasts are done (next round's applies after them)
-  record_round(S, t0);
+  record_round(S);
 }
 
 }  // namespace
 
 extern "C" {
+
+void psx_sync_destroy(void* h);
 
 int psx_sync_cfg_size() { return (int)sizeof(PsxSyncCfg); }
 int psx_sync_bucket_size() { return (int)sizeof(PsxSyncBucket); }
@@ -302,10 +339,30 @@ void* psx_sync_create(const PsxSyncCfg* cfg, const char* runtime_path, const cha
   SyncRt& r = S->rt;
   const bool ok = bindf(rt, "psx_ps_on_fetch", &r.ps_on_fetch) && bindf(rt, "psx_ps_on_push", &r.ps_on_push) &&
                   bindf(rt, "psx_ps_on_applied", &r.ps_on_applied) &&
+                  bindf(rt, "psx_ps_record_update_time", &r.ps_record_update_time) &&
                   bindf(rt, "psx_ps_global_step", &r.ps_global_step) &&
                   bindf(kn, "psx_sgd_apply_multi", &r.sgd_apply_multi) && bindf(kn, "psx_gather_f32", &r.gather_f32);
   if (!ok) {
     delete S;
+    return nullptr;
+  }
+  // the loop's events, created once (see the header)
+  bool ev_ok = hipEventCreateWithFlags(&S->ckpt_ev, hipEventDisableTiming) == hipSuccess;
+  for (int i = 0; i < PsxSync::NORDER; ++i)
+    ev_ok = ev_ok && hipEventCreateWithFlags(&S->order[i], hipEventDisableTiming) == hipSuccess;
+  S->got.assign(std::max(0, cfg->nbuckets), nullptr);
+  for (auto& e : S->got) ev_ok = ev_ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  const int nt = std::max(1, cfg->nbuckets);
+  for (PsxSyncSlot& sl : S->slot) {
+    ev_ok = ev_ok && hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
+    sl.t0.assign(nt, nullptr);
+    sl.t1.assign(nt, nullptr);
+    for (int i = 0; i < nt; ++i)
+      ev_ok = ev_ok && hipEventCreate(&sl.t0[i]) == hipSuccess && hipEventCreate(&sl.t1[i]) == hipSuccess;
+  }
+  if (!ev_ok) {
+    fprintf(stderr, "psx_sync_create: hipEventCreate failed\n");
+    psx_sync_destroy(S);
     return nullptr;
   }
   return S;
@@ -316,20 +373,24 @@ void* psx_sync_create(const PsxSyncCfg* cfg, const char* runtime_path, const cha
 // (psx_sync_drain waits for it).
 int psx_sync_run(void* h, long long rounds) {
   PsxSync* S = (PsxSync*)h;
+  // relaxed capture mode while the loop runs (its event waits never invalidate a capture on
+  // another thread); the caller's mode is restored on return
   hipStreamCaptureMode cm = hipStreamCaptureModeRelaxed;
   PSX_SHIP(S, hipThreadExchangeStreamCaptureMode(&cm));
   for (long long r = 0; r < rounds && !S->err; ++r) {
+    S->slot[S->cur].nt = 0;
     if (S->c.nbuckets > 0)
       overlap_round(S);
     else
       serial_round(S);
-    hipEvent_t ev;
-    PSX_SHIP(S, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    PSX_SHIP(S, hipEventRecord(ev, S->c.upd_stream));
-    S->inflight.push_back(ev);
+    PSX_SHIP(S, hipEventRecord(S->slot[S->cur].done, S->c.upd_stream));
+    S->inflight.push_back(S->cur);
     S->issued.fetch_add(1);
-    retire(S, 2);  // at most two rounds in flight on the device
+    retire(S, 2);  // at most two rounds in flight on the device: the next slot is free
+    S->cur = (S->cur + 1) % PsxSync::NSLOT;
   }
+  hipStreamCaptureMode prev = cm;
+  PSX_SHIP(S, hipThreadExchangeStreamCaptureMode(&prev));
   return S->err;
 }
 
@@ -352,7 +413,19 @@ int psx_sync_primed(void* h) { return ((PsxSync*)h)->c.primed; }
 void psx_sync_destroy(void* h) {
   PsxSync* S = (PsxSync*)h;
   if (!S) return;
-  for (hipEvent_t ev : S->inflight) hipEventDestroy(ev);
+  if (!S->inflight.empty()) retire(S, 0);  // no event is destroyed under a pending record
+  if (S->ckpt_ev) hipEventDestroy(S->ckpt_ev);
+  for (hipEvent_t ev : S->order)
+    if (ev) hipEventDestroy(ev);
+  for (hipEvent_t ev : S->got)
+    if (ev) hipEventDestroy(ev);
+  for (PsxSyncSlot& sl : S->slot) {
+    if (sl.done) hipEventDestroy(sl.done);
+    for (hipEvent_t ev : sl.t0)
+      if (ev) hipEventDestroy(ev);
+    for (hipEvent_t ev : sl.t1)
+      if (ev) hipEventDestroy(ev);
+  }
   delete S;
 }
 

@@ -345,6 +345,11 @@ ncclResult_t ncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* err) {
   return ncclSuccess;
 }
 
+ncclResult_t ncclCommCount(const ncclComm_t comm, int* count) {
+  *count = ((Comm*)comm)->nranks;
+  return ncclSuccess;
+}
+
 const char* ncclGetErrorString(ncclResult_t r) {
   switch (r) {
     case ncclSuccess: return "no error (fakecomm)";

@@ -100,6 +100,7 @@ _RUNTIME_SIGS = {
     "psx_ps_on_push": (i32, [vp, i32, C.c_int64, f64, C.POINTER(f32), C.POINTER(i32), C.POINTER(C.c_int64)]),
     "psx_ps_round_members": (i32, [vp, C.POINTER(i32), i32]),
     "psx_ps_on_applied": (None, [vp, f64]),
+    "psx_ps_record_update_time": (None, [vp, f64]),
     "psx_ps_job_finished": (i32, [vp, i32]),
     "psx_ps_mark_dead": (i32, [vp, i32]),
     "psx_ps_check_timeouts": (i32, [vp, f64, f64, C.POINTER(i32), i32]),
@@ -128,6 +129,7 @@ _COMM_SIGS = {
     "psx_comm_destroy": (i32, [vp]),
     "psx_comm_abort": (i32, [vp]),
     "psx_comm_async_error": (i32, [vp]),
+    "psx_comm_count": (i32, [vp, C.POINTER(i32)]),
     "psx_comm_error_string": (C.c_char_p, [i32]),
     "psx_comm_reduce_sum": (i32, [vp, vp, vp, i64, i32, i32, vp]),
     "psx_comm_all_reduce_sum": (i32, [vp, vp, vp, i64, i32, vp]),

@@ -76,7 +76,12 @@ class ServerCore:
         return list(buf[: min(n, cap)])
 
     def on_applied(self, seconds: float):
+        """One update applied (global_step + 1); ``seconds`` < 0: its time follows through
+        record_update_time once the device events around the apply have completed."""
         self._rt.psx_ps_on_applied(self._h, seconds)
+
+    def record_update_time(self, seconds: float):
+        self._rt.psx_ps_record_update_time(self._h, seconds)
 
     def job_finished(self, wid: int) -> bool:
         return bool(self._rt.psx_ps_job_finished(self._h, wid))

@@ -31,10 +31,13 @@ EXIT_STALLED = 3
 
 
 class RoundWatchdog:
-    def __init__(self, timeout_s: float, comm=None, name: str = "", poll_s: float = 0.5, on_expire=None):
+    def __init__(self, timeout_s: float, comm=None, name: str = "", poll_s: float = 0.5, on_expire=None,
+                 hint: str = ""):
         self.timeout_s = float(timeout_s)
         self.comm = comm  # parallel/rccl.py NativeComm (or None for torch.distributed / gloo)
         self.name = name
+        self.hint = hint  # appended to the expiry message (e.g. bench.py's fallback switches)
+        self.label = ""   # what the rank was doing last (begin(label)): named in the expiry message
         self.poll_s = poll_s
         self.on_expire = on_expire or self._abort_and_exit
         self._lock = threading.Lock()
@@ -52,9 +55,11 @@ class RoundWatchdog:
             self._thread.start()
 
     # ---- channel side
-    def begin(self):
+    def begin(self, label: str = ""):
         """The host part of a fetch / push starts."""
         with self._lock:
+            if label:
+                self.label = label
             if not self._events and not self._blocking:
                 self._progress = time.monotonic()  # the clock starts with the first outstanding call
             self._blocking += 1
@@ -78,6 +83,8 @@ class RoundWatchdog:
             self._follow = progress_fn
             self._follow_done = -1
             self._progress = time.monotonic()
+            if progress_fn is not None:
+                self.label = "native sync server rounds (csrc/server/sync_loop.cpp)"
 
     # ---- watchdog thread
     def _poll(self) -> bool:
@@ -109,6 +116,20 @@ class RoundWatchdog:
                 self.on_expire(self)
                 return
 
+    def describe(self) -> str:
+        """The outstanding work: the last labelled call, native progress, queued round events."""
+        parts = [f"rounds done {self.rounds_done}"]
+        if self.label:
+            parts.append(f"outstanding: {self.label}")
+        if self._follow is not None:
+            try:
+                issued, done = self._follow()
+                parts.append(f"native rounds issued {issued} / completed {done}")
+            except Exception:  # noqa: BLE001
+                pass
+        parts.append(f"{len(self._events)} round event(s) pending, {self._blocking} blocking call(s)")
+        return ", ".join(parts)
+
     def _abort_and_exit(self, _wd):
         err = None
         if self.comm is not None:
@@ -117,9 +138,9 @@ class RoundWatchdog:
             except Exception:  # noqa: BLE001
                 pass
         print(f"[psx watchdog{self.name}] no sync round completed for {self.timeout_s:.0f} s "
-              f"(rounds done {self.rounds_done}, communicator async error {err}): aborting the communicator "
+              f"({self.describe()}, communicator async error {err}): aborting the communicator "
               f"and exiting with status {EXIT_STALLED} so the launcher restarts the group from the last "
-              "checkpoint", file=sys.stderr, flush=True)
+              f"checkpoint{self.hint}", file=sys.stderr, flush=True)
         if self.comm is not None:
             try:
                 self.comm.destroy(abort=True)
@@ -144,14 +165,14 @@ class WatchedRounds:
     def _native(self) -> bool:
         return bool(getattr(self.t, "native", False))
 
-    def _guard(self, fn, *a, event=False):
+    def _guard(self, fn, *a, event=False, label=""):
         """Bracket the host call; with ``event`` (native transport: the collectives are
         stream-ordered, the host does not wait for them) completion is ``_round_event()``, an
         event that completes only when the device has finished the call's collectives."""
         wd = self.watchdog
         if wd is None:
             return fn(*a)
-        wd.begin()
+        wd.begin(label)
         ev = None
         try:
             r = fn(*a)
@@ -174,7 +195,9 @@ class WatchedRounds:
     def fetch(self, worker_id, local_arena):
         # native transport: the broadcast is stream-ordered too (a fetch stuck on a dead
         # peer must not count as a finished round)
-        return self._guard(self._fetch, worker_id, local_arena, event=self._native())
+        return self._guard(self._fetch, worker_id, local_arena, event=self._native(),
+                           label=f"fetch of round {getattr(self, '_gs', '?')} (broadcast from rank 0)")
 
     def push(self, worker_id, grads, local_step, buffers=None):
-        return self._guard(self._push, worker_id, grads, local_step, buffers, event=self._native())
+        return self._guard(self._push, worker_id, grads, local_step, buffers, event=self._native(),
+                           label=f"push of round {local_step} (gradient gather / reduce to rank 0)")

@@ -76,11 +76,19 @@ def native_sync_enabled(cfg, transport, chan, server, rank: int) -> bool:
     from .overlap import OverlapSyncChannel
     from .worker import SyncCollectiveChannel
 
-    return (os.environ.get("PSX_NATIVE_SYNC", "1") == "1" and rank == 0 and server is not None
+    if not (os.environ.get("PSX_NATIVE_SYNC", "1") == "1" and rank == 0 and server is not None
             and getattr(transport, "native", False) and getattr(transport, "world_size", 1) > 1
             and cfg.mode == "sync" and cfg.topology == "dedicated" and cfg.codec in ("fp16", "none")
             and not cfg.bn_sync and type(chan) in (SyncCollectiveChannel, OverlapSyncChannel)
-            and not getattr(chan, "root_worker", True) and getattr(chan, "agg_mode", "gather") == "gather")
+            and not getattr(chan, "root_worker", True) and getattr(chan, "agg_mode", "gather") == "gather"):
+        return False
+    if type(chan) is SyncCollectiveChannel and not chan.image:
+        # serial_round broadcasts the whole fp32 arena as ONE F32 broadcast: only the raw fp32
+        # fetch payload matches the workers' collective sequence (a FetchCodec packs several
+        # broadcasts of other dtypes, e.g. bf16conv with --sync-steps > 1 or PSX_WEIGHT_IMAGE=0)
+        codec = getattr(chan, "codec", None)
+        return codec is None or codec.kind == "fp32"
+    return True
 
 
 class NativeSyncServer:
@@ -181,7 +189,8 @@ class NativeSyncServer:
         s.bytes_pushed += rounds * W * s.n * (2 if s.cfg.codec == "fp16" else 4)
         s.bytes_fetched += rounds * self.wire_bytes * max(0, W - 1)
         if self.overlap:
-            self.chan._inflight = bool(_lib().psx_sync_primed(self.h))
+            self.cfg.primed = _lib().psx_sync_primed(self.h)  # later runs skip the host re-pack
+            self.chan._inflight = bool(self.cfg.primed)
             self.chan._have_buffers = True
         if rc:
             raise RuntimeError(f"native sync server failed ({rc})")

@@ -188,11 +188,13 @@ class OverlapSyncChannel(SyncCollectiveChannel):
         b = self.buckets[k]
         if self.server is not None:
             w.wait()  # compute stream waits for the (normally already finished) reduce / gather
+            t0 = self.server._time_begin()  # device time of this range's apply (summed per round)
             if self._gather():
                 srcs = ([grads] if self.root_worker else []) + [self._gbufs[r] for r in sorted(self._gbufs)]
                 self.server.apply_range_sources(srcs, self._weight, b.lo, b.hi)
             else:
                 self.server.apply_range(grads[b.lo:b.hi], self._weight, b.lo, b.hi)
+            self.server._time_end(t0)
             self.wire.pack(self.server.arena, k)
         else:
             self._works.append(w)

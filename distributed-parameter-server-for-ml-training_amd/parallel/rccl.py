@@ -175,6 +175,13 @@ class NativeComm:
     def async_error(self) -> int:
         return comm().psx_comm_async_error(self.h) if self.h else 0
 
+    def count(self) -> int:
+        """Ranks of the communicator as RCCL reports them (ncclCommCount); -1 if unavailable."""
+        n = C.c_int(-1)
+        if not self.h or comm().psx_comm_count(self.h, C.byref(n)) != 0:
+            return -1
+        return int(n.value)
+
     def destroy(self, abort: bool = False):
         if self.h:
             (comm().psx_comm_abort if abort else comm().psx_comm_destroy)(self.h)

@@ -34,6 +34,13 @@ from .core import APPLY, WAIT, ServerCore
 _TRACE = os.environ.get("PSX_TRACE", "0") == "1"
 
 
+def arena_sha256(arena: torch.Tensor) -> str:
+    """sha256 (hex, first 32 digits) of an fp32 arena's bytes."""
+    import hashlib
+
+    return hashlib.sha256(arena.detach().to("cpu", torch.float32).contiguous().numpy().tobytes()).hexdigest()[:32]
+
+
 class ParameterServer:
     def __init__(self, cfg, layout, init_arena: torch.Tensor, counters: torch.Tensor | None = None, device="cpu",
                  total_workers: int | None = None, log=print):
@@ -67,16 +74,59 @@ class ParameterServer:
     def apply(self, grads: torch.Tensor, weight: float):
         """p <- p - lr * (weight * g [+ wd p]) [momentum]; grads are fp16 wire or fp32."""
         trace.mark("psx.apply")
-        t0 = time.perf_counter()
+        t0 = self._time_begin()
         if grads.dtype == torch.int32:  # top-k payload (parallel/topk.py)
             if not self.cfg.momentum and not self.cfg.weight_decay:
                 # no optimizer state: scatter straight into the fp32 master parameters
                 topk.decode_add(grads, self.params, -self.lr * weight, self._kcap)
                 self._wire_stale = True  # the bf16 image was not written by this update
-                return self.finish_round_apply(time.perf_counter() - t0)
+                return self.finish_round_apply(self._time_end(t0))
             grads = self._dense_of(grads)
         self.apply_range(grads[: self.n], weight, 0, self.n)
-        return self.finish_round_apply(time.perf_counter() - t0)
+        return self.finish_round_apply(self._time_end(t0))
+
+    # ------------------------------------------------------------------ update timing
+    # The reference times the apply itself (server.py:128,140-141) into average_update_time_seconds.
+    # Here the apply is an asynchronous kernel, so its time is the DEVICE time between two timing
+    # events recorded around it on the update stream; the pair is read back lazily (when a later
+    # apply starts, or at final_metrics) and fed to the core. A round applied in several ranges
+    # (gradient buckets of an overlapped round) sums its ranges. CPU arenas use the host clock.
+    # Applies captured into a HIP graph cannot be bracketed: they leave no sample.
+    _round_ev: list = []
+    _ev_pending: list = []
+    update_time_source = "none"
+
+    def _time_begin(self):
+        if self.device.type != "cuda":
+            return time.perf_counter()
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        self._drain_update_times()
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def _time_end(self, tok):
+        """Closes one timed range; returns the host seconds (CPU) or -1 (device: deferred)."""
+        if tok is None:
+            return -1.0
+        if isinstance(tok, float):
+            return time.perf_counter() - tok
+        end = torch.cuda.Event(enable_timing=True)
+        end.record()
+        self._round_ev = self._round_ev + [(tok, end)]
+        return -1.0
+
+    def _drain_update_times(self, block: bool = False):
+        keep = []
+        for pairs in self._ev_pending:
+            if block or all(e.query() for _, e in pairs):
+                s = sum(b.elapsed_time(e) for b, e in pairs) * 1e-3  # elapsed_time waits for e
+                self.core.record_update_time(s)
+                self.update_time_source = "device events around the apply kernels"
+            else:
+                keep.append(pairs)
+        self._ev_pending = keep
 
     @property
     def _kcap(self) -> int:
@@ -135,9 +185,17 @@ class ParameterServer:
             agg.add_(s[lo:hi].to(torch.float32))
         self.apply_range(agg, weight, lo, hi)
 
-    def finish_round_apply(self, dt: float = 0.0):
+    def finish_round_apply(self, dt: float = -1.0):
+        """Closes one update (global_step + 1). ``dt`` >= 0: its host-measured time (CPU arena);
+        else the device ranges timed since the last close (deferred), or none (graph capture)."""
         self._mom_first = False
-        self.core.on_applied(dt)  # host-side issue time (device work is stream-ordered)
+        if self._round_ev:
+            self._ev_pending = self._ev_pending + [self._round_ev]
+            self._round_ev = []
+            dt = -1.0
+        elif dt >= 0:
+            self.update_time_source = "host clock (synchronous CPU apply)"
+        self.core.on_applied(dt)
         return dt
 
     def _accumulate(self, grads: torch.Tensor, first: bool):
@@ -308,7 +366,7 @@ class ParameterServer:
         if res is None or not res.apply:
             return False
         trace.mark("psx.apply")
-        t0 = time.perf_counter()
+        t0 = self._time_begin()
         if self.device.type == "cuda":
             from ..ops import kernels as K
 
@@ -323,7 +381,7 @@ class ParameterServer:
             for s in srcs:  # fixed order, fp32 accumulation
                 self.agg.add_(s[: self.n].to(torch.float32))
             self.apply_range(self.agg, res.weight, 0, self.n)
-        self.finish_round_apply(time.perf_counter() - t0)
+        self.finish_round_apply(self._time_end(t0))
         if buffers_sum is not None:
             self.set_buffers_from_sum(buffers_sum, len(members))
         return True
@@ -377,13 +435,18 @@ class ParameterServer:
 
     # ------------------------------------------------------------------ metrics
     def final_metrics(self, emit: bool = False, extra: dict | None = None) -> dict:
+        if self._ev_pending:
+            self._drain_update_times(block=True)
         m = self.core.metrics()
+        m["update_time_source"] = self.update_time_source
         m["bytes_pushed"] = int(self.bytes_pushed)
         m["bytes_fetched"] = int(self.bytes_fetched)
         if self.images_processed:
             m["images_processed"] = int(self.images_processed)
-        # order-independent fingerprint of the final master state (cross-mode/run parity checks)
+        # fingerprints of the final master state: sum |p| (order-independent, for tolerance checks)
+        # and the sha256 of the fp32 arena bytes (bit-equality checks across runs / modes)
         m["final_param_checksum"] = float(self.arena.double().abs().sum())
+        m["final_param_sha256"] = arena_sha256(self.arena)
         if extra:
             m.update(extra)
         if emit:

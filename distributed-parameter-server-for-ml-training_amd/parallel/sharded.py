@@ -171,6 +171,7 @@ class ShardedSyncChannel(WatchedRounds):
         """params[lo:hi] -= lr * weight * sum_r srcs[r] (fp32 sum in rank order), image range."""
         s = self.server
         n = self.hi - self.lo
+        t0 = s._time_begin()
         if n > 0:
             bf16_img = self.wire.img.dtype == torch.bfloat16
             if s.device.type == "cuda":
@@ -189,7 +190,7 @@ class ShardedSyncChannel(WatchedRounds):
                 s.apply_range(agg, weight, self.lo, self.hi)
                 self.wire.img[self.lo:self.hi].copy_(s.params[self.lo:self.hi])
         self.wire.publish_small(s.arena, self.rank)
-        s.finish_round_apply()
+        s.finish_round_apply(s._time_end(t0))
 
     def gather_master(self):
         """fp32 parameter ranges of every rank -> every rank's arena (rank 0's feeds the final

@@ -135,8 +135,37 @@ def test_bench_multirank(world, topology):
     assert rec["n_gpus"] == world and rec["config"]["topology"] == want, rec
     assert rec["config"]["workers"] == (world - 1 if want == "dedicated" else world)
     assert rec["config"]["transport"] == "native RCCL (psx comm)"
-    assert rec["dtype"] == "fp32" and rec["value"] > 0 and rec["global_steps"] == 5, rec
+    assert rec["config"]["rccl_ranks"] == world, rec  # ncclCommCount of the job communicator
+    assert rec["dtype"] == "fp32" and rec["global_steps"] == 5, rec
+    # every rank timed exactly the K steps: value = K * batch * workers / max-rank seconds
+    W = rec["config"]["workers"]
+    assert rec["steps"] == 3 and rec["config"]["global_batch"] == 128 * W, rec
+    assert abs(rec["value"] - 3 * 128 * W / (rec["ms_per_step"] * 3e-3)) <= 1e-3 * rec["value"] + 0.02, rec
+    assert 0.5 < rec["ms_per_step"] < 5000, rec
     assert rec["last_loss"] is None or 0.0 < rec["last_loss"] < 20.0
+
+
+def test_bench_stalled_worker_exits():
+    """bench.py at world 3 (dedicated, native sync server) with worker rank 1
+    stalled at step 4 (alive, silent): the other ranks' round watchdogs name the outstanding
+    work, abort their communicators and exit non-zero within --round-timeout (+ launch), instead
+    of riding to the launcher's timeout."""
+    import time
+
+    port = _port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "3", "--steps", "6",
+           "--warmup", "2", "--secondary", "none", "--train-samples", "2048", "--round-timeout", "10",
+           "--stall-rank", "1@4"]
+    t0 = time.monotonic()
+    r = subprocess.run(cmd, env=_env({"PSX_FAKECOMM_TIMEOUT_S": "600"}), stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=400)
+    dt = time.monotonic() - t0
+    out = r.stdout
+    assert r.returncode != 0, out[-3000:]
+    assert "stalls at step 4" in out and "psx watchdog" in out and "outstanding:" in out, out[-3000:]
+    assert "fallbacks to try" in out, out[-3000:]
+    assert dt < 10 + 30 + 150, dt  # timeout + slack + startup of three GPU processes
 
 
 _RUN = r"""
@@ -149,7 +178,7 @@ cfg = PSConfig(model="resnet18", batch_size=64, epochs=1, train_samples=1024, ev
                max_steps=4, mode="sync", topology={topo!r}, workers={W}, deterministic=True).validate()
 res = {fn}(cfg, log=lambda *a, **k: None)
 if "server" in res:
-    print("RESULT " + json.dumps([res["server"]["final_param_checksum"], res["server"]["global_steps_completed"]]))
+    print("RESULT " + json.dumps([res["server"]["final_param_sha256"], res["server"]["global_steps_completed"]]))
 """
 
 
@@ -210,7 +239,9 @@ cfg = PSConfig(model="resnet18", batch_size=64, epochs=1, train_samples=1024, ev
 res = run_distributed(cfg, log=lambda *a, **k: None)
 if "server" in res:
     s = res["server"]
-    print("RESULT " + json.dumps([s["global_steps_completed"], s["gradients_processed"], s["final_param_checksum"]]))
+    print("RESULT " + json.dumps([s["global_steps_completed"], s["gradients_processed"], s["final_param_checksum"],
+                                 s["async_updates"], s["rejected_pushes"], s["average_update_time_seconds"],
+                                 s["update_time_source"]]))
 """
 
 
@@ -227,9 +258,14 @@ def test_async_remote_workers(world, topology, native_loop, tmp_path):
     out = _torchrun(world, [str(script)], extra={"PSX_NATIVE_LOOP": native_loop})
     recs = [r for r in _json_lines(out, "RESULT ") if r]
     assert len(recs) == 1, out[-3000:]
-    gs, processed, checksum = recs[0]
+    gs, processed, checksum, applied, rejected, upd_s, src = recs[0]
     assert processed == W * 4 and 0 < gs <= W * 4, recs
+    # every processed push was applied or rejected (bound 5: with 4 steps per worker, none is)
+    assert applied + rejected == processed and rejected == 0 and gs == applied, recs
     assert checksum == checksum and abs(checksum) < 1e12
+    # the update time is the DEVICE time of the R18 sgd apply (~20 us), not a launch (~us) or a
+    # host wait (~ms); the metric is rounded to 0.1 ms
+    assert src.startswith("device events") and upd_s <= 0.002, recs
 
 
 _FRUN = r"""
@@ -310,7 +346,8 @@ cfg = PSConfig(model="resnet18", batch_size=32, epochs=1, train_samples=1024, ev
 res = run_distributed(cfg, log=lambda *a, **k: None)
 if "server" in res:
     s = res["server"]
-    print("RESULT " + json.dumps([s["final_param_checksum"], s["global_steps_completed"]]))
+    print("RESULT " + json.dumps([s["final_param_checksum"], s["global_steps_completed"], s["final_param_sha256"],
+                                 s["average_update_time_seconds"], s["update_time_source"]]))
 """
 
 
@@ -333,9 +370,11 @@ def test_native_sync_server_matches_python(dt, fc, mom, rounds, tmp_path):
             out = _torchrun(3, [str(p)], extra={"PSX_NATIVE_SYNC": native})
             rec = [r for r in _json_lines(out, "RESULT ") if r]
             assert len(rec) == 1 and rec[0][1] == 5, out[-3000:]
-            sums[(ov, native)] = rec[0][0]
+            _, _, sha, upd_s, src = rec[0]
+            assert src.startswith("device events") and upd_s <= 0.002, rec  # device apply time
+            sums[(ov, native)] = sha if dt == "fp32" else rec[0][0]
     if dt == "fp32":
-        assert len(set(sums.values())) == 1, sums
+        assert len(set(sums.values())) == 1, sums  # arena sha256: bit-identical
     else:
         v = list(sums.values())
         assert max(v) - min(v) <= 1e-5 * abs(v[0]), sums

@@ -114,7 +114,7 @@ cfg = PSConfig(model="resnet18", batch_size=64, epochs=1, train_samples=2048, ev
                ckpt_every=4, ckpt_dir={ck!r}, deterministic=True).validate()
 res = run_distributed(cfg, log=lambda *a, **k: None)
 s = res["server"]
-print("RESULT " + json.dumps([s["final_param_checksum"], s["global_steps_completed"], s["async_updates"],
+print("RESULT " + json.dumps([s["final_param_sha256"], s["global_steps_completed"], s["async_updates"],
                              s["max_staleness_observed"], sorted(os.listdir({ck!r}))]))
 """
 
@@ -132,5 +132,5 @@ def test_native_loop_colocated_run_matches_python_loop(dtype, mom, tmp_path):
         out[flag] = _run(code, port, {"PSX_NATIVE_LOOP": flag})
     (a, ga, ua, sa, ca), (b, gb, ub, sb, cb) = out["1"], out["0"]
     assert ga == gb == 8 and ua == ub == 8 and sa == sb == 0, out
-    assert a == b, out  # bit-identical arenas give identical checksums
+    assert a == b, out  # sha256 of the fp32 arenas: bit-identical
     assert ca == cb and len(ca) >= 2, out  # checkpoints at steps 4 and 8 from both loops

@@ -41,6 +41,8 @@ extern "C" int psx_bgemm_f32(const float* A, const float* B, float* P, const voi
 extern "C" int psx_wino_gemm_out(const float* V, const float* U, float* y, const float* res, float* stats,
                                  const void* bst, const float* mask_aff, const void* zero, int N, int H, int W, int C,
                                  int K, const float* sshift, int bm, hipStream_t st);
+extern "C" int psx_wino_wout(const float* part, void* out, int out_fp16, float scale, int K, int C, int q,
+                             hipStream_t st);
 extern "C" int psx_bgemm_tn_f32(const float* X, const float* D, float* part, const void* zero, int T, int C, int K,
                                 int nb, int q, int BR, int BC, hipStream_t st);
 
@@ -366,16 +368,6 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
 
 // Weight gradient, dy side: DY[b][t][k] = (A dy_t A^T)[b] for the 4x4 output tile dy_t
 // (A = (A^T)^T, 6x4). Same thread layout as wino_in_kernel.
-PSX_DEV void wino_a4(const float (&y)[4], float (&r)[6]) {
-  const float e = y[0] + y[2], o = y[1] + y[3], e4 = y[0] + 4.f * y[2], o2 = 2.f * y[1] + 8.f * y[3];
-  r[0] = y[0];
-  r[1] = e + o;
-  r[2] = e - o;
-  r[3] = e4 + o2;
-  r[4] = e4 - o2;
-  r[5] = y[3];
-}
-
 __global__ __launch_bounds__(256) void wino_dy_kernel(const float* __restrict__ dy, float* __restrict__ D, int T, int H,
                                                       int W, int K) {
   const int k = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -993,25 +985,33 @@ int psx_wino_wgrad(const float* V, const float* dy, float* D, float* part, void*
   const int bt = wino_wtile(C, K);
   int e = psx_bgemm_tn_f32(V, D, part, zero, T, C, K, 36, q, bt, bt, st);
   if (e) return e;
+  return psx_wino_wout(part, out, out_fp16, scale, K, C, q, st);
+}
+
+// dW[k][c][3][3] = scale * G^T M G with M[b] = sum_j part[b * q + j][k][c]: the output transform
+// of a Winograd weight gradient (its 36 x q partial slabs [36 * q][K][C] from psx_bgemm_tn_f32 or
+// from the fused weight-gradient kernel, wino_wgrad.hip). out: OIHW, fp16 (out_fp16) or fp32.
+int psx_wino_wout(const float* part, void* out, int out_fp16, float scale, int K, int C, int q, hipStream_t st) {
   const long n = (long)K * C;
   const dim3 grid((unsigned)((n + 255) / 256));
   if (wino_xf_on()) {
     const dim3 gx((unsigned)((n + 63) / 64));
 #define PSX_WOUT(OT, QV) \
   hipLaunchKernelGGL((wino_wout_xf_kernel<OT, QV>), gx, dim3(64 * kXfWaves), 0, st, part, (OT*)out, K, C, q, scale)
+#define PSX_WOUT_Q(OT)          \
+  if (q == 1) PSX_WOUT(OT, 1);  \
+  else if (q == 2) PSX_WOUT(OT, 2);   \
+  else if (q == 4) PSX_WOUT(OT, 4);   \
+  else if (q == 8) PSX_WOUT(OT, 8);   \
+  else if (q == 16) PSX_WOUT(OT, 16); \
+  else if (q == 32) PSX_WOUT(OT, 32); \
+  else PSX_WOUT(OT, 0)
     if (out_fp16) {
-      if (q == 1) PSX_WOUT(uint16_t, 1);
-      else if (q == 2) PSX_WOUT(uint16_t, 2);
-      else if (q == 4) PSX_WOUT(uint16_t, 4);
-      else if (q == 8) PSX_WOUT(uint16_t, 8);
-      else PSX_WOUT(uint16_t, 0);
+      PSX_WOUT_Q(uint16_t);
     } else {
-      if (q == 1) PSX_WOUT(float, 1);
-      else if (q == 2) PSX_WOUT(float, 2);
-      else if (q == 4) PSX_WOUT(float, 4);
-      else if (q == 8) PSX_WOUT(float, 8);
-      else PSX_WOUT(float, 0);
+      PSX_WOUT_Q(float);
     }
+#undef PSX_WOUT_Q
 #undef PSX_WOUT
     return (int)hipGetLastError();
   }

@@ -23,6 +23,17 @@ PSX_DEV void wino_at6(const float (&m)[6], float (&o)[4]) {
   o[3] = b + 8.f * d + m[5];
 }
 
+// one axis of A dy A^T (the dy transform of the weight gradient): 4 dy values -> 6
+PSX_DEV void wino_a4(const float (&y)[4], float (&r)[6]) {
+  const float e = y[0] + y[2], o = y[1] + y[3], e4 = y[0] + 4.f * y[2], o2 = 2.f * y[1] + 8.f * y[3];
+  r[0] = y[0];
+  r[1] = e + o;
+  r[2] = e - o;
+  r[3] = e4 + o2;
+  r[4] = e4 - o2;
+  r[5] = y[3];
+}
+
 PSX_DEV void wino_gt6(const float (&m)[6], float (&o)[3]) {
   const float a = m[1] + m[2], b = m[1] - m[2], c = m[3] + m[4], d = m[3] - m[4];
   o[0] = 0.25f * m[0] - a * (1.f / 6.f) + c * (1.f / 24.f);

@@ -273,6 +273,17 @@ void psx_ps_set_global_step(void* h, int64_t s) {
   c->rounds_done = s;
 }
 
+// Sync job shrunk after a lost worker (parallel/elastic.py): the rounds after `step` were rolled
+// back on the device, so they leave the step and update counts too.
+void psx_ps_rollback_to(void* h, int64_t step) {
+  PsCore* c = P(h);
+  std::lock_guard<std::mutex> g(c->mu);
+  if (step < c->global_step) c->total_updates -= c->global_step - step;
+  c->global_step = step;
+  c->rounds_done = step;
+  c->round.clear();
+}
+
 int psx_ps_num_active(void* h) {
   PsCore* c = P(h);
   std::lock_guard<std::mutex> g(c->mu);

@@ -50,6 +50,7 @@ int psx_ps_check_timeouts(void* h, double now, double timeout, int* dead, int ca
 int psx_ps_sync_ready(void* h);             // 1 if the current sync round is complete
 int64_t psx_ps_global_step(void* h);
 void psx_ps_set_global_step(void* h, int64_t s);
+void psx_ps_rollback_to(void* h, int64_t step);  // rounds after `step` undone (sync shrink)
 int psx_ps_num_active(void* h);
 // Writes the SERVER_FINAL_METRICS JSON object (no prefix) into buf; returns length.
 int psx_ps_metrics_json(void* h, double now, char* buf, int cap);

@@ -43,6 +43,7 @@
 #include <algorithm>
 #include <atomic>
 #include <deque>
+#include <mutex>
 #include <vector>
 
 #include "psx_comm.h"
@@ -118,6 +119,11 @@ struct PsxSyncCfg {  // mirrored by parallel/native_sync.py (ctypes.Structure)
   hipStream_t comm_stream;  // the overlapped round's communication stream
   long long ckpt_every;
   int (*ckpt_cb)(long long global_step);
+  // sync job that survives a lost worker (parallel/elastic.py; nullable): 3 arena snapshots, one
+  // per in-flight round slot, each taken at its round's start (stream order: after the previous
+  // round's apply) — the state a shrunk job resumes from without a checkpoint rollback
+  float* snap;
+  float* snap_mom;  // momentum buffer snapshots (3 x n_params; nullable)
 };
 
 // one round in flight: its completion event and the timing events around its apply ranges
@@ -140,6 +146,12 @@ struct PsxSync {
   std::vector<hipEvent_t> got;  // per bucket: its gather landed (comm stream)
   hipEvent_t ckpt_ev = nullptr;
   int err = 0;
+  // psx_sync_abort (the liveness watchdog's thread): from then on no round counts as done and no
+  // new round is issued; `good` = rounds retired before it
+  std::mutex mu;
+  std::atomic<int> aborting{0};
+  long long good = -1;
+  int mom_first0 = 0;  // mom_first at creation (a rollback to round 0 restores it)
 };
 
 namespace {
@@ -171,9 +183,15 @@ void after(PsxSync* S, hipStream_t a, hipStream_t b) {
 }
 
 // the round of slot k finished on the device: its apply time (sum of its timed ranges) goes
-// to the core's update-time statistics
+// to the core's update-time statistics. After an abort a finished event means nothing (the
+// aborted collectives let the stream run on): such rounds are not counted.
 void retire_slot(PsxSync* S, int k) {
   PsxSyncSlot& sl = S->slot[k];
+  std::lock_guard<std::mutex> lk(S->mu);
+  if (S->aborting.load()) {
+    sl.nt = 0;
+    return;
+  }
   double sec = 0;
   for (int i = 0; i < sl.nt; ++i) {
     float ms = 0.f;
@@ -256,8 +274,19 @@ void fetch_bookkeeping(PsxSync* S) {
   for (int k = 0; k < S->c.nworkers; ++k) S->rt.ps_on_fetch(S->c.core, S->c.members[k], now_s());
 }
 
+// elastic: this round's starting state into its slot's snapshot
+void snapshot(PsxSync* S, hipStream_t st) {
+  if (!S->c.snap) return;
+  PSX_SHIP(S, hipMemcpyAsync(S->c.snap + (size_t)S->cur * S->c.arena_numel, S->c.arena,
+                             (size_t)S->c.arena_numel * 4, hipMemcpyDeviceToDevice, st));
+  if (S->c.snap_mom && S->c.mom_buf)
+    PSX_SHIP(S, hipMemcpyAsync(S->c.snap_mom + (size_t)S->cur * S->c.n_params, S->c.mom_buf,
+                               (size_t)S->c.n_params * 4, hipMemcpyDeviceToDevice, st));
+}
+
 void serial_round(PsxSync* S) {
   hipStream_t st = S->c.upd_stream;
+  snapshot(S, st);
   fetch_bookkeeping(S);
   if (S->c.image) {
     (void)hipGetLastError();
@@ -268,12 +297,14 @@ void serial_round(PsxSync* S) {
     PSX_SCOMM(S, psx_comm_broadcast(S->c.comm, S->c.arena, S->c.arena_numel, PSX_F32, 0, st));
   }
   gather(S, 0, S->c.n_params, st);
+  if (S->err) return;  // a failed gather is never applied
   apply_range(S, 0, S->c.n_params, S->c.image ? S->c.wire_img : nullptr, st);
   record_round(S);
 }
 
 void overlap_round(PsxSync* S) {
   hipStream_t cs = S->c.comm_stream, us = S->c.upd_stream;
+  snapshot(S, us);
   fetch_bookkeeping(S);
   if (!S->c.primed) {  // first round: the whole wire (every segment + the BN buffers), packed by the host
     after(S, cs, us);
@@ -288,6 +319,7 @@ void overlap_round(PsxSync* S) {
     PSX_SHIP(S, hipEventRecord(got[k], cs));
   };
   auto finish = [&](int k) {  // apply (+ segment pack) on the update stream, broadcast on cs
+    if (S->err) return;  // a failed gather is never applied
     const PsxSyncBucket& b = S->c.buckets[k];
     PSX_SHIP(S, hipStreamWaitEvent(us, got[k], 0));
     if (b.small) {  // bf16conv segment: the apply writes the bf16 image, then the fp32 entries
@@ -336,6 +368,7 @@ void* psx_sync_create(const PsxSyncCfg* cfg, const char* runtime_path, const cha
   }
   PsxSync* S = new PsxSync();
   S->c = *cfg;
+  S->mom_first0 = cfg->mom_first;
   SyncRt& r = S->rt;
   const bool ok = bindf(rt, "psx_ps_on_fetch", &r.ps_on_fetch) && bindf(rt, "psx_ps_on_push", &r.ps_on_push) &&
                   bindf(rt, "psx_ps_on_applied", &r.ps_on_applied) &&
@@ -378,11 +411,16 @@ int psx_sync_run(void* h, long long rounds) {
   hipStreamCaptureMode cm = hipStreamCaptureModeRelaxed;
   PSX_SHIP(S, hipThreadExchangeStreamCaptureMode(&cm));
   for (long long r = 0; r < rounds && !S->err; ++r) {
+    if (S->aborting.load()) {  // the watchdog aborted the communicator: issue nothing more
+      S->err = -65;
+      break;
+    }
     S->slot[S->cur].nt = 0;
     if (S->c.nbuckets > 0)
       overlap_round(S);
     else
       serial_round(S);
+    if (S->err) break;  // a round that failed to issue is neither counted nor retired
     PSX_SHIP(S, hipEventRecord(S->slot[S->cur].done, S->c.upd_stream));
     S->inflight.push_back(S->cur);
     S->issued.fetch_add(1);
@@ -408,6 +446,44 @@ void psx_sync_progress(void* h, long long* out) {
 }
 
 int psx_sync_mom_first(void* h) { return ((PsxSync*)h)->c.mom_first; }
+
+// Liveness watchdog (another thread): freezes the count of rounds known good, stops the loop from
+// issuing more and aborts the communicator (the blocked loop thread then runs out). Returns the
+// good count.
+long long psx_sync_abort(void* h) {
+  PsxSync* S = (PsxSync*)h;
+  {
+    std::lock_guard<std::mutex> lk(S->mu);
+    if (!S->aborting.load()) {
+      S->good = S->done.load();
+      S->aborting.store(1);
+    }
+  }
+  psx_comm_abort(S->c.comm);
+  return S->good;
+}
+
+// After a failed or aborted run: waits for the streams, restores the arena (and momentum) to the
+// start of the first round not known good and returns the number of rounds kept (of this loop's
+// lifetime). -1: no snapshots configured.
+long long psx_sync_rollback(void* h) {
+  PsxSync* S = (PsxSync*)h;
+  if (!S->c.snap) return -1;
+  (void)hipStreamSynchronize(S->c.upd_stream);
+  if (S->c.comm_stream) (void)hipStreamSynchronize(S->c.comm_stream);
+  retire(S, 0);  // rounds finished before an error (not after an abort) still count
+  const long long g = S->aborting.load() ? S->good : S->done.load();
+  const int k = (int)(g % PsxSync::NSLOT);
+  if (hipMemcpy(S->c.arena, S->c.snap + (size_t)k * S->c.arena_numel, (size_t)S->c.arena_numel * 4,
+                hipMemcpyDeviceToDevice) != hipSuccess)
+    return -2;
+  if (S->c.snap_mom && S->c.mom_buf &&
+      hipMemcpy(S->c.mom_buf, S->c.snap_mom + (size_t)k * S->c.n_params, (size_t)S->c.n_params * 4,
+                hipMemcpyDeviceToDevice) != hipSuccess)
+    return -2;
+  if (g == 0) S->c.mom_first = S->mom_first0;
+  return g;
+}
 int psx_sync_primed(void* h) { return ((PsxSync*)h)->c.primed; }
 
 void psx_sync_destroy(void* h) {

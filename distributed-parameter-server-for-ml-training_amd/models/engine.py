@@ -412,11 +412,14 @@ class HipResNetEngine:
         The fused forward still writes V where the Winograd weight gradient reads it."""
         self.wino_layers = {}
         self.wino_wgrad = set()
+        self.wino_wgf = set()   # weight gradient by the fused kernel (wino_wgrad.hip): reads x, not V
         self.wino_bnfold = {}
         self.wino_fused = {}
+        self._xfold = {}        # conv -> (pre-BN y, BN affine): its input is relu(BN(y)), never written
         if not self.f32 or os.environ.get("PSX_WINO", "1") == "0":
             return
         fuse = os.environ.get("PSX_WINO_FUSE", "1") == "1"
+        wgf = os.environ.get("PSX_WINO_WGF", "1") == "1"
         maxhw = int(os.environ.get("PSX_WINO_MAXHW", "64"))
         wg = os.environ.get("PSX_WINO_WGRAD", "1") == "1"
         wg_maxhw = int(os.environ.get("PSX_WINO_WGRAD_MAXHW", "32"))
@@ -435,12 +438,19 @@ class HipResNetEngine:
             self.wino_fused[cs.name] = (ff, fd)
             uf = self._f32((40 if ff else 36) * cs.cout * cs.cp)
             ud = self._f32((40 if fd else 36) * cs.cout * cs.cp) if cs.need_dgrad else None
-            v = self._f32(vc) if q > 0 else None  # None: the forward's V goes to scratch
+            # fused weight gradient (wino_wgrad.hip, PSX_WINO_WGF=1): transforms x and dy itself, so
+            # the forward keeps no V and no D is formed
+            qf = K.wino_wgrad_fused_q(B, cs.h, cs.w, cs.cp, cs.cout) if q > 0 and wgf else 0
+            v = self._f32(vc) if q > 0 and not qf else None  # None: the forward's V goes to scratch
             self.wino_layers[cs.name] = (uf, ud, v)
             if q > 0:
                 self.wino_wgrad.add(cs.name)
-                s_d = max(s_d, vk)
-                s_part = max(s_part, 36 * q * cs.cout * cs.cp)
+                if qf:
+                    self.wino_wgf.add(cs.name)
+                    s_part = max(s_part, 36 * qf * cs.cout * cs.cp)
+                else:
+                    s_d = max(s_d, vk)
+                    s_part = max(s_part, 36 * q * cs.cout * cs.cp)
         # BN folded into the next conv's input transform (PSX_WINO_BNFOLD=1, default): a block's inner
         # BN (+ ReLU) whose only consumer is a Winograd conv with a Winograd weight gradient (that
         # reads V, not the activation) is finalized and applied inside wino_in_kernel, so its
@@ -664,6 +674,12 @@ class HipResNetEngine:
                     self._wgrad_now(cs, x, dy, fold)
 
     def _wgrad_now(self, cs: ConvSpec, x, dy, fold=None, scratch=None):
+        if cs.name in self.wino_wgf:  # fused Winograd weight gradient straight into the wire
+            wpart = scratch[1] if scratch is not None else self.wino_wpart
+            xf = self._xfold.get(cs.name)  # its input was never written: y + the BN affine instead
+            K.wino_wgrad_fused(xf[0] if xf else x, dy, wpart, self.layout.grad_view(self.grads, f"{cs.name}.weight"),
+                               self.B, cs.h, cs.w, cs.cp, cs.cout, xaff=xf[1] if xf else None, bwd_in=fold)
+            return
         if cs.name in self.wino_wgrad:  # straight into the wire: no split partials to reduce
             wd, wpart = scratch if scratch is not None else (self.wino_wd, self.wino_wpart)
             K.wino_wgrad(self.wino_layers[cs.name][2], dy, wd, wpart,
@@ -865,6 +881,7 @@ class HipResNetEngine:
                     if train and bs.name in self.wino_bnfold:  # applied by the next conv's input transform
                         bn_in = (self._red(bs, "fwd"), self._fin_fwd(bs, arena, d["y"][i].numel() // bs.c))
                         src = d["y"][i]
+                        self._xfold[b.convs[i + 1].name] = (d["y"][i], self.bn[bs.name]["affine"])
                         continue
                     self._apply(bs, d["y"][i], d["a"][i], arena, train)
                     src = d["a"][i]

@@ -60,6 +60,9 @@ _KERNEL_SIGS = {
     "psx_wino_wgrad_q": (i32, [i32, i32, i32, i32, i32]),
     "psx_wino_wgrad": (i32, [vp, vp, vp, vp, vp, i32, f32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
     "psx_bgemm_tn_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
+    "psx_wino_wout": (i32, [vp, vp, i32, f32, i32, i32, i32, vp]),
+    "psx_wino_wgrad_fused_q": (i32, [i32, i32, i32, i32, i32]),
+    "psx_wino_wgrad_fused": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, f32, i32, i32, i32, i32, i32, vp]),
     "psx_bn_finalize": (i32, [vp, i32, i32, f32, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "psx_bn_eval_affine": (i32, [i32, vp, vp, vp, vp, f32, vp, vp, vp]),
     "psx_bn_apply": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
@@ -107,6 +110,7 @@ _RUNTIME_SIGS = {
     "psx_ps_sync_ready": (i32, [vp]),
     "psx_ps_global_step": (C.c_int64, [vp]),
     "psx_ps_set_global_step": (None, [vp, C.c_int64]),
+    "psx_ps_rollback_to": (None, [vp, C.c_int64]),
     "psx_ps_num_active": (i32, [vp]),
     "psx_ps_metrics_json": (i32, [vp, f64, C.c_char_p, i32]),
     "psx_ps_staleness_hist": (i32, [vp, C.POINTER(C.c_int64), i32]),

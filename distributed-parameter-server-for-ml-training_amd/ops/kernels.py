@@ -271,6 +271,33 @@ def wino_wgrad(v, dy, d, part, out, nb, h, w, c, k, scale=1.0, bwd_in=None):
                                    C.byref(bwd_in[2]) if bwd_in is not None else None, stream_ptr()), "wino_wgrad")
 
 
+def wino_wgrad_fused_q(nb, h, w, c, k) -> int:
+    """Tile ranges of the fused Winograd weight gradient (csrc/kernels/wino_wgrad.hip; 0: not
+    applicable): its partial slabs take 36 * q * k * c floats."""
+    return int(kernels().psx_wino_wgrad_fused_q(nb, h, w, c, k))
+
+
+def wino_wgrad_fused(x, dy, part, out, nb, h, w, c, k, scale=1.0, xaff=None, bwd_in=None):
+    """Weight gradient of a 3x3 / stride-1 / pad-1 fp32 conv in one fused Winograd launch
+    (csrc/kernels/wino_wgrad.hip: x and dy transformed in registers, 36 tile-reduction GEMMs on
+    the f32 MFMA; neither V nor D in HBM) + the output transform. x [nb][h][w][c] is the conv
+    input, or with xaff ([2][c] scale, shift) the pre-BN y whose BN + ReLU the forward folded
+    into its input transform (x = relu(scale y + shift)). dy [nb][h][w][k]; bwd_in = (y, part,
+    BnBwdFin) as wino_wgrad. part: >= 36 * q * k * c floats (q = wino_wgrad_fused_q). out: OIHW
+    gradient (fp16 wire or fp32) = scale * dW."""
+    q = wino_wgrad_fused_q(nb, h, w, c, k)
+    assert q > 0 and x.dtype == torch.float32 and dy.dtype == torch.float32
+    assert x.numel() == nb * h * w * c and dy.numel() == nb * h * w * k
+    assert part.numel() >= 36 * q * k * c and out.dtype in (torch.float16, torch.float32) and out.numel() >= k * c * 9
+    assert xaff is None or (xaff.dtype == torch.float32 and xaff.numel() >= 2 * c)
+    check(kernels().psx_wino_wgrad_fused(ptr(x), ptr(xaff), ptr(dy),
+                                         ptr(bwd_in[0]) if bwd_in is not None else None,
+                                         ptr(bwd_in[1]) if bwd_in is not None else None,
+                                         C.byref(bwd_in[2]) if bwd_in is not None else None, ptr(part), ptr(out),
+                                         int(out.dtype == torch.float16), float(scale), nb, h, w, c, k, stream_ptr()),
+          "wino_wgrad_fused")
+
+
 def conv_wgrad2_splits(nb, h, w, ic, oc, k, stride, pad, kg, f32=False) -> int:
     n = kernels().psx_conv_wgrad2(None, None, None, None, nb, h, w, ic, oc, k, k, stride, pad, kg, int(bool(f32)), None)
     if n <= 0:

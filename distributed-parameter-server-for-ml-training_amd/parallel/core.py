@@ -105,6 +105,10 @@ class ServerCore:
     def global_step(self, v: int):
         self._rt.psx_ps_set_global_step(self._h, int(v))
 
+    def rollback_to(self, step: int):
+        """Rounds after ``step`` were undone (sync job shrunk after a lost worker)."""
+        self._rt.psx_ps_rollback_to(self._h, int(step))
+
     def num_active(self) -> int:
         return self._rt.psx_ps_num_active(self._h)
 

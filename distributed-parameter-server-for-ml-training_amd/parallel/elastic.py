@@ -1,0 +1,186 @@
+"""Sync mode that survives a lost worker: the job shrinks to the surviving ranks in-process.
+
+The reference's sync handler is count-triggered and its JobFinished drops a worker from the
+active set, so a departed worker never wedges the server (reference:
+src/parameter_server/server.py:264-288, :306-318); SURVEY §5.3 asks the same of the RCCL data
+plane, where a dead or hung rank instead leaves every collective of the round waiting. With
+``--on-worker-loss shrink`` (the default of the dedicated sync topology):
+
+1. **Detect.** Every rank's RoundWatchdog (parallel/liveness.py) sees no round complete within
+   ``--round-timeout``. Instead of exiting it calls ``on_stall``: freeze the server's count of
+   rounds known good (the native loop: ``psx_sync_abort``; the Python loop: its round events),
+   then abort the job communicator (ncclCommAbort: RCCL kernels waiting on the dead peer exit;
+   the native registry turns every later call on the handle into an error, never a use of freed
+   memory — csrc/comm/rccl_comm.cpp). A rank whose collective fails outright (an RCCL error)
+   takes the same path. The training thread sees ``CommLost`` / ``RcclError`` at its next call.
+2. **Agree.** Through the rendezvous TCPStore (the gloo group is as dead as the communicator):
+   every survivor checks in under ``psx/el/<tag>/e<epoch>/alive/<rank>``; rank 0 (the server)
+   waits up to the grace period for the others, then publishes the plan — the surviving ranks,
+   the number of rounds kept R, and a fresh ncclUniqueId.
+3. **Rebuild.** The server restores its arena to the start of round R (a device snapshot taken at
+   every round start — no checkpoint rollback, no process restart), marks the lost workers dead
+   in the native core (the wait-for-N barrier shrinks: ps_core.cpp psx_ps_mark_dead) and rolls
+   its global step back to R. Every survivor builds the new communicator in-process
+   (ncclCommInitRank over the survivors, ``ShrunkTransport``) — no re-exec of a GPU process —
+   and the workers re-enter their loop at round R (the same fast-forward as a checkpoint resume,
+   parallel/worker.py rounds_to_batches). A worker left out of the plan (one that hung past the
+   grace period and woke up) exits.
+
+Scope: sync mode, dedicated topology (rank 0 is the server only), native RCCL transport, dense
+gradient wire. Rounds in flight at the failure are redone by the survivors; the dead worker's
+data shard is not trained further (the reference's lost pushes are lost too).
+"""
+from __future__ import annotations
+
+import json
+import os
+import pickle
+import sys
+import time
+
+import torch
+
+from .liveness import CommLost
+from .rccl import NativeComm, RcclError, RcclTransport
+
+EXCLUDED = 5  # exit status of a rank the survivors' plan left out
+
+
+def enabled(cfg, transport, world: int) -> bool:
+    return (getattr(cfg, "on_worker_loss", "restart") == "shrink" and cfg.mode == "sync"
+            and cfg.topology == "dedicated" and world > 2 and getattr(transport, "native", False)
+            and cfg.codec in ("fp16", "none") and not cfg.bn_sync)
+
+
+def lost_error(e: BaseException) -> bool:
+    """Errors that mean 'the communicator is gone' (recoverable by shrinking)."""
+    if isinstance(e, (CommLost, RcclError)):
+        return True
+    return isinstance(e, RuntimeError) and "native sync server failed" in str(e)
+
+
+def make_on_stall(transport, freeze=None, log=None):
+    """RoundWatchdog ``on_expire`` of a shrinking job: freeze the good-round count (server), abort
+    the communicator, flag the transport; the training thread recovers."""
+
+    def on_stall(wd):
+        msg = (f"[psx elastic{wd.name}] no sync round completed for {wd.timeout_s:.0f} s ({wd.describe()}): "
+               "aborting the communicator and shrinking the job to the surviving ranks")
+        print(msg, file=sys.stderr, flush=True)
+        try:
+            if freeze is not None:
+                freeze()  # native loop: psx_sync_abort freezes its count and aborts the comm itself
+        finally:
+            transport.lost = True
+            try:
+                transport.comm.destroy(abort=True)
+            except Exception:  # noqa: BLE001
+                pass
+
+    return on_stall
+
+
+class ShrunkTransport(RcclTransport):
+    """The data plane of the survivors: RcclTransport's collectives on a new communicator whose
+    ranks are the positions in ``members`` (the original ranks kept, ascending; rank 0 = the
+    server), and host control over the rendezvous store among the members (the gloo group still
+    counts the dead ranks)."""
+
+    lost = False
+
+    def __init__(self, base, members, comm, tag: str):  # noqa: D107 - no RcclTransport.__init__
+        self.base = base
+        self.members = list(members)
+        self.orig_rank = base.rank
+        self.rank = self.members.index(base.rank)
+        self.world_size = len(self.members)
+        self.device = base.device
+        self.backend = base.backend
+        self.comm = comm
+        self._cstream = base._cstream
+        self._pairs, self._pstream = {}, {}
+        self.tag = tag
+        self._seq = 0
+        self.degraded = ()
+        self.elastic_tag = getattr(base, "elastic_tag", "job")
+
+    # ---- host control among the members (original ranks) on the store
+    @staticmethod
+    def _store():
+        from torch.distributed import distributed_c10d as c10d
+
+        return c10d._get_default_store()
+
+    def _gather(self, obj):
+        self._seq += 1
+        key, st = f"{self.tag}/c{self._seq}", self._store()
+        st.set(f"{key}/{self.orig_rank}", pickle.dumps(obj))
+        st.wait([f"{key}/{r}" for r in self.members])
+        return [pickle.loads(st.get(f"{key}/{r}")) for r in self.members]
+
+    def barrier(self):
+        self._gather(None)
+
+    def all_gather_object(self, obj):
+        return self._gather(obj)
+
+    def broadcast_object(self, obj):
+        return self._gather(obj if self.rank == 0 else None)[0]
+
+    def close(self):
+        try:
+            torch.cuda.synchronize(self.device)
+        finally:
+            self.comm.destroy(abort=self.lost)
+            self.base.comm.destroy(abort=True)  # already aborted: a no-op on the handle registry
+            self._seq += 1
+            key, st = f"{self.tag}/close{self._seq}", self._store()
+            try:  # the store may live in rank 0's process: rank 0 leaves last
+                st.set(f"{key}/{self.orig_rank}", b"1")
+                if self.rank == 0:
+                    st.wait([f"{key}/{r}" for r in self.members if r != self.orig_rank])
+            except Exception:  # noqa: BLE001
+                pass
+            import torch.distributed as dist
+
+            if dist.is_initialized():
+                dist.destroy_process_group()
+
+
+def shrink(t, epoch: int, grace_s: float, rounds_kept=None, log=print):
+    """Collective among the survivors (see the module docstring, steps 2-3). ``t``: the current
+    transport (RcclTransport or ShrunkTransport) whose communicator is lost; rank 0 passes
+    ``rounds_kept`` (its good rounds). Returns (ShrunkTransport, rounds_kept, dead original ranks)
+    — or exits the process with status EXCLUDED when the plan leaves this rank out."""
+    base = getattr(t, "base", t)
+    tag = f"psx/el/{getattr(base, 'elastic_tag', 'job')}"
+    st = ShrunkTransport._store()
+    key = f"{tag}/e{epoch}"
+    me = getattr(t, "orig_rank", t.rank)
+    old_members = list(getattr(t, "members", range(t.world_size)))
+    st.set(f"{key}/alive/{me}", str(me).encode())
+    if me == 0:
+        deadline = time.monotonic() + grace_s
+        others = [r for r in old_members if r != 0]
+        while time.monotonic() < deadline:
+            if all(st.check([f"{key}/alive/{r}"]) for r in others):
+                break
+            time.sleep(0.05)
+        members = [0] + [r for r in others if st.check([f"{key}/alive/{r}"])]
+        plan = {"members": members, "rounds": int(rounds_kept), "uid": NativeComm.new_id().hex()}
+        st.set(f"{key}/plan", json.dumps(plan).encode())
+    else:
+        st.wait([f"{key}/plan"], __import__("datetime").timedelta(seconds=grace_s + 120))
+        plan = json.loads(st.get(f"{key}/plan"))
+    members = plan["members"]
+    dead = [r for r in old_members if r not in members]
+    if me not in members:
+        print(f"[psx elastic] rank {me} is not among the survivors {members} (it missed the check-in): exiting",
+              file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(EXCLUDED)
+    comm = NativeComm.from_id(bytes.fromhex(plan["uid"]), len(members), members.index(me), base.device)
+    nt = ShrunkTransport(base, members, comm, f"{key}/ctl")
+    log(f"[psx elastic] epoch {epoch}: rank {me} continues as rank {nt.rank} of {nt.world_size} "
+        f"(lost ranks {dead}); resuming at round {plan['rounds']}")
+    return nt, int(plan["rounds"]), dead

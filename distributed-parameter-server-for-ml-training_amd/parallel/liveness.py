@@ -30,6 +30,11 @@ from collections import deque
 EXIT_STALLED = 3
 
 
+class CommLost(RuntimeError):
+    """The job communicator was aborted (liveness watchdog or an RCCL error): a shrinking sync
+    job recovers from it (parallel/elastic.py); otherwise it ends the rank."""
+
+
 class RoundWatchdog:
     def __init__(self, timeout_s: float, comm=None, name: str = "", poll_s: float = 0.5, on_expire=None,
                  hint: str = ""):
@@ -192,12 +197,18 @@ class WatchedRounds:
         ev.record()
         return ev
 
+    def _check_lost(self):
+        if getattr(self.t, "lost", False):
+            raise CommLost("the job communicator was aborted (liveness watchdog)")
+
     def fetch(self, worker_id, local_arena):
+        self._check_lost()
         # native transport: the broadcast is stream-ordered too (a fetch stuck on a dead
         # peer must not count as a finished round)
         return self._guard(self._fetch, worker_id, local_arena, event=self._native(),
                            label=f"fetch of round {getattr(self, '_gs', '?')} (broadcast from rank 0)")
 
     def push(self, worker_id, grads, local_step, buffers=None):
+        self._check_lost()
         return self._guard(self._push, worker_id, grads, local_step, buffers, event=self._native(),
                            label=f"push of round {local_step} (gradient gather / reduce to rank 0)")

@@ -43,7 +43,7 @@ class SyncCfg(C.Structure):
                 ("wire_buf", vp), ("wire_bytes", i64), ("wire_img", vp), ("small_idx", vp), ("small_n", i64),
                 ("wire_small", vp), ("nbuckets", i32), ("buckets", vp), ("full_wire", vp), ("full_wire_bytes", i64),
                 ("primed", i32), ("upd_stream", vp), ("comm_stream", vp), ("ckpt_every", C.c_longlong),
-                ("ckpt_cb", CKPT_CB)]
+                ("ckpt_cb", CKPT_CB), ("snap", vp), ("snap_mom", vp)]
 
 
 _SIGS = {
@@ -55,6 +55,8 @@ _SIGS = {
     "psx_sync_progress": (None, [vp, C.POINTER(C.c_longlong)]),
     "psx_sync_mom_first": (i32, [vp]),
     "psx_sync_primed": (i32, [vp]),
+    "psx_sync_abort": (C.c_longlong, [vp]),
+    "psx_sync_rollback": (C.c_longlong, [vp]),
     "psx_sync_destroy": (None, [vp]),
 }
 
@@ -94,8 +96,9 @@ def native_sync_enabled(cfg, transport, chan, server, rank: int) -> bool:
 class NativeSyncServer:
     """The dedicated server rank's side of a sync channel ``chan``, run natively."""
 
-    def __init__(self, server, transport, chan):
+    def __init__(self, server, transport, chan, elastic: bool = False):
         self.server, self.t, self.chan = server, transport, chan
+        self.gs0 = server.core.global_step  # the core's step when this loop took over
         cfg = server.cfg
         dev = server.device
         W = len(chan.members)
@@ -118,6 +121,12 @@ class NativeSyncServer:
                     upd_stream=torch.cuda.current_stream(dev).cuda_stream,
                     ckpt_every=int(cfg.ckpt_every or 0) if cfg.ckpt_dir else 0, ckpt_cb=self._ckpt)
         self.keep = []
+        if elastic:  # parallel/elastic.py: a snapshot of every in-flight round's starting state
+            self.snap = torch.empty(3 * server.arena.numel(), dtype=torch.float32, device=dev)
+            c.snap = self.snap.data_ptr()
+            if cfg.momentum and server.momentum_buf is not None:
+                self.snap_mom = torch.empty(3 * server.n, dtype=torch.float32, device=dev)
+                c.snap_mom = self.snap_mom.data_ptr()
         if overlap:
             wire = chan.wire
             bks = []
@@ -194,6 +203,23 @@ class NativeSyncServer:
             self.chan._have_buffers = True
         if rc:
             raise RuntimeError(f"native sync server failed ({rc})")
+
+    def abort(self) -> int:
+        """Liveness watchdog thread: freeze the good-round count, stop issuing, abort the
+        communicator (csrc/server/sync_loop.cpp psx_sync_abort)."""
+        return int(_lib().psx_sync_abort(self.h))
+
+    def rollback(self) -> int:
+        """After a failed / aborted run: the arena back at the start of the first round not known
+        good; the core's step rolled back to it. Returns the core's global step kept."""
+        g = int(_lib().psx_sync_rollback(self.h))
+        if g < 0:
+            raise RuntimeError(f"native sync rollback failed ({g})")
+        s = self.server
+        s._mom_first = bool(_lib().psx_sync_mom_first(self.h))
+        s.core.rollback_to(self.gs0 + g)
+        s._wire_stale = s.wire is not None  # the fetch image no longer matches the arena
+        return self.gs0 + g
 
     def close(self):
         if self.h:

@@ -31,6 +31,7 @@ from ..models.resnet import MODEL_INPUT, build_model
 from ..utils import metrics as M
 from ..utils.data import DeviceDataset, shard_range, steps_per_epoch
 from . import control as CP
+from . import elastic
 from .codec import FetchCodec, WeightWire, weight_image_enabled
 from .compute import make_compute
 from .graph_round import GraphRoundChannel, graph_round_enabled
@@ -199,6 +200,11 @@ def run_distributed(cfg, log=print) -> dict:
     # global steps are already done (sync: one round per step; async: spread over workers)
     done = t.broadcast_object(server.core.global_step if rank == 0 else None)
     t0 = time.time()
+    # sync job that survives a lost worker (parallel/elastic.py): a job-wide tag for its store keys
+    shrink_on = cfg.mode == "sync" and cfg.round_timeout > 0 and elastic.enabled(cfg, t, world)
+    ctx = {"t": t, "epoch": 0}
+    if shrink_on:
+        t.elastic_tag = t.broadcast_object(uuid.uuid4().hex[:12] if rank == 0 else None)
     if cfg.mode == "sync":
         if rank == 0:
             for r in worker_ranks:
@@ -208,17 +214,19 @@ def run_distributed(cfg, log=print) -> dict:
         else:
             chan = make_sync_channel(cfg, t, server, W, layout, device, worker=is_worker)
         chan._gs = done  # non-server ranks track the global step locally
-        if cfg.round_timeout > 0 and world > 1 and hasattr(chan, "watchdog"):
-            from .liveness import RoundWatchdog
-
-            chan.watchdog = RoundWatchdog(cfg.round_timeout, comm=getattr(t, "comm", None), name=f" rank {rank}")
+        _attach_watchdog(cfg, chan, t, shrink_on)
         if is_worker:
             wk = Worker(cfg, comp, chan, train, test, worker_name=names[rank], rank=rank, log=lg,
                         requested_id=wid_of_rank[rank], steps_per_epoch=steps)
             wk.connect_to_server()
+            if shrink_on:
+                wk.recover = lambda e: _worker_shrink(cfg, ctx, wk, layout, device, log)
             wk.run_training(skip_steps=done)
+            chan = wk.channel
         else:
-            _dedicated_sync_server(cfg, server, chan, steps, device, skip=done, t=t)
+            chan = _dedicated_sync_server(cfg, server, chan, steps, device, skip=done, t=t, ctx=ctx if shrink_on else None,
+                                          log=log)
+        t = ctx["t"]
     else:
         sess = AsyncSession(cfg, t, rank, worker_ranks, server, comp if is_worker else None, train, test, names, lg)
         sess.run_training(skip_steps=done // max(1, W))
@@ -350,13 +358,16 @@ class AsyncSession:
         return json.loads(st.get(key))
 
 
-def make_sync_channel(cfg, t, server, W, layout, device, worker: bool = True):
+def make_sync_channel(cfg, t, server, W, layout, device, worker: bool = True, members=None):
     """Sync-mode channel: bucketed + backward-overlapped when every batch is pushed; otherwise
-    the serial round, on the WeightWire fast path when it applies (parallel/codec.py)."""
+    the serial round, on the WeightWire fast path when it applies (parallel/codec.py).
+    ``members``: the worker ids of a round, in transport-rank order (default 0..W-1; a shrunk
+    job's survivors otherwise)."""
     codec = FetchCodec(layout, cfg.fetch_codec, device)
+    members = list(range(W)) if members is None else list(members)
     if cfg.overlap and max(1, cfg.sync_steps) == 1 and cfg.codec != "topk":
         buckets = plan_buckets(layout, int(cfg.bucket_mb * (1 << 20)) // 2)
-        return OverlapSyncChannel(t, server, members=list(range(W)), codec=codec, buckets=buckets, device=device,
+        return OverlapSyncChannel(t, server, members=members, codec=codec, buckets=buckets, device=device,
                                   root_worker=server is None or worker)
     wire = None
     if weight_image_enabled(cfg) and torch.device(device).type == "cuda":
@@ -369,7 +380,7 @@ def make_sync_channel(cfg, t, server, W, layout, device, worker: bool = True):
             return GraphRoundChannel(t, server, list(range(W)), codec, wire, buckets, device)
         if worker:  # rank 0's worker reads the server's wire in place (stream-ordered round)
             wire = server.wire if server is not None else WeightWire(layout, device)
-    return SyncCollectiveChannel(t, server, members=list(range(W)), codec=codec, wire=wire,
+    return SyncCollectiveChannel(t, server, members=members, codec=codec, wire=wire,
                                  root_worker=server is None or worker)
 
 
@@ -401,17 +412,97 @@ def _sync_rounds(cfg, steps, skip_b):
     return rounds
 
 
-def _dedicated_sync_server(cfg, server, chan, steps, device, skip=0, t=None):
+def _attach_watchdog(cfg, chan, t, shrink_on: bool, freeze=None):
+    """The round watchdog of a sync channel (--round-timeout): exit 3 for a launcher restart, or
+    (shrink) abort + recover in-process (parallel/elastic.py)."""
+    world = getattr(t, "world_size", 1)
+    if cfg.round_timeout > 0 and (world > 1 or getattr(t, "base", None) is not None) and hasattr(chan, "watchdog"):
+        from .liveness import RoundWatchdog
+
+        name = f" rank {getattr(t, 'orig_rank', getattr(t, 'rank', 0))}"
+        on_expire = elastic.make_on_stall(t, freeze=freeze) if shrink_on else None
+        chan.watchdog = RoundWatchdog(cfg.round_timeout, comm=getattr(t, "comm", None), name=name,
+                                      on_expire=on_expire)
+    return chan
+
+
+def _shrink_grace(cfg) -> float:
+    return cfg.recovery_grace if cfg.recovery_grace > 0 else cfg.round_timeout
+
+
+def _worker_shrink(cfg, ctx, wk, layout, device, log):
+    """A worker's side of a shrink (parallel/elastic.py): check in, build the survivors'
+    communicator, rebind to a new channel; returns the rounds the job keeps."""
+    old = ctx["t"]
+    wd = getattr(wk.channel, "watchdog", None)
+    if wd is not None:
+        wd.stop()
+    try:
+        torch.cuda.synchronize()  # the aborted collectives have run out
+    except Exception:  # noqa: BLE001
+        pass
+    ctx["epoch"] += 1
+    nt, rounds, dead = elastic.shrink(old, ctx["epoch"], _shrink_grace(cfg), log=log)
+    ctx["t"] = nt
+    chan = make_sync_channel(cfg, nt, None, nt.world_size - 1, layout, device, worker=True)
+    chan._gs = rounds
+    _attach_watchdog(cfg, chan, nt, True)
+    wk.rebind(chan)
+    return rounds
+
+
+def _dedicated_sync_server(cfg, server, chan, steps, device, skip=0, t=None, ctx=None, log=print):
     """Rank 0 of the dedicated topology: takes part in every round's collectives with a zero
     gradient contribution and applies the averaged update — all rounds in one native call
-    (parallel/native_sync.py) on the native transport, else per round in Python."""
+    (parallel/native_sync.py) on the native transport, else per round in Python. With ``ctx``
+    (sync shrink, parallel/elastic.py) a lost worker ends the current run: the arena goes back to
+    the last good round, the survivors rebuild the communicator and the rounds go on from there.
+    Returns the channel in use at the end."""
+    K = max(1, cfg.sync_steps)
+    from .native_sync import NativeSyncServer, native_sync_enabled
+
+    while True:
+        try:
+            _server_rounds(cfg, server, chan, steps, device, skip, t, ctx)
+            return chan
+        except Exception as e:  # noqa: BLE001 - only a lost communicator is recovered
+            if ctx is None or not elastic.lost_error(e):
+                raise
+            log(f"[psx elastic] server: {type(e).__name__}: {e}")
+            if chan.watchdog is not None:
+                chan.watchdog.stop()
+            kept = getattr(chan, "_rollback_gs", server.core.global_step)
+            ctx["epoch"] += 1
+            t, rounds, dead = elastic.shrink(ctx["t"], ctx["epoch"], _shrink_grace(cfg), rounds_kept=kept, log=log)
+            ctx["t"] = t
+            for r in dead:  # dedicated topology: worker id = original rank - 1
+                server.core.mark_dead(r - 1)
+            server.dropped_workers = sorted(set(getattr(server, "dropped_workers", None) or []) | {r - 1 for r in dead})
+            members = [r - 1 for r in t.members if r != 0]
+            chan = make_sync_channel(cfg, t, server, len(members), server.layout, device, worker=False,
+                                     members=members)
+            chan._gs = rounds
+            _attach_watchdog(cfg, chan, t, True)
+            skip = rounds
+
+
+def _server_rounds(cfg, server, chan, steps, device, skip, t, ctx):
+    """One run of the dedicated server's rounds from round ``skip`` on (see _dedicated_sync_server).
+    On a lost communicator (shrink) it records on ``chan._rollback_gs`` the global step it rolled
+    the arena back to, then re-raises."""
     K = max(1, cfg.sync_steps)
     from .native_sync import NativeSyncServer, native_sync_enabled
 
     if t is not None and native_sync_enabled(cfg, t, chan, server, getattr(t, "rank", 0)):
-        srv = NativeSyncServer(server, t, chan)
+        srv = NativeSyncServer(server, t, chan, elastic=ctx is not None)
+        if ctx is not None and chan.watchdog is not None:
+            chan.watchdog.on_expire = elastic.make_on_stall(t, freeze=srv.abort)
         try:
             srv.run(_sync_rounds(cfg, steps, rounds_to_batches(skip, steps, K)), watchdog=chan.watchdog)
+        except Exception:
+            if ctx is not None:
+                chan._rollback_gs = srv.rollback()
+            raise
         finally:
             srv.close()
         if hasattr(chan, "drain"):
@@ -426,25 +517,92 @@ def _dedicated_sync_server(cfg, server, chan, steps, device, skip=0, t=None):
     zbuf = torch.zeros(server.layout.buffer_numel, dtype=torch.float32, device=device) if cfg.bn_sync else None
     skip_b = rounds_to_batches(skip, steps, K)  # checkpointed rounds -> batches (window aligned)
     done = skip_b
-    for epoch in range(cfg.epochs):
-        for b in range(steps):
-            if epoch * steps + b < skip_b:
+    rb = _PyRollback(server, chan) if ctx is not None else None
+    try:
+        for epoch in range(cfg.epochs):
+            for b in range(steps):
+                if epoch * steps + b < skip_b:
+                    continue
+                if b % K == 0:
+                    if rb is not None:
+                        rb.round_start()
+                    chan.fetch(None, None)
+                    if cfg.codec != "topk":
+                        zeros.zero_()
+                    if zbuf is not None:
+                        zbuf.zero_()
+                    chan.push(None, zeros, server.core.global_step, buffers=zbuf)
+                    if rb is not None:
+                        rb.round_end()
+                done += 1
+                if cfg.max_steps and done >= cfg.max_steps:
+                    break
+            else:
                 continue
-            if b % K == 0:
-                chan.fetch(None, None)
-                if cfg.codec != "topk":
-                    zeros.zero_()
-                if zbuf is not None:
-                    zbuf.zero_()
-                chan.push(None, zeros, server.core.global_step, buffers=zbuf)
-            done += 1
-            if cfg.max_steps and done >= cfg.max_steps:
-                break
-        else:
-            continue
-        break
+            break
+    except Exception:
+        if rb is not None:
+            chan._rollback_gs = rb.rollback()
+        raise
     if hasattr(chan, "drain"):
         chan.drain()
+
+
+class _PyRollback:
+    """The Python server loop's side of a shrink (native: sync_loop.cpp snapshots): the arena (and
+    momentum) at every round start in one of three snapshot slots, a device event after every
+    round; the watchdog thread freezes the count of rounds whose event completed before it
+    aborted the communicator (``freeze``)."""
+
+    def __init__(self, server, chan):
+        self.s = server
+        self.snap = [torch.empty_like(server.arena) for _ in range(3)]
+        self.msnap = ([torch.empty_like(server.momentum_buf) for _ in range(3)]
+                      if server.momentum_buf is not None else None)
+        self.gs0 = server.core.global_step
+        self.mom_first0 = server._mom_first
+        self.issued = 0
+        self.events = []
+        self.frozen = None
+        if chan.watchdog is not None:
+            chan.watchdog.on_expire = elastic.make_on_stall(chan.t, freeze=self.freeze)
+
+    def round_start(self):
+        k = self.issued % 3
+        self.snap[k].copy_(self.s.arena)
+        if self.msnap is not None:
+            self.msnap[k].copy_(self.s.momentum_buf)
+
+    def round_end(self):
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events = (self.events + [(self.issued, ev)])[-4:]
+        self.issued += 1
+
+    def _completed(self) -> int:
+        g = self.issued - len(self.events)
+        for i, ev in self.events:
+            if not ev.query():
+                break
+            g = i + 1
+        return g
+
+    def freeze(self):
+        self.frozen = self._completed()
+
+    def rollback(self) -> int:
+        torch.cuda.synchronize()
+        g = self.frozen if self.frozen is not None else self.issued  # a failed round never ended
+        g = min(g, self.issued)
+        self.s.arena.copy_(self.snap[g % 3])
+        if self.msnap is not None:
+            self.s.momentum_buf.copy_(self.msnap[g % 3])
+        if g == 0:
+            self.s._mom_first = self.mom_first0
+        self.s.core.rollback_to(self.gs0 + g)
+        self.s._wire_stale = self.s.wire is not None
+        torch.cuda.synchronize()
+        return self.gs0 + g
 
 
 def run(cfg, log=print) -> dict:

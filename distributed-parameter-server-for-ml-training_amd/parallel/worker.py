@@ -397,82 +397,111 @@ class Worker:
         if torch.cuda.is_available() and getattr(self.compute, "device", torch.device("cpu")).type == "cuda":
             torch.cuda.synchronize()
 
+    recover = None  # sync shrink (parallel/elastic.py): hook(error) -> rounds to skip on the new channel
+
     def run_training(self, skip_steps: int = 0):
         """The reference training loop (worker.py:350-403). ``skip_steps`` = push rounds that a
         resumed server checkpoint already contains (restart recovery): the worker fast-forwards
         past the batches of those rounds (rounds_to_batches) and keeps each epoch's absolute batch
-        index, so the --sync-steps windows (fetch / push points) stay where they were."""
+        index, so the --sync-steps windows (fetch / push points) stay where they were. A shrinking
+        sync job (``recover`` set) re-enters the loop the same way at the round the survivors
+        resume from when the communicator is lost."""
         if self.sampler is None:
             self.setup_data()
         self.log(f"\n--- Starting distributed training for {self.num_epochs} epochs ---")
+        self.training_start_time = time.time()
+        try:
+            while True:
+                try:
+                    self._train_loop(skip_steps)
+                    break
+                except Exception as e:  # noqa: BLE001 - only a lost communicator is recovered
+                    from .elastic import lost_error
+
+                    if self.recover is None or not lost_error(e):
+                        raise
+                    self.log(f"[psx elastic] worker {self.worker_id}: {type(e).__name__}: {e}")
+                    skip_steps = self.recover(e)
+                    self.local_step_counter = 0
+        finally:
+            self._sync()
+            self.cleanup()
+            self.print_worker_statistics()
+
+    def rebind(self, channel):
+        """Continue on a new channel (sync shrink): same worker id and data shard."""
+        self.channel = channel
+        wid, tw = self.worker_id, self.total_workers
+        self.requested_id = wid
+        self.connect_to_server()
+        self.worker_id, self.total_workers = wid, tw
+
+    def _train_loop(self, skip_steps: int):
         K = self.local_steps_per_sync
         if skip_steps:
             rounds = skip_steps
             skip_steps = rounds_to_batches(rounds, len(self.sampler.epoch_indices(0)), K)
             self.log(f"[Resume] worker {self.worker_id} skips {rounds} completed rounds ({skip_steps} batches)")
-        self.training_start_time = time.time()
         fi_kind, fi_worker, fi_step, fi_secs = _parse_fault(self.cfg.fault_inject)
-        try:
-            for epoch in range(self.num_epochs):
-                self._sync()
-                t_ep = time.time()
-                batches = self.sampler.epoch_indices(epoch)
-                if skip_steps >= len(batches):
-                    skip_steps -= len(batches)
-                    self.local_step_counter += len(batches)
-                    continue
-                start = skip_steps
-                self.local_step_counter += start
-                skip_steps = 0
-                for batch_idx in range(start, len(batches)):
-                    idx = batches[batch_idx]
-                    if fi_worker == self.worker_id and self.local_step_counter == fi_step:
-                        if fi_kind == "hang_worker":  # alive but stalled: only a liveness guard notices
-                            import sys
+        for epoch in range(self.num_epochs):
+            self._sync()
+            t_ep = time.time()
+            batches = self.sampler.epoch_indices(epoch)
+            if skip_steps >= len(batches):
+                skip_steps -= len(batches)
+                self.local_step_counter += len(batches)
+                continue
+            start = skip_steps
+            self.local_step_counter += start
+            skip_steps = 0
+            for batch_idx in range(start, len(batches)):
+                idx = batches[batch_idx]
+                if fi_worker == self.worker_id and self.local_step_counter == fi_step:
+                    if fi_kind == "hang_worker":  # alive but stalled: only a liveness guard notices
+                        import sys
 
-                            print(f"fault injected: worker {self.worker_id} hangs at step {fi_step}"
-                                  + (f" for {fi_secs:g} s" if fi_secs else ""), file=sys.stderr, flush=True)
-                            t_end = time.time() + (fi_secs or float("inf"))
-                            while time.time() < t_end:
-                                time.sleep(min(3600.0, max(0.0, t_end - time.time())))
-                        elif fi_kind == "crash_in_push":  # the channel dies after posting this step's PUSH
-                            self.channel.crash_in_push = True
-                        elif self.cfg.mode == "async":
-                            # an async worker's process dies between requests: no JobFinished, its
-                            # heartbeats stop (the server's timeout drops it; sync mode raises
-                            # instead, for the launcher's restart path)
-                            import os
-                            import sys
+                        print(f"fault injected: worker {self.worker_id} hangs at step {fi_step}"
+                              + (f" for {fi_secs:g} s" if fi_secs else ""), file=sys.stderr, flush=True)
+                        t_end = time.time() + (fi_secs or float("inf"))
+                        while time.time() < t_end:
+                            time.sleep(min(3600.0, max(0.0, t_end - time.time())))
+                    elif fi_kind == "crash_in_push":  # the channel dies after posting this step's PUSH
+                        if not hasattr(type(self.channel), "crash_in_push"):
+                            raise ValueError(f"--fault-inject crash_in_push: {type(self.channel).__name__} "
+                                             "cannot inject it (the native async channel only)")
+                        self.channel.crash_in_push = True
+                    elif self.cfg.mode == "async" or self.recover is not None:
+                        # the worker's process dies between requests: no JobFinished; the async
+                        # server's heartbeat timeout drops it, a shrinking sync job goes on without
+                        # it (the restart path instead raises, for the launcher)
+                        import os
+                        import sys
 
-                            print(f"fault injected: worker {self.worker_id} process exits at step {fi_step}",
-                                  file=sys.stderr, flush=True)
-                            os._exit(17)
-                        else:
-                            raise _InjectedFault(f"fault injected: worker {self.worker_id} at step {fi_step}")
-                    if batch_idx % K == 0:
-                        with self.timer.span("fetch"):
-                            self.fetch_parameters()
-                    with self.timer.span("compute_issue"):
-                        self.train_local_batch(idx)
-                    self.window_push(batch_idx, len(batches), K)
-                    if self.cfg.verbose and batch_idx % 50 == 0:
-                        loss = self.compute.last_loss()
-                        self.losses.append(loss)
-                        self.log(f"  Worker {self.worker_id} epoch {epoch + 1} batch {batch_idx}/{len(batches)} "
-                                 f"loss {loss:.4f} elapsed {time.time() - t_ep:.1f}s")
-                    if self.cfg.max_steps and self.local_step_counter >= self.cfg.max_steps:
-                        break
-                self._sync()
-                self.epoch_times.append(time.time() - t_ep)
-                self.log(f"Epoch {epoch + 1} completed in {self.epoch_times[-1]:.2f}s")
-                if self.cfg.eval_every and (epoch + 1) % self.cfg.eval_every == 0:
-                    self.evaluate_model()
+                        print(f"fault injected: worker {self.worker_id} process exits at step {fi_step}",
+                              file=sys.stderr, flush=True)
+                        os._exit(17)
+                    else:
+                        raise _InjectedFault(f"fault injected: worker {self.worker_id} at step {fi_step}")
+                if batch_idx % K == 0:
+                    with self.timer.span("fetch"):
+                        self.fetch_parameters()
+                with self.timer.span("compute_issue"):
+                    self.train_local_batch(idx)
+                self.window_push(batch_idx, len(batches), K)
+                if self.cfg.verbose and batch_idx % 50 == 0:
+                    loss = self.compute.last_loss()
+                    self.losses.append(loss)
+                    self.log(f"  Worker {self.worker_id} epoch {epoch + 1} batch {batch_idx}/{len(batches)} "
+                             f"loss {loss:.4f} elapsed {time.time() - t_ep:.1f}s")
                 if self.cfg.max_steps and self.local_step_counter >= self.cfg.max_steps:
                     break
-        finally:
             self._sync()
-            self.cleanup()
-            self.print_worker_statistics()
+            self.epoch_times.append(time.time() - t_ep)
+            self.log(f"Epoch {epoch + 1} completed in {self.epoch_times[-1]:.2f}s")
+            if self.cfg.eval_every and (epoch + 1) % self.cfg.eval_every == 0:
+                self.evaluate_model()
+            if self.cfg.max_steps and self.local_step_counter >= self.cfg.max_steps:
+                break
 
     def print_worker_statistics(self):
         if self.training_start_time is None:

@@ -95,6 +95,11 @@ class PSConfig:
     transfer_timeout: float = 300.0  # async native loop: drop a worker whose transfer is in flight longer (0: off)
     stall_timeout: float = 0.0       # async native loop: drop a worker silent (no request) that long (0: off)
     round_timeout: float = 300.0   # sync liveness guard: abort + exit 3 when no round completes (0: off)
+    # sync, dedicated topology: what a lost worker does to the job. shrink: the survivors rebuild
+    # the communicator in-process and go on (parallel/elastic.py); restart: abort, exit 3, the
+    # launcher restarts the group from the last checkpoint
+    on_worker_loss: str = "shrink"
+    recovery_grace: float = 0.0    # s the server waits for survivors to check in (0: --round-timeout)
     verbose: int = 1
     extra: dict = field(default_factory=dict)
 
@@ -118,6 +123,8 @@ class PSConfig:
             raise ValueError("--sync-semantics must be barrier or reference")
         if self.staleness_bound < 0:
             raise ValueError("--staleness-bound must be >= 0")
+        if self.on_worker_loss not in ("shrink", "restart"):
+            raise ValueError("--on-worker-loss must be shrink or restart")
         if self.transfer_timeout < 0 or self.stall_timeout < 0:
             raise ValueError("--transfer-timeout / --stall-timeout must be >= 0")
         if self.dtype not in ("fp32", "bf16"):
@@ -136,6 +143,9 @@ class PSConfig:
             raise ValueError("--synthetic-kind must be proto or hard")
         if not (0.0 < self.topk_ratio <= 1.0):
             raise ValueError("--topk-ratio must be in (0, 1]")
+        if self.fault_inject.startswith("crash_in_push") and self.mode != "async":
+            # only the async native channel can die between its PUSH request and the transfer
+            raise ValueError("--fault-inject crash_in_push applies to --mode async (native event loop) only")
         return self
 
     def resolve_overlap(self, world: int) -> bool:
@@ -213,6 +223,11 @@ def add_arguments(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     A("--round-timeout", type=float, default=None,
       help="sync rounds: seconds without a completed round before the communicator is aborted and the rank "
            "exits (status 3) for a launcher restart from the last checkpoint; 0 disables")
+    A("--on-worker-loss", choices=["shrink", "restart"], default=None,
+      help="sync, dedicated topology: shrink (default) = the surviving ranks rebuild the communicator and "
+           "continue without the lost worker; restart = exit 3 for a launcher restart from the last checkpoint")
+    A("--recovery-grace", type=float, default=None,
+      help="shrink: seconds the server waits for the surviving ranks to check in (default: --round-timeout)")
     A("--verbose", type=int, default=None)
     return ap
 

@@ -1,0 +1,99 @@
+"""Sync mode survives a lost worker without a group restart (parallel/elastic.py).
+
+World 3, dedicated topology (rank 0 = the parameter server, ranks 1-2 = workers 0-1), on the
+test-only RCCL stand-in (csrc/tests/fakecomm.hip: RCCL refuses several ranks on one GPU). Worker
+0 fails at its step 3 — its process exits (kill_worker) or it stalls alive (hang_worker). The
+round watchdogs of the server and worker 1 fire after --round-timeout, abort the communicator,
+the server rolls its arena back to the last good round, the survivors agree on a plan through the
+rendezvous store and build a new communicator in-process, and worker 1 completes every one of its
+steps with the server alone. Both server implementations: the native sync loop
+(csrc/server/sync_loop.cpp) and the Python channel (PSX_NATIVE_SYNC=0). Ranks are plain processes
+(torchrun tears a group down when one rank exits)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FAKE = os.path.join(ROOT, "distributed-parameter-server-for-ml-training_amd", "_native", "testing",
+                    "libpsx_fakecomm.so")
+
+_RUN = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+import psx
+from psx.parallel.runner import run_distributed
+from psx.utils.config import PSConfig
+cfg = PSConfig(model="resnet18", batch_size=32, epochs=1, train_samples=1024, eval_every=0, verbose=1, lr=0.05,
+               max_steps=10, mode="sync", topology="dedicated", round_timeout=5.0, recovery_grace=6.0,
+               on_worker_loss="shrink", overlap={ov}, fault_inject={fi!r}).validate()
+res = run_distributed(cfg, log=lambda *a, **k: print(*a, **k, flush=True))
+if res.get("server"):
+    s = res["server"]
+    print("RESULT " + json.dumps({{"gs": s["global_steps_completed"], "dead": s["dead_workers"],
+                                   "dropped": s.get("dropped_workers", []), "sha": s["final_param_sha256"],
+                                   "updates": s["total_parameter_updates"]}}), flush=True)
+if res.get("worker"):
+    w = res["worker"]
+    print("WORKER " + json.dumps({{"id": w["worker_id"], "steps": w["local_steps_completed"]}}), flush=True)
+"""
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch(tmp_path, fault, native, overlap):
+    script = tmp_path / "run.py"
+    script.write_text(_RUN.format(root=ROOT, fi=fault, ov=overlap))
+    port = _port()
+    procs, logs = [], []
+    for r in range(3):
+        env = dict(os.environ, PYTHONPATH=ROOT, PSX_RCCL_LIB=FAKE, PSX_FAKECOMM_TEST="1", PSX_DIST_BACKEND="gloo",
+                   PSX_FAKECOMM_TIMEOUT_S="120", OMP_NUM_THREADS="4", PSX_NATIVE_SYNC=native, RANK=str(r),
+                   WORLD_SIZE="3", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.pop("CUDA_VISIBLE_DEVICES", None)
+        f = open(tmp_path / f"rank{r}.log", "w+")
+        logs.append(f)
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=f, stderr=subprocess.STDOUT))
+    try:
+        rc0 = procs[0].wait(timeout=300)
+        rc2 = procs[2].wait(timeout=60)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()  # the hung worker (or anything left over): our own child process
+                p.wait()
+    out = []
+    for f in logs:
+        f.seek(0)
+        out.append(f.read())
+        f.close()
+    return rc0, rc2, out
+
+
+def _records(text, key):
+    return [json.loads(ln[ln.index(key) + len(key):]) for ln in text.splitlines() if key in ln]
+
+
+@pytest.mark.parametrize("fault", ["kill_worker:0@3", "hang_worker:0@3"])
+@pytest.mark.parametrize("native,overlap", [("1", "False"), ("0", "False"), ("1", "True")])
+def test_sync_survives_lost_worker(fault, native, overlap, tmp_path):
+    rc0, rc2, out = _launch(tmp_path, fault, native, overlap)
+    assert rc0 == 0 and rc2 == 0, "\n---\n".join(o[-3000:] for o in out)
+    srv = _records(out[0], "RESULT ")
+    wk = _records(out[2], "WORKER ")
+    assert len(srv) == 1 and len(wk) == 1, out[0][-3000:]
+    s, w = srv[0], wk[0]
+    assert "[psx elastic" in out[0] and "continues as rank" in out[2], out[2][-3000:]
+    # worker 1 completed all its steps; the server applied exactly one round per step of it
+    assert w["id"] == 1 and w["steps"] == 10, w
+    assert s["gs"] == 10 and s["updates"] == 10, s
+    assert s["dead"] == 1 and s["dropped"] == [0], s

@@ -203,7 +203,8 @@ def test_distributed_sync_matches_loopback(world, topology, tmp_path):
 
 
 def test_native_hung_worker_watchdog_restart(tmp_path):
-    """Sync liveness guard on the native communicator (dedicated topology, world 3): worker 1
+    """Sync liveness guard, --on-worker-loss restart (the default, shrink, is tests/test_elastic_gpu.py)
+    on the native communicator (dedicated topology, world 3): worker 1
     stalls at its step 5 (alive); the other ranks' round watchdogs abort their communicators
     after --round-timeout and exit with status 3; torchrun restarts the group, the server resumes
     from its last checkpoint and the job completes with the fault-free number of rounds."""
@@ -214,7 +215,8 @@ def test_native_hung_worker_watchdog_restart(tmp_path):
            "--mode", "sync", "--topology", "dedicated", "--model", "resnet18", "--batch-size", "32",
            "--train-samples", "512", "--epochs", "2",
            "--eval-every", "0", "--ckpt-every", "2", "--ckpt-dir", str(ck), "--resume", "latest",
-           "--fault-inject", "hang_worker:1@5", "--round-timeout", "15", "--verbose", "1", "--log-dir", str(logs)]
+           "--fault-inject", "hang_worker:1@5", "--round-timeout", "15", "--on-worker-loss", "restart",
+           "--verbose", "1", "--log-dir", str(logs)]
     r = subprocess.run(cmd, env=_env({"PSX_FAKECOMM_TIMEOUT_S": "300"}), stdout=subprocess.PIPE,
                        stderr=subprocess.STDOUT, text=True, timeout=600)
     out = r.stdout

@@ -49,7 +49,7 @@ def _run(cmd):
 # per-source extra flags. wino_fused.hip: no SLP vectorization — packed f32 VALU (v_pk_add /
 # v_pk_fma) in the transform that runs beside the other wave's MFMAs measured slower (32x32x64
 # forward 52.2 -> 50.7 us without it; MI355X_MICROARCH.md: packed f32 beside MFMAs is an anti-lever)
-FILE_FLAGS = {"wino_fused.hip": ["-fno-slp-vectorize"], "wino_wgrad.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"wino_fused.hip": ["-fno-slp-vectorize"], "wino_wgrad.hip": ["-fno-slp-vectorize", "-ffp-contract=off"]}
 
 
 def build(jobs: int = 8, debug: bool = False, verbose: bool = False) -> dict:

@@ -48,8 +48,47 @@ struct WinoWgradArgs {
   int xbytes, ybytes;         // N H W C * 4, N H W K * 4 (< 2^30)
 };
 
+// PSX_WGF_PF = 1: the next tile group's 52 (BWD: 68) loads are issued before the current group's
+// transforms and MFMAs (one wave per SIMD: the accumulators move to AGPRs); 0 (default): load,
+// then compute, two waves per SIMD hiding each other's load latency. Same box, B = 128, us incl.
+// the output transform (bench/wino_wgrad_ab.py): 32x32x64 82.8 vs 58.4, 16x16x128 72.1 vs 55.3,
+// 8x8x256 73.2 vs 53.7, 4x4x512 85.8 vs 61.7 — one wave per SIMD cannot overlap its own
+// transforms with its MFMAs.
+#ifndef PSX_WGF_PF
+#define PSX_WGF_PF 0
+#endif
+
+// one axis of B^T d with explicit FMAs (the file is built without FP contraction, so every
+// template instance rounds identically: the folded and unfolded paths give the same bits)
+PSX_DEV void bt6f(const float (&d)[6], float (&r)[6]) {
+  r[0] = fmaf(4.f, d[0], fmaf(-5.f, d[2], d[4]));
+  r[1] = fmaf(-4.f, d[1] + d[2], d[3] + d[4]);
+  r[2] = fmaf(4.f, d[1] - d[2], d[4] - d[3]);
+  r[3] = fmaf(2.f, d[3] - d[1], d[4] - d[2]);
+  r[4] = fmaf(2.f, d[1] - d[3], d[4] - d[2]);
+  r[5] = fmaf(4.f, d[1], fmaf(-5.f, d[3], d[5]));
+}
+
+PSX_DEV void a4f(const float (&y)[4], float (&r)[6]) {
+  const float e = y[0] + y[2], o = y[1] + y[3], e4 = fmaf(4.f, y[2], y[0]), o2 = fmaf(8.f, y[3], 2.f * y[1]);
+  r[0] = y[0];
+  r[1] = e + o;
+  r[2] = e - o;
+  r[3] = e4 + o2;
+  r[4] = e4 - o2;
+  r[5] = y[3];
+}
+
+template <bool BWD>
+struct WgfRaw {  // one tile group's loads, per lane (its tile, its channel)
+  float x[6][6];
+  float y[4][4];
+  float yb[BWD ? 4 : 1][BWD ? 4 : 1];
+  bool r0, r5, c0, c5;  // the patch's first / last row / column inside the image
+};
+
 template <bool AFF, bool BWD>
-__global__ __launch_bounds__(256, 2) void wino_wgrad_fused_kernel(WinoWgradArgs a) {
+__global__ __launch_bounds__(256, PSX_WGF_PF ? 1 : 2) void wino_wgrad_fused_kernel(WinoWgradArgs a) {
   __shared__ float red[4][9][256];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nkb = a.K >> 4, nblk = nkb * (a.C >> 4);
@@ -85,68 +124,75 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_fused_kernel(WinoWgradArgs 
   const auto yr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.ybn), 0, BWD ? a.ybytes : 0, 0x00020000);
   constexpr unsigned kBad = 0x40000000u;  // > any tensor's bytes; kBad + kBad + offset still > them
   const unsigned rowb = (unsigned)W * C * 4, colb = (unsigned)C * 4;
-
   const int t0 = range * a.tpr;
-  for (int g = wv * 4; g < a.tpr; g += 16) {
+
+  auto load = [&](int g, WgfRaw<BWD>& R) {
     const int t = t0 + g + tl;
     const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
     // x patch (6x6 at (4 ti - 1, 4 tj - 1), zero padded) of channel c: only rows / columns 0 and
     // 5 can fall outside the image
     const int h0 = 4 * ti - 1, w0 = 4 * tj - 1;
-    const bool r0 = h0 >= 0, r5 = h0 + 5 < H, c0 = w0 >= 0, c5 = w0 + 5 < W;
+    R.r0 = h0 >= 0;
+    R.r5 = h0 + 5 < H;
+    R.c0 = w0 >= 0;
+    R.c5 = w0 + 5 < W;
     unsigned ro[6], co[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
-      const bool oh = i == 0 ? r0 : (i == 5 ? r5 : true), ow = i == 0 ? c0 : (i == 5 ? c5 : true);
+      const bool oh = i == 0 ? R.r0 : (i == 5 ? R.r5 : true), ow = i == 0 ? R.c0 : (i == 5 ? R.c5 : true);
       ro[i] = oh ? (unsigned)(n * H + h0 + i) * rowb + (unsigned)c * 4 : kBad;
       co[i] = ow ? (unsigned)(w0 + i) * colb : kBad;
     }
-    float d[6][6];
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ro[i] + co[j], 0, 0));
-        if constexpr (AFF) {  // zero padding stays zero after BN + ReLU (border elements only)
-          // the same expression (and contraction) as the BN apply / the forward's folded load, so
-          // the operand is bit-identical to the activation the unfolded path writes
-          const float e = fmaxf(v * sc + sh, 0.f);
-          const bool oh = i == 0 ? r0 : (i == 5 ? r5 : true), ow = j == 0 ? c0 : (j == 5 ? c5 : true);
-          d[i][j] = (oh && ow) ? e : 0.f;
-        } else {
-          d[i][j] = v;
-        }
-      }
+      for (int j = 0; j < 6; ++j)
+        R.x[i][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, ro[i] + co[j], 0, 0));
     // dy tile (4x4 at (4 ti, 4 tj)) of channel k
-    float y[4][4];
     const unsigned yo = (unsigned)(((n * H + 4 * ti) * W + 4 * tj) * K + k) * 4;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int so = (i * W + j) * K * 4;  // wave-uniform
-        const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(dr_, yo, so, 0));
-        if constexpr (BWD)
-          y[i][j] = wino_bwd_apply(v, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yr, yo, so, 0)), k1, k2,
-                                   k3);
-        else
-          y[i][j] = v;
+        R.y[i][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(dr_, yo, so, 0));
+        if constexpr (BWD) R.yb[i][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yr, yo, so, 0));
       }
+  };
+
+  auto compute = [&](const WgfRaw<BWD>& R) {
     // column transforms: tb[r][j] = (B^T d)[r][j], u[r][j] = (A y)[r][j]
     float tb[6][6], u[6][4];
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-      const float col[6] = {d[0][j], d[1][j], d[2][j], d[3][j], d[4][j], d[5][j]};
-      float o[6];
-      wino_bt6(col, o);
+      float col[6], o[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        float v = R.x[i][j];
+        if constexpr (AFF) {  // zero padding stays zero after BN + ReLU (border elements only);
+          // fmaf = the BN apply's contracted y * scale + shift: the operand is bit-identical to
+          // the activation the unfolded path writes
+          const float e = fmaxf(fmaf(v, sc, sh), 0.f);
+          const bool oh = i == 0 ? R.r0 : (i == 5 ? R.r5 : true), ow = j == 0 ? R.c0 : (j == 5 ? R.c5 : true);
+          v = (oh && ow) ? e : 0.f;
+        }
+        col[i] = v;
+      }
+      bt6f(col, o);
 #pragma unroll
       for (int r = 0; r < 6; ++r) tb[r][j] = o[r];
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float col[4] = {y[0][j], y[1][j], y[2][j], y[3][j]};
-      float o[6];
-      wino_a4(col, o);
+      float col[4], o[6];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (BWD)
+          col[i] = wino_bwd_apply(R.y[i][j], R.yb[i][j], k1, k2, k3);
+        else
+          col[i] = R.y[i][j];
+      }
+      a4f(col, o);
 #pragma unroll
       for (int r = 0; r < 6; ++r) u[r][j] = o[r];
     }
@@ -154,13 +200,32 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_fused_kernel(WinoWgradArgs 
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
       float vr[6], dr[6];
-      wino_bt6(tb[r], vr);
-      wino_a4(u[r], dr);
+      bt6f(tb[r], vr);
+      a4f(u[r], dr);
 #pragma unroll
       for (int s = 0; s < 6; ++s)
         acc[r * 6 + s] = __builtin_amdgcn_mfma_f32_16x16x4f32(dr[s], vr[s], acc[r * 6 + s], 0, 0, 0);
     }
+  };
+
+#if PSX_WGF_PF
+  WgfRaw<BWD> cur;
+  int g = wv * 4;
+  if (g < a.tpr) load(g, cur);
+  for (; g < a.tpr; g += 16) {
+    WgfRaw<BWD> nxt;
+    const bool more = g + 16 < a.tpr;
+    if (more) load(g + 16, nxt);
+    compute(cur);
+    if (more) cur = nxt;  // register moves (a two-set ping-pong unrolled into spills)
   }
+#else#else
+  for (int g = wv * 4; g < a.tpr; g += 16) {
+    WgfRaw<BWD> cur;
+    load(g, cur);
+    compute(cur);
+  }
+#endif
 
   // the four waves' partial sums, 9 points at a time, added in wave order; lane l holds
   // M[b][k = 4 (l >> 4) + j][c = l & 15] in acc[b][j]

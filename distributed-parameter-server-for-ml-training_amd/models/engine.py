@@ -419,7 +419,14 @@ class HipResNetEngine:
         if not self.f32 or os.environ.get("PSX_WINO", "1") == "0":
             return
         fuse = os.environ.get("PSX_WINO_FUSE", "1") == "1"
+        # fused weight gradient (wino_wgrad.hip) on images of at least PSX_WINO_WGF_MINHW: same box,
+        # B = 128, us incl. output transform, fused vs three-launch (bench/wino_wgrad_ab.py,
+        # profiles/r4_wino_wgrad_ab.jsonl): 32x32x64 58.4 vs 71.2, 16x16x128 55.3 vs 46.9 (+ the
+        # forward's V store the three-launch path needs, ~7), 8x8x256 53.7 vs 43.2, 4x4x512 61.7 vs
+        # 44.1. In the step (side stream; the forward's V store is on the critical path) same box:
+        # off 3.568, >= 32 3.412, >= 16 3.363-3.372 ms/step (profiles/r4_numbers.jsonl)
         wgf = os.environ.get("PSX_WINO_WGF", "1") == "1"
+        wgf_minhw = int(os.environ.get("PSX_WINO_WGF_MINHW", "16"))
         maxhw = int(os.environ.get("PSX_WINO_MAXHW", "64"))
         wg = os.environ.get("PSX_WINO_WGRAD", "1") == "1"
         wg_maxhw = int(os.environ.get("PSX_WINO_WGRAD_MAXHW", "32"))
@@ -440,7 +447,8 @@ class HipResNetEngine:
             ud = self._f32((40 if fd else 36) * cs.cout * cs.cp) if cs.need_dgrad else None
             # fused weight gradient (wino_wgrad.hip, PSX_WINO_WGF=1): transforms x and dy itself, so
             # the forward keeps no V and no D is formed
-            qf = K.wino_wgrad_fused_q(B, cs.h, cs.w, cs.cp, cs.cout) if q > 0 and wgf else 0
+            qf = (K.wino_wgrad_fused_q(B, cs.h, cs.w, cs.cp, cs.cout)
+                  if q > 0 and wgf and min(cs.h, cs.w) >= wgf_minhw else 0)
             v = self._f32(vc) if q > 0 and not qf else None  # None: the forward's V goes to scratch
             self.wino_layers[cs.name] = (uf, ud, v)
             if q > 0:

@@ -245,8 +245,14 @@ def test_augment_and_maxpool_f32():
     assert torch.equal(y, F.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1))
 
 
-# per-tensor / median bars of the whole-step test, by conv path (see the test's comment)
-STEP_BARS = {"1": (2e-2, 8e-3), "0": (1e-2, 4e-3)}
+# Bars of the whole-step test RELATIVE to torch's own fp32 autograd error against the same fp64
+# reference: per tensor err <= max(STEP_K * err32, STEP_FLOOR), and the
+# median over tensors <= max(STEP_MED_K * median(err32), STEP_MED_FLOOR). Measured (round 4,
+# both conv paths): engine worst 2.6e-3 / median 1.5e-3 against torch-fp32 0.7-4.5e-3 per tensor
+# (median ~1.5e-3; MIOpen's algorithm choice moves it run to run, hence the floors). A 3x
+# regression of the engine's error fails the median bar.
+STEP_K, STEP_FLOOR = 3.0, 4e-3
+STEP_MED_K, STEP_MED_FLOOR = 2.0, 2.5e-3
 
 
 @pytest.mark.parametrize("wino", ["1", "0"])
@@ -302,13 +308,14 @@ def test_engine_step_f32_matches_torch_fp64(wino, monkeypatch):
     # conv1.weight 3.1e-3 in one run, 8.4e-4 in the next). The engine runs deterministic, but the
     # amplified value still depends on the association of its reductions: with Winograd (~3e-6
     # forward rounding per layer, 15x direct fp32's) two reduction trees measured median 3.9e-3 /
-    # 7e-3, worst 6.6e-3 / 1.1e-2. Bars (STEP_BARS): per tensor and median by conv path, the head
-    # (no BN amplification) tight.
-    worst, median = STEP_BARS[wino]
+    # 7e-3, worst 6.6e-3 / 1.1e-2 (round 3; the fused Winograd weight gradient of round 4 measures
+    # median 1.5e-3, worst 2.6e-3). Bars: relative to torch-fp32's own error (STEP_K, STEP_MED_K
+    # above), the head (no BN amplification) tight.
     for name, err, err32 in rows:
-        assert err < worst, (name, err, err32)
-    errs = sorted(r[1] for r in rows)
-    assert errs[len(errs) // 2] < median, errs
+        assert err <= max(STEP_K * err32, STEP_FLOOR), (name, err, err32)
+    errs, errs32 = sorted(r[1] for r in rows), sorted(r[2] for r in rows)
+    med, med32 = errs[len(errs) // 2], errs32[len(errs32) // 2]
+    assert med <= max(STEP_MED_K * med32, STEP_MED_FLOOR), (med, med32)
     assert dict((r[0], r[1]) for r in rows)["fc.weight"] < 1e-5
     sd = ref.state_dict()
     for name in ("bn1.running_mean", "layer2.0.bn1.running_var", "layer4.1.bn2.running_mean"):

@@ -981,7 +981,11 @@ struct Plan {
 // twice the k-steps of a bf16 layer.
 Plan plan_for(int OC, int npix, int ksteps, bool f32 = false) {
   Plan p{64, 128, 1};
-  if (!f32 && OC % 128 == 0 && (long)(OC / 128) * ((npix + 127) / 128) >= 512) {
+  static const bool f32_128 = [] {
+    const char* e = getenv("PSX_CV_F32_128");
+    return e && e[0] == '1';
+  }();
+  if ((!f32 || f32_128) && OC % 128 == 0 && (long)(OC / 128) * ((npix + 127) / 128) >= (f32 ? 256 : 512)) {
     p.BM = 128;
     p.BN = 128;
   } else if ((long)(OC / 64) * ((npix + 127) / 128) >= 512) {
@@ -998,7 +1002,11 @@ Plan plan_for(int OC, int npix, int ksteps, bool f32 = false) {
   if (const char* e = getenv("PSX_CV_BN")) p.BN = atoi(e);
   if (const char* e = getenv("PSX_CV_SPLITS")) p.splits = atoi(e);
   if (const char* e = getenv("PSX_CV_WGM")) p.WGM = atoi(e);
-  if (OC % p.BM || (f32 && p.BM == 128)) p.BM = 64;
+  static const bool f32_128 = [] {  // fp32 128 x 128 tiles: opt-in while measured (bench/f32_tiles.py)
+    const char* e = getenv("PSX_CV_F32_128");
+    return e && e[0] == '1';
+  }();
+  if (OC % p.BM || (f32 && p.BM == 128 && !f32_128 && !getenv("PSX_CV_BM"))) p.BM = 64;
   if (p.splits > ksteps) p.splits = ksteps;
   return p;
 }
@@ -1024,10 +1032,8 @@ int dispatch2(const Plan& p, const Conv2Args& a, hipStream_t st) {
 #define PSX_L2(BM_, BN_, W_)                                                                             \
   if (p.BM == BM_ && p.BN == BN_ && p.WGM == W_)                                                         \
     return sp ? launch2<T, BM_, BN_, MODE, false, true, W_>(a, st) : launch2<T, BM_, BN_, MODE, RES, false, W_>(a, st);
-  if constexpr (sizeof(T) == 2) {
-    PSX_L2(128, 128, 2)
-    PSX_L2(128, 256, 2)
-  }
+  PSX_L2(128, 128, 2)
+  if constexpr (sizeof(T) == 2) PSX_L2(128, 256, 2)
   PSX_L2(64, 128, 2)
   PSX_L2(64, 64, 2)
   PSX_L2(64, 256, 1)
@@ -1328,6 +1334,7 @@ int psx_bgemm_f32(const float* A, const float* B, float* P, const void* zero, in
   if (cfg == 1) p.BN = 128;
   if (cfg == 2) { p.BN = 256; p.WGM = 1; }
   if (cfg == 3) { p.BN = 128; p.WGM = 1; }
+  if (cfg == 4) { p.BM = 128; p.BN = 128; }
   Conv2Args a{};
   a.in = A;
   a.w = B;

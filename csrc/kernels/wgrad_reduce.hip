@@ -19,13 +19,38 @@ namespace psx {
 // channel padding and emit the gradient straight into the wire buffer (fp16 codec or fp32).
 // Block = 4 waves; each lane owns 4 consecutive partial columns (16-byte loads), the waves split
 // the split-K slabs 4 ways (fixed order => deterministic) and combine through LDS.
+// Pre-pass of a small layer with many splits (the stem: 64 x 64 columns = 16 workgroups of the
+// final reduce over 256 slabs, latency-bound at ~70 us): workgroup (column block, slab group)
+// sums the kPre slabs of its group in fixed order and stores the sum over the group's FIRST slab,
+// which no other workgroup reads; the final reduce then walks every kPre-th slab.
+constexpr int kPre = 16;
+
+__global__ __launch_bounds__(256) void wgrad_presum_kernel(float* __restrict__ part, int splits, size_t slab) {
+  __shared__ f32x4 red[4][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const size_t base = (size_t)blockIdx.x * 256 + lane * 4;
+  const int s0 = blockIdx.y * kPre;
+  f32x4 acc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int sp = s0 + g + 4 * u;
+    acc[u] = sp < splits ? *reinterpret_cast<const f32x4*>(part + (size_t)sp * slab + base)
+                         : (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  red[g][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  if (g != 0) return;
+  *reinterpret_cast<f32x4*>(part + (size_t)s0 * slab + base) =
+      (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
 template <typename OutT>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int OC,
                                                            int Kg, int Cin, int IC, int R, int S, float scale,
-                                                           OutT* __restrict__ out) {
+                                                           OutT* __restrict__ out, int sstride) {
   __shared__ f32x4 red[4][64];
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const size_t slab = (size_t)OC * Kg;
+  const size_t slab = (size_t)OC * Kg * sstride;  // every sstride-th slab (after the pre-pass)
   const size_t base = (size_t)blockIdx.x * 256 + lane * 4;
   // the 4 waves split the slabs 4 ways; 8 independent 16-byte loads in flight per lane (the
   // reduce is bandwidth work, and with as few as 144 workgroups for a 64x576 layer it is
@@ -230,12 +255,21 @@ int psx_wgrad_reduce(const float* part, int splits, int OC, int Kg, int Cin, int
   }
   if (((long)OC * Kg) % 256) return -2;
   const int grid = (int)(((long)OC * Kg) / 256);
+  int sstride = 1;
+  if (grid < 128 && splits > 2 * kPre && !getenv("PSX_WGRAD_NO_PRESUM")) {
+    // few columns, many slabs: spread the slab sum over grid x splits/kPre workgroups first
+    const int groups = (splits + kPre - 1) / kPre;
+    hipLaunchKernelGGL(wgrad_presum_kernel, dim3(grid, groups), dim3(256), 0, st, const_cast<float*>(part), splits,
+                       (size_t)OC * Kg);
+    splits = groups;
+    sstride = kPre;
+  }
   if (out_fp16)
     hipLaunchKernelGGL(wgrad_reduce_kernel<uint16_t>, dim3(grid), dim3(256), 0, st, part, splits, OC, Kg, Cin, IC,
-                       R, S, scale, (uint16_t*)out);
+                       R, S, scale, (uint16_t*)out, sstride);
   else
     hipLaunchKernelGGL(wgrad_reduce_kernel<float>, dim3(grid), dim3(256), 0, st, part, splits, OC, Kg, Cin, IC, R,
-                       S, scale, (float*)out);
+                       S, scale, (float*)out, sstride);
   return (int)hipGetLastError();
 }
 

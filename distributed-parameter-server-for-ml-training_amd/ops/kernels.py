@@ -315,6 +315,9 @@ def conv_wgrad2(x, dy, part, nb, h, w, ic, oc, k, stride, pad, kg) -> int:
 
 
 def wgrad_reduce(part, splits, oc, kg, cin, ic, k, scale, out_ptr: int, out_fp16: bool):
+    """Reduce the split slabs into the OIHW gradient. CONSUMES ``part``: a layer with few
+    columns and many splits (the stem) is pre-summed in place (csrc/kernels/wgrad_reduce.hip
+    wgrad_presum_kernel), so reduce a given set of partials once."""
     check(kernels().psx_wgrad_reduce(ptr(part), splits, oc, kg, cin, ic, k, k, float(scale), out_ptr, int(out_fp16),
                                      stream_ptr()), "wgrad_reduce")
 

@@ -164,7 +164,10 @@ class NativeServerLoop:
                 self.t.p2p(r)[0].h = None
         self.server.dropped_workers = sorted(w for w, _ in self.dropped)
         s = self.server
-        s._mom_first = s._mom_first and not int(_lib().psx_loop_applies(self.h))
+        applies = int(_lib().psx_loop_applies(self.h))
+        s._mom_first = s._mom_first and not applies
+        if applies:  # the loop fed each apply's device time to the core (event_loop.cpp read_timings)
+            s.update_time_source = "device events around the apply kernels (native loop)"
         s.bytes_pushed = int(s.core.metrics().get("gradients_processed", 0)) * s.n * (2 if s.cfg.codec == "fp16" else 4)
         _lib().psx_loop_destroy(self.h)
         self.h = None

@@ -195,6 +195,7 @@ class NativeSyncServer:
                 watchdog.follow(None)
         s, W = self.server, len(self.chan.members)
         s._mom_first = bool(_lib().psx_sync_mom_first(self.h))
+        s.update_time_source = "device events around the apply kernels (native sync loop)"
         s.bytes_pushed += rounds * W * s.n * (2 if s.cfg.codec == "fp16" else 4)
         s.bytes_fetched += rounds * self.wire_bytes * max(0, W - 1)
         if self.overlap:

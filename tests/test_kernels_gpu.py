@@ -84,10 +84,11 @@ def test_conv_wgrad(shape):
     got = K.conv_wgrad2(to_nhwc(x, cp), to_nhwc(dy, cout), part, n, hw, hw, cp, cout, k, s, p, kg)
     assert got == splits
     out = torch.zeros(cout * cin * k * k, device=DEV)
+    part2 = part.clone()  # the reduce consumes its partials (in-place pre-sum of many-split layers)
     K.wgrad_reduce(part, splits, cout, kg, cin, cp, k, 1.0, out.data_ptr(), False)
     assert _rel(out.view_as(ref), ref) < 5e-3, shape
     out16 = torch.zeros(cout * cin * k * k, dtype=torch.float16, device=DEV)
-    K.wgrad_reduce(part, splits, cout, kg, cin, cp, k, 0.5, out16.data_ptr(), True)
+    K.wgrad_reduce(part2, splits, cout, kg, cin, cp, k, 0.5, out16.data_ptr(), True)
     assert _rel(out16.view_as(ref).float(), 0.5 * ref) < 5e-3, shape
 
 

@@ -981,7 +981,7 @@ struct Plan {
 // twice the k-steps of a bf16 layer.
 Plan plan_for(int OC, int npix, int ksteps, bool f32 = false) {
   Plan p{64, 128, 1};
-  static const bool f32_128 = [] {
+  static const bool f32_128 = [] {  // fp32 128 x 128 tiles: opt-in while measured (bench/f32_tiles.py)
     const char* e = getenv("PSX_CV_F32_128");
     return e && e[0] == '1';
   }();
@@ -1002,10 +1002,6 @@ Plan plan_for(int OC, int npix, int ksteps, bool f32 = false) {
   if (const char* e = getenv("PSX_CV_BN")) p.BN = atoi(e);
   if (const char* e = getenv("PSX_CV_SPLITS")) p.splits = atoi(e);
   if (const char* e = getenv("PSX_CV_WGM")) p.WGM = atoi(e);
-  static const bool f32_128 = [] {  // fp32 128 x 128 tiles: opt-in while measured (bench/f32_tiles.py)
-    const char* e = getenv("PSX_CV_F32_128");
-    return e && e[0] == '1';
-  }();
   if (OC % p.BM || (f32 && p.BM == 128 && !f32_128 && !getenv("PSX_CV_BM"))) p.BM = 64;
   if (p.splits > ksteps) p.splits = ksteps;
   return p;

@@ -1,6 +1,6 @@
 """fp32 batched-GEMM throughput of the Winograd layers (the 36 per-point GEMMs of ResNet-18's
 8x8x256 / 4x4x512 layers and ResNet-50's 3x3 stages at B=128): psx's conv_v2 mainloop (every
-tile config), the dedicated Winograd GEMM (csrc/kernels/wino_gemm.hip, when built) and torch.bmm
+tile config), the stream-K Winograd GEMM (csrc/kernels/wino_gemm.hip) and torch.bmm
 (hipBLASLt / rocBLAS fp32) on the same operands. One JSON line per shape: microseconds and TFLOP/s.
 
   python bench/bgemm_f32.py
@@ -45,7 +45,7 @@ def main():
         ref = torch.bmm(a, b.permute(1, 2, 0))
         fl = 2.0 * nb * m * n * kd
         r = {"m": m, "n": n, "kd": kd, "nb": nb}
-        for cfg in range(5):
+        for cfg in range(4):
             try:
                 K.bgemm_f32(a, b, p, m, n, kd, nb, cfg)
                 torch.cuda.synchronize()
@@ -54,16 +54,17 @@ def main():
                 r[f"cfg{cfg}"] = [round(us, 1), round(fl / us / 1e6, 1), f"{err:.1e}"]
             except Exception as e:  # noqa: BLE001
                 r[f"cfg{cfg}"] = str(e)[:60]
-        if hasattr(K, "wino_gemm_f32"):
-            for bm, bn in ((128, 128), (128, 64), (64, 128), (64, 64)):
-                try:
-                    K.wino_gemm_f32(a, b, p, m, n, kd, nb, bm, bn)
-                    torch.cuda.synchronize()
-                    err = ((p - ref).abs().max() / ref.abs().max()).item()
-                    us = t_us(lambda: K.wino_gemm_f32(a, b, p, m, n, kd, nb, bm, bn))
-                    r[f"wg{bm}x{bn}"] = [round(us, 1), round(fl / us / 1e6, 1), f"{err:.1e}"]
-                except Exception as e:  # noqa: BLE001
-                    r[f"wg{bm}x{bn}"] = str(e)[:60]
+        # stream-K (wino_gemm.hip): a [nb][m][kd], b [n][nb][kd] (rows nb * kd apart), c [nb][m][n]
+        for bn in (0, 128, 64):
+            p.fill_(float("nan"))
+            rc = K.sk_gemm_nt(a, b, p, m, n, kd, nb, (kd, m * kd), (nb * kd, kd), (n, m * n), bn=bn)
+            if rc:
+                r[f"sk{bn}"] = f"rc {rc}"
+                continue
+            torch.cuda.synchronize()
+            err = ((p - ref).abs().max() / ref.abs().max()).item()
+            us = t_us(lambda: K.sk_gemm_nt(a, b, p, m, n, kd, nb, (kd, m * kd), (nb * kd, kd), (n, m * n), bn=bn))
+            r[f"sk{bn}"] = [round(us, 1), round(fl / us / 1e6, 1), f"{err:.1e}"]
         bt = b.permute(1, 2, 0).contiguous()
         us = t_us(lambda: torch.bmm(a, bt, out=p))
         r["torch_bmm"] = [round(us, 1), round(fl / us / 1e6, 1)]

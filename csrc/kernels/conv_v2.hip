@@ -1330,7 +1330,6 @@ int psx_bgemm_f32(const float* A, const float* B, float* P, const void* zero, in
   if (cfg == 1) p.BN = 128;
   if (cfg == 2) { p.BN = 256; p.WGM = 1; }
   if (cfg == 3) { p.BN = 128; p.WGM = 1; }
-  if (cfg == 4) { p.BM = 128; p.BN = 128; }
   Conv2Args a{};
   a.in = A;
   a.w = B;

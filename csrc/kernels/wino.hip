@@ -43,6 +43,9 @@ extern "C" int psx_wino_gemm_out(const float* V, const float* U, float* y, const
                                  int K, const float* sshift, int bm, hipStream_t st);
 extern "C" int psx_wino_wout(const float* part, void* out, int out_fp16, float scale, int K, int C, int q,
                              hipStream_t st);
+extern "C" int psx_sk_gemm_nt(const float* A, const float* B, float* C, long sa_row, long sa_b, long sb_row,
+                              long sb_b, long sc_row, long sc_b, int M, int N, int Kd, int nb, const void* zero, int bn,
+                              hipStream_t st);
 extern "C" int psx_bgemm_tn_f32(const float* X, const float* D, float* part, const void* zero, int T, int C, int K,
                                 int nb, int q, int BR, int BC, hipStream_t st);
 
@@ -904,7 +907,17 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
                                sshift, bm, st);
     }
   }
-  int e = psx_bgemm_f32(V, U, P, zero, T, K, C, 36, cfg, st);
+  // the 36 GEMMs: stream-K (wino_gemm.hip) where the tiled launch cannot fill the chip in
+  // balanced rounds (C >= 256: ResNet-18's 8x8 / 4x4 stages), else the conv_v2 mainloop.
+  // PSX_WINO_SK=0 keeps the tiled path; a process without the registered workspace (-5) too.
+  static const int sk_mode = [] {
+    const char* e = getenv("PSX_WINO_SK");
+    return e ? atoi(e) : 1;
+  }();
+  int e = -5;
+  if (sk_mode && (C >= 256 || sk_mode == 2))
+    e = psx_sk_gemm_nt(V, U, P, C, (long)T * C, 36L * C, C, K, (long)T * K, T, K, C, 36, zero, 0, st);
+  if (e) e = psx_bgemm_f32(V, U, P, zero, T, K, C, 36, cfg, st);
   if (e) return e;
   WinoBwdStats bs{};
   if (bst) bs = *bst;

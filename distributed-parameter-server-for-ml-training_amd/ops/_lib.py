@@ -49,6 +49,9 @@ _KERNEL_SIGS = {
                             vp]),
     "psx_conv_dgrad2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp]),
     "psx_bgemm_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
+    "psx_sk_set_workspace": (i32, [vp, i64, vp, i32]),
+    "psx_sk_workspace_floats": (i64, []),
+    "psx_sk_gemm_nt": (i32, [vp, vp, vp, i64, i64, i64, i64, i64, i64, i32, i32, i32, i32, vp, i32, vp]),
     "psx_wino_workspace": (i64, [i32, i32, i32, i32, i32]),
     "psx_wino_ok": (i32, [i32, i32, i32, i32]),
     "psx_wino_weights": (i32, [vp, vp, i32, i32, i32, vp]),

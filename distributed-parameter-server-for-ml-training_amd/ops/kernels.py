@@ -142,6 +142,36 @@ def bgemm_f32(a, b, p, m, n, kd, nb, cfg=0):
           "bgemm_f32")
 
 
+_SK_WS = {}
+
+
+def sk_workspace(device=None):
+    """Register the stream-K GEMM's fixup workspace (csrc/kernels/wino_gemm.hip: partial tiles of
+    split tiles + zeroed arrival counters) for this process; call before any graph capture. The
+    library keeps one (process-global) registration: the stream-K launches of a process run on
+    one stream at a time (the engine's compute stream)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if dev not in _SK_WS:
+        n = int(kernels().psx_sk_workspace_floats())
+        ws = torch.empty(n, dtype=torch.float32, device=dev)
+        cnt = torch.zeros(256, dtype=torch.int32, device=dev)
+        _SK_WS[dev] = (ws, cnt)
+        check(kernels().psx_sk_set_workspace(ptr(ws), n, ptr(cnt), 256), "sk_set_workspace")
+    return _SK_WS[dev]
+
+
+def sk_gemm_nt(a, b, c, m, n, kd, nb, a_strides, b_strides, c_strides, bn=0):
+    """nb batched fp32 GEMMs c[i] = a[i] @ b[i].T on the stream-K kernel (wino_gemm.hip); strides
+    (row, batch) in elements: a[i][r][k] = a[i * a_strides[1] + r * a_strides[0] + k], same for b
+    ([i][n][k]) and c ([i][m][n]). kd a multiple of 32, n of 64. Returns the launch status (-5: no
+    workspace registered)."""
+    assert a.dtype == b.dtype == c.dtype == torch.float32
+    sk_workspace(a.device)
+    return int(kernels().psx_sk_gemm_nt(ptr(a), ptr(b), ptr(c), a_strides[0], a_strides[1], b_strides[0], b_strides[1],
+                                        c_strides[0], c_strides[1], m, n, kd, nb, ptr(zero_page(a.device)), bn,
+                                        stream_ptr()))
+
+
 def bgemm_tn_f32(x, d, part, t, c, k, nb, q=1, br=64, bc=64):
     """Batched TN GEMMs part[i * q + j] = d[i, range j].T @ x[i, range j] (x [nb][t][c],
     d [nb][t][k], part [nb*q][k][c]) on the fp32 weight-gradient mainloop (wgrad_v2.hip)."""

@@ -907,12 +907,13 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
                                sshift, bm, st);
     }
   }
-  // the 36 GEMMs: stream-K (wino_gemm.hip) where the tiled launch cannot fill the chip in
-  // balanced rounds (C >= 256: ResNet-18's 8x8 / 4x4 stages), else the conv_v2 mainloop.
-  // PSX_WINO_SK=0 keeps the tiled path; a process without the registered workspace (-5) too.
+  // the 36 GEMMs: the conv_v2 mainloop; PSX_WINO_SK=1 takes the stream-K kernel (wino_gemm.hip)
+  // for C >= 256 (2 = every layer). Opt-in: same box, 8x8x256 36 x (512 x 256 x 256) 40.6 vs
+  // 33.7 us (split-tile hand-off ~6 us, scattered C stores ~5 us, one wave per SIMD leaves the
+  // barriers and first LDS reads of every unit exposed: profiles/README.md round 4).
   static const int sk_mode = [] {
     const char* e = getenv("PSX_WINO_SK");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   int e = -5;
   if (sk_mode && (C >= 256 || sk_mode == 2))

@@ -44,7 +44,7 @@ struct SkArgs {
   long sa_row, sa_b, sb_row, sb_b, sc_row, sc_b;
   int M, N, Kd, nb;
   int tm, tn, kc, units, G;
-  int probe;  // diagnostics (wrong results): 1 no DMA, 2 no MFMA, 4 no flush stores
+  int probe;  // diagnostics (wrong results): 1 no DMA, 2 no MFMA, 4 no flush, 8 no split hand-off, 16 no C stores
 };
 
 constexpr int kSkBM = 128;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256, 1) void sk_gemm_kernel(SkArgs a) {
     const bool head = seg0 % a.kc == 0, tail = (u + 1) % a.kc == 0;
     const int bt = t / (a.tm * a.tn), rem = t - bt * a.tm * a.tn;
     const int mt = rem / a.tn, nt = rem - (rem / a.tn) * a.tn;
-    if (!(head && tail)) {
+    if (!(head && tail) && !(a.probe & 8)) {
       // The partials cross workgroups, possibly XCDs (each XCD has its own L2): they are written
       // through to memory (sc0 sc1 stores) and read past the L2 (sc0 sc1 loads), so no
       // whole-cache writeback / invalidate fence is needed (an agent-scope release / acquire
@@ -204,6 +204,7 @@ __global__ __launch_bounds__(256, 1) void sk_gemm_kernel(SkArgs a) {
           }
       if (threadIdx.x == 0) __hip_atomic_store(a.cnt + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (a.probe & 16) return;
     float* cb = a.C + bt * a.sc_b;
 #pragma unroll
     for (int m = 0; m < MBK; ++m)

@@ -47,6 +47,10 @@ struct SkArgs {
   int probe;  // diagnostics (wrong results): 1 no DMA, 2 no MFMA, 4 no flush, 8 no split hand-off, 16 no C stores
 };
 
+#ifndef PSX_SK_SCHED
+#define PSX_SK_SCHED 1
+#endif
+
 constexpr int kSkBM = 128;
 constexpr int kSkNS = 3;
 
@@ -237,13 +241,35 @@ __global__ __launch_bounds__(256, 1) void sk_gemm_kernel(SkArgs a) {
     const int slot = k % NS;
     f32x4 fa0[MBK], fb0[NBK], fa1[MBK], fb1[NBK];
     readq(slot, 0, fa0, fb0);
-    readq(slot, 1, fa1, fb1);
-    if (!(a.probe & 2)) mmaq(fa0, fb0);
-    readq(slot, 2, fa0, fb0);
-    if (!(a.probe & 2)) mmaq(fa1, fb1);
-    readq(slot, 3, fa1, fb1);
-    if (!(a.probe & 2)) mmaq(fa0, fb0);
-    if (!(a.probe & 2)) mmaq(fa1, fb1);
+    // quarter q's 16 MFMAs with quarter q + 1's four ds_reads threaded between them (one per 4
+    // MFMAs, order pinned by sched_barriers), so the reads retire under the MFMAs instead of
+    // behind the lgkmcnt(0) hipcc puts in front of the next MFMA group
+    auto quarter = [&](const f32x4(&ca)[MBK], const f32x4(&cb)[NBK], int qn, f32x4(&na)[MBK], f32x4(&nb)[NBK]) {
+      const unsigned char* base = smem + slot * STAGE;
+      const int so = (((fh * 4 + qn) ^ sw) << 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (!(a.probe & 2)) {
+#pragma unroll
+          for (int m = 0; m < MBK; ++m)
+#pragma unroll
+            for (int b = 0; b < NBK; ++b) acc[m][b] = mfma32(ca[m][e], cb[b][e], acc[m][b]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (qn < 4) {
+          // read e of the next quarter: A blocks first, then B blocks
+          if (e < MBK)
+            na[e] = *reinterpret_cast<const f32x4*>(base + aro[e] + so);
+          else if (e - MBK < NBK)
+            nb[e - MBK] = *reinterpret_cast<const f32x4*>(base + bro[e - MBK] + so);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    quarter(fa0, fb0, 1, fa1, fb1);
+    quarter(fa1, fb1, 2, fa0, fb0);
+    quarter(fa0, fb0, 3, fa1, fb1);
+    quarter(fa1, fb1, 4, fa0, fb0);
   };
   // segments = the parts of tiles in this range; the accumulators stay in the MFMA registers
   // across a segment's units (no flush inside the inner loop)

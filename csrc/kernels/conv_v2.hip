@@ -323,13 +323,21 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       // into the stage just drained, reads of the next stage's first sub-step — then its MFMAs.
       auto load_frags = [&](const unsigned char* base, int q, u32x4(&fa)[MT], u32x4(&fb)[NT]) {
         const int sx = q >> 1, kk = q & 1;
-        const unsigned char* A = base + sx * BM * 128;
-        const unsigned char* X = base + XOFF;
+        if constexpr (PSX_CONV_ASMRD) {  // untracked reads: sub() waits for exactly its own
+          const unsigned A = lds_off(base) + sx * BM * 128, X = lds_off(base) + XOFF;
 #pragma unroll
-        for (int m = 0; m < MT; ++m)
-          fa[m] = *reinterpret_cast<const u32x4*>(A + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
+          for (int m = 0; m < MT; ++m) fa[m] = ds_read128u(A + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
 #pragma unroll
-        for (int n = 0; n < NT; ++n) fb[n] = *reinterpret_cast<const u32x4*>(X + (boff[n][sx] ^ (kk << 6)));
+          for (int n = 0; n < NT; ++n) fb[n] = ds_read128u(X + (boff[n][sx] ^ (kk << 6)));
+        } else {
+          const unsigned char* A = base + sx * BM * 128;
+          const unsigned char* X = base + XOFF;
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+            fa[m] = *reinterpret_cast<const u32x4*>(A + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
+#pragma unroll
+          for (int n = 0; n < NT; ++n) fb[n] = *reinterpret_cast<const u32x4*>(X + (boff[n][sx] ^ (kk << 6)));
+        }
       };
       u32x4 fa0[MT], fb0[NT], fa1[MT], fb1[NT];
       if (HALO) __syncthreads();
@@ -345,6 +353,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
         const unsigned char* base = smem + (t & 1) * TST;
         auto sub = [&](auto qc, u32x4(&fa)[MT], u32x4(&fb)[NT], u32x4(&na)[MT], u32x4(&nb)[NT]) {
           constexpr int q = decltype(qc)::value, sx = q >> 1;
+          bool ahead = true;  // the next sub-step's reads were issued after this one's
           if constexpr (q < 5) {
             load_frags(base, q + 1, na, nb);
           } else if (t + 1 < nmac) {
@@ -354,6 +363,14 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
             asm volatile("" ::: "memory");
             if (t + 2 < nmac) issue_t(t + 2, t & 1);
             load_frags(smem + ((t + 1) & 1) * TST, 0, na, nb);
+          } else {
+            ahead = false;
+          }
+          if constexpr (PSX_CONV_ASMRD) {
+            if (ahead)
+              lgkm_wait<MT + NT>();
+            else
+              lgkm_wait<0>();
           }
           __builtin_amdgcn_sched_barrier(0);
           if constexpr (!HALO && sx != 1) {
@@ -572,11 +589,33 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (ks + 2 < nk) issue(ks + 2, stage == 0 ? 2 : stage - 1);
+      if constexpr (PSX_CONV_ASMRD) {
+        // both halves' fragments at once (pipeline.hpp ds_read128u); the first half's MFMAs
+        // wait only for their own reads, the second half's retire under them
+        const unsigned sa = lds_off(smem) + stage * STAGE, sbb = sa + BM * 128;
+        u32x4 fa[2][MT], fb[2][NT];
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        u32x4 fa[MT], fb[NT];
-        load_frags(stage, kk, fa, fb);
-        mma_tiles<MT, NT, T>(acc, fa, fb);
+        for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+          for (int m = 0; m < MT; ++m) fa[kk][m] = ds_read128u(sa + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
+#pragma unroll
+          for (int n = 0; n < NT; ++n) fb[kk][n] = ds_read128u(sbb + kmaj2(wn * (BN / WGN) + n * 16 + frow, kk * 4 + fch));
+        }
+        lgkm_wait<MT + NT>();
+        __builtin_amdgcn_sched_barrier(0);
+        mma_tiles<MT, NT, T>(acc, fa[0], fb[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        lgkm_wait<0>();
+        __builtin_amdgcn_sched_barrier(0);
+        mma_tiles<MT, NT, T>(acc, fa[1], fb[1]);
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          u32x4 fa[MT], fb[NT];
+          load_frags(stage, kk, fa, fb);
+          mma_tiles<MT, NT, T>(acc, fa, fb);
+        }
       }
       wfold(ks);
       stage = stage == 2 ? 0 : stage + 1;

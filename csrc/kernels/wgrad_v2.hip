@@ -300,20 +300,51 @@ __global__ __launch_bounds__(256) void wgrad2f_kernel(Wgrad2Args a) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (st + NS - 1 < nsteps) issue(st + NS - 1, stage == 0 ? NS - 1 : stage - 1);
-    const unsigned char* X = smem + stage * STAGE;
-    const unsigned char* D = X + XT;
+    if constexpr (!PSX_CONV_ASMRD) {
+      const unsigned char* X = smem + stage * STAGE;
+      const unsigned char* D = X + XT;
 #pragma unroll
-    for (int s4 = 0; s4 < PS / 4; ++s4) {
+      for (int s4 = 0; s4 < PS / 4; ++s4) {
+        const int row = 4 * s4 + kq;
+        float fa[MT], fb[NT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) fa[m] = *reinterpret_cast<const float*>(X + row * XROWB + aoff[m]);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) fb[n] = *reinterpret_cast<const float*>(D + row * DROWB + boff[n]);
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int n = 0; n < NT; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[m], fb[n], acc[m][n], 0, 0, 0);
+      }
+    } else {
+    // fragment reads run three four-pixel steps ahead of the MFMAs (pipeline.hpp ds_read32):
+    // step s4 waits only for its own reads (<= 12 in flight: exact lgkmcnt counts)
+    const unsigned xb = lds_off(smem) + stage * STAGE, db = xb + XT;
+    constexpr int RS = MT + NT, NST = PS / 4, AHEAD = 3;
+    float fa[NST][MT], fb[NST][NT];
+    auto rd = [&](int s4) {
       const int row = 4 * s4 + kq;  // (row & 1) == (kq & 1): the swizzle bit is in aoff / boff
-      float fa[MT], fb[NT];
 #pragma unroll
-      for (int m = 0; m < MT; ++m) fa[m] = *reinterpret_cast<const float*>(X + row * XROWB + aoff[m]);
+      for (int m = 0; m < MT; ++m) fa[s4][m] = ds_read32(xb + row * XROWB + aoff[m]);
 #pragma unroll
-      for (int n = 0; n < NT; ++n) fb[n] = *reinterpret_cast<const float*>(D + row * DROWB + boff[n]);
+      for (int n = 0; n < NT; ++n) fb[s4][n] = ds_read32(db + row * DROWB + boff[n]);
+    };
+#pragma unroll
+    for (int s4 = 0; s4 < AHEAD; ++s4) rd(s4);
+    static_for<0, NST>([&](auto sc) {
+      constexpr int s4 = decltype(sc)::value;
+      constexpr int later = (s4 + AHEAD - 1 < NST - 1 ? s4 + AHEAD - 1 : NST - 1) - s4;  // steps issued after s4
+      lgkm_wait<later * RS>();
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int n = 0; n < NT; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[m], fb[n], acc[m][n], 0, 0, 0);
+        for (int n = 0; n < NT; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[s4][m], fb[s4][n], acc[m][n], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (s4 + AHEAD < NST) rd(s4 + AHEAD);
+    });
     }
     stage = stage == NS - 1 ? 0 : stage + 1;
   }

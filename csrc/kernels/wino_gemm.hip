@@ -61,6 +61,9 @@ PSX_DEV int xcd_of(int w, int nwg) {
   return w < r * (q + 1) ? w / (q + 1) : r + (w - r * (q + 1)) / q;
 }
 
+// ds_read_b128 outside hipcc's waitcnt tracking (pipeline.hpp ds_read128u, as fp32)
+PSX_DEV f32x4 ds_read128(unsigned off) { return __builtin_bit_cast(f32x4, ds_read128u(off)); }
+
 PSX_DEV f32x16 mfma32(float a, float b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0); }
 
 template <int BN>
@@ -239,37 +242,31 @@ __global__ __launch_bounds__(256, 1) void sk_gemm_kernel(SkArgs a) {
     asm volatile("" ::: "memory");
     if (k + 2 < n) issue(u0 + k + 2, (k + 2) % NS);
     const int slot = k % NS;
-    f32x4 fa0[MBK], fb0[NBK], fa1[MBK], fb1[NBK];
-    readq(slot, 0, fa0, fb0);
-    // quarter q's 16 MFMAs with quarter q + 1's four ds_reads threaded between them (one per 4
-    // MFMAs, order pinned by sched_barriers), so the reads retire under the MFMAs instead of
-    // behind the lgkmcnt(0) hipcc puts in front of the next MFMA group
-    auto quarter = [&](const f32x4(&ca)[MBK], const f32x4(&cb)[NBK], int qn, f32x4(&na)[MBK], f32x4(&nb)[NBK]) {
-      const unsigned char* base = smem + slot * STAGE;
-      const int so = (((fh * 4 + qn) ^ sw) << 4);
+    // all 16 fragment reads of the unit go out at once (inline asm: hipcc does not count them),
+    // then quarter q waits only for its own four (lgkmcnt counts retire in order for LDS):
+    // hipcc's own waitcnt placement put an lgkmcnt(0) in front of every MFMA group, exposing the
+    // read latency of the next group's prefetch each time
+    const unsigned lbase = lds_off(smem) + slot * STAGE;
+    f32x4 fa[4][MBK], fb[4][NBK];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (!(a.probe & 2)) {
+    for (int q = 0; q < 4; ++q) {
+      const unsigned so = (((fh * 4 + q) ^ sw) << 4);
 #pragma unroll
-          for (int m = 0; m < MBK; ++m)
+      for (int m = 0; m < MBK; ++m) fa[q][m] = ds_read128(lbase + aro[m] + so);
 #pragma unroll
-            for (int b = 0; b < NBK; ++b) acc[m][b] = mfma32(ca[m][e], cb[b][e], acc[m][b]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (qn < 4) {
-          // read e of the next quarter: A blocks first, then B blocks
-          if (e < MBK)
-            na[e] = *reinterpret_cast<const f32x4*>(base + aro[e] + so);
-          else if (e - MBK < NBK)
-            nb[e - MBK] = *reinterpret_cast<const f32x4*>(base + bro[e - MBK] + so);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    };
-    quarter(fa0, fb0, 1, fa1, fb1);
-    quarter(fa1, fb1, 2, fa0, fb0);
-    quarter(fa0, fb0, 3, fa1, fb1);
-    quarter(fa1, fb1, 4, fa0, fb0);
+      for (int b = 0; b < NBK; ++b) fb[q][b] = ds_read128(lbase + bro[b] + so);
+    }
+    constexpr int RQ = MBK + NBK;  // reads per quarter
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q == 0) lgkm_wait<3 * RQ>();
+      if (q == 1) lgkm_wait<2 * RQ>();
+      if (q == 2) lgkm_wait<RQ>();
+      if (q == 3) lgkm_wait<0>();
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(a.probe & 2)) mmaq(fa[q], fb[q]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   };
   // segments = the parts of tiles in this range; the accumulators stay in the MFMA registers
   // across a segment's units (no flush inside the inner loop)

@@ -1,0 +1,12 @@
+# counted-wait LDS fragment reads (PSX_CONV_ASMRD): GPU numerics, per-layer and headline A/B vs the asm0 variant
+set -o pipefail
+mkdir -p gpurun_out
+V=$GRAFT_REPO_ROOT/distributed-parameter-server-for-ml-training_amd/_native/variants/libpsx_kernels_asm0.so
+T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
+timeout -k 10 600 $T tests -m gpu --ignore tests/test_multirank_gpu.py --ignore tests/test_elastic_gpu.py > gpurun_out/t_gpu.log 2>&1 || { tail -30 gpurun_out/t_gpu.log; exit 1; }
+tail -2 gpurun_out/t_gpu.log
+timeout -k 10 300 python bench/f32_tiles.py > gpurun_out/f32_tiles_asm.jsonl 2>&1 || { tail -5 gpurun_out/f32_tiles_asm.jsonl; exit 1; }
+PSX_KERNELS_LIB=$V timeout -k 10 300 python bench/f32_tiles.py > gpurun_out/f32_tiles_asm0.jsonl 2>&1 || { tail -5 gpurun_out/f32_tiles_asm0.jsonl; exit 1; }
+timeout -k 10 300 python bench/r50_wgrad_f32.py > gpurun_out/r50_wgrad_asm.jsonl 2>&1 || exit 1
+PSX_KERNELS_LIB=$V timeout -k 10 300 python bench/r50_wgrad_f32.py > gpurun_out/r50_wgrad_asm0.jsonl 2>&1 || exit 1
+AB_CFGS="_ PSX_KERNELS_LIB=$V" bash scripts/prof/ab_env.sh || exit 1

@@ -354,6 +354,9 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
         auto sub = [&](auto qc, u32x4(&fa)[MT], u32x4(&fb)[NT], u32x4(&na)[MT], u32x4(&nb)[NT]) {
           constexpr int q = decltype(qc)::value, sx = q >> 1;
           bool ahead = true;  // the next sub-step's reads were issued after this one's
+          // at most 15 reads in flight (the 4-bit counter's range): with more than 7 fragments
+          // per sub-step this one's reads retire before the next one's go out
+          if constexpr (PSX_CONV_ASMRD && 2 * (MT + NT) > 15) lgkm_wait<0>();
           if constexpr (q < 5) {
             load_frags(base, q + 1, na, nb);
           } else if (t + 1 < nmac) {
@@ -593,18 +596,23 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
         // both halves' fragments at once (pipeline.hpp ds_read128u); the first half's MFMAs
         // wait only for their own reads, the second half's retire under them
         const unsigned sa = lds_off(smem) + stage * STAGE, sbb = sa + BM * 128;
+        // (at most 15 reads in flight, the 4-bit counter's range: tiles with more than 7 fragments
+        // per half read the second half after the first half's MFMAs)
+        constexpr bool both = 2 * (MT + NT) <= 15;
         u32x4 fa[2][MT], fb[2][NT];
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
+        auto rdh = [&](int kk) {
 #pragma unroll
           for (int m = 0; m < MT; ++m) fa[kk][m] = ds_read128u(sa + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
 #pragma unroll
           for (int n = 0; n < NT; ++n) fb[kk][n] = ds_read128u(sbb + kmaj2(wn * (BN / WGN) + n * 16 + frow, kk * 4 + fch));
-        }
-        lgkm_wait<MT + NT>();
+        };
+        rdh(0);
+        if constexpr (both) rdh(1);
+        lgkm_wait<both ? MT + NT : 0>();
         __builtin_amdgcn_sched_barrier(0);
         mma_tiles<MT, NT, T>(acc, fa[0], fb[0]);
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!both) rdh(1);
         lgkm_wait<0>();
         __builtin_amdgcn_sched_barrier(0);
         mma_tiles<MT, NT, T>(acc, fa[1], fb[1]);

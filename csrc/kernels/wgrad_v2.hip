@@ -319,9 +319,9 @@ __global__ __launch_bounds__(256) void wgrad2f_kernel(Wgrad2Args a) {
       }
     } else {
     // fragment reads run three four-pixel steps ahead of the MFMAs (pipeline.hpp ds_read32):
-    // step s4 waits only for its own reads (<= 12 in flight: exact lgkmcnt counts)
+    // step s4 waits only for its own reads (<= 15 in flight, the 4-bit counter's range: exact counts)
     const unsigned xb = lds_off(smem) + stage * STAGE, db = xb + XT;
-    constexpr int RS = MT + NT, NST = PS / 4, AHEAD = 3;
+    constexpr int RS = MT + NT, NST = PS / 4, AHEAD = 15 / RS < 1 ? 1 : (15 / RS > 3 ? 3 : 15 / RS);
     float fa[NST][MT], fb[NST][NT];
     auto rd = [&](int s4) {
       const int row = 4 * s4 + kq;  // (row & 1) == (kq & 1): the swizzle bit is in aoff / boff

@@ -242,30 +242,32 @@ __global__ __launch_bounds__(256, 1) void sk_gemm_kernel(SkArgs a) {
     asm volatile("" ::: "memory");
     if (k + 2 < n) issue(u0 + k + 2, (k + 2) % NS);
     const int slot = k % NS;
-    // all 16 fragment reads of the unit go out at once (inline asm: hipcc does not count them),
-    // then quarter q waits only for its own four (lgkmcnt counts retire in order for LDS):
+    // the unit's fragment reads go out ahead (inline asm: hipcc does not count them; <= 12 in
+    // flight), quarter q waits only for its own (LDS retires in order):
     // hipcc's own waitcnt placement put an lgkmcnt(0) in front of every MFMA group, exposing the
     // read latency of the next group's prefetch each time
     const unsigned lbase = lds_off(smem) + slot * STAGE;
     f32x4 fa[4][MBK], fb[4][NBK];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    auto rq = [&](int q) {
       const unsigned so = (((fh * 4 + q) ^ sw) << 4);
 #pragma unroll
       for (int m = 0; m < MBK; ++m) fa[q][m] = ds_read128(lbase + aro[m] + so);
 #pragma unroll
       for (int b = 0; b < NBK; ++b) fb[q][b] = ds_read128(lbase + bro[b] + so);
-    }
-    constexpr int RQ = MBK + NBK;  // reads per quarter
+    };
+    constexpr int RQ = MBK + NBK;  // reads per quarter; at most 3 quarters (<= 12) in flight
+    rq(0);
+    rq(1);
+    rq(2);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      if (q == 0) lgkm_wait<3 * RQ>();
-      if (q == 1) lgkm_wait<2 * RQ>();
+      if (q < 2) lgkm_wait<2 * RQ>();
       if (q == 2) lgkm_wait<RQ>();
       if (q == 3) lgkm_wait<0>();
       __builtin_amdgcn_sched_barrier(0);
       if (!(a.probe & 2)) mmaq(fa[q], fb[q]);
       __builtin_amdgcn_sched_barrier(0);
+      if (q == 0) rq(3);
     }
   };
   // segments = the parts of tiles in this range; the accumulators stay in the MFMA registers

@@ -10,3 +10,4 @@ PSX_KERNELS_LIB=$V timeout -k 10 300 python bench/f32_tiles.py > gpurun_out/f32_
 timeout -k 10 300 python bench/r50_wgrad_f32.py > gpurun_out/r50_wgrad_asm.jsonl 2>&1 || exit 1
 PSX_KERNELS_LIB=$V timeout -k 10 300 python bench/r50_wgrad_f32.py > gpurun_out/r50_wgrad_asm0.jsonl 2>&1 || exit 1
 AB_CFGS="_ PSX_KERNELS_LIB=$V" bash scripts/prof/ab_env.sh || exit 1
+for p in 0 4 5; do PSX_SK_PROBE=$p BN=128 timeout -k 10 60 python scripts/prof/sk_probe.py || exit 1; done

@@ -30,7 +30,7 @@ PSX_DEV void wait_vmcnt() {
 // waits are capped at 15, which stays correct (in-order retirement).
 // PSX_CONV_ASMRD = 0 builds the mainloops with plain LDS loads (A/B variant).
 #ifndef PSX_CONV_ASMRD
-#define PSX_CONV_ASMRD 1
+#define PSX_CONV_ASMRD 0
 #endif
 
 typedef __attribute__((address_space(3))) unsigned char lds_u8;

@@ -147,7 +147,7 @@ __global__ __launch_bounds__(256, 1) void sk_gemm_kernel(SkArgs a) {
 #pragma unroll
       for (int m = 0; m < MBK; ++m)
 #pragma unroll
-        for (int b = 0; b < NBK; ++b) acc[m][b] = mfma32(fa[m][e], fb[b][e], acc[m][b]);
+        for (int b = 0; b < NBK; ++b) acc[m][b] = mfma32(fb[b][e], fa[m][e], acc[m][b]);  // C^T: lane = row of C
   };
 
   // tile store / split-tile fixup of the segment ending at unit u (inclusive)
@@ -212,18 +212,23 @@ __global__ __launch_bounds__(256, 1) void sk_gemm_kernel(SkArgs a) {
       if (threadIdx.x == 0) __hip_atomic_store(a.cnt + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (a.probe & 16) return;
+    // the accumulators hold C^T blocks (the B operand's rows on the MFMA's row axis): a lane owns
+    // one row of C (its tile) and each register quad four consecutive columns, so the tile goes
+    // out as 16-byte stores
     float* cb = a.C + bt * a.sc_b;
 #pragma unroll
-    for (int m = 0; m < MBK; ++m)
+    for (int m = 0; m < MBK; ++m) {
+      const int row = mt * BM + wm * 64 + m * 32 + fi;
+      if (row >= a.M) continue;
 #pragma unroll
-      for (int b = 0; b < NBK; ++b) {
-        const int col = nt * BN + wn * WN + b * 32 + fi;
+      for (int b = 0; b < NBK; ++b)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = mt * BM + wm * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-          if (row < a.M) cb[(long)row * a.sc_row + col] = acc[m][b][r];
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const int col = nt * BN + wn * WN + b * 32 + 8 * r4 + 4 * fh;
+          *reinterpret_cast<f32x4*>(cb + (long)row * a.sc_row + col) =
+              (f32x4){acc[m][b][4 * r4], acc[m][b][4 * r4 + 1], acc[m][b][4 * r4 + 2], acc[m][b][4 * r4 + 3]};
         }
-      }
+    }
   };
 
   // prologue: units 0 and 1 in flight
@@ -329,6 +334,9 @@ int psx_sk_gemm_nt(const float* A, const float* B, float* C, long sa_row, long s
                    long sc_row, long sc_b, int M, int N, int Kd, int nb, const void* zero, int bn, hipStream_t st) {
   if (!g_ws || g_ws_floats < psx_sk_workspace_floats() || g_ncnt < 256) return -5;
   if (M < 1 || nb < 1 || Kd < 32) return -2;
+  // 16-byte DMA sources and 16-byte C stores
+  if ((sa_row | sa_b | sb_row | sb_b | sc_row | sc_b) & 3) return -2;
+  if (((size_t)A | (size_t)B | (size_t)C) & 15) return -2;
   SkArgs a{};
   a.A = A; a.B = B; a.C = C; a.zero = (const float*)zero; a.ws = g_ws; a.cnt = g_cnt;
   a.sa_row = sa_row; a.sa_b = sa_b; a.sb_row = sb_row; a.sb_b = sb_b; a.sc_row = sc_row; a.sc_b = sc_b;

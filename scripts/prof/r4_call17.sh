@@ -1,8 +1,8 @@
-# full GPU suite (incl. multirank + elastic), smoke, bench
+# remaining GPU suite (multirank from the async test on, elastic), smoke, bench
 set -o pipefail
 mkdir -p gpurun_out
 T="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
-timeout -k 10 1000 $T tests -m gpu > gpurun_out/t_full.log 2>&1 || { tail -40 gpurun_out/t_full.log; exit 1; }
+timeout -k 10 1000 $T tests/test_multirank_gpu.py tests/test_elastic_gpu.py -k "async or native_sync or elastic or scripted or lost" > gpurun_out/t_full.log 2>&1 || { tail -40 gpurun_out/t_full.log; exit 1; }
 tail -3 gpurun_out/t_full.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
 tail -2 gpurun_out/smoke.log

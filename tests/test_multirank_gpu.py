@@ -262,8 +262,10 @@ def test_async_remote_workers(world, topology, native_loop, tmp_path):
     assert len(recs) == 1, out[-3000:]
     gs, processed, checksum, applied, rejected, upd_s, src = recs[0]
     assert processed == W * 4 and 0 < gs <= W * 4, recs
-    # every processed push was applied or rejected (bound 5: with 4 steps per worker, none is)
-    assert applied + rejected == processed and rejected == 0 and gs == applied, recs
+    # every processed push was applied or rejected; the global step counts the applied ones.
+    # Rejections (staleness bound 5) are possible but rare: a worker whose fetch is more than 5
+    # other pushes old (measured: 1 of 12 once, Python loop at world 3 co-located)
+    assert applied + rejected == processed and gs == applied and rejected <= W, recs
     assert checksum == checksum and abs(checksum) < 1e12
     # the update time is the DEVICE time of the R18 sgd apply (~20 us), not a launch (~us) or a
     # host wait (~ms); the metric is rounded to 0.1 ms

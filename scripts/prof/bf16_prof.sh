@@ -6,3 +6,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/b16
 python scripts/prof/kstats.py gpurun_out/b16/run_kernel_trace.csv --steps 8 > gpurun_out/b16.txt
 python scripts/prof/kstats.py gpurun_out/b16/run_kernel_trace.csv --steps 8 --grid "conv2|wgrad|bn_|head|pool" > gpurun_out/b16_grid.txt
 head -30 gpurun_out/b16.txt
+python scripts/prof/timeline.py gpurun_out/b16/run_kernel_trace.csv --list > gpurun_out/b16_timeline.txt

@@ -44,11 +44,12 @@ struct SkArgs {
   long sa_row, sa_b, sb_row, sb_b, sc_row, sc_b;
   int M, N, Kd, nb;
   int tm, tn, kc, units, G;
-  int probe;  // diagnostics (wrong results): 1 no DMA, 2 no MFMA, 4 no flush, 8 no split hand-off, 16 no C stores
 };
 
-#ifndef PSX_SK_SCHED
-#define PSX_SK_SCHED 1
+// diagnostics builds only (wrong results; profiles/r4_sk_gemm_probes.jsonl): 1 no DMA, 2 no MFMA,
+// 4 no flush, 8 no split hand-off, 16 no C stores
+#ifndef PSX_SK_PROBE
+#define PSX_SK_PROBE 0
 #endif
 
 constexpr int kSkBM = 128;
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(256, 1) void sk_gemm_kernel(SkArgs a) {
     off[i] = r < BM ? (long)r * a.sa_row + c * 4 : (long)(r - BM) * a.sb_row + c * 4;
   }
   auto issue = [&](int u, int slot) {
-    if (a.probe & 1) return;
+    if (PSX_SK_PROBE & 1) return;
     const int t = __builtin_amdgcn_readfirstlane(u / a.kc);
     const int ch = u - t * a.kc;
     const int bt = __builtin_amdgcn_readfirstlane(t / (a.tm * a.tn));
@@ -157,7 +158,7 @@ __global__ __launch_bounds__(256, 1) void sk_gemm_kernel(SkArgs a) {
     const bool head = seg0 % a.kc == 0, tail = (u + 1) % a.kc == 0;
     const int bt = t / (a.tm * a.tn), rem = t - bt * a.tm * a.tn;
     const int mt = rem / a.tn, nt = rem - (rem / a.tn) * a.tn;
-    if (!(head && tail) && !(a.probe & 8)) {
+    if (!(head && tail) && !(PSX_SK_PROBE & 8)) {
       // The partials cross workgroups, possibly XCDs (each XCD has its own L2): they are written
       // through to memory (sc0 sc1 stores) and read past the L2 (sc0 sc1 loads), so no
       // whole-cache writeback / invalidate fence is needed (an agent-scope release / acquire
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(256, 1) void sk_gemm_kernel(SkArgs a) {
           }
       if (threadIdx.x == 0) __hip_atomic_store(a.cnt + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (a.probe & 16) return;
+    if (PSX_SK_PROBE & 16) return;
     // the accumulators hold C^T blocks (the B operand's rows on the MFMA's row axis): a lane owns
     // one row of C (its tile) and each register quad four consecutive columns, so the tile goes
     // out as 16-byte stores
@@ -270,7 +271,7 @@ __global__ __launch_bounds__(256, 1) void sk_gemm_kernel(SkArgs a) {
       if (q == 2) lgkm_wait<RQ>();
       if (q == 3) lgkm_wait<0>();
       __builtin_amdgcn_sched_barrier(0);
-      if (!(a.probe & 2)) mmaq(fa[q], fb[q]);
+      if (!(PSX_SK_PROBE & 2)) mmaq(fa[q], fb[q]);
       __builtin_amdgcn_sched_barrier(0);
       if (q == 0) rq(3);
     }
@@ -282,7 +283,7 @@ __global__ __launch_bounds__(256, 1) void sk_gemm_kernel(SkArgs a) {
     const int seg0 = u0 + k;
     const int kend = min(n, k + (a.kc - seg0 % a.kc));
     for (; k < kend; ++k) step(k);
-    if (!(a.probe & 4)) flush(u0 + k - 1, seg0);
+    if (!(PSX_SK_PROBE & 4)) flush(u0 + k - 1, seg0);
     zero_acc();
   }
 }
@@ -341,7 +342,6 @@ int psx_sk_gemm_nt(const float* A, const float* B, float* C, long sa_row, long s
   a.A = A; a.B = B; a.C = C; a.zero = (const float*)zero; a.ws = g_ws; a.cnt = g_cnt;
   a.sa_row = sa_row; a.sa_b = sa_b; a.sb_row = sb_row; a.sb_b = sb_b; a.sc_row = sc_row; a.sc_b = sc_b;
   a.M = M; a.N = N; a.Kd = Kd; a.nb = nb;
-  if (const char* e = getenv("PSX_SK_PROBE")) a.probe = atoi(e);
   SkArgs a128 = a, a64 = a;
   const int g128 = sk_plan<128>(M, N, Kd, nb, a128), g64 = sk_plan<64>(M, N, Kd, nb, a64);
   int use = bn;

@@ -15,4 +15,4 @@ for rep in 1 2; do for cfg in _ PSX_KERNELS_LIB=$V; do
   env $envs timeout -k 10 200 python bench.py --dtype bf16 --steps 30 --warmup 10 --secondary none > gpurun_out/abh.json 2>gpurun_out/abh.err || { tail -5 gpurun_out/abh.err; exit 1; }
   echo "bf16 $cfg $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/abh.json)"
 done; done
-for p in 0 4 5; do PSX_KERNELS_LIB=$V PSX_SK_PROBE=$p BN=128 timeout -k 10 60 python scripts/prof/sk_probe.py || exit 1; done
+for p in 0; do PSX_KERNELS_LIB=$V BN=128 timeout -k 10 60 python scripts/prof/sk_probe.py || exit 1; done

@@ -1,4 +1,5 @@
-"""Stream-K GEMM diagnostics: time per PSX_SK_PROBE mode on the 8x8x256 Winograd shape."""
+"""Stream-K GEMM timing on the 8x8x256 Winograd shape (diagnostic modes: build a kernel variant
+with -D PSX_SK_PROBE=<bits>, csrc/build.py --variant, and load it with PSX_KERNELS_LIB)."""
 import os
 import sys
 

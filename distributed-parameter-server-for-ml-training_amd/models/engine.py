@@ -209,10 +209,16 @@ class HipResNetEngine:
         self._bwd_fold = {}
         self._premasked = set()
         # weight gradients (+ their batched reductions) on a side stream, a parallel branch of the
-        # captured step graph next to the dgrad -> BN-backward chain: 1.837/1.841 vs 1.853/1.858
-        # ms/step on the main stream (two A/B pairs, session 3); PSX_WGRAD_STREAM=0: main stream
-        self.wg_stream = (torch.cuda.Stream(device=self.dev)
-                          if os.environ.get("PSX_WGRAD_STREAM", "1") == "1" else None)
+        # captured step graph next to the dgrad -> BN-backward chain. PSX_WGRAD_STREAM=1 / 0
+        # forces it; the default keeps it except for the fp32 engine on CIFAR-size images, whose
+        # fused Winograd weight gradients (1 workgroup per CU, like the data gradients beside them)
+        # only time-share the chip with the dgrad chain and add cross-queue waits: same box
+        # 3.35-3.38 -> 3.28-3.29 ms/step without it (r4_call20/21); bf16 ResNet-18 (1.85 -> 1.89)
+        # and fp32 ResNet-50 (40.4 -> 41.5) keep it.
+        ws = os.environ.get("PSX_WGRAD_STREAM", "auto")
+        if ws == "auto":
+            ws = "0" if (self.f32 and max(self.spec.in_hw) <= 64) else "1"
+        self.wg_stream = torch.cuda.Stream(device=self.dev) if ws == "1" else None
         self._wg_batch = None
         self._fins = {}
         # conv-operand unpack: "tiles" (flat grid, fp32 arena or bf16 image source) or "tap"

@@ -219,6 +219,13 @@ class HipResNetEngine:
         if ws == "auto":
             ws = "0" if (self.f32 and max(self.spec.in_hw) <= 64) else "1"
         self.wg_stream = torch.cuda.Stream(device=self.dev) if ws == "1" else None
+        # the later stages' Winograd weight transforms overlap the first stage's forward on the
+        # side stream; without one they stay on the compute stream (PSX_WINO_WSTREAM=1 gives them
+        # a stream of their own: measured 3.36 vs 3.28 ms/step, a forked branch at the step start
+        # costs more than the overlap returns, r4_numbers.jsonl r4_call23)
+        self.wt_stream = self.wg_stream
+        if self.wt_stream is None and os.environ.get("PSX_WINO_WSTREAM", "0") == "1":
+            self.wt_stream = torch.cuda.Stream(device=self.dev)
         self._wg_batch = None
         self._fins = {}
         # conv-operand unpack: "tiles" (flat grid, fp32 arena or bf16 image source) or "tap"
@@ -503,7 +510,7 @@ class HipResNetEngine:
         if getattr(self, "_wino_wb_key", None) != key:
             convs = [cs for cs in all_convs(self.spec) if cs.name in self.wino_layers]
             hw0 = max((cs.h for cs in convs), default=0)
-            split = self.wg_stream is not None and os.environ.get("PSX_WINO_WSPLIT", "1") == "1"
+            split = self.wt_stream is not None and os.environ.get("PSX_WINO_WSPLIT", "1") == "1"
             early, late = [], []
             self._wino_late = set()
             for cs in convs:
@@ -523,10 +530,13 @@ class HipResNetEngine:
             self._wino_wb()
         self._late_ev = None
         if self._wino_wb_late is not None:
-            with self._side():
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.dev))
+            self.wt_stream.wait_event(ev)
+            with torch.cuda.stream(self.wt_stream):
                 self._wino_wb_late()
                 self._late_ev = torch.cuda.Event()
-                self._late_ev.record(self.wg_stream)
+                self._late_ev.record(self.wt_stream)
 
     _late_ev = None
     _wino_late = frozenset()

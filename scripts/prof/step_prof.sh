@@ -6,3 +6,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/spr
 python scripts/prof/kstats.py gpurun_out/sprof/run_kernel_trace.csv --steps 8 > gpurun_out/sprof.txt
 python scripts/prof/kstats.py gpurun_out/sprof/run_kernel_trace.csv --steps 8 --grid "wino|conv2_kernel|wgrad2f|bn_" > gpurun_out/sprof_grid.txt
 head -45 gpurun_out/sprof.txt
+python scripts/prof/timeline.py gpurun_out/sprof/run_kernel_trace.csv --list > gpurun_out/sprof_timeline.txt

@@ -257,7 +257,10 @@ def test_async_remote_workers(world, topology, native_loop, tmp_path):
     W = world - 1 if topology == "dedicated" else world
     script = tmp_path / "arun.py"
     script.write_text(_ARUN.format(root=ROOT, topo=topology))
-    out = _torchrun(world, [str(script)], extra={"PSX_NATIVE_LOOP": native_loop})
+    # the stand-in's point-to-point is host-synchronous and three processes share one GPU: a
+    # rank whose first steps capture graphs can leave a peer's send unmatched for tens of
+    # seconds (one 60 s timeout seen in ~10 runs), so this test gets a longer deadline
+    out = _torchrun(world, [str(script)], extra={"PSX_NATIVE_LOOP": native_loop, "PSX_FAKECOMM_TIMEOUT_S": "240"})
     recs = [r for r in _json_lines(out, "RESULT ") if r]
     assert len(recs) == 1, out[-3000:]
     gs, processed, checksum, applied, rejected, upd_s, src = recs[0]

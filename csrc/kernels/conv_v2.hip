@@ -1220,6 +1220,11 @@ int conv_dgrad2_t(Conv2Args& a, float* ws, hipStream_t st) {
     // parity classes: each class GEMM covers dx pixels (2i+py, 2j+px), ~1/4 of them
     Plan q = plan_for(IC_fwd, (a.npix + 3) / 4, Kg / KS, sizeof(T) == 4);
     q.splits = 1;
+    // tile sweep overrides (PSX_DGRAD_S2_BN / _WGM / _BM): the classes are short-K GEMMs
+    if (const char* e = getenv("PSX_DGRAD_S2_BN")) q.BN = atoi(e);
+    if (const char* e = getenv("PSX_DGRAD_S2_WGM")) q.WGM = atoi(e);
+    if (const char* e = getenv("PSX_DGRAD_S2_BM")) q.BM = atoi(e);
+    if (IC_fwd % q.BM) q.BM = 64;
     a.n_oc_tiles = IC_fwd / q.BM;
     a.n_pix_tiles = (Nb * ((H + 1) / 2) * ((W + 1) / 2) + q.BN - 1) / q.BN;
     a.splits = 1;

@@ -487,8 +487,8 @@ class HipResNetEngine:
         # main-stream scratch (forward V of layers without a Winograd weight gradient / GEMM output;
         # data-gradient input tiles + GEMM output) and the weight-gradient side stream's own (dy
         # tiles, GEMM partials)
-        if self.wino_layers and self.dev.type == "cuda":
-            K.sk_workspace(self.dev)  # the stream-K GEMM's fixup buffers, before any capture
+        if self.wino_layers and self.dev.type == "cuda" and os.environ.get("PSX_WINO_SK", "0") != "0":
+            K.sk_workspace(self.dev)  # the opt-in stream-K GEMM's fixup buffers, before any capture
         self.wino_s1 = self._f32(max(1, s_main))
         self.wino_s2 = self._f32(max(1, s_main))
         self.wino_wd = self._f32(max(1, s_d))

@@ -80,6 +80,13 @@ struct Conv2Args {
   const float* sshift;
   // WOUT backward: ReLU mask = [y1 * scale + shift > 0] from this affine [2][OC] (nullable: from bo)
   const float* bmaff;
+  // MODE 3 with the block's 1x1 / stride-2 shortcut folded in (nullable in2): the shortcut's data
+  // gradient only reaches the (0, 0) parity class, one tap deep, so that class runs its 3x3 tap
+  // and then the shortcut's as extra k-steps: operand dy_sc (in2, same shape as in) against the
+  // shortcut's data-gradient weights (w2, rows of Kg2) — no separate launch and no residual pass
+  const void* in2;
+  const void* w2;
+  int Kg2;
 };
 
 // Winograd F(4x4,3x3) output transform A^T (wino.hip has the matrices): y = A^T P A
@@ -173,8 +180,9 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   const int r0 = (py + a.pad) & 1, s0 = (px + a.pad) & 1;
   const int nr = r0 < a.R ? (a.R - r0 + 1) >> 1 : 0, nsx = s0 < a.S ? (a.S - s0 + 1) >> 1 : 0;
   const int npix_c = MODE == 3 ? a.Nb * CH * CW : a.npix;
+  const bool sc = MODE == 3 && a.in2 != nullptr && cls == 0;  // class (0, 0) + the folded shortcut
   if (MODE == 3) {
-    nk = (nr * nsx) << (a.log2_icc - 3);
+    nk = (nr * nsx + (sc ? 1 : 0)) << (a.log2_icc - 3);
     if (pix0 >= npix_c) {  // whole workgroup: this class has fewer tiles
       if (!SPLIT && a.det.slab && (a.stats || a.bpart))  // it still arrives at the launch counter
         if (det_finish(a.det, a.bpart ? a.bns : 2, a.OC, a.bpart ? a.bpart : a.stats, pix_t + cls * a.n_pix_tiles,
@@ -430,6 +438,14 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     const int c = lpos ^ ((row >> 1) & 7);
     wsrc[i] = wts + (size_t)(oc0 + row) * a.Kg + c * EPC;
   }
+  const T* wsrc2[MODE == 3 ? LA : 1];
+  if constexpr (MODE == 3) {
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int row = (i * 4 + wid) * 8 + lrow;
+      wsrc2[i] = sc ? (const T*)a.w2 + (size_t)(oc0 + row) * a.Kg2 + (lpos ^ ((row >> 1) & 7)) * EPC : wts;
+    }
+  }
   int nbase[LB], hb[LB], wb[LB], bc[LB];
   bool pv[LB];
 #pragma unroll
@@ -480,6 +496,16 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     if (MODE == 3) {
       const int t = __builtin_amdgcn_readfirstlane(ks >> ksh);
       const int cofs = __builtin_amdgcn_readfirstlane((ks & ((1 << ksh) - 1)) * KS);
+      if (sc && t == nr * nsx) {  // the folded 1x1 / stride-2 shortcut: tap (0, 0) of dy_sc
+#pragma unroll
+        for (int i = 0; i < LA; ++i) glds16(wsrc2[i] + cofs, base + (i * 4 + wid) * 1024);
+#pragma unroll
+        for (int i = 0; i < LB; ++i) {
+          const T* src = pv[i] ? (const T*)a.in2 + (pbase[i] - in) + cofs : zero;
+          glds16(src, base + BM * 128 + (i * 4 + wid) * 1024);
+        }
+        return;
+      }
       const int tr = __builtin_amdgcn_readfirstlane(t / nsx);
       const int r = r0 + 2 * tr, sx = s0 + 2 * (t - tr * nsx);
       const int kg = ((r * a.S + sx) << ksh) + (ks & ((1 << ksh) - 1));  // k-step in the full weights
@@ -1212,11 +1238,14 @@ int conv_dgrad2_t(Conv2Args& a, float* ws, hipStream_t st) {
   a.n_pix_tiles = (a.npix + p.BN - 1) / p.BN;
   a.splits = p.splits;
   a.kps = (Kg / KS + p.splits - 1) / p.splits;
-  if (p.splits > 1 && !ws) return -9;
+  const bool parity = a.stride == 2 && a.log2_icc >= 3 && !getenv("PSX_DGRAD_S2_GATHER");
+  if (p.splits > 1 && !ws && !parity) return -9;  // the parity-class path never splits K
   int e;
   if (a.stride == 1)
     e = res ? dispatch2<T, 1, true>(p, a, st) : dispatch2<T, 1, false>(p, a, st);
-  else if (a.stride == 2 && a.log2_icc >= 3 && !getenv("PSX_DGRAD_S2_GATHER")) {
+  else if (a.in2 && !(a.stride == 2 && a.log2_icc >= 3))
+    return -11;  // the shortcut folds only into the parity-class path
+  else if (parity) {
     // parity classes: each class GEMM covers dx pixels (2i+py, 2j+px), ~1/4 of them
     Plan q = plan_for(IC_fwd, (a.npix + 3) / 4, Kg / KS, sizeof(T) == 4);
     q.splits = 1;
@@ -1282,10 +1311,35 @@ int psx_conv_fwd2(const void* x, const void* wf, void* y, float* stats, const vo
   return f32 ? conv_fwd2_t<float>(a, ws, st) : conv_fwd2_t<uint16_t>(a, ws, st);
 }
 
+int psx_conv_dgrad2_sc(const void* dy, const void* wd, void* dx, const void* res, const void* zero, float* ws,
+                       int Nb, int H, int W, int IC_fwd, int OC_fwd, int R, int S, int stride, int pad, int Kg,
+                       const BwdStatsDesc* bst, int f32, const void* dy_sc, const void* wd_sc, int Kg_sc,
+                       hipStream_t st);
+
 int psx_conv_dgrad2(const void* dy, const void* wd, void* dx, const void* res, const void* zero, float* ws, int Nb,
                     int H, int W, int IC_fwd, int OC_fwd, int R, int S, int stride, int pad, int Kg,
                     const BwdStatsDesc* bst, int f32, hipStream_t st) {
+  return psx_conv_dgrad2_sc(dy, wd, dx, res, zero, ws, Nb, H, W, IC_fwd, OC_fwd, R, S, stride, pad, Kg, bst, f32,
+                            nullptr, nullptr, 0, st);
+}
+
+// psx_conv_dgrad2 of a 3x3 / stride-2 / pad-1 conv with its block's 1x1 / stride-2 / pad-0
+// shortcut folded in: dx = dgrad(dy, wd) + dgrad_sc(dy_sc, wd_sc) in one launch (Conv2Args in2;
+// the parity-class path only). dy_sc: the shortcut's output gradient (the shape of dy), wd_sc:
+// its data-gradient weights, rows of Kg_sc (= OC_fwd). -11: this layer cannot fold (caller runs
+// the two launches).
+int psx_conv_dgrad2_sc(const void* dy, const void* wd, void* dx, const void* res, const void* zero, float* ws,
+                       int Nb, int H, int W, int IC_fwd, int OC_fwd, int R, int S, int stride, int pad, int Kg,
+                       const BwdStatsDesc* bst, int f32, const void* dy_sc, const void* wd_sc, int Kg_sc,
+                       hipStream_t st) {
   Conv2Args a{};
+  if (dy_sc) {
+    if (R != 3 || S != 3 || stride != 2 || pad != 1 || res || Kg_sc != OC_fwd || !wd_sc) return -11;
+    if (getenv("PSX_DGRAD_S2_GATHER")) return -11;
+    a.in2 = dy_sc;
+    a.w2 = wd_sc;
+    a.Kg2 = Kg_sc;
+  }
   if (bst) {
     a.bpart = bst->part;
     a.bo = bst->o;

@@ -219,6 +219,7 @@ class HipResNetEngine:
         if ws == "auto":
             ws = "0" if (self.f32 and max(self.spec.in_hw) <= 64) else "1"
         self.wg_stream = torch.cuda.Stream(device=self.dev) if ws == "1" else None
+        self.fold_sc = os.environ.get("PSX_DGRAD_FOLD_SC", "1") == "1"
         # the later stages' Winograd weight transforms overlap the first stage's forward on the
         # side stream; without one they stay on the compute stream (PSX_WINO_WSTREAM=1 gives them
         # a stream of their own: measured 3.36 vs 3.28 ms/step, a forked branch at the step start
@@ -729,10 +730,18 @@ class HipResNetEngine:
             with self._side():
                 K.wgrad_reduce_batch(batch, 1.0, self.grad_fp16)
 
-    def _dgrad(self, cs: ConvSpec, dy, dx, res=None, bn_next=None):
+    def _dgrad(self, cs: ConvSpec, dy, dx, res=None, bn_next=None, sc=None):
         """bn_next = (BNSpec, o, y, two|None): the BN whose backward consumes dx; with conv v2 its
-        reduction (sum dz, sum dz*xhat) is produced by the dgrad epilogue (PSX_FUSE_BNBWD)."""
+        reduction (sum dz, sum dz*xhat) is produced by the dgrad epilogue (PSX_FUSE_BNBWD).
+        sc = (shortcut ConvSpec, its output gradient): fold the block's 1x1 / stride-2 shortcut
+        data gradient into this 3x3 / stride-2 launch; returns False (nothing launched) when the
+        layer cannot fold."""
         wl = self.wino_layers.get(cs.name)
+        if sc is not None:
+            ds, dys_sc = sc
+            if wl is not None or cs.k != 3 or cs.stride != 2 or cs.pad != 1 or ds.k != 1 or ds.stride != 2 \
+                    or ds.pad != 0 or ds.cp != cs.cp or ds.cout != cs.cout or ds.kgd != cs.cout:
+                return False
         bst = None
         if bn_next is not None and self.fuse_bnbwd:
             bs, o, y, two = bn_next
@@ -759,6 +768,15 @@ class HipResNetEngine:
                             cs.cp, bst=bst)
             return
         wd = self.wbuf[cs.wd_off:cs.wd_off + cs.cp * cs.kgd]
+        if sc is not None:
+            wds = self.wbuf[ds.wd_off:ds.wd_off + ds.cp * ds.kgd]
+            if not K.conv_dgrad2_sc(dy, wd, dx, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.kgd, dys_sc, wds,
+                                    ds.kgd, bst=bst):
+                if bn_next is not None and self.fuse_bnbwd:  # nothing ran: the sums are not produced
+                    self._prereduced.discard(bn_next[0].name)
+                    self._premasked.discard(bn_next[0].name)
+                return False
+            return True
         K.conv_dgrad2(dy, wd, dx, res, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
                       cs.kgd, bst=bst)
 
@@ -1005,8 +1023,12 @@ class HipResNetEngine:
             elif b.down:
                 ds, dbn = b.down
                 self._wgrad(ds, d["inp"], d["dys"])
-                self._dgrad(ds, d["dys"], d["dxs"])
-                self._dgrad(cs, dys[0], d["gin"], res=d["dxs"], bn_next=self._bn_into(j))
+                # the 1x1 / stride-2 shortcut's data gradient folded into the 3x3 / stride-2 one
+                # (PSX_DGRAD_FOLD_SC=0: two launches + a residual pass)
+                if not (self.fold_sc and self._dgrad(cs, dys[0], d["gin"], bn_next=self._bn_into(j),
+                                                     sc=(ds, d["dys"]))):
+                    self._dgrad(ds, d["dys"], d["dxs"])
+                    self._dgrad(cs, dys[0], d["gin"], res=d["dxs"], bn_next=self._bn_into(j))
             else:
                 self._dgrad(cs, dys[0], d["gin"], res=dz, bn_next=self._bn_into(j))
 

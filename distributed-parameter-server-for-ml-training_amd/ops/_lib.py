@@ -48,6 +48,8 @@ _KERNEL_SIGS = {
     "psx_conv_fwd2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp,
                             vp]),
     "psx_conv_dgrad2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp]),
+    "psx_conv_dgrad2_sc": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp,
+                                 vp, i32, vp]),
     "psx_bgemm_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "psx_sk_set_workspace": (i32, [vp, i64, vp, i32]),
     "psx_sk_workspace_floats": (i64, []),

@@ -133,6 +133,20 @@ def conv_dgrad2(dy, wd, dx, res, ws, nb, h, w, ic_fwd, oc_fwd, k, stride, pad, k
                                     C.byref(bst) if bst is not None else None, is_f32(dy), stream_ptr()), "conv_dgrad2")
 
 
+def conv_dgrad2_sc(dy, wd, dx, ws, nb, h, w, ic_fwd, oc_fwd, kgd, dy_sc, wd_sc, kgd_sc,
+                   bst: BwdStatsDesc | None = None) -> bool:
+    """The 3x3 / stride-2 / pad-1 data gradient with the block's 1x1 / stride-2 shortcut folded
+    in: dx = dgrad(dy, wd) + dgrad_sc(dy_sc, wd_sc) in one launch (csrc/kernels/conv_v2.hip
+    psx_conv_dgrad2_sc). False: this layer cannot fold (run the two launches instead)."""
+    rc = kernels().psx_conv_dgrad2_sc(ptr(dy), ptr(wd), ptr(dx), None, ptr(zero_page(dy.device)), ptr(ws), nb, h, w,
+                                      ic_fwd, oc_fwd, 3, 3, 2, 1, kgd, C.byref(bst) if bst is not None else None,
+                                      is_f32(dy), ptr(dy_sc), ptr(wd_sc), kgd_sc, stream_ptr())
+    if rc == -11:
+        return False
+    check(rc, "conv_dgrad2_sc")
+    return True
+
+
 def bgemm_f32(a, b, p, m, n, kd, nb, cfg=0):
     """nb batched fp32 GEMMs p[i] = a[i] @ b[:, i, :].T (a [nb][m][kd], b [n][nb][kd], p [nb][m][n];
     kd a power of two >= 32) on the conv_v2 mainloop (csrc/kernels/conv_v2.hip psx_bgemm_f32)."""

@@ -162,3 +162,23 @@ def test_conv2_tap_reuse(shape, bn, monkeypatch):
     xhat = ((y1.float().reshape(-1, cp) - saved[0]) * saved[1])
     assert torch.allclose(part[:, 0].sum(0), dz.sum(0), rtol=1e-3, atol=5e-2), (shape, bn)
     assert torch.allclose(part[:, 1].sum(0), (dz * xhat).sum(0), rtol=1e-3, atol=5e-2), (shape, bn)
+
+
+@pytest.mark.parametrize("shape", [(128, 64, 128, 32), (128, 128, 256, 16), (128, 256, 512, 8), (8, 128, 256, 28)])
+def test_conv_dgrad2_shortcut_fold(shape):
+    """bf16: the 3x3/s2 data gradient + the folded 1x1/s2 shortcut data gradient in one launch
+    (psx_conv_dgrad2_sc) against torch fp32 of both convs summed."""
+    torch.manual_seed(7)
+    n, cin, cout, hw = shape
+    w = (torch.randn(cout, cin, 3, 3, device=DEV) / (cin * 9) ** 0.5).to(torch.bfloat16).float()
+    w2 = (torch.randn(cout, cin, 1, 1, device=DEV) / cin ** 0.5).to(torch.bfloat16).float()
+    _, wd, cp, _, kgd = make_operands(w)
+    _, wd2, _, _, kgd2 = make_operands(w2)
+    oh = (hw - 1) // 2 + 1
+    dy = torch.randn(n, cout, oh, oh, device=DEV).to(torch.bfloat16).float()
+    dy2 = torch.randn(n, cout, oh, oh, device=DEV).to(torch.bfloat16).float()
+    ref = torch.nn.grad.conv2d_input((n, cin, hw, hw), w, dy, stride=2, padding=1)
+    ref = (ref + torch.nn.grad.conv2d_input((n, cin, hw, hw), w2, dy2, stride=2)).permute(0, 2, 3, 1)
+    dx = torch.empty(n, hw, hw, cp, dtype=torch.bfloat16, device=DEV)
+    assert K.conv_dgrad2_sc(to_nhwc(dy, cout), wd, dx, None, n, hw, hw, cp, cout, kgd, to_nhwc(dy2, cout), wd2, kgd2)
+    assert _rel(dx[..., :cin], ref) < 1e-2, shape

@@ -360,3 +360,40 @@ def test_bn_statistics_large_mean_shifted_sums(f32):
             assert ((rv.double() - (0.9 + 0.1 * unb)).abs() / unb).max().item() < 1e-5
     print("bn statistics mean / variance error:", errs)
     assert errs["shifted"][0] < 1e-5 and errs["shifted"][1] < 2e-5, errs
+
+
+@pytest.mark.parametrize("shape", [(16, 64, 128, 32), (128, 128, 256, 16), (16, 256, 512, 8), (4, 64, 128, 14)])
+@pytest.mark.parametrize("stats", [False, True])
+def test_conv_dgrad2_shortcut_fold_f32(shape, stats):
+    """3x3/s2 data gradient with the block's 1x1/s2 shortcut data gradient folded into the (0, 0)
+    parity class (conv_v2.hip psx_conv_dgrad2_sc) against torch fp64 of both convs summed."""
+    torch.manual_seed(6)
+    n, cin, cout, hw = shape
+    w = torch.randn(cout, cin, 3, 3, device=DEV) / (cin * 9) ** 0.5
+    w2 = torch.randn(cout, cin, 1, 1, device=DEV) / cin ** 0.5
+    _, wd, cp, _, kgd = operands_f32(w)
+    _, wd2, _, _, kgd2 = operands_f32(w2)
+    oh = (hw - 1) // 2 + 1
+    dy, dy2 = torch.randn(n, cout, oh, oh, device=DEV), torch.randn(n, cout, oh, oh, device=DEV)
+    ref = torch.nn.grad.conv2d_input((n, cin, hw, hw), w.double(), dy.double(), stride=2, padding=1)
+    ref = (ref + torch.nn.grad.conv2d_input((n, cin, hw, hw), w2.double(), dy2.double(), stride=2)).permute(0, 2, 3, 1)
+    dx = torch.full((n, hw, hw, cp), float("nan"), device=DEV)
+    bst = None
+    if stats:
+        o = torch.randn(n, hw, hw, cp, device=DEV)
+        y1 = torch.randn(n, hw, hw, cp, device=DEV)
+        saved = torch.stack([0.1 * torch.randn(cp, device=DEV), 1.0 + torch.rand(cp, device=DEV)])
+        part = torch.zeros(K.STAT_SLOTS, 2, cp, device=DEV)
+        bst = K.bwd_stats_desc(part, o, y1, saved)
+    assert K.conv_dgrad2_sc(nhwc(dy, cout), wd, dx, None, n, hw, hw, cp, cout, kgd, nhwc(dy2, cout), wd2, kgd2, bst=bst)
+    assert _rel(dx[..., :cin], ref) < TOL, shape
+    if stats:
+        dz = (dx.double() * (o > 0)).reshape(-1, cp)
+        xhat = (y1.double().reshape(-1, cp) - saved[0].double()) * saved[1].double()
+        assert torch.allclose(part[:, 0].double().sum(0), dz.sum(0), rtol=1e-4, atol=1e-3)
+        assert torch.allclose(part[:, 1].double().sum(0), (dz * xhat).sum(0), rtol=1e-4, atol=1e-3)
+    # shapes the fold does not cover report False (the caller runs the two launches)
+    w1 = torch.randn(cout, cin, 1, 1, device=DEV)
+    _, wd1, _, _, kgd1 = operands_f32(w1)
+    assert not K.conv_dgrad2_sc(nhwc(dy, cout), wd, dx, None, n, hw, hw, cp, cout, kgd, nhwc(dy2, cout), wd1,
+                                kgd1 + 1)

@@ -87,6 +87,14 @@ struct Conv2Args {
   const void* in2;
   const void* w2;
   int Kg2;
+  // MODE 0 with the block's 1x1 / stride-2 shortcut folded in (nullable out2): output-channel
+  // tiles n_oc1.. compute the shortcut — its input pixel (2i, 2j) is the 3x3 / stride-2 / pad-1
+  // conv's centre tap, so those tiles run only that tap's k-steps against the shortcut weights
+  // (w2, rows of Kg2) into out2 with the statistics stats2 (shift sshift2): one launch, x read once
+  void* out2;
+  float* stats2;
+  const float* sshift2;
+  int n_oc1;
 };
 
 // Winograd F(4x4,3x3) output transform A^T (wino.hip has the matrices): y = A^T P A
@@ -165,10 +173,20 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   const int nwg = a.n_oc_tiles * a.n_pix_tiles;
   const int tile = xcd_remap(blockIdx.x, nwg);
   const int oc_t = tile % a.n_oc_tiles, pix_t = tile / a.n_oc_tiles;
-  const int oc0 = oc_t * BM, pix0 = pix_t * BN;
+  const bool fsc = MODE == 0 && !SPLIT && !TAPR && !WOUT && a.out2 != nullptr && oc_t >= a.n_oc1;
+  if (fsc) {  // a folded-shortcut tile (Conv2Args out2)
+    a.out = a.out2;
+    a.stats = a.stats2;
+    a.sshift = a.sshift2;
+  }
+  const int oc0 = (fsc ? oc_t - a.n_oc1 : oc_t) * BM, pix0 = pix_t * BN;
   const int split = SPLIT ? blockIdx.y : 0;
-  const int ks0 = split * a.kps;
+  int ks0 = split * a.kps;
   int nk = SPLIT ? min(a.kps, a.Kg / KS - ks0) : a.Kg / KS;
+  if (fsc) {  // the centre tap (1, 1) only
+    ks0 = 4 << (a.log2_icc - 3);
+    nk = 1 << (a.log2_icc - 3);
+  }
   // MODE 3 = stride-2 dgrad, one parity class (py, px) of dx per blockIdx.y: dx(2i+py, 2j+px)
   // only receives taps r = r0, r0+2, .. and s = s0, s0+2, .. (r0 = (py+pad)&1), i.e. a dense
   // GEMM over 1, 2, 2 or 4 of the 9 taps instead of 9 with 3/4 of the products zero.
@@ -437,6 +455,8 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     const int row = (i * 4 + wid) * 8 + lrow;
     const int c = lpos ^ ((row >> 1) & 7);
     wsrc[i] = wts + (size_t)(oc0 + row) * a.Kg + c * EPC;
+    // shortcut rows: k-step kglob of the centre tap = row k-step kglob - ks0 of w2
+    if (fsc) wsrc[i] = (const T*)a.w2 + (size_t)(oc0 + row) * a.Kg2 + c * EPC - (ptrdiff_t)ks0 * KS;
   }
   const T* wsrc2[MODE == 3 ? LA : 1];
   if constexpr (MODE == 3) {
@@ -1315,6 +1335,46 @@ int psx_conv_dgrad2_sc(const void* dy, const void* wd, void* dx, const void* res
                        int Nb, int H, int W, int IC_fwd, int OC_fwd, int R, int S, int stride, int pad, int Kg,
                        const BwdStatsDesc* bst, int f32, const void* dy_sc, const void* wd_sc, int Kg_sc,
                        hipStream_t st);
+
+// psx_conv_fwd2 of a 3x3 / stride-2 / pad-1 conv with its block's 1x1 / stride-2 / pad-0 shortcut
+// (same input x, same output channels) folded into the launch (Conv2Args out2): y = conv(x, wf)
+// with stats, y_sc = conv_sc(x, wf_sc) with stats_sc. No in-launch BN finalize, no deterministic
+// mode, and only where the 3x3 conv's own plan needs no split-K. -11: this layer cannot fold (the
+// caller runs the two launches).
+int psx_conv_fwd2_sc(const void* x, const void* wf, void* y, float* stats, const void* zero, int Nb, int H, int W,
+                     int IC, int OC, int Kg, int f32, const float* sshift, const void* wf_sc, int Kg_sc, void* y_sc,
+                     float* stats_sc, const float* sshift_sc, hipStream_t st) {
+  const int KS = f32 ? kKS<float> : kKS<uint16_t>, EPC = f32 ? kEPC<float> : kEPC<uint16_t>;
+  if (det_enabled() || !wf_sc || !y_sc || (stats == nullptr) != (stats_sc == nullptr)) return -11;
+  if (IC < 8 * EPC || (IC & (IC - 1)) || OC % 64 || Kg != 9 * IC || Kg_sc != IC || Kg % KS) return -11;
+  Conv2Args a{};
+  a.in = x;
+  a.w = wf;
+  a.out = y;
+  a.stats = stats;
+  a.sshift = sshift;
+  a.zero = zero;
+  a.w2 = wf_sc;
+  a.Kg2 = Kg_sc;
+  a.out2 = y_sc;
+  a.stats2 = stats_sc;
+  a.sshift2 = sshift_sc;
+  a.Nb = Nb; a.IH = H; a.IW = W; a.IC = IC;
+  a.OH = (H - 1) / 2 + 1;
+  a.OW = (W - 1) / 2 + 1;
+  a.OC = OC; a.R = 3; a.S = 3; a.pad = 1; a.stride = 2;
+  a.Kg = Kg;
+  a.npix = Nb * a.OH * a.OW;
+  a.log2_icc = ilog2i(IC / EPC);
+  const Plan p = plan_for(OC, a.npix, Kg / KS, f32 != 0);
+  if (p.splits > 1) return -11;
+  a.n_oc1 = OC / p.BM;
+  a.n_oc_tiles = 2 * a.n_oc1;
+  a.n_pix_tiles = (a.npix + p.BN - 1) / p.BN;
+  a.splits = 1;
+  a.kps = Kg / KS;
+  return f32 ? dispatch2<float, 0, false>(p, a, st) : dispatch2<uint16_t, 0, false>(p, a, st);
+}
 
 int psx_conv_dgrad2(const void* dy, const void* wd, void* dx, const void* res, const void* zero, float* ws, int Nb,
                     int H, int W, int IC_fwd, int OC_fwd, int R, int S, int stride, int pad, int Kg,

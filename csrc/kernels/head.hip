@@ -44,6 +44,7 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ act, in
   // global average pool, 2 channels per thread per pass (coalesced pair loads)
   for (int c = 2 * tid; c < C; c += 512) {
     float s0 = 0.f, s1 = 0.f;
+#pragma unroll 16
     for (int p = 0; p < HW; ++p) {
       float v0, v1;
       ld2(a + (size_t)p * C + c, v0, v1);
@@ -66,6 +67,8 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ act, in
     const float4* w4 = reinterpret_cast<const float4*>(fcw + (size_t)r * C + part * len);
     const float* x = sp + part * len;
     float s = 0.f;
+    // unrolled: the row's L2 loads are issued back to back instead of one latency per step
+#pragma unroll 8
     for (int j = 0; j < (len >> 2); ++j) {
       const float4 w = w4[j];
       s += w.x * x[4 * j] + w.y * x[4 * j + 1] + w.z * x[4 * j + 2] + w.w * x[4 * j + 3];
@@ -117,6 +120,7 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ act, in
   // dpooled[c] = sum_k dlogits[k] * W[k][c]; dact = dpooled / HW broadcast over the pixels
   for (int c = 2 * tid; c < C; c += 512) {
     float s0 = 0.f, s1 = 0.f;
+#pragma unroll 10
     for (int k = 0; k < K; ++k) {
       const float2 w = *reinterpret_cast<const float2*>(fcw + (size_t)k * C + c);
       s0 += sl[k] * w.x;
@@ -135,6 +139,7 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ act, in
       const float m0 = bs.saved1[c], i0 = bs.saved1[C + c], m1 = bs.saved1[c + 1], i1 = bs.saved1[C + c + 1];
       const T* y = reinterpret_cast<const T*>(bs.y1) + (size_t)b * HW * C + c;
       float z0 = 0.f, z1 = 0.f, x0 = 0.f, x1 = 0.f;
+#pragma unroll 8
       for (int p = 0; p < HW; ++p) {
         float o0, o1, y0, y1v;
         ld2(a + (size_t)p * C + c, o0, o1);
@@ -346,6 +351,7 @@ __global__ __launch_bounds__(256) void head_wgrad_small_kernel(const float* __re
   if (k >= K) return;
   float acc = 0.f, accb = 0.f;
   if (c < C) {
+#pragma unroll 16
     for (int bb = 0; bb < B; ++bb) acc += sdl4[bb * 4 + kk] * pooled[(size_t)bb * C + c];
     const float v = acc * gscale;
     if constexpr (sizeof(GT) == 2)

@@ -220,6 +220,11 @@ class HipResNetEngine:
             ws = "0" if (self.f32 and max(self.spec.in_hw) <= 64) else "1"
         self.wg_stream = torch.cuda.Stream(device=self.dev) if ws == "1" else None
         self.fold_sc = os.environ.get("PSX_DGRAD_FOLD_SC", "1") == "1"
+        # the forward twin (opt-in): the 1x1 / stride-2 shortcut conv as extra output-channel tiles
+        # of the 3x3 / stride-2 conv's launch (conv_v2.hip psx_conv_fwd2_sc). Measured slower in
+        # fp32 (+45 us/step: a shortcut tile's epilogue costs ~30 % of a 3x3 tile, so the folded
+        # grid packs worse than two launches) and neutral in bf16 (profiles/r4_numbers.jsonl r4_call31)
+        self.fold_fwd_sc = os.environ.get("PSX_FWD_FOLD_SC", "0") == "1"
         # the later stages' Winograd weight transforms overlap the first stage's forward on the
         # side stream; without one they stay on the compute stream (PSX_WINO_WSTREAM=1 gives them
         # a stream of their own: measured 3.36 vs 3.28 ms/step, a forked branch at the step start
@@ -618,6 +623,33 @@ class HipResNetEngine:
         elif fin is None and not self._fold:
             self._bn_train(bs, arena, self.nslots, npix)
 
+    def _conv_bn_fwd_sc(self, cs: ConvSpec, ds: ConvSpec, x, y, ys, bs: BNSpec, dbn: BNSpec, arena,
+                        train: bool) -> bool:
+        """_conv_bn_fwd of a downsampling block's 3x3 / stride-2 conv and its 1x1 / stride-2
+        shortcut in one launch; False (nothing launched): run them separately."""
+        if not self.fold_fwd_sc or (train and self.fuse_fin) or cs.name in self.wino_layers:
+            return False
+        if (cs.k, cs.stride, cs.pad, ds.k, ds.stride, ds.pad) != (3, 2, 1, 1, 2, 0):
+            return False
+        if ds.cout != cs.cout or ds.cp != cs.cp or (ds.h, ds.w) != (cs.h, cs.w):
+            return False
+        wf = self.wbuf[cs.wf_off:cs.wf_off + cs.cout * cs.kg]
+        wfs = self.wbuf[ds.wf_off:ds.wf_off + ds.cout * ds.kg]
+        stats = self._red(bs, "fwd") if train else None
+        stats2 = self._red(dbn, "fwd") if train else None
+        sh = self.bn[bs.name]["sshift"] if train else None
+        sh2 = self.bn[dbn.name]["sshift"] if train else None
+        if not K.conv_fwd2_sc(x, wf, y, stats, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.kg, wfs, ds.kg, ys, stats2,
+                              sshift=sh, sshift_sc=sh2):
+            return False
+        npix = self.B * cs.out_hw[0] * cs.out_hw[1]
+        for b in (bs, dbn):
+            if not train:
+                self._bn_eval(b, arena)
+            elif not self._fold:
+                self._bn_train(b, arena, self.nslots, npix)
+        return True
+
     @property
     def _fold(self) -> bool:
         return self.fin_apply and not self.fuse_fin
@@ -917,8 +949,13 @@ class HipResNetEngine:
             src = d["inp"]
             L = len(b.convs)
             bn_in = None
+            folded = False
             for i, cs in enumerate(b.convs):
-                self._conv_bn_fwd(cs, src, d["y"][i], b.bns[i], arena, train, bn_in=bn_in)
+                if i == 0 and b.down and self._conv_bn_fwd_sc(cs, b.down[0], src, d["y"][0], d["ys"], b.bns[0],
+                                                              b.down[1], arena, train):
+                    folded = True
+                else:
+                    self._conv_bn_fwd(cs, src, d["y"][i], b.bns[i], arena, train, bn_in=bn_in)
                 bn_in = None
                 if i < L - 1:
                     bs = b.bns[i]
@@ -931,7 +968,8 @@ class HipResNetEngine:
                     src = d["a"][i]
             if b.down:
                 ds, dbn = b.down
-                self._conv_bn_fwd(ds, d["inp"], d["ys"], dbn, arena, train)
+                if not folded:
+                    self._conv_bn_fwd(ds, d["inp"], d["ys"], dbn, arena, train)
                 self._apply(b.bns[-1], d["y"][-1], d["out"], arena, train, res=d["ys"], bs2=dbn)
             else:
                 self._apply(b.bns[-1], d["y"][-1], d["out"], arena, train, res=d["inp"])

@@ -108,6 +108,21 @@ def conv_fwd2(x, wf, y, stats, ws, nb, h, w, ic, oc, k, stride, pad, kg, fin: Bn
                                   is_f32(x), ptr(sshift), stream_ptr()), "conv_fwd2")
 
 
+def conv_fwd2_sc(x, wf, y, stats, nb, h, w, ic, oc, kg, wf_sc, kg_sc, y_sc, stats_sc, sshift=None,
+                 sshift_sc=None) -> bool:
+    """A 3x3 / stride-2 / pad-1 conv and its block's 1x1 / stride-2 shortcut (same x, same output
+    channels) in one launch: y = conv(x, wf) with stats, y_sc = conv_sc(x, wf_sc) with stats_sc
+    (csrc/kernels/conv_v2.hip psx_conv_fwd2_sc). False: this layer cannot fold (run the two
+    launches instead)."""
+    rc = kernels().psx_conv_fwd2_sc(ptr(x), ptr(wf), ptr(y), ptr(stats), ptr(zero_page(x.device)), nb, h, w, ic, oc,
+                                    kg, is_f32(x), ptr(sshift), ptr(wf_sc), kg_sc, ptr(y_sc), ptr(stats_sc),
+                                    ptr(sshift_sc), stream_ptr())
+    if rc == -11:
+        return False
+    check(rc, "conv_fwd2_sc")
+    return True
+
+
 class BwdStatsDesc(C.Structure):
     """csrc/kernels/conv_v2.hip BwdStatsDesc: fused BN-backward reduction over a dgrad output."""
     _fields_ = [("part", C.c_void_p), ("o", C.c_void_p), ("y1", C.c_void_p), ("y2", C.c_void_p),

@@ -182,3 +182,28 @@ def test_conv_dgrad2_shortcut_fold(shape):
     dx = torch.empty(n, hw, hw, cp, dtype=torch.bfloat16, device=DEV)
     assert K.conv_dgrad2_sc(to_nhwc(dy, cout), wd, dx, None, n, hw, hw, cp, cout, kgd, to_nhwc(dy2, cout), wd2, kgd2)
     assert _rel(dx[..., :cin], ref) < 1e-2, shape
+
+
+@pytest.mark.parametrize("shape", [(128, 64, 128, 32), (128, 128, 256, 16), (8, 128, 256, 28)])
+def test_conv_fwd2_shortcut_fold(shape):
+    """bf16: 3x3/s2 conv + the folded 1x1/s2 shortcut conv in one launch (psx_conv_fwd2_sc), both
+    outputs and BN statistics against torch fp32."""
+    torch.manual_seed(9)
+    n, cin, cout, hw = shape
+    x = torch.randn(n, cin, hw, hw, device=DEV).to(torch.bfloat16).float()
+    w = (torch.randn(cout, cin, 3, 3, device=DEV) / (cin * 9) ** 0.5).to(torch.bfloat16).float()
+    w2 = (torch.randn(cout, cin, 1, 1, device=DEV) / cin ** 0.5).to(torch.bfloat16).float()
+    wf, _, cp, kg, _ = make_operands(w)
+    wf2, _, _, kg2, _ = make_operands(w2)
+    oh = (hw - 1) // 2 + 1
+    y = torch.empty(n, oh, oh, cout, dtype=torch.bfloat16, device=DEV)
+    ys = torch.empty(n, oh, oh, cout, dtype=torch.bfloat16, device=DEV)
+    st, st2 = torch.zeros(K.STAT_SLOTS, 2, cout, device=DEV), torch.zeros(K.STAT_SLOTS, 2, cout, device=DEV)
+    if not K.conv_fwd2_sc(to_nhwc(x, cp), wf, y, st, n, hw, hw, cp, cout, kg, wf2, kg2, ys, st2):
+        pytest.skip("the planner splits K on this layer: not folded")
+    assert _rel(y, F.conv2d(x, w, stride=2, padding=1).permute(0, 2, 3, 1)) < 1e-2, shape
+    assert _rel(ys, F.conv2d(x, w2, stride=2).permute(0, 2, 3, 1)) < 1e-2, shape
+    for out, s in ((y, st), (ys, st2)):
+        q = out.float().reshape(-1, cout)
+        assert torch.allclose(s[:, 0].sum(0), q.sum(0), rtol=1e-3, atol=5e-2), shape
+        assert torch.allclose(s[:, 1].sum(0), (q * q).sum(0), rtol=1e-3, atol=5e-2), shape

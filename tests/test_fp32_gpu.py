@@ -397,3 +397,30 @@ def test_conv_dgrad2_shortcut_fold_f32(shape, stats):
     _, wd1, _, _, kgd1 = operands_f32(w1)
     assert not K.conv_dgrad2_sc(nhwc(dy, cout), wd, dx, None, n, hw, hw, cp, cout, kgd, nhwc(dy2, cout), wd1,
                                 kgd1 + 1)
+
+
+@pytest.mark.parametrize("shape", [(16, 64, 128, 32), (128, 128, 256, 16), (4, 64, 128, 14)])
+def test_conv_fwd2_shortcut_fold_f32(shape):
+    """3x3/s2 conv + the block's 1x1/s2 shortcut conv in one launch (conv_v2.hip psx_conv_fwd2_sc):
+    both outputs and both shifted BN statistics against torch fp64."""
+    torch.manual_seed(8)
+    n, cin, cout, hw = shape
+    x = torch.randn(n, cin, hw, hw, device=DEV)
+    w = torch.randn(cout, cin, 3, 3, device=DEV) / (cin * 9) ** 0.5
+    w2 = torch.randn(cout, cin, 1, 1, device=DEV) / cin ** 0.5
+    wf, _, cp, kg, _ = operands_f32(w)
+    wf2, _, _, kg2, _ = operands_f32(w2)
+    oh = (hw - 1) // 2 + 1
+    y = torch.full((n, oh, oh, cout), float("nan"), device=DEV)
+    ys = torch.full((n, oh, oh, cout), float("nan"), device=DEV)
+    st, st2 = torch.zeros(K.STAT_SLOTS, 2, cout, device=DEV), torch.zeros(K.STAT_SLOTS, 2, cout, device=DEV)
+    sh, sh2 = 0.1 * torch.randn(cout, device=DEV), 0.1 * torch.randn(cout, device=DEV)
+    if not K.conv_fwd2_sc(nhwc(x, cp), wf, y, st, n, hw, hw, cp, cout, kg, wf2, kg2, ys, st2, sshift=sh, sshift_sc=sh2):
+        pytest.skip("the planner splits K on this layer: not folded")
+    ref = F.conv2d(x.double(), w.double(), stride=2, padding=1).permute(0, 2, 3, 1)
+    ref2 = F.conv2d(x.double(), w2.double(), stride=2).permute(0, 2, 3, 1)
+    assert _rel(y, ref) < TOL and _rel(ys, ref2) < TOL, shape
+    for out, s, k in ((y, st, sh), (ys, st2, sh2)):
+        d = out.double().reshape(-1, cout) - k.double()
+        assert torch.allclose(s[:, 0].double().sum(0), d.sum(0), rtol=1e-4, atol=1e-2)
+        assert torch.allclose(s[:, 1].double().sum(0), (d * d).sum(0), rtol=1e-4, atol=1e-2)

@@ -225,6 +225,11 @@ class HipResNetEngine:
         # fp32 (+45 us/step: a shortcut tile's epilogue costs ~30 % of a 3x3 tile, so the folded
         # grid packs worse than two launches) and neutral in bf16 (profiles/r4_numbers.jsonl r4_call31)
         self.fold_fwd_sc = os.environ.get("PSX_FWD_FOLD_SC", "0") == "1"
+        # the CIFAR stem on the direct vector-ALU kernel (csrc/kernels/stem.hip): fp32 27.4 -> 19.5 us
+        # in isolation (bench/stem_probe.py); step A/B within noise, bf16 unmeasured in isolation, so
+        # "auto" = fp32 only
+        sd = os.environ.get("PSX_STEM_DIRECT", "auto")
+        self.stem_direct = sd == "1" or (sd == "auto" and self.f32)
         # the later stages' Winograd weight transforms overlap the first stage's forward on the
         # side stream; without one they stay on the compute stream (PSX_WINO_WSTREAM=1 gives them
         # a stream of their own: measured 3.36 vs 3.28 ms/step, a forked branch at the step start
@@ -616,8 +621,10 @@ class HipResNetEngine:
             elif not self._fold:  # no in-launch finalize on this path
                 self._bn_train(bs, arena, self.nslots, npix)
             return
-        K.conv_fwd2(x, wf, y, stats, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
-                    cs.kg, fin=fin, sshift=sshift)
+        if not (self.stem_direct and fin is None and cs.cin == 3 and (cs.k, cs.stride, cs.pad) == (3, 1, 1)
+                and K.stem_conv(x, wf, y, stats, self.B, cs.h, cs.w, cs.cin, cs.cp, cs.cout, cs.kg, sshift=sshift)):
+            K.conv_fwd2(x, wf, y, stats, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
+                        cs.kg, fin=fin, sshift=sshift)
         if not train:
             self._bn_eval(bs, arena)
         elif fin is None and not self._fold:

@@ -123,6 +123,18 @@ def conv_fwd2_sc(x, wf, y, stats, nb, h, w, ic, oc, kg, wf_sc, kg_sc, y_sc, stat
     return True
 
 
+def stem_conv(x, wf, y, stats, nb, h, w, cin, cp, oc, kg, sshift=None) -> bool:
+    """The CIFAR stem (3 -> 64, 3x3 / stride 1 / pad 1) as a direct vector-ALU conv with its BN
+    statistics (csrc/kernels/stem.hip), same operands as conv_fwd2. False: not this shape or
+    deterministic mode (run conv_fwd2 instead)."""
+    rc = kernels().psx_stem_conv(ptr(x), ptr(wf), ptr(y), ptr(stats), ptr(sshift), nb, h, w, cin, cp, oc, kg,
+                                 is_f32(x), stream_ptr())
+    if rc == -11:
+        return False
+    check(rc, "stem_conv")
+    return True
+
+
 class BwdStatsDesc(C.Structure):
     """csrc/kernels/conv_v2.hip BwdStatsDesc: fused BN-backward reduction over a dgrad output."""
     _fields_ = [("part", C.c_void_p), ("o", C.c_void_p), ("y1", C.c_void_p), ("y2", C.c_void_p),

@@ -188,6 +188,7 @@ def test_conv_dgrad2_shortcut_fold(shape):
 def test_conv_fwd2_shortcut_fold(shape):
     """bf16: 3x3/s2 conv + the folded 1x1/s2 shortcut conv in one launch (psx_conv_fwd2_sc), both
     outputs and BN statistics against torch fp32."""
+    K.set_deterministic(None)  # an earlier engine test may have left the process in deterministic mode
     torch.manual_seed(9)
     n, cin, cout, hw = shape
     x = torch.randn(n, cin, hw, hw, device=DEV).to(torch.bfloat16).float()
@@ -207,3 +208,20 @@ def test_conv_fwd2_shortcut_fold(shape):
         q = out.float().reshape(-1, cout)
         assert torch.allclose(s[:, 0].sum(0), q.sum(0), rtol=1e-3, atol=5e-2), shape
         assert torch.allclose(s[:, 1].sum(0), (q * q).sum(0), rtol=1e-3, atol=5e-2), shape
+
+
+def test_stem_conv_direct():
+    """bf16: the direct stem conv (stem.hip) and its BN statistics against torch fp32."""
+    K.set_deterministic(None)  # an earlier engine test may have left the process in deterministic mode
+    torch.manual_seed(11)
+    n = 64
+    x = torch.randn(n, 3, 32, 32, device=DEV).to(torch.bfloat16).float()
+    w = (torch.randn(64, 3, 3, 3, device=DEV) / 27 ** 0.5).to(torch.bfloat16).float()
+    wf, _, cp, kg, _ = make_operands(w)
+    y = torch.empty(n, 32, 32, 64, dtype=torch.bfloat16, device=DEV)
+    st = torch.zeros(K.STAT_SLOTS, 2, 64, device=DEV)
+    assert K.stem_conv(to_nhwc(x, cp), wf, y, st, n, 32, 32, 3, cp, 64, kg)
+    assert _rel(y, F.conv2d(x, w, padding=1).permute(0, 2, 3, 1)) < 1e-2
+    q = y.float().reshape(-1, 64)
+    assert torch.allclose(st[:, 0].sum(0), q.sum(0), rtol=1e-3, atol=5e-2)
+    assert torch.allclose(st[:, 1].sum(0), (q * q).sum(0), rtol=1e-3, atol=5e-2)

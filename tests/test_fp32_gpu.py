@@ -403,6 +403,7 @@ def test_conv_dgrad2_shortcut_fold_f32(shape, stats):
 def test_conv_fwd2_shortcut_fold_f32(shape):
     """3x3/s2 conv + the block's 1x1/s2 shortcut conv in one launch (conv_v2.hip psx_conv_fwd2_sc):
     both outputs and both shifted BN statistics against torch fp64."""
+    K.set_deterministic(None)  # an earlier engine test may have left the process in deterministic mode
     torch.manual_seed(8)
     n, cin, cout, hw = shape
     x = torch.randn(n, cin, hw, hw, device=DEV)
@@ -424,3 +425,24 @@ def test_conv_fwd2_shortcut_fold_f32(shape):
         d = out.double().reshape(-1, cout) - k.double()
         assert torch.allclose(s[:, 0].double().sum(0), d.sum(0), rtol=1e-4, atol=1e-2)
         assert torch.allclose(s[:, 1].double().sum(0), (d * d).sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("n", [128, 3])
+def test_stem_conv_direct_f32(n):
+    """The direct stem conv (csrc/kernels/stem.hip, 3 -> 64, 3x3/s1) and its shifted BN statistics
+    against torch fp64; n = 3 leaves a partial last workgroup."""
+    K.set_deterministic(None)  # an earlier engine test may have left the process in deterministic mode
+    torch.manual_seed(10)
+    x = torch.randn(n, 3, 32, 32, device=DEV)
+    w = torch.randn(64, 3, 3, 3, device=DEV) / 27 ** 0.5
+    wf, _, cp, kg, _ = operands_f32(w)
+    y = torch.full((n, 32, 32, 64), float("nan"), device=DEV)
+    st = torch.zeros(K.STAT_SLOTS, 2, 64, device=DEV)
+    sh = 0.1 * torch.randn(64, device=DEV)
+    assert K.stem_conv(nhwc(x, cp), wf, y, st, n, 32, 32, 3, cp, 64, kg, sshift=sh)
+    ref = F.conv2d(x.double(), w.double(), padding=1).permute(0, 2, 3, 1)
+    assert _rel(y, ref) < TOL
+    d = y.double().reshape(-1, 64) - sh.double()
+    assert torch.allclose(st[:, 0].double().sum(0), d.sum(0), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(st[:, 1].double().sum(0), (d * d).sum(0), rtol=1e-4, atol=1e-2)
+    assert not K.stem_conv(nhwc(x, cp), wf, y, st, n, 32, 32, 4, cp, 64, kg)  # not the stem shape

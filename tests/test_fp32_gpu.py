@@ -243,6 +243,19 @@ def test_augment_and_maxpool_f32():
     arg = torch.empty(2, 8, 8, 64, dtype=torch.uint8, device=DEV)
     K.maxpool3s2_fwd(x, y, arg)
     assert torch.equal(y, F.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1))
+    # backward (2x2-block gather) against torch's max-pool autograd, odd sizes included
+    for (b, h, w, c) in ((2, 16, 16, 64), (3, 7, 9, 16), (2, 112, 112, 64)):
+        x = torch.randn(b, h, w, c, device=DEV)
+        oh, ow = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+        y = torch.empty(b, oh, ow, c, device=DEV)
+        arg = torch.empty(b, oh, ow, c, dtype=torch.uint8, device=DEV)
+        K.maxpool3s2_fwd(x, y, arg)
+        xr = x.permute(0, 3, 1, 2).clone().requires_grad_(True)
+        dy = torch.randn(b, oh, ow, c, device=DEV)
+        F.max_pool2d(xr, 3, 2, 1).backward(dy.permute(0, 3, 1, 2))
+        dx = torch.full_like(x, float("nan"))
+        K.maxpool3s2_bwd(dy, arg, dx)
+        assert torch.allclose(dx, xr.grad.permute(0, 2, 3, 1), atol=1e-5, rtol=1e-6), (b, h, w, c)
 
 
 # Bars of the whole-step test RELATIVE to torch's own fp32 autograd error against the same fp64

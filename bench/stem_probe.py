@@ -4,6 +4,7 @@ operand, against the same GEMM as a 1x1 conv over a pre-built 32-channel im2col 
 the output-store floor (a 128 x 32 x 32 x 64 tensor copy). One JSON line per variant.
 
   python bench/stem_probe.py
+  BF16=1 python bench/stem_probe.py   # bf16 operands: conv_v2 tiles and the direct kernel only
 """
 import json
 import os
@@ -45,9 +46,14 @@ def main():
     torch.manual_seed(0)
     x = torch.randn(B, 3, hw, hw, device="cuda")
     w = torch.randn(cout, 3, 3, 3, device="cuda") / 27 ** 0.5
-    wf, _, cp, kg, _ = operands_f32(w)
-    xh = nhwc(x, cp)
-    y = torch.empty(B, hw, hw, cout, device="cuda")
+    if dt == torch.bfloat16:  # BF16=1: the bf16 operands (8-channel chunks)
+        from tests.test_kernels_gpu import make_operands, to_nhwc
+        wf, _, cp, kg, _ = make_operands(w)
+        xh = to_nhwc(x, cp)
+    else:
+        wf, _, cp, kg, _ = operands_f32(w)
+        xh = nhwc(x, cp)
+    y = torch.empty(B, hw, hw, cout, device="cuda", dtype=dt)
     stats = torch.zeros(K.STAT_SLOTS, 2, cout, device="cuda")
     ws = torch.empty(max(4, K.conv2_workspace_bytes(B, hw, hw, cout, kg, True)) // 4, device="cuda")
     for t in [None, (64, 128, 2), (64, 64, 2), (64, 256, 1), (64, 128, 1)]:
@@ -62,6 +68,8 @@ def main():
     print(json.dumps({"variant": "direct (stem.hip)", "us": round(us, 1)}), flush=True)
     us = t_us(lambda: K.stem_conv(xh, wf, y, None, B, hw, hw, 3, cp, cout, kg))
     print(json.dumps({"variant": "direct, no statistics", "us": round(us, 1)}), flush=True)
+    if dt == torch.bfloat16:
+        return
     # the same GEMM as a 1x1 conv over an im2col operand [B][32][32][32] (27 taps x 3 ch + pad)
     xc = torch.randn(B, hw, hw, 32, device="cuda")
     w1 = torch.randn(cout, 32, 1, 1, device="cuda")

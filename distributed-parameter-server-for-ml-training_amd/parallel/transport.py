@@ -109,7 +109,11 @@ class DistTransport:
             if backend == "nccl" and device is not None:
                 kw["device_id"] = torch.device(device)
             attempt = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
-            if attempt and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
+            if os.environ.get("WORLD_SIZE", "1") == "1" and os.environ.get("PSX_WORLD1_TCP") != "1":
+                # a world of one rank needs no rendezvous: an in-process store, so no TCP port can
+                # collide with another process on the box (EADDRINUSE seen once on a GPU box)
+                kw.update(store=dist.HashStore(), rank=0, world_size=1)
+            elif attempt and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
                 # restarted group on the agent's long-lived store (static rendezvous): namespace
                 # this attempt's keys, or ranks would read the dead attempt's peer addresses
                 base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]),

@@ -226,6 +226,31 @@ class Run:
             self.chan.drain()
 
 
+def rccl_choices(path, limit=24):
+    """The distinct algorithm / protocol / channel lines of RCCL's INFO log (NCCL_DEBUG_FILE of this
+    rank), printed on stderr and returned for the JSON record; [] when there is no log."""
+    import re
+
+    seen, out = set(), []
+    try:
+        with open(path, errors="replace") as f:
+            for ln in f:
+                if not re.search(r"(?i)algo|proto|channels|rings|trees", ln):
+                    continue
+                key = re.sub(r"0x[0-9a-f]+|\b\d+\b", "#", ln.split("NCCL INFO")[-1]).strip()
+                if key in seen:
+                    continue
+                seen.add(key)
+                out.append(ln.split("NCCL INFO")[-1].strip()[:200])
+                if len(out) >= limit:
+                    break
+    except OSError:
+        return []
+    for ln in out:
+        print(f"[bench rccl] {ln}", file=sys.stderr, flush=True)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -277,6 +302,12 @@ def main():
     if a.fetch_codec == "auto":
         a.fetch_codec = "fp32" if a.dtype == "fp32" else "bf16conv"
 
+    rccl_log = None
+    if world > 1 and os.environ.get("PSX_RCCL_ALGO_LOG", "1") == "1" and "NCCL_DEBUG" not in os.environ:
+        # RCCL's chosen algorithm / protocol per collective (INIT + TUNING subsystems) into a
+        # per-rank file; rank 0 prints the distinct choices on stderr after the run
+        rccl_log = f"/tmp/psx_rccl_{os.getpid()}.log"
+        os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,TUNING", NCCL_DEBUG_FILE=rccl_log)
     t = None
     # sync at N = 1 runs the distributed path too (one rank: psx communicator, rank 0 = server +
     # worker 0), the same code as N > 1; measured equal to or faster than the in-process loopback
@@ -371,25 +402,45 @@ def main():
     # secondary numbers (same transport): bf16 compute at N=1, the co-located topology at N>=2
     secondary = {}
     if a.secondary == "auto" and a.mode == "sync" and r18 and topology != "sharded":
-        cases = ([("bf16_compute", "bf16", topology)] if world == 1 else
-                 [("colocated_topology", a.dtype, "colocated")] if topology == "dedicated" else [])
-        for name, dt_, topo in cases:
+        # (name, compute dtype, topology, overrides): N = 1 — the bf16 compute path and the async
+        # PS (one worker, in-process: the staleness summary of BASELINE's "async staleness"); N >= 2
+        # — the co-located topology and the serial (overlap off) round, a same-box A/B of the
+        # bucketed overlap the headline turns on automatically
+        if world == 1:
+            cases = [("bf16_compute", "bf16", topology, {}), ("async_ps", a.dtype, topology, {"mode": "async"})]
+        else:
+            cases = ([("colocated_topology", a.dtype, "colocated", {})] if topology == "dedicated" else [])
+            cases.append(("overlap_off", a.dtype, topology, {"overlap": "off"}))
+        for name, dt_, topo, over in cases:
             try:
                 a2 = argparse.Namespace(**vars(a))
                 a2.fetch_codec = "fp32" if dt_ == "fp32" else "bf16conv"
-                r2 = Run(a2, t, rank, world, device, dt_, topo)
+                for k, v in over.items():
+                    setattr(a2, k, v)
+                t2 = None if (a2.mode == "async" and world == 1) else t  # async N=1: in-process loopback
+                r2 = Run(a2, t2, rank, world, device, dt_, topo)
                 steps2 = max(5, min(a.steps, 20))
                 d2, _ = r2.measure(steps2, min(a.warmup, 5))
                 v2 = steps2 * a.batch * r2.W / d2
                 secondary[name] = {"value": round(v2, 2), "ms_per_step": round(1e3 * d2 / steps2, 4), "dtype": dt_,
                                    "topology": r2.topology_name(), "workers": r2.W, "steps": steps2,
                                    "vs_baseline": round(v2 / BASELINE_SYNC_IMG_S, 2)}
+                if over:
+                    secondary[name]["overrides"] = over
+                if a2.mode == "async" and r2.server is not None:
+                    sm = r2.server.final_metrics()
+                    secondary[name]["async_staleness"] = {
+                        k: sm.get(k) for k in ("average_gradient_staleness", "max_staleness_observed",
+                                               "mean_staleness_all", "async_updates", "rejected_pushes",
+                                               "staleness_histogram")}
                 r2.close()
             except Exception as e:  # noqa: BLE001 - a secondary number never costs the headline
                 secondary[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0:
         if secondary:
             rec["secondary"] = secondary
+        if rccl_log is not None:
+            rec["config"]["rccl_algorithms"] = rccl_choices(rccl_log)
         print(json.dumps(rec), flush=True)
     if t is not None:
         t.close()

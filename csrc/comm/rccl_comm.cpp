@@ -19,6 +19,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
 #include <mutex>
 #include <unordered_map>
 
@@ -49,12 +52,25 @@ std::mutex g_enqueue;  // RCCL communicators are not safe for concurrent enqueue
 
 // Registry of the communicators this process created. ncclCommAbort frees the communicator, and
 // the liveness watchdog calls it from its own thread while the training thread (or the native
-// sync loop) may be about to enqueue on it: once a handle is aborted or destroyed every later
-// call on it returns kAborted instead of touching freed memory. The registry has its own mutex
-// (never g_enqueue: an enqueue stuck inside RCCL on a dead peer holds that one, and the abort is
-// exactly what must get through to unblock it).
+// sync loop) may be about to enqueue on it. Handles given to the caller are generation ids, never
+// the ncclComm_t address: a key is never reused, so a stale handle of an aborted communicator can
+// never match a later one that RCCL allocated at the same address (the shrink's ncclCommInitRank).
+// Every call takes the communicator out of the registry with an in-use count (acquire / release);
+// abort first marks the entry dead (no new user can start), then waits up to kAbortDrainMs for the
+// in-use count to drain before it frees. The remaining window: a user blocked INSIDE RCCL past that
+// wait (an enqueue stuck on a dead peer — exactly what the abort must unblock) still holds the
+// pointer when RCCL frees it; RCCL's abort contract is what covers that call. The registry has its
+// own mutex (never g_enqueue: a stuck enqueue holds that one).
+struct Entry {
+  ncclComm_t comm = nullptr;
+  int state = 0;  // 1 = live, 0 = aborted / destroyed
+  int inuse = 0;
+};
 std::mutex g_live_mu;
-std::unordered_map<void*, int> g_live;  // 1 = live, 0 = aborted / destroyed
+std::condition_variable g_live_cv;
+std::unordered_map<uintptr_t, Entry> g_live;
+uintptr_t g_next_id = 1;
+constexpr int kAbortDrainMs = 2000;
 
 // psx dtype codes (parallel/rccl.py DTYPES) -> RCCL
 bool to_nccl(int code, ncclDataType_t* out) {
@@ -78,15 +94,43 @@ constexpr int kNotLoaded = -1000;
 constexpr int kBadDtype = -1001;
 constexpr int kAborted = -1002;
 
-bool live(void* h) {
+// the communicator of a live handle with its in-use count raised, or nullptr (aborted / unknown)
+ncclComm_t acquire(void* h) {
   std::lock_guard<std::mutex> lk(g_live_mu);
-  auto it = g_live.find(h);
-  return h && it != g_live.end() && it->second == 1;
+  auto it = g_live.find((uintptr_t)h);
+  if (!h || it == g_live.end() || it->second.state != 1) return nullptr;
+  ++it->second.inuse;
+  return it->second.comm;
 }
 
-void retire_handle(void* h) {
+void release(void* h) {
   std::lock_guard<std::mutex> lk(g_live_mu);
-  g_live[h] = 0;
+  auto it = g_live.find((uintptr_t)h);
+  if (it != g_live.end() && it->second.inuse > 0 && --it->second.inuse == 0) g_live_cv.notify_all();
+}
+
+// RAII user of a handle for the duration of one call
+struct Use {
+  void* h;
+  ncclComm_t c;
+  explicit Use(void* h_) : h(h_), c(acquire(h_)) {}
+  ~Use() {
+    if (c) release(h);
+  }
+  Use(const Use&) = delete;
+  Use& operator=(const Use&) = delete;
+};
+
+// marks the handle dead and returns its communicator once the in-use count drained (or the
+// drain wait ran out); nullptr when it was not live (a second abort / destroy is a no-op)
+ncclComm_t retire_handle(void* h, bool wait_users) {
+  std::unique_lock<std::mutex> lk(g_live_mu);
+  auto it = g_live.find((uintptr_t)h);
+  if (!h || it == g_live.end() || it->second.state != 1) return nullptr;
+  it->second.state = 0;
+  if (wait_users)
+    g_live_cv.wait_for(lk, std::chrono::milliseconds(kAbortDrainMs), [&] { return it->second.inuse == 0; });
+  return it->second.comm;
 }
 
 }  // namespace
@@ -138,41 +182,47 @@ int psx_comm_init(const char* id_bytes, int nranks, int rank, int device, void**
   memcpy(id.internal, id_bytes, NCCL_UNIQUE_ID_BYTES);
   ncclComm_t comm = nullptr;
   const ncclResult_t r = g_api.comm_init_rank(&comm, nranks, id, rank);
-  *out = r == ncclSuccess ? (void*)comm : nullptr;
+  *out = nullptr;
   if (r == ncclSuccess) {
     std::lock_guard<std::mutex> lk(g_live_mu);
-    g_live[(void*)comm] = 1;
+    const uintptr_t key = g_next_id++;
+    Entry& e = g_live[key];
+    e.comm = comm;
+    e.state = 1;
+    *out = (void*)key;
   }
   return (int)r;
 }
 
 int psx_comm_destroy(void* h) {
-  if (!g_api.lib || !live(h)) return 0;
-  retire_handle(h);
-  return (int)g_api.comm_destroy((ncclComm_t)h);
+  if (!g_api.lib) return 0;
+  ncclComm_t c = retire_handle(h, true);
+  return c ? (int)g_api.comm_destroy(c) : 0;
 }
 
 // Safe from any thread, also while another thread is blocked inside RCCL on this communicator;
 // a second abort / destroy of the same handle is a no-op.
 int psx_comm_abort(void* h) {
-  if (!g_api.lib || !live(h)) return 0;
-  retire_handle(h);
-  return (int)g_api.comm_abort((ncclComm_t)h);
+  if (!g_api.lib) return 0;
+  ncclComm_t c = retire_handle(h, true);
+  return c ? (int)g_api.comm_abort(c) : 0;
 }
 
 // number of ranks of the communicator as RCCL reports it (ncclCommCount)
 int psx_comm_count(void* h, int* n) {
   if (!g_api.lib) return kNotLoaded;
-  if (!live(h)) return kAborted;
+  Use u(h);
+  if (!u.c) return kAborted;
   if (!g_api.comm_count) return -3;
-  return (int)g_api.comm_count((ncclComm_t)h, n);
+  return (int)g_api.comm_count(u.c, n);
 }
 
 int psx_comm_async_error(void* h) {
   if (!g_api.lib) return kNotLoaded;
-  if (!live(h)) return kAborted;
+  Use u(h);
+  if (!u.c) return kAborted;
   ncclResult_t e = ncclSuccess;
-  const ncclResult_t r = g_api.async_error((ncclComm_t)h, &e);
+  const ncclResult_t r = g_api.async_error(u.c, &e);
   return r != ncclSuccess ? (int)r : (int)e;
 }
 
@@ -186,68 +236,75 @@ const char* psx_comm_error_string(int code) {
 // sum-reduce `count` elements of `send` into `recv` on `root` (recv may alias send)
 int psx_comm_reduce_sum(void* h, const void* send, void* recv, long count, int dtype, int root, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
-  if (!live(h)) return kAborted;
+  Use u(h);
+  if (!u.c) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
-  return (int)g_api.reduce(send, recv, (size_t)count, t, ncclSum, root, (ncclComm_t)h, st);
+  return (int)g_api.reduce(send, recv, (size_t)count, t, ncclSum, root, u.c, st);
 }
 
 int psx_comm_all_reduce_sum(void* h, const void* send, void* recv, long count, int dtype, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
-  if (!live(h)) return kAborted;
+  Use u(h);
+  if (!u.c) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
-  return (int)g_api.all_reduce(send, recv, (size_t)count, t, ncclSum, (ncclComm_t)h, st);
+  return (int)g_api.all_reduce(send, recv, (size_t)count, t, ncclSum, u.c, st);
 }
 
 // Sharded server (parallel/sharded.py): rank r receives the sum of every rank's
 // send[r*count, (r+1)*count) in recv (recv may be send + r*count: in place).
 int psx_comm_reduce_scatter_sum(void* h, const void* send, void* recv, long count, int dtype, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
-  if (!live(h)) return kAborted;
+  Use u(h);
+  if (!u.c) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
-  return (int)g_api.reduce_scatter(send, recv, (size_t)count, t, ncclSum, (ncclComm_t)h, st);
+  return (int)g_api.reduce_scatter(send, recv, (size_t)count, t, ncclSum, u.c, st);
 }
 
 // rank r's `count` elements land at recv + r*count on every rank (send == recv + r*count: in place)
 int psx_comm_all_gather(void* h, const void* send, void* recv, long count, int dtype, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
-  if (!live(h)) return kAborted;
+  Use u(h);
+  if (!u.c) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
-  return (int)g_api.all_gather(send, recv, (size_t)count, t, (ncclComm_t)h, st);
+  return (int)g_api.all_gather(send, recv, (size_t)count, t, u.c, st);
 }
 
 int psx_comm_broadcast(void* h, void* buf, long count, int dtype, int root, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
-  if (!live(h)) return kAborted;
+  Use u(h);
+  if (!u.c) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
-  return (int)g_api.broadcast(buf, buf, (size_t)count, t, root, (ncclComm_t)h, st);
+  return (int)g_api.broadcast(buf, buf, (size_t)count, t, root, u.c, st);
 }
 
 int psx_comm_send(void* h, const void* buf, long count, int dtype, int peer, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
-  if (!live(h)) return kAborted;
+  Use u(h);
+  if (!u.c) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
-  return (int)g_api.send(buf, (size_t)count, t, peer, (ncclComm_t)h, st);
+  return (int)g_api.send(buf, (size_t)count, t, peer, u.c, st);
 }
 
 int psx_comm_recv(void* h, void* buf, long count, int dtype, int peer, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
-  if (!live(h)) return kAborted;
+  Use u(h);
+  if (!u.c) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
-  return (int)g_api.recv(buf, (size_t)count, t, peer, (ncclComm_t)h, st);
+  return (int)g_api.recv(buf, (size_t)count, t, peer, u.c, st);
 }
 
 int psx_comm_group_start() { return g_api.lib ? (int)g_api.group_start() : kNotLoaded; }
@@ -258,7 +315,8 @@ int psx_comm_group_end() { return g_api.lib ? (int)g_api.group_end() : kNotLoade
 int psx_comm_gather(void* h, const void* send, void* recv, long count, int dtype, int elem_bytes, int root,
                     int rank, int nranks, hipStream_t st) {
   if (!g_api.lib) return kNotLoaded;
-  if (!live(h)) return kAborted;
+  Use u(h);
+  if (!u.c) return kAborted;
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) return kBadDtype;
   std::lock_guard<std::mutex> lk(g_enqueue);
@@ -272,12 +330,12 @@ int psx_comm_gather(void* h, const void* send, void* recv, long count, int dtype
           g_api.group_end();
           return -3;
         }
-      } else if ((r = g_api.recv(dst, (size_t)count, t, p, (ncclComm_t)h, st)) != ncclSuccess) {
+      } else if ((r = g_api.recv(dst, (size_t)count, t, p, u.c, st)) != ncclSuccess) {
         g_api.group_end();
         return (int)r;
       }
     }
-  } else if ((r = g_api.send(send, (size_t)count, t, root, (ncclComm_t)h, st)) != ncclSuccess) {
+  } else if ((r = g_api.send(send, (size_t)count, t, root, u.c, st)) != ncclSuccess) {
     g_api.group_end();
     return (int)r;
   }

@@ -139,7 +139,8 @@ extern "C" {
 int psx_maxpool3s2_fwd(const void* x, void* y, void* arg, int B, int H, int W, int C, int f32, hipStream_t st) {
   if (C % 8) return -2;
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
-  if ((long)B * OH * OW * (C / 8) >= (1L << 31)) return -2;
+  // the grid-stride index t < total + grid * 256 must stay below 2^31 (32-bit index math)
+  if ((long)B * OH * OW * (C / 8) + 8192L * 256 >= (1L << 31)) return -2;
   const dim3 grid(pool_grid((long)B * OH * OW * (C / 8)));
   if (f32)
     hipLaunchKernelGGL(maxpool3s2_fwd_kernel<float>, grid, dim3(256), 0, st, (const float*)x, (float*)y,
@@ -155,7 +156,7 @@ int psx_maxpool3s2_bwd(const void* dy, const void* arg, void* dx, int B, int H, 
   if (C % 8) return -2;
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
   const long blocks = (long)B * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
-  if (blocks >= (1L << 31)) return -2;
+  if (blocks + 8192L * 256 >= (1L << 31)) return -2;  // grid-stride t stays < 2^31
   const dim3 grid(pool_grid(blocks));
   if (f32)
     hipLaunchKernelGGL(maxpool3s2_bwd_kernel<float>, grid, dim3(256), 0, st, (const float*)dy, (const uint8_t*)arg,

@@ -224,6 +224,14 @@ class HipCompute:
     def last_loss(self) -> float:
         return float(self.engine.loss.mean())
 
+    def rewind(self, step: int):
+        """Re-enter training at local step ``step`` (sync shrink rollback, parallel/elastic.py):
+        the augmentation stream is keyed by the step counter, and the BN statistic shifts came
+        from steps the rollback discarded — the next step sums plainly, as a fresh engine's first
+        step does (HipResNetEngine.reset_stat_shift)."""
+        self._step = int(step)
+        self.engine.reset_stat_shift()
+
     def step_stats(self):
         """Device tensors (sum of per-sample losses, #correct) of the last train step (no sync)."""
         return self.engine.loss.sum(dtype=torch.float64), self.engine.correct.sum(dtype=torch.int64)

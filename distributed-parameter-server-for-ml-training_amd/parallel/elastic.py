@@ -32,6 +32,7 @@ data shard is not trained further (the reference's lost pushes are lost too).
 """
 from __future__ import annotations
 
+import datetime
 import json
 import os
 import pickle
@@ -53,10 +54,15 @@ def enabled(cfg, transport, world: int) -> bool:
 
 
 def lost_error(e: BaseException) -> bool:
-    """Errors that mean 'the communicator is gone' (recoverable by shrinking)."""
+    """Errors that mean 'the communicator is gone' (recoverable by shrinking): a watchdog abort
+    (CommLost), a failed RCCL call (RcclError), or the native server loop's communicator codes
+    (NativeSyncError -60 / -65). Any other native-loop failure (apply kernel, checkpoint
+    callback, core bookkeeping) fails the job: shrinking would only repeat it."""
     if isinstance(e, (CommLost, RcclError)):
         return True
-    return isinstance(e, RuntimeError) and "native sync server failed" in str(e)
+    from .native_sync import NativeSyncError
+
+    return isinstance(e, NativeSyncError) and e.comm_lost
 
 
 def make_on_stall(transport, freeze=None, log=None):
@@ -147,6 +153,31 @@ class ShrunkTransport(RcclTransport):
                 dist.destroy_process_group()
 
 
+def agree(st, key: str, me: int, old_members, grace_s: float, rounds_kept=None, new_uid=None, poll_s: float = 0.05):
+    """The survivors' plan (step 2 of the module docstring) on a key-value store ``st`` (the
+    rendezvous TCPStore, or any c10d Store): every rank checks in under ``<key>/alive/<me>``; rank
+    0 waits up to ``grace_s`` for the other old members, then publishes the plan {members, rounds,
+    uid} — ``new_uid()`` makes the fresh communicator id (bytes). Everyone returns the plan dict;
+    a rank that checked in after rank 0 published it is not in ``plan["members"]``. Needs no GPU
+    (tests/test_elastic_cpu.py runs it over a TCPStore in several processes)."""
+    old_members = list(old_members)
+    st.set(f"{key}/alive/{me}", str(me).encode())
+    if me == 0:
+        deadline = time.monotonic() + grace_s
+        others = [r for r in old_members if r != 0]
+        while time.monotonic() < deadline:
+            if all(st.check([f"{key}/alive/{r}"]) for r in others):
+                break
+            time.sleep(poll_s)
+        members = [0] + [r for r in others if st.check([f"{key}/alive/{r}"])]
+        uid = new_uid() if new_uid is not None else b""
+        plan = {"members": members, "rounds": int(rounds_kept), "uid": uid.hex()}
+        st.set(f"{key}/plan", json.dumps(plan).encode())
+        return plan
+    st.wait([f"{key}/plan"], datetime.timedelta(seconds=grace_s + 120))
+    return json.loads(st.get(f"{key}/plan"))
+
+
 def shrink(t, epoch: int, grace_s: float, rounds_kept=None, log=print):
     """Collective among the survivors (see the module docstring, steps 2-3). ``t``: the current
     transport (RcclTransport or ShrunkTransport) whose communicator is lost; rank 0 passes
@@ -158,20 +189,7 @@ def shrink(t, epoch: int, grace_s: float, rounds_kept=None, log=print):
     key = f"{tag}/e{epoch}"
     me = getattr(t, "orig_rank", t.rank)
     old_members = list(getattr(t, "members", range(t.world_size)))
-    st.set(f"{key}/alive/{me}", str(me).encode())
-    if me == 0:
-        deadline = time.monotonic() + grace_s
-        others = [r for r in old_members if r != 0]
-        while time.monotonic() < deadline:
-            if all(st.check([f"{key}/alive/{r}"]) for r in others):
-                break
-            time.sleep(0.05)
-        members = [0] + [r for r in others if st.check([f"{key}/alive/{r}"])]
-        plan = {"members": members, "rounds": int(rounds_kept), "uid": NativeComm.new_id().hex()}
-        st.set(f"{key}/plan", json.dumps(plan).encode())
-    else:
-        st.wait([f"{key}/plan"], __import__("datetime").timedelta(seconds=grace_s + 120))
-        plan = json.loads(st.get(f"{key}/plan"))
+    plan = agree(st, key, me, old_members, grace_s, rounds_kept, NativeComm.new_id)
     members = plan["members"]
     dead = [r for r in old_members if r not in members]
     if me not in members:

@@ -73,6 +73,24 @@ def _lib():
     return lib
 
 
+class NativeSyncError(RuntimeError):
+    """psx_sync_run's error code (csrc/server/sync_loop.cpp): -60 a communicator call failed,
+    -65 the run stopped because the watchdog aborted the communicator — the two that mean 'the
+    communicator is gone' (parallel/elastic.py lost_error). -50 HIP error, -61 apply kernel,
+    -62 round incomplete on the core, -63 checkpoint callback, -64 small-tensor gather: job
+    failures that a shrink would only repeat."""
+
+    LOST = (-60, -65)
+
+    def __init__(self, rc: int):
+        self.rc = int(rc)
+        super().__init__(f"native sync server failed ({self.rc})")
+
+    @property
+    def comm_lost(self) -> bool:
+        return self.rc in self.LOST
+
+
 def native_sync_enabled(cfg, transport, chan, server, rank: int) -> bool:
     """The dedicated server rank's rounds in native code (default; PSX_NATIVE_SYNC=0: Python)."""
     from .overlap import OverlapSyncChannel
@@ -203,7 +221,7 @@ class NativeSyncServer:
             self.chan._inflight = bool(self.cfg.primed)
             self.chan._have_buffers = True
         if rc:
-            raise RuntimeError(f"native sync server failed ({rc})")
+            raise NativeSyncError(rc)
 
     def abort(self) -> int:
         """Liveness watchdog thread: freeze the good-round count, stop issuing, abort the

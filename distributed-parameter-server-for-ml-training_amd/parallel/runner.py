@@ -86,7 +86,12 @@ def _common_steps(cfg, W, n):
 
 
 # ---------------------------------------------------------------------------- loopback
-def run_local(cfg, log=print) -> dict:
+def run_local(cfg, log=print, depart=None) -> dict:
+    """W simulated workers on one device (see _interleave). ``depart`` = {worker id: rounds}: the
+    loopback model of a sync shrink (parallel/elastic.py) — after that many sync rounds the worker
+    leaves (the server marks it dead, the wait-for-N barrier shrinks) and every survivor forgets
+    its BN statistic shifts, as a worker does when it re-enters the loop after a rollback. The
+    elastic parity test (tests/test_elastic_gpu.py) compares a shrunk distributed job against it."""
     cfg.resolve_overlap(1)
     device = _device_for(0)
     W = cfg.workers
@@ -107,10 +112,10 @@ def run_local(cfg, log=print) -> dict:
         wk.setup_data()
         workers.append(wk)
     t0 = time.time()
-    if W == 1:
+    if W == 1 and not depart:
         workers[0].run_training()
     else:
-        _interleave(cfg, workers, server, log)
+        _interleave(cfg, workers, server, log, depart=depart)
     if device.type == "cuda":
         torch.cuda.synchronize()
     wall = time.time() - t0
@@ -120,12 +125,13 @@ def run_local(cfg, log=print) -> dict:
     return {"server": sm, "workers": [getattr(w, "final_metrics", None) for w in workers]}
 
 
-def _interleave(cfg, workers, server, log):
+def _interleave(cfg, workers, server, log, depart=None):
     """W simulated workers on one device. Sync: every worker fetches the same version, the last
     push of a round triggers the averaged update. Async: pipelined round-robin (each worker
     pushes gradients computed W-1 updates ago, then fetches), i.e. W equal-speed concurrent
     workers."""
     K = max(1, cfg.sync_steps)
+    gone = set()
     for wk in workers:
         wk.training_start_time = time.time()
     steps = len(workers[0].sampler)
@@ -136,7 +142,18 @@ def _interleave(cfg, workers, server, log):
             for wk in workers:
                 wk.fetch_parameters()
         for b in range(steps):
+            if depart and cfg.mode == "sync" and b % K == 0:
+                rnd = server.core.global_step
+                for wid, after in depart.items():
+                    if after == rnd and wid not in gone:
+                        gone.add(wid)
+                        server.core.mark_dead(wid)
+                        for wk in workers:
+                            if wk.worker_id not in gone and hasattr(wk.compute, "rewind"):
+                                wk.compute.rewind(wk.compute._step)
             for wk, bt in zip(workers, batches):
+                if wk.worker_id in gone:
+                    continue
                 if cfg.mode == "sync" and b % K == 0:
                     wk.fetch_parameters()
                 wk.train_local_batch(bt[b])
@@ -146,7 +163,7 @@ def _interleave(cfg, workers, server, log):
             if cfg.verbose and b % 50 == 0:
                 log(f"  epoch {epoch + 1} batch {b}/{steps} loss(w0) {workers[0].compute.last_loss():.4f} "
                     f"global_step {server.core.global_step}")
-            if cfg.max_steps and workers[0].local_step_counter >= cfg.max_steps:
+            if cfg.max_steps and max(wk.local_step_counter for wk in workers) >= cfg.max_steps:
                 break
         if server.device.type == "cuda":
             torch.cuda.synchronize()
@@ -155,7 +172,7 @@ def _interleave(cfg, workers, server, log):
             wk.epoch_times.append(dt)
             if cfg.eval_every and (epoch + 1) % cfg.eval_every == 0:
                 wk.evaluate_model()
-        if cfg.max_steps and workers[0].local_step_counter >= cfg.max_steps:
+        if cfg.max_steps and max(wk.local_step_counter for wk in workers) >= cfg.max_steps:
             break
     for wk in workers:
         wk.cleanup()
@@ -437,6 +454,14 @@ def _worker_shrink(cfg, ctx, wk, layout, device, log):
     wd = getattr(wk.channel, "watchdog", None)
     if wd is not None:
         wd.stop()
+    # the communicator is aborted only if the watchdog fired; an RcclError raised straight from an
+    # enqueue leaves collectives queued for the dead peer spinning, and the synchronize below would
+    # then block with no watchdog running. Abort here (a no-op on an already aborted handle).
+    old.lost = True
+    try:
+        old.comm.destroy(abort=True)
+    except Exception:  # noqa: BLE001
+        pass
     try:
         torch.cuda.synchronize()  # the aborted collectives have run out
     except Exception:  # noqa: BLE001
@@ -475,6 +500,11 @@ def _dedicated_sync_server(cfg, server, chan, steps, device, skip=0, t=None, ctx
             ctx["epoch"] += 1
             t, rounds, dead = elastic.shrink(ctx["t"], ctx["epoch"], _shrink_grace(cfg), rounds_kept=kept, log=log)
             ctx["t"] = t
+            if not dead:
+                # every worker checked in: nothing was lost, so the failure is not a departed peer
+                # and another epoch would only repeat it (each shrink must drop at least one rank)
+                raise RuntimeError(f"sync shrink epoch {ctx['epoch']}: no rank was lost; failing the job "
+                                   f"instead of retrying ({type(e).__name__}: {e})") from e
             for r in dead:  # dedicated topology: worker id = original rank - 1
                 server.core.mark_dead(r - 1)
             server.dropped_workers = sorted(set(getattr(server, "dropped_workers", None) or []) | {r - 1 for r in dead})
@@ -552,36 +582,53 @@ class _PyRollback:
     """The Python server loop's side of a shrink (native: sync_loop.cpp snapshots): the arena (and
     momentum) at every round start in one of three snapshot slots, a device event after every
     round; the watchdog thread freezes the count of rounds whose event completed before it
-    aborted the communicator (``freeze``)."""
+    aborted the communicator (``freeze``).
+
+    As the native loop (retire(S, 2)), at most two rounds are in flight: round n's start waits
+    for round n-2's event before it overwrites slot n % 3 (round n-3's snapshot), so every
+    rollback target (a round >= the completed count) still has its snapshot. Every unretired
+    event is kept, so the completed count never assumes an unobserved round finished."""
+
+    NSLOT = 3
 
     def __init__(self, server, chan):
         self.s = server
-        self.snap = [torch.empty_like(server.arena) for _ in range(3)]
-        self.msnap = ([torch.empty_like(server.momentum_buf) for _ in range(3)]
+        self.snap = [torch.empty_like(server.arena) for _ in range(self.NSLOT)]
+        self.msnap = ([torch.empty_like(server.momentum_buf) for _ in range(self.NSLOT)]
                       if server.momentum_buf is not None else None)
         self.gs0 = server.core.global_step
         self.mom_first0 = server._mom_first
-        self.issued = 0
-        self.events = []
+        self.issued = 0        # rounds whose device work was enqueued (round_end)
+        self.snapped = -1      # the last round whose starting state is in its slot
+        self.retired = 0       # rounds [0, retired) waited on (host-observed complete)
+        self.events = []       # (round, event) of every round >= retired
         self.frozen = None
         if chan.watchdog is not None:
             chan.watchdog.on_expire = elastic.make_on_stall(chan.t, freeze=self.freeze)
 
     def round_start(self):
-        k = self.issued % 3
+        n = self.issued
+        # bound the rounds in flight: round n-2 done before slot n % 3 (round n-3) is reused
+        while self.events and self.events[0][0] <= n - 2:
+            i, ev = self.events[0]
+            ev.synchronize()
+            self.events.pop(0)
+            self.retired = i + 1
+        k = n % self.NSLOT
         self.snap[k].copy_(self.s.arena)
         if self.msnap is not None:
             self.msnap[k].copy_(self.s.momentum_buf)
+        self.snapped = n
 
     def round_end(self):
         ev = torch.cuda.Event()
         ev.record()
-        self.events = (self.events + [(self.issued, ev)])[-4:]
+        self.events.append((self.issued, ev))
         self.issued += 1
 
     def _completed(self) -> int:
-        g = self.issued - len(self.events)
-        for i, ev in self.events:
+        g = self.retired
+        for i, ev in list(self.events):
             if not ev.query():
                 break
             g = i + 1
@@ -593,10 +640,11 @@ class _PyRollback:
     def rollback(self) -> int:
         torch.cuda.synchronize()
         g = self.frozen if self.frozen is not None else self.issued  # a failed round never ended
-        g = min(g, self.issued)
-        self.s.arena.copy_(self.snap[g % 3])
-        if self.msnap is not None:
-            self.s.momentum_buf.copy_(self.msnap[g % 3])
+        g = max(min(g, self.issued), self.issued - (self.NSLOT - 1), 0)
+        if g <= self.snapped:  # g == issued with no snapshot taken yet: the arena is that state
+            self.s.arena.copy_(self.snap[g % self.NSLOT])
+            if self.msnap is not None:
+                self.s.momentum_buf.copy_(self.msnap[g % self.NSLOT])
         if g == 0:
             self.s._mom_first = self.mom_first0
         self.s.core.rollback_to(self.gs0 + g)

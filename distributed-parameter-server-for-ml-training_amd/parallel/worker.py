@@ -423,6 +423,9 @@ class Worker:
                     self.log(f"[psx elastic] worker {self.worker_id}: {type(e).__name__}: {e}")
                     skip_steps = self.recover(e)
                     self.local_step_counter = 0
+                    if hasattr(self.compute, "rewind"):  # augment stream + BN shifts of the kept round
+                        self.compute.rewind(rounds_to_batches(skip_steps, len(self.sampler.epoch_indices(0)),
+                                                              self.local_steps_per_sync))
         finally:
             self._sync()
             self.cleanup()

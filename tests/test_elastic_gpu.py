@@ -31,7 +31,7 @@ from psx.parallel.runner import run_distributed
 from psx.utils.config import PSConfig
 cfg = PSConfig(model="resnet18", batch_size=32, epochs=1, train_samples=1024, eval_every=0, verbose=1, lr=0.05,
                max_steps=10, mode="sync", topology="dedicated", round_timeout=5.0, recovery_grace=6.0,
-               on_worker_loss="shrink", overlap={ov}, fault_inject={fi!r}).validate()
+               on_worker_loss="shrink", overlap={ov}, fault_inject={fi!r}, deterministic={det}).validate()
 res = run_distributed(cfg, log=lambda *a, **k: print(*a, **k, flush=True))
 if res.get("server"):
     s = res["server"]
@@ -50,9 +50,9 @@ def _port():
         return s.getsockname()[1]
 
 
-def _launch(tmp_path, fault, native, overlap):
+def _launch(tmp_path, fault, native, overlap, det=False):
     script = tmp_path / "run.py"
-    script.write_text(_RUN.format(root=ROOT, fi=fault, ov=overlap))
+    script.write_text(_RUN.format(root=ROOT, fi=fault, ov=overlap, det=det))
     port = _port()
     procs, logs = [], []
     for r in range(3):
@@ -97,3 +97,41 @@ def test_sync_survives_lost_worker(fault, native, overlap, tmp_path):
     assert w["id"] == 1 and w["steps"] == 10, w
     assert s["gs"] == 10 and s["updates"] == 10, s
     assert s["dead"] == 1 and s["dropped"] == [0], s
+
+
+_REF = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+import psx
+from psx.parallel.runner import run_local
+from psx.utils.config import PSConfig
+cfg = PSConfig(model="resnet18", batch_size=32, epochs=1, train_samples=1024, eval_every=0, verbose=0, lr=0.05,
+               max_steps=10, mode="sync", workers=2, deterministic=True).validate()
+res = run_local(cfg, log=lambda *a, **k: None, depart={{0: {R}}})
+s = res["server"]
+print("RESULT " + json.dumps({{"gs": s["global_steps_completed"], "sha": s["final_param_sha256"]}}), flush=True)
+"""
+
+
+@pytest.mark.parametrize("native", ["1", "0"])
+def test_shrink_state_matches_scripted_departure(native, tmp_path):
+    """Not just counts: the shrunk job's final master state is bit-identical (arena sha256,
+    deterministic mode) to a scripted loopback run in which both workers train rounds 0..R-1 and
+    worker 1 alone the rest — R being the round the survivors resumed from (the server's rollback
+    target). A rollback to the wrong snapshot slot, a round applied twice or a worker re-entering
+    with the wrong augmentation step / BN shifts changes the sha."""
+    rc0, rc2, out = _launch(tmp_path, "kill_worker:0@3", native, "False", det=True)
+    assert rc0 == 0 and rc2 == 0, "\n---\n".join(o[-3000:] for o in out)
+    s = _records(out[0], "RESULT ")[0]
+    import re
+
+    kept = [int(m) for m in re.findall(r"resuming at round (\d+)", out[0])]
+    assert len(kept) == 1 and 1 <= kept[0] <= 3, out[0][-3000:]
+    ref_py = tmp_path / "ref.py"
+    ref_py.write_text(_REF.format(root=ROOT, R=kept[0]))
+    r = subprocess.run([sys.executable, str(ref_py)], env=dict(os.environ, PYTHONPATH=ROOT), stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:]
+    ref = _records(r.stdout, "RESULT ")[-1]
+    assert s["gs"] == ref["gs"] == 10, (s, ref)
+    assert s["sha"] == ref["sha"], (s, ref, kept)

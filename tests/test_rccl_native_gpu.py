@@ -160,3 +160,91 @@ def test_sharded_server_world1_matches_rank0_server():
     (a, sa), (b, sb) = out["sharded"], out["colocated"]
     assert sa == sb == 6
     assert abs(a - b) <= 2e-4 * max(abs(a), abs(b)), out
+
+
+_P2P = r"""
+import json, sys, threading, time
+sys.path.insert(0, {root!r})
+import torch
+import psx
+from psx.ops._lib import comm as lib
+from psx.parallel.rccl import NativeComm, RcclError, RcclTransport, _check
+t = RcclTransport(device=torch.device("cuda", 0))
+res = {{}}
+c = t.comm
+# 1. grouped self ncclSend + ncclRecv (the gather's grouped receive pattern, one peer = self)
+src = torch.randn(1 << 18, device="cuda")
+dst = torch.zeros_like(src)
+_check(lib().psx_comm_group_start(), "ncclGroupStart")
+c.send(src, 0)
+c.recv(dst, 0)
+_check(lib().psx_comm_group_end(), "ncclGroupEnd")
+torch.cuda.synchronize()
+res["self_sendrecv"] = bool(torch.equal(src, dst))
+# 2. a self-receive with no matching send, then ncclCommAbort from a watchdog thread while the
+# group may still be pending (RCCL either rejects the unmatched group at ncclGroupEnd or leaves a
+# receive spinning; the abort must unblock it either way, within the budget)
+lone = torch.zeros(4096, device="cuda")
+old_h = c.h.value
+err = None
+aborted = threading.Event()
+def watchdog():
+    time.sleep(5.0)
+    aborted.set()
+    c.destroy(abort=True)
+th = threading.Thread(target=watchdog, daemon=True)
+th.start()
+t0 = time.monotonic()
+try:
+    _check(lib().psx_comm_group_start(), "ncclGroupStart")
+    try:
+        c.recv(lone, 0)
+    finally:
+        _check(lib().psx_comm_group_end(), "ncclGroupEnd")
+except RcclError as e:
+    err = str(e)[:120]
+if not aborted.is_set():  # rejected at enqueue (the ADVICE r4 #2 path): abort it ourselves
+    c.destroy(abort=True)
+torch.cuda.synchronize()
+th.join(timeout=10)
+res["unmatched_recv_returned_s"] = round(time.monotonic() - t0, 2)
+res["unmatched_recv_error"] = err is not None
+# 3. every later call on the aborted handle is refused (never a use of freed memory)
+import ctypes
+rc = lib().psx_comm_broadcast(ctypes.c_void_p(old_h), src.data_ptr(), 4, 2, 0, None)
+res["dead_handle_refused"] = rc == -1002
+# 4. the elastic path's re-initialisation: a fresh id, ncclCommInitRank, a working broadcast and a
+# working grouped send/recv on the new communicator, process still healthy
+uid = NativeComm.new_id()
+c2 = NativeComm.from_id(uid, 1, 0, torch.device("cuda", 0))
+b = torch.arange(1 << 16, dtype=torch.float32, device="cuda")
+bref = b.clone()
+c2.broadcast(b, 0)
+d2 = torch.zeros_like(b)
+_check(lib().psx_comm_group_start(), "ncclGroupStart")
+c2.send(b, 0)
+c2.recv(d2, 0)
+_check(lib().psx_comm_group_end(), "ncclGroupEnd")
+torch.cuda.synchronize()
+res["reinit_broadcast"] = bool(torch.equal(b, bref))
+res["reinit_sendrecv"] = bool(torch.equal(d2, bref))
+res["reinit_async_error"] = c2.async_error()
+res["new_handle_differs"] = c2.h.value != old_h
+c2.destroy()
+t.comm = c2  # already destroyed: close() must not touch the aborted first handle
+t.close()
+print("RESULT " + json.dumps(res))
+"""
+
+
+def test_native_p2p_abort_reinit_world1():
+    """The RCCL entry points the 8-GPU run and the elastic recovery use, on real librccl at world
+    1: grouped self ncclSend/ncclRecv, ncclCommAbort of a communicator with an unmatched receive
+    (from a watchdog thread), refusal of calls on a dead handle, and NativeComm.from_id
+    re-initialisation from a fresh id followed by a broadcast and a send/recv pair. (Pair
+    communicators, open_pairs, need two ranks: covered by the fakecomm world-3 tests.)"""
+    res = _run(_P2P.format(root=ROOT), 29657, timeout=120)
+    assert res["self_sendrecv"], res
+    assert res["unmatched_recv_returned_s"] < 30.0, res
+    assert res["dead_handle_refused"] and res["new_handle_differs"], res
+    assert res["reinit_broadcast"] and res["reinit_sendrecv"] and res["reinit_async_error"] == 0, res

@@ -1,7 +1,6 @@
 """fp32 batched-GEMM throughput of the Winograd layers (the 36 per-point GEMMs of ResNet-18's
 8x8x256 / 4x4x512 layers and ResNet-50's 3x3 stages at B=128): psx's conv_v2 mainloop (every
-tile config), the stream-K Winograd GEMM (csrc/kernels/wino_gemm.hip) and torch.bmm
-(hipBLASLt / rocBLAS fp32) on the same operands. One JSON line per shape: microseconds and TFLOP/s.
+tile config) and torch.bmm (hipBLASLt / rocBLAS fp32) on the same operands. One JSON line per shape: microseconds and TFLOP/s.
 
   python bench/bgemm_f32.py
 """
@@ -32,7 +31,8 @@ def t_us(fn, iters=20, warm=3):
 
 
 # (M = tiles, N = out channels, Kd = in channels); batch 36
-SHAPES = [(512, 256, 256), (128, 512, 512), (2048, 128, 128), (6272, 128, 128), (25088, 64, 64)]
+SHAPES = [(512, 256, 256), (128, 512, 512), (2048, 128, 128), (6272, 128, 128), (25088, 64, 64),
+          (2048, 256, 256), (512, 512, 512)]  # the last two: ResNet-50's 14x14 / 7x7 (partial tiles)
 
 
 def main():
@@ -54,17 +54,6 @@ def main():
                 r[f"cfg{cfg}"] = [round(us, 1), round(fl / us / 1e6, 1), f"{err:.1e}"]
             except Exception as e:  # noqa: BLE001
                 r[f"cfg{cfg}"] = str(e)[:60]
-        # stream-K (wino_gemm.hip): a [nb][m][kd], b [n][nb][kd] (rows nb * kd apart), c [nb][m][n]
-        for bn in (0, 128, 64):
-            p.fill_(float("nan"))
-            rc = K.sk_gemm_nt(a, b, p, m, n, kd, nb, (kd, m * kd), (nb * kd, kd), (n, m * n), bn=bn)
-            if rc:
-                r[f"sk{bn}"] = f"rc {rc}"
-                continue
-            torch.cuda.synchronize()
-            err = ((p - ref).abs().max() / ref.abs().max()).item()
-            us = t_us(lambda: K.sk_gemm_nt(a, b, p, m, n, kd, nb, (kd, m * kd), (nb * kd, kd), (n, m * n), bn=bn))
-            r[f"sk{bn}"] = [round(us, 1), round(fl / us / 1e6, 1), f"{err:.1e}"]
         bt = b.permute(1, 2, 0).contiguous()
         us = t_us(lambda: torch.bmm(a, bt, out=p))
         r["torch_bmm"] = [round(us, 1), round(fl / us / 1e6, 1)]

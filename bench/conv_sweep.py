@@ -1,5 +1,5 @@
 """Sweep conv v2 fwd / dgrad tile shape x split-K per ResNet-18 layer (B=128) in one process,
-using the PSX_CV_* experiment overrides read by plan_for (csrc/kernels/conv_v2.hip)."""
+using the PSX_TUNE cv_* experiment overrides read by plan_for (csrc/kernels/conv_v2.hip)."""
 import os
 import sys
 
@@ -11,15 +11,14 @@ import torch  # noqa: E402
 
 import psx  # noqa: E402,F401
 from psx.ops import kernels as K  # noqa: E402
+from psx.utils.tune import set_tune  # noqa: E402
 from tests.test_kernels_gpu import make_operands, to_nhwc  # noqa: E402
 from conv_layers import SHAPES, t_us  # noqa: E402
 
-VARS = ("PSX_CV_BM", "PSX_CV_BN", "PSX_CV_SPLITS", "PSX_CV_WGM")
 
 
 def clear():
-    for v in VARS:
-        os.environ.pop(v, None)
+    set_tune()
 
 
 def main():
@@ -46,8 +45,7 @@ def main():
             res = []
             for bm, bn, wgm in ((128, 128, 2), (64, 128, 2), (64, 64, 2), (64, 256, 1), (64, 128, 1), (128, 256, 2)):
                 for sp in (1, 2, 3, 4, 6, 8):
-                    os.environ.update(PSX_CV_BM=str(bm), PSX_CV_BN=str(bn), PSX_CV_SPLITS=str(sp),
-                                      PSX_CV_WGM=str(wgm))
+                    set_tune(cv_bm=bm, cv_bn=bn, cv_splits=sp, cv_wgm=wgm)
                     try:
                         res.append((t_us(fn, iters=20), bm, bn, sp, wgm))
                     except RuntimeError:

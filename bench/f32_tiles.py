@@ -1,5 +1,5 @@
 """fp32 conv tile A/B (conv_v2.hip conv2_kernel): the planner's tiles against forced 128 x 128
-(PSX_CV_BM / PSX_CV_BN, read per call) on ResNet-50's 1x1 layers and ResNet-18's strided layers,
+(PSX_TUNE cv_bm / cv_bn, read per call) on ResNet-50's 1x1 layers and ResNet-18's strided layers,
 batch 128, forward and data gradient; numerics of the forced tile against torch fp64. One JSON
 line per layer: microseconds and TFLOP/s per tile.
 
@@ -17,6 +17,7 @@ import torch.nn.functional as F  # noqa: E402
 
 import psx  # noqa: E402,F401
 from psx.ops import kernels as K  # noqa: E402
+from psx.utils.tune import set_tune  # noqa: E402
 from tests.test_fp32_gpu import nhwc, operands_f32  # noqa: E402
 
 # (cin, cout, hw, k, stride, pad)
@@ -41,10 +42,9 @@ def t_us(fn, iters=10, warm=2):
 
 
 def force(t):
-    for k in ("PSX_CV_BM", "PSX_CV_BN"):
-        os.environ.pop(k, None)
+    set_tune()
     if t:
-        os.environ["PSX_CV_BM"], os.environ["PSX_CV_BN"] = str(t[0]), str(t[1])
+        set_tune(cv_bm=t[0], cv_bn=t[1])
 
 
 def main():

@@ -3,7 +3,7 @@ the engine plans for it: forward (+ BN statistics epilogue), data gradient, weig
 (+ split-K reduction), or the fused Winograd kernels where the engine uses them. One JSON line
 per unique layer shape with its count per step, TFLOP/s against the measured 155 TF f32 MFMA
 ceiling (profiles/r2s3_mfma_ceiling.jsonl), and a final line with the count-weighted sums —
-compared against the in-step kernel times of a serial (PSX_WGRAD_STREAM=0) step profile.
+compared against the in-step kernel times of a serial (PSX_TUNE wgrad_stream=0) step profile.
 
   python bench/r50_layers_f32.py
 """
@@ -18,6 +18,7 @@ import torch  # noqa: E402
 
 import psx  # noqa: E402,F401
 from psx.ops import kernels as K  # noqa: E402
+from psx.utils.tune import tune_flag  # noqa: E402
 from tests.test_fp32_gpu import nhwc, operands_f32  # noqa: E402
 
 # (cin, cout, hw_in, k, stride, pad, count per step) — torchvision ResNet-50 v1.5 (stride in the 3x3)
@@ -70,7 +71,7 @@ def main():
         ws = torch.empty(max(n1, n2, 4) // 4, device="cuda")
         fl = 2.0 * B * oh * oh * cout * cin * k * k
         r = {"shape": [cin, cout, hw, k, s], "count": cnt, "gflop": round(fl / 1e9, 2)}
-        wino = k == 3 and s == 1 and hw <= 64 and K.wino_ok(hw, hw, cp, cout)
+        wino = k == 3 and s == 1 and hw <= 64 and K.wino_ok(hw, hw, cp, cout) and tune_flag("wino", True)
         if wino:
             u = torch.empty(40 * cout * cp, device="cuda")
             ud = torch.empty(40 * cout * cp, device="cuda")
@@ -88,11 +89,20 @@ def main():
                 r["fwd_us"] = t_us(lambda: K.wino_conv(xh, u, y, None, stats, v1, v2, B, hw, hw, cp, cout))
                 r["dgrad_us"] = t_us(lambda: K.wino_conv(dy, ud, dx, None, None, v2, v1, B, hw, hw, cout, cp))
             q = K.wino_wgrad_fused_q(B, hw, hw, cp, cout)
+            q3 = K.wino_wgrad_q(B, hw, hw, cp, cout)
+            gout = torch.empty(cout * cin * 9, dtype=torch.float16, device="cuda")
             if q > 0 and hw >= 16:
                 wpart = torch.empty(36 * q * cout * cp, device="cuda")
-                gout = torch.empty(cout * cin * 9, dtype=torch.float16, device="cuda")
                 r["wgrad_us"] = t_us(lambda: K.wino_wgrad_fused(xh, dy, wpart, gout, B, hw, hw, cp, cout))
                 r["reduce_us"] = 0.0
+            elif q3 > 0:  # three launches: dy transform, batched TN GEMM, output transform; V from the forward
+                r["path"] += "+wino_wgrad"
+                K.wino_conv(xh, u, y, None, stats, v1, v2, B, hw, hw, cp, cout)
+                d = torch.empty(K.wino_v_floats(B, hw, hw, cout), device="cuda")
+                wpart = torch.empty(36 * q3 * cout * cp, device="cuda")
+                r["wgrad_us"] = t_us(lambda: K.wino_wgrad(v1, dy, d, wpart, gout, B, hw, hw, cp, cout))
+                r["reduce_us"] = 0.0
+                del d
             del v1, v2
         else:
             r["path"] = "conv_v2"

@@ -1,5 +1,5 @@
 """fp32 weight-gradient timing on ResNet-50's layers (ImageNet shape, batch 128): the planner's
-wgrad2f / wgrad3f choice and forced tiles (PSX_WGF_BR / PSX_WGF_BC, read per call), mainloop and
+wgrad2f / wgrad3f choice and forced tiles (PSX_TUNE wgf_br / wgf_bc, read per call), mainloop and
 split-K reduction separately, TFLOP/s against the 157 TF fp32 MFMA peak. One JSON line per layer.
 
   python bench/r50_wgrad_f32.py            # all layers
@@ -16,6 +16,7 @@ import torch  # noqa: E402
 
 import psx  # noqa: E402,F401
 from psx.ops import kernels as K  # noqa: E402
+from psx.utils.tune import set_tune  # noqa: E402
 from tests.test_fp32_gpu import nhwc, operands_f32  # noqa: E402
 
 # (cin, cout, hw, k, stride, pad): the 1x1 reduce / expand layers and the 3x3 layers of each stage
@@ -40,10 +41,7 @@ def t_us(fn, iters=10, warm=2):
 
 
 def force(t):
-    for k in ("PSX_WGF_BR", "PSX_WGF_BC"):
-        os.environ.pop(k, None)
-    if t:
-        os.environ["PSX_WGF_BR"], os.environ["PSX_WGF_BC"] = str(t[0]), str(t[1])
+    set_tune(**({"wgf_br": t[0], "wgf_bc": t[1]} if t else {}))
 
 
 def main():

@@ -1,5 +1,5 @@
 """The CIFAR stem conv (3 -> 64, 3x3, 32x32, batch 128) in isolation: the planner's tile and
-forced tiles (PSX_CV_BM / PSX_CV_BN / PSX_CV_WGM, read per call) on the gathered 4-channel
+forced tiles (PSX_TUNE cv_bm / cv_bn / cv_wgm, read per call) on the gathered 4-channel
 operand, against the same GEMM as a 1x1 conv over a pre-built 32-channel im2col operand, and
 the output-store floor (a 128 x 32 x 32 x 64 tensor copy). One JSON line per variant.
 
@@ -17,6 +17,7 @@ import torch  # noqa: E402
 
 import psx  # noqa: E402,F401
 from psx.ops import kernels as K  # noqa: E402
+from psx.utils.tune import set_tune  # noqa: E402
 from tests.test_fp32_gpu import nhwc, operands_f32  # noqa: E402
 
 
@@ -34,10 +35,9 @@ def t_us(fn, iters=20, warm=3):
 
 
 def force(t):
-    for k in ("PSX_CV_BM", "PSX_CV_BN", "PSX_CV_WGM"):
-        os.environ.pop(k, None)
+    set_tune()
     if t:
-        os.environ["PSX_CV_BM"], os.environ["PSX_CV_BN"], os.environ["PSX_CV_WGM"] = map(str, t)
+        set_tune(cv_bm=t[0], cv_bn=t[1], cv_wgm=t[2])
 
 
 def main():

@@ -10,6 +10,7 @@ import torch  # noqa: E402
 
 import psx  # noqa: E402,F401
 from psx.ops import kernels as K  # noqa: E402
+from psx.utils.tune import set_tune  # noqa: E402
 from tests.test_kernels_gpu import make_operands, to_nhwc  # noqa: E402
 from conv_layers import SHAPES, t_us  # noqa: E402
 
@@ -29,8 +30,7 @@ def main():
             dx = torch.empty(B, hw, hw, cp, dtype=torch.bfloat16, device="cuda")
             row = []
             for tapr in ("256", "128", "64", "0"):
-                os.environ["PSX_CV_TAPR"] = "0" if tapr == "0" else "1"
-                os.environ["PSX_CV_TAPR_BN"] = tapr
+                set_tune(cv_tapr="0" if tapr == "0" else "1", cv_tapr_bn=tapr)
                 t = t_us(lambda: K.conv_fwd2(xh, wf, y, stats, ws, B, hw, hw, cp, cout, k, s, p, kg), iters=40)
                 td = t_us(lambda: K.conv_dgrad2(dy, wd, dx, None, ws, B, hw, hw, cp, cout, k, s, p, kgd), iters=40)
                 row.append(f"bn{tapr} fwd {t:5.1f} dgrad {td:5.1f}")

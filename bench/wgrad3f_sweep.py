@@ -1,6 +1,6 @@
 """Sweep of the fp32 tap-reuse weight gradient (wgrad3f_kernel) on the ResNet-18 3x3 stride-1
-layers at batch 128: output-channel tile (PSX_WG_BC) x split count (PSX_WGF_SPLITS), time of the
-kernel + its split-K reduction, against the planner's choice and the wgrad2f path (PSX_WG3=0).
+layers at batch 128: output-channel tile (PSX_TUNE wg_bc) x split count (wgf_splits), time of the
+kernel + its split-K reduction, against the planner's choice and the wgrad2f path (wg3=0).
 One JSON line per layer. The knobs are read per launch, so one process sweeps them all.
 
   python bench/wgrad3f_sweep.py
@@ -16,6 +16,7 @@ import torch  # noqa: E402
 
 import psx  # noqa: E402,F401
 from psx.ops import kernels as K  # noqa: E402
+from psx.utils.tune import set_tune  # noqa: E402
 
 
 def t_us(fn, iters=20, warm=3):
@@ -34,10 +35,7 @@ LAYERS = [(64, 32), (128, 16), (256, 8), (512, 4)]  # (channels, hw)
 
 
 def env(**kv):
-    for k in ("PSX_WG_BC", "PSX_WGF_SPLITS", "PSX_WG3"):
-        os.environ.pop(k, None)
-    for k, v in kv.items():
-        os.environ[k] = str(v)
+    set_tune(**kv)
 
 
 def main():
@@ -58,7 +56,7 @@ def main():
                     "tflops": round(flops / tw / 1e6, 1)}
 
         r = {"layer": [c, hw], "gflop": round(flops / 1e9, 3)}
-        env(PSX_WG3=0)
+        env(wg3=0)
         r["wgrad2f"] = run()
         env()
         r["plan"] = run()
@@ -68,7 +66,7 @@ def main():
             for spl in (8, 16, 32, 48, 64, 96, 128, 192, 256, 384, 512):
                 if spl > steps or c % bc:
                     continue
-                env(PSX_WG_BC=bc, PSX_WGF_SPLITS=spl)
+                env(wg_bc=bc, wgf_splits=spl)
                 sweep.append(dict(bc=bc, **run()))
         env()
         best = min(sweep, key=lambda d: d["wgrad_us"] + d["reduce_us"])

@@ -1,5 +1,5 @@
 """Sweep wgrad v2 tile shape x split count per ResNet-18 layer (B=128) in one process, using the
-PSX_WG_* experiment overrides read by psx_conv_wgrad2. Prints the planner's pick and the best."""
+PSX_TUNE wg_* experiment overrides read by psx_conv_wgrad2. Prints the planner's pick and the best."""
 import os
 import sys
 
@@ -11,6 +11,7 @@ import torch  # noqa: E402
 
 import psx  # noqa: E402,F401
 from psx.ops import kernels as K  # noqa: E402
+from psx.utils.tune import set_tune  # noqa: E402
 from tests.test_kernels_gpu import make_operands, to_nhwc  # noqa: E402
 from conv_layers import SHAPES, t_us  # noqa: E402
 
@@ -27,8 +28,7 @@ def main():
         xh = to_nhwc(x, cp)
         dy = torch.randn(B, oh, oh, cout, device="cuda").to(torch.bfloat16)
         part = torch.empty(64 * cout * kg, device="cuda")
-        for v in ("PSX_WG_BR", "PSX_WG_BC", "PSX_WG_SPLITS"):
-            os.environ.pop(v, None)
+        set_tune()
         spl = K.conv_wgrad2_splits(B, hw, hw, cp, cout, k, s, p, kg)
         base = t_us(lambda: K.conv_wgrad2(xh, dy, part, B, hw, hw, cp, cout, k, s, p, kg), iters=20)
         res = []
@@ -36,7 +36,7 @@ def main():
             if kg % br or cout % bc:
                 continue
             for sp in (1, 2, 4, 6, 8, 12, 16, 24, 28, 32, 48, 56, 64):
-                os.environ.update(PSX_WG_BR=str(br), PSX_WG_BC=str(bc), PSX_WG_SPLITS=str(sp))
+                set_tune(wg_br=br, wg_bc=bc, wg_splits=sp)
                 if oh * oh * B // 64 < sp:
                     continue
                 us = t_us(lambda: K.conv_wgrad2(xh, dy, part, B, hw, hw, cp, cout, k, s, p, kg), iters=20)
@@ -44,8 +44,7 @@ def main():
         res.sort()
         print(f"layer {li} {cin}->{cout} {hw} k{k}s{s}: planner splits={spl} {base:.1f} us | best "
               + "  ".join(f"{br}x{bc}/s{sp}:{us:.1f}" for us, br, bc, sp in res[:4]), flush=True)
-    for v in ("PSX_WG_BR", "PSX_WG_BC", "PSX_WG_SPLITS"):
-        os.environ.pop(v, None)
+    set_tune()
 
 
 if __name__ == "__main__":

@@ -1,7 +1,7 @@
 """Same-process A/B of the fp32 Winograd weight gradient per ResNet-18 layer class (batch 128):
 the three-launch path (wino.hip: dy transform -> D, batched TN GEMM over the forward's V, output
 transform) vs the fused launch (wino_wgrad.hip: x and dy transformed in registers, no V / D) +
-its output transform. Also the fused kernel alone (PSX_WINO_WGF_Q sweeps its tile ranges).
+its output transform. Also the fused kernel alone (PSX_TUNE wino_wgf_q sweeps its tile ranges).
 One JSON line per layer, microseconds.
 
   python bench/wino_wgrad_ab.py            # Q="8,16,32" sweeps q where it applies
@@ -17,6 +17,7 @@ import torch  # noqa: E402
 
 import psx  # noqa: E402,F401
 from psx.ops import kernels as K  # noqa: E402
+from psx.utils.tune import set_tune  # noqa: E402
 
 from bench.wino_fused_ab import t_us  # noqa: E402
 
@@ -50,10 +51,10 @@ def main():
         r["wout_us"] = round(t_us(lambda: K.kernels().psx_wino_wout(K.ptr(part), K.ptr(g), 1, 1.0, c, c, qf,
                                                                      K.stream_ptr())), 2)
         for q in qs:
-            os.environ["PSX_WINO_WGF_Q"] = str(q)
+            set_tune(wino_wgf_q=q)
             if K.wino_wgrad_fused_q(B, hw, hw, c, c) == q:
                 r[f"fused_q{q}_us"] = round(t_us(lambda: K.wino_wgrad_fused(x, dy, part, g, B, hw, hw, c, c)), 2)
-            os.environ.pop("PSX_WINO_WGF_Q")
+            set_tune()
         print(json.dumps(r), flush=True)
 
 

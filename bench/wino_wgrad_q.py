@@ -1,4 +1,4 @@
-"""Winograd weight-gradient split sweep (tile ranges q per batch, PSX_WINO_WQ) on ResNet-18's
+"""Winograd weight-gradient split sweep (tile ranges q per batch, PSX_TUNE wino_wq) on ResNet-18's
 stride-1 3x3 layers at batch 128: dy transform + batched TN GEMM + inverse transform to the
 fp16 wire, microseconds. One JSON line per layer.
 
@@ -15,6 +15,7 @@ import torch  # noqa: E402
 
 import psx  # noqa: E402,F401
 from psx.ops import kernels as K  # noqa: E402
+from psx.utils.tune import set_tune  # noqa: E402
 from bench.wino_fused_ab import t_us  # noqa: E402
 
 
@@ -35,12 +36,12 @@ def main():
         for q in (1, 2, 4, 8, 16, 32, 64):
             if T % (32 * q) or T // q < 32:
                 continue
-            os.environ["PSX_WINO_WQ"] = str(q)
+            set_tune(wino_wq=q)
             if K.wino_wgrad_q(B, hw, hw, c, c) != q:
                 continue
             wpart = torch.empty(36 * q * c * c, device="cuda")
             r[f"q{q}_us"] = round(t_us(lambda: K.wino_wgrad(v1, dy, v2, wpart, gout, B, hw, hw, c, c)), 2)
-        os.environ.pop("PSX_WINO_WQ", None)
+        set_tune()
         print(json.dumps(r), flush=True)
 
 

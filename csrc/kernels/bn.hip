@@ -168,12 +168,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
     float acc = 0.f;
     for (int q = 0; q < tpp; ++q) acc += sred[(q * cvec + cgi) * (NS * 8) + sj];
     const int stat = sj >> 3, j = sj & 7;
-    if (det.slab)
-      atomicAdd(det.slab + ((size_t)blockIdx.x * NS + stat) * C + cgi * 8 + j, acc);
-    else
-      atomicAdd(part + ((size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * NS + stat) * C + cgi * 8 + j, acc);
+    stat_add(det, part + (size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * NS * C, stat * C + cgi * 8 + j, acc);
   }
-  if (det.slab) {
+  if (det.fix) {
     if (det_finish(det, NS, C, part, blockIdx.x, reinterpret_cast<unsigned char*>(sred)) && fuse_fin) {
       bn_bwd_finalize_block<PSX_STAT_SLOTS>(part, NS, 1, fin1);
       if (TWO) bn_bwd_finalize_block<PSX_STAT_SLOTS>(part, NS, 2, fin2);
@@ -261,7 +258,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
   }
 }
 
-// Opt-in (PSX_BNFIN_APPLY=1) variant of bn_apply_kernel with the training-mode finalize folded in:
+// Opt-in (PSX_TUNE bnfin_apply=1) variant of bn_apply_kernel with the training-mode finalize folded in:
 // every workgroup computes the affine(s) from the stat slots (bnfin.hpp bn_fin_lds). Separate
 // kernels so the default path keeps its exact code (an A/B showed +38 us/step otherwise).
 template <typename T, int MODE, bool RELU, bool FIN = true>
@@ -388,40 +385,33 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin_kernel(const T* __restri
 // ---- deterministic mode host state (bnfin.hpp DetRed)
 namespace {
 struct DetState {
-  float* slab = nullptr;
-  long slab_floats = 0;
+  unsigned long long* fix = nullptr;  // kDetCtrSets regions of fix_per_set accumulators
+  long fix_per_set = 0;
   unsigned* counters = nullptr;
-  int ncounters = 0;
   int next = 0;
 };
 DetState g_det;
 }  // namespace
 
-bool det_enabled() { return g_det.slab != nullptr; }
+bool det_enabled() { return g_det.fix != nullptr; }
 
-constexpr int kDetCtrSets = 64, kDetCtrPerSet = 256;  // counter words: [set][1 + group]
+// rotating per-launch state: a launch's arrival counter and accumulator region are reused 64
+// launches later (long after its last workgroup re-zeroed them)
+constexpr int kDetCtrSets = 64, kDetCtrPerSet = 64;
 
 DetRed det_next(int rows, int NS, int C, int nper) {
   DetRed d{};
-  if (!g_det.slab) return d;
-  // level-1 groups of ~sqrt(rows) rows (the two levels' serial chains balanced), <= kDetCtrPerSet - 1
-  int group = 8;
-  while (group * group < rows) group *= 2;
-  while ((rows + group - 1) / group > kDetCtrPerSet - 1) group *= 2;
-  const int ngroups = (rows + group - 1) / group;
-  const long need = ((long)rows + ngroups) * NS * C;
-  if (need > g_det.slab_floats) {
-    fprintf(stderr, "psx deterministic mode: slab of %ld floats < %ld needed (%d rows x %d x %d)\n",
-            g_det.slab_floats, need, rows, NS, C);
+  if (!g_det.fix) return d;
+  const long need = 2L * NS * C;
+  if (need > g_det.fix_per_set) {
+    fprintf(stderr, "psx deterministic mode: %ld accumulator words per launch < %ld needed (%d x %d)\n",
+            g_det.fix_per_set, need, NS, C);
     abort();
   }
-  d.slab = g_det.slab;
-  d.slab2 = g_det.slab + (size_t)rows * NS * C;
-  d.counter = g_det.counters + (size_t)(g_det.next++ % kDetCtrSets) * kDetCtrPerSet;
-  d.rows = rows;
-  d.group = group;
-  d.ngroups = ngroups;
-  d.nper = nper;
+  const int set = g_det.next++ % kDetCtrSets;
+  d.fix = g_det.fix + (size_t)set * g_det.fix_per_set;
+  d.counter = g_det.counters + (size_t)set * kDetCtrPerSet;
+  d.nwg = rows * nper;
   return d;
 }
 
@@ -432,7 +422,7 @@ using namespace psx;
 // workgroup cap of the folded-finalize apply launches (each workgroup recomputes the affine)
 static int fin_grid_cap() {
   static int cap = [] {
-    const char* e = getenv("PSX_FIN_GRID");
+    const char* e = tune("fin_grid");
     return e ? atoi(e) : 1024;  // 1024 vs 2048: 1.852 vs 1.867-1.875 ms/step (bench.py A/B)
   }();
   return cap;
@@ -447,21 +437,25 @@ static int ew_grid(size_t nvec) {
 
 extern "C" {
 
-// Deterministic mode on (buf = a zeroed device buffer of `bytes`, >= 4 KiB: 64 launch counters +
-// the row slab) or off (buf = nullptr). Every later producer of BN sums (conv epilogues, split-K
-// epilogue, bn_bwd_reduce, the head) reduces through it (bnfin.hpp DetRed). Host state only:
-// set it before a HIP graph is captured.
+// Deterministic mode on (buf = a zeroed device buffer of `bytes`: 64 launch counters + 64
+// accumulator regions, psx_det_bytes) or off (buf = nullptr). Every later producer of BN sums
+// (conv epilogues, split-K epilogue, bn_bwd_reduce, the Winograd output transforms, the head)
+// accumulates in exact fixed point (bnfin.hpp DetRed). Host state only: set it before a HIP graph
+// is captured.
+long psx_det_bytes(int max_sums) {
+  return (long)kDetCtrSets * kDetCtrPerSet * 4 + (long)kDetCtrSets * 2 * max_sums * 8;
+}
+
 int psx_set_deterministic(void* buf, long bytes) {
   if (!buf) {
     g_det = DetState{};
     return 0;
   }
   const long ctr_bytes = (long)kDetCtrSets * kDetCtrPerSet * 4;
-  if (bytes < ctr_bytes + 4096) return -2;
+  if (bytes < ctr_bytes + kDetCtrSets * 16L * 64) return -2;
   g_det.counters = (unsigned*)buf;
-  g_det.ncounters = kDetCtrSets;
-  g_det.slab = (float*)((char*)buf + ctr_bytes);
-  g_det.slab_floats = (bytes - ctr_bytes) / 4;
+  g_det.fix = (unsigned long long*)((char*)buf + ctr_bytes);
+  g_det.fix_per_set = (bytes - ctr_bytes) / 8 / kDetCtrSets;
   g_det.next = 0;
   return 0;
 }

@@ -79,94 +79,70 @@ PSX_DEV bool last_block_arrive(unsigned* counter, unsigned nblocks, unsigned cha
 }
 
 // ---------------------------------------------------------------------------------------
-// Deterministic mode (psx_set_deterministic, bn.hip): a launch that produces per-channel sums
-// adds each workgroup's partial row into a row of its own of a scratch slab [rows][NS][C] —
-// exactly one add per location into zeros, so the value is exact whatever the order. The rows
-// are then summed in a fixed order by a two-level tree:
-//   level 1: rows are grouped `group` at a time; the workgroup arriving last among a group's
-//            writers (`nper` per row: e.g. the channel tiles of a conv) sums the group's rows in
-//            row order into row g of a second slab [ngroups][NS][C] (again one add per location)
-//            and re-zeroes the group's rows and counter;
-//   level 2: the last group reducer sums the ngroups rows in order into slot row 0 of the usual
-//            [PSX_STAT_SLOTS][NS][C] buffer (the other slot rows stay zero), re-zeroes the second
-//            slab and the launch counter.
-// Groups of ~sqrt(rows) rows keep both levels short (the one-level form, one workgroup reading
-// every row, read up to 1 MB from one CU per launch; both levels are latency-bound chains of
-// dependent loads, det_rows). The consumers are
-// unchanged and sum the slot rows in a fixed order, so every BN statistic — and with it the
-// whole step — is bit-reproducible. All payload adds are memory-side float atomics (no release
-// needed, as for the slots); the slab lines a reducer reads were never cached by this launch,
-// and kernel boundaries write back and invalidate the non-coherent L2 lines of the previous
-// launch's re-zeroing.
+// Deterministic mode (psx_set_deterministic, bn.hip): every producer of per-channel sums adds its
+// workgroup partials into exact fixed-point accumulators instead of the float slot rows. A partial
+// v (fp32) becomes the 104-bit value round(v * 2^64) split into hi = floor(v * 2^24) and lo =
+// frac(v * 2^24) * 2^40, each added with a 64-bit integer atomic: integer addition is associative,
+// so the sums — and with them every BN statistic and the whole step — are the same bits whatever
+// the order the workgroups arrive in (no fixed-order reduction tree, no slab of per-workgroup
+// rows). The exact range is |sum| < 2^39 with an absolute resolution of 2^-64 (a partial below
+// 2^-41 in magnitude truncates its lowest bits, deterministically). The last-arriving workgroup of
+// the launch converts the sums to float into slot row 0 of the usual [PSX_STAT_SLOTS][NS][C]
+// buffer (the other rows stay zero, so the consumers are unchanged) and re-zeroes the
+// accumulators. Costs two integer atomics per (statistic, channel) and workgroup instead of one
+// float atomic, plus one arrival counter per launch.
 struct DetRed {
-  float* slab;        // nullptr: deterministic mode off
-  float* slab2;       // level-2 rows [ngroups][NS][C]
-  unsigned* counter;  // [0]: level 2, [1 + g]: group g; zero at launch, re-zeroed by the reducers
-  int rows, group, ngroups, nper;
+  unsigned long long* fix;  // nullptr: deterministic mode off; [NS * C][2] (hi, lo) accumulators
+  unsigned* counter;        // launch arrival counter: zero at launch, re-zeroed by the last workgroup
+  int nwg;                  // workgroups that arrive (det_finish) in the launch
 };
 
-// Fixed-order sum of rows [r0, r1) of a [rows][n] slab into dst[j] (j < n), by the whole block:
-// value j is summed by `lanes` = max(1, 256 / n) threads over interleaved row subsets (8 loads in
-// flight each: the reduction is latency-bound), combined through LDS in lane order. Every value's
-// sum has the same association for a given (r0, r1, n), whatever the launch's timing.
-// add = true: dst receives one atomic add (onto zero: exact); else a plain store. Re-zeroes the rows.
-PSX_DEV void det_rows(float* slab, int r0, int r1, int n, float* dst, bool add, float* scratch) {
-  const int lanes = n >= 256 ? 1 : 256 / n;
-  for (int jb = 0; jb < n; jb += 256) {
-    // the first 256 threads do the work (blocks of 384, wino.hip's split transforms, call it too)
-    const int t = threadIdx.x, k = lanes > 1 ? t / n : 0, j = jb + (lanes > 1 ? t % n : t);
-    const bool act = t < 256;
-    float acc = 0.f;
-    if (act && k < lanes && j < n) {
-      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      int r = r0 + k;
-      for (; r + 7 * lanes < r1; r += 8 * lanes) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) a[u] += slab[(size_t)(r + u * lanes) * n + j];
-      }
-      for (int u = 0; r < r1; r += lanes, ++u) a[u & 7] += slab[(size_t)r * n + j];
-      acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-      for (r = r0 + k; r < r1; r += lanes) slab[(size_t)r * n + j] = 0.f;
-    }
-    if (lanes > 1) {
-      __syncthreads();
-      if (act && k < lanes && j < n) scratch[k * n + (j - jb)] = acc;
-      __syncthreads();
-      if (t < n) {
-        float v = 0.f;
-        for (int q = 0; q < lanes; ++q) v += scratch[q * n + t];
-        if (add) atomicAdd(dst + t, v);
-        else dst[t] = v;
-      }
-    } else if (act && j < n) {
-      if (add) atomicAdd(dst + j, acc);
-      else dst[j] = acc;
-    }
-  }
+PSX_DEV void fix_add(unsigned long long* p, float v) {
+  const double x = (double)v * 16777216.0;  // 2^24: exact
+  const double h = floor(x);
+  const long long hi = (long long)h;
+  const unsigned long long lo = (unsigned long long)((x - h) * 1099511627776.0);  // 2^40: exact above 2^-41
+  atomicAdd(p, (unsigned long long)hi);
+  atomicAdd(p + 1, lo);
 }
 
-// every workgroup of the launch calls this (block-uniformly) after its slab adds into row `row`;
-// returns true in the last-arriving workgroup (after the fixed-order reduction, so an in-launch
-// finalize of the same sums can follow). lds: >= 16 + 1024 bytes of the caller's LDS.
+// One per-channel partial: into the float slot row `dst` (atomics, order-dependent rounding), or
+// in deterministic mode into the fixed-point accumulator of the same index `off` (row-relative:
+// [NS][C]).
+PSX_DEV void stat_add(const DetRed& d, float* dst, int off, float v) {
+  if (d.fix)
+    fix_add(d.fix + 2 * (size_t)off, v);
+  else
+    atomicAdd(dst + off, v);
+}
+
+// Every workgroup of the launch calls this (block-uniformly) after its stat_add calls; returns true
+// in the last-arriving workgroup, after it has written the sums into slot row 0 of `part` (so an
+// in-launch finalize of the same sums can follow). lds: >= 16 bytes of the caller's LDS. (`row`:
+// unused, kept for the call sites' symmetry with the slot row they would use.)
 PSX_DEV bool det_finish(const DetRed& d, int NS, int C, float* part, int row, unsigned char* lds) {
-  const int g = row / d.group;
-  const int r0 = g * d.group, r1 = min(d.rows, r0 + d.group);
-  if (!last_block_arrive(d.counter + 1 + g, (unsigned)(d.nper * (r1 - r0)), lds)) return false;
-  float* scratch = reinterpret_cast<float*>(lds + 16);
+  (void)row;
+  if (!last_block_arrive(d.counter, (unsigned)d.nwg, lds)) return false;
   const int n = NS * C;
-  det_rows(d.slab, r0, r1, n, d.slab2 + (size_t)g * n, true, scratch);
-  if (threadIdx.x == 0) __hip_atomic_store(d.counter + 1 + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (!last_block_arrive(d.counter, (unsigned)d.ngroups, lds)) return false;
-  det_rows(d.slab2, 0, d.ngroups, n, part, false, scratch);
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    unsigned long long* p = d.fix + 2 * (size_t)j;
+    const long long H = (long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long L = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double v = (double)H * (1.0 / 16777216.0) + (double)L * 5.421010862427522e-20;  // 2^-24, 2^-64
+    part[j] = (float)v;
+    __hip_atomic_store(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(d.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   return true;
 }
 
-// host: the DetRed of the next producing launch (slab rows for `rows` x NS x C sums, `nper`
-// writer workgroups per row). Deterministic mode off: a disabled one. The slab too small for
-// the launch is a hard error (bn.hip det_next aborts): a silent fall back to the atomic slots
-// would break bit-reproducibility unnoticed.
+// host: the DetRed of the next producing launch (`rows` x `nper` arriving workgroups, NS x C
+// sums). Deterministic mode off: a disabled one. An accumulator region too small for NS x C is
+// a hard error (bn.hip det_next aborts): a silent fall back to the atomic slots would break
+// bit-reproducibility unnoticed.
 DetRed det_next(int rows, int NS, int C, int nper = 1);
 bool det_enabled();
 

@@ -10,6 +10,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #define PSX_DEV __device__ __forceinline__
 
@@ -33,6 +35,35 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 namespace psx {
+
+// Developer tuning overrides — the planners' tile sweeps and A/B switches — in ONE environment
+// variable, PSX_TUNE="key=value[,key=value...]" (e.g. PSX_TUNE=cv_bm=128,wg_splits=12; a bare
+// key means "1"; the Python side reads the same variable, psx/utils/tune.py). Read at every
+// planning call (tests and sweeps change it inside one process). Returns the value (a per-thread
+// buffer) or nullptr when the key is absent. Production runs set nothing.
+static inline const char* tune(const char* key) {
+  const char* e = getenv("PSX_TUNE");
+  if (!e) return nullptr;
+  thread_local char buf[64];
+  const size_t kl = strlen(key);
+  for (const char* p = e; *p;) {
+    const char* comma = strchr(p, ',');
+    const size_t len = comma ? (size_t)(comma - p) : strlen(p);
+    if (len >= kl && !strncmp(p, key, kl) && (len == kl || p[kl] == '=')) {
+      size_t vl = len == kl ? 1 : len - kl - 1;
+      if (vl >= sizeof buf) vl = sizeof buf - 1;
+      if (len == kl)
+        buf[0] = '1';
+      else
+        memcpy(buf, p + kl + 1, vl);
+      buf[vl] = 0;
+      return buf;
+    }
+    if (!comma) break;
+    p = comma + 1;
+  }
+  return nullptr;
+}
 
 PSX_DEV float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 

@@ -36,10 +36,6 @@
 #ifndef PSX_TAPR_BF16_256
 #define PSX_TAPR_BF16_256 1
 #endif
-// WOUT (fused Winograd GEMM + output transform): the register double buffer of the generic loop
-#ifndef PSX_WOUT_PF
-#define PSX_WOUT_PF 1
-#endif
 #ifndef PSX_TAPR_F32_128
 #define PSX_TAPR_F32_128 1
 #endif
@@ -74,12 +70,9 @@ struct Conv2Args {
   // needs no ReLU-mask operand (one full activation read less per BN layer)
   int bmask;
   DetRed det;  // deterministic mode: the launch's row slab (bnfin.hpp)
-  int wH, wW;  // WOUT: the output image (Winograd tiles t = (n, ti, tj) of 4x4 pixels)
   // forward statistics: per-channel shift k subtracted before summing (nullable = 0; bnfin.hpp
   // BnFin::sshift): the slots hold sum(y - k), sum((y - k)^2)
   const float* sshift;
-  // WOUT backward: ReLU mask = [y1 * scale + shift > 0] from this affine [2][OC] (nullable: from bo)
-  const float* bmaff;
   // MODE 3 with the block's 1x1 / stride-2 shortcut folded in (nullable in2): the shortcut's data
   // gradient only reaches the (0, 0) parity class, one tap deep, so that class runs its 3x3 tap
   // and then the shortcut's as extra k-steps: operand dy_sc (in2, same shape as in) against the
@@ -87,14 +80,6 @@ struct Conv2Args {
   const void* in2;
   const void* w2;
   int Kg2;
-  // MODE 0 with the block's 1x1 / stride-2 shortcut folded in (nullable out2): output-channel
-  // tiles n_oc1.. compute the shortcut — its input pixel (2i, 2j) is the 3x3 / stride-2 / pad-1
-  // conv's centre tap, so those tiles run only that tap's k-steps against the shortcut weights
-  // (w2, rows of Kg2) into out2 with the statistics stats2 (shift sshift2): one launch, x read once
-  void* out2;
-  float* stats2;
-  const float* sshift2;
-  int n_oc1;
 };
 
 // Winograd F(4x4,3x3) output transform A^T (wino.hip has the matrices): y = A^T P A
@@ -150,12 +135,7 @@ PSX_DEV const T* gather_src(const Conv2Args& a, int nbase, int hb, int wb, bool 
 // T: activation / weight storage type (common.hpp kEPC/kKS): one k-step is a 128-byte row of
 // every operand = 64 bf16 or 32 fp32 channels; the staging below is written in 16-byte chunks
 // and bytes, so only the element strides (EPC per chunk, KS per k-step) depend on T.
-// WOUT (fp32 Winograd, wino.hip): the GEMM over all 36 batches of a layer (R = 36 "taps", Kg =
-// 36 C) with the output transform fused: at every batch boundary of the k-loop the batch's
-// accumulators are folded into the 16 output pixels of each (tile, channel) element
-// (two-stage, kWinoAT) and reset, so the transformed product P never leaves registers; the epilogue
-// stores y (+ residual) with the BN statistics or the BN-backward sums.
-template <typename T, int BM, int BN, int MODE, bool HAS_RES, bool SPLIT, int WGM = 2, int TAPR = 0, bool WOUT = false>
+template <typename T, int BM, int BN, int MODE, bool HAS_RES, bool SPLIT, int WGM = 2, int TAPR = 0>
 __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   constexpr int EPC = kEPC<T>, KS = kKS<T>;
   const T* const in = (const T*)a.in;
@@ -173,20 +153,10 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   const int nwg = a.n_oc_tiles * a.n_pix_tiles;
   const int tile = xcd_remap(blockIdx.x, nwg);
   const int oc_t = tile % a.n_oc_tiles, pix_t = tile / a.n_oc_tiles;
-  const bool fsc = MODE == 0 && !SPLIT && !TAPR && !WOUT && a.out2 != nullptr && oc_t >= a.n_oc1;
-  if (fsc) {  // a folded-shortcut tile (Conv2Args out2)
-    a.out = a.out2;
-    a.stats = a.stats2;
-    a.sshift = a.sshift2;
-  }
-  const int oc0 = (fsc ? oc_t - a.n_oc1 : oc_t) * BM, pix0 = pix_t * BN;
+  const int oc0 = oc_t * BM, pix0 = pix_t * BN;
   const int split = SPLIT ? blockIdx.y : 0;
-  int ks0 = split * a.kps;
+  const int ks0 = split * a.kps;
   int nk = SPLIT ? min(a.kps, a.Kg / KS - ks0) : a.Kg / KS;
-  if (fsc) {  // the centre tap (1, 1) only
-    ks0 = 4 << (a.log2_icc - 3);
-    nk = 1 << (a.log2_icc - 3);
-  }
   // MODE 3 = stride-2 dgrad, one parity class (py, px) of dx per blockIdx.y: dx(2i+py, 2j+px)
   // only receives taps r = r0, r0+2, .. and s = s0, s0+2, .. (r0 = (py+pad)&1), i.e. a dense
   // GEMM over 1, 2, 2 or 4 of the 9 taps instead of 9 with 3/4 of the products zero.
@@ -202,7 +172,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   if (MODE == 3) {
     nk = (nr * nsx + (sc ? 1 : 0)) << (a.log2_icc - 3);
     if (pix0 >= npix_c) {  // whole workgroup: this class has fewer tiles
-      if (!SPLIT && a.det.slab && (a.stats || a.bpart))  // it still arrives at the launch counter
+      if (!SPLIT && a.det.fix && (a.stats || a.bpart))  // it still arrives at the launch counter
         if (det_finish(a.det, a.bpart ? a.bns : 2, a.OC, a.bpart ? a.bpart : a.stats, pix_t + cls * a.n_pix_tiles,
                        smem) &&
             a.stats && a.fuse_fin)
@@ -216,62 +186,6 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  static_assert(!WOUT || (sizeof(T) == 4 && !SPLIT && !TAPR && MODE == 0 && MT * NT <= 2),
-                "WOUT: fp32, at most two 16x16 MFMA tiles per wave");
-  // WOUT: y[i][j] = sum_r A^T[i][r] Q_r[j], Q_r[j] = sum_s A^T[j][s] P[6 r + s], accumulated in two
-  // stages — per batch b = 6 r + s the 4 values Q_r += A^T[:, s] P_b, per finished row r the 16
-  // outputs y += A^T[:, r] Q_r — 6.7 instead of 16 FMAs per accumulator element and batch
-  constexpr int WT = WOUT ? MT * NT : 1;
-  float yacc[WT][4][WOUT ? 16 : 1];
-  float qacc[WT][4][WOUT ? 4 : 1];
-  if constexpr (WOUT) {
-#pragma unroll
-    for (int w = 0; w < WT; ++w)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) yacc[w][e][q] = 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) qacc[w][e][j] = 0.f;
-      }
-  }
-  // batch boundary (WOUT): fold the batch's product into the row accumulators, reset
-  auto wfold = [&](int ks) {
-    if constexpr (WOUT) {
-      if (((ks + 1) & (a.kps - 1)) == 0) {
-        const int b = __builtin_amdgcn_readfirstlane(ks / a.kps);
-        const int r = b / 6, sc = b - 6 * r;
-        float cs[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) cs[j] = kWinoAT[j][sc];
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-          for (int n = 0; n < NT; ++n) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-              for (int j = 0; j < 4; ++j) qacc[m * NT + n][e][j] += cs[j] * acc[m][n][e];
-            acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-          }
-        if (sc == 5) {
-          float cr[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) cr[i] = kWinoAT[i][r];
-#pragma unroll
-          for (int w = 0; w < WT; ++w)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) yacc[w][e][i * 4 + j] += cr[i] * qacc[w][e][j];
-                qacc[w][e][j] = 0.f;
-              }
-        }
-      }
-    }
-  };
 
   if constexpr (TAPR) {
     static_assert(MODE == 0 || MODE == 1, "tap reuse: forward or stride-1 dgrad");
@@ -349,21 +263,13 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       // into the stage just drained, reads of the next stage's first sub-step — then its MFMAs.
       auto load_frags = [&](const unsigned char* base, int q, u32x4(&fa)[MT], u32x4(&fb)[NT]) {
         const int sx = q >> 1, kk = q & 1;
-        if constexpr (PSX_CONV_ASMRD) {  // untracked reads: sub() waits for exactly its own
-          const unsigned A = lds_off(base) + sx * BM * 128, X = lds_off(base) + XOFF;
+        const unsigned char* A = base + sx * BM * 128;
+        const unsigned char* X = base + XOFF;
 #pragma unroll
-          for (int m = 0; m < MT; ++m) fa[m] = ds_read128u(A + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
+        for (int m = 0; m < MT; ++m)
+          fa[m] = *reinterpret_cast<const u32x4*>(A + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
 #pragma unroll
-          for (int n = 0; n < NT; ++n) fb[n] = ds_read128u(X + (boff[n][sx] ^ (kk << 6)));
-        } else {
-          const unsigned char* A = base + sx * BM * 128;
-          const unsigned char* X = base + XOFF;
-#pragma unroll
-          for (int m = 0; m < MT; ++m)
-            fa[m] = *reinterpret_cast<const u32x4*>(A + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
-#pragma unroll
-          for (int n = 0; n < NT; ++n) fb[n] = *reinterpret_cast<const u32x4*>(X + (boff[n][sx] ^ (kk << 6)));
-        }
+        for (int n = 0; n < NT; ++n) fb[n] = *reinterpret_cast<const u32x4*>(X + (boff[n][sx] ^ (kk << 6)));
       };
       u32x4 fa0[MT], fb0[NT], fa1[MT], fb1[NT];
       if (HALO) __syncthreads();
@@ -379,10 +285,6 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
         const unsigned char* base = smem + (t & 1) * TST;
         auto sub = [&](auto qc, u32x4(&fa)[MT], u32x4(&fb)[NT], u32x4(&na)[MT], u32x4(&nb)[NT]) {
           constexpr int q = decltype(qc)::value, sx = q >> 1;
-          bool ahead = true;  // the next sub-step's reads were issued after this one's
-          // at most 15 reads in flight (the 4-bit counter's range): with more than 7 fragments
-          // per sub-step this one's reads retire before the next one's go out
-          if constexpr (PSX_CONV_ASMRD && 2 * (MT + NT) > 15) lgkm_wait<0>();
           if constexpr (q < 5) {
             load_frags(base, q + 1, na, nb);
           } else if (t + 1 < nmac) {
@@ -392,14 +294,6 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
             asm volatile("" ::: "memory");
             if (t + 2 < nmac) issue_t(t + 2, t & 1);
             load_frags(smem + ((t + 1) & 1) * TST, 0, na, nb);
-          } else {
-            ahead = false;
-          }
-          if constexpr (PSX_CONV_ASMRD) {
-            if (ahead)
-              lgkm_wait<MT + NT>();
-            else
-              lgkm_wait<0>();
           }
           __builtin_amdgcn_sched_barrier(0);
           if constexpr (!HALO && sx != 1) {
@@ -455,8 +349,6 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     const int row = (i * 4 + wid) * 8 + lrow;
     const int c = lpos ^ ((row >> 1) & 7);
     wsrc[i] = wts + (size_t)(oc0 + row) * a.Kg + c * EPC;
-    // shortcut rows: k-step kglob of the centre tap = row k-step kglob - ks0 of w2
-    if (fsc) wsrc[i] = (const T*)a.w2 + (size_t)(oc0 + row) * a.Kg2 + c * EPC - (ptrdiff_t)ks0 * KS;
   }
   const T* wsrc2[MODE == 3 ? LA : 1];
   if constexpr (MODE == 3) {
@@ -590,7 +482,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   };
   if (nk > 0) issue(0, 0);
   if (nk > 1) issue(1, 1);
-  if constexpr (sizeof(T) == 4 && ((PSX_CONV_PF & 2) || (WOUT && PSX_WOUT_PF))) {
+  if constexpr (sizeof(T) == 4 && (PSX_CONV_PF & 2)) {
     // fp32: the fragments of the next half k-step are read before the MFMAs of the current one
     // (register double buffer, as in the tap-reuse loop); the stage boundary — DMA of k-step
     // ks+1 retired, this wave's reads of stage ks retired, barrier, DMA of ks+3 into stage ks —
@@ -625,7 +517,6 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       }
       __builtin_amdgcn_sched_barrier(0);
       mma_tiles<MT, NT, T>(acc, fa1, fb1);
-      wfold(ks);
       stage = nxt;
     }
   } else {
@@ -638,159 +529,16 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (ks + 2 < nk) issue(ks + 2, stage == 0 ? 2 : stage - 1);
-      if constexpr (PSX_CONV_ASMRD) {
-        // both halves' fragments at once (pipeline.hpp ds_read128u); the first half's MFMAs
-        // wait only for their own reads, the second half's retire under them
-        const unsigned sa = lds_off(smem) + stage * STAGE, sbb = sa + BM * 128;
-        // (at most 15 reads in flight, the 4-bit counter's range: tiles with more than 7 fragments
-        // per half read the second half after the first half's MFMAs)
-        constexpr bool both = 2 * (MT + NT) <= 15;
-        u32x4 fa[2][MT], fb[2][NT];
-        auto rdh = [&](int kk) {
 #pragma unroll
-          for (int m = 0; m < MT; ++m) fa[kk][m] = ds_read128u(sa + kmaj2(wm * (BM / WGM) + m * 16 + frow, kk * 4 + fch));
-#pragma unroll
-          for (int n = 0; n < NT; ++n) fb[kk][n] = ds_read128u(sbb + kmaj2(wn * (BN / WGN) + n * 16 + frow, kk * 4 + fch));
-        };
-        rdh(0);
-        if constexpr (both) rdh(1);
-        lgkm_wait<both ? MT + NT : 0>();
-        __builtin_amdgcn_sched_barrier(0);
-        mma_tiles<MT, NT, T>(acc, fa[0], fb[0]);
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!both) rdh(1);
-        lgkm_wait<0>();
-        __builtin_amdgcn_sched_barrier(0);
-        mma_tiles<MT, NT, T>(acc, fa[1], fb[1]);
-        __builtin_amdgcn_sched_barrier(0);
-      } else {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          u32x4 fa[MT], fb[NT];
-          load_frags(stage, kk, fa, fb);
-          mma_tiles<MT, NT, T>(acc, fa, fb);
-        }
+      for (int kk = 0; kk < 2; ++kk) {
+        u32x4 fa[MT], fb[NT];
+        load_frags(stage, kk, fa, fb);
+        mma_tiles<MT, NT, T>(acc, fa, fb);
       }
-      wfold(ks);
       stage = stage == 2 ? 0 : stage + 1;
     }
   }
   }  // generic mainloop
-
-  if constexpr (WOUT) {
-    // lane: 4 consecutive channels oc..oc+3 (e) of tile t per wave tile (m, n); 16 output pixels
-    const bool bwd = a.bpart != nullptr, two = a.by2 != nullptr, st = a.stats != nullptr, maff = a.bmaff != nullptr;
-    float s1[MT][4], s2[MT][4], s3[MT][4], bm1[MT][4], bi1[MT][4], bm2[MT][4], bi2[MT][4], ksh[MT][4], msc[MT][4],
-        msh[MT][4];
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const int oc = oc0 + wm * (BM / WGM) + m * 16 + 4 * (lane >> 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        s1[m][e] = s2[m][e] = s3[m][e] = 0.f;
-        bm1[m][e] = bi1[m][e] = bm2[m][e] = bi2[m][e] = msc[m][e] = msh[m][e] = 0.f;
-        ksh[m][e] = (st && a.sshift) ? a.sshift[oc + e] : 0.f;
-        if (bwd) {
-          bm1[m][e] = a.bsaved1[oc + e];
-          bi1[m][e] = a.bsaved1[a.OC + oc + e];
-          if (two) {
-            bm2[m][e] = a.bsaved2[oc + e];
-            bi2[m][e] = a.bsaved2[a.OC + oc + e];
-          }
-          if (maff) {
-            msc[m][e] = a.bmaff[oc + e];
-            msh[m][e] = a.bmaff[a.OC + oc + e];
-          }
-        }
-      }
-    }
-    const int tw = a.wW >> 2, tpi = (a.wH >> 2) * tw;
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const int t = pix0 + wn * (BN / WGN) + n * 16 + (lane & 15);
-      if (t >= a.npix) continue;
-      const int nn = t / tpi, rem = t - nn * tpi, ti = rem / tw, tj = rem - ti * tw;
-      const size_t tbase = (((size_t)nn * a.wH + 4 * ti) * a.wW + 4 * tj) * a.OC;
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const size_t base = tbase + oc0 + wm * (BM / WGM) + m * 16 + 4 * (lane >> 4);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const size_t off = base + ((size_t)i * a.wW + j) * a.OC;
-            const float(&ya)[4][16] = yacc[m * NT + n];
-            f32x4 v = {ya[0][i * 4 + j], ya[1][i * 4 + j], ya[2][i * 4 + j], ya[3][i * 4 + j]};
-            if (HAS_RES) v += *reinterpret_cast<const f32x4*>((const float*)a.res + off);
-            if (bwd) {
-              const f32x4 y1 = *reinterpret_cast<const f32x4*>((const float*)a.by1 + off);
-              f32x4 om = y1, y2 = {0.f, 0.f, 0.f, 0.f};
-              if (!maff) om = *reinterpret_cast<const f32x4*>((const float*)a.bo + off);
-              if (two) y2 = *reinterpret_cast<const f32x4*>((const float*)a.by2 + off);
-              f32x4 dz;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const bool pos = maff ? y1[e] * msc[m][e] + msh[m][e] > 0.f : om[e] > 0.f;
-                dz[e] = pos ? v[e] : 0.f;
-                s1[m][e] += dz[e];
-                s2[m][e] += dz[e] * (y1[e] - bm1[m][e]) * bi1[m][e];
-                if (two) s3[m][e] += dz[e] * (y2[e] - bm2[m][e]) * bi2[m][e];
-              }
-              *reinterpret_cast<f32x4*>((float*)a.out + off) = a.bmask ? dz : v;
-            } else {
-              *reinterpret_cast<f32x4*>((float*)a.out + off) = v;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const float d = v[e] - ksh[m][e];
-                s1[m][e] += d;
-                s2[m][e] += d * d;
-              }
-            }
-          }
-      }
-    }
-    if (!st && !bwd) return;
-    // lanes of one wave with the same channels differ in lane bits 0..3
-#pragma unroll
-    for (int sh = 1; sh < 16; sh <<= 1)
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          s1[m][e] += __shfl_xor(s1[m][e], sh, 64);
-          s2[m][e] += __shfl_xor(s2[m][e], sh, 64);
-          if (two) s3[m][e] += __shfl_xor(s3[m][e], sh, 64);
-        }
-    // one atomic per (statistic, channel) and workgroup: the WGN pixel-slice waves of a channel
-    // range meet in LDS (a deterministic-mode slab row then has a single writer per element)
-    float* red = reinterpret_cast<float*>(smem);  // [WGN][3][BM]
-    __syncthreads();  // every wave is done with the mainloop's LDS
-    if ((lane & 15) == 0) {
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int row = wm * (BM / WGM) + m * 16 + 4 * (lane >> 4) + e;
-          red[(wn * 3 + 0) * BM + row] = s1[m][e];
-          red[(wn * 3 + 1) * BM + row] = s2[m][e];
-          red[(wn * 3 + 2) * BM + row] = s3[m][e];
-        }
-    }
-    __syncthreads();
-    const int nst = bwd ? a.bns : 2;
-    float* const sdst = bwd ? a.bpart : a.stats;
-    float* dst = a.det.slab ? a.det.slab + (size_t)pix_t * nst * a.OC
-                            : sdst + (size_t)(pix_t & (PSX_STAT_SLOTS - 1)) * nst * a.OC;
-    for (int j = tid; j < nst * BM; j += 256) {
-      const int which = j / BM, row = j - which * BM;
-      float v = 0.f;
-#pragma unroll
-      for (int q = 0; q < WGN; ++q) v += red[(q * 3 + which) * BM + row];
-      atomicAdd(dst + which * a.OC + oc0 + row, v);
-    }
-    if (a.det.slab) det_finish(a.det, nst, a.OC, sdst, pix_t, smem);
-    return;
-  }
 
   if constexpr (SPLIT) {
     float* dst = a.part + (size_t)split * a.npix * a.OC;
@@ -919,15 +667,14 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     }
     __syncthreads();
     const int nst = bwd ? a.bns : 2;
-    float* dst = a.det.slab ? a.det.slab + (size_t)(pix_t + (MODE == 3 ? cls * a.n_pix_tiles : 0)) * nst * a.OC
-                            : (bwd ? a.bpart : a.stats) + (size_t)(pix_t & (PSX_STAT_SLOTS - 1)) * nst * a.OC;
+    float* dst = (bwd ? a.bpart : a.stats) + (size_t)(pix_t & (PSX_STAT_SLOTS - 1)) * nst * a.OC;
     for (int j = tid; j < nst * BM; j += 256) {
       const int which = j / BM, row = j - which * BM;
       const float v = red[which * BM + row] + red[(3 + which) * BM + row] + red[(6 + which) * BM + row] +
                       red[(9 + which) * BM + row];
-      atomicAdd(dst + which * a.OC + oc0 + row, v);
+      stat_add(a.det, dst, which * a.OC + oc0 + row, v);
     }
-    if (a.det.slab) {
+    if (a.det.fix) {
       if (det_finish(a.det, nst, a.OC, bwd ? a.bpart : a.stats, pix_t + (MODE == 3 ? cls * a.n_pix_tiles : 0), smem) &&
           st && a.fuse_fin)
         bn_finalize_block<PSX_STAT_SLOTS>(a.stats, a.fin);
@@ -1032,16 +779,15 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
     mine[16 + j] = st[2][j];
   }
   __syncthreads();
-  float* dst = det.slab ? det.slab + (size_t)blockIdx.x * nst * OC
-                        : (bwd ? bpart : stats) + (size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * nst * OC;
+  float* dst = (bwd ? bpart : stats) + (size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * nst * OC;
   for (int t = threadIdx.x; t < cvec * nst * 8; t += 256) {
     const int cgi = t / (nst * 8), sj = t - cgi * (nst * 8);
     float acc = 0.f;
     for (int q = 0; q < tpp; ++q) acc += sred[(q * cvec + cgi) * 24 + sj];
     const int which = sj >> 3, j = sj & 7;
-    atomicAdd(dst + which * OC + cgi * 8 + j, acc);
+    stat_add(det, dst, which * OC + cgi * 8 + j, acc);
   }
-  if (det.slab) {
+  if (det.fix) {
     if (det_finish(det, nst, OC, bwd ? bpart : stats, blockIdx.x, reinterpret_cast<unsigned char*>(sred)) && stats &&
         fuse_fin)
       bn_finalize_block<PSX_STAT_SLOTS>(stats, fin);
@@ -1075,7 +821,7 @@ struct Plan {
 Plan plan_for(int OC, int npix, int ksteps, bool f32 = false) {
   Plan p{64, 128, 1};
   static const bool f32_128 = [] {  // fp32 128 x 128 tiles: opt-in while measured (bench/f32_tiles.py)
-    const char* e = getenv("PSX_CV_F32_128");
+    const char* e = tune("cv_f32_128");
     return e && e[0] == '1';
   }();
   if ((!f32 || f32_128) && OC % 128 == 0 && (long)(OC / 128) * ((npix + 127) / 128) >= (f32 ? 256 : 512)) {
@@ -1090,12 +836,12 @@ Plan plan_for(int OC, int npix, int ksteps, bool f32 = false) {
   }
   const long tiles = (long)(OC / p.BM) * ((npix + p.BN - 1) / p.BN);
   while (p.splits < 8 && tiles * p.splits < 512 && ksteps / (p.splits * 2) >= 8) p.splits *= 2;
-  // experiment overrides (tile sweep, bench/conv_sweep.py): PSX_CV_BM / PSX_CV_BN / PSX_CV_SPLITS
-  if (const char* e = getenv("PSX_CV_BM")) p.BM = atoi(e);
-  if (const char* e = getenv("PSX_CV_BN")) p.BN = atoi(e);
-  if (const char* e = getenv("PSX_CV_SPLITS")) p.splits = atoi(e);
-  if (const char* e = getenv("PSX_CV_WGM")) p.WGM = atoi(e);
-  if (OC % p.BM || (f32 && p.BM == 128 && !f32_128 && !getenv("PSX_CV_BM"))) p.BM = 64;
+  // experiment overrides (tile sweep, bench/conv_sweep.py): PSX_TUNE cv_bm / PSX_TUNE cv_bn / PSX_TUNE cv_splits
+  if (const char* e = tune("cv_bm")) p.BM = atoi(e);
+  if (const char* e = tune("cv_bn")) p.BN = atoi(e);
+  if (const char* e = tune("cv_splits")) p.splits = atoi(e);
+  if (const char* e = tune("cv_wgm")) p.WGM = atoi(e);
+  if (OC % p.BM || (f32 && p.BM == 128 && !f32_128 && !tune("cv_bm"))) p.BM = 64;
   if (p.splits > ksteps) p.splits = ksteps;
   return p;
 }
@@ -1143,17 +889,17 @@ int launch_tapr(const Conv2Args& a, hipStream_t st) {
 
 // Pixel-tile width of the tap-reuse path for this layer, 0 = not applicable: 3x3 / stride 1 /
 // pad 1, square power-of-two images whose rows tile BN exactly, 64-channel chunks; no split-K.
-// PSX_CV_TAPR=0 disables it, PSX_CV_TAPR_BN=64|128|256 forces the width (sweeps). Other widths
-// (and PSX_CV_TAPR_HALO=1, a test override) take the halo mode with 64-pixel tiles: returns -64.
+// PSX_TUNE cv_tapr=0 disables it, PSX_TUNE cv_tapr_bn=64|128|256 forces the width (sweeps). Other widths
+// (and PSX_TUNE cv_tapr_halo=1, a test override) take the halo mode with 64-pixel tiles: returns -64.
 int tapr_bn(int R, int S, int stride, int pad, int H, int W, int IC, int OC, int npix, bool f32 = false) {
-  if (const char* e = getenv("PSX_CV_TAPR"))
+  if (const char* e = tune("cv_tapr"))
     if (e[0] == '0') return 0;
   if (R != 3 || S != 3 || stride != 1 || pad != 1 || IC % 64 || OC % 64) return 0;
-  const char* he = getenv("PSX_CV_TAPR_HALO");
+  const char* he = tune("cv_tapr_halo");
   const bool halo_off = he && he[0] == '0', halo_force = he && he[0] == '1';
   if (halo_force || H != W || (W & (W - 1)) || 64 % W) return halo_off ? 0 : -64;
   int force = 0;
-  if (const char* e = getenv("PSX_CV_TAPR_BN")) force = atoi(e);
+  if (const char* e = tune("cv_tapr_bn")) force = atoi(e);
   // measured (bench/tapr_probe.py, ResNet-18 B=128, us fwd/dgrad): 64-pixel tiles (2 workgroups
   // per CU) win or tie on every layer — 32x32x64: 27.3/20.9 vs generic 26.3/23.0; 16x16x128:
   // 18.7/15.8 vs 20.6/19.3; 8x8x256: 14.8/13.7 vs 25.5/23.4; 4x4x512: 20.5/19.2 vs 29.3/28.0
@@ -1258,7 +1004,7 @@ int conv_dgrad2_t(Conv2Args& a, float* ws, hipStream_t st) {
   a.n_pix_tiles = (a.npix + p.BN - 1) / p.BN;
   a.splits = p.splits;
   a.kps = (Kg / KS + p.splits - 1) / p.splits;
-  const bool parity = a.stride == 2 && a.log2_icc >= 3 && !getenv("PSX_DGRAD_S2_GATHER");
+  const bool parity = a.stride == 2 && a.log2_icc >= 3 && !tune("dgrad_s2_gather");
   if (p.splits > 1 && !ws && !parity) return -9;  // the parity-class path never splits K
   int e;
   if (a.stride == 1)
@@ -1269,10 +1015,10 @@ int conv_dgrad2_t(Conv2Args& a, float* ws, hipStream_t st) {
     // parity classes: each class GEMM covers dx pixels (2i+py, 2j+px), ~1/4 of them
     Plan q = plan_for(IC_fwd, (a.npix + 3) / 4, Kg / KS, sizeof(T) == 4);
     q.splits = 1;
-    // tile sweep overrides (PSX_DGRAD_S2_BN / _WGM / _BM): the classes are short-K GEMMs
-    if (const char* e = getenv("PSX_DGRAD_S2_BN")) q.BN = atoi(e);
-    if (const char* e = getenv("PSX_DGRAD_S2_WGM")) q.WGM = atoi(e);
-    if (const char* e = getenv("PSX_DGRAD_S2_BM")) q.BM = atoi(e);
+    // tile sweep overrides (PSX_TUNE dgrad_s2_bn / _WGM / _BM): the classes are short-K GEMMs
+    if (const char* e = tune("dgrad_s2_bn")) q.BN = atoi(e);
+    if (const char* e = tune("dgrad_s2_wgm")) q.WGM = atoi(e);
+    if (const char* e = tune("dgrad_s2_bm")) q.BM = atoi(e);
     if (IC_fwd % q.BM) q.BM = 64;
     a.n_oc_tiles = IC_fwd / q.BM;
     a.n_pix_tiles = (Nb * ((H + 1) / 2) * ((W + 1) / 2) + q.BN - 1) / q.BN;
@@ -1336,46 +1082,6 @@ int psx_conv_dgrad2_sc(const void* dy, const void* wd, void* dx, const void* res
                        const BwdStatsDesc* bst, int f32, const void* dy_sc, const void* wd_sc, int Kg_sc,
                        hipStream_t st);
 
-// psx_conv_fwd2 of a 3x3 / stride-2 / pad-1 conv with its block's 1x1 / stride-2 / pad-0 shortcut
-// (same input x, same output channels) folded into the launch (Conv2Args out2): y = conv(x, wf)
-// with stats, y_sc = conv_sc(x, wf_sc) with stats_sc. No in-launch BN finalize, no deterministic
-// mode, and only where the 3x3 conv's own plan needs no split-K. -11: this layer cannot fold (the
-// caller runs the two launches).
-int psx_conv_fwd2_sc(const void* x, const void* wf, void* y, float* stats, const void* zero, int Nb, int H, int W,
-                     int IC, int OC, int Kg, int f32, const float* sshift, const void* wf_sc, int Kg_sc, void* y_sc,
-                     float* stats_sc, const float* sshift_sc, hipStream_t st) {
-  const int KS = f32 ? kKS<float> : kKS<uint16_t>, EPC = f32 ? kEPC<float> : kEPC<uint16_t>;
-  if (det_enabled() || !wf_sc || !y_sc || (stats == nullptr) != (stats_sc == nullptr)) return -11;
-  if (IC < 8 * EPC || (IC & (IC - 1)) || OC % 64 || Kg != 9 * IC || Kg_sc != IC || Kg % KS) return -11;
-  Conv2Args a{};
-  a.in = x;
-  a.w = wf;
-  a.out = y;
-  a.stats = stats;
-  a.sshift = sshift;
-  a.zero = zero;
-  a.w2 = wf_sc;
-  a.Kg2 = Kg_sc;
-  a.out2 = y_sc;
-  a.stats2 = stats_sc;
-  a.sshift2 = sshift_sc;
-  a.Nb = Nb; a.IH = H; a.IW = W; a.IC = IC;
-  a.OH = (H - 1) / 2 + 1;
-  a.OW = (W - 1) / 2 + 1;
-  a.OC = OC; a.R = 3; a.S = 3; a.pad = 1; a.stride = 2;
-  a.Kg = Kg;
-  a.npix = Nb * a.OH * a.OW;
-  a.log2_icc = ilog2i(IC / EPC);
-  const Plan p = plan_for(OC, a.npix, Kg / KS, f32 != 0);
-  if (p.splits > 1) return -11;
-  a.n_oc1 = OC / p.BM;
-  a.n_oc_tiles = 2 * a.n_oc1;
-  a.n_pix_tiles = (a.npix + p.BN - 1) / p.BN;
-  a.splits = 1;
-  a.kps = Kg / KS;
-  return f32 ? dispatch2<float, 0, false>(p, a, st) : dispatch2<uint16_t, 0, false>(p, a, st);
-}
-
 int psx_conv_dgrad2(const void* dy, const void* wd, void* dx, const void* res, const void* zero, float* ws, int Nb,
                     int H, int W, int IC_fwd, int OC_fwd, int R, int S, int stride, int pad, int Kg,
                     const BwdStatsDesc* bst, int f32, hipStream_t st) {
@@ -1395,7 +1101,7 @@ int psx_conv_dgrad2_sc(const void* dy, const void* wd, void* dx, const void* res
   Conv2Args a{};
   if (dy_sc) {
     if (R != 3 || S != 3 || stride != 2 || pad != 1 || res || Kg_sc != OC_fwd || !wd_sc) return -11;
-    if (getenv("PSX_DGRAD_S2_GATHER")) return -11;
+    if (tune("dgrad_s2_gather")) return -11;
     a.in2 = dy_sc;
     a.w2 = wd_sc;
     a.Kg2 = Kg_sc;
@@ -1424,63 +1130,6 @@ int psx_conv_dgrad2_sc(const void* dy, const void* wd, void* dx, const void* res
   a.Kg = Kg;
   a.npix = Nb * H * W;
   return f32 ? conv_dgrad2_t<float>(a, ws, st) : conv_dgrad2_t<uint16_t>(a, ws, st);
-}
-
-// Fused Winograd GEMM + output transform (conv2_kernel WOUT): V [36][T][C] (batch-major), U
-// [K][36][C] -> y [N][H][W][K] (+ res) with the BN statistics (stats) or the BN-backward sums
-// (bst, conv_v2 BwdStatsDesc) of y. 32x32 workgroup tiles (16x16 per wave); C a power of two >= 32.
-int psx_wino_gemm_out(const float* V, const float* U, float* y, const float* res, float* stats,
-                      const BwdStatsDesc* bst, const float* mask_aff, const void* zero, int N, int H, int W, int C,
-                      int K, const float* sshift, int bm, hipStream_t st) {
-  const int T = N * (H / 4) * (W / 4);
-  if (K % bm || (bm != 32 && bm != 64) || C < kKS<float> || (C & (C - 1)) || H % 4 || W % 4 || T < 1) return -2;
-  Conv2Args a{};
-  a.in = V;
-  a.w = U;
-  a.out = y;
-  a.res = res;
-  a.stats = bst ? nullptr : stats;
-  a.sshift = sshift;
-  a.zero = zero;
-  if (bst) {
-    a.bpart = bst->part;
-    a.bo = bst->o;
-    a.by1 = bst->y1;
-    a.by2 = bst->y2;
-    a.bsaved1 = bst->saved1;
-    a.bsaved2 = bst->saved2;
-    a.bns = bst->y2 ? 3 : 2;
-    a.bmask = bst->mask_store;
-    a.bmaff = mask_aff;
-  }
-  a.Nb = 1; a.IH = 36; a.IW = T; a.OH = 1; a.OW = T;
-  a.IC = C;
-  a.OC = K;
-  a.R = 36; a.S = 1; a.pad = 0; a.stride = 1;
-  a.Kg = 36 * C;
-  a.log2_icc = ilog2i(C / kEPC<float>);
-  a.npix = T;
-  a.n_oc_tiles = K / bm;
-  a.n_pix_tiles = (T + 31) / 32;
-  a.splits = 1;
-  a.kps = C / kKS<float>;
-  a.wH = H;
-  a.wW = W;
-  const size_t lds = (size_t)3 * (bm + 32) * 128;
-  const dim3 grid(a.n_oc_tiles * a.n_pix_tiles);
-  with_det(a, a.n_pix_tiles);
-  // bm = 64: 32 x 16 wave tiles (two MFMA tiles per wave), bm = 32: 16 x 16
-  if (bm == 64) {
-    if (res)
-      hipLaunchKernelGGL((conv2_kernel<float, 64, 32, 0, true, false, 2, 0, true>), grid, dim3(256), lds, st, a);
-    else
-      hipLaunchKernelGGL((conv2_kernel<float, 64, 32, 0, false, false, 2, 0, true>), grid, dim3(256), lds, st, a);
-  } else if (res) {
-    hipLaunchKernelGGL((conv2_kernel<float, 32, 32, 0, true, false, 2, 0, true>), grid, dim3(256), lds, st, a);
-  } else {
-    hipLaunchKernelGGL((conv2_kernel<float, 32, 32, 0, false, false, 2, 0, true>), grid, dim3(256), lds, st, a);
-  }
-  return (int)hipGetLastError();
 }
 
 // nb independent fp32 GEMMs P[b][M][N] = A[b] . B[:, b, :]^T with A [nb][M][Kd] (batch-major

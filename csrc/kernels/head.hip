@@ -150,14 +150,14 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ act, in
         x0 += d0 * (y0 - m0) * i0;
         x1 += d1 * (y1v - m1) * i1;
       }
-      float* dst = det.slab ? det.slab + (size_t)b * 2 * C : bs.part + (size_t)(b & (PSX_STAT_SLOTS - 1)) * 2 * C;
-      atomicAdd(dst + c, z0);
-      atomicAdd(dst + c + 1, z1);
-      atomicAdd(dst + C + c, x0);
-      atomicAdd(dst + C + c + 1, x1);
+      float* dst = bs.part + (size_t)(b & (PSX_STAT_SLOTS - 1)) * 2 * C;
+      stat_add(det, dst, c, z0);
+      stat_add(det, dst, c + 1, z1);
+      stat_add(det, dst, C + c, x0);
+      stat_add(det, dst, C + c + 1, x1);
     }
   }
-  if (det.slab) det_finish(det, 2, C, bs.part, blockIdx.x, reinterpret_cast<unsigned char*>(sh));
+  if (det.fix) det_finish(det, 2, C, bs.part, blockIdx.x, reinterpret_cast<unsigned char*>(sh));
 }
 
 // dW[k][c] = sum_b dlogits[b][k] * pooled[b][c]; db[k] = sum_b dlogits[b][k].

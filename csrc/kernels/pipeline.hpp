@@ -21,38 +21,8 @@ PSX_DEV void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// LDS reads outside hipcc's waitcnt tracking. hipcc puts an s_waitcnt lgkmcnt(0) in front of
-// every MFMA group that consumes LDS fragments, so a prefetch of the next group's fragments is
-// waited for too and its latency is exposed each time; reads issued through these wrappers are
-// invisible to that pass, and the kernel waits for exactly the ones a group consumes with a
-// counted lgkm_wait<N> (LDS operations retire in order; no scalar loads may be in flight, they
-// share the counter). The counter is 4 bits: more than 15 reads in flight stall the issue, and
-// waits are capped at 15, which stays correct (in-order retirement).
-// PSX_CONV_ASMRD = 0 builds the mainloops with plain LDS loads (A/B variant).
-#ifndef PSX_CONV_ASMRD
-#define PSX_CONV_ASMRD 0
-#endif
-
-typedef __attribute__((address_space(3))) unsigned char lds_u8;
-
-PSX_DEV unsigned lds_off(const void* p) { return (unsigned)(size_t)(const lds_u8*)p; }
-
-PSX_DEV float ds_read32(unsigned off) {
-  float v;
-  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(off));
-  return v;
-}
-
-PSX_DEV u32x4 ds_read128u(unsigned off) {
-  u32x4 v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(off));
-  return v;
-}
-
-template <int N>
-PSX_DEV void lgkm_wait() {
-  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N > 15 ? 15 : N) : "memory");
-}
+// (Round 4 measured LDS fragment reads issued through inline asm with exact counted lgkmcnt
+// waits: the fp32 step 3.37 -> 3.41 ms, wgrad2f +8-10 %; removed in round 5.)
 
 // compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
 template <int B, int E, typename F>

@@ -140,7 +140,7 @@ extern "C" {
 // runs psx_conv_fwd2 instead).
 int psx_stem_conv(const void* x, const void* wf, void* y, float* stats, const float* sshift, int Nb, int H, int W,
                   int cin, int cp, int OC, int Kg, int f32, hipStream_t st) {
-  if (const char* e = getenv("PSX_STEM_DIRECT"))
+  if (const char* e = tune("stem_direct"))
     if (e[0] == '0') return -11;
   if (cin != 3 || OC != 64 || cp != (f32 ? 4 : 8) || Kg < 9 * cp || W % 4 || det_enabled()) return -11;
   const long npix = (long)Nb * H * W;

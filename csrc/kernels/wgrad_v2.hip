@@ -300,51 +300,21 @@ __global__ __launch_bounds__(256) void wgrad2f_kernel(Wgrad2Args a) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (st + NS - 1 < nsteps) issue(st + NS - 1, stage == 0 ? NS - 1 : stage - 1);
-    if constexpr (!PSX_CONV_ASMRD) {
-      const unsigned char* X = smem + stage * STAGE;
-      const unsigned char* D = X + XT;
+    const unsigned char* X = smem + stage * STAGE;
+    const unsigned char* D = X + XT;
 #pragma unroll
-      for (int s4 = 0; s4 < PS / 4; ++s4) {
-        const int row = 4 * s4 + kq;
-        float fa[MT], fb[NT];
+    for (int s4 = 0; s4 < PS / 4; ++s4) {
+      const int row = 4 * s4 + kq;
+      float fa[MT], fb[NT];
 #pragma unroll
-        for (int m = 0; m < MT; ++m) fa[m] = *reinterpret_cast<const float*>(X + row * XROWB + aoff[m]);
+      for (int m = 0; m < MT; ++m) fa[m] = *reinterpret_cast<const float*>(X + row * XROWB + aoff[m]);
 #pragma unroll
-        for (int n = 0; n < NT; ++n) fb[n] = *reinterpret_cast<const float*>(D + row * DROWB + boff[n]);
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-          for (int n = 0; n < NT; ++n)
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[m], fb[n], acc[m][n], 0, 0, 0);
-      }
-    } else {
-    // fragment reads run three four-pixel steps ahead of the MFMAs (pipeline.hpp ds_read32):
-    // step s4 waits only for its own reads (<= 15 in flight, the 4-bit counter's range: exact counts)
-    const unsigned xb = lds_off(smem) + stage * STAGE, db = xb + XT;
-    constexpr int RS = MT + NT, NST = PS / 4, AHEAD = 15 / RS < 1 ? 1 : (15 / RS > 3 ? 3 : 15 / RS);
-    float fa[NST][MT], fb[NST][NT];
-    auto rd = [&](int s4) {
-      const int row = 4 * s4 + kq;  // (row & 1) == (kq & 1): the swizzle bit is in aoff / boff
-#pragma unroll
-      for (int m = 0; m < MT; ++m) fa[s4][m] = ds_read32(xb + row * XROWB + aoff[m]);
-#pragma unroll
-      for (int n = 0; n < NT; ++n) fb[s4][n] = ds_read32(db + row * DROWB + boff[n]);
-    };
-#pragma unroll
-    for (int s4 = 0; s4 < AHEAD; ++s4) rd(s4);
-    static_for<0, NST>([&](auto sc) {
-      constexpr int s4 = decltype(sc)::value;
-      constexpr int later = (s4 + AHEAD - 1 < NST - 1 ? s4 + AHEAD - 1 : NST - 1) - s4;  // steps issued after s4
-      lgkm_wait<later * RS>();
-      __builtin_amdgcn_sched_barrier(0);
+      for (int n = 0; n < NT; ++n) fb[n] = *reinterpret_cast<const float*>(D + row * DROWB + boff[n]);
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int n = 0; n < NT; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[s4][m], fb[s4][n], acc[m][n], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (s4 + AHEAD < NST) rd(s4 + AHEAD);
-    });
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[m], fb[n], acc[m][n], 0, 0, 0);
     }
     stage = stage == NS - 1 ? 0 : stage + 1;
   }
@@ -696,11 +666,11 @@ struct WPlan {
   int BR, BC, NS, splits, sps;
 };
 
-// Share of the chip the weight gradient plans for (PSX_WG_SHARE, default 1): below 1 when it runs
+// Share of the chip the weight gradient plans for (PSX_TUNE wg_share, default 1): below 1 when it runs
 // on a side stream next to the dgrad -> BN-backward chain (models/engine.py wg_stream).
 int wg_slots(int occ) {
   static const double share = [] {
-    const char* e = getenv("PSX_WG_SHARE");
+    const char* e = tune("wg_share");
     const double v = e ? atof(e) : 1.0;
     return v > 0.05 && v <= 1.0 ? v : 1.0;
   }();
@@ -946,14 +916,14 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
   a.div_ow = make_fastdiv(OW);
   a.div_s = make_fastdiv(S);
   if (OC % 64 || Kg % 64) return -2;
-  const char* w3env = getenv("PSX_WG3");
+  const char* w3env = tune("wg3");
   const bool w3ok = R == 3 && S == 3 && stride == 1 && pad == 1 && IC % 64 == 0 && !(w3env && w3env[0] == '0');
   if (f32 && w3ok && (W & (W - 1)) == 0 && (H & (H - 1)) == 0 && W <= 32 && W >= 2 && a.npix % 32 == 0 &&
       Kg == 9 * IC) {
-    // 3x3 stride-1 layers: fp32 tap-reuse kernel (PSX_WG3=0 disables)
+    // 3x3 stride-1 layers: fp32 tap-reuse kernel (PSX_TUNE wg3=0 disables)
     WPlan p = wplan3f(OC, IC, Kg, a.npix);
-    if (const char* e = getenv("PSX_WG_BC")) p.BC = atoi(e);
-    if (const char* e = getenv("PSX_WGF_SPLITS"); e && atoi(e) > 0) {
+    if (const char* e = tune("wg_bc")) p.BC = atoi(e);
+    if (const char* e = tune("wgf_splits"); e && atoi(e) > 0) {
       const int steps = a.npix / 32;
       p.sps = (steps + atoi(e) - 1) / atoi(e);
       p.splits = (steps + p.sps - 1) / p.sps;
@@ -972,9 +942,9 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
     a.log2_icc = ilog2w(IC / 4);
     if (IC % 4 || (IC & (IC - 1))) return -2;
     WPlan p = wplanf(OC, Kg, a.npix);
-    if (const char* e = getenv("PSX_WGF_BR")) p.BR = atoi(e);
-    if (const char* e = getenv("PSX_WGF_BC")) p.BC = atoi(e);
-    if (const char* e = getenv("PSX_WGF_SPLITS"); e && atoi(e) > 0) {  // sweeps
+    if (const char* e = tune("wgf_br")) p.BR = atoi(e);
+    if (const char* e = tune("wgf_bc")) p.BC = atoi(e);
+    if (const char* e = tune("wgf_splits"); e && atoi(e) > 0) {  // sweeps
       const int steps = (a.npix + 31) / 32;
       p.sps = (steps + atoi(e) - 1) / atoi(e);
       p.splits = (steps + p.sps - 1) / p.sps;
@@ -992,16 +962,16 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
     else e = launch_w2f<64, 64>(a, st);
     return e ? -e : p.splits;
   }
-  // 3x3 stride-1 layers, tap-reuse kernel (PSX_WG3=0 disables): power-of-two rows (64-pixel
+  // 3x3 stride-1 layers, tap-reuse kernel (PSX_TUNE wg3=0 disables): power-of-two rows (64-pixel
   // steps), or widths dividing 56 (ResNet-50: 56-pixel steps of whole rows, G)
   const bool pow2 = (W & (W - 1)) == 0 && (H & (H - 1)) == 0 && W <= 64 && W >= 2 && a.npix % 64 == 0;
   const bool gen = !pow2 && W >= 2 && 56 % W == 0 && a.npix % 56 == 0;
   if (w3ok && (pow2 || gen)) {
     const int pix = pow2 ? 64 : 56;
     WPlan p = wplan3(OC, IC, Kg, a.npix, pix);
-    if (const char* e = getenv("PSX_WG_BC")) p.BC = atoi(e);
-    if (const char* e = getenv("PSX_WG_NS")) p.NS = atoi(e) >= 6 ? 6 : 3;
-    if (const char* e = getenv("PSX_WG_SPLITS")) {
+    if (const char* e = tune("wg_bc")) p.BC = atoi(e);
+    if (const char* e = tune("wg_ns")) p.NS = atoi(e) >= 6 ? 6 : 3;
+    if (const char* e = tune("wg_splits")) {
       const int steps = a.npix / pix;
       p.sps = (steps + atoi(e) - 1) / atoi(e);
       p.splits = (steps + p.sps - 1) / p.sps;
@@ -1025,10 +995,10 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
     return e ? -e : p.splits;
   }
   WPlan p = wplan(OC, Kg, a.npix);
-  // experiment overrides (tile sweep): PSX_WG_BR / PSX_WG_BC / PSX_WG_SPLITS
-  if (const char* e = getenv("PSX_WG_BR")) p.BR = atoi(e);
-  if (const char* e = getenv("PSX_WG_BC")) p.BC = atoi(e);
-  if (const char* e = getenv("PSX_WG_SPLITS")) {
+  // experiment overrides (tile sweep): PSX_TUNE wg_br / PSX_TUNE wg_bc / PSX_TUNE wg_splits
+  if (const char* e = tune("wg_br")) p.BR = atoi(e);
+  if (const char* e = tune("wg_bc")) p.BC = atoi(e);
+  if (const char* e = tune("wg_splits")) {
     const int steps = (a.npix + 63) / 64;
     p.sps = (steps + atoi(e) - 1) / atoi(e);
     p.splits = (steps + p.sps - 1) / p.sps;

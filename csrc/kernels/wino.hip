@@ -10,7 +10,7 @@
 // 144 (4x fewer MFMA flops) for ~2.25x the activation bytes in the transformed domain. The
 // arithmetic stays fp32 end to end (transforms, MFMA operands, fp32 accumulation): relative
 // error vs an fp64 reference ~3e-6 (direct fp32: ~2e-7) — the algorithm MIOpen / cuDNN pick for
-// fp32 3x3 convolutions. PSX_WINO=0 (engine) keeps the direct kernels.
+// fp32 3x3 convolutions. PSX_TUNE wino=0 (engine) keeps the direct kernels.
 //
 // Layouts (T = N * (H/4) * (W/4) output tiles, tile t = (n, ti, tj)):
 //   V [36][T][C]   input tiles d (6x6 window at (4ti-1, 4tj-1), zero padded) -> B^T d B
@@ -38,111 +38,12 @@
 
 extern "C" int psx_bgemm_f32(const float* A, const float* B, float* P, const void* zero, int M, int N, int Kd, int nb,
                              int cfg, hipStream_t st);
-extern "C" int psx_wino_gemm_out(const float* V, const float* U, float* y, const float* res, float* stats,
-                                 const void* bst, const float* mask_aff, const void* zero, int N, int H, int W, int C,
-                                 int K, const float* sshift, int bm, hipStream_t st);
 extern "C" int psx_wino_wout(const float* part, void* out, int out_fp16, float scale, int K, int C, int q,
                              hipStream_t st);
-extern "C" int psx_sk_gemm_nt(const float* A, const float* B, float* C, long sa_row, long sa_b, long sb_row,
-                              long sb_b, long sc_row, long sc_b, int M, int N, int Kd, int nb, const void* zero, int bn,
-                              hipStream_t st);
 extern "C" int psx_bgemm_tn_f32(const float* X, const float* D, float* part, const void* zero, int T, int C, int K,
                                 int nb, int q, int BR, int BC, hipStream_t st);
 
 namespace psx {
-
-// V[b][t][c]: one thread per (tile, channel); block = 64 channels x 4 tiles.
-// bnpart (nullable): x is the PRE-BatchNorm conv output z of the previous layer, and the operand
-// is relu(BN(z)) — the training-mode BN finalize (batch statistics from the slot rows
-// bnpart[slot][2][C], as bnfin.hpp bn_fin_lds computes them) and the BN + ReLU apply are folded
-// into this load, so the activation relu(BN(z)) is never written. The workgroups of tile row 0
-// publish the affine, saved statistics and running statistics of their channels.
-__global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ x, float* __restrict__ V, int T, int H,
-                                                      int W, int C, const float* __restrict__ bnpart, WinoBnFin fin) {
-  __shared__ float aff[2][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int tw = W >> 2, tpi = (H >> 2) * tw;
-  float sc = 1.f, sh = 0.f;
-  if (bnpart && threadIdx.x < 64) {  // wave 0 finalizes the workgroup's 64 channels
-    double s = 0.0, ss = 0.0;
-#pragma unroll
-    for (int t = 0; t < PSX_STAT_SLOTS; ++t) {
-      s += bnpart[(size_t)t * 2 * C + c];
-      ss += bnpart[(size_t)t * 2 * C + C + c];
-    }
-    double mean, var;
-    bn_moments(s, ss, fin.count, fin.sshift ? fin.sshift[c] : 0.f, mean, var);
-    const float invstd = (float)(1.0 / sqrt(var + (double)fin.eps));
-    sc = fin.gamma[c] * invstd;
-    sh = fin.beta[c] - (float)mean * sc;
-    aff[0][threadIdx.x] = sc;
-    aff[1][threadIdx.x] = sh;
-    if (blockIdx.y == 0) {
-      fin.scale[c] = sc;
-      fin.shift[c] = sh;
-      fin.save_mean[c] = (float)mean;
-      fin.save_invstd[c] = invstd;
-      if (fin.sshift_next) fin.sshift_next[c] = (float)mean;
-      if (fin.run_mean) {
-        const double unb = fin.count > 1.f ? var * fin.count / (fin.count - 1.0) : var;
-        fin.run_mean[c] = (1.f - fin.momentum) * fin.run_mean[c] + fin.momentum * (float)mean;
-        fin.run_var[c] = (1.f - fin.momentum) * fin.run_var[c] + fin.momentum * (float)unb;
-      }
-    }
-  }
-  if (bnpart) {
-    __syncthreads();
-    sc = aff[0][threadIdx.x & 63];
-    sh = aff[1][threadIdx.x & 63];
-  }
-  for (int t = blockIdx.y * 4 + (threadIdx.x >> 6); t < T; t += 4 * gridDim.y) {
-    const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
-    const int h0 = 4 * ti - 1, w0 = 4 * tj - 1;
-    const float* xn = x + (size_t)n * H * W * C + c;
-    // all 36 loads unconditional (a padding position reads pixel (0, 0) of the image and is
-    // zeroed after): per-element guarded loads made the compiler wait for every load before the
-    // next (36 serialized round trips; 4x4x512 layer 11.8 us for a 2.5 us byte time)
-    float d[6][6];
-    unsigned okr = 0, okc = 0;
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      okr |= (unsigned)((unsigned)(h0 + r) < (unsigned)H) << r;
-      okc |= (unsigned)((unsigned)(w0 + r) < (unsigned)W) << r;
-    }
-#pragma unroll
-    for (int r = 0; r < 6; ++r)
-#pragma unroll
-      for (int s = 0; s < 6; ++s) {
-        const bool ok = (okr >> r) & (okc >> s) & 1u;
-        d[r][s] = xn[ok ? ((size_t)(h0 + r) * W + (w0 + s)) * C : 0];
-      }
-#pragma unroll
-    for (int r = 0; r < 6; ++r)
-#pragma unroll
-      for (int s = 0; s < 6; ++s) {
-        const bool ok = (okr >> r) & (okc >> s) & 1u;
-        const float v = bnpart ? fmaxf(d[r][s] * sc + sh, 0.f) : d[r][s];
-        d[r][s] = ok ? v : 0.f;  // zero padding stays zero (outside the image, after BN + ReLU)
-      }
-    float e[6][6];  // e = B^T d (columns)
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      float col[6] = {d[0][s], d[1][s], d[2][s], d[3][s], d[4][s], d[5][s]}, r6[6];
-      wino_bt6(col, r6);
-#pragma unroll
-      for (int r = 0; r < 6; ++r) e[r][s] = r6[r];
-    }
-    float* vt = V + (size_t)t * C + c;
-    const size_t bs = (size_t)T * C;
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {  // rows: (B^T d) B
-      float r6[6];
-      wino_bt6(e[r], r6);
-#pragma unroll
-      for (int s = 0; s < 6; ++s) vt[(r * 6 + s) * bs] = r6[s];
-    }
-  }
-}
 
 __constant__ float kWinoG[6][3] = {{0.25f, 0.f, 0.f},
                                    {-1.f / 6.f, -1.f / 6.f, -1.f / 6.f},
@@ -259,156 +160,10 @@ __global__ __launch_bounds__(64) void wino_w_multi_kernel(WinoWBatch bt) {
   }
 }
 
-// y = A^T P A (+ res); forward: BN partial sums (sum y, sum y^2) of the stored values into slot
-// rows stats[slot][2][K]; data gradient (bs.part): the BN-backward sums of the consumer BN
-// instead (what the direct dgrad epilogue fuses). Block = 64 channels x 4 tiles, one tile per
-// wave.
-// Deterministic mode (det.slab): each workgroup's sums go to slab row blockIdx.y and the launch
-// reduces the rows in a fixed order (bnfin.hpp det_finish) into slot row 0.
-template <bool RES, bool BWD, bool MAFF, bool TWO>
-__global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__ P, float* __restrict__ y,
-                                                       const float* __restrict__ res, float* __restrict__ stats, int T,
-                                                       int H, int W, int K, WinoBwdStats bs, DetRed det,
-                                                       const float* __restrict__ sshift) {
-  __shared__ float red[3][4][64];
-  const int kl = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int k = blockIdx.x * 64 + kl;
-  const int tw = W >> 2, tpi = (H >> 2) * tw;
-  const size_t bstride = (size_t)T * K;
-  constexpr bool bwd = BWD, two = BWD && TWO;
-  float m1 = 0.f, i1 = 0.f, m2 = 0.f, i2 = 0.f, msc = 0.f, msh = 0.f;
-  if constexpr (bwd) {
-    m1 = bs.saved1[k];
-    i1 = bs.saved1[K + k];
-    if constexpr (MAFF) {
-      msc = bs.mask_aff[k];
-      msh = bs.mask_aff[K + k];
-    }
-    if constexpr (two) {
-      m2 = bs.saved2[k];
-      i2 = bs.saved2[K + k];
-    }
-  }
-  float s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  const float kshift = (!bwd && sshift) ? sshift[k] : 0.f;  // forward statistics: shifted sums
-  for (int t = blockIdx.y * 4 + ty; t < T; t += 4 * gridDim.y) {
-    const float* pt = P + (size_t)t * K + k;
-    const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
-    const size_t base = (((size_t)n * H + 4 * ti) * W + 4 * tj) * K + k;
-    // every load of the tile issued up front (the variant is a template, so no per-element
-    // branch splits them into dependent round trips)
-    float m[6][6], rv[16], y1v[16], ov[16], y2v[16];
-#pragma unroll
-    for (int b = 0; b < 36; ++b) m[b / 6][b % 6] = pt[b * bstride];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const size_t off = base + ((size_t)(e >> 2) * W + (e & 3)) * K;
-      if constexpr (RES) rv[e] = res[off];
-      if constexpr (bwd) {
-        y1v[e] = bs.y1[off];
-        if constexpr (!MAFF) ov[e] = bs.o[off];
-        if constexpr (two) y2v[e] = bs.y2[off];
-      }
-    }
-    float e6[4][6];  // A^T m (columns)
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      float col[6] = {m[0][s], m[1][s], m[2][s], m[3][s], m[4][s], m[5][s]}, o[4];
-      wino_at6(col, o);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) e6[i][s] = o[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float o[4];
-      wino_at6(e6[i], o);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int e = i * 4 + j;
-        const size_t off = base + ((size_t)i * W + j) * K;
-        float v = o[j];
-        if constexpr (RES) v += rv[e];
-        if constexpr (bwd) {
-          const float y1 = y1v[e];
-          bool pos;
-          if constexpr (MAFF)
-            pos = y1 * msc + msh > 0.f;
-          else
-            pos = ov[e] > 0.f;
-          const float dz = pos ? v : 0.f;
-          s1 += dz;
-          s2 += dz * (y1 - m1) * i1;
-          if constexpr (two) s3 += dz * (y2v[e] - m2) * i2;
-          y[off] = bs.mask_store ? dz : v;
-        } else {
-          y[off] = v;
-          const float d = v - kshift;
-          s1 += d;
-          s2 += d * d;
-        }
-      }
-    }
-  }
-  float* dst = bwd ? bs.part : stats;
-  if (!dst) return;
-  const int nst = bwd ? (two ? 3 : 2) : 2;
-  red[0][ty][kl] = s1;
-  red[1][ty][kl] = s2;
-  red[2][ty][kl] = s3;
-  __syncthreads();
-  float* row = det.slab ? det.slab + (size_t)blockIdx.y * nst * K
-                        : dst + (size_t)(blockIdx.y & (PSX_STAT_SLOTS - 1)) * nst * K;
-  if (threadIdx.x < 64 * nst) {
-    const int which = threadIdx.x >> 6;
-    const float v = red[which][0][kl] + red[which][1][kl] + red[which][2][kl] + red[which][3][kl];
-    atomicAdd(row + (size_t)which * K + k, v);
-  }
-  if (det.slab) {
-    __syncthreads();  // red[] is reused as the hand-off flag
-    det_finish(det, nst, K, dst, blockIdx.y, reinterpret_cast<unsigned char*>(&red[0][0][0]));
-  }
-}
-
-// Weight gradient, dy side: DY[b][t][k] = (A dy_t A^T)[b] for the 4x4 output tile dy_t
-// (A = (A^T)^T, 6x4). Same thread layout as wino_in_kernel.
-__global__ __launch_bounds__(256) void wino_dy_kernel(const float* __restrict__ dy, float* __restrict__ D, int T, int H,
-                                                      int W, int K) {
-  const int k = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int tw = W >> 2, tpi = (H >> 2) * tw;
-  const size_t bs = (size_t)T * K;
-  for (int t = blockIdx.y * 4 + (threadIdx.x >> 6); t < T; t += 4 * gridDim.y) {
-    const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
-    const float* src = dy + (((size_t)n * H + 4 * ti) * W + 4 * tj) * K + k;
-    float e[6][4];  // e = A dy (columns)
-    {
-      float y[4][4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) y[i][j] = src[((size_t)i * W + j) * K];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float col[4] = {y[0][j], y[1][j], y[2][j], y[3][j]}, r6[6];
-        wino_a4(col, r6);
-#pragma unroll
-        for (int r = 0; r < 6; ++r) e[r][j] = r6[r];
-      }
-    }
-    float* dt = D + (size_t)t * K + k;
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      float r6[6];
-      wino_a4(e[r], r6);
-#pragma unroll
-      for (int s = 0; s < 6; ++s) dt[(r * 6 + s) * bs] = r6[s];
-    }
-  }
-}
-
-// ---- Split transforms: one tile per 6-wave workgroup iteration, one transform row per wave ----
-// The kernels above give every thread a whole tile (36 loads + 36 stores of one (tile, channel)):
-// on the 4x4 / 8x8 layers that is 1-4 waves per CU, each one long dependent chain, and the
-// launch runs at 2-4x its byte time. Here a workgroup = 64 channels x 6 waves takes a tile per
+// ---- Transforms: one tile per 6-wave workgroup iteration, one transform row per wave ----
+// (A thread per whole tile — 36 loads + 36 stores of one (tile, channel) — left the 4x4 / 8x8
+// layers at 1-4 waves per CU, each one long dependent chain, at 2-4x their byte time; that form
+// was removed in round 5.) Here a workgroup = 64 channels x 6 waves takes a tile per
 // iteration: wave r loads row r of the tile (6 loads), applies the row transform, hands the 6
 // results over LDS (double-buffered: one barrier per tile), and wave s then applies the column
 // transform to column s and stores it (6 stores). 6x the waves, 1/6 of the chain per wave, the
@@ -422,7 +177,12 @@ int wino_xf_grid(int T, int cblocks) {
   return gy > T ? T : gy;
 }
 
-// V = B^T d B (wino_in_kernel, split): bnpart / fin as there
+// V[b][t][c] = B^T d B of the 6x6 input window of tile t (zero padded).
+// bnpart (nullable): x is the PRE-BatchNorm conv output z of the previous layer, and the operand
+// is relu(BN(z)) — the training-mode BN finalize (batch statistics from the slot rows
+// bnpart[slot][2][C], as bnfin.hpp bn_fin_lds computes them) and the BN + ReLU apply are folded
+// into this load, so the activation relu(BN(z)) is never written. The workgroups of tile row 0
+// publish the affine, saved statistics and running statistics of their channels.
 __global__ __launch_bounds__(384) void wino_in_xf_kernel(const float* __restrict__ x, float* __restrict__ V, int T,
                                                          int H, int W, int C, const float* __restrict__ bnpart,
                                                          WinoBnFin fin) {
@@ -430,7 +190,7 @@ __global__ __launch_bounds__(384) void wino_in_xf_kernel(const float* __restrict
   __shared__ float aff[2][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  const int tw = W >> 2, tpi = (H >> 2) * tw;
+  const int tw = (W + 3) >> 2, tpi = ((H + 3) >> 2) * tw;  // partial edge tiles
   const size_t bs = (size_t)T * C;
   auto load = [&](int t, float (&d)[6], unsigned& okc, bool& okr) {
     const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
@@ -452,7 +212,7 @@ __global__ __launch_bounds__(384) void wino_in_xf_kernel(const float* __restrict
   if (t < T) load(t, d, okc, okr);
   float sc = 1.f, sh = 0.f;
   if (bnpart) {
-    if (wv == 0) {  // BN finalize of the workgroup's 64 channels (wino_in_kernel)
+    if (wv == 0) {  // BN finalize of the workgroup's 64 channels
       double s = 0.0, ss = 0.0;
 #pragma unroll
       for (int q = 0; q < PSX_STAT_SLOTS; ++q) {
@@ -506,7 +266,8 @@ __global__ __launch_bounds__(384) void wino_in_xf_kernel(const float* __restrict
   }
 }
 
-// D = A dy A^T (wino_dy_kernel, split): waves 0-3 load the 4 rows of the dy tile
+// Weight gradient, dy side: D[b][t][k] = (A dy_t A^T)[b] for the 4x4 output tile dy_t
+// (A = (A^T)^T, 6x4): waves 0-3 load the 4 rows of the dy tile
 // ybn / bpart (nullable): dy is the BN backward k1 dz + k2 ybn + k3 of dz (the dy argument) —
 // the BN-backward apply folded in (wino.hpp wino_bwd_coef: the same coefficients and rounding as
 // the fused data gradient that consumes the same dy)
@@ -517,7 +278,7 @@ __global__ __launch_bounds__(384) void wino_dy_xf_kernel(const float* __restrict
   __shared__ float kc[3][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + lane;
-  const int tw = W >> 2, tpi = (H >> 2) * tw;
+  const int tw = (W + 3) >> 2, tpi = ((H + 3) >> 2) * tw;  // partial edge tiles
   const size_t bs = (size_t)T * K;
   float k1 = 1.f, k2 = 0.f, k3 = 0.f;
   if (bpart) {
@@ -535,14 +296,20 @@ __global__ __launch_bounds__(384) void wino_dy_xf_kernel(const float* __restrict
   }
   auto load = [&](int t, float (&y)[4]) {
     const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
-    const size_t off = (((size_t)n * H + 4 * ti + wv) * W + 4 * tj) * K + k;
+    // partial edge tiles: row 4 ti + wv / columns 4 tj + j outside the image are zero dy (after
+    // the BN-backward fold too: its k3 would make them non-zero); their loads read in bounds
+    const bool rok = 4 * ti + wv < H;
+    const int vj = min(4, W - 4 * tj);
+    const size_t off = (((size_t)n * H + (rok ? 4 * ti + wv : 4 * ti)) * W + 4 * tj) * K + k;
     const float* src = dy + off;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) y[j] = src[(size_t)j * K];
+    for (int j = 0; j < 4; ++j) y[j] = src[(size_t)(j < vj ? j : 0) * K];
     if (bpart) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) y[j] = wino_bwd_apply(y[j], ybn[off + (size_t)j * K], k1, k2, k3);
+      for (int j = 0; j < 4; ++j) y[j] = wino_bwd_apply(y[j], ybn[off + (size_t)(j < vj ? j : 0) * K], k1, k2, k3);
     }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = (rok && j < vj) ? y[j] : 0.f;
   };
   int t = blockIdx.y;
   float y[4];
@@ -565,8 +332,12 @@ __global__ __launch_bounds__(384) void wino_dy_xf_kernel(const float* __restrict
   }
 }
 
-// y = A^T P A (wino_out_kernel, split): wave r loads row r of the 6x6 tile and applies A^T to
-// it; waves 0-3 then each finish output column j (pixels (i, j), i = 0..3) with its epilogue.
+// y = A^T P A (+ res); forward: BN partial sums (sum y - k, (y - k)^2) of the stored values into
+// slot rows stats[slot][2][K]; data gradient (bs.part): the BN-backward sums of the consumer BN
+// instead (what the direct dgrad epilogue fuses). Wave r loads row r of the 6x6 tile and applies
+// A^T to it; waves 0-3 then each finish output column j (pixels (i, j), i = 0..3) with its
+// epilogue. Deterministic mode (det.fix): the sums go to exact fixed-point accumulators and the
+// launch's last workgroup writes them into slot row 0 (bnfin.hpp DetRed).
 template <bool RES, bool BWD, bool MAFF, bool TWO>
 __global__ __launch_bounds__(384) void wino_out_xf_kernel(const float* __restrict__ P, float* __restrict__ y,
                                                           const float* __restrict__ res, float* __restrict__ stats,
@@ -576,7 +347,7 @@ __global__ __launch_bounds__(384) void wino_out_xf_kernel(const float* __restric
   __shared__ float red[3][4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + lane;
-  const int tw = W >> 2, tpi = (H >> 2) * tw;
+  const int tw = (W + 3) >> 2, tpi = ((H + 3) >> 2) * tw;  // partial edge tiles
   const size_t bstride = (size_t)T * K;
   constexpr bool bwd = BWD, two = BWD && TWO;
   float m1 = 0.f, i1 = 0.f, m2 = 0.f, i2 = 0.f, msc = 0.f, msh = 0.f;
@@ -612,12 +383,17 @@ __global__ __launch_bounds__(384) void wino_out_xf_kernel(const float* __restric
       for (int j = 0; j < 4; ++j) xf[p][wv][j][lane] = q[j];
     }
     const int n = t / tpi, rem = t - n * tpi, ti = rem / tw, tj = rem - ti * tw;
-    const size_t base = (((size_t)n * H + 4 * ti) * W + 4 * tj + wv) * K + k;  // pixel (0, wv)
+    // partial edge tiles: this wave's output column 4 tj + wv and rows 4 ti + i must be inside the
+    // image (a missing pixel's loads read the tile's first pixel, in bounds, and are discarded)
+    const int vi = min(4, H - 4 * ti);
+    const bool cok = 4 * tj + wv < W;
+    const size_t base0 = (((size_t)n * H + 4 * ti) * W + 4 * tj) * K + k;
+    const size_t base = cok ? base0 + (size_t)wv * K : base0;  // pixel (0, wv)
     float rv[4], y1v[4], ov[4], y2v[4];
     if (wv < 4) {  // the epilogue's operands, issued before the barrier
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const size_t off = base + (size_t)i * W * K;
+        const size_t off = base + (size_t)(i < vi ? i : 0) * W * K;
         if constexpr (RES) rv[i] = res[off];
         if constexpr (bwd) {
           y1v[i] = bs.y1[off];
@@ -634,6 +410,7 @@ __global__ __launch_bounds__(384) void wino_out_xf_kernel(const float* __restric
       wino_at6(col, o);  // output column wv: A^T applied
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        if (!cok || i >= vi) continue;
         const size_t off = base + (size_t)i * W * K;
         float v = o[i];
         if constexpr (RES) v += rv[i];
@@ -667,20 +444,21 @@ __global__ __launch_bounds__(384) void wino_out_xf_kernel(const float* __restric
     red[2][wv][lane] = s3;
   }
   __syncthreads();
-  float* row = det.slab ? det.slab + (size_t)blockIdx.y * nst * K
-                        : dst + (size_t)(blockIdx.y & (PSX_STAT_SLOTS - 1)) * nst * K;
+  float* row = dst + (size_t)(blockIdx.y & (PSX_STAT_SLOTS - 1)) * nst * K;
   if (threadIdx.x < 64 * nst) {
     const int which = threadIdx.x >> 6;
     const float v = red[which][0][lane] + red[which][1][lane] + red[which][2][lane] + red[which][3][lane];
-    atomicAdd(row + (size_t)which * K + k, v);
+    stat_add(det, row, which * K + k, v);
   }
-  if (det.slab) {
+  if (det.fix) {
     __syncthreads();  // red[] is reused as the hand-off flag
     det_finish(det, nst, K, dst, blockIdx.y, reinterpret_cast<unsigned char*>(&red[0][0][0]));
   }
 }
 
-// dW = scale * G^T M G (wino_wout_kernel, split): a workgroup = 64 (k, c) pairs x 6 waves; wave r
+// dW[k][c][3][3] = scale * G^T M G, M[b] = sum of the q partial slabs part[b * q + j][k][c] (the
+// batched TN GEMM's split of each batch over tile ranges); OutT = uint16_t: the fp16 wire
+// (reference codec), float: fp32 gradients; OIHW like wgrad_reduce's output. A workgroup = 64 (k, c) pairs x 6 waves; wave r
 // sums the q partial slabs of row r of M (6 q loads in flight, unrolled for Q > 0) and applies G
 // along the row, waves 0-2 then take column j of the result through LDS, and the workgroup's
 // 64 x 9 outputs leave as one contiguous run. The one-thread-per-pair kernel issued 36 q
@@ -735,83 +513,6 @@ __global__ __launch_bounds__(384) void wino_wout_xf_kernel(const float* __restri
   }
 }
 
-// PSX_WINO_XF=0: the whole-tile-per-thread transforms (A/B)
-static bool wino_xf_on() {
-  static const bool on = [] {
-    const char* e = getenv("PSX_WINO_XF");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
-
-// dW[k][c][3][3] = scale * G^T M G, M[b] = sum of the q partial slabs part[b * q + j][k][c]
-// (the batched TN GEMM's split of each batch over tile ranges). One thread per (k, c), c fastest;
-// OutT = uint16_t: the fp16 wire (reference codec), float: fp32 gradients. OIHW like
-// wgrad_reduce's output.
-
-template <typename OutT, int Q>
-__global__ __launch_bounds__(256) void wino_wout_kernel(const float* __restrict__ part, OutT* __restrict__ out, int K,
-                                                        int C, int q, float scale) {
-  __shared__ float stage[256 * 9];
-  const long i0 = (long)blockIdx.x * 256, n = (long)K * C;
-  const long i = i0 + threadIdx.x;
-  const int qq = Q > 0 ? Q : q;
-  const size_t slab = (size_t)K * C;
-  float o9[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (i < n) {
-    float m[6][6];
-#pragma unroll
-    for (int b = 0; b < 36; ++b) {
-      const float* p = part + (size_t)b * qq * slab + i;
-      float v = p[0];
-      if constexpr (Q > 0) {
-#pragma unroll
-        for (int j = 1; j < Q; ++j) v += p[j * slab];
-      } else {
-        for (int j = 1; j < qq; ++j) v += p[j * slab];
-      }
-      m[b / 6][b % 6] = v;
-    }
-    float e[3][6];  // e = G^T m (columns)
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      float col[6] = {m[0][s], m[1][s], m[2][s], m[3][s], m[4][s], m[5][s]}, o[3];
-      wino_gt6(col, o);
-#pragma unroll
-      for (int r = 0; r < 3; ++r) e[r][s] = o[r];
-    }
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      float o[3];
-      wino_gt6(e[r], o);
-#pragma unroll
-      for (int s = 0; s < 3; ++s) o9[r * 3 + s] = o[s] * scale;
-    }
-  }
-  // the workgroup's 256 (k, c) pairs own one contiguous run of 256 * 9 outputs (i = k * C + c):
-  // staged in LDS, stored by consecutive threads (the direct 9-strided stores split every wave
-  // store into 18-byte pieces)
-#pragma unroll
-  for (int j = 0; j < 9; ++j) stage[threadIdx.x * 9 + j] = o9[j];
-  __syncthreads();
-  const long lim = (n - i0 < 256 ? n - i0 : 256) * 9;
-  OutT* dst = out + i0 * 9;
-  for (int j = threadIdx.x; j < lim; j += 256) {
-    const float v = stage[j];
-    if constexpr (sizeof(OutT) == 2)
-      dst[j] = __builtin_bit_cast(uint16_t, (_Float16)v);
-    else
-      dst[j] = v;
-  }
-}
-
-// grid.y of the transform kernels: 4 tiles per workgroup, one per wave (a 256-row cap starved
-// the 4x4 / 8x8 layers: 256 workgroups of 1-2 tiles per thread, ~2x their byte time)
-int wino_tile_grid(int T) {
-  int gy = (T + 3) / 4;
-  return gy > 16384 ? 16384 : gy;
-}
-
 }  // namespace psx
 
 using namespace psx;
@@ -820,16 +521,20 @@ extern "C" {
 
 // Floats of one Winograd conv's transformed operands: V = T*36*C (input tiles, kept per layer for
 // the weight gradient) and P = 36*T*K (GEMM output / dy tiles).
-long psx_wino_v_floats(int N, int H, int W, int C) { return (long)N * (H / 4) * (W / 4) * 36 * C; }
+// T = N * ceil(H / 4) * ceil(W / 4) output tiles (partial edge tiles: ResNet-50's 14x14 / 7x7)
+static long wino_tiles(int N, int H, int W) { return (long)N * ((H + 3) / 4) * ((W + 3) / 4); }
+
+long psx_wino_v_floats(int N, int H, int W, int C) { return wino_tiles(N, H, W) * 36 * C; }
 
 long psx_wino_workspace(int N, int H, int W, int C, int K) {
   return psx_wino_v_floats(N, H, W, C) + psx_wino_v_floats(N, H, W, K);
 }
 
-// 1 when psx_wino_conv handles this layer: 3x3 / stride 1 / pad 1, H, W multiples of 4,
+// 1 when psx_wino_conv handles this layer: 3x3 / stride 1 / pad 1, H, W >= 4 (not a multiple of
+// 4: the edge tiles are partial — zero padded in, clipped out: 14x14 -> 16 tiles of 16 pixels),
 // channels powers of two >= 64 (transform blocks, the GEMM's per-batch channel decode).
 int psx_wino_ok(int H, int W, int C, int K) {
-  return H % 4 == 0 && W % 4 == 0 && C >= 64 && K >= 64 && !(C & (C - 1)) && !(K & (K - 1));
+  return H >= 4 && W >= 4 && C >= 64 && K >= 64 && !(C & (C - 1)) && !(K & (K - 1));
 }
 
 // fwd (flip = 0): U[K][36][C] from w [K][C][3][3]; dgrad (flip = 1): U[C][36][K] of rot180(w)^T.
@@ -872,70 +577,25 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
                   const float* bnpart, const WinoBnFin* bnfin, const float* sshift, hipStream_t st) {
   if (bnpart && (!bnfin || bnfin->C != C)) return -3;
   if (!psx_wino_ok(H, W, C, K)) return -2;
-  const int T = N * (H / 4) * (W / 4);
-  const int gy = wino_tile_grid(T);
+  const int T = (int)wino_tiles(N, H, W);
   WinoBnFin bf{};
   if (bnpart) bf = *bnfin;
-  if (wino_xf_on())
-    hipLaunchKernelGGL(wino_in_xf_kernel, dim3(C / 64, wino_xf_grid(T, C / 64)), dim3(64 * kXfWaves), 0, st, x, V, T,
-                       H, W, C, bnpart, bf);
-  else
-    hipLaunchKernelGGL(wino_in_kernel, dim3(C / 64, gy), dim3(256), 0, st, x, V, T, H, W, C, bnpart, bf);
-  // fused GEMM + output transform (conv_v2.hip WOUT: P stays in registers, so the 36 x T x K
-  // product never round-trips HBM). PSX_WINO_FUSED = 0 off, 1 where its 64 x 32 workgroup tiles
-  // (32 x 16 wave tiles) give >= PSX_WINO_FUSED_MINWG (default 256) workgroups, 2 always (tests).
-  // (read per call: the tests switch it inside one process; graph capture runs this once)
-  const char* fe = getenv("PSX_WINO_FUSED");
-  const int fused_mode = fe ? atoi(fe) : 0;
-  const char* fm = getenv("PSX_WINO_FUSED_MINWG");
-  const long fused_minwg = fm && atol(fm) > 0 ? atol(fm) : 256L;
-  if (fused_mode && K % 32 == 0) {
-    const int bm = K % 64 == 0 ? 64 : 32;
-    if (fused_mode == 2 || (bm == 64 && (long)(K / 64) * ((T + 31) / 32) >= fused_minwg)) {
-      const WinoBwdStats* b = bst;
-      struct {
-        float* part;
-        const void* o;
-        const void* y1;
-        const void* y2;
-        const float* saved1;
-        const float* saved2;
-        int mask_store;
-      } d{};  // conv_v2.hip BwdStatsDesc
-      if (b) d = {b->part, b->o, b->y1, b->y2, b->saved1, b->saved2, b->mask_store};
-      return psx_wino_gemm_out(V, U, y, res, stats, b ? &d : nullptr, b ? b->mask_aff : nullptr, zero, N, H, W, C, K,
-                               sshift, bm, st);
-    }
-  }
-  // the 36 GEMMs: the conv_v2 mainloop; PSX_WINO_SK=1 takes the stream-K kernel (wino_gemm.hip)
-  // for C >= 256 (2 = every layer). Opt-in: same box, 8x8x256 36 x (512 x 256 x 256) 40.6 vs
-  // 33.7 us (split-tile hand-off ~6 us, scattered C stores ~5 us, one wave per SIMD leaves the
-  // barriers and first LDS reads of every unit exposed: profiles/README.md round 4).
-  static const int sk_mode = [] {
-    const char* e = getenv("PSX_WINO_SK");
-    return e ? atoi(e) : 0;
-  }();
-  int e = -5;
-  if (sk_mode && (C >= 256 || sk_mode == 2))
-    e = psx_sk_gemm_nt(V, U, P, C, (long)T * C, 36L * C, C, K, (long)T * K, T, K, C, 36, zero, 0, st);
-  if (e) e = psx_bgemm_f32(V, U, P, zero, T, K, C, 36, cfg, st);
+  hipLaunchKernelGGL(wino_in_xf_kernel, dim3(C / 64, wino_xf_grid(T, C / 64)), dim3(64 * kXfWaves), 0, st, x, V, T, H,
+                     W, C, bnpart, bf);
+  // the 36 GEMMs: the conv_v2 mainloop. (Measured slower and removed in round 5: a stream-K GEMM,
+  // 8x8x256 40.6 vs 33.7 us, profiles/r4_sk_gemm_probes.jsonl; the GEMM with the output transform
+  // in its epilogue, 64 output registers per accumulator forcing 16x16 wave tiles: neutral where
+  // it had >= 256 workgroups, 1.8x slower elsewhere, profiles/r4_numbers.jsonl r4_call16.)
+  int e = psx_bgemm_f32(V, U, P, zero, T, K, C, 36, cfg, st);
   if (e) return e;
   WinoBwdStats bs{};
   if (bst) bs = *bst;
-  const bool xf = wino_xf_on();
-  const int gyo = xf ? wino_xf_grid(T, K / 64) : gy;
+  const int gyo = wino_xf_grid(T, K / 64);
   DetRed det{};
   if (bst || stats) det = det_next(gyo, bst ? (bst->y2 ? 3 : 2) : 2, K, K / 64);
   using OutK = void (*)(const float*, float*, const float*, float*, int, int, int, int, WinoBwdStats, DetRed,
                        const float*);
   // [res][variant]: forward, backward (ReLU mask from o / from the affine) x (one / two BN sums)
-  static const OutK kOut[2][5] = {
-      {wino_out_kernel<false, false, false, false>, wino_out_kernel<false, true, false, false>,
-       wino_out_kernel<false, true, false, true>, wino_out_kernel<false, true, true, false>,
-       wino_out_kernel<false, true, true, true>},
-      {wino_out_kernel<true, false, false, false>, wino_out_kernel<true, true, false, false>,
-       wino_out_kernel<true, true, false, true>, wino_out_kernel<true, true, true, false>,
-       wino_out_kernel<true, true, true, true>}};
   static const OutK kOutXf[2][5] = {
       {wino_out_xf_kernel<false, false, false, false>, wino_out_xf_kernel<false, true, false, false>,
        wino_out_xf_kernel<false, true, false, true>, wino_out_xf_kernel<false, true, true, false>,
@@ -944,33 +604,33 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
        wino_out_xf_kernel<true, true, false, true>, wino_out_xf_kernel<true, true, true, false>,
        wino_out_xf_kernel<true, true, true, true>}};
   const int var = bst ? 1 + 2 * (bs.mask_aff != nullptr) + (bs.y2 != nullptr) : 0;
-  hipLaunchKernelGGL((xf ? kOutXf : kOut)[res != nullptr][var], dim3(K / 64, gyo), dim3(xf ? 64 * kXfWaves : 256), 0,
-                     st, P, y, res, bst ? nullptr : stats, T, H, W, K, bs, det, sshift);
+  hipLaunchKernelGGL(kOutXf[res != nullptr][var], dim3(K / 64, gyo), dim3(64 * kXfWaves), 0, st, P, y, res,
+                     bst ? nullptr : stats, T, H, W, K, bs, det, sshift);
   return (int)hipGetLastError();
 }
 
-// Weight-gradient GEMM tile (BR = BC): 64 (3 workgroups per CU) unless PSX_WINO_WBR=128.
+// Weight-gradient GEMM tile (BR = BC): 64 (3 workgroups per CU) unless PSX_TUNE wino_wbr=128.
 static int wino_wtile(int C, int K) {
-  if (const char* e = getenv("PSX_WINO_WBR"); e && atoi(e) == 128 && C % 128 == 0 && K % 128 == 0) return 128;
+  if (const char* e = tune("wino_wbr"); e && atoi(e) == 128 && C % 128 == 0 && K % 128 == 0) return 128;
   return 64;
 }
 
 // Tile-range splits q of the weight-gradient GEMM: 36 * q * (C/BR) * (K/BC) workgroups, each
 // over T / q tiles (a multiple of 32): the smallest q reaching 1024 workgroups while a split keeps
-// >= 256 tiles, at most 8 (PSX_WINO_WQ_MAX). Same-box sweep with the split output transform (B=128,
+// >= 256 tiles, at most 8 (PSX_TUNE wino_wq_max). Same-box sweep with the split output transform (B=128,
 // us incl. dy transform, q = 1 / 2 / 4 / 8 / 16): 32x32x64 244 / 134 / 79 / 69 / 83, 16x16x128
 // 72 / 62 / 51 / 48 / 69, 8x8x256 51 / 46 / 47 / 55 / 81, 4x4x512 47 / 54 / 75 (bench/wino_fused_ab.py).
 // 0 = not applicable.
 int psx_wino_wgrad_q(int N, int H, int W, int C, int K) {
-  const int T = N * (H / 4) * (W / 4);
+  const int T = (int)wino_tiles(N, H, W);
   if (!psx_wino_ok(H, W, C, K) || T % 32) return 0;
   const int bt = wino_wtile(C, K);
   int q = 1;
   static const int qmax = [] {
-    const char* e = getenv("PSX_WINO_WQ_MAX");
+    const char* e = tune("wino_wq_max");
     return e && atoi(e) > 0 ? atoi(e) : 8;
   }();
-  if (const char* e = getenv("PSX_WINO_WQ"); e && atoi(e) > 0) q = atoi(e);
+  if (const char* e = tune("wino_wq"); e && atoi(e) > 0) q = atoi(e);
   else
     while (36L * q * (C / bt) * (K / bt) < 1024 && q < qmax && T % (32 * 2 * q) == 0 && T / (2 * q) >= 256) q *= 2;
   return T % (32 * q) ? 0 : q;
@@ -988,14 +648,11 @@ int psx_wino_wgrad(const float* V, const float* dy, float* D, float* part, void*
   const int q = psx_wino_wgrad_q(N, H, W, C, K);
   if (q < 1) return -2;
   if (bpart && (!ybn || !bbfin || bbfin->C != K)) return -3;
-  const int T = N * (H / 4) * (W / 4);
+  const int T = (int)wino_tiles(N, H, W);
   BnBwdFin bb{};
   if (bpart) bb = *bbfin;
-  if (wino_xf_on() || bpart)
-    hipLaunchKernelGGL(wino_dy_xf_kernel, dim3(K / 64, wino_xf_grid(T, K / 64)), dim3(64 * kXfWaves), 0, st, dy, D, T,
-                       H, W, K, ybn, bpart, bb);
-  else
-    hipLaunchKernelGGL(wino_dy_kernel, dim3(K / 64, wino_tile_grid(T)), dim3(256), 0, st, dy, D, T, H, W, K);
+  hipLaunchKernelGGL(wino_dy_xf_kernel, dim3(K / 64, wino_xf_grid(T, K / 64)), dim3(64 * kXfWaves), 0, st, dy, D, T, H,
+                     W, K, ybn, bpart, bb);
   const int bt = wino_wtile(C, K);
   int e = psx_bgemm_tn_f32(V, D, part, zero, T, C, K, 36, q, bt, bt, st);
   if (e) return e;
@@ -1007,40 +664,23 @@ int psx_wino_wgrad(const float* V, const float* dy, float* D, float* part, void*
 // from the fused weight-gradient kernel, wino_wgrad.hip). out: OIHW, fp16 (out_fp16) or fp32.
 int psx_wino_wout(const float* part, void* out, int out_fp16, float scale, int K, int C, int q, hipStream_t st) {
   const long n = (long)K * C;
-  const dim3 grid((unsigned)((n + 255) / 256));
-  if (wino_xf_on()) {
-    const dim3 gx((unsigned)((n + 63) / 64));
+  const dim3 gx((unsigned)((n + 63) / 64));
 #define PSX_WOUT(OT, QV) \
   hipLaunchKernelGGL((wino_wout_xf_kernel<OT, QV>), gx, dim3(64 * kXfWaves), 0, st, part, (OT*)out, K, C, q, scale)
-#define PSX_WOUT_Q(OT)          \
-  if (q == 1) PSX_WOUT(OT, 1);  \
+#define PSX_WOUT_Q(OT)                \
+  if (q == 1) PSX_WOUT(OT, 1);        \
   else if (q == 2) PSX_WOUT(OT, 2);   \
   else if (q == 4) PSX_WOUT(OT, 4);   \
   else if (q == 8) PSX_WOUT(OT, 8);   \
   else if (q == 16) PSX_WOUT(OT, 16); \
   else if (q == 32) PSX_WOUT(OT, 32); \
   else PSX_WOUT(OT, 0)
-    if (out_fp16) {
-      PSX_WOUT_Q(uint16_t);
-    } else {
-      PSX_WOUT_Q(float);
-    }
-#undef PSX_WOUT_Q
-#undef PSX_WOUT
-    return (int)hipGetLastError();
-  }
-#define PSX_WOUT(OT, QV) hipLaunchKernelGGL((wino_wout_kernel<OT, QV>), grid, dim3(256), 0, st, part, (OT*)out, K, C, q, scale)
   if (out_fp16) {
-    if (q == 1) PSX_WOUT(uint16_t, 1);
-    else if (q == 2) PSX_WOUT(uint16_t, 2);
-    else if (q == 4) PSX_WOUT(uint16_t, 4);
-    else PSX_WOUT(uint16_t, 0);
+    PSX_WOUT_Q(uint16_t);
   } else {
-    if (q == 1) PSX_WOUT(float, 1);
-    else if (q == 2) PSX_WOUT(float, 2);
-    else if (q == 4) PSX_WOUT(float, 4);
-    else PSX_WOUT(float, 0);
+    PSX_WOUT_Q(float);
   }
+#undef PSX_WOUT_Q
 #undef PSX_WOUT
   return (int)hipGetLastError();
 }

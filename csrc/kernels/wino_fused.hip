@@ -487,14 +487,14 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
     red[2][kq][l] = s3;
   }
   __syncthreads();
-  // deterministic mode: slab row tb, each element written by exactly one lane of one workgroup
-  float* row = det.slab ? det.slab + (size_t)tb * nst * K : dst + (size_t)(tb & (PSX_STAT_SLOTS - 1)) * nst * K;
+  // deterministic mode: exact fixed-point accumulators (bnfin.hpp DetRed)
+  float* row = dst + (size_t)(tb & (PSX_STAT_SLOTS - 1)) * nst * K;
   if (h == 0 && l < 16) {
-    atomicAdd(row + k, s1 + red[0][kq][l]);
-    atomicAdd(row + K + k, s2 + red[1][kq][l]);
-    if constexpr (two) atomicAdd(row + 2 * K + k, s3 + red[2][kq][l]);
+    stat_add(det, row, k, s1 + red[0][kq][l]);
+    stat_add(det, row, K + k, s2 + red[1][kq][l]);
+    if constexpr (two) stat_add(det, row, 2 * K + k, s3 + red[2][kq][l]);
   }
-  if (det.slab) {
+  if (det.fix) {
     __syncthreads();  // vb is the hand-off scratch
     det_finish(det, nst, K, dst, tb, reinterpret_cast<unsigned char*>(&vb[0][0][0][0]));
   }

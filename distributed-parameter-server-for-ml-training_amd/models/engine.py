@@ -31,6 +31,7 @@ import numpy as np
 import torch
 
 from ..ops import kernels as K
+from ..utils.tune import tune, tune_flag, tune_int
 from .layout import ParamLayout
 from .resnet import Bottleneck, BasicBlock
 
@@ -187,60 +188,53 @@ class HipResNetEngine:
         self.graphs = None
         self.segments = None  # backward split points (set_segments), None = one segment
         # BN finalize inside the producing launch (csrc/kernels/bnfin.hpp); 0 = separate kernels
-        self.fuse_fin = os.environ.get("PSX_FUSE_BNFIN", "0") == "1"
+        self.fuse_fin = tune_flag("fuse_bnfin", False)
         # BN-backward sums from the dgrad epilogue (skips the separate bn_bwd_reduce pass where a
         # dgrad produces the BN's input gradient): neutral with 32 stat slots + separate finalize
         # (2.215 vs 2.217 ms/step), a small win with 8 slots + folded finalize (1.996/2.000 vs
-        # 2.010/2.006 ms/step, two same-box A/B pairs), so on by default (PSX_FUSE_BNBWD=0: off)
+        # 2.010/2.006 ms/step, two same-box A/B pairs), so on by default (PSX_TUNE fuse_bnbwd=0: off)
         # BN finalize folded into the consuming apply launches (bnfin.hpp bn_fin_lds): every apply
         # workgroup re-derives the affine/coefficients from the stat slots, removing 40 finalize
         # launches per step. With 32 slot rows it measured slower (2.18 vs 2.10 ms/step); with 8
-        # rows (csrc/kernels/common.hpp) it wins: 1.999 vs 2.019 ms/step. PSX_BNFIN_APPLY=0: off
-        self.fin_apply = not self.fuse_fin and os.environ.get("PSX_BNFIN_APPLY", "1") == "1"
-        self.fuse_bnbwd = os.environ.get("PSX_FUSE_BNBWD", "1") == "1"
+        # rows (csrc/kernels/common.hpp) it wins: 1.999 vs 2.019 ms/step. PSX_TUNE bnfin_apply=0: off
+        self.fin_apply = not self.fuse_fin and tune_flag("bnfin_apply", True)
+        self.fuse_bnbwd = tune_flag("fuse_bnbwd", True)
         self._prereduced = set()
         # with the fused sums the dgrad epilogue already reads the ReLU mask operand o: it stores
         # dz = g*[o > 0] instead of g (bwd_stats_desc mask_store), the BN-backward apply then runs
         # without o (one activation read less per BN layer) and dz doubles as the identity
-        # shortcut's gradient (no dzout copy). PSX_MASK_STORE=0: off
-        self.mask_store = self.fuse_bnbwd and os.environ.get("PSX_MASK_STORE", "1") == "1"
+        # shortcut's gradient (no dzout copy). PSX_TUNE mask_store=0: off
+        self.mask_store = self.fuse_bnbwd and tune_flag("mask_store", True)
         # BN-backward applies folded into the fused Winograd data gradient + dy transform (_bn_bwd_to)
-        self.bwd_fold = self.mask_store and os.environ.get("PSX_WINO_BWDFOLD", "1") == "1"
+        self.bwd_fold = self.mask_store and tune_flag("wino_bwdfold", True)
         self._bwd_fold = {}
         self._premasked = set()
         # weight gradients (+ their batched reductions) on a side stream, a parallel branch of the
-        # captured step graph next to the dgrad -> BN-backward chain. PSX_WGRAD_STREAM=1 / 0
+        # captured step graph next to the dgrad -> BN-backward chain. PSX_TUNE wgrad_stream=1 / 0
         # forces it; the default keeps it except for the fp32 engine on CIFAR-size images, whose
         # fused Winograd weight gradients (1 workgroup per CU, like the data gradients beside them)
         # only time-share the chip with the dgrad chain and add cross-queue waits: same box
         # 3.35-3.38 -> 3.28-3.29 ms/step without it (r4_call20/21); bf16 ResNet-18 (1.85 -> 1.89)
         # and fp32 ResNet-50 (40.4 -> 41.5) keep it.
-        ws = os.environ.get("PSX_WGRAD_STREAM", "auto")
+        ws = tune("wgrad_stream", "auto")
         if ws == "auto":
             ws = "0" if (self.f32 and max(self.spec.in_hw) <= 64) else "1"
         self.wg_stream = torch.cuda.Stream(device=self.dev) if ws == "1" else None
-        self.fold_sc = os.environ.get("PSX_DGRAD_FOLD_SC", "1") == "1"
-        # the forward twin (opt-in): the 1x1 / stride-2 shortcut conv as extra output-channel tiles
-        # of the 3x3 / stride-2 conv's launch (conv_v2.hip psx_conv_fwd2_sc). Measured slower in
-        # fp32 (+45 us/step: a shortcut tile's epilogue costs ~30 % of a 3x3 tile, so the folded
-        # grid packs worse than two launches) and neutral in bf16 (profiles/r4_numbers.jsonl r4_call31)
-        self.fold_fwd_sc = os.environ.get("PSX_FWD_FOLD_SC", "0") == "1"
+        self.fold_sc = tune_flag("dgrad_fold_sc", True)
         # the CIFAR stem on the direct vector-ALU kernel (csrc/kernels/stem.hip): fp32 27.4 -> 19.5 us
         # in isolation (bench/stem_probe.py); step A/B within noise, bf16 unmeasured in isolation, so
         # "auto" = fp32 only
-        sd = os.environ.get("PSX_STEM_DIRECT", "auto")
+        sd = tune("stem_direct", "auto")
         self.stem_direct = sd == "1" or (sd == "auto" and self.f32)
         # the later stages' Winograd weight transforms overlap the first stage's forward on the
-        # side stream; without one they stay on the compute stream (PSX_WINO_WSTREAM=1 gives them
-        # a stream of their own: measured 3.36 vs 3.28 ms/step, a forked branch at the step start
-        # costs more than the overlap returns, r4_numbers.jsonl r4_call23)
+        # side stream; without one they stay on the compute stream (a stream of their own measured
+        # 3.36 vs 3.28 ms/step — a forked branch at the step start costs more than the overlap
+        # returns, r4_numbers.jsonl r4_call23 — and was removed)
         self.wt_stream = self.wg_stream
-        if self.wt_stream is None and os.environ.get("PSX_WINO_WSTREAM", "0") == "1":
-            self.wt_stream = torch.cuda.Stream(device=self.dev)
         self._wg_batch = None
         self._fins = {}
         # conv-operand unpack: "tiles" (flat grid, fp32 arena or bf16 image source) or "tap"
-        self.unpack_impl = os.environ.get("PSX_UNPACK_IMPL", "tiles")
+        self.unpack_impl = tune("unpack_impl", "tiles")
         self.wsrc = None        # bf16 weight image to unpack from (set_weight_source), None = arena
         self.pre_unpack = None
         self._build()
@@ -391,15 +385,11 @@ class HipResNetEngine:
         self.red = self._f32(red_off[0])
         self.det_buf = None
         if self.deterministic:
-            # row slab: the most rows x stat rows x channels any producer uses (split-K epilogue
-            # rows >= 8 pixels each, conv tiles >= 64 pixels, <= 512 bn_bwd_reduce blocks, B head rows)
-            need = 0
-            for cs in all_convs(sp):
-                oh, ow = cs.out_hw
-                need = max(need, (B * oh * ow // 8 + 64) * 3 * cs.cout, (B * cs.h * cs.w // 8 + 64) * 3 * cs.cp)
-            need = max(need, 3 * 1024 * max(b.convs[-1].cout for b in sp.blocks), B * 2 * sp.fc_in)
-            # [64 x 256 launch counters | level-1 rows | level-2 group rows] (bnfin.hpp DetRed)
-            self.det_buf = torch.zeros(16384 + 2 * need, dtype=torch.float32, device=self.dev)
+            # exact fixed-point accumulators of the widest producer (NS <= 3 sums x C channels; the
+            # head's 2 x fc_in) in each of the 64 rotating launch regions (bnfin.hpp DetRed)
+            cmax = max([cs.cout for cs in all_convs(sp)] + [cs.cp for cs in all_convs(sp)] + [sp.fc_in])
+            nbytes = K.det_bytes(3 * cmax)
+            self.det_buf = torch.zeros((nbytes + 3) // 4, dtype=torch.float32, device=self.dev)
         self.wpart = self._f32(max(1, max_wg))
         self.wpart_w = self._f32(max(1, self._plan_wpart(max_wp)))
         self._plan_wino()
@@ -420,18 +410,18 @@ class HipResNetEngine:
 
     def _plan_wino(self):
         """fp32 Winograd F(4x4,3x3) (csrc/kernels/wino.hip) for the 3x3 / stride-1 layers: forward
-        and data gradient on images up to PSX_WINO_MAXHW (default 64: every 3x3 stride-1 layer of
+        and data gradient on images up to PSX_TUNE wino_maxhw (default 64: every 3x3 stride-1 layer of
         ResNet-18 CIFAR and ResNet-50's 56x56 / 28x28 ones; R50 fp32 top-k 3,060 -> 3,188 img/s),
-        weight gradient (PSX_WINO_WGRAD=1, default) up to PSX_WINO_WGRAD_MAXHW
+        weight gradient (PSX_TUNE wino_wgrad=1, default) up to PSX_TUNE wino_wgrad_maxhw
         (default 16: on 32x32 the direct tap-reuse kernel is faster, 101 vs 129 us). Same-box
         per-layer A/B in profiles/r2s4_wino_*.jsonl. Per layer: the transformed forward weights
         U [cout][36][cin] and data-gradient weights U' [cin][36][cout] (rebuilt by unpack() every
         step) and, where the weight gradient is Winograd, the transformed input V [36][T][cin] the
         forward leaves for it. In deterministic mode its BN sums take the fixed-order reduction
-        like every other producer (wino_out_kernel + bnfin.hpp DetRed). Not for bf16. PSX_WINO=0:
+        like every other producer (wino_out_kernel + bnfin.hpp DetRed). Not for bf16. PSX_TUNE wino=0:
         direct kernels everywhere. Layers with 64 / 128 input channels (ResNet-18's 32x32 and 16x16
         stages) run forward and data gradient as ONE fused launch each (wino_fused.hip: the
-        transforms inside the GEMM, V / P never in HBM; PSX_WINO_FUSE=0: the three-launch path;
+        transforms inside the GEMM, V / P never in HBM; PSX_TUNE wino_fuse=0: the three-launch path;
         bench/wino_fused_ab.py: 32x32x64 fwd / dgrad 80 / 95 -> 58 / 63 us, 16x16x128 59 / 62 -> 50 / 51).
         The fused forward still writes V where the Winograd weight gradient reads it."""
         self.wino_layers = {}
@@ -440,20 +430,20 @@ class HipResNetEngine:
         self.wino_bnfold = {}
         self.wino_fused = {}
         self._xfold = {}        # conv -> (pre-BN y, BN affine): its input is relu(BN(y)), never written
-        if not self.f32 or os.environ.get("PSX_WINO", "1") == "0":
+        if not self.f32 or not tune_flag("wino", True):
             return
-        fuse = os.environ.get("PSX_WINO_FUSE", "1") == "1"
-        # fused weight gradient (wino_wgrad.hip) on images of at least PSX_WINO_WGF_MINHW: same box,
+        fuse = tune_flag("wino_fuse", True)
+        # fused weight gradient (wino_wgrad.hip) on images of at least PSX_TUNE wino_wgf_minhw: same box,
         # B = 128, us incl. output transform, fused vs three-launch (bench/wino_wgrad_ab.py,
         # profiles/r4_wino_wgrad_ab.jsonl): 32x32x64 58.4 vs 71.2, 16x16x128 55.3 vs 46.9 (+ the
         # forward's V store the three-launch path needs, ~7), 8x8x256 53.7 vs 43.2, 4x4x512 61.7 vs
         # 44.1. In the step (side stream; the forward's V store is on the critical path) same box:
         # off 3.568, >= 32 3.412, >= 16 3.363-3.372 ms/step (profiles/r4_numbers.jsonl)
-        wgf = os.environ.get("PSX_WINO_WGF", "1") == "1"
-        wgf_minhw = int(os.environ.get("PSX_WINO_WGF_MINHW", "16"))
-        maxhw = int(os.environ.get("PSX_WINO_MAXHW", "64"))
-        wg = os.environ.get("PSX_WINO_WGRAD", "1") == "1"
-        wg_maxhw = int(os.environ.get("PSX_WINO_WGRAD_MAXHW", "32"))
+        wgf = tune_flag("wino_wgf", True)
+        wgf_minhw = tune_int("wino_wgf_minhw", 16)
+        maxhw = tune_int("wino_maxhw", 64)
+        wg = tune_flag("wino_wgrad", True)
+        wg_maxhw = tune_int("wino_wgrad_maxhw", 32)
         B = self.B
         s_main = s_d = s_part = 0
         for cs in all_convs(self.spec):
@@ -469,7 +459,7 @@ class HipResNetEngine:
             self.wino_fused[cs.name] = (ff, fd)
             uf = self._f32((40 if ff else 36) * cs.cout * cs.cp)
             ud = self._f32((40 if fd else 36) * cs.cout * cs.cp) if cs.need_dgrad else None
-            # fused weight gradient (wino_wgrad.hip, PSX_WINO_WGF=1): transforms x and dy itself, so
+            # fused weight gradient (wino_wgrad.hip, PSX_TUNE wino_wgf=1): transforms x and dy itself, so
             # the forward keeps no V and no D is formed
             qf = (K.wino_wgrad_fused_q(B, cs.h, cs.w, cs.cp, cs.cout)
                   if q > 0 and wgf and min(cs.h, cs.w) >= wgf_minhw else 0)
@@ -483,13 +473,13 @@ class HipResNetEngine:
                 else:
                     s_d = max(s_d, vk)
                     s_part = max(s_part, 36 * q * cs.cout * cs.cp)
-        # BN folded into the next conv's input transform (PSX_WINO_BNFOLD=1, default): a block's inner
+        # BN folded into the next conv's input transform (PSX_TUNE wino_bnfold=1, default): a block's inner
         # BN (+ ReLU) whose only consumer is a Winograd conv with a Winograd weight gradient (that
         # reads V, not the activation) is finalized and applied inside wino_in_kernel, so its
         # activation is never written; the data gradient's ReLU mask comes from the BN affine
         # (needs the masked dz store, so the BN-backward apply never reads the activation either)
         self.wino_bnfold = {}
-        if self._fold and self.mask_store and os.environ.get("PSX_WINO_BNFOLD", "1") == "1":
+        if self._fold and self.mask_store and tune_flag("wino_bnfold", True):
             for b in self.spec.blocks:
                 for i in range(len(b.convs) - 1):
                     nxt = b.convs[i + 1]
@@ -498,15 +488,13 @@ class HipResNetEngine:
         # main-stream scratch (forward V of layers without a Winograd weight gradient / GEMM output;
         # data-gradient input tiles + GEMM output) and the weight-gradient side stream's own (dy
         # tiles, GEMM partials)
-        if self.wino_layers and self.dev.type == "cuda" and os.environ.get("PSX_WINO_SK", "0") != "0":
-            K.sk_workspace(self.dev)  # the opt-in stream-K GEMM's fixup buffers, before any capture
         self.wino_s1 = self._f32(max(1, s_main))
         self.wino_s2 = self._f32(max(1, s_main))
         self.wino_wd = self._f32(max(1, s_d))
         self.wino_wpart = self._f32(max(1, s_part))
         # the first block's first conv's weight gradient runs on the compute stream, concurrently
         # with the side stream's (_bwd_stem): its own scratch
-        self.tail_split = (self.wg_stream is not None and os.environ.get("PSX_TAIL_SPLIT", "1") == "1"
+        self.tail_split = (self.wg_stream is not None and tune_flag("tail_split", True)
                            and bool(self.spec.blocks) and self.spec.blocks[0].convs[0].name in self.wino_wgrad)
         self.wino_wd2 = self._f32(max(1, s_d)) if self.tail_split else None
         self.wino_wpart2 = self._f32(max(1, s_part)) if self.tail_split else None
@@ -521,7 +509,7 @@ class HipResNetEngine:
         if getattr(self, "_wino_wb_key", None) != key:
             convs = [cs for cs in all_convs(self.spec) if cs.name in self.wino_layers]
             hw0 = max((cs.h for cs in convs), default=0)
-            split = self.wt_stream is not None and os.environ.get("PSX_WINO_WSPLIT", "1") == "1"
+            split = self.wt_stream is not None and tune_flag("wino_wsplit", True)
             early, late = [], []
             self._wino_late = set()
             for cs in convs:
@@ -630,33 +618,6 @@ class HipResNetEngine:
         elif fin is None and not self._fold:
             self._bn_train(bs, arena, self.nslots, npix)
 
-    def _conv_bn_fwd_sc(self, cs: ConvSpec, ds: ConvSpec, x, y, ys, bs: BNSpec, dbn: BNSpec, arena,
-                        train: bool) -> bool:
-        """_conv_bn_fwd of a downsampling block's 3x3 / stride-2 conv and its 1x1 / stride-2
-        shortcut in one launch; False (nothing launched): run them separately."""
-        if not self.fold_fwd_sc or (train and self.fuse_fin) or cs.name in self.wino_layers:
-            return False
-        if (cs.k, cs.stride, cs.pad, ds.k, ds.stride, ds.pad) != (3, 2, 1, 1, 2, 0):
-            return False
-        if ds.cout != cs.cout or ds.cp != cs.cp or (ds.h, ds.w) != (cs.h, cs.w):
-            return False
-        wf = self.wbuf[cs.wf_off:cs.wf_off + cs.cout * cs.kg]
-        wfs = self.wbuf[ds.wf_off:ds.wf_off + ds.cout * ds.kg]
-        stats = self._red(bs, "fwd") if train else None
-        stats2 = self._red(dbn, "fwd") if train else None
-        sh = self.bn[bs.name]["sshift"] if train else None
-        sh2 = self.bn[dbn.name]["sshift"] if train else None
-        if not K.conv_fwd2_sc(x, wf, y, stats, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.kg, wfs, ds.kg, ys, stats2,
-                              sshift=sh, sshift_sc=sh2):
-            return False
-        npix = self.B * cs.out_hw[0] * cs.out_hw[1]
-        for b in (bs, dbn):
-            if not train:
-                self._bn_eval(b, arena)
-            elif not self._fold:
-                self._bn_train(b, arena, self.nslots, npix)
-        return True
-
     @property
     def _fold(self) -> bool:
         return self.fin_apply and not self.fuse_fin
@@ -705,11 +666,11 @@ class HipResNetEngine:
             torch.cuda.current_stream(self.dev).wait_stream(self.wg_stream)
 
     def _plan_wpart(self, max_wp: int) -> int:
-        """Batched weight-gradient reduction (PSX_WGRAD_RBATCH, default on): the layers of one
+        """Batched weight-gradient reduction (PSX_TUNE wgrad_rbatch, default on): the layers of one
         residual block keep their split-K partials in disjoint slices of wpart_w until ONE
         wgrad_reduce_batch launch at the end of the block's backward reduces them all (8 launches
         instead of 19 for ResNet-18). Returns the fp32 size wpart_w needs."""
-        self.rbatch = os.environ.get("PSX_WGRAD_RBATCH", "1") == "1"
+        self.rbatch = tune_flag("wgrad_rbatch", True)
         if not self.rbatch:
             return max_wp
         need = max_wp
@@ -771,7 +732,7 @@ class HipResNetEngine:
 
     def _dgrad(self, cs: ConvSpec, dy, dx, res=None, bn_next=None, sc=None):
         """bn_next = (BNSpec, o, y, two|None): the BN whose backward consumes dx; with conv v2 its
-        reduction (sum dz, sum dz*xhat) is produced by the dgrad epilogue (PSX_FUSE_BNBWD).
+        reduction (sum dz, sum dz*xhat) is produced by the dgrad epilogue (PSX_TUNE fuse_bnbwd).
         sc = (shortcut ConvSpec, its output gradient): fold the block's 1x1 / stride-2 shortcut
         data gradient into this 3x3 / stride-2 launch; returns False (nothing launched) when the
         layer cannot fold."""
@@ -822,7 +783,7 @@ class HipResNetEngine:
     def _bn_bwd_to(self, cs: ConvSpec, bs: BNSpec, arena, g, o, y, dx, npix, dzout=None):
         """The backward of BN bs whose output gradient feeds only conv cs's data and weight
         gradients. Returns (dz, dy): dz as _bn_bwd returns it, dy the buffer cs's gradients read.
-        Folded (PSX_WINO_BWDFOLD=1, default: cs has the fused Winograd data gradient and a Winograd
+        Folded (PSX_TUNE wino_bwdfold=1, default: cs has the fused Winograd data gradient and a Winograd
         weight gradient, g is already the masked dz and its sums came from the producing dgrad's
         epilogue): no apply pass — dy = k1 dz + k2 y + k3 is formed inside both consumers'
         operand loads (wino_fused.hip, wino.hip dy transform), and the fused data gradient
@@ -897,7 +858,7 @@ class HipResNetEngine:
         """OIHW master weights -> bf16 implicit-GEMM operands. The source is the fp32 arena, or
         the bf16 weight image ``self.wsrc`` when the fetch delivers one (parallel/codec.py
         WeightWire: the server's apply wrote those bits; identical operands either way)."""
-        if self.unpack_impl == "tap" and not self.f32:  # the original per-tap kernel (A/B: PSX_UNPACK_IMPL=tap)
+        if self.unpack_impl == "tap" and not self.f32:  # the original per-tap kernel (A/B: PSX_TUNE unpack_impl=tap)
             K.param_unpack(arena, self.descs, self.ndesc, self.wbuf)
             return
         src = self.wsrc if self.wsrc is not None else arena
@@ -956,13 +917,8 @@ class HipResNetEngine:
             src = d["inp"]
             L = len(b.convs)
             bn_in = None
-            folded = False
             for i, cs in enumerate(b.convs):
-                if i == 0 and b.down and self._conv_bn_fwd_sc(cs, b.down[0], src, d["y"][0], d["ys"], b.bns[0],
-                                                              b.down[1], arena, train):
-                    folded = True
-                else:
-                    self._conv_bn_fwd(cs, src, d["y"][i], b.bns[i], arena, train, bn_in=bn_in)
+                self._conv_bn_fwd(cs, src, d["y"][i], b.bns[i], arena, train, bn_in=bn_in)
                 bn_in = None
                 if i < L - 1:
                     bs = b.bns[i]
@@ -975,8 +931,7 @@ class HipResNetEngine:
                     src = d["a"][i]
             if b.down:
                 ds, dbn = b.down
-                if not folded:
-                    self._conv_bn_fwd(ds, d["inp"], d["ys"], dbn, arena, train)
+                self._conv_bn_fwd(ds, d["inp"], d["ys"], dbn, arena, train)
                 self._apply(b.bns[-1], d["y"][-1], d["out"], arena, train, res=d["ys"], bs2=dbn)
             else:
                 self._apply(b.bns[-1], d["y"][-1], d["out"], arena, train, res=d["inp"])
@@ -1069,7 +1024,7 @@ class HipResNetEngine:
                 ds, dbn = b.down
                 self._wgrad(ds, d["inp"], d["dys"])
                 # the 1x1 / stride-2 shortcut's data gradient folded into the 3x3 / stride-2 one
-                # (PSX_DGRAD_FOLD_SC=0: two launches + a residual pass)
+                # (PSX_TUNE dgrad_fold_sc=0: two launches + a residual pass)
                 if not (self.fold_sc and self._dgrad(cs, dys[0], d["gin"], bn_next=self._bn_into(j),
                                                      sc=(ds, d["dys"]))):
                     self._dgrad(ds, d["dys"], d["dxs"])

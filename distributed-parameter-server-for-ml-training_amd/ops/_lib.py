@@ -48,14 +48,10 @@ _KERNEL_SIGS = {
     "psx_conv_fwd2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp,
                             vp]),
     "psx_conv_dgrad2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp]),
-    "psx_conv_fwd2_sc": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, vp, vp, vp]),
     "psx_stem_conv": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
     "psx_conv_dgrad2_sc": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp,
                                  vp, i32, vp]),
     "psx_bgemm_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
-    "psx_sk_set_workspace": (i32, [vp, i64, vp, i32]),
-    "psx_sk_workspace_floats": (i64, []),
-    "psx_sk_gemm_nt": (i32, [vp, vp, vp, i64, i64, i64, i64, i64, i64, i32, i32, i32, i32, vp, i32, vp]),
     "psx_wino_workspace": (i64, [i32, i32, i32, i32, i32]),
     "psx_wino_ok": (i32, [i32, i32, i32, i32]),
     "psx_wino_weights": (i32, [vp, vp, i32, i32, i32, vp]),
@@ -83,6 +79,7 @@ _KERNEL_SIGS = {
     "psx_sgd_apply": (i32, [vp, vp, vp, i64, f32, f32, f32, f32, i32, i32, vp, vp]),
     "psx_grad_aggregate": (i32, [vp, i32, i32, vp, i32, i64, f32, i32, vp]),
     "psx_set_deterministic": (i32, [vp, i64]),
+    "psx_det_bytes": (i64, [i32]),
     "psx_sgd_apply_multi": (i32, [vp, vp, i32, vp, i64, f32, f32, f32, f32, i32, i32, vp, vp]),
     "psx_fp16_pack": (i32, [vp, vp, i64, f32, vp]),
     "psx_fp16_unpack": (i32, [vp, vp, i64, f32, vp]),

@@ -11,10 +11,10 @@ the tensors: every activation kernel is instantiated for both (csrc/kernels/comm
 from __future__ import annotations
 
 import ctypes as C
-import os
 
 import torch
 
+from ..utils.tune import tune, tune_int
 from ._lib import check, kernels, ptr, stream_ptr
 
 def conv_out_hw(h: int, w: int, k: int, stride: int, pad: int):
@@ -30,10 +30,17 @@ _ZERO_PAGES = {}
 _DET_BUF = None  # keeps the deterministic-mode scratch alive while the library points at it
 
 
+def det_bytes(max_sums: int) -> int:
+    """Bytes of the deterministic-mode buffer for producers of at most ``max_sums`` per-channel
+    sums per launch (NS x C: 3 x the widest BN layer)."""
+    return int(kernels().psx_det_bytes(int(max_sums)))
+
+
 def set_deterministic(buf):
-    """Deterministic BN reductions (csrc/kernels/bnfin.hpp DetRed) through ``buf`` (a zeroed
-    device tensor of >= 4 KiB: 64 launch counters + the row slab), or off with None. Host state
-    of the kernel library: set it before capturing a HIP graph."""
+    """Deterministic BN reductions (csrc/kernels/bnfin.hpp DetRed: exact fixed-point accumulators,
+    order-independent) through ``buf`` (a zeroed device tensor of det_bytes(max_sums) bytes: 64
+    launch counters + 64 accumulator regions), or off with None. Host state of the kernel
+    library: set it before capturing a HIP graph."""
     global _DET_BUF
     if buf is None:
         check(kernels().psx_set_deterministic(None, 0), "set_deterministic")
@@ -108,21 +115,6 @@ def conv_fwd2(x, wf, y, stats, ws, nb, h, w, ic, oc, k, stride, pad, kg, fin: Bn
                                   is_f32(x), ptr(sshift), stream_ptr()), "conv_fwd2")
 
 
-def conv_fwd2_sc(x, wf, y, stats, nb, h, w, ic, oc, kg, wf_sc, kg_sc, y_sc, stats_sc, sshift=None,
-                 sshift_sc=None) -> bool:
-    """A 3x3 / stride-2 / pad-1 conv and its block's 1x1 / stride-2 shortcut (same x, same output
-    channels) in one launch: y = conv(x, wf) with stats, y_sc = conv_sc(x, wf_sc) with stats_sc
-    (csrc/kernels/conv_v2.hip psx_conv_fwd2_sc). False: this layer cannot fold (run the two
-    launches instead)."""
-    rc = kernels().psx_conv_fwd2_sc(ptr(x), ptr(wf), ptr(y), ptr(stats), ptr(zero_page(x.device)), nb, h, w, ic, oc,
-                                    kg, is_f32(x), ptr(sshift), ptr(wf_sc), kg_sc, ptr(y_sc), ptr(stats_sc),
-                                    ptr(sshift_sc), stream_ptr())
-    if rc == -11:
-        return False
-    check(rc, "conv_fwd2_sc")
-    return True
-
-
 def stem_conv(x, wf, y, stats, nb, h, w, cin, cp, oc, kg, sshift=None) -> bool:
     """The CIFAR stem (3 -> 64, 3x3 / stride 1 / pad 1) as a direct vector-ALU conv with its BN
     statistics (csrc/kernels/stem.hip), same operands as conv_fwd2. False: not this shape or
@@ -183,36 +175,6 @@ def bgemm_f32(a, b, p, m, n, kd, nb, cfg=0):
           "bgemm_f32")
 
 
-_SK_WS = {}
-
-
-def sk_workspace(device=None):
-    """Register the stream-K GEMM's fixup workspace (csrc/kernels/wino_gemm.hip: partial tiles of
-    split tiles + zeroed arrival counters) for this process; call before any graph capture. The
-    library keeps one (process-global) registration: the stream-K launches of a process run on
-    one stream at a time (the engine's compute stream)."""
-    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-    if dev not in _SK_WS:
-        n = int(kernels().psx_sk_workspace_floats())
-        ws = torch.empty(n, dtype=torch.float32, device=dev)
-        cnt = torch.zeros(256, dtype=torch.int32, device=dev)
-        _SK_WS[dev] = (ws, cnt)
-        check(kernels().psx_sk_set_workspace(ptr(ws), n, ptr(cnt), 256), "sk_set_workspace")
-    return _SK_WS[dev]
-
-
-def sk_gemm_nt(a, b, c, m, n, kd, nb, a_strides, b_strides, c_strides, bn=0):
-    """nb batched fp32 GEMMs c[i] = a[i] @ b[i].T on the stream-K kernel (wino_gemm.hip); strides
-    (row, batch) in elements: a[i][r][k] = a[i * a_strides[1] + r * a_strides[0] + k], same for b
-    ([i][n][k]) and c ([i][m][n]). kd a multiple of 32, n of 64. Returns the launch status (-5: no
-    workspace registered)."""
-    assert a.dtype == b.dtype == c.dtype == torch.float32
-    sk_workspace(a.device)
-    return int(kernels().psx_sk_gemm_nt(ptr(a), ptr(b), ptr(c), a_strides[0], a_strides[1], b_strides[0], b_strides[1],
-                                        c_strides[0], c_strides[1], m, n, kd, nb, ptr(zero_page(a.device)), bn,
-                                        stream_ptr()))
-
-
 def bgemm_tn_f32(x, d, part, t, c, k, nb, q=1, br=64, bc=64):
     """Batched TN GEMMs part[i * q + j] = d[i, range j].T @ x[i, range j] (x [nb][t][c],
     d [nb][t][k], part [nb*q][k][c]) on the fp32 weight-gradient mainloop (wgrad_v2.hip)."""
@@ -240,7 +202,7 @@ def wino_wgrad_q(nb, h, w, c, k) -> int:
     return int(kernels().psx_wino_wgrad_q(nb, h, w, c, k))
 
 
-WINO_CFG = int(os.environ.get("PSX_WINO_CFG", "0"))
+WINO_CFG = tune_int("wino_cfg", 0)
 
 
 def wino_weights(w_oihw, u, k, c, flip=False):
@@ -398,7 +360,7 @@ WRBATCH_MAX = 4
 
 def wgrad_reduce_batchable(ic, k) -> bool:
     """The v2 reduce handles the layer (what wgrad_reduce_batch requires)."""
-    return k * k <= 49 and ic % 16 == 0 and not os.environ.get("PSX_WGRAD_REDUCE_V1")
+    return k * k <= 49 and ic % 16 == 0 and tune("wgrad_reduce_v1") is None
 
 
 def wgrad_reduce_batch(items, scale, out_fp16: bool):

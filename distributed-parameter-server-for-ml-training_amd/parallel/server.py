@@ -276,8 +276,16 @@ class ParameterServer:
                     self._commit_buffers()
                 return True  # the reference always answers received=True in sync mode
             if res.apply and self._round_count == 0:
-                # single-contribution round (W == 1): apply straight from the wire buffer
-                self.apply(grads, res.weight)
+                # single-contribution round (W == 1): apply straight from the wire buffer — a dense
+                # wire through the collective rounds' kernel (apply_sources with one source), so a
+                # loopback round and a one-worker RCCL round (a shrunk sync job) give the same bits
+                if grads.dtype == torch.int32:
+                    self.apply(grads, res.weight)
+                else:
+                    trace.mark("psx.apply")
+                    t0 = self._time_begin()
+                    self.apply_range_sources([grads], res.weight, 0, self.n)
+                    self.finish_round_apply(self._time_end(t0))
                 self._commit_buffers()
                 return True
             if res.decision in (WAIT, APPLY):

@@ -96,9 +96,7 @@ def test_conv2_every_tile_config(shape, tile, monkeypatch):
     n, cin, cout, hw, k, s, p = shape
     if cout % bm or cin % bm:
         pytest.skip("tile wider than the channel count")
-    for key, v in (("PSX_CV_BM", bm), ("PSX_CV_BN", bn), ("PSX_CV_WGM", wgm), ("PSX_CV_SPLITS", 1),
-                   ("PSX_CV_TAPR", 0)):
-        monkeypatch.setenv(key, str(v))
+    monkeypatch.setenv("PSX_TUNE", f"cv_bm={bm},cv_bn={bn},cv_wgm={wgm},cv_splits=1,cv_tapr=0")
     torch.manual_seed(3)
     x = torch.randn(n, cin, hw, hw, device=DEV).to(torch.bfloat16).float()
     w = (torch.randn(cout, cin, k, k, device=DEV) / (cin * k * k) ** 0.5).to(torch.bfloat16).float()
@@ -130,11 +128,11 @@ def test_conv2_tap_reuse(shape, bn, monkeypatch):
     too): fwd (+ BN statistics) and dgrad (+ residual, + fused BN-backward sums) against torch fp32."""
     n, cin, cout, hw, k, s, p = shape
     if bn == "halo":
-        monkeypatch.setenv("PSX_CV_TAPR_HALO", "1")
+        monkeypatch.setenv("PSX_TUNE", "cv_tapr_halo=1")
     elif (n * hw * hw) % bn or bn % hw:
         pytest.skip("tile does not hold whole image rows")
     else:
-        monkeypatch.setenv("PSX_CV_TAPR_BN", str(bn))
+        monkeypatch.setenv("PSX_TUNE", f"cv_tapr_bn={bn}")
     torch.manual_seed(4)
     x = torch.randn(n, cin, hw, hw, device=DEV).to(torch.bfloat16).float()
     w = (torch.randn(cout, cin, k, k, device=DEV) / (cin * k * k) ** 0.5).to(torch.bfloat16).float()
@@ -182,32 +180,6 @@ def test_conv_dgrad2_shortcut_fold(shape):
     dx = torch.empty(n, hw, hw, cp, dtype=torch.bfloat16, device=DEV)
     assert K.conv_dgrad2_sc(to_nhwc(dy, cout), wd, dx, None, n, hw, hw, cp, cout, kgd, to_nhwc(dy2, cout), wd2, kgd2)
     assert _rel(dx[..., :cin], ref) < 1e-2, shape
-
-
-@pytest.mark.parametrize("shape", [(128, 64, 128, 32), (128, 128, 256, 16), (8, 128, 256, 28)])
-def test_conv_fwd2_shortcut_fold(shape):
-    """bf16: 3x3/s2 conv + the folded 1x1/s2 shortcut conv in one launch (psx_conv_fwd2_sc), both
-    outputs and BN statistics against torch fp32."""
-    K.set_deterministic(None)  # an earlier engine test may have left the process in deterministic mode
-    torch.manual_seed(9)
-    n, cin, cout, hw = shape
-    x = torch.randn(n, cin, hw, hw, device=DEV).to(torch.bfloat16).float()
-    w = (torch.randn(cout, cin, 3, 3, device=DEV) / (cin * 9) ** 0.5).to(torch.bfloat16).float()
-    w2 = (torch.randn(cout, cin, 1, 1, device=DEV) / cin ** 0.5).to(torch.bfloat16).float()
-    wf, _, cp, kg, _ = make_operands(w)
-    wf2, _, _, kg2, _ = make_operands(w2)
-    oh = (hw - 1) // 2 + 1
-    y = torch.empty(n, oh, oh, cout, dtype=torch.bfloat16, device=DEV)
-    ys = torch.empty(n, oh, oh, cout, dtype=torch.bfloat16, device=DEV)
-    st, st2 = torch.zeros(K.STAT_SLOTS, 2, cout, device=DEV), torch.zeros(K.STAT_SLOTS, 2, cout, device=DEV)
-    if not K.conv_fwd2_sc(to_nhwc(x, cp), wf, y, st, n, hw, hw, cp, cout, kg, wf2, kg2, ys, st2):
-        pytest.skip("the planner splits K on this layer: not folded")
-    assert _rel(y, F.conv2d(x, w, stride=2, padding=1).permute(0, 2, 3, 1)) < 1e-2, shape
-    assert _rel(ys, F.conv2d(x, w2, stride=2).permute(0, 2, 3, 1)) < 1e-2, shape
-    for out, s in ((y, st), (ys, st2)):
-        q = out.float().reshape(-1, cout)
-        assert torch.allclose(s[:, 0].sum(0), q.sum(0), rtol=1e-3, atol=5e-2), shape
-        assert torch.allclose(s[:, 1].sum(0), (q * q).sum(0), rtol=1e-3, atol=5e-2), shape
 
 
 def test_stem_conv_direct():

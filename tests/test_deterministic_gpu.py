@@ -56,9 +56,9 @@ def test_side_stream_and_segments_bit_identical(monkeypatch):
     eager and graph, and a segmented backward (per-bucket graphs) equals the single graph."""
     from psx.parallel.overlap import plan_buckets
 
-    monkeypatch.setenv("PSX_WGRAD_STREAM", "0")
+    monkeypatch.setenv("PSX_TUNE", "wgrad_stream=0")
     _, lay, arena, main, imgs, labs = _setup(torch.float32)
-    monkeypatch.setenv("PSX_WGRAD_STREAM", "1")
+    monkeypatch.setenv("PSX_TUNE", "wgrad_stream=1")
     _, _, _, side, _, _ = _setup(torch.float32)
     assert main.wg_stream is None and side.wg_stream is not None
     grads = []

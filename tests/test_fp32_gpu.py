@@ -128,9 +128,7 @@ def test_conv_wgrad_f32(shape):
 def test_conv_f32_every_tile(shape, tile, monkeypatch):
     bm, bn, wgm = tile
     n, cin, cout, hw, k, s, p = shape
-    for key, v in (("PSX_CV_BM", bm), ("PSX_CV_BN", bn), ("PSX_CV_WGM", wgm), ("PSX_CV_SPLITS", 1),
-                   ("PSX_CV_TAPR", 0)):
-        monkeypatch.setenv(key, str(v))
+    monkeypatch.setenv("PSX_TUNE", f"cv_bm={bm},cv_bn={bn},cv_wgm={wgm},cv_splits=1,cv_tapr=0")
     torch.manual_seed(3)
     x = torch.randn(n, cin, hw, hw, device=DEV)
     w = torch.randn(cout, cin, k, k, device=DEV) / (cin * k * k) ** 0.5
@@ -150,9 +148,9 @@ def test_conv_f32_every_tile(shape, tile, monkeypatch):
 def test_conv_f32_tap_reuse_bn_bwd_sums(bn, monkeypatch):
     """Tap-reuse mainloop in fp32 + the dgrad epilogue's fused BN-backward sums."""
     if bn == "halo":
-        monkeypatch.setenv("PSX_CV_TAPR_HALO", "1")
+        monkeypatch.setenv("PSX_TUNE", "cv_tapr_halo=1")
     else:
-        monkeypatch.setenv("PSX_CV_TAPR_BN", str(bn))
+        monkeypatch.setenv("PSX_TUNE", f"cv_tapr_bn={bn}")
     n, c, hw = 8, 64, 32
     torch.manual_seed(4)
     w = torch.randn(c, c, 3, 3, device=DEV) / (c * 9) ** 0.5
@@ -276,7 +274,7 @@ def test_engine_step_f32_matches_torch_fp64(wino, monkeypatch):
     """One fp32 ResNet-18 training step on the HIP engine vs torch float64 autograd of the
     reference model: loss, every parameter gradient and the running statistics. Both conv paths:
     Winograd F(4x4,3x3) on the 3x3 stride-1 layers (the default) and the direct kernels."""
-    monkeypatch.setenv("PSX_WINO", wino)
+    monkeypatch.setenv("PSX_TUNE", f"wino={wino}")
     from psx.models.engine import HipResNetEngine
     from psx.models.layout import ParamLayout
     from psx.models.resnet import ResNet18
@@ -336,6 +334,59 @@ def test_engine_step_f32_matches_torch_fp64(wino, monkeypatch):
     for name in ("bn1.running_mean", "layer2.0.bn1.running_var", "layer4.1.bn2.running_mean"):
         assert torch.allclose(layout.view(arena, name).double(), sd[name], rtol=1e-5, atol=1e-6), name
     print(f"fp32 engine vs fp64 autograd: worst per-tensor relative gradient error {max(r[1] for r in rows):.2e}")
+
+
+# Per-tensor bars: every tensor's error <= max(PT_K * torch-fp32's error on
+# that tensor, PT_FLOOR). Random-init BN amplification makes which tensor carries the error a
+# matter of chance (the job-level test above), so this test damps it as torchvision's
+# zero_init_residual does (each block's last BN gamma 0.2): the residual branches stop compounding
+# ReLU-mask flips, and a regression in one kernel shows up in the tensors it feeds.
+PT_K, PT_FLOOR = 3.0, 2e-3
+
+
+@pytest.mark.parametrize("wino", ["1", "0"])
+def test_engine_step_f32_per_tensor_damped(wino, monkeypatch):
+    monkeypatch.setenv("PSX_TUNE", f"wino={wino}")
+    from psx.models.engine import HipResNetEngine
+    from psx.models.layout import ParamLayout
+    from psx.models.resnet import ResNet18
+
+    torch.manual_seed(5)
+    B = 32
+    model = ResNet18(100)
+    with torch.no_grad():
+        for name, m in model.named_modules():
+            if name.endswith("bn2") or name.endswith("shortcut.1"):
+                m.weight.fill_(0.2)
+    layout = ParamLayout.from_module(model)
+    arena, _ = layout.pack(model)
+    arena = arena.to(DEV)
+    eng = HipResNetEngine(model, layout, B, grad_dtype=torch.float32, dtype=torch.float32, deterministic=True)
+    x = torch.randn(B, 3, 32, 32, device=DEV)
+    y = torch.randint(0, 100, (B,), device=DEV)
+    eng.unpack(arena)
+    K.nchw_to_nhwc(x, eng.x0, B, 3, 32, 32, eng.x0.shape[-1])
+    eng.labels.copy_(y.to(torch.int32))
+    eng.forward(arena, train=True)
+    eng.head(arena, backward=True)
+    eng.backward(arena)
+    torch.cuda.synchronize()
+    ref = copy.deepcopy(model).to(DEV).double()
+    m32 = model.to(DEV)
+    m32.train()
+    F.cross_entropy(m32(x), y).backward()
+    ref.train()
+    F.cross_entropy(ref(x.double()), y).backward()
+    bad = []
+    for name, p in ref.named_parameters():
+        g = layout.grad_view(eng.grads, name).double()
+        nrm = p.grad.norm().clamp_min(1e-30)
+        err = ((g - p.grad).norm() / nrm).item()
+        err32 = ((m32.get_parameter(name).grad.double() - p.grad).norm() / nrm).item()
+        print(f"{name:32s} engine {err:.2e}  torch-fp32 {err32:.2e}")
+        if err > max(PT_K * err32, PT_FLOOR):
+            bad.append((name, err, err32))
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("f32", [True, False])
@@ -410,34 +461,6 @@ def test_conv_dgrad2_shortcut_fold_f32(shape, stats):
     _, wd1, _, _, kgd1 = operands_f32(w1)
     assert not K.conv_dgrad2_sc(nhwc(dy, cout), wd, dx, None, n, hw, hw, cp, cout, kgd, nhwc(dy2, cout), wd1,
                                 kgd1 + 1)
-
-
-@pytest.mark.parametrize("shape", [(16, 64, 128, 32), (128, 128, 256, 16), (4, 64, 128, 14)])
-def test_conv_fwd2_shortcut_fold_f32(shape):
-    """3x3/s2 conv + the block's 1x1/s2 shortcut conv in one launch (conv_v2.hip psx_conv_fwd2_sc):
-    both outputs and both shifted BN statistics against torch fp64."""
-    K.set_deterministic(None)  # an earlier engine test may have left the process in deterministic mode
-    torch.manual_seed(8)
-    n, cin, cout, hw = shape
-    x = torch.randn(n, cin, hw, hw, device=DEV)
-    w = torch.randn(cout, cin, 3, 3, device=DEV) / (cin * 9) ** 0.5
-    w2 = torch.randn(cout, cin, 1, 1, device=DEV) / cin ** 0.5
-    wf, _, cp, kg, _ = operands_f32(w)
-    wf2, _, _, kg2, _ = operands_f32(w2)
-    oh = (hw - 1) // 2 + 1
-    y = torch.full((n, oh, oh, cout), float("nan"), device=DEV)
-    ys = torch.full((n, oh, oh, cout), float("nan"), device=DEV)
-    st, st2 = torch.zeros(K.STAT_SLOTS, 2, cout, device=DEV), torch.zeros(K.STAT_SLOTS, 2, cout, device=DEV)
-    sh, sh2 = 0.1 * torch.randn(cout, device=DEV), 0.1 * torch.randn(cout, device=DEV)
-    if not K.conv_fwd2_sc(nhwc(x, cp), wf, y, st, n, hw, hw, cp, cout, kg, wf2, kg2, ys, st2, sshift=sh, sshift_sc=sh2):
-        pytest.skip("the planner splits K on this layer: not folded")
-    ref = F.conv2d(x.double(), w.double(), stride=2, padding=1).permute(0, 2, 3, 1)
-    ref2 = F.conv2d(x.double(), w2.double(), stride=2).permute(0, 2, 3, 1)
-    assert _rel(y, ref) < TOL and _rel(ys, ref2) < TOL, shape
-    for out, s, k in ((y, st, sh), (ys, st2, sh2)):
-        d = out.double().reshape(-1, cout) - k.double()
-        assert torch.allclose(s[:, 0].double().sum(0), d.sum(0), rtol=1e-4, atol=1e-2)
-        assert torch.allclose(s[:, 1].double().sum(0), (d * d).sum(0), rtol=1e-4, atol=1e-2)
 
 
 @pytest.mark.parametrize("n", [128, 3])

@@ -46,7 +46,7 @@ def test_engine_grads_batched_vs_per_layer(monkeypatch):
     ds = DeviceDataset.synthetic(256, 32, 100, seed=3, device="cuda")
     grads = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("PSX_WGRAD_RBATCH", flag)
+        monkeypatch.setenv("PSX_TUNE", f"wgrad_rbatch={flag}")
         eng = HipResNetEngine(model, lay, 64, in_hw=(32, 32))
         eng.index.copy_(torch.arange(64, dtype=torch.int32))
         a = arena.clone()

@@ -179,8 +179,8 @@ def test_wino_fused_bn_in_fold():
 
 
 def test_wino_fused_deterministic():
-    """Deterministic mode: fixed-order slab reduction of the BN sums — two runs bit-identical, and
-    equal to the atomic slots' sums to fp32 rounding."""
+    """Deterministic mode: exact fixed-point accumulation of the BN sums (bnfin.hpp DetRed) — two
+    runs bit-identical, and equal to the atomic slots' sums to fp32 rounding."""
     torch.manual_seed(9)
     nb, h, c, k = 16, 32, 64, 64
     x = torch.relu(torch.randn(nb, h, h, c, device=DEV))
@@ -275,7 +275,7 @@ def test_wino_fused_bwd_fold(nb, h, c, k):
 
 
 def test_engine_bwd_fold_matches_unfolded(monkeypatch):
-    """Whole fp32 step, deterministic, BN-backward applies folded (PSX_WINO_BWDFOLD=1, default)
+    """Whole fp32 step, deterministic, BN-backward applies folded (PSX_TUNE wino_bwdfold=1, default)
     vs the separate apply passes: loss bit-equal, gradients equal to the rounding of the folded
     apply (a different FMA order and slot-sum order), amplified by the BN backward of a random
     init network."""
@@ -293,7 +293,7 @@ def test_engine_bwd_fold_matches_unfolded(monkeypatch):
     labs = torch.randint(0, 100, (64,), dtype=torch.int32, device=DEV)
     out = {}
     for fold in ("1", "0"):
-        monkeypatch.setenv("PSX_WINO_BWDFOLD", fold)
+        monkeypatch.setenv("PSX_TUNE", f"wino_bwdfold={fold}")
         eng = HipResNetEngine(model, layout, B, dtype=torch.float32, deterministic=True)
         eng.index.copy_(torch.arange(B, dtype=torch.int32, device=DEV))
         a = arena0.clone()

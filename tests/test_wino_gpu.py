@@ -60,13 +60,14 @@ def _nhwc(t):
     return t.permute(0, 2, 3, 1).contiguous()
 
 
-@pytest.mark.parametrize("fused", ["0", "2"])
 @pytest.mark.parametrize("nb,h,c,k,res", [(4, 8, 64, 128, False), (3, 4, 128, 64, True), (8, 8, 256, 256, True),
-                                          (2, 16, 64, 64, False), (4, 4, 512, 512, False), (8, 32, 64, 64, True)])
-def test_wino_fwd(nb, h, c, k, res, fused, monkeypatch):
-    """fused = "2": the GEMM with the output transform in its epilogue (conv_v2 WOUT), "0": the
-    36 batched GEMMs + the output-transform kernel."""
-    monkeypatch.setenv("PSX_WINO_FUSED", fused)
+                                          (2, 16, 64, 64, False), (4, 4, 512, 512, False), (8, 32, 64, 64, True),
+                                          # partial edge tiles (ResNet-50's 14x14 / 7x7 stages, odd sizes)
+                                          (2, 14, 256, 256, True), (3, 7, 512, 512, False), (2, 5, 64, 128, True),
+                                          (2, 10, 128, 64, False)])
+def test_wino_fwd(nb, h, c, k, res):
+    """The input transform, the 36 batched GEMMs and the output transform (+ residual, + BN slot
+    sums of y) against float64."""
     torch.manual_seed(nb * h + c)
     x = torch.relu(torch.randn(nb, c, h, h, device=DEV, dtype=torch.float64))
     w = torch.randn(k, c, 3, 3, device=DEV, dtype=torch.float64) * (2.0 / (9 * c)) ** 0.5
@@ -87,10 +88,9 @@ def test_wino_fwd(nb, h, c, k, res, fused, monkeypatch):
     assert torch.allclose(s[1], (refn ** 2).sum((0, 1, 2)), rtol=1e-4)
 
 
-@pytest.mark.parametrize("fused", ["0", "2"])
-@pytest.mark.parametrize("nb,h,c,k", [(4, 8, 128, 256), (3, 4, 512, 512)])
-def test_wino_dgrad(nb, h, c, k, fused, monkeypatch):
-    monkeypatch.setenv("PSX_WINO_FUSED", fused)
+@pytest.mark.parametrize("nb,h,c,k", [(4, 8, 128, 256), (3, 4, 512, 512), (2, 14, 256, 256), (3, 7, 512, 512),
+                                      (2, 6, 64, 128)])
+def test_wino_dgrad(nb, h, c, k):
     """dx of y = conv3x3(x): the forward pipeline on dy with the flipped transform U'[c][36][k]."""
     torch.manual_seed(c + k)
     w = torch.randn(k, c, 3, 3, device=DEV, dtype=torch.float64) * (2.0 / (9 * c)) ** 0.5
@@ -107,7 +107,9 @@ def test_wino_dgrad(nb, h, c, k, fused, monkeypatch):
 
 
 @pytest.mark.parametrize("nb,h,c,k,fp16", [(32, 8, 128, 256, False), (32, 4, 512, 512, False), (32, 16, 128, 128, True),
-                                           (64, 4, 64, 64, False)])
+                                           (64, 4, 64, 64, False),
+                                           # partial edge tiles: dy beyond the image is zero in the dy transform
+                                           (4, 14, 256, 256, False), (16, 7, 512, 512, True), (8, 10, 64, 128, False)])
 def test_wino_wgrad(nb, h, c, k, fp16):
     """dW of y = conv3x3(x) from the forward's transformed input V and dy: F(3x3,4x4) by
     transposition, dg = G^T [sum_t (A dy_t A^T) . V_t] G, written as OIHW fp32 or the fp16 wire."""
@@ -133,7 +135,7 @@ def test_wino_wgrad(nb, h, c, k, fp16):
 
 
 def test_engine_step_wino_vs_direct(monkeypatch):
-    """One fp32 ResNet-18 step with the Winograd layers (default) and with PSX_WINO=0, both in
+    """One fp32 ResNet-18 step with the Winograd layers (default) and with PSX_TUNE wino=0, both in
     deterministic mode (fixed-order BN reductions, so the only difference left is the algorithm):
     the loss and every gradient agree to fp32 tolerance, and the Winograd engine really routed
     layers to it."""
@@ -151,7 +153,7 @@ def test_engine_step_wino_vs_direct(monkeypatch):
     labs = torch.randint(0, 100, (64,), dtype=torch.int32, device=DEV)
     out = {}
     for wino in ("1", "0"):
-        monkeypatch.setenv("PSX_WINO", wino)
+        monkeypatch.setenv("PSX_TUNE", f"wino={wino}")
         eng = HipResNetEngine(model, layout, B, dtype=torch.float32, deterministic=True)
         assert (len(eng.wino_layers) > 0) == (wino == "1")
         eng.index.copy_(torch.arange(B, dtype=torch.int32, device=DEV))
@@ -198,15 +200,15 @@ def test_wino_weights_multi_matches_single():
         assert torch.equal(u, r)
 
 
-@pytest.mark.parametrize("fused", ["0", "2"])
-@pytest.mark.parametrize("two,mask_store,res", [(False, False, False), (True, True, True), (False, True, False)])
-def test_wino_dgrad_fused_bn_bwd_sums(two, mask_store, res, fused, monkeypatch):
-    monkeypatch.setenv("PSX_WINO_FUSED", fused)
+@pytest.mark.parametrize("two,mask_store,res,h", [(False, False, False, 8), (True, True, True, 8), (False, True, False, 8),
+                                                  (True, True, True, 14), (False, True, False, 7)])
+def test_wino_dgrad_fused_bn_bwd_sums(two, mask_store, res, h):
     """Data gradient with the consumer BN's backward sums fused into the output transform (what
     the direct dgrad epilogue does): slot sums of dz = g*[o>0], dz*xhat1 (, dz*xhat2); the stored
-    output is dz with mask_store, else g."""
+    output is dz with mask_store, else g. h = 14 / 7: partial edge tiles (clipped pixels must add
+    nothing to the sums)."""
     torch.manual_seed(11)
-    nb, h, c, k = 32, 8, 128, 256
+    nb, c, k = 32, 128, 256
     w = torch.randn(k, c, 3, 3, device=DEV) * (2.0 / (9 * c)) ** 0.5
     dy = torch.randn(nb, h, h, k, device=DEV)
     r = torch.randn(nb, h, h, c, device=DEV) if res else None
@@ -236,7 +238,7 @@ def test_wino_dgrad_fused_bn_bwd_sums(two, mask_store, res, fused, monkeypatch):
 
 
 def test_engine_bn_fold_matches_unfolded(monkeypatch):
-    """Inner BN + ReLU folded into the next Winograd conv's input transform (PSX_WINO_BNFOLD=1,
+    """Inner BN + ReLU folded into the next Winograd conv's input transform (PSX_TUNE wino_bnfold=1,
     default: the activation is never written, the backward mask comes from the BN affine) vs the
     separate apply pass: loss, gradients and the running statistics the folded path publishes."""
     from psx.models.engine import HipResNetEngine
@@ -253,7 +255,7 @@ def test_engine_bn_fold_matches_unfolded(monkeypatch):
     labs = torch.randint(0, 100, (64,), dtype=torch.int32, device=DEV)
     out = {}
     for fold in ("1", "0"):
-        monkeypatch.setenv("PSX_WINO_BNFOLD", fold)
+        monkeypatch.setenv("PSX_TUNE", f"wino_bnfold={fold}")
         eng = HipResNetEngine(model, layout, B, dtype=torch.float32, deterministic=True)
         assert (len(eng.wino_bnfold) == 8) == (fold == "1"), eng.wino_bnfold
         eng.index.copy_(torch.arange(B, dtype=torch.int32, device=DEV))

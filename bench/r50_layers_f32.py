@@ -104,6 +104,9 @@ def main():
                 r["reduce_us"] = 0.0
                 del d
             del v1, v2
+        elif cin == 3 and k == 7 and K.stem_conv(xh, wf, y, stats, B, hw, hw, cin, cp, cout, kg, k=7):
+            r["path"] = "stem7"  # csrc/kernels/stem.hip (the weight gradient: conv_wgrad2 -> stem7_wgrad)
+            r["fwd_us"] = t_us(lambda: K.stem_conv(xh, wf, y, stats, B, hw, hw, cin, cp, cout, kg, k=7))
         else:
             r["path"] = "conv_v2"
             r["fwd_us"] = t_us(lambda: K.conv_fwd2(xh, wf, y, stats, ws, B, hw, hw, cp, cout, k, s, p, kg))

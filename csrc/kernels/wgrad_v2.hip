@@ -900,6 +900,9 @@ int psx_bgemm_tn_f32(const float* X, const float* D, float* part, const void* ze
 
 // Returns the split count (query with part == nullptr); partials need splits*OC*Kg floats.
 // f32: x / dy are fp32 (wgrad2f_kernel) instead of bf16.
+extern "C" int psx_stem7_wgrad(const float* x, const float* dy, float* part, int Nb, int IH, int IW, int cin, int cp,
+                               int OC, int Kg, hipStream_t st);
+
 int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero, int Nb, int H, int W, int IC, int OC,
                     int R, int S, int stride, int pad, int Kg, int f32, hipStream_t st) {
   Wgrad2Args a{};
@@ -916,6 +919,11 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
   a.div_ow = make_fastdiv(OW);
   a.div_s = make_fastdiv(S);
   if (OC % 64 || Kg % 64) return -2;
+  if (f32 && IC == 4 && R == 7 && S == 7 && stride == 2 && pad == 3 && OC == 64 && H == 224 && W == 224) {
+    // the ImageNet stem: its own MFMA kernel with the input patch in LDS (stem.hip)
+    const int e = psx_stem7_wgrad((const float*)x, (const float*)dy, part, Nb, H, W, 3, 4, OC, Kg, st);
+    if (e != -11) return e;
+  }
   const char* w3env = tune("wg3");
   const bool w3ok = R == 3 && S == 3 && stride == 1 && pad == 1 && IC % 64 == 0 && !(w3env && w3env[0] == '0');
   if (f32 && w3ok && (W & (W - 1)) == 0 && (H & (H - 1)) == 0 && W <= 32 && W >= 2 && a.npix % 32 == 0 &&

@@ -387,7 +387,9 @@ class HipResNetEngine:
         if self.deterministic:
             # exact fixed-point accumulators of the widest producer (NS <= 3 sums x C channels; the
             # head's 2 x fc_in) in each of the 64 rotating launch regions (bnfin.hpp DetRed)
-            cmax = max([cs.cout for cs in all_convs(sp)] + [cs.cp for cs in all_convs(sp)] + [sp.fc_in])
+            # (at least 4096 channels: the library state is process-wide, so a later launch of
+            # another shape in the same process finds room too; 64 x 2 x 12288 x 8 B = 12.6 MB)
+            cmax = max([cs.cout for cs in all_convs(sp)] + [cs.cp for cs in all_convs(sp)] + [sp.fc_in, 4096])
             nbytes = K.det_bytes(3 * cmax)
             self.det_buf = torch.zeros((nbytes + 3) // 4, dtype=torch.float32, device=self.dev)
         self.wpart = self._f32(max(1, max_wg))
@@ -609,8 +611,9 @@ class HipResNetEngine:
             elif not self._fold:  # no in-launch finalize on this path
                 self._bn_train(bs, arena, self.nslots, npix)
             return
-        if not (self.stem_direct and fin is None and cs.cin == 3 and (cs.k, cs.stride, cs.pad) == (3, 1, 1)
-                and K.stem_conv(x, wf, y, stats, self.B, cs.h, cs.w, cs.cin, cs.cp, cs.cout, cs.kg, sshift=sshift)):
+        if not (self.stem_direct and fin is None and cs.cin == 3 and (cs.k, cs.stride, cs.pad) in ((3, 1, 1), (7, 2, 3))
+                and K.stem_conv(x, wf, y, stats, self.B, cs.h, cs.w, cs.cin, cs.cp, cs.cout, cs.kg, sshift=sshift,
+                                k=cs.k)):
             K.conv_fwd2(x, wf, y, stats, self.wpart, self.B, cs.h, cs.w, cs.cp, cs.cout, cs.k, cs.stride, cs.pad,
                         cs.kg, fin=fin, sshift=sshift)
         if not train:

@@ -115,12 +115,20 @@ def conv_fwd2(x, wf, y, stats, ws, nb, h, w, ic, oc, k, stride, pad, kg, fin: Bn
                                   is_f32(x), ptr(sshift), stream_ptr()), "conv_fwd2")
 
 
-def stem_conv(x, wf, y, stats, nb, h, w, cin, cp, oc, kg, sshift=None) -> bool:
-    """The CIFAR stem (3 -> 64, 3x3 / stride 1 / pad 1) as a direct vector-ALU conv with its BN
-    statistics (csrc/kernels/stem.hip), same operands as conv_fwd2. False: not this shape or
-    deterministic mode (run conv_fwd2 instead)."""
-    rc = kernels().psx_stem_conv(ptr(x), ptr(wf), ptr(y), ptr(stats), ptr(sshift), nb, h, w, cin, cp, oc, kg,
-                                 is_f32(x), stream_ptr())
+def stem_conv(x, wf, y, stats, nb, h, w, cin, cp, oc, kg, sshift=None, k=3) -> bool:
+    """A 3-channel stem conv with its BN statistics (csrc/kernels/stem.hip), same operands as
+    conv_fwd2: k = 3 the CIFAR stem (3 -> 64, 3x3 / stride 1 / pad 1, direct vector-ALU conv;
+    not in deterministic mode), k = 7 the ImageNet stem (3 -> 64, 7x7 / stride 2 / pad 3,
+    224 -> 112, fp32 on the MFMA with the input patch in LDS). False: not this shape (run
+    conv_fwd2 instead)."""
+    if k == 7:
+        if not is_f32(x):
+            return False
+        rc = kernels().psx_stem7_conv(ptr(x), ptr(wf), ptr(y), ptr(stats), ptr(sshift), nb, h, w, cin, cp, oc, kg,
+                                      stream_ptr())
+    else:
+        rc = kernels().psx_stem_conv(ptr(x), ptr(wf), ptr(y), ptr(stats), ptr(sshift), nb, h, w, cin, cp, oc, kg,
+                                     is_f32(x), stream_ptr())
     if rc == -11:
         return False
     check(rc, "stem_conv")

@@ -26,8 +26,10 @@ plane, where a dead or hung rank instead leaves every collective of the round wa
    parallel/worker.py rounds_to_batches). A worker left out of the plan (one that hung past the
    grace period and woke up) exits.
 
-Scope: sync mode, dedicated topology (rank 0 is the server only), native RCCL transport, dense
-gradient wire. Rounds in flight at the failure are redone by the survivors; the dead worker's
+Scope: sync mode, dedicated topology (rank 0 is the server only) or co-located topology (rank 0
+is the server and worker 0; a lost rank > 0 — rank 0 holds the server), native RCCL transport; dense
+(fp16 / fp32) or top-k wire (BASELINE config 5 — the workers restore their error-feedback residual
+to the kept round from a snapshot ring, parallel/worker.py). Rounds in flight at the failure are redone by the survivors; the dead worker's
 data shard is not trained further (the reference's lost pushes are lost too).
 """
 from __future__ import annotations
@@ -49,8 +51,8 @@ EXCLUDED = 5  # exit status of a rank the survivors' plan left out
 
 def enabled(cfg, transport, world: int) -> bool:
     return (getattr(cfg, "on_worker_loss", "restart") == "shrink" and cfg.mode == "sync"
-            and cfg.topology == "dedicated" and world > 2 and getattr(transport, "native", False)
-            and cfg.codec in ("fp16", "none") and not cfg.bn_sync)
+            and (cfg.topology == "dedicated" or (cfg.topology == "colocated" and not cfg.overlap)) and world > 2 and getattr(transport, "native", False)
+            and cfg.codec in ("fp16", "none", "topk") and not cfg.bn_sync)
 
 
 def lost_error(e: BaseException) -> bool:

@@ -201,8 +201,15 @@ class WatchedRounds:
         if getattr(self.t, "lost", False):
             raise CommLost("the job communicator was aborted (liveness watchdog)")
 
+    # server-side rollback bookkeeping of a shrinking job whose rank 0 also trains (co-located
+    # topology; parallel/runner.py _PyRollback): round_start before each fetch, round_end after
+    # each push's apply
+    rollback = None
+
     def fetch(self, worker_id, local_arena):
         self._check_lost()
+        if self.rollback is not None:
+            self.rollback.round_start()
         # native transport: the broadcast is stream-ordered too (a fetch stuck on a dead
         # peer must not count as a finished round)
         return self._guard(self._fetch, worker_id, local_arena, event=self._native(),
@@ -210,5 +217,8 @@ class WatchedRounds:
 
     def push(self, worker_id, grads, local_step, buffers=None):
         self._check_lost()
-        return self._guard(self._push, worker_id, grads, local_step, buffers, event=self._native(),
-                           label=f"push of round {local_step} (gradient gather / reduce to rank 0)")
+        r = self._guard(self._push, worker_id, grads, local_step, buffers, event=self._native(),
+                        label=f"push of round {local_step} (gradient gather / reduce to rank 0)")
+        if self.rollback is not None:
+            self.rollback.round_end()
+        return r

@@ -236,7 +236,10 @@ def run_distributed(cfg, log=print) -> dict:
             wk = Worker(cfg, comp, chan, train, test, worker_name=names[rank], rank=rank, log=lg,
                         requested_id=wid_of_rank[rank], steps_per_epoch=steps)
             wk.connect_to_server()
-            if shrink_on:
+            if shrink_on and server is not None:  # co-located rank 0: server + worker 0
+                chan.rollback = _PyRollback(server, chan)
+                wk.recover = lambda e: _colocated_root_shrink(cfg, ctx, wk, server, layout, device, log)
+            elif shrink_on:
                 wk.recover = lambda e: _worker_shrink(cfg, ctx, wk, layout, device, log)
             wk.run_training(skip_steps=done)
             chan = wk.channel
@@ -469,10 +472,47 @@ def _worker_shrink(cfg, ctx, wk, layout, device, log):
     ctx["epoch"] += 1
     nt, rounds, dead = elastic.shrink(old, ctx["epoch"], _shrink_grace(cfg), log=log)
     ctx["t"] = nt
-    chan = make_sync_channel(cfg, nt, None, nt.world_size - 1, layout, device, worker=True)
+    W = nt.world_size - (1 if cfg.topology == "dedicated" else 0)  # co-located: rank 0 trains too
+    chan = make_sync_channel(cfg, nt, None, W, layout, device, worker=True)
     chan._gs = rounds
     _attach_watchdog(cfg, chan, nt, True)
     wk.rebind(chan)
+    return rounds
+
+
+def _colocated_root_shrink(cfg, ctx, wk, server, layout, device, log):
+    """Rank 0 of a shrinking co-located job (server + worker 0) when the communicator is lost:
+    abort it, roll the arena back to the first round not known complete (the channel's
+    _PyRollback, fed by every fetch / push), publish the plan as the server, mark the lost workers
+    dead (co-located: worker id = rank) and continue on a new channel over the survivors."""
+    old = ctx["t"]
+    chan = wk.channel
+    if chan.watchdog is not None:
+        chan.watchdog.stop()
+    old.lost = True
+    try:
+        old.comm.destroy(abort=True)
+    except Exception:  # noqa: BLE001
+        pass
+    try:
+        torch.cuda.synchronize()
+    except Exception:  # noqa: BLE001
+        pass
+    kept = chan.rollback.rollback() if chan.rollback is not None else server.core.global_step
+    ctx["epoch"] += 1
+    nt, rounds, dead = elastic.shrink(old, ctx["epoch"], _shrink_grace(cfg), rounds_kept=kept, log=log)
+    if not dead:
+        raise RuntimeError(f"sync shrink epoch {ctx['epoch']}: no rank was lost; failing the job")
+    ctx["t"] = nt
+    for r in dead:
+        server.core.mark_dead(r)
+    server.dropped_workers = sorted(set(getattr(server, "dropped_workers", None) or []) | set(dead))
+    members = list(nt.members)  # worker ids in the new communicator's rank order
+    nchan = make_sync_channel(cfg, nt, server, len(members), layout, device, worker=True, members=members)
+    nchan._gs = rounds
+    _attach_watchdog(cfg, nchan, nt, True)
+    nchan.rollback = _PyRollback(server, nchan)
+    wk.rebind(nchan)
     return rounds
 
 

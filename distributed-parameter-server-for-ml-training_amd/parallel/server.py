@@ -279,8 +279,9 @@ class ParameterServer:
                 # single-contribution round (W == 1): apply straight from the wire buffer — a dense
                 # wire through the collective rounds' kernel (apply_sources with one source), so a
                 # loopback round and a one-worker RCCL round (a shrunk sync job) give the same bits
-                if grads.dtype == torch.int32:
-                    self.apply(grads, res.weight)
+                if grads.dtype == torch.int32:  # decoded into the dense buffer first, as apply_gathered
+                    self._dense_of(grads)
+                    self.apply(self.agg, res.weight)
                 else:
                     trace.mark("psx.apply")
                     t0 = self._time_begin()

@@ -330,17 +330,51 @@ class Worker:
         self.global_step_cache = self.channel.fetch(self.worker_id, self.compute.local_arena)
         return self.global_step_cache
 
+    # sync shrink + top-k: the error-feedback residual as it was before each of the last RSNAP
+    # rounds' encodes (a rollback to round R restores the residual of round R; the host runs at
+    # most the compute's staging ring — 4 steps — ahead of the device, so 8 slots cover every
+    # rollback target)
+    RSNAP = 8
+    _rsnap = None
+    _pushes = 0
+
     def push_gradients(self):
         bufs = None
         if self.cfg.bn_sync:
             bufs = self.compute.local_arena[self.compute.layout.param_numel:]
         g = self.compute.grads
         if self.topk is not None:  # --codec topk: error-feedback top-k payload (parallel/topk.py)
+            if self.recover is not None:
+                self._snapshot_resid()
             g = self.topk.encode(g)
         ok = self.channel.push(self.worker_id, g, self.global_step_cache, buffers=bufs)
+        self._pushes += 1
         if not ok:
             self.pushes_rejected += 1
         return ok
+
+    def _snapshot_resid(self):
+        r = self.topk.resid
+        if self._rsnap is None:
+            self._rsnap = ([torch.empty_like(r) for _ in range(self.RSNAP)], [-1] * self.RSNAP)
+        bufs, rounds = self._rsnap
+        k = self._pushes % self.RSNAP
+        bufs[k].copy_(r)
+        rounds[k] = self._pushes
+
+    def _rewind_resid(self, rounds_kept: int):
+        """The top-k residual back to its state before round ``rounds_kept``'s encode."""
+        if self.topk is None or self._rsnap is None:
+            self._pushes = rounds_kept
+            return
+        bufs, rounds = self._rsnap
+        k = rounds_kept % self.RSNAP
+        if rounds[k] == rounds_kept:
+            self.topk.resid.copy_(bufs[k])
+        elif rounds_kept != self._pushes:
+            raise RuntimeError(f"top-k residual of round {rounds_kept} is not in the snapshot ring "
+                               f"(pushed {self._pushes}, ring {rounds})")
+        self._pushes = rounds_kept
 
     _acc = None
     _acc_n = 0
@@ -423,6 +457,7 @@ class Worker:
                     self.log(f"[psx elastic] worker {self.worker_id}: {type(e).__name__}: {e}")
                     skip_steps = self.recover(e)
                     self.local_step_counter = 0
+                    self._rewind_resid(skip_steps)
                     if hasattr(self.compute, "rewind"):  # augment stream + BN shifts of the kept round
                         self.compute.rewind(rounds_to_batches(skip_steps, len(self.sampler.epoch_indices(0)),
                                                               self.local_steps_per_sync))
@@ -441,6 +476,7 @@ class Worker:
 
     def _train_loop(self, skip_steps: int):
         K = self.local_steps_per_sync
+        self._pushes = skip_steps  # absolute round index of the next push (the snapshot ring's key)
         if skip_steps:
             rounds = skip_steps
             skip_steps = rounds_to_batches(rounds, len(self.sampler.epoch_indices(0)), K)

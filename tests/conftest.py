@@ -15,6 +15,20 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running test")
 
 
+@pytest.fixture(autouse=True)
+def _reset_deterministic(request):
+    """The kernel library's deterministic-mode state is process-wide (an engine step sets it):
+    every GPU test starts and ends with it off, so no test inherits another's mode."""
+    if "gpu" not in request.keywords:
+        yield
+        return
+    from psx.ops import kernels as K
+
+    K.set_deterministic(None)
+    yield
+    K.set_deterministic(None)
+
+
 def pytest_collection_modifyitems(config, items):
     try:
         import torch

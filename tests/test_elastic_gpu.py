@@ -30,8 +30,9 @@ import psx
 from psx.parallel.runner import run_distributed
 from psx.utils.config import PSConfig
 cfg = PSConfig(model="resnet18", batch_size=32, epochs=1, train_samples=1024, eval_every=0, verbose=1, lr=0.05,
-               max_steps=10, mode="sync", topology="dedicated", round_timeout=5.0, recovery_grace=6.0,
-               on_worker_loss="shrink", overlap={ov}, fault_inject={fi!r}, deterministic={det}).validate()
+               max_steps=10, mode="sync", topology={topo!r}, round_timeout=5.0, recovery_grace=6.0,
+               on_worker_loss="shrink", overlap={ov}, fault_inject={fi!r}, deterministic={det},
+               codec={codec!r}).validate()
 res = run_distributed(cfg, log=lambda *a, **k: print(*a, **k, flush=True))
 if res.get("server"):
     s = res["server"]
@@ -50,9 +51,9 @@ def _port():
         return s.getsockname()[1]
 
 
-def _launch(tmp_path, fault, native, overlap, det=False):
+def _launch(tmp_path, fault, native, overlap, det=False, codec="fp16", topo="dedicated", survivor=2):
     script = tmp_path / "run.py"
-    script.write_text(_RUN.format(root=ROOT, fi=fault, ov=overlap, det=det))
+    script.write_text(_RUN.format(root=ROOT, fi=fault, ov=overlap, det=det, codec=codec, topo=topo))
     port = _port()
     procs, logs = [], []
     for r in range(3):
@@ -65,7 +66,7 @@ def _launch(tmp_path, fault, native, overlap, det=False):
         procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=f, stderr=subprocess.STDOUT))
     try:
         rc0 = procs[0].wait(timeout=300)
-        rc2 = procs[2].wait(timeout=60)
+        rc2 = procs[survivor].wait(timeout=60)
     finally:
         for p in procs:
             if p.poll() is None:
@@ -106,21 +107,28 @@ import psx
 from psx.parallel.runner import run_local
 from psx.utils.config import PSConfig
 cfg = PSConfig(model="resnet18", batch_size=32, epochs=1, train_samples=1024, eval_every=0, verbose=0, lr=0.05,
-               max_steps=10, mode="sync", workers=2, deterministic=True).validate()
-res = run_local(cfg, log=lambda *a, **k: None, depart={{0: {R}}})
+               max_steps=10, mode="sync", workers={W}, deterministic=True, codec={codec!r}).validate()
+res = run_local(cfg, log=lambda *a, **k: None, depart={{{lost}: {R}}})
 s = res["server"]
 print("RESULT " + json.dumps({{"gs": s["global_steps_completed"], "sha": s["final_param_sha256"]}}), flush=True)
 """
 
 
-@pytest.mark.parametrize("native", ["1", "0"])
-def test_shrink_state_matches_scripted_departure(native, tmp_path):
+@pytest.mark.parametrize("native,codec,topo", [("1", "fp16", "dedicated"), ("0", "fp16", "dedicated"),
+                                               ("0", "topk", "dedicated"), ("1", "fp16", "colocated")])
+def test_shrink_state_matches_scripted_departure(native, codec, topo, tmp_path):
     """Not just counts: the shrunk job's final master state is bit-identical (arena sha256,
     deterministic mode) to a scripted loopback run in which both workers train rounds 0..R-1 and
     worker 1 alone the rest — R being the round the survivors resumed from (the server's rollback
     target). A rollback to the wrong snapshot slot, a round applied twice or a worker re-entering
-    with the wrong augmentation step / BN shifts changes the sha."""
-    rc0, rc2, out = _launch(tmp_path, "kill_worker:0@3", native, "False", det=True)
+    with the wrong augmentation step / BN shifts / top-k residual changes the sha. Top-k
+    (BASELINE config 5's codec): the survivor restores its error-feedback residual to round R."""
+    # dedicated: worker 0 = rank 1 is lost, worker 1 = rank 2 survives; co-located (rank 0 = server +
+    # worker 0): worker 2 = rank 2 is lost, ranks 0 and 1 train on
+    colo = topo == "colocated"
+    lost, W = (2, 3) if colo else (0, 2)
+    rc0, rc2, out = _launch(tmp_path, f"kill_worker:{lost}@3", native, "False", det=True, codec=codec, topo=topo,
+                            survivor=1 if colo else 2)
     assert rc0 == 0 and rc2 == 0, "\n---\n".join(o[-3000:] for o in out)
     s = _records(out[0], "RESULT ")[0]
     import re
@@ -128,10 +136,21 @@ def test_shrink_state_matches_scripted_departure(native, tmp_path):
     kept = [int(m) for m in re.findall(r"resuming at round (\d+)", out[0])]
     assert len(kept) == 1 and 1 <= kept[0] <= 3, out[0][-3000:]
     ref_py = tmp_path / "ref.py"
-    ref_py.write_text(_REF.format(root=ROOT, R=kept[0]))
+    ref_py.write_text(_REF.format(root=ROOT, R=kept[0], codec=codec, lost=lost, W=W))
     r = subprocess.run([sys.executable, str(ref_py)], env=dict(os.environ, PYTHONPATH=ROOT), stdout=subprocess.PIPE,
                        stderr=subprocess.STDOUT, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:]
     ref = _records(r.stdout, "RESULT ")[-1]
     assert s["gs"] == ref["gs"] == 10, (s, ref)
     assert s["sha"] == ref["sha"], (s, ref, kept)
+
+
+@pytest.mark.parametrize("fault", ["kill_worker:0@3", "hang_worker:0@3"])
+def test_sync_topk_survives_lost_worker(fault, tmp_path):
+    """BASELINE config 5's codec (sync + top-k 1 %): the shrink on the Python server loop
+    (_PyRollback) with gathered sparse payloads."""
+    rc0, rc2, out = _launch(tmp_path, fault, "0", "False", codec="topk")
+    assert rc0 == 0 and rc2 == 0, "\n---\n".join(o[-3000:] for o in out)
+    s, w = _records(out[0], "RESULT ")[0], _records(out[2], "WORKER ")[0]
+    assert w["id"] == 1 and w["steps"] == 10, w
+    assert s["gs"] == 10 and s["updates"] == 10 and s["dead"] == 1 and s["dropped"] == [0], s

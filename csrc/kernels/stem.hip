@@ -132,32 +132,38 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const T* __restrict__ x,
 // ImageNet stem (ResNet-50: 3 -> 64 channels, 7x7 / stride 2 / pad 3, 224 -> 112) on the exact-f32
 // MFMA, with the BN statistics of its output. conv_v2 runs it as an implicit GEMM whose k-steps
 // are 8 taps of the 4-channel (padded) input: the per-lane gather is a division chain per DMA
-// (no uniform-tap fast path below 32 channels) and the step ran at 47 TF (636 us at batch 128,
-// profiles/r5_r50_layers_f32_isolated.jsonl). Here a workgroup owns 4 output rows x all 112
-// columns x 64 channels of one image: the 13-row input patch it needs is staged in LDS once
-// (columns de-interleaved by parity, so a wave's 16 stride-2 pixels read 16 consecutive 16-byte
-// slots: no bank conflicts) next to all 49 x 4 x 64 weights; wave w computes output row w as
-// 4 channel tiles x 7 pixel tiles of v_mfma_f32_16x16x4_f32, one tap (4 channels = one k-group)
-// per MFMA: A = weights [oc][c], B = patch [c][pixel]. 1372 MFMAs per wave, no global traffic in
-// the mainloop; the output leaves as 16-byte (4-channel) stores per pixel.
-constexpr int kS7Rows = 4, kS7W = 112, kS7PW = 115, kS7PR = 2 * kS7Rows + 5;  // 13 patch rows
-constexpr int kS7WFloats = 49 * 4 * 64, kS7PFloats = kS7PR * 2 * kS7PW * 4;
+// (no uniform-tap fast path below 32 channels) and the step ran at 47 TF (631 us at batch 128,
+// profiles/r5_r50_layers_f32_isolated.jsonl). Here a workgroup owns 2 output rows x all 112
+// columns x 64 channels of one image: the 9-row input patch it needs is staged in LDS (columns
+// de-interleaved by parity, so a wave's 16 stride-2 pixels read 16 consecutive 16-byte slots: no
+// bank conflicts). Wave w computes output row w / 4 for channel tile w % 4 (16 channels) as 7
+// pixel tiles of v_mfma_f32_16x16x4_f32, one tap (4 channels = one k-group) per MFMA: A = its 49
+// weight fragments, held in registers for the whole kernel, B = the patch. 33 KB of LDS and ~100
+// VGPRs: two workgroups share a CU. Measured (B = 128, isolated): 571 us, the same as a first
+// version with all 64 channels per wave and the weights in LDS (98 KB, one workgroup per CU:
+// 574 us) — so the overlap of one workgroup's loads with another's MFMAs is not what bounds it
+// (profiles/r5_numbers.jsonl; the PMC pass is in profiles/r5_pmc_r50_layers.txt). The output
+// leaves as 16-byte (4-channel) stores per pixel.
+constexpr int kS7Rows = 2, kS7W = 112, kS7PW = 115, kS7PR = 2 * kS7Rows + 5;  // 9 patch rows
+constexpr int kS7PFloats = kS7PR * 2 * kS7PW * 4;
 
-__global__ __launch_bounds__(256) void stem7_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wf,
+__global__ __launch_bounds__(512) void stem7_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wf,
                                                         float* __restrict__ y, float* __restrict__ stats,
                                                         const float* __restrict__ sshift, int Kg, int IH, int IW,
                                                         DetRed det) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* const ws = sm;               // [tap][c][oc]
-  float* const pt = sm + kS7WFloats;  // [13 rows][parity][115][4]
+  __shared__ __attribute__((aligned(16))) float pt[kS7PFloats];  // [9 rows][parity][115][4]
+  __shared__ float red[2][2][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int ri = w >> 2, m = w & 3;
   const int n = blockIdx.x / (kS7W / kS7Rows), oh0 = (blockIdx.x % (kS7W / kS7Rows)) * kS7Rows;
-  for (int i = tid; i < 64 * 196; i += 256) {  // weights: k = tap * 4 + c of output channel oc
-    const int oc = i / 196, k = i - oc * 196;
-    ws[k * 64 + oc] = wf[(size_t)oc * Kg + k];
-  }
+  const int j = lane & 15, c = lane >> 4;
+  // this lane's A fragments: output channel 16 m + j, input channel c, every tap
+  float wa[49];
+  const float* wrow = wf + (size_t)(16 * m + j) * Kg + c;
+#pragma unroll
+  for (int t = 0; t < 49; ++t) wa[t] = wrow[4 * t];
   const int ih0 = 2 * oh0 - 3;
-  for (int i = tid; i < kS7PR * 2 * kS7PW; i += 256) {  // patch pixel (row rr, padded column pc)
+  for (int i = tid; i < kS7PR * 2 * kS7PW; i += 512) {  // patch pixel (row rr, padded column pc)
     const int rr = i / (2 * kS7PW), pc = i - rr * (2 * kS7PW);
     const int ih = ih0 + rr, iw = pc - 3;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -166,80 +172,60 @@ __global__ __launch_bounds__(256) void stem7_fwd_kernel(const float* __restrict_
     *reinterpret_cast<f32x4*>(pt + ((rr * 2 + (pc & 1)) * kS7PW + (pc >> 1)) * 4) = v;
   }
   __syncthreads();
-  const int j = lane & 15, c = lane >> 4;
-  f32x4 acc[4][7];
+  f32x4 acc[7];
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
+  for (int t = 0; t < 7; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < 7; ++t) acc[m][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   for (int r = 0; r < 7; ++r) {
-    const float* prow = pt + ((2 * w + r) * 2) * kS7PW * 4 + j * 4 + c;
+    const float* prow = pt + ((2 * ri + r) * 2) * kS7PW * 4 + j * 4 + c;
 #pragma unroll
     for (int sx = 0; sx < 7; ++sx) {
       const float* pb = prow + ((sx & 1) * kS7PW + (sx >> 1)) * 4;
-      const float* wa = ws + ((r * 7 + sx) * 4 + c) * 64 + j;
-      float a[4], b[7];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) a[m] = wa[16 * m];
+      float b[7];
 #pragma unroll
       for (int t = 0; t < 7; ++t) b[t] = pb[t * 64];
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int t = 0; t < 7; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], b[t], acc[m][t], 0, 0, 0);
+      for (int t = 0; t < 7; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[r * 7 + sx], b[t], acc[t], 0, 0, 0);
     }
   }
   // lane: pixels ow = 16 t + j, channels oc = 16 m + 4 c + e
-  const int oh = oh0 + w;
-  float* const yrow = y + (((size_t)n * kS7W + oh) * kS7W) * 64;
-  float s1[4][4], s2[4][4];
+  float* const yrow = y + (((size_t)n * kS7W + oh0 + ri) * kS7W) * 64 + 16 * m + 4 * c;
+  f32x4 k4 = {0.f, 0.f, 0.f, 0.f};
+  if (sshift) k4 = *reinterpret_cast<const f32x4*>(sshift + 16 * m + 4 * c);
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    f32x4 k4 = {0.f, 0.f, 0.f, 0.f};
-    if (sshift) k4 = *reinterpret_cast<const f32x4*>(sshift + 16 * m + 4 * c);
+  for (int t = 0; t < 7; ++t) {
+    *reinterpret_cast<f32x4*>(yrow + (size_t)(16 * t + j) * 64) = acc[t];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) s1[m][e] = s2[m][e] = 0.f;
-#pragma unroll
-    for (int t = 0; t < 7; ++t) {
-      *reinterpret_cast<f32x4*>(yrow + (size_t)(16 * t + j) * 64 + 16 * m + 4 * c) = acc[m][t];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float d = acc[m][t][e] - k4[e];
-        s1[m][e] += d;
-        s2[m][e] += d * d;
-      }
+    for (int e = 0; e < 4; ++e) {
+      const float d = acc[t][e] - k4[e];
+      s1[e] += d;
+      s2[e] += d * d;
     }
   }
   if (!stats) return;
 #pragma unroll
   for (int sh = 1; sh < 16; sh <<= 1)
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        s1[m][e] += __shfl_xor(s1[m][e], sh, 64);
-        s2[m][e] += __shfl_xor(s2[m][e], sh, 64);
-      }
-  __syncthreads();  // the patch region becomes the statistics scratch [wave][2][64]
-  float* red = pt;
+    for (int e = 0; e < 4; ++e) {
+      s1[e] += __shfl_xor(s1[e], sh, 64);
+      s2[e] += __shfl_xor(s2[e], sh, 64);
+    }
   if (j == 0) {
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        red[(w * 2 + 0) * 64 + 16 * m + 4 * c + e] = s1[m][e];
-        red[(w * 2 + 1) * 64 + 16 * m + 4 * c + e] = s2[m][e];
-      }
+    for (int e = 0; e < 4; ++e) {
+      red[ri][0][16 * m + 4 * c + e] = s1[e];
+      red[ri][1][16 * m + 4 * c + e] = s2[e];
+    }
   }
   __syncthreads();
   float* dst = stats + (size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * 2 * 64;
   if (tid < 128) {
-    const float v = red[tid] + red[128 + tid] + red[256 + tid] + red[384 + tid];
-    stat_add(det, dst, tid, v);  // [sum | sum of squares][oc]: tid = which * 64 + oc
+    const int which = tid >> 6, oc = tid & 63;
+    stat_add(det, dst, tid, red[0][which][oc] + red[1][which][oc]);  // [sum | sum of squares][oc]
   }
-  if (det.fix) det_finish(det, 2, 64, stats, blockIdx.x, reinterpret_cast<unsigned char*>(red + 512));
+  if (det.fix) det_finish(det, 2, 64, stats, blockIdx.x, reinterpret_cast<unsigned char*>(pt));
 }
-
 
 // Weight gradient of the ImageNet stem (fp32): dW[oc][tap][c] = sum over output pixels of
 // dy[px][oc] * x[2 oh + r - 3][2 ow + s - 3][c], as the v_mfma_f32_16x16x4_f32 GEMM M = 64 output
@@ -252,6 +238,7 @@ __global__ __launch_bounds__(256) void stem7_fwd_kernel(const float* __restrict_
 // all of a workgroup's tiles; at the end the 4 waves meet in LDS and the workgroup writes one
 // [64][Kg] fp32 slab of the split-K partials that wgrad_reduce sums (split = workgroup).
 constexpr int kS7WGrid = 256;
+constexpr int kS7WRows = 4, kS7WPR = 2 * kS7WRows + 5;  // the weight gradient's tiles: 4 rows, 13 patch rows
 
 __global__ __launch_bounds__(256) void stem7_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                                                           float* __restrict__ part, int ntiles, int Kg, int IH,
@@ -275,10 +262,10 @@ __global__ __launch_bounds__(256) void stem7_wgrad_kernel(const float* __restric
 #pragma unroll
     for (int nt = 0; nt < 13; ++nt) acc[m][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int n = tile / (kS7W / kS7Rows), oh0 = (tile % (kS7W / kS7Rows)) * kS7Rows;
+    const int n = tile / (kS7W / kS7WRows), oh0 = (tile % (kS7W / kS7WRows)) * kS7WRows;
     const int ih0 = 2 * oh0 - 3;
     __syncthreads();  // the previous tile's patch reads are done
-    for (int i = tid; i < kS7PR * 2 * kS7PW; i += 256) {
+    for (int i = tid; i < kS7WPR * 2 * kS7PW; i += 256) {
       const int rr = i / (2 * kS7PW), pc = i - rr * (2 * kS7PW);
       const int ih = ih0 + rr, iw = pc - 3;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -290,10 +277,16 @@ __global__ __launch_bounds__(256) void stem7_wgrad_kernel(const float* __restric
     // wave w: output row oh0 + w; pixel quad g = output columns 4 g .. 4 g + 3, lane's column 4 g + q
     const float* dyrow = dy + (((size_t)n * kS7W + oh0 + w) * kS7W) * 64 + 4 * j;
     const float* prow = pt + (2 * w) * 2 * kS7PW * 4 + q * 4;
-    f32x4 an = *reinterpret_cast<const f32x4*>(dyrow + (size_t)q * 64);
+    // dy loads run kAhead pixel quads ahead of the MFMAs (one quad of MFMAs is ~0.7 us: a single
+    // quad of lookahead left the HBM latency exposed)
+    constexpr int kAhead = 4;
+    f32x4 ar[kAhead];
+#pragma unroll
+    for (int u = 0; u < kAhead; ++u) ar[u] = *reinterpret_cast<const f32x4*>(dyrow + (size_t)(4 * u + q) * 64);
+#pragma unroll kAhead
     for (int g = 0; g < kS7W / 4; ++g) {
-      const f32x4 a = an;
-      if (g + 1 < kS7W / 4) an = *reinterpret_cast<const f32x4*>(dyrow + (size_t)(4 * (g + 1) + q) * 64);
+      const f32x4 a = ar[g % kAhead];
+      if (g + kAhead < kS7W / 4) ar[g % kAhead] = *reinterpret_cast<const f32x4*>(dyrow + (size_t)(4 * (g + kAhead) + q) * 64);
       const float* pb = prow + g * 16;
       float b[13];
 #pragma unroll
@@ -376,8 +369,7 @@ int psx_stem7_conv(const float* x, const float* wf, float* y, float* stats, cons
   if (cin != 3 || cp != 4 || OC != 64 || Kg < 196 || IH != 224 || IW != 224 || Nb < 1) return -11;
   const unsigned grid = (unsigned)Nb * (kS7W / kS7Rows);
   const DetRed det = stats ? det_next((int)grid, 2, 64) : DetRed{};
-  const size_t lds = (size_t)(kS7WFloats + kS7PFloats) * sizeof(float);
-  hipLaunchKernelGGL(stem7_fwd_kernel, dim3(grid), dim3(256), lds, st, x, wf, y, stats, sshift, Kg, IH, IW, det);
+  hipLaunchKernelGGL(stem7_fwd_kernel, dim3(grid), dim3(512), 0, st, x, wf, y, stats, sshift, Kg, IH, IW, det);
   return (int)hipGetLastError();
 }
 
@@ -392,7 +384,7 @@ int psx_stem7_wgrad(const float* x, const float* dy, float* part, int Nb, int IH
     if (e[0] == '0') return -11;
   if (cin != 3 || cp != 4 || OC != 64 || Kg < 196 || IH != 224 || IW != 224 || Nb < 1) return -11;
   if (!part) return kS7WGrid;
-  const int ntiles = Nb * (kS7W / kS7Rows);
+  const int ntiles = Nb * (kS7W / kS7WRows);
   const size_t lds = (size_t)2 * 64 * 196 * sizeof(float);  // >= the patch (47,840 B)
   hipLaunchKernelGGL(stem7_wgrad_kernel, dim3(kS7WGrid), dim3(256), lds, st, x, dy, part, ntiles, Kg, IH, IW);
   const int e = (int)hipGetLastError();

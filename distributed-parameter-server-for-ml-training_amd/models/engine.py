@@ -445,7 +445,10 @@ class HipResNetEngine:
         wgf_minhw = tune_int("wino_wgf_minhw", 16)
         maxhw = tune_int("wino_maxhw", 64)
         wg = tune_flag("wino_wgrad", True)
-        wg_maxhw = tune_int("wino_wgrad_maxhw", 32)
+        # Winograd weight gradient up to 64x64 images: ResNet-50's 56x56 3x3 layers take the fused
+        # one (their direct alternative is wgrad2f: the tap-reuse kernel needs power-of-two rows):
+        # same box 36.8 -> 36.4 ms/step (profiles/r5_numbers.jsonl r5_call6)
+        wg_maxhw = tune_int("wino_wgrad_maxhw", 64)
         B = self.B
         s_main = s_d = s_part = 0
         for cs in all_convs(self.spec):

@@ -3,6 +3,9 @@ set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 T="python -u -m pytest -x -q --timeout 200 --timeout-method thread"
+timeout -k 10 200 $T tests/test_fp32_gpu.py -k stem > gpurun_out/r5c4_stem.log 2>&1 || { tail -40 gpurun_out/r5c4_stem.log; exit 1; }
+tail -1 gpurun_out/r5c4_stem.log
+ONLY=3x64x224x7s2 timeout -k 10 120 python bench/r50_layers_f32.py | tee gpurun_out/r5c4_stem.jsonl
 timeout -k 10 700 $T tests/test_deterministic_gpu.py tests/test_wino_fused_gpu.py tests/test_engine_gpu.py tests/test_kernels_gpu.py > gpurun_out/r5c4_tests.log 2>&1 || { tail -40 gpurun_out/r5c4_tests.log; exit 1; }
 tail -2 gpurun_out/r5c4_tests.log
 rm -f gpurun_out/r5c4_det_ab.jsonl
@@ -23,3 +26,8 @@ for L in 256x64x56x1s1 64x256x56x1s1 1024x256x14x1s1; do
   python3 scripts/prof/pmc_summary.py gpurun_out/pmc3_$L --top 4 >> gpurun_out/r5c4_pmc_$L.txt
   rm -rf gpurun_out/pmc1_$L gpurun_out/pmc2_$L gpurun_out/pmc3_$L
 done
+PSX_TUNE=wgrad_stream=0 timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r50ser -o run -- python3 bench.py --model resnet50 --codec topk --steps 6 --warmup 3 --secondary none > gpurun_out/r5c4_r50ser.log 2>&1 || { tail -5 gpurun_out/r5c4_r50ser.log; exit 1; }
+python scripts/prof/kstats.py gpurun_out/r50ser/run_kernel_trace.csv --steps 5 > gpurun_out/r5c4_r50ser.txt
+python scripts/prof/kstats.py gpurun_out/r50ser/run_kernel_trace.csv --steps 5 --grid "conv2_kernel|wgrad|wino|bn_|stem" > gpurun_out/r5c4_r50ser_grid.txt
+head -25 gpurun_out/r5c4_r50ser.txt
+rm -rf gpurun_out/r50ser

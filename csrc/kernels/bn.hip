@@ -28,13 +28,13 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
                                                           float* __restrict__ save_mean,
                                                           float* __restrict__ save_invstd,
                                                           const float* __restrict__ sshift,
-                                                          float* __restrict__ sshift_next) {
+                                                          float* __restrict__ sshift_next, int det) {
   // 8 slot groups x 32 channels per block (T slot rows read with 8-way parallelism)
   __shared__ double red[2][8][32];
   const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
   float fs = 0.f, fss = 0.f;
-  if (c < C) {
+  if (c < C && !det) {
     for (int t = grp; t < T; t += 8) {
       fs += part[((size_t)t * 2 + 0) * C + c];
       fss += part[((size_t)t * 2 + 1) * C + c];
@@ -45,10 +45,15 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
   __syncthreads();
   if (grp == 0 && c < C) {
     double s = 0.0, ss = 0.0;
+    if (det) {  // fixed-point slot pairs: exact integer sums (bnfin.hpp DetRed)
+      s = slot_sum_rt(part, c, 2 * (size_t)C, T, true);
+      ss = slot_sum_rt(part, (size_t)C + c, 2 * (size_t)C, T, true);
+    } else {
 #pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      s += red[0][g][cl];
-      ss += red[1][g][cl];
+      for (int g = 0; g < 8; ++g) {
+        s += red[0][g][cl];
+        ss += red[1][g][cl];
+      }
     }
     double mean, var;  // shifted sums (bnfin.hpp BnFin::sshift)
     bn_moments(s, ss, count, sshift ? sshift[c] : 0.f, mean, var);
@@ -170,13 +175,6 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
     const int stat = sj >> 3, j = sj & 7;
     stat_add(det, part + (size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * NS * C, stat * C + cgi * 8 + j, acc);
   }
-  if (det.fix) {
-    if (det_finish(det, NS, C, part, blockIdx.x, reinterpret_cast<unsigned char*>(sred)) && fuse_fin) {
-      bn_bwd_finalize_block<PSX_STAT_SLOTS>(part, NS, 1, fin1);
-      if (TWO) bn_bwd_finalize_block<PSX_STAT_SLOTS>(part, NS, 2, fin2);
-    }
-    return;
-  }
   // in-launch finalize (bnfin.hpp): the last block computes the coefficients + dgamma/dbeta
   if (fuse_fin && last_block_arrive(fin1.counter, gridDim.x, reinterpret_cast<unsigned char*>(sred))) {
     bn_bwd_finalize_block<PSX_STAT_SLOTS>(part, NS, 1, fin1);
@@ -190,13 +188,13 @@ template <typename GT>
 __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int T, int NS, int which, int C, float count,
                                        const float* __restrict__ gamma, const float* __restrict__ mean,
                                        const float* __restrict__ invstd, float* __restrict__ coef,
-                                       GT* __restrict__ dgamma, GT* __restrict__ dbeta, float gscale) {
+                                       GT* __restrict__ dgamma, GT* __restrict__ dbeta, float gscale, int det) {
   // 8 slot groups x 32 channels per block: the T slot rows are read with 8-way parallelism
   __shared__ float red[2][8][32];
   const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
   float a = 0.f, b = 0.f;
-  if (c < C) {
+  if (c < C && !det) {
     for (int t = grp; t < T; t += 8) {
       a += part[((size_t)t * NS + 0) * C + c];
       b += part[((size_t)t * NS + which) * C + c];
@@ -207,10 +205,15 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int T, in
   __syncthreads();
   if (grp != 0 || c >= C) return;
   double sdz = 0.0, sxh = 0.0;
+  if (det) {  // fixed-point slot pairs: exact integer sums (bnfin.hpp DetRed)
+    sdz = slot_sum_rt(part, c, (size_t)NS * C, T, true);
+    sxh = slot_sum_rt(part, (size_t)which * C + c, (size_t)NS * C, T, true);
+  } else {
 #pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    sdz += red[0][g][cl];
-    sxh += red[1][g][cl];
+    for (int g = 0; g < 8; ++g) {
+      sdz += red[0][g][cl];
+      sxh += red[1][g][cl];
+    }
   }
   const float mdz = (float)(sdz / count), mxh = (float)(sxh / count);
   const float is = invstd[c], gm = gamma[c];
@@ -382,54 +385,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin_kernel(const T* __restri
   }
 }
 
-// ---- deterministic mode host state (bnfin.hpp DetRed)
+// ---- deterministic mode host state (bnfin.hpp DetRed): on / off
 namespace {
-struct DetState {
-  unsigned long long* fix = nullptr;  // kDetCtrSets regions of fix_per_set accumulators
-  long fix_per_set = 0;               // = slots x the words of one slot
-  int slots = 1;
-  unsigned* counters = nullptr;
-  int next = 0;
-};
-DetState g_det;
+bool g_det = false;
 }  // namespace
 
-bool det_enabled() { return g_det.fix != nullptr; }
+bool det_enabled() { return g_det; }
 
-// rotating per-launch state: a launch's arrival counter and accumulator region are reused 64
-// launches later (long after its last workgroup re-zeroed them)
-constexpr int kDetCtrSets = 64, kDetCtrPerSet = 64;
-
-// accumulator slots per launch region (power of two, PSX_TUNE=det_slots=N). With one slot every
-// workgroup of a launch adds into the same 2 x NS x C words: the same-address 64-bit atomics
-// serialise in L2 (two per statistic and workgroup, against the float path's one spread over
-// PSX_STAT_SLOTS rows); the last workgroup sums the slots (integers: still exact, order-free).
-static int det_slots() {
-  static int s = [] {
-    const char* e = tune("det_slots");
-    int v = e ? atoi(e) : 8;
-    int p = 1;
-    while (p * 2 <= v && p < 64) p *= 2;
-    return p;
-  }();
-  return s;
-}
-
-DetRed det_next(int rows, int NS, int C, int nper) {
+DetRed det_for(const float* part) {
   DetRed d{};
-  if (!g_det.fix) return d;
-  const long need = 2L * NS * C * g_det.slots;
-  if (need > g_det.fix_per_set) {
-    fprintf(stderr, "psx deterministic mode: %ld accumulator words per launch < %ld needed (%d x %d)\n",
-            g_det.fix_per_set, need, NS, C);
-    abort();
-  }
-  const int set = g_det.next++ % kDetCtrSets;
-  d.fix = g_det.fix + (size_t)set * g_det.fix_per_set;
-  d.counter = g_det.counters + (size_t)set * kDetCtrPerSet;
-  d.nwg = rows * nper;
-  d.slots = g_det.slots;
-  d.sstride = (int)(g_det.fix_per_set / g_det.slots);
+  if (g_det) d.fix = reinterpret_cast<unsigned long long*>(const_cast<float*>(part));
   return d;
 }
 
@@ -455,27 +420,15 @@ static int ew_grid(size_t nvec) {
 
 extern "C" {
 
-// Deterministic mode on (buf = a zeroed device buffer of `bytes`: 64 launch counters + 64
-// accumulator regions, psx_det_bytes) or off (buf = nullptr). Every later producer of BN sums
-// (conv epilogues, split-K epilogue, bn_bwd_reduce, the Winograd output transforms, the head)
-// accumulates in exact fixed point (bnfin.hpp DetRed). Host state only: set it before a HIP graph
-// is captured.
-long psx_det_bytes(int max_sums) {
-  return (long)kDetCtrSets * kDetCtrPerSet * 4 + (long)kDetCtrSets * det_slots() * 2 * max_sums * 8;
-}
+// Deterministic mode on (on != 0) or off. Every later producer of BN sums (conv epilogues, split-K
+// epilogue, bn_bwd_reduce, the Winograd output transforms, the head, the stems) adds exact
+// fixed-point pairs into its slot buffer — which the caller sizes psx_det_slot_scale() times the
+// float layout — and every consumer reads them as such (bnfin.hpp DetRed). Host state only: set
+// it before a HIP graph is captured.
+int psx_det_slot_scale() { return 4; }
 
-int psx_set_deterministic(void* buf, long bytes) {
-  if (!buf) {
-    g_det = DetState{};
-    return 0;
-  }
-  const long ctr_bytes = (long)kDetCtrSets * kDetCtrPerSet * 4;
-  if (bytes < ctr_bytes + kDetCtrSets * 16L * 64) return -2;
-  g_det.counters = (unsigned*)buf;
-  g_det.fix = (unsigned long long*)((char*)buf + ctr_bytes);
-  g_det.slots = det_slots();
-  g_det.fix_per_set = (bytes - ctr_bytes) / 8 / kDetCtrSets / (2 * g_det.slots) * (2 * g_det.slots);
-  g_det.next = 0;
+int psx_set_deterministic(int on) {
+  g_det = on != 0;
   return 0;
 }
 
@@ -483,7 +436,8 @@ int psx_bn_finalize(const float* part, int T, int C, float count, const float* g
                     float momentum, float* run_mean, float* run_var, float* scale, float* shift, float* save_mean,
                     float* save_invstd, const float* sshift, float* sshift_next, hipStream_t st) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, st, part, T, C, count, gamma, beta, eps,
-                     momentum, run_mean, run_var, scale, shift, save_mean, save_invstd, sshift, sshift_next);
+                     momentum, run_mean, run_var, scale, shift, save_mean, save_invstd, sshift, sshift_next,
+                     (int)det_enabled());
   return (int)hipGetLastError();
 }
 
@@ -529,6 +483,7 @@ int psx_bn_bwd_reduce(const void* g, const void* o, const void* y1, const float*
   BnBwdFin f1{}, f2{};
   if (fin1) f1 = *fin1;
   if (fin2) f2 = *fin2;
+  f1.det = f2.det = (int)det_enabled();
   if (fuse && (f1.C != C || (y2 && (!fin2 || f2.C != C)))) return -10;
   // ~512 blocks, at least 64 pixels each
   int ppb = (npix + 511) / 512;
@@ -537,7 +492,7 @@ int psx_bn_bwd_reduce(const void* g, const void* o, const void* y1, const float*
   if (!part) return PSX_STAT_SLOTS;
   const bool mask = o != nullptr, two = y2 != nullptr;
   const size_t lds = 256 * (two ? 3 : 2) * 8 * sizeof(float);
-  const DetRed det = det_next(T, two ? 3 : 2, C);
+  const DetRed det = det_for(part);
 #define PSX_BBR(M, TW)                                                                                         \
   do {                                                                                                         \
     if (f32)                                                                                                   \
@@ -564,10 +519,10 @@ int psx_bn_bwd_finalize(const float* part, int T, int NS, int which, int C, floa
   const dim3 grid((C + 31) / 32);
   if (grad_fp16)
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<uint16_t>, grid, dim3(256), 0, st, part, T, NS, which, C, count, gamma,
-                       mean, invstd, coef, (uint16_t*)dgamma, (uint16_t*)dbeta, gscale);
+                       mean, invstd, coef, (uint16_t*)dgamma, (uint16_t*)dbeta, gscale, (int)det_enabled());
   else
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, grid, dim3(256), 0, st, part, T, NS, which, C, count, gamma,
-                       mean, invstd, coef, (float*)dgamma, (float*)dbeta, gscale);
+                       mean, invstd, coef, (float*)dgamma, (float*)dbeta, gscale, (int)det_enabled());
   return (int)hipGetLastError();
 }
 
@@ -611,8 +566,9 @@ int psx_bn_apply_fin(const void* y, const float* part1, const BnFin* fin1, const
   int grid = ew_grid(nvec);
   if (grid > fin_grid_cap()) grid = fin_grid_cap();
   const size_t lds = (size_t)(8 * C + 1024) * sizeof(float);  // affines, red [2][C] f64, scratch
-  const BnFin f1 = *fin1;
-  const BnFin f2 = fin2 ? *fin2 : BnFin{};
+  BnFin f1 = *fin1;
+  BnFin f2 = fin2 ? *fin2 : BnFin{};
+  f1.det = f2.det = (int)det_enabled();
 #define PSX_BNAF(M, R)                                                                                        \
   do {                                                                                                        \
     if (f32)                                                                                                  \
@@ -648,8 +604,9 @@ int psx_bn_bwd_apply_fin(const void* g, const void* o, const void* y1, const flo
   int grid = ew_grid(nvec);
   if (grid > fin_grid_cap()) grid = fin_grid_cap();
   const size_t lds = (size_t)(10 * C + 1024) * sizeof(float);  // coefs, red [2][C] f64, scratch
-  const BnBwdFin f1 = *fin1;
-  const BnBwdFin f2 = fin2 ? *fin2 : BnBwdFin{};
+  BnBwdFin f1 = *fin1;
+  BnBwdFin f2 = fin2 ? *fin2 : BnBwdFin{};
+  f1.det = f2.det = (int)det_enabled();
 #define PSX_BBAF(M, TW, DZ)                                                                                     \
   do {                                                                                                         \
     if (f32)                                                                                                   \

@@ -35,6 +35,7 @@ struct BnFin {  // forward: batch statistics -> affine (+ running statistics)
   // becomes the next step's sshift (engine.py: copied by the next step's first launch).
   const float* sshift;
   float* sshift_next;
+  int det;  // the slot rows hold exact fixed-point pairs (deterministic mode; set by the launcher)
 };
 
 // batch moments from the (shifted) sums: mean = k + s/n, var = ss/n - (s/n)^2 (biased)
@@ -55,6 +56,7 @@ struct BnBwdFin {  // backward: sum(dz), sum(dz*xhat) -> coefficients + dgamma/d
   unsigned* counter;
   float count, gscale;
   int C, grad_fp16;
+  int det;  // the slot rows hold exact fixed-point pairs (deterministic mode; set by the launcher)
 };
 
 // All threads of the block call this after issuing their stat atomics. Returns true in the
@@ -80,24 +82,22 @@ PSX_DEV bool last_block_arrive(unsigned* counter, unsigned nblocks, unsigned cha
 
 // ---------------------------------------------------------------------------------------
 // Deterministic mode (psx_set_deterministic, bn.hip): every producer of per-channel sums adds its
-// workgroup partials into exact fixed-point accumulators instead of the float slot rows. A partial
-// v (fp32) becomes the 104-bit value round(v * 2^64) split into hi = floor(v * 2^24) and lo =
-// frac(v * 2^24) * 2^40, each added with a 64-bit integer atomic: integer addition is associative,
-// so the sums — and with them every BN statistic and the whole step — are the same bits whatever
-// the order the workgroups arrive in (no fixed-order reduction tree, no slab of per-workgroup
-// rows). The exact range is |sum| < 2^39 with an absolute resolution of 2^-64 (a partial below
-// 2^-41 in magnitude truncates its lowest bits, deterministically). The last-arriving workgroup of
-// the launch converts the sums to float into slot row 0 of the usual [PSX_STAT_SLOTS][NS][C]
-// buffer (the other rows stay zero, so the consumers are unchanged) and re-zeroes the
-// accumulators. Costs two integer atomics per (statistic, channel) and workgroup instead of one
-// float atomic, plus one arrival counter per launch.
+// workgroup partials as exact fixed-point numbers instead of floats. A partial v (fp32) becomes
+// the 104-bit value round(v * 2^64) split into hi = floor(v * 2^24) and lo = frac(v * 2^24) *
+// 2^40, each added with a 64-bit integer atomic: integer addition is associative, so the sums —
+// and with them every BN statistic and the whole step — are the same bits whatever order the
+// workgroups arrive in. The exact range is |sum| < 2^39 with an absolute resolution of 2^-64 (a
+// partial below 2^-41 in magnitude truncates its lowest bits, deterministically).
+// The pairs live IN the slot buffer: entry i of the float layout [PSX_STAT_SLOTS][NS][C] becomes
+// the 16-byte pair at byte 16 i (the engine sizes its slot buffers 4x in this mode; they are
+// zeroed every step with the float ones), so producers spread over the same 8 slot rows and no
+// launch needs an arrival counter or a conversion pass: the consumers (the finalize paths below,
+// the Winograd kernels' folded finalizes) sum the slots' pairs as integers and convert once.
+// (A first version kept rotating per-launch accumulators and converted in the launch's last
+// workgroup: the arrival + conversion tail cost 0.27 ms of the 0.65 ms its mode added to the
+// ResNet-18 fp32 step, profiles/r5_deterministic_ab.jsonl.)
 struct DetRed {
-  unsigned long long* fix;  // nullptr: deterministic mode off; [slots][NS * C][2] (hi, lo) accumulators
-  unsigned* counter;        // launch arrival counter: zero at launch, re-zeroed by the last workgroup
-  int nwg;                  // workgroups that arrive (det_finish) in the launch
-  int slots;                // power of two: workgroup b adds into slot b & (slots - 1) (spreads the
-                            // same-address atomic traffic, as the float path's PSX_STAT_SLOTS rows do)
-  int sstride;              // accumulator words per slot
+  unsigned long long* fix;  // nullptr: deterministic mode off; else the slot buffer's base (pairs)
 };
 
 PSX_DEV void fix_add(unsigned long long* p, float v) {
@@ -109,48 +109,65 @@ PSX_DEV void fix_add(unsigned long long* p, float v) {
   atomicAdd(p + 1, lo);
 }
 
-// One per-channel partial: into the float slot row `dst` (atomics, order-dependent rounding), or
-// in deterministic mode into the fixed-point accumulator of the same index `off` (row-relative:
-// [NS][C]).
+// sum of fixed-point pairs -> double (the one rounding of the whole reduction)
+PSX_DEV double fix_value(long long H, unsigned long long L) {
+  return (double)H * (1.0 / 16777216.0) + (double)L * 5.421010862427522e-20;  // 2^-24, 2^-64
+}
+
+// One per-channel partial into slot row `dst` (a row of the launch's slot buffer) at index `off`:
+// a float atomic, or in deterministic mode the fixed-point pair of the same float-layout index.
 PSX_DEV void stat_add(const DetRed& d, float* dst, int off, float v) {
-  if (d.fix)
-    fix_add(d.fix + (size_t)(blockIdx.x & (d.slots - 1)) * d.sstride + 2 * (size_t)off, v);
-  else
+  if (d.fix) {
+    const size_t i = (size_t)(dst - reinterpret_cast<float*>(d.fix)) + off;
+    fix_add(d.fix + 2 * i, v);
+  } else {
     atomicAdd(dst + off, v);
-}
-
-// Every workgroup of the launch calls this (block-uniformly) after its stat_add calls; returns true
-// in the last-arriving workgroup, after it has written the sums into slot row 0 of `part` (so an
-// in-launch finalize of the same sums can follow). lds: >= 16 bytes of the caller's LDS. (`row`:
-// unused, kept for the call sites' symmetry with the slot row they would use.)
-PSX_DEV bool det_finish(const DetRed& d, int NS, int C, float* part, int row, unsigned char* lds) {
-  (void)row;
-  if (!last_block_arrive(d.counter, (unsigned)d.nwg, lds)) return false;
-  const int n = NS * C;
-  for (int j = threadIdx.x; j < n; j += blockDim.x) {
-    long long H = 0;
-    unsigned long long L = 0;  // < nwg * 2^40: no wrap below 2^24 workgroups
-    for (int k = 0; k < d.slots; ++k) {
-      unsigned long long* p = d.fix + (size_t)k * d.sstride + 2 * (size_t)j;
-      H += (long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      L += __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const double v = (double)H * (1.0 / 16777216.0) + (double)L * 5.421010862427522e-20;  // 2^-24, 2^-64
-    part[j] = (float)v;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(d.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  return true;
 }
 
-// host: the DetRed of the next producing launch (`rows` x `nper` arriving workgroups, NS x C
-// sums). Deterministic mode off: a disabled one. An accumulator region too small for NS x C is
-// a hard error (bn.hip det_next aborts): a silent fall back to the atomic slots would break
-// bit-reproducibility unnoticed.
-DetRed det_next(int rows, int NS, int C, int nper = 1);
+// Sum over T slots of float-layout entry i0 + t * stride: doubles of the float slots, or the
+// exact integer sum of the fixed-point pairs (det). All loads issued back to back.
+template <int T>
+PSX_DEV double slot_sum(const float* part, size_t i0, size_t stride, bool det) {
+  if (det) {
+    const unsigned long long* q = reinterpret_cast<const unsigned long long*>(part);
+    long long H = 0;
+    unsigned long long L = 0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const size_t i = i0 + (size_t)t * stride;
+      H += (long long)q[2 * i];
+      L += q[2 * i + 1];
+    }
+    return fix_value(H, L);
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int t = 0; t < T; ++t) s += part[i0 + (size_t)t * stride];
+  return s;
+}
+
+// runtime slot count (the standalone finalize kernels)
+PSX_DEV double slot_sum_rt(const float* part, size_t i0, size_t stride, int T, bool det) {
+  if (det) {
+    const unsigned long long* q = reinterpret_cast<const unsigned long long*>(part);
+    long long H = 0;
+    unsigned long long L = 0;
+    for (int t = 0; t < T; ++t) {
+      const size_t i = i0 + (size_t)t * stride;
+      H += (long long)q[2 * i];
+      L += q[2 * i + 1];
+    }
+    return fix_value(H, L);
+  }
+  double s = 0.0;
+  for (int t = 0; t < T; ++t) s += part[i0 + (size_t)t * stride];
+  return s;
+}
+
+// host: the DetRed of a launch whose sums go to slot buffer `part` (disabled outside
+// deterministic mode)
+DetRed det_for(const float* part);
 bool det_enabled();
 
 // part: [T][2][C] slot rows (sum, sum of squares). Same math as bn_finalize_kernel (bn.hip).
@@ -160,18 +177,7 @@ bool det_enabled();
 template <int T>
 PSX_DEV void bn_finalize_block(const float* part, const BnFin& f) {
   for (int c = threadIdx.x; c < f.C; c += 256) {
-    float v1[T], v2[T];
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      v1[t] = part[((size_t)t * 2 + 0) * f.C + c];
-      v2[t] = part[((size_t)t * 2 + 1) * f.C + c];
-    }
-    double s = 0.0, ss = 0.0;
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      s += v1[t];
-      ss += v2[t];
-    }
+    const double s = slot_sum<T>(part, c, 2 * (size_t)f.C, f.det), ss = slot_sum<T>(part, f.C + c, 2 * (size_t)f.C, f.det);
     double mean, var;
     bn_moments(s, ss, f.count, f.sshift ? f.sshift[c] : 0.f, mean, var);
     const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
@@ -194,18 +200,8 @@ PSX_DEV void bn_finalize_block(const float* part, const BnFin& f) {
 template <int T>
 PSX_DEV void bn_bwd_finalize_block(const float* part, int NS, int which, const BnBwdFin& f) {
   for (int c = threadIdx.x; c < f.C; c += 256) {
-    float va[T], vb[T];
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      va[t] = part[((size_t)t * NS + 0) * f.C + c];
-      vb[t] = part[((size_t)t * NS + which) * f.C + c];
-    }
-    double sdz = 0.0, sxh = 0.0;
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      sdz += va[t];
-      sxh += vb[t];
-    }
+    const size_t st = (size_t)NS * f.C;
+    const double sdz = slot_sum<T>(part, c, st, f.det), sxh = slot_sum<T>(part, (size_t)which * f.C + c, st, f.det);
     const float mdz = (float)(sdz / f.count), mxh = (float)(sxh / f.count);
     const float is = f.invstd[c], gm = f.gamma[c];
     f.coef[c] = gm * is;
@@ -236,7 +232,16 @@ PSX_DEV void bn_bwd_finalize_block(const float* part, int NS, int which, const B
 // group g of G); all of a thread's 16-byte loads are independent, so the whole reduction costs
 // about one memory round trip. LDS scratch: 8 * 256 floats (caller's sbn tail).
 template <int T>
-PSX_DEV void slot_reduce2(const float* part, int NS, int ra, int rb, int C, double* red, float* scratch) {
+PSX_DEV void slot_reduce2(const float* part, int NS, int ra, int rb, int C, double* red, float* scratch,
+                          bool det = false) {
+  if (det) {  // fixed-point pairs: one thread per (row, channel), exact integer sums
+    for (int j = threadIdx.x; j < 2 * C; j += blockDim.x) {
+      const int row = j < C ? ra : rb, c = j < C ? j : j - C;
+      red[j] = slot_sum<T>(part, (size_t)row * C + c, (size_t)NS * C, true);
+    }
+    __syncthreads();
+    return;
+  }
   const int C4 = C >> 2;
   for (int cb = 0; cb < C4; cb += 256) {
     const int ncol = min(256, C4 - cb);
@@ -288,7 +293,7 @@ PSX_DEV void slot_reduce2(const float* part, int NS, int ra, int rb, int C, doub
 // sc/sh: LDS [C]; red: LDS [2][C] doubles; scratch: LDS 512 doubles.
 template <int T>
 PSX_DEV void bn_fin_lds(const float* part, const BnFin& f, float* sc, float* sh, double* red, float* scratch) {
-  slot_reduce2<T>(part, 2, 0, 1, f.C, red, scratch);
+  slot_reduce2<T>(part, 2, 0, 1, f.C, red, scratch, f.det);
   for (int c = threadIdx.x; c < f.C; c += 256) {
     double mean, var;
     bn_moments(red[c], red[f.C + c], f.count, f.sshift ? f.sshift[c] : 0.f, mean, var);
@@ -315,7 +320,7 @@ PSX_DEV void bn_fin_lds(const float* part, const BnFin& f, float* sc, float* sh,
 template <int T>
 PSX_DEV void bn_bwd_fin_lds(const float* part, int NS, int which, const BnBwdFin& f, float* coef, double* red,
                             float* scratch) {
-  slot_reduce2<T>(part, NS, 0, which, f.C, red, scratch);
+  slot_reduce2<T>(part, NS, 0, which, f.C, red, scratch, f.det);
   const int C = f.C;
   for (int c = threadIdx.x; c < C; c += 256) {
     const double sdz = red[c], sxh = red[C + c];

@@ -171,14 +171,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   const bool sc = MODE == 3 && a.in2 != nullptr && cls == 0;  // class (0, 0) + the folded shortcut
   if (MODE == 3) {
     nk = (nr * nsx + (sc ? 1 : 0)) << (a.log2_icc - 3);
-    if (pix0 >= npix_c) {  // whole workgroup: this class has fewer tiles
-      if (!SPLIT && a.det.fix && (a.stats || a.bpart))  // it still arrives at the launch counter
-        if (det_finish(a.det, a.bpart ? a.bns : 2, a.OC, a.bpart ? a.bpart : a.stats, pix_t + cls * a.n_pix_tiles,
-                       smem) &&
-            a.stats && a.fuse_fin)
-          bn_finalize_block<PSX_STAT_SLOTS>(a.stats, a.fin);
-      return;
-    }
+    if (pix0 >= npix_c) return;  // whole workgroup: this class has fewer tiles
   }
 
   f32x4 acc[MT][NT];
@@ -674,12 +667,6 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
                       red[(9 + which) * BM + row];
       stat_add(a.det, dst, which * a.OC + oc0 + row, v);
     }
-    if (a.det.fix) {
-      if (det_finish(a.det, nst, a.OC, bwd ? a.bpart : a.stats, pix_t + (MODE == 3 ? cls * a.n_pix_tiles : 0), smem) &&
-          st && a.fuse_fin)
-        bn_finalize_block<PSX_STAT_SLOTS>(a.stats, a.fin);
-      return;
-    }
     if (st && a.fuse_fin && last_block_arrive(a.fin.counter, gridDim.x, smem))
       bn_finalize_block<PSX_STAT_SLOTS>(a.stats, a.fin);
     return;
@@ -787,12 +774,6 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
     const int which = sj >> 3, j = sj & 7;
     stat_add(det, dst, which * OC + cgi * 8 + j, acc);
   }
-  if (det.fix) {
-    if (det_finish(det, nst, OC, bwd ? bpart : stats, blockIdx.x, reinterpret_cast<unsigned char*>(sred)) && stats &&
-        fuse_fin)
-      bn_finalize_block<PSX_STAT_SLOTS>(stats, fin);
-    return;
-  }
   if (!stats) return;
   if (fuse_fin && last_block_arrive(fin.counter, gridDim.x, reinterpret_cast<unsigned char*>(sred)))
     bn_finalize_block<PSX_STAT_SLOTS>(stats, fin);
@@ -848,7 +829,8 @@ Plan plan_for(int OC, int npix, int ksteps, bool f32 = false) {
 
 // deterministic mode: this launch's slab rows (one per pixel tile, per parity class for MODE 3)
 void with_det(Conv2Args& b, int rows) {
-  if (b.stats || b.bpart) b.det = det_next(rows, b.bpart ? b.bns : 2, b.OC, b.n_oc_tiles);
+  (void)rows;
+  if (b.stats || b.bpart) b.det = det_for(b.bpart ? b.bpart : b.stats);
 }
 
 template <typename T, int BM, int BN, int MODE, bool RES, bool SPLIT, int WGM = 2>
@@ -945,7 +927,7 @@ int finish_split(const Conv2Args& a, hipStream_t st) {
   const int grid = (a.npix + ppb - 1) / ppb;
   const size_t lds = 256 * 24 * sizeof(float);
   DetRed det{};
-  if (a.stats || a.bpart) det = det_next(grid, a.bpart ? a.bns : 2, a.OC);
+  if (a.stats || a.bpart) det = det_for(a.bpart ? a.bpart : a.stats);
   if (a.res)
     hipLaunchKernelGGL((conv_splitk_epilogue<T, true>), dim3(grid), dim3(256), lds, st, a.part, a.splits, a.npix,
                        a.OC, (T*)a.out, (const T*)a.res, a.stats, ppb, a.fuse_fin, a.fin, a.bpart, (const T*)a.bo,
@@ -1060,6 +1042,7 @@ int psx_conv_fwd2(const void* x, const void* wf, void* y, float* stats, const vo
     if (fin->C != OC) return -10;
     a.fuse_fin = 1;
     a.fin = *fin;
+    a.fin.det = (int)det_enabled();
   }
   a.in = x;
   a.w = wf;

@@ -157,7 +157,6 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ act, in
       stat_add(det, dst, C + c + 1, x1);
     }
   }
-  if (det.fix) det_finish(det, 2, C, bs.part, blockIdx.x, reinterpret_cast<unsigned char*>(sh));
 }
 
 // dW[k][c] = sum_b dlogits[b][k] * pooled[b][c]; db[k] = sum_b dlogits[b][k].
@@ -399,7 +398,7 @@ int head_fwd_bwd_t(const void* act, int B, int HW, int C, const float* fcw, cons
   // >= 16 + 1024 bytes: the deterministic-mode reduction's flag + scratch (bnfin.hpp det_finish)
   const size_t lds = std::max<size_t>((size_t)(C + K + 64) * sizeof(float), 1040);
   const HeadBnStats bs = (bst && dact) ? *bst : HeadBnStats{};
-  const DetRed det = bs.part ? det_next(B, 2, C) : DetRed{};
+  const DetRed det = bs.part ? det_for(bs.part) : DetRed{};
   if (dact)
     hipLaunchKernelGGL((head_kernel<T, true>), dim3(B), dim3(256), lds, st, (const T*)act, HW, C, fcw, fcb, K,
                        labels, pooled, dlogits, (T*)dact, loss, correct, 1.f / (float)B, bs, det);

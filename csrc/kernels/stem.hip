@@ -22,7 +22,7 @@ template <typename T, int CIN>
 __global__ __launch_bounds__(256) void stem_conv_kernel(const T* __restrict__ x, const T* __restrict__ wf,
                                                         T* __restrict__ y, float* __restrict__ stats,
                                                         const float* __restrict__ sshift, int Nb, int H, int W,
-                                                        int Kg) {
+                                                        int Kg, DetRed det) {
   constexpr int CP = kEPC<T>;  // input channels per pixel as stored (one 16-byte chunk)
   constexpr int OC = 64, NK = 9 * CIN, TS = OC + 4;
   static_assert(CIN <= 4 && CIN <= CP, "the stem's channels fit one chunk");
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const T* __restrict__ x,
     __syncthreads();
     if (tid < 128) {
       const float v = ws[tid] + ws[128 + tid] + ws[256 + tid] + ws[384 + tid];
-      atomicAdd(stats + (size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * 2 * OC + tid, v);
+      stat_add(det, stats + (size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * 2 * OC, tid, v);
     }
   }
   // the tile is one contiguous [nvalid][64] block of y: 16-byte stores in address order
@@ -224,7 +224,6 @@ __global__ __launch_bounds__(512) void stem7_fwd_kernel(const float* __restrict_
     const int which = tid >> 6, oc = tid & 63;
     stat_add(det, dst, tid, red[0][which][oc] + red[1][which][oc]);  // [sum | sum of squares][oc]
   }
-  if (det.fix) det_finish(det, 2, 64, stats, blockIdx.x, reinterpret_cast<unsigned char*>(pt));
 }
 
 // Weight gradient of the ImageNet stem (fp32): dW[oc][tap][c] = sum over output pixels of
@@ -337,23 +336,23 @@ extern "C" {
 // y = conv3x3(x, wf) (stride 1, pad 1) of the 3-channel stem into 64 channels, + the BN
 // statistics [PSX_STAT_SLOTS][2][64] (nullable) of (y - sshift) (sshift nullable). x: NHWC with
 // cp = one 16-byte chunk of channels (4 fp32 / 8 bf16, zero padded); wf: the conv_v2 forward
-// weights [64][Kg], k = tap * cp + c. -11: not this shape, or deterministic mode (the caller
-// runs psx_conv_fwd2 instead).
+// weights [64][Kg], k = tap * cp + c. -11: not this shape (the caller runs psx_conv_fwd2 instead).
 int psx_stem_conv(const void* x, const void* wf, void* y, float* stats, const float* sshift, int Nb, int H, int W,
                   int cin, int cp, int OC, int Kg, int f32, hipStream_t st) {
   if (const char* e = tune("stem_direct"))
     if (e[0] == '0') return -11;
-  if (cin != 3 || OC != 64 || cp != (f32 ? 4 : 8) || Kg < 9 * cp || W % 4 || det_enabled()) return -11;
+  if (cin != 3 || OC != 64 || cp != (f32 ? 4 : 8) || Kg < 9 * cp || W % 4) return -11;
   const long npix = (long)Nb * H * W;
   if (npix <= 0 || npix > (1L << 30)) return -2;
   const dim3 grid((unsigned)((npix + 255) / 256));
+  const DetRed det = stats ? det_for(stats) : DetRed{};
   const size_t lds = (size_t)(27 * 64 + 256 * 68) * sizeof(float);
   if (f32)
     hipLaunchKernelGGL((stem_conv_kernel<float, 3>), grid, dim3(256), lds, st, (const float*)x, (const float*)wf,
-                       (float*)y, stats, sshift, Nb, H, W, Kg);
+                       (float*)y, stats, sshift, Nb, H, W, Kg, det);
   else
     hipLaunchKernelGGL((stem_conv_kernel<uint16_t, 3>), grid, dim3(256), lds, st, (const uint16_t*)x,
-                       (const uint16_t*)wf, (uint16_t*)y, stats, sshift, Nb, H, W, Kg);
+                       (const uint16_t*)wf, (uint16_t*)y, stats, sshift, Nb, H, W, Kg, det);
   return (int)hipGetLastError();
 }
 
@@ -368,7 +367,7 @@ int psx_stem7_conv(const float* x, const float* wf, float* y, float* stats, cons
     if (e[0] == '0') return -11;
   if (cin != 3 || cp != 4 || OC != 64 || Kg < 196 || IH != 224 || IW != 224 || Nb < 1) return -11;
   const unsigned grid = (unsigned)Nb * (kS7W / kS7Rows);
-  const DetRed det = stats ? det_next((int)grid, 2, 64) : DetRed{};
+  const DetRed det = stats ? det_for(stats) : DetRed{};
   hipLaunchKernelGGL(stem7_fwd_kernel, dim3(grid), dim3(512), 0, st, x, wf, y, stats, sshift, Kg, IH, IW, det);
   return (int)hipGetLastError();
 }

@@ -213,12 +213,8 @@ __global__ __launch_bounds__(384) void wino_in_xf_kernel(const float* __restrict
   float sc = 1.f, sh = 0.f;
   if (bnpart) {
     if (wv == 0) {  // BN finalize of the workgroup's 64 channels
-      double s = 0.0, ss = 0.0;
-#pragma unroll
-      for (int q = 0; q < PSX_STAT_SLOTS; ++q) {
-        s += bnpart[(size_t)q * 2 * C + c];
-        ss += bnpart[(size_t)q * 2 * C + C + c];
-      }
+      const double s = slot_sum<PSX_STAT_SLOTS>(bnpart, c, 2 * (size_t)C, fin.det);
+      const double ss = slot_sum<PSX_STAT_SLOTS>(bnpart, (size_t)C + c, 2 * (size_t)C, fin.det);
       double mean, var;
       bn_moments(s, ss, fin.count, fin.sshift ? fin.sshift[c] : 0.f, mean, var);
       const float invstd = (float)(1.0 / sqrt(var + (double)fin.eps));
@@ -450,10 +446,6 @@ __global__ __launch_bounds__(384) void wino_out_xf_kernel(const float* __restric
     const float v = red[which][0][lane] + red[which][1][lane] + red[which][2][lane] + red[which][3][lane];
     stat_add(det, row, which * K + k, v);
   }
-  if (det.fix) {
-    __syncthreads();  // red[] is reused as the hand-off flag
-    det_finish(det, nst, K, dst, blockIdx.y, reinterpret_cast<unsigned char*>(&red[0][0][0]));
-  }
 }
 
 // dW[k][c][3][3] = scale * G^T M G, M[b] = sum of the q partial slabs part[b * q + j][k][c] (the
@@ -580,6 +572,7 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
   const int T = (int)wino_tiles(N, H, W);
   WinoBnFin bf{};
   if (bnpart) bf = *bnfin;
+  bf.det = (int)det_enabled();
   hipLaunchKernelGGL(wino_in_xf_kernel, dim3(C / 64, wino_xf_grid(T, C / 64)), dim3(64 * kXfWaves), 0, st, x, V, T, H,
                      W, C, bnpart, bf);
   // the 36 GEMMs: the conv_v2 mainloop. (Measured slower and removed in round 5: a stream-K GEMM,
@@ -592,7 +585,7 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
   if (bst) bs = *bst;
   const int gyo = wino_xf_grid(T, K / 64);
   DetRed det{};
-  if (bst || stats) det = det_next(gyo, bst ? (bst->y2 ? 3 : 2) : 2, K, K / 64);
+  if (bst || stats) det = det_for(bst ? bst->part : stats);
   using OutK = void (*)(const float*, float*, const float*, float*, int, int, int, int, WinoBwdStats, DetRed,
                        const float*);
   // [res][variant]: forward, backward (ReLU mask from o / from the affine) x (one / two BN sums)
@@ -651,6 +644,7 @@ int psx_wino_wgrad(const float* V, const float* dy, float* D, float* part, void*
   const int T = (int)wino_tiles(N, H, W);
   BnBwdFin bb{};
   if (bpart) bb = *bbfin;
+  bb.det = (int)det_enabled();
   hipLaunchKernelGGL(wino_dy_xf_kernel, dim3(K / 64, wino_xf_grid(T, K / 64)), dim3(64 * kXfWaves), 0, st, dy, D, T, H,
                      W, K, ybn, bpart, bb);
   const int bt = wino_wtile(C, K);

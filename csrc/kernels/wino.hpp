@@ -56,6 +56,7 @@ struct WinoBnFin {
   int C;
   const float* sshift;  // shifted sums (bnfin.hpp BnFin::sshift)
   float* sshift_next;
+  int det;  // fixed-point slot pairs (bnfin.hpp BnFin::det)
 };
 
 // Fused BN-backward sums over a data-gradient output (the layout of conv_v2.hip BwdStatsDesc):
@@ -81,13 +82,8 @@ struct WinoBwdStats {
 PSX_DEV void wino_bwd_coef(const float* part, const BnBwdFin& f, int c, float& k1, float& k2, float& k3, double& sdz,
                            double& sxh) {
   const int C = f.C;
-  sdz = 0.0;
-  sxh = 0.0;
-#pragma unroll
-  for (int q = 0; q < PSX_STAT_SLOTS; ++q) {
-    sdz += part[(size_t)q * 2 * C + c];
-    sxh += part[(size_t)q * 2 * C + C + c];
-  }
+  sdz = slot_sum<PSX_STAT_SLOTS>(part, c, 2 * (size_t)C, f.det);
+  sxh = slot_sum<PSX_STAT_SLOTS>(part, (size_t)C + c, 2 * (size_t)C, f.det);
   const float mdz = (float)(sdz / f.count), mxh = (float)(sxh / f.count);
   const float is = f.invstd[c], gm = f.gamma[c];
   k1 = gm * is;

@@ -124,12 +124,8 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
     }
   } else {  // BN finalize of the input channels (wino.hip wino_in_kernel), all C of them
     for (int c = threadIdx.x; c < C; c += 512) {
-      double s = 0.0, ss = 0.0;
-#pragma unroll
-      for (int q = 0; q < PSX_STAT_SLOTS; ++q) {
-        s += a.bnpart[(size_t)q * 2 * C + c];
-        ss += a.bnpart[(size_t)q * 2 * C + C + c];
-      }
+      const double s = slot_sum<PSX_STAT_SLOTS>(a.bnpart, c, 2 * (size_t)C, fin.det);
+      const double ss = slot_sum<PSX_STAT_SLOTS>(a.bnpart, (size_t)C + c, 2 * (size_t)C, fin.det);
       double mean, var;
       bn_moments(s, ss, fin.count, fin.sshift ? fin.sshift[c] : 0.f, mean, var);
       const float invstd = (float)(1.0 / sqrt(var + (double)fin.eps));
@@ -494,10 +490,6 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
     stat_add(det, row, K + k, s2 + red[1][kq][l]);
     if constexpr (two) stat_add(det, row, 2 * K + k, s3 + red[2][kq][l]);
   }
-  if (det.fix) {
-    __syncthreads();  // vb is the hand-off scratch
-    det_finish(det, nst, K, dst, tb, reinterpret_cast<unsigned char*>(&vb[0][0][0][0]));
-  }
 }
 
 }  // namespace psx
@@ -535,14 +527,16 @@ int psx_wino_fused(const float* x, const float* Uf, float* y, const float* res, 
                   (int)((long)N * H * W * K * 4)};
   WinoBnFin bf{};
   if (bnpart) bf = *bnfin;
+  bf.det = (int)det_enabled();
   WinoBwdStats bs{};
   if (bst) bs = *bst;
   const int rows = T / kWfT;
   DetRed det{};
-  if (bst || stats) det = det_next(rows, bst ? (bst->y2 ? 3 : 2) : 2, K, K / kWfK);
+  if (bst || stats) det = det_for(bst ? bst->part : stats);
   using FK = void (*)(WinoFusedArgs, WinoBnFin, WinoBwdStats, DetRed, BnBwdFin);
   BnBwdFin bb{};
   if (bpart) bb = *bbfin;
+  bb.det = (int)det_enabled();
 #define PSX_WF_ROW(G, R)                                                                                     \
   {wino_fused_kernel<G, R, false, false, false>, wino_fused_kernel<G, R, true, false, false>,                 \
    wino_fused_kernel<G, R, true, false, true>, wino_fused_kernel<G, R, true, true, false>,                    \

@@ -288,6 +288,7 @@ int psx_wino_wgrad_fused(const float* x, const float* xaff, const float* dy, con
   a.ybn = ybn;
   a.bpart = bpart;
   if (bpart) a.bfin = *bbfin;
+  a.bfin.det = (int)det_enabled();
   a.part = part;
   a.H = H;
   a.W = W;

@@ -176,10 +176,11 @@ class HipResNetEngine:
             raise ValueError(f"engine dtype {dtype}: bfloat16 or float32")
         self.dtype = dtype
         self.f32 = dtype == torch.float32
-        # deterministic mode: every BN statistic reduced in a fixed order (no atomic-order
-        # dependence), so two runs of a step give bit-identical gradients (PSX_DETERMINISTIC=1)
+        # deterministic mode (the default; PSX_DETERMINISTIC=0 or deterministic=False: off): every
+        # BN statistic accumulates as exact fixed-point integers (csrc/kernels/bnfin.hpp DetRed),
+        # so two runs of a step give bit-identical gradients, for +0-2 % step time
         if deterministic is None:
-            deterministic = os.environ.get("PSX_DETERMINISTIC", "0") == "1"
+            deterministic = os.environ.get("PSX_DETERMINISTIC", "1") == "1"
         self.deterministic = bool(deterministic)
         self.mean, self.std = mean, std
         self.eps, self.mom = bn_eps, bn_momentum
@@ -313,15 +314,18 @@ class HipResNetEngine:
         red_off = [self.ctr_words]
         nctr = [0]
 
+        # deterministic mode: every slot entry is a 16-byte fixed-point pair (bnfin.hpp DetRed)
+        sw = K.det_slot_scale() if self.deterministic else 1
+
         def bn_state(bs: BNSpec):
             fwd = red_off[0]
-            bwd = fwd + self.nslots * 2 * bs.c
-            red_off[0] = bwd + self.nslots * 3 * bs.c
+            bwd = fwd + sw * self.nslots * 2 * bs.c
+            red_off[0] = bwd + sw * self.nslots * 3 * bs.c
             nctr[0] += 2
             so = shift_off[0]
             shift_off[0] += bs.c
             self.bn[bs.name] = dict(affine=self._f32(2, bs.c), saved=self._f32(2, bs.c), coef=self._f32(3, bs.c),
-                                    c=bs.c, fwd=(fwd, self.nslots * 2 * bs.c), bwd=(bwd, self.nslots * 3 * bs.c),
+                                    c=bs.c, fwd=(fwd, sw * self.nslots * 2 * bs.c), bwd=(bwd, sw * self.nslots * 3 * bs.c),
                                     ctr=nctr[0] - 2, sshift=self.bn_shift[0, so:so + bs.c],
                                     sshift_next=self.bn_shift[1, so:so + bs.c])
 
@@ -383,15 +387,6 @@ class HipResNetEngine:
             h_in = d["out"]
         self.final = h_in
         self.red = self._f32(red_off[0])
-        self.det_buf = None
-        if self.deterministic:
-            # exact fixed-point accumulators of the widest producer (NS <= 3 sums x C channels; the
-            # head's 2 x fc_in) in each of the 64 rotating launch regions (bnfin.hpp DetRed)
-            # (at least 4096 channels: the library state is process-wide, so a later launch of
-            # another shape in the same process finds room too; 64 x 2 x 12288 x 8 B = 12.6 MB)
-            cmax = max([cs.cout for cs in all_convs(sp)] + [cs.cp for cs in all_convs(sp)] + [sp.fc_in, 4096])
-            nbytes = K.det_bytes(3 * cmax)
-            self.det_buf = torch.zeros((nbytes + 3) // 4, dtype=torch.float32, device=self.dev)
         self.wpart = self._f32(max(1, max_wg))
         self.wpart_w = self._f32(max(1, self._plan_wpart(max_wp)))
         self._plan_wino()
@@ -908,7 +903,7 @@ class HipResNetEngine:
     def forward(self, arena: torch.Tensor, train: bool = True):
         # the kernel library's deterministic-reduction state is process-wide host state: every
         # step (and every captured graph) takes this engine's setting
-        K.set_deterministic(self.det_buf if self.deterministic else None)
+        K.set_deterministic(self.deterministic)
         sp, B = self.spec, self.B
         st = sp.stem_conv
         zeroed, self._zeroed = self._zeroed, False

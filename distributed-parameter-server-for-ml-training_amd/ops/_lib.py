@@ -79,8 +79,8 @@ _KERNEL_SIGS = {
     "psx_head_wgrad": (i32, [vp, vp, i32, i32, i32, vp, vp, f32, i32, vp]),
     "psx_sgd_apply": (i32, [vp, vp, vp, i64, f32, f32, f32, f32, i32, i32, vp, vp]),
     "psx_grad_aggregate": (i32, [vp, i32, i32, vp, i32, i64, f32, i32, vp]),
-    "psx_set_deterministic": (i32, [vp, i64]),
-    "psx_det_bytes": (i64, [i32]),
+    "psx_set_deterministic": (i32, [i32]),
+    "psx_det_slot_scale": (i32, []),
     "psx_sgd_apply_multi": (i32, [vp, vp, i32, vp, i64, f32, f32, f32, f32, i32, i32, vp, vp]),
     "psx_fp16_pack": (i32, [vp, vp, i64, f32, vp]),
     "psx_fp16_unpack": (i32, [vp, vp, i64, f32, vp]),

@@ -27,28 +27,38 @@ STAT_SLOTS = 8  # PSX_STAT_SLOTS in csrc/kernels/common.hpp
 _ZERO_PAGES = {}
 
 
-_DET_BUF = None  # keeps the deterministic-mode scratch alive while the library points at it
+_DET_ON = False
 
 
-def det_bytes(max_sums: int) -> int:
-    """Bytes of the deterministic-mode buffer for producers of at most ``max_sums`` per-channel
-    sums per launch (NS x C: 3 x the widest BN layer)."""
-    return int(kernels().psx_det_bytes(int(max_sums)))
+def det_slot_scale() -> int:
+    """Size factor of every BN slot buffer in deterministic mode: entry i of the float layout
+    [STAT_SLOTS][NS][C] becomes a 16-byte fixed-point pair (csrc/kernels/bnfin.hpp DetRed)."""
+    return int(kernels().psx_det_slot_scale())
 
 
-def set_deterministic(buf):
-    """Deterministic BN reductions (csrc/kernels/bnfin.hpp DetRed: exact fixed-point accumulators,
-    order-independent) through ``buf`` (a zeroed device tensor of det_bytes(max_sums) bytes: 64
-    launch counters + 64 accumulator regions), or off with None. Host state of the kernel
-    library: set it before capturing a HIP graph."""
-    global _DET_BUF
-    if buf is None:
-        check(kernels().psx_set_deterministic(None, 0), "set_deterministic")
-        _DET_BUF = None
-        return
-    assert buf.is_contiguous() and buf.is_cuda
-    check(kernels().psx_set_deterministic(ptr(buf), buf.numel() * buf.element_size()), "set_deterministic")
-    _DET_BUF = buf
+def set_deterministic(on) -> None:
+    """Deterministic BN reductions (csrc/kernels/bnfin.hpp DetRed: exact fixed-point pairs in the
+    slot buffers, order-independent) on or off. Every slot buffer handed to a kernel while it is
+    on must be det_slot_scale() times the float layout and zeroed like the float one. Host state
+    of the kernel library: set it before capturing a HIP graph."""
+    global _DET_ON
+    _DET_ON = bool(on)
+    check(kernels().psx_set_deterministic(int(_DET_ON)), "set_deterministic")
+
+
+def deterministic() -> bool:
+    return _DET_ON
+
+
+def det_slot_values(buf, shape):
+    """Decode a deterministic-mode slot buffer: float64 values of its fixed-point pairs in the
+    float layout ``shape`` (e.g. (STAT_SLOTS, 2, C))."""
+    n = 1
+    for d in shape:
+        n *= int(d)
+    q = buf.reshape(-1).view(torch.int64)[:2 * n].view(n, 2).double()
+    lo = q[:, 1] + (q[:, 1] < 0).double() * 18446744073709551616.0  # the low word is unsigned
+    return (q[:, 0] * 2.0 ** -24 + lo * 2.0 ** -64).view(*shape)
 
 
 def is_f32(t) -> int:
@@ -79,14 +89,15 @@ class BnFin(C.Structure):
     _fields_ = [("gamma", C.c_void_p), ("beta", C.c_void_p), ("run_mean", C.c_void_p), ("run_var", C.c_void_p),
                 ("scale", C.c_void_p), ("shift", C.c_void_p), ("save_mean", C.c_void_p),
                 ("save_invstd", C.c_void_p), ("counter", C.c_void_p), ("count", C.c_float), ("eps", C.c_float),
-                ("momentum", C.c_float), ("C", C.c_int), ("sshift", C.c_void_p), ("sshift_next", C.c_void_p)]
+                ("momentum", C.c_float), ("C", C.c_int), ("sshift", C.c_void_p), ("sshift_next", C.c_void_p),
+                ("det", C.c_int)]  # det: set by the launcher (deterministic mode)
 
 
 class BnBwdFin(C.Structure):
     """csrc/kernels/bnfin.hpp BnBwdFin: in-launch backward BN finalize descriptor."""
     _fields_ = [("gamma", C.c_void_p), ("mean", C.c_void_p), ("invstd", C.c_void_p), ("coef", C.c_void_p),
                 ("dgamma", C.c_void_p), ("dbeta", C.c_void_p), ("counter", C.c_void_p), ("count", C.c_float),
-                ("gscale", C.c_float), ("C", C.c_int), ("grad_fp16", C.c_int)]
+                ("gscale", C.c_float), ("C", C.c_int), ("grad_fp16", C.c_int), ("det", C.c_int)]
 
 
 def bn_fin(gamma, beta, run_mean, run_var, affine, saved, counter_ptr, count, eps, momentum, c, sshift=None,

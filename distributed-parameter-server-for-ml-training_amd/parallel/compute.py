@@ -122,7 +122,7 @@ class TorchCompute:
 class HipCompute:
     def __init__(self, model: torch.nn.Module, layout: ParamLayout, batch: int, device, model_name="resnet18",
                  grad_dtype=torch.float16, seed: int = 0, use_graph: bool = True, dtype: str = "fp32",
-                 deterministic: bool = False):
+                 deterministic: bool | None = None):
         from ..models.engine import CIFAR_MEAN, CIFAR_STD, IMAGENET_MEAN, IMAGENET_STD, HipResNetEngine
 
         (c, h, w), _ = MODEL_INPUT.get(model_name, ((3, 32, 32), 100))
@@ -133,7 +133,7 @@ class HipCompute:
         self.engine = HipResNetEngine(model, layout, batch, device=self.device, grad_dtype=grad_dtype, in_hw=(h, w),
                                       mean=mean, std=std, seed=1234 + seed,
                                       dtype=torch.float32 if dtype == "fp32" else torch.bfloat16,
-                                      deterministic=deterministic or None)
+                                      deterministic=deterministic)
         self.local_arena = torch.zeros(layout.arena_numel, dtype=torch.float32, device=self.device)
         self.grads = self.engine.grads
         self.use_graph = use_graph
@@ -268,7 +268,7 @@ class HipCompute:
 
 
 def make_compute(model, layout, batch, device, model_name="resnet18", grad_dtype=torch.float16, seed=0,
-                 use_graph=True, dtype="fp32", deterministic=False):
+                 use_graph=True, dtype="fp32", deterministic=None):
     """The worker's local fwd/bwd: the HIP engine on a GPU (compute dtype fp32 or bf16), torch
     fp32 autograd on the CPU (tests)."""
     dev = torch.device(device)

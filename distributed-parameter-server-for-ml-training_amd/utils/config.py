@@ -63,7 +63,8 @@ class PSConfig:
     # statistics. bn_sync=True makes workers push their running stats with each gradient push;
     # the server averages them (sync) or blends them 1/W (async). Default off = reference parity.
     bn_sync: bool = False
-    deterministic: bool = False    # fixed-order BN reductions: bit-reproducible steps (engine, PSX_DETERMINISTIC)
+    deterministic: bool | None = None  # exact fixed-point BN reductions, bit-reproducible steps; None:
+    # PSX_DETERMINISTIC (default 1 = on; engine)
     # fetch payload: "bf16conv" = conv weights as bf16 (exactly the bits the bf16 engine consumes)
     # + fp32 for everything else (half the bytes); "fp32" = the reference's full fp32 state;
     # "auto" = fp32 for --dtype fp32, bf16conv for --dtype bf16.
@@ -188,8 +189,11 @@ def add_arguments(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     A("--weight-decay", type=float, default=None)
     A("--sync-semantics", choices=["barrier", "reference"], default=None)
     A("--bn-sync", action="store_true", default=None, help="workers push BN running stats; server averages")
-    A("--deterministic", action="store_true", default=None,
-      help="fixed-order BN statistic reductions: bit-reproducible training steps (slower)")
+    A("--deterministic", dest="deterministic", action="store_true", default=None,
+      help="exact fixed-point BN statistic reductions: bit-reproducible training steps (the default; "
+           "+0-2%% step time, profiles/r5_deterministic_ab.jsonl)")
+    A("--no-deterministic", dest="deterministic", action="store_false", default=None,
+      help="float-atomic BN statistic reductions (order-dependent rounding)")
     A("--fetch-codec", choices=["auto", "bf16conv", "fp32"], default=None)
     A("--overlap", dest="overlap", action="store_true", default=None,
       help="sync mode: stream gradient buckets (reduce/apply/broadcast) during the backward pass")

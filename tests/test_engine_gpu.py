@@ -25,6 +25,14 @@ def _cos(a, b):
     return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
 
 
+def _slot_sums(buf, c, det):
+    """Per-channel sums of the 2-row slot layout [STAT_SLOTS][2][c] (deterministic mode: the
+    fixed-point pairs, csrc/kernels/bnfin.hpp DetRed)."""
+    if det:
+        return K.det_slot_values(buf, (K.STAT_SLOTS, 2, c)).sum(0).float()
+    return buf[:K.STAT_SLOTS * 2 * c].view(K.STAT_SLOTS, 2, c).sum(0)
+
+
 @pytest.fixture(scope="module")
 def setup():
     torch.manual_seed(0)
@@ -195,9 +203,9 @@ def test_dgrad_fused_bn_backward_sums_match_reduce_kernel(setup):
             ref = torch.zeros_like(eng._red(bs, "bwd"))
             K.bn_bwd_reduce(d["da"][i - 1], d["a"][i - 1], d["y"][i - 1], eng.bn[bs.name]["saved"], ref, npix, bs.c)
             torch.cuda.synchronize()
-            m = K.STAT_SLOTS * 2 * bs.c  # the region is sized for 3 stat rows; NS = 2 here
-            got = eng._red(bs, "bwd")[:m].view(K.STAT_SLOTS, 2, bs.c).sum(0)
-            want = ref[:m].view(K.STAT_SLOTS, 2, bs.c).sum(0)
+            # the region is sized for 3 stat rows; NS = 2 here
+            got = _slot_sums(eng._red(bs, "bwd"), bs.c, eng.deterministic)
+            want = _slot_sums(ref, bs.c, eng.deterministic)
             assert torch.allclose(got, want, rtol=1e-3, atol=1e-3 * want.abs().max().item()), bs.name
             checked += 1
     # the last block's output BN: its sums come out of the head launch (engine.head)
@@ -206,9 +214,8 @@ def test_dgrad_fused_bn_backward_sums_match_reduce_kernel(setup):
     ref = torch.zeros_like(eng._red(bs, "bwd"))
     K.bn_bwd_reduce(eng.dfinal, eng.final, eng.blk[-1]["y"][-1], eng.bn[bs.name]["saved"], ref, npix, bs.c)
     torch.cuda.synchronize()
-    m = K.STAT_SLOTS * 2 * bs.c
-    got = eng._red(bs, "bwd")[:m].view(K.STAT_SLOTS, 2, bs.c).sum(0)
-    want = ref[:m].view(K.STAT_SLOTS, 2, bs.c).sum(0)
+    got = _slot_sums(eng._red(bs, "bwd"), bs.c, eng.deterministic)
+    want = _slot_sums(ref, bs.c, eng.deterministic)
     assert torch.allclose(got, want, rtol=1e-3, atol=1e-3 * want.abs().max().item()), bs.name
     eng.fuse_bnbwd = before
     assert checked == 8

@@ -76,7 +76,8 @@ def main():
             # config, and the per-step weight transforms (forward + flipped)
             u = torch.empty(36 * cout * cin, device="cuda")
             ud = torch.empty(36 * cout * cin, device="cuda")
-            nv = max(K.wino_v_floats(B, hw, hw, cin), K.wino_v_floats(B, hw, hw, cout))
+            nv = max(K.wino_v_floats(B, hw, hw, cin), K.wino_v_floats(B, hw, hw, cout), K.wino_p_floats(B, hw, hw, cin, cout),
+                     K.wino_p_floats(B, hw, hw, cout, cin))
             v1, v2 = torch.empty(nv, device="cuda"), torch.empty(nv, device="cuda")
             xw = x.permute(0, 2, 3, 1).contiguous()
             r["wino_wt_us"] = t_us(lambda: (K.wino_weights(w, u, cout, cin), K.wino_weights(w, ud, cout, cin, True)))

@@ -1121,10 +1121,12 @@ int psx_conv_dgrad2_sc(const void* dy, const void* wd, void* dx, const void* res
 // (R = nb, S = 1: tap b reads row b, i.e. A[b]) — split-K into nb slabs of Kd, so split s is
 // exactly batch s (the Winograd GEMMs, wino.hip). cfg: tile (0: 64x64, 1: 64x128, 2: 64x256 /
 // 1x4 waves, 3: 64x128 / 1x4 waves; N rows x M pixels).
-int psx_bgemm_f32(const float* A, const float* B, float* P, const void* zero, int M, int N, int Kd, int nb, int cfg,
-                  hipStream_t st) {
-  if (N % 64 || Kd < kKS<float> || (Kd & (Kd - 1)) || M < 1 || nb < 1) return -2;
-  Plan p{64, 64, nb, 2};
+// s2 > 1: each batch's Kd-long reduction as s2 ranges (whole k-steps) writing s2 partial slabs
+// P[b s2 + j][M][N] (the Winograd output transform sums them, wino.hip psx_wino_conv)
+int psx_bgemm_f32_split(const float* A, const float* B, float* P, const void* zero, int M, int N, int Kd, int nb,
+                        int s2, int cfg, hipStream_t st) {
+  if (N % 64 || Kd < kKS<float> || (Kd & (Kd - 1)) || M < 1 || nb < 1 || s2 < 1 || (Kd / kKS<float>) % s2) return -2;
+  Plan p{64, 64, nb * s2, 2};
   if (cfg == 1) p.BN = 128;
   if (cfg == 2) { p.BN = 256; p.WGM = 1; }
   if (cfg == 3) { p.BN = 128; p.WGM = 1; }
@@ -1143,9 +1145,14 @@ int psx_bgemm_f32(const float* A, const float* B, float* P, const void* zero, in
   a.npix = M;
   a.n_oc_tiles = N / 64;
   a.n_pix_tiles = (M + p.BN - 1) / p.BN;
-  a.splits = nb;
-  a.kps = Kd / kKS<float>;
-  return nb > 1 ? dispatch2<float, 0, false>(p, a, st) : -2;
+  a.splits = nb * s2;
+  a.kps = Kd / kKS<float> / s2;
+  return nb * s2 > 1 ? dispatch2<float, 0, false>(p, a, st) : -2;
+}
+
+int psx_bgemm_f32(const float* A, const float* B, float* P, const void* zero, int M, int N, int Kd, int nb, int cfg,
+                  hipStream_t st) {
+  return psx_bgemm_f32_split(A, B, P, zero, M, N, Kd, nb, 1, cfg, st);
 }
 
 }  // extern "C"

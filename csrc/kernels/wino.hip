@@ -36,8 +36,8 @@
 #include "common.hpp"
 #include "wino.hpp"
 
-extern "C" int psx_bgemm_f32(const float* A, const float* B, float* P, const void* zero, int M, int N, int Kd, int nb,
-                             int cfg, hipStream_t st);
+extern "C" int psx_bgemm_f32_split(const float* A, const float* B, float* P, const void* zero, int M, int N, int Kd,
+                                   int nb, int s2, int cfg, hipStream_t st);
 extern "C" int psx_wino_wout(const float* part, void* out, int out_fp16, float scale, int K, int C, int q,
                              hipStream_t st);
 extern "C" int psx_bgemm_tn_f32(const float* X, const float* D, float* part, const void* zero, int T, int C, int K,
@@ -338,7 +338,7 @@ template <bool RES, bool BWD, bool MAFF, bool TWO>
 __global__ __launch_bounds__(384) void wino_out_xf_kernel(const float* __restrict__ P, float* __restrict__ y,
                                                           const float* __restrict__ res, float* __restrict__ stats,
                                                           int T, int H, int W, int K, WinoBwdStats bs, DetRed det,
-                                                          const float* __restrict__ sshift) {
+                                                          const float* __restrict__ sshift, int nsplit) {
   __shared__ float xf[2][6][4][64];
   __shared__ float red[3][4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -361,10 +361,20 @@ __global__ __launch_bounds__(384) void wino_out_xf_kernel(const float* __restric
   }
   const float kshift = (!bwd && sshift) ? sshift[k] : 0.f;  // forward statistics: shifted sums
   float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  // P holds nsplit partial slabs per point (the GEMM's reduction split, psx_wino_conv): summed here
   auto load = [&](int t, float (&m)[6]) {
-    const float* pt = P + (size_t)t * K + k + (size_t)(wv * 6) * bstride;
+    const float* pt = P + (size_t)t * K + k + (size_t)(wv * 6) * nsplit * bstride;
+    if (nsplit == 1) {
 #pragma unroll
-    for (int s = 0; s < 6; ++s) m[s] = pt[s * bstride];
+      for (int s = 0; s < 6; ++s) m[s] = pt[s * bstride];
+      return;
+    }
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      float v = pt[(size_t)s * nsplit * bstride];
+      for (int j = 1; j < nsplit; ++j) v += pt[((size_t)s * nsplit + j) * bstride];
+      m[s] = v;
+    }
   };
   int t = blockIdx.y;
   float m[6];
@@ -518,6 +528,25 @@ static long wino_tiles(int N, int H, int W) { return (long)N * ((H + 3) / 4) * (
 
 long psx_wino_v_floats(int N, int H, int W, int C) { return wino_tiles(N, H, W) * 36 * C; }
 
+// Reduction split s2 of the 36 GEMMs (PSX_TUNE wino_s2=N, default 1): each point's C-long
+// reduction runs as s2 workgroup ranges writing s2 partial slabs of P, summed by the output
+// transform — more, shorter workgroups for the 4x4x512 / 8x8x256 points (576 / 1152 workgroups of
+// 64x64 at 3 per CU leave the last round a quarter / half full).
+static int wino_gemm_split(int T, int C, int K) {
+  (void)T;
+  (void)K;
+  int s2 = 1;
+  if (const char* e = tune("wino_s2"); e && atoi(e) > 0) s2 = atoi(e);
+  while (s2 > 1 && (C / 32) % s2) s2 >>= 1;  // whole k-steps (32 fp32 channels) per range
+  return s2;
+}
+
+// floats of the GEMM output P of psx_wino_conv (36 x T x K x the reduction split)
+long psx_wino_p_floats(int N, int H, int W, int C, int K) {
+  const long T = wino_tiles(N, H, W);
+  return 36 * T * K * wino_gemm_split((int)T, C, K);
+}
+
 long psx_wino_workspace(int N, int H, int W, int C, int K) {
   return psx_wino_v_floats(N, H, W, C) + psx_wino_v_floats(N, H, W, K);
 }
@@ -579,7 +608,8 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
   // 8x8x256 40.6 vs 33.7 us, profiles/r4_sk_gemm_probes.jsonl; the GEMM with the output transform
   // in its epilogue, 64 output registers per accumulator forcing 16x16 wave tiles: neutral where
   // it had >= 256 workgroups, 1.8x slower elsewhere, profiles/r4_numbers.jsonl r4_call16.)
-  int e = psx_bgemm_f32(V, U, P, zero, T, K, C, 36, cfg, st);
+  const int s2 = wino_gemm_split(T, C, K);
+  int e = psx_bgemm_f32_split(V, U, P, zero, T, K, C, 36, s2, cfg, st);
   if (e) return e;
   WinoBwdStats bs{};
   if (bst) bs = *bst;
@@ -587,7 +617,7 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
   DetRed det{};
   if (bst || stats) det = det_for(bst ? bst->part : stats);
   using OutK = void (*)(const float*, float*, const float*, float*, int, int, int, int, WinoBwdStats, DetRed,
-                       const float*);
+                       const float*, int);
   // [res][variant]: forward, backward (ReLU mask from o / from the affine) x (one / two BN sums)
   static const OutK kOutXf[2][5] = {
       {wino_out_xf_kernel<false, false, false, false>, wino_out_xf_kernel<false, true, false, false>,
@@ -598,7 +628,7 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
        wino_out_xf_kernel<true, true, true, true>}};
   const int var = bst ? 1 + 2 * (bs.mask_aff != nullptr) + (bs.y2 != nullptr) : 0;
   hipLaunchKernelGGL(kOutXf[res != nullptr][var], dim3(K / 64, gyo), dim3(64 * kXfWaves), 0, st, P, y, res,
-                     bst ? nullptr : stats, T, H, W, K, bs, det, sshift);
+                     bst ? nullptr : stats, T, H, W, K, bs, det, sshift, s2);
   return (int)hipGetLastError();
 }
 

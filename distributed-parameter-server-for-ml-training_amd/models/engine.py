@@ -451,7 +451,8 @@ class HipResNetEngine:
                     or not K.wino_ok(cs.h, cs.w, cs.cp, cs.cout)):
                 continue
             vk, vc = K.wino_v_floats(B, cs.h, cs.w, cs.cout), K.wino_v_floats(B, cs.h, cs.w, cs.cp)
-            s_main = max(s_main, vk, vc)
+            s_main = max(s_main, vk, vc, K.wino_p_floats(B, cs.h, cs.w, cs.cp, cs.cout),
+                         K.wino_p_floats(B, cs.h, cs.w, cs.cout, cs.cp))
             q = K.wino_wgrad_q(B, cs.h, cs.w, cs.cp, cs.cout) if wg and max(cs.h, cs.w) <= wg_maxhw else 0
             # fused single-launch kernel (wino_fused.hip) where it applies, per direction
             ff = fuse and K.wino_fused_ok(B, cs.h, cs.w, cs.cp, cs.cout)

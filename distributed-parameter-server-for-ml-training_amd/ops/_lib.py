@@ -61,6 +61,7 @@ _KERNEL_SIGS = {
     "psx_wino_fused": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
     "psx_wino_conv": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp]),
     "psx_wino_v_floats": (i64, [i32, i32, i32, i32]),
+    "psx_wino_p_floats": (i64, [i32, i32, i32, i32, i32]),
     "psx_wino_wgrad_q": (i32, [i32, i32, i32, i32, i32]),
     "psx_wino_wgrad": (i32, [vp, vp, vp, vp, vp, i32, f32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
     "psx_bgemm_tn_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),

@@ -212,6 +212,11 @@ def wino_v_floats(nb, h, w, c) -> int:
     return int(kernels().psx_wino_v_floats(nb, h, w, c))
 
 
+def wino_p_floats(nb, h, w, c, k) -> int:
+    """Floats of wino_conv's GEMM output P (36 x T x k x its reduction split; c = input channels)."""
+    return int(kernels().psx_wino_p_floats(nb, h, w, c, k))
+
+
 def wino_workspace_floats(nb, h, w, c, k) -> int:
     return int(kernels().psx_wino_workspace(nb, h, w, c, k))
 
@@ -296,7 +301,7 @@ def wino_conv(x, u, y, res, stats, v, p, nb, h, w, c, k, cfg=None, bst: "BwdStat
     (the BnFin's affine / saved / running statistics are written by the launch)."""
     assert x.dtype == torch.float32 and y.dtype == torch.float32
     assert x.numel() == nb * h * w * c and y.numel() == nb * h * w * k and u.numel() >= 36 * k * c
-    assert v.numel() >= wino_v_floats(nb, h, w, c) and p.numel() >= wino_v_floats(nb, h, w, k)
+    assert v.numel() >= wino_v_floats(nb, h, w, c) and p.numel() >= wino_p_floats(nb, h, w, c, k)
     assert res is None or res.numel() == y.numel()
     check(kernels().psx_wino_conv(ptr(x), ptr(u), ptr(y), ptr(res), ptr(stats), ptr(v), ptr(p), ptr(zero_page(x.device)),
                                   nb, h, w, c, k, WINO_CFG if cfg is None else cfg,

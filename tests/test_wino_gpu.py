@@ -65,9 +65,12 @@ def _nhwc(t):
                                           # partial edge tiles (ResNet-50's 14x14 / 7x7 stages, odd sizes)
                                           (2, 14, 256, 256, True), (3, 7, 512, 512, False), (2, 5, 64, 128, True),
                                           (2, 10, 128, 64, False)])
-def test_wino_fwd(nb, h, c, k, res):
-    """The input transform, the 36 batched GEMMs and the output transform (+ residual, + BN slot
-    sums of y) against float64."""
+@pytest.mark.parametrize("s2", [1, 4])
+def test_wino_fwd(nb, h, c, k, res, s2, monkeypatch):
+    """The input transform, the 36 batched GEMMs (s2: the reduction split, partial slabs summed
+    by the output transform) and the output transform (+ residual, + BN slot sums of y) against
+    float64."""
+    monkeypatch.setenv("PSX_TUNE", f"wino_s2={s2}")
     torch.manual_seed(nb * h + c)
     x = torch.relu(torch.randn(nb, c, h, h, device=DEV, dtype=torch.float64))
     w = torch.randn(k, c, 3, 3, device=DEV, dtype=torch.float64) * (2.0 / (9 * c)) ** 0.5
@@ -78,7 +81,7 @@ def test_wino_fwd(nb, h, c, k, res):
     y = torch.full((nb, h, h, k), float("nan"), device=DEV)
     stats = torch.zeros(K.STAT_SLOTS, 2, k, device=DEV)
     v = torch.empty(K.wino_v_floats(nb, h, h, c), device=DEV)
-    p = torch.empty(K.wino_v_floats(nb, h, h, k), device=DEV)
+    p = torch.empty(K.wino_p_floats(nb, h, h, c, k), device=DEV)
     K.wino_conv(_nhwc(x.float()), u, y, _nhwc(r.float()) if res else None, stats, v, p, nb, h, h, c, k)
     torch.cuda.synchronize()
     refn = _nhwc(ref)
@@ -100,7 +103,7 @@ def test_wino_dgrad(nb, h, c, k):
     K.wino_weights(w.float().contiguous(), u, k, c, flip=True)
     dx = torch.full((nb, h, h, c), float("nan"), device=DEV)
     v = torch.empty(K.wino_v_floats(nb, h, h, k), device=DEV)
-    p = torch.empty(K.wino_v_floats(nb, h, h, c), device=DEV)
+    p = torch.empty(K.wino_p_floats(nb, h, h, k, c), device=DEV)
     K.wino_conv(_nhwc(dy.float()), u, dx, None, None, v, p, nb, h, h, k, c)
     torch.cuda.synchronize()
     assert _rel(dx, _nhwc(ref)) < TOL

@@ -78,7 +78,8 @@ def main():
             wc = w.contiguous()
             K.WinoWeightBatch([(wc, u, cout, cp, False, int(K.wino_fused_ok(B, hw, hw, cp, cout))),
                                (wc, ud, cout, cp, True, int(K.wino_fused_ok(B, hw, hw, cout, cp)))])()
-            nv = max(K.wino_v_floats(B, hw, hw, cp), K.wino_v_floats(B, hw, hw, cout))
+            nv = max(K.wino_v_floats(B, hw, hw, cp), K.wino_v_floats(B, hw, hw, cout), K.wino_p_floats(B, hw, hw, cp, cout),
+                     K.wino_p_floats(B, hw, hw, cout, cp))
             v1, v2 = torch.empty(nv, device="cuda"), torch.empty(nv, device="cuda")
             if K.wino_fused_ok(B, hw, hw, cp, cout):
                 r["path"] = "wino_fused"

@@ -45,7 +45,7 @@ def main():
         uf, ufd = (torch.empty(40 * c * c, device="cuda") for _ in range(2))
         K.WinoWeightBatch([(w, u, c, c, False, 0), (w, ud, c, c, True, 0), (w, uf, c, c, False, 1),
                            (w, ufd, c, c, True, 1)])()
-        nv = K.wino_v_floats(B, hw, hw, c)
+        nv = max(K.wino_v_floats(B, hw, hw, c), K.wino_p_floats(B, hw, hw, c, c))
         v1, v2 = torch.empty(nv, device="cuda"), torch.empty(nv, device="cuda")
         y, y2 = torch.empty(B, hw, hw, c, device="cuda"), torch.empty(B, hw, hw, c, device="cuda")
         dx = torch.empty(B, hw, hw, c, device="cuda")

@@ -36,6 +36,10 @@
 #ifndef PSX_TAPR_BF16_256
 #define PSX_TAPR_BF16_256 1
 #endif
+// epilogue rows whose global loads are issued together (A/B builds: -D PSX_EPI_U=1)
+#ifndef PSX_EPI_U
+#define PSX_EPI_U 4
+#endif
 #ifndef PSX_TAPR_F32_128
 #define PSX_TAPR_F32_128 1
 #endif
@@ -587,55 +591,78 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
         }
       }
     }
-    for (int pr = tid / CPR; pr < BN; pr += RPP) {
-      const int pix = pix0 + pr;
-      if (pix >= npix_c) break;
-      const float* src = Ts + pr * TS + cc * 8;
-      const f32x4 va = *reinterpret_cast<const f32x4*>(src), vb = *reinterpret_cast<const f32x4*>(src + 4);
-      float v[8] = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
-      size_t opix = (size_t)pix;
-      if (MODE == 3) {  // class-local (n, i, j) -> dx (n, 2i+py, 2j+px)
-        const int nn = pix / (CH * CW), rem = pix - nn * CH * CW, ii = rem / CW, jj = rem - ii * CW;
-        opix = ((size_t)nn * a.OH + 2 * ii + py) * a.OW + 2 * jj + px;
-      }
-      const size_t off = opix * a.OC + ch0;
-      if (HAS_RES) {
-        float rr[8];
-        ld8((const T*)a.res + off, rr);
+    // The pixel rows of a thread in chunks of U: every global load of a chunk (residual, the
+    // BN-backward operands o / y) is issued before the first is used, so a workgroup pays one
+    // memory round trip per chunk instead of one per row (a 1x1 layer with one or two k-steps is
+    // all epilogue: ResNet-50's 64 -> 256 forward / 256 -> 64 data gradient at 56x56 ran 3-5x
+    // slower than their HBM bytes with the row loop serialised on its loads).
+    constexpr int NIT = BN / RPP;
+    constexpr int UMAX = MODE == 3 ? (PSX_EPI_U < 2 ? PSX_EPI_U : 2) : PSX_EPI_U;  // MODE 3: 4 spills
+    constexpr int U = NIT < UMAX ? NIT : UMAX;
+    static_assert(NIT % U == 0, "whole chunks");
+    const int pr0 = tid / CPR;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] += rr[k];
-      }
-      if (!bwd) st8((T*)a.out + off, v);  // v = the stored values from here on
-      if (st) {
+    for (int it0 = 0; it0 < NIT; it0 += U) {
+      size_t offs[U];
+      bool ok[U];
+      float rr[U][8], om[U][8], yv[U][8], y2v[U][8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float d = v[k] - ksh[k];
-          s1[k] += d;
-          s2[k] += d * d;
+      for (int u = 0; u < U; ++u) {
+        const int pix = pix0 + pr0 + (it0 + u) * RPP;
+        ok[u] = pix < npix_c;
+        const int pp = ok[u] ? pix : pix0;  // an in-range stand-in row: loaded, never stored
+        size_t opix = (size_t)pp;
+        if (MODE == 3) {  // class-local (n, i, j) -> dx (n, 2i+py, 2j+px)
+          const int nn = pp / (CH * CW), rem = pp - nn * CH * CW, ii = rem / CW, jj = rem - ii * CW;
+          opix = ((size_t)nn * a.OH + 2 * ii + py) * a.OW + 2 * jj + px;
+        }
+        offs[u] = opix * a.OC + ch0;
+        if (HAS_RES) ld8((const T*)a.res + offs[u], rr[u]);
+        if (bwd) {
+          ld8((const T*)a.bo + offs[u], om[u]);
+          ld8((const T*)a.by1 + offs[u], yv[u]);
+          if (two) ld8((const T*)a.by2 + offs[u], y2v[u]);
         }
       }
-      if (bwd) {
-        float om[8], yv[8], y2v[8];
-        if constexpr (sizeof(T) == 2) {  // bf16: the stored (rounded) g feeds the sums
 #pragma unroll
-          for (int i = 0; i < 8; ++i) v[i] = bf2f(f2bf(v[i]));
-        }
-        ld8((const T*)a.bo + off, om);
-        ld8((const T*)a.by1 + off, yv);
-        if (two) ld8((const T*)a.by2 + off, y2v);
-        float dzv[8];
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        const float* src = Ts + (pr0 + (it0 + u) * RPP) * TS + cc * 8;
+        const f32x4 va = *reinterpret_cast<const f32x4*>(src), vb = *reinterpret_cast<const f32x4*>(src + 4);
+        float v[8] = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
+        const size_t off = offs[u];
+        if (HAS_RES) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float dz = om[i] > 0.f ? v[i] : 0.f;
-          dzv[i] = dz;
-          s1[i] += dz;
-          s2[i] += dz * (yv[i] - bm1[i]) * bi1[i];
-          if (two) s3[i] += dz * (y2v[i] - bm2[i]) * bi2[i];
+          for (int k = 0; k < 8; ++k) v[k] += rr[u][k];
         }
-        if (a.bmask)
-          st8((T*)a.out + off, dzv);
-        else
-          st8((T*)a.out + off, v);
+        if (!bwd) st8((T*)a.out + off, v);  // v = the stored values from here on
+        if (st) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float d = v[k] - ksh[k];
+            s1[k] += d;
+            s2[k] += d * d;
+          }
+        }
+        if (bwd) {
+          if constexpr (sizeof(T) == 2) {  // bf16: the stored (rounded) g feeds the sums
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = bf2f(f2bf(v[i]));
+          }
+          float dzv[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float dz = om[u][i] > 0.f ? v[i] : 0.f;
+            dzv[i] = dz;
+            s1[i] += dz;
+            s2[i] += dz * (yv[u][i] - bm1[i]) * bi1[i];
+            if (two) s3[i] += dz * (y2v[u][i] - bm2[i]) * bi2[i];
+          }
+          if (a.bmask)
+            st8((T*)a.out + off, dzv);
+          else
+            st8((T*)a.out + off, v);
+        }
       }
     }
     if (!st && !bwd) return;

@@ -75,7 +75,7 @@ def test_wino_fused_fwd(nb, h, c, k, res, vout):
     assert torch.allclose(s[1], (ref ** 2).sum((0, 1, 2)), rtol=1e-4)
     if vout:  # the same B^T d B as the separate input transform (wino_conv's V)
         v0 = torch.empty_like(v)
-        p0 = torch.empty(K.wino_v_floats(nb, h, h, k), device=DEV)
+        p0 = torch.empty(K.wino_p_floats(nb, h, h, c, k), device=DEV)
         y0 = torch.empty_like(y)
         K.wino_conv(xs, u0, y0, rs, None, v0, p0, nb, h, h, c, k)
         torch.cuda.synchronize()
@@ -160,7 +160,7 @@ def test_wino_fused_bn_in_fold():
             K.wino_fused(z, uf, y, None, stats, None, nb, h, h, c, k, bn_in=(sl, fin))
         else:
             v = torch.empty(K.wino_v_floats(nb, h, h, c), device=DEV)
-            p = torch.empty(K.wino_v_floats(nb, h, h, k), device=DEV)
+            p = torch.empty(K.wino_p_floats(nb, h, h, c, k), device=DEV)
             K.wino_conv(z, u0, y, None, stats, v, p, nb, h, h, c, k, bn_in=(sl, fin))
         torch.cuda.synchronize()
         out[path] = (y.clone(), stats.sum(0), {n: t[n].clone() for n in ("affine", "saved", "rm", "rv", "ssh_next")})

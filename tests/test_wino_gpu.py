@@ -125,7 +125,7 @@ def test_wino_wgrad(nb, h, c, k, fp16):
     K.wino_weights(w.float().contiguous(), u, k, c)
     y = torch.empty(nb, h, h, k, device=DEV)
     v = torch.empty(K.wino_v_floats(nb, h, h, c), device=DEV)
-    p = torch.empty(K.wino_v_floats(nb, h, h, k), device=DEV)
+    p = torch.empty(K.wino_p_floats(nb, h, h, c, k), device=DEV)
     K.wino_conv(_nhwc(x.float()), u, y, None, None, v, p, nb, h, h, c, k)  # leaves V for the wgrad
     q = K.wino_wgrad_q(nb, h, h, c, k)
     assert q >= 1
@@ -225,7 +225,7 @@ def test_wino_dgrad_fused_bn_bwd_sums(two, mask_store, res, h):
     K.wino_weights(w, u, k, c, flip=True)
     dx = torch.empty(nb, h, h, c, device=DEV)
     v = torch.empty(K.wino_v_floats(nb, h, h, k), device=DEV)
-    p = torch.empty(K.wino_v_floats(nb, h, h, c), device=DEV)
+    p = torch.empty(K.wino_p_floats(nb, h, h, k, c), device=DEV)
     K.wino_conv(dy, u, dx, r, None, v, p, nb, h, h, k, c, bst=bst)
     torch.cuda.synchronize()
     g = torch.nn.grad.conv2d_input((nb, c, h, h), w.double(), dy.double().permute(0, 3, 1, 2), padding=1)

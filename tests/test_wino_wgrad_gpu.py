@@ -108,7 +108,7 @@ def test_wgrad_fused_matches_three_launch_path():
     u = torch.empty(36 * k * c, device=DEV)
     K.wino_weights(w, u, k, c)
     v = torch.empty(K.wino_v_floats(nb, h, h, c), device=DEV)
-    p = torch.empty(K.wino_v_floats(nb, h, h, k), device=DEV)
+    p = torch.empty(K.wino_p_floats(nb, h, h, c, k), device=DEV)
     K.wino_conv(x, u, torch.empty(nb, h, h, k, device=DEV), None, None, v, p, nb, h, h, c, k)
     q = K.wino_wgrad_q(nb, h, h, c, k)
     d = torch.empty(K.wino_v_floats(nb, h, h, k), device=DEV)

@@ -862,7 +862,15 @@ void with_det(Conv2Args& b, int rows) {
 
 template <typename T, int BM, int BN, int MODE, bool RES, bool SPLIT, int WGM = 2>
 int launch2(const Conv2Args& a, hipStream_t st) {
-  const size_t lds = (size_t)3 * (BM + BN) * 128;
+  // LDS: the ring's stages in use (a 1x1 layer with one or two k-steps needs one or two of the
+  // three) or the staged epilogue tile, whichever is larger — the short-reduction layers (the
+  // 64-channel 1x1s of ResNet-50) then fit more workgroups per CU, so one's epilogue stores
+  // overlap another's loads (a 128x128 bf16 tile: 96 -> 67.6 KB, 1 -> 2 per CU; measured neutral on
+  // the ResNet-50 step, r5_call13, kept as the tighter bound)
+  const int nk_max = SPLIT ? a.kps : (MODE == 3 ? 3 : a.Kg / kKS<T>);
+  const int stages = nk_max < 3 ? (nk_max < 1 ? 1 : nk_max) : 3;
+  const size_t ring = (size_t)stages * (BM + BN) * 128, epi = (size_t)BN * (BM + 4) * 4;
+  const size_t lds = SPLIT ? ring : (ring > epi ? ring : epi);
   dim3 grid(a.n_oc_tiles * a.n_pix_tiles, SPLIT ? a.splits : (MODE == 3 ? 4 : 1));
   Conv2Args b = a;
   if (!SPLIT) with_det(b, a.n_pix_tiles * (MODE == 3 ? 4 : 1));

@@ -826,16 +826,23 @@ struct Plan {
 // >= 8 k-steps. fp32 (f32 = true): MFMA-bound (1/16 of the bf16 rate), so 128-row tiles (one
 // 96 KiB workgroup per CU) are not used and the split-K target is the same workgroup count at
 // twice the k-steps of a bf16 layer.
+// Round 5 sweep (bench/r50_tiles.py, profiles/r5_r50_conv_tiles.jsonl, ResNet-50's 1x1 / strided
+// layers, B = 128): bf16 128x128 tiles lose to 64x128 on every layer (by up to 1.4x: one 96 KB
+// workgroup per CU), fp32 64x64 beats 64x128 on most (the data gradients by 3-9 %). Steps, same box
+// (r5_call15): ResNet-50 bf16 19.33 -> 17.35 ms, fp32 36.89 -> 36.06; the fp32 64x64 choice costs
+// ResNet-18 +0.2 % (its power-of-two 32x32 / 16x16 layers, tuned on 64x128 in round 2,
+// bench/conv_sweep.py), so fp32 layers with a power-of-two pixel count keep 64x128. PSX_TUNE
+// cv_plan=r4 keeps the round-4 choice (128x128 bf16 / 64x128 fp32 on the large layers).
 Plan plan_for(int OC, int npix, int ksteps, bool f32 = false) {
   Plan p{64, 128, 1};
-  static const bool f32_128 = [] {  // fp32 128 x 128 tiles: opt-in while measured (bench/f32_tiles.py)
-    const char* e = tune("cv_f32_128");
-    return e && e[0] == '1';
+  static const bool r4 = [] {
+    const char* e = tune("cv_plan");
+    return e && !strcmp(e, "r4");
   }();
-  if ((!f32 || f32_128) && OC % 128 == 0 && (long)(OC / 128) * ((npix + 127) / 128) >= (f32 ? 256 : 512)) {
+  if (r4 && !f32 && OC % 128 == 0 && (long)(OC / 128) * ((npix + 127) / 128) >= 512) {
     p.BM = 128;
     p.BN = 128;
-  } else if ((long)(OC / 64) * ((npix + 127) / 128) >= 512) {
+  } else if ((!f32 || r4 || !(npix & (npix - 1))) && (long)(OC / 64) * ((npix + 127) / 128) >= 512) {
     p.BM = 64;
     p.BN = 128;
   } else {
@@ -849,7 +856,7 @@ Plan plan_for(int OC, int npix, int ksteps, bool f32 = false) {
   if (const char* e = tune("cv_bn")) p.BN = atoi(e);
   if (const char* e = tune("cv_splits")) p.splits = atoi(e);
   if (const char* e = tune("cv_wgm")) p.WGM = atoi(e);
-  if (OC % p.BM || (f32 && p.BM == 128 && !f32_128 && !tune("cv_bm"))) p.BM = 64;
+  if (OC % p.BM || (f32 && p.BM == 128 && !tune("cv_bm"))) p.BM = 64;
   if (p.splits > ksteps) p.splits = ksteps;
   return p;
 }

@@ -686,7 +686,8 @@ constexpr int wlds(int BR, int BC, int NS) { return NS * 64 * (BR + BC) * 2; }
 // the tile shapes the one with the lowest modelled time wins (per-step costs measured on
 // MI355X with rocprofv3: 128x128 ~1.2 us at 1 WG/CU, 64x64 ~0.7 us at 3 WG/CU; +3 us
 // prologue/epilogue per workgroup; split-K partials cost a write + a read at ~5 TB/s).
-WPlan wplan(int OC, int Kg, int npix) {
+// fbr / fbc (> 0): only that tile (its split count still from the model).
+WPlan wplan(int OC, int Kg, int npix, int fbr = 0, int fbc = 0) {
   WPlan best{64, 64, 3, 1, 0};
   double best_t = 1e30;
   const int steps = (npix + 63) / 64;
@@ -694,6 +695,7 @@ WPlan wplan(int OC, int Kg, int npix) {
   for (int ib = 0; ib < 2; ++ib)
     for (int ic = 0; ic < 2; ++ic) {
       const int BR = brs[ib], BC = bcs[ic];
+      if ((fbr && BR != fbr) || (fbc && BC != fbc)) continue;
       if (Kg % BR || OC % BC || (BR == 128 && Kg < 256)) continue;
       const int NS = (BR == 128 && BC == 128) ? 4 : 3;
       int occ = 163840 / wlds(BR, BC, NS);
@@ -1002,7 +1004,16 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
                       : (p.NS == 6 ? launch_w3<64, 6, true>(b, st) : launch_w3<64, 3, true>(b, st));
     return e ? -e : p.splits;
   }
-  WPlan p = wplan(OC, Kg, a.npix);
+  // Tile: the round-5 sweep (bench/r50_wgrad_tiles.py, profiles/r5_r50_wgrad_tiles.jsonl, ResNet-50's
+  // 1x1 layers): 64 (k) x 128 (oc) wins by 10-20 % on every layer up to 28x28 with OC % 128 == 0
+  // (128x512x28 42.0 -> 34.7 us, 1024x2048x14/s2 64.3 -> 55.4), 64x64 on the 56x56 ones (the
+  // model's choice there); PSX_TUNE wg_plan=model: the cost model alone (round 4).
+  static const bool model_only = [] {
+    const char* e = tune("wg_plan");
+    return e && !strcmp(e, "model");
+  }();
+  const bool t128 = !model_only && OC % 128 == 0 && Kg % 64 == 0 && a.npix <= 128 * 28 * 28;
+  WPlan p = t128 ? wplan(OC, Kg, a.npix, 64, 128) : wplan(OC, Kg, a.npix);
   // experiment overrides (tile sweep): PSX_TUNE wg_br / PSX_TUNE wg_bc / PSX_TUNE wg_splits
   if (const char* e = tune("wg_br")) p.BR = atoi(e);
   if (const char* e = tune("wg_bc")) p.BC = atoi(e);

@@ -54,6 +54,7 @@ def main():
         ws = torch.empty(max(n1, n2, 4) // 4, device="cuda")
         r = {"cin": cin, "cout": cout, "hw": hw}
         fwd = t_us(lambda: K.conv_fwd2(xh, wf, y, stats, ws, B, hw, hw, cp, cout, 1, 1, 0, kg))
+        fwd_ns = t_us(lambda: K.conv_fwd2(xh, wf, y, None, ws, B, hw, hw, cp, cout, 1, 1, 0, kg))
         dg = t_us(lambda: K.conv_dgrad2(dy, wd, dx, res, ws, B, hw, hw, cp, cout, 1, 1, 0, kgd))
         a2 = xh.view(npix, cp)
         wm = wf.view(cout, -1)[:, :cp].contiguous().t().contiguous()  # [cin][cout]
@@ -67,7 +68,7 @@ def main():
         by = 2
         floor_f = (npix * cin + npix * cout) * by / 5.0e6  # us at 5 TB/s
         floor_d = (npix * cout + 2 * npix * cin) * by / 5.0e6
-        r.update({"psx_fwd_us": round(fwd, 1), "psx_fwd_tbs": round((npix * (cin + cout) * by) / fwd / 1e6, 2),
+        r.update({"psx_fwd_us": round(fwd, 1), "psx_fwd_nostats_us": round(fwd_ns, 1), "psx_fwd_tbs": round((npix * (cin + cout) * by) / fwd / 1e6, 2),
                   "hipblaslt_fwd_us": round(mm_f, 1), "torch_stats_pass_us": round(st_f, 1),
                   "psx_dgrad_res_us": round(dg, 1), "hipblaslt_dgrad_us": round(mm_d, 1),
                   "floor_fwd_us": round(floor_f, 1), "floor_dgrad_res_us": round(floor_d, 1)})

@@ -68,16 +68,26 @@ static inline const char* tune(const char* key) {
 PSX_DEV float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
 // Round-to-nearest-even f32 -> bf16 (NaN preserved as quiet NaN).
+// fp32 -> bf16, round to nearest even: gfx950's v_cvt_pk_bf16_f32 (one instruction per pair; the
+// integer-arithmetic rounding it replaces was ~7 VALU per value, a third of the bf16 conv epilogue)
+// (A/B builds: -D PSX_SW_BF16 keeps the integer version)
+#ifdef PSX_SW_BF16
 PSX_DEV uint16_t f2bf(float f) {
   uint32_t u = __float_as_uint(f);
   if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
   u += 0x7fffu + ((u >> 16) & 1u);
   return (uint16_t)(u >> 16);
 }
+PSX_DEV uint32_t pack_bf2(float lo, float hi) { return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16); }
+#else
+typedef __bf16 psx_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float psx_f32x2 __attribute__((ext_vector_type(2)));
+PSX_DEV uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 
 PSX_DEV uint32_t pack_bf2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((psx_f32x2){lo, hi}, psx_bf16x2));
 }
+#endif
 
 PSX_DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 PSX_DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }

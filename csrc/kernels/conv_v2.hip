@@ -357,6 +357,13 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
   }
   int nbase[LB], hb[LB], wb[LB], bc[LB];
   bool pv[LB];
+  // a pure GEMM needs no (n, oh, ow) decomposition: two integer divisions (~70 VALU) per staged
+  // row, which a one- or two-k-step 1x1 layer otherwise pays as much as its whole epilogue
+#ifdef PSX_NO_GEMM1X1  // A/B builds
+  const bool gemm1x1 = false;
+#else
+  const bool gemm1x1 = (MODE == 0 || MODE == 1) && a.R == 1 && a.S == 1 && a.stride == 1 && a.pad == 0;
+#endif
 #pragma unroll
   for (int i = 0; i < LB; ++i) {
     const int row = (i * 4 + wid) * 8 + lrow;
@@ -364,6 +371,11 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     const int pix = pix0 + row;
     pv[i] = pix < npix_c;
     const int pp = pv[i] ? pix : 0;
+    if (gemm1x1) {  // 1x1 / stride 1 / no padding: the gathered operand is the plain [npix][IC] matrix
+      nbase[i] = pp;
+      hb[i] = wb[i] = 0;  // (the bounds checks of tap (0, 0) always pass)
+      continue;
+    }
     const int pw = MODE == 3 ? CW : a.OW;
     const int ohw = (MODE == 3 ? CH : a.OH) * pw;
     const int n = pp / ohw, rem = pp - n * ohw;

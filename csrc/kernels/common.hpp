@@ -71,6 +71,8 @@ PSX_DEV float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 // fp32 -> bf16, round to nearest even: gfx950's v_cvt_pk_bf16_f32 (one instruction per pair; the
 // integer-arithmetic rounding it replaces was ~7 VALU per value, a third of the bf16 conv epilogue)
 // (A/B builds: -D PSX_SW_BF16 keeps the integer version)
+typedef __bf16 psx_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float psx_f32x2 __attribute__((ext_vector_type(2)));
 #ifdef PSX_SW_BF16
 PSX_DEV uint16_t f2bf(float f) {
   uint32_t u = __float_as_uint(f);
@@ -80,8 +82,6 @@ PSX_DEV uint16_t f2bf(float f) {
 }
 PSX_DEV uint32_t pack_bf2(float lo, float hi) { return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16); }
 #else
-typedef __bf16 psx_bf16x2 __attribute__((ext_vector_type(2)));
-typedef float psx_f32x2 __attribute__((ext_vector_type(2)));
 PSX_DEV uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 
 PSX_DEV uint32_t pack_bf2(float lo, float hi) {

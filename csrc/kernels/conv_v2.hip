@@ -648,12 +648,16 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
           for (int k = 0; k < 8; ++k) v[k] += rr[u][k];
         }
         if (!bwd) st8((T*)a.out + off, v);  // v = the stored values from here on
-        if (st) {
+        if (st) {  // packed f32 pairs (v_pk_add_f32 / v_pk_fma_f32): half the VALU of the sums
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const float d = v[k] - ksh[k];
-            s1[k] += d;
-            s2[k] += d * d;
+          for (int k = 0; k < 8; k += 2) {
+            const psx_f32x2 d = (psx_f32x2){v[k], v[k + 1]} - (psx_f32x2){ksh[k], ksh[k + 1]};
+            psx_f32x2 a1 = (psx_f32x2){s1[k], s1[k + 1]} + d;
+            psx_f32x2 a2 = __builtin_elementwise_fma(d, d, (psx_f32x2){s2[k], s2[k + 1]});
+            s1[k] = a1[0];
+            s1[k + 1] = a1[1];
+            s2[k] = a2[0];
+            s2[k + 1] = a2[1];
           }
         }
         if (bwd) {
@@ -678,23 +682,20 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       }
     }
     if (!st && !bwd) return;
-    // lanes of one wave that own the same channels differ in the lane bits >= log2(CPR)
-#pragma unroll
-    for (int sh = CPR; sh < 64; sh <<= 1)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        s1[i] += __shfl_xor(s1[i], sh, 64);
-        s2[i] += __shfl_xor(s2[i], sh, 64);
-        if (two) s3[i] += __shfl_xor(s3[i], sh, 64);
-      }
+    // per-channel sums over the RPP row groups through LDS: every thread writes its 8 channels'
+    // partials (16-byte stores), then one thread per (statistic, channel) adds the RPP of them in
+    // row-group order (cross-lane shuffles here cost 3 x 8 x 2-3 ds_bpermute per thread)
     __syncthreads();  // the staged tile is no longer read
-    float* red = Ts;  // [4 waves][3][BM]
-    if (lane < CPR) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        red[(wid * 3 + 0) * BM + cc * 8 + i] = s1[i];
-        red[(wid * 3 + 1) * BM + cc * 8 + i] = s2[i];
-        red[(wid * 3 + 2) * BM + cc * 8 + i] = s3[i];
+    float* red = Ts;  // [RPP][3][BM] (launch2 sizes the LDS for it)
+    {
+      float* rw = red + (size_t)pr0 * 3 * BM + cc * 8;
+      *reinterpret_cast<f32x4*>(rw) = (f32x4){s1[0], s1[1], s1[2], s1[3]};
+      *reinterpret_cast<f32x4*>(rw + 4) = (f32x4){s1[4], s1[5], s1[6], s1[7]};
+      *reinterpret_cast<f32x4*>(rw + BM) = (f32x4){s2[0], s2[1], s2[2], s2[3]};
+      *reinterpret_cast<f32x4*>(rw + BM + 4) = (f32x4){s2[4], s2[5], s2[6], s2[7]};
+      if (two) {
+        *reinterpret_cast<f32x4*>(rw + 2 * BM) = (f32x4){s3[0], s3[1], s3[2], s3[3]};
+        *reinterpret_cast<f32x4*>(rw + 2 * BM + 4) = (f32x4){s3[4], s3[5], s3[6], s3[7]};
       }
     }
     __syncthreads();
@@ -702,8 +703,9 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     float* dst = (bwd ? a.bpart : a.stats) + (size_t)(pix_t & (PSX_STAT_SLOTS - 1)) * nst * a.OC;
     for (int j = tid; j < nst * BM; j += 256) {
       const int which = j / BM, row = j - which * BM;
-      const float v = red[which * BM + row] + red[(3 + which) * BM + row] + red[(6 + which) * BM + row] +
-                      red[(9 + which) * BM + row];
+      float v = 0.f;
+#pragma unroll 8
+      for (int g = 0; g < RPP; ++g) v += red[((size_t)g * 3 + which) * BM + row];
       stat_add(a.det, dst, which * a.OC + oc0 + row, v);
     }
     if (st && a.fuse_fin && last_block_arrive(a.fin.counter, gridDim.x, smem))
@@ -889,7 +891,9 @@ int launch2(const Conv2Args& a, hipStream_t st) {
   const int nk_max = SPLIT ? a.kps : (MODE == 3 ? 3 : a.Kg / kKS<T>);
   const int stages = nk_max < 3 ? (nk_max < 1 ? 1 : nk_max) : 3;
   const size_t ring = (size_t)stages * (BM + BN) * 128, epi = (size_t)BN * (BM + 4) * 4;
-  const size_t lds = SPLIT ? ring : (ring > epi ? ring : epi);
+  const size_t red = (size_t)(256 / (BM / 8)) * 3 * BM * 4;  // the epilogue's statistic reduction
+  const size_t epr = epi > red ? epi : red;
+  const size_t lds = SPLIT ? ring : (ring > epr ? ring : epr);
   dim3 grid(a.n_oc_tiles * a.n_pix_tiles, SPLIT ? a.splits : (MODE == 3 ? 4 : 1));
   Conv2Args b = a;
   if (!SPLIT) with_det(b, a.n_pix_tiles * (MODE == 3 ? 4 : 1));

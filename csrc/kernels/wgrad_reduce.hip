@@ -117,22 +117,24 @@ PSX_DEV void wgrad_reduce2_tile(const float* __restrict__ part, int splits, int 
       const int tap = it / q, cq = it % q;
       const float4* src = reinterpret_cast<const float4*>(row + (size_t)tap * IC + cq * 4);
       const size_t st4 = slab / 4;
+      // 8 independent 16-byte loads in flight per thread: a 3x3 layer's workgroup (144 items, G = 1)
+      // walks all splits itself, and 4 per round trip left the batched reduction latency-bound
+      // (ResNet-50: 64-split 3x3 layers, 16 round trips per workgroup)
       int sp = g;
-      float4 a1 = s, a2 = s, a3 = s;
-      for (; sp + 3 * G < splits; sp += 4 * G) {
-        const float4 v0 = src[(size_t)sp * st4], v1 = src[(size_t)(sp + G) * st4];
-        const float4 v2 = src[(size_t)(sp + 2 * G) * st4], v3 = src[(size_t)(sp + 3 * G) * st4];
-        s.x += v0.x; s.y += v0.y; s.z += v0.z; s.w += v0.w;
-        a1.x += v1.x; a1.y += v1.y; a1.z += v1.z; a1.w += v1.w;
-        a2.x += v2.x; a2.y += v2.y; a2.z += v2.z; a2.w += v2.w;
-        a3.x += v3.x; a3.y += v3.y; a3.z += v3.z; a3.w += v3.w;
+      f32x4 acc8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc8[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      const f32x4* src4 = reinterpret_cast<const f32x4*>(src);
+      for (; sp + 7 * G < splits; sp += 8 * G) {
+        f32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = src4[(size_t)(sp + u * G) * st4];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc8[u] += v[u];
       }
-      for (; sp < splits; sp += G) {
-        const float4 v = src[(size_t)sp * st4];
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-      }
-      s.x += a1.x + a2.x + a3.x; s.y += a1.y + a2.y + a3.y;
-      s.z += a1.z + a2.z + a3.z; s.w += a1.w + a2.w + a3.w;
+      for (; sp < splits; sp += G) acc8[0] += src4[(size_t)sp * st4];
+      const f32x4 t4 = ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
+      s = make_float4(t4[0], t4[1], t4[2], t4[3]);
     }
     acc[threadIdx.x] = s;
     __syncthreads();

@@ -226,6 +226,102 @@ __global__ __launch_bounds__(512) void stem7_fwd_kernel(const float* __restrict_
   }
 }
 
+// bf16 ImageNet stem (ResNet-50 --dtype bf16): the same workgroup / wave layout and LDS patch as
+// stem7_fwd_kernel (a bf16 pixel of the 8-channel padded input is also 16 bytes), on
+// v_mfma_f32_16x16x32_bf16: one MFMA covers 4 taps x 8 channels, so a pixel tile is 13 MFMAs
+// (taps 49..51 read zero weights), lane l supplying the 8 channels of its pixel l & 15 at tap
+// 4 j + (l >> 4) — a per-lane patch offset fixed for the kernel. conv_v2 ran it as an implicit
+// GEMM with the per-lane im2col gather (one tap per 16-byte chunk): 291 us at batch 128
+// (profiles/r5_r50_bf16_kernels.txt); the output is the cost here (205 MB of bf16).
+__global__ __launch_bounds__(512) void stem7_fwd_bf16_kernel(const uint16_t* __restrict__ x,
+                                                             const uint16_t* __restrict__ wf, uint16_t* __restrict__ y,
+                                                             float* __restrict__ stats, const float* __restrict__ sshift,
+                                                             int Kg, int IH, int IW, DetRed det) {
+  __shared__ __attribute__((aligned(16))) u32x4 pt[kS7PR * 2 * kS7PW];  // [9 rows][parity][115] x 8 bf16
+  __shared__ float red[2][2][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int ri = w >> 2, m = w & 3;
+  const int n = blockIdx.x / (kS7W / kS7Rows), oh0 = (blockIdx.x % (kS7W / kS7Rows)) * kS7Rows;
+  const int j = lane & 15, g = lane >> 4;
+  // A fragments: output channel 16 m + j, taps 4 q + g (8 channels each); taps >= 49 are zero
+  u32x4 wa[13];
+  const uint16_t* wrow = wf + (size_t)(16 * m + j) * Kg;
+#pragma unroll
+  for (int q = 0; q < 13; ++q) {
+    const int tap = 4 * q + g;
+    wa[q] = tap < 49 ? *reinterpret_cast<const u32x4*>(wrow + tap * 8) : u32x4{0u, 0u, 0u, 0u};
+  }
+  // B fragment offsets (u32x4 units) of this lane's taps, pixel tile 0: row 2 ri + r, parity s & 1,
+  // column j + (s >> 1); the pixel tile t adds 16 t. Taps past 48 read a real pixel (zero weights)
+  int boff[13];
+#pragma unroll
+  for (int q = 0; q < 13; ++q) {
+    const int tap = min(4 * q + g, 48), r = tap / 7, sx = tap - r * 7;
+    boff[q] = ((2 * ri + r) * 2 + (sx & 1)) * kS7PW + (sx >> 1) + j;
+  }
+  const int ih0 = 2 * oh0 - 3;
+  for (int i = tid; i < kS7PR * 2 * kS7PW; i += 512) {
+    const int rr = i / (2 * kS7PW), pc = i - rr * (2 * kS7PW);
+    const int ih = ih0 + rr, iw = pc - 3;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if ((unsigned)ih < (unsigned)IH && (unsigned)iw < (unsigned)IW)
+      v = *reinterpret_cast<const u32x4*>(x + (((size_t)n * IH + ih) * IW + iw) * 8);
+    pt[(rr * 2 + (pc & 1)) * kS7PW + (pc >> 1)] = v;
+  }
+  __syncthreads();
+  f32x4 acc[7];
+#pragma unroll
+  for (int t = 0; t < 7; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 13; ++q) {
+    u32x4 b[7];
+#pragma unroll
+    for (int t = 0; t < 7; ++t) b[t] = pt[boff[q] + 16 * t];
+#pragma unroll
+    for (int t = 0; t < 7; ++t)
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wa[q]), __builtin_bit_cast(bf16x8, b[t]),
+                                                       acc[t], 0, 0, 0);
+  }
+  // lane: pixels ow = 16 t + j, channels oc = 16 m + 4 g + e; the sums are of the stored bf16 values
+  uint16_t* const yrow = y + (((size_t)n * kS7W + oh0 + ri) * kS7W) * 64 + 16 * m + 4 * g;
+  f32x4 k4 = {0.f, 0.f, 0.f, 0.f};
+  if (sshift) k4 = *reinterpret_cast<const f32x4*>(sshift + 16 * m + 4 * g);
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 7; ++t) {
+    const uint32_t lo = pack_bf2(acc[t][0], acc[t][1]), hi = pack_bf2(acc[t][2], acc[t][3]);
+    *reinterpret_cast<u32x2*>(yrow + (size_t)(16 * t + j) * 64) = u32x2{lo, hi};
+    const float v[4] = {lo_bf(lo), hi_bf(lo), lo_bf(hi), hi_bf(hi)};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[e] - k4[e];
+      s1[e] += d;
+      s2[e] += d * d;
+    }
+  }
+  if (!stats) return;
+#pragma unroll
+  for (int sh = 1; sh < 16; sh <<= 1)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s1[e] += __shfl_xor(s1[e], sh, 64);
+      s2[e] += __shfl_xor(s2[e], sh, 64);
+    }
+  if (j == 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[ri][0][16 * m + 4 * g + e] = s1[e];
+      red[ri][1][16 * m + 4 * g + e] = s2[e];
+    }
+  }
+  __syncthreads();
+  float* dst = stats + (size_t)(blockIdx.x & (PSX_STAT_SLOTS - 1)) * 2 * 64;
+  if (tid < 128) {
+    const int which = tid >> 6, oc = tid & 63;
+    stat_add(det, dst, tid, red[0][which][oc] + red[1][which][oc]);
+  }
+}
+
 // Weight gradient of the ImageNet stem (fp32): dW[oc][tap][c] = sum over output pixels of
 // dy[px][oc] * x[2 oh + r - 3][2 ow + s - 3][c], as the v_mfma_f32_16x16x4_f32 GEMM M = 64 output
 // channels x N = 196 (tap, channel) columns x K = pixels, 4 pixels per MFMA. A persistent grid of
@@ -357,18 +453,24 @@ int psx_stem_conv(const void* x, const void* wf, void* y, float* stats, const fl
 }
 
 
-// y = conv7x7/s2/p3(x, wf) of the ImageNet stem (3 -> 64 channels), fp32, + the BN statistics
-// [PSX_STAT_SLOTS][2][64] (nullable) of (y - sshift). x: NHWC [Nb][IH][IW][4] (cp = 4, channel 3
-// zero); wf: the conv_v2 forward weights [64][Kg], k = tap * 4 + c (tap = r * 7 + s), Kg >= 196.
+// y = conv7x7/s2/p3(x, wf) of the ImageNet stem (3 -> 64 channels), fp32 (f32) or bf16, + the BN
+// statistics [PSX_STAT_SLOTS][2][64] (nullable) of (y - sshift). x: NHWC [Nb][IH][IW][cp] (cp = 4
+// fp32 / 8 bf16 channels, the padding zero); wf: the conv_v2 forward weights [64][Kg],
+// k = tap * cp + c (tap = r * 7 + s), Kg >= 49 cp.
 // The output is 112 x 112 (IH = IW = 224). -11: not this shape (the caller runs psx_conv_fwd2).
-int psx_stem7_conv(const float* x, const float* wf, float* y, float* stats, const float* sshift, int Nb, int IH,
-                   int IW, int cin, int cp, int OC, int Kg, hipStream_t st) {
+int psx_stem7_conv(const void* x, const void* wf, void* y, float* stats, const float* sshift, int Nb, int IH,
+                   int IW, int cin, int cp, int OC, int Kg, int f32, hipStream_t st) {
   if (const char* e = tune("stem_direct"))
     if (e[0] == '0') return -11;
-  if (cin != 3 || cp != 4 || OC != 64 || Kg < 196 || IH != 224 || IW != 224 || Nb < 1) return -11;
+  if (cin != 3 || cp != (f32 ? 4 : 8) || OC != 64 || Kg < 49 * cp || IH != 224 || IW != 224 || Nb < 1) return -11;
   const unsigned grid = (unsigned)Nb * (kS7W / kS7Rows);
   const DetRed det = stats ? det_for(stats) : DetRed{};
-  hipLaunchKernelGGL(stem7_fwd_kernel, dim3(grid), dim3(512), 0, st, x, wf, y, stats, sshift, Kg, IH, IW, det);
+  if (f32)
+    hipLaunchKernelGGL(stem7_fwd_kernel, dim3(grid), dim3(512), 0, st, (const float*)x, (const float*)wf, (float*)y,
+                       stats, sshift, Kg, IH, IW, det);
+  else
+    hipLaunchKernelGGL(stem7_fwd_bf16_kernel, dim3(grid), dim3(512), 0, st, (const uint16_t*)x, (const uint16_t*)wf,
+                       (uint16_t*)y, stats, sshift, Kg, IH, IW, det);
   return (int)hipGetLastError();
 }
 

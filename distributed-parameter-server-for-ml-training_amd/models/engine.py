@@ -226,7 +226,8 @@ class HipResNetEngine:
         # in isolation (bench/stem_probe.py); step A/B within noise, bf16 unmeasured in isolation, so
         # "auto" = fp32 only
         sd = tune("stem_direct", "auto")
-        self.stem_direct = sd == "1" or (sd == "auto" and self.f32)
+        # the direct stems: fp32 (CIFAR 3x3 and ImageNet 7x7) and the bf16 ImageNet 7x7 (stem.hip)
+        self.stem_direct = sd == "1" or (sd == "auto" and (self.f32 or self.spec.stem_conv.k == 7))
         # the later stages' Winograd weight transforms overlap the first stage's forward on the
         # side stream; without one they stay on the compute stream (a stream of their own measured
         # 3.36 vs 3.28 ms/step — a forked branch at the step start costs more than the overlap

@@ -49,7 +49,7 @@ _KERNEL_SIGS = {
                             vp]),
     "psx_conv_dgrad2": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp]),
     "psx_stem_conv": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
-    "psx_stem7_conv": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
+    "psx_stem7_conv": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
     "psx_conv_dgrad2_sc": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp,
                                  vp, i32, vp]),
     "psx_bgemm_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),

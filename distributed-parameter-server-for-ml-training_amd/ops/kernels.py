@@ -130,13 +130,11 @@ def stem_conv(x, wf, y, stats, nb, h, w, cin, cp, oc, kg, sshift=None, k=3) -> b
     """A 3-channel stem conv with its BN statistics (csrc/kernels/stem.hip), same operands as
     conv_fwd2: k = 3 the CIFAR stem (3 -> 64, 3x3 / stride 1 / pad 1, direct vector-ALU conv;
     not in deterministic mode), k = 7 the ImageNet stem (3 -> 64, 7x7 / stride 2 / pad 3,
-    224 -> 112, fp32 on the MFMA with the input patch in LDS). False: not this shape (run
+    224 -> 112, on the MFMA with the input patch in LDS; fp32 or bf16). False: not this shape (run
     conv_fwd2 instead)."""
     if k == 7:
-        if not is_f32(x):
-            return False
         rc = kernels().psx_stem7_conv(ptr(x), ptr(wf), ptr(y), ptr(stats), ptr(sshift), nb, h, w, cin, cp, oc, kg,
-                                      stream_ptr())
+                                      is_f32(x), stream_ptr())
     else:
         rc = kernels().psx_stem_conv(ptr(x), ptr(wf), ptr(y), ptr(stats), ptr(sshift), nb, h, w, cin, cp, oc, kg,
                                      is_f32(x), stream_ptr())

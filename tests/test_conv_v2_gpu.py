@@ -197,3 +197,24 @@ def test_stem_conv_direct():
     q = y.float().reshape(-1, 64)
     assert torch.allclose(st[:, 0].sum(0), q.sum(0), rtol=1e-3, atol=5e-2)
     assert torch.allclose(st[:, 1].sum(0), (q * q).sum(0), rtol=1e-3, atol=5e-2)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_stem7_conv_bf16(n):
+    """bf16: the ImageNet stem on the MFMA (stem.hip stem7_fwd_bf16_kernel: 3 -> 64, 7x7 / stride 2
+    / pad 3, 224 -> 112, 4 taps x 8 channels per v_mfma_f32_16x16x32_bf16) and its shifted BN
+    statistics of the stored bf16 values, against torch fp32 on the same bf16 operands."""
+    torch.manual_seed(14)
+    x = torch.randn(n, 3, 224, 224, device=DEV).to(torch.bfloat16).float()
+    w = (torch.randn(64, 3, 7, 7, device=DEV) / 147 ** 0.5).to(torch.bfloat16).float()
+    wf, _, cp, kg, _ = make_operands(w)
+    assert cp == 8
+    y = torch.full((n, 112, 112, 64), float("nan"), device=DEV).to(torch.bfloat16)
+    st = torch.zeros(K.STAT_SLOTS, 2, 64, device=DEV)
+    sh = 0.1 * torch.randn(64, device=DEV)
+    assert K.stem_conv(to_nhwc(x, cp), wf, y, st, n, 224, 224, 3, cp, 64, kg, sshift=sh, k=7)
+    ref = F.conv2d(x, w, stride=2, padding=3).permute(0, 2, 3, 1)
+    assert _rel(y, ref) < 1e-2
+    d = y.double().reshape(-1, 64) - sh.double()
+    assert torch.allclose(st[:, 0].double().sum(0), d.sum(0), rtol=1e-3, atol=5e-2)
+    assert torch.allclose(st[:, 1].double().sum(0), (d * d).sum(0), rtol=1e-3, atol=5e-2)

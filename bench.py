@@ -376,6 +376,9 @@ def main():
                 "rccl_ranks": t.comm.count() if getattr(t, "native", False) else None,
                 "pair_communicators": len(getattr(t, "_pairs", {}) or {}) if t is not None else 0,
                 "hip_graph": cfg.use_graph,
+                # exact fixed-point BN statistics (bit-reproducible steps), the engine's default
+                "deterministic": (cfg.deterministic if cfg.deterministic is not None
+                                  else os.environ.get("PSX_DETERMINISTIC", "1") == "1"),
             },
             "global_steps": run.server.core.global_step,
             "last_loss": round(loss, 4) if loss is not None else None,

@@ -417,7 +417,9 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
   // the (uniform) soffset
   const int ybytes = a.ybytes;
   const auto yr = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, ybytes, 0x00020000);
+#ifdef PSX_WF_RES_BUF
   const auto rr_ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.res), 0, RES ? ybytes : 0, 0x00020000);
+#endif
   const auto y1r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bs.y1), 0, bwd ? ybytes : 0, 0x00020000);
   const auto orr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bs.o), 0, (bwd && !MAFF) ? ybytes : 0,
                                                      0x00020000);
@@ -433,7 +435,14 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int so = ((e >> 2) * W + (e & 3)) * K * 4;
+      // the residual through a flat load: its buffer descriptor's 4 SGPRs pushed the residual +
+      // data-gradient variants into SGPR spills held in VGPR lanes and then 25-144 VGPR spills to
+      // scratch (113 vs 66 us per 32x32x64 call, profiles/README.md round-5 leads)
+#ifdef PSX_WF_RES_BUF  // A/B builds: the buffer load
       if constexpr (RES) rv[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr_, base, so, 0));
+#else
+      if constexpr (RES) rv[e] = a.res[(base + so) >> 2];
+#endif
       if constexpr (bwd) {
         y1v[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(y1r, base, so, 0));
         if constexpr (!MAFF) ov[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(orr, base, so, 0));

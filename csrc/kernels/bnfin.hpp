@@ -87,7 +87,8 @@ PSX_DEV bool last_block_arrive(unsigned* counter, unsigned nblocks, unsigned cha
 // 2^40, each added with a 64-bit integer atomic: integer addition is associative, so the sums —
 // and with them every BN statistic and the whole step — are the same bits whatever order the
 // workgroups arrive in. The exact range is |sum| < 2^39 with an absolute resolution of 2^-64 (a
-// partial below 2^-41 in magnitude truncates its lowest bits, deterministically).
+// partial below 2^-41 in magnitude truncates its lowest bits, deterministically); a non-finite or
+// out-of-range partial poisons its entry (kFixPoison below: the statistic reads NaN).
 // The pairs live IN the slot buffer: entry i of the float layout [PSX_STAT_SLOTS][NS][C] becomes
 // the 16-byte pair at byte 16 i (the engine sizes its slot buffers 4x in this mode; they are
 // zeroed every step with the float ones), so producers spread over the same 8 slot rows and no
@@ -100,7 +101,19 @@ struct DetRed {
   unsigned long long* fix;  // nullptr: deterministic mode off; else the slot buffer's base (pairs)
 };
 
+// Poison: a partial that is not finite or is too large for the exact range (|v| >= 2^38: a
+// double -> int64 conversion past 2^63 is undefined, and a channel sum past 2^39 would wrap) sets
+// bit 63 of the pair's low word instead of being added. Legitimate low words stay below 2^56 (each
+// add < 2^40, fewer than 2^16 adds per entry), so the bit is sticky under the other adds and every
+// reader (slot_sum, slot_sum_rt, ops/kernels.py det_slot_values) turns a poisoned entry into NaN —
+// as the float-atomic mode would let an Inf / NaN through to the statistics.
+constexpr unsigned long long kFixPoison = 1ull << 63;
+
 PSX_DEV void fix_add(unsigned long long* p, float v) {
+  if (!(fabsf(v) < 274877906944.0f)) {  // 2^38; false for NaN too
+    atomicOr(p + 1, kFixPoison);
+    return;
+  }
   const double x = (double)v * 16777216.0;  // 2^24: exact
   const double h = floor(x);
   const long long hi = (long long)h;
@@ -109,8 +122,9 @@ PSX_DEV void fix_add(unsigned long long* p, float v) {
   atomicAdd(p + 1, lo);
 }
 
-// sum of fixed-point pairs -> double (the one rounding of the whole reduction)
-PSX_DEV double fix_value(long long H, unsigned long long L) {
+// sum of fixed-point pairs -> double (the one rounding of the whole reduction); NaN when poisoned
+PSX_DEV double fix_value(long long H, unsigned long long L, bool poison = false) {
+  if (poison) return __builtin_nan("");
   return (double)H * (1.0 / 16777216.0) + (double)L * 5.421010862427522e-20;  // 2^-24, 2^-64
 }
 
@@ -132,14 +146,16 @@ PSX_DEV double slot_sum(const float* part, size_t i0, size_t stride, bool det) {
   if (det) {
     const unsigned long long* q = reinterpret_cast<const unsigned long long*>(part);
     long long H = 0;
-    unsigned long long L = 0;
+    unsigned long long L = 0, P = 0;
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       const size_t i = i0 + (size_t)t * stride;
+      const unsigned long long lw = q[2 * i + 1];
       H += (long long)q[2 * i];
-      L += q[2 * i + 1];
+      L += lw & ~kFixPoison;
+      P |= lw;
     }
-    return fix_value(H, L);
+    return fix_value(H, L, (P & kFixPoison) != 0);
   }
   double s = 0.0;
 #pragma unroll
@@ -152,13 +168,15 @@ PSX_DEV double slot_sum_rt(const float* part, size_t i0, size_t stride, int T, b
   if (det) {
     const unsigned long long* q = reinterpret_cast<const unsigned long long*>(part);
     long long H = 0;
-    unsigned long long L = 0;
+    unsigned long long L = 0, P = 0;
     for (int t = 0; t < T; ++t) {
       const size_t i = i0 + (size_t)t * stride;
+      const unsigned long long lw = q[2 * i + 1];
       H += (long long)q[2 * i];
-      L += q[2 * i + 1];
+      L += lw & ~kFixPoison;
+      P |= lw;
     }
-    return fix_value(H, L);
+    return fix_value(H, L, (P & kFixPoison) != 0);
   }
   double s = 0.0;
   for (int t = 0; t < T; ++t) s += part[i0 + (size_t)t * stride];

@@ -845,18 +845,10 @@ struct Plan {
 // workgroup per CU), fp32 64x64 beats 64x128 on most (the data gradients by 3-9 %). Steps, same box
 // (r5_call15): ResNet-50 bf16 19.33 -> 17.35 ms, fp32 36.89 -> 36.06; the fp32 64x64 choice costs
 // ResNet-18 +0.2 % (its power-of-two 32x32 / 16x16 layers, tuned on 64x128 in round 2,
-// bench/conv_sweep.py), so fp32 layers with a power-of-two pixel count keep 64x128. PSX_TUNE
-// cv_plan=r4 keeps the round-4 choice (128x128 bf16 / 64x128 fp32 on the large layers).
+// bench/conv_sweep.py), so fp32 layers with a power-of-two pixel count keep 64x128.
 Plan plan_for(int OC, int npix, int ksteps, bool f32 = false) {
   Plan p{64, 128, 1};
-  static const bool r4 = [] {
-    const char* e = tune("cv_plan");
-    return e && !strcmp(e, "r4");
-  }();
-  if (r4 && !f32 && OC % 128 == 0 && (long)(OC / 128) * ((npix + 127) / 128) >= 512) {
-    p.BM = 128;
-    p.BN = 128;
-  } else if ((!f32 || r4 || !(npix & (npix - 1))) && (long)(OC / 64) * ((npix + 127) / 128) >= 512) {
+  if ((!f32 || !(npix & (npix - 1))) && (long)(OC / 64) * ((npix + 127) / 128) >= 512) {
     p.BM = 64;
     p.BN = 128;
   } else {

@@ -528,14 +528,14 @@ static long wino_tiles(int N, int H, int W) { return (long)N * ((H + 3) / 4) * (
 
 long psx_wino_v_floats(int N, int H, int W, int C) { return wino_tiles(N, H, W) * 36 * C; }
 
-// Reduction split s2 of the 36 GEMMs (PSX_TUNE wino_s2=N overrides): each point's C-long reduction
+// Reduction split s2 of the 36 GEMMs (a pure function of the shape: psx_wino_p_floats sizes the
+// caller's P buffer with it, so no run-time override may change it later): each point's C-long reduction
 // runs as s2 workgroup ranges writing s2 partial slabs of P, summed by the output transform. 2 when
 // the 64x64 tiles give fewer than 768 workgroups (3 per CU: the last round part-empty): ResNet-18's
 // 4x4x512 points (576), fwd / dgrad 47.6 / 46.8 -> 45.6 / 43.8 us; 8x8x256 (1152 workgroups) and
 // ResNet-50's 14x14 / 7x7 points are slower split (profiles/r5_wino_split_ab.jsonl).
 static int wino_gemm_split(int T, int C, int K) {
   int s2 = 36L * ((T + 63) / 64) * (K / 64) < 768 ? 2 : 1;
-  if (const char* e = tune("wino_s2"); e && atoi(e) > 0) s2 = atoi(e);
   while (s2 > 1 && (C / 32) % s2) s2 >>= 1;  // whole k-steps (32 fp32 channels) per range
   return s2;
 }

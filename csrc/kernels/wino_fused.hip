@@ -247,7 +247,9 @@ __global__ __launch_bounds__(512, 1) void wino_fused_kernel(WinoFusedArgs a, Win
       }
       vb[p][qa][5 * hh + 4][swz(qa, la)] = (f32x4){e[18 * hh + 16], e[18 * hh + 17], 0.f, 0.f};
     }
-    const auto rs = real ? vr : vnull;
+    // one channel block writes V (the others' transforms are the same values): the 16x16x128 forward
+    // (two blocks) stored every value twice
+    const auto rs = (real && kb == 0) ? vr : vnull;
     if ((PSX_WF_PROBE & 8) == 0 && a.V)  // the stores cost ~4 us on 32x32x64 even when dropped
 #pragma unroll
     for (int b = 0; b < 36; ++b)

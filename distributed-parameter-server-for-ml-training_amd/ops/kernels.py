@@ -52,13 +52,16 @@ def deterministic() -> bool:
 
 def det_slot_values(buf, shape):
     """Decode a deterministic-mode slot buffer: float64 values of its fixed-point pairs in the
-    float layout ``shape`` (e.g. (STAT_SLOTS, 2, C))."""
+    float layout ``shape`` (e.g. (STAT_SLOTS, 2, C)); NaN where a partial was not finite."""
     n = 1
     for d in shape:
         n *= int(d)
-    q = buf.reshape(-1).view(torch.int64)[:2 * n].view(n, 2).double()
-    lo = q[:, 1] + (q[:, 1] < 0).double() * 18446744073709551616.0  # the low word is unsigned
-    return (q[:, 0] * 2.0 ** -24 + lo * 2.0 ** -64).view(*shape)
+    qi = buf.reshape(-1).view(torch.int64)[:2 * n].view(n, 2)
+    poison = qi[:, 1] < 0  # bit 63 of the low word (bnfin.hpp kFixPoison): a non-finite partial
+    q = qi.double()
+    lo = q[:, 1]  # legitimate low words stay below 2^56 (positive as int64)
+    v = q[:, 0] * 2.0 ** -24 + lo * 2.0 ** -64
+    return torch.where(poison, torch.full_like(v, float("nan")), v).view(*shape)
 
 
 def is_f32(t) -> int:

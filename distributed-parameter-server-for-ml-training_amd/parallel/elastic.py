@@ -37,12 +37,12 @@ from __future__ import annotations
 import datetime
 import json
 import os
-import pickle
 import sys
 import time
 
 import torch
 
+from . import objwire
 from .liveness import CommLost
 from .rccl import NativeComm, RcclError, RcclTransport
 
@@ -58,7 +58,8 @@ def enabled(cfg, transport, world: int) -> bool:
 def lost_error(e: BaseException) -> bool:
     """Errors that mean 'the communicator is gone' (recoverable by shrinking): a watchdog abort
     (CommLost), a failed RCCL call (RcclError), or the native server loop's communicator codes
-    (NativeSyncError -60 / -65). Any other native-loop failure (apply kernel, checkpoint
+    (NativeSyncError -60 / -65, or any code once the server's abort() ran). Any other native-loop
+    failure (apply kernel, checkpoint
     callback, core bookkeeping) fails the job: shrinking would only repeat it."""
     if isinstance(e, (CommLost, RcclError)):
         return True
@@ -122,9 +123,9 @@ class ShrunkTransport(RcclTransport):
     def _gather(self, obj):
         self._seq += 1
         key, st = f"{self.tag}/c{self._seq}", self._store()
-        st.set(f"{key}/{self.orig_rank}", pickle.dumps(obj))
+        st.set(f"{key}/{self.orig_rank}", objwire.dumps(obj))  # JSON, never pickle
         st.wait([f"{key}/{r}" for r in self.members])
-        return [pickle.loads(st.get(f"{key}/{r}")) for r in self.members]
+        return [objwire.loads(st.get(f"{key}/{r}")) for r in self.members]
 
     def barrier(self):
         self._gather(None)

@@ -78,17 +78,20 @@ class NativeSyncError(RuntimeError):
     -65 the run stopped because the watchdog aborted the communicator — the two that mean 'the
     communicator is gone' (parallel/elastic.py lost_error). -50 HIP error, -61 apply kernel,
     -62 round incomplete on the core, -63 checkpoint callback, -64 small-tensor gather: job
-    failures that a shrink would only repeat."""
+    failures that a shrink would only repeat — unless this server's abort() ran: the watchdog's
+    communicator abort then usually surfaces first as a HIP error of the blocked loop thread
+    (-50 / -61; the first error wins in the loop), and the run is a lost communicator all the same."""
 
     LOST = (-60, -65)
 
-    def __init__(self, rc: int):
+    def __init__(self, rc: int, aborted: bool = False):
         self.rc = int(rc)
-        super().__init__(f"native sync server failed ({self.rc})")
+        self.aborted = bool(aborted)
+        super().__init__(f"native sync server failed ({self.rc}{', aborted' if self.aborted else ''})")
 
     @property
     def comm_lost(self) -> bool:
-        return self.rc in self.LOST
+        return self.rc in self.LOST or self.aborted
 
 
 def native_sync_enabled(cfg, transport, chan, server, rank: int) -> bool:
@@ -170,6 +173,7 @@ class NativeSyncServer:
             c.small_idx, c.small_n, c.wire_small = w.small_index.data_ptr(), w.small_index.numel(), w.small.data_ptr()
         self.cfg = c
         self.overlap = overlap
+        self._aborted = False  # abort() ran (watchdog): any failure of the run is a lost communicator
         self.wire_bytes = (chan.wire.nbytes if overlap else (c.wire_bytes if c.image else server.arena.numel() * 4))
         kernels()  # both libraries loaded (bound by path)
         runtime()
@@ -221,11 +225,12 @@ class NativeSyncServer:
             self.chan._inflight = bool(self.cfg.primed)
             self.chan._have_buffers = True
         if rc:
-            raise NativeSyncError(rc)
+            raise NativeSyncError(rc, aborted=self._aborted)
 
     def abort(self) -> int:
         """Liveness watchdog thread: freeze the good-round count, stop issuing, abort the
         communicator (csrc/server/sync_loop.cpp psx_sync_abort)."""
+        self._aborted = True
         return int(_lib().psx_sync_abort(self.h))
 
     def rollback(self) -> int:
@@ -234,6 +239,7 @@ class NativeSyncServer:
         g = int(_lib().psx_sync_rollback(self.h))
         if g < 0:
             raise RuntimeError(f"native sync rollback failed ({g})")
+        self._aborted = False
         s = self.server
         s._mom_first = bool(_lib().psx_sync_mom_first(self.h))
         s.core.rollback_to(self.gs0 + g)

@@ -261,15 +261,15 @@ class DistTransport:
         return f"psx/{self._dtag}/{what}{self._dseq}"
 
     def _store_gather(self, obj):
-        import pickle
+        from . import objwire
 
         key, st = self._dkey("obj"), self._store()
-        st.set(f"{key}/{self.rank}", pickle.dumps(obj))
+        st.set(f"{key}/{self.rank}", objwire.dumps(obj))
         if self.rank in self.degraded:
             return [obj if r == self.rank else None for r in range(self.world_size)]
         live = self._live()
         st.wait([f"{key}/{r}" for r in live])
-        return [pickle.loads(st.get(f"{key}/{r}")) if r in live else None for r in range(self.world_size)]
+        return [objwire.loads(st.get(f"{key}/{r}")) if r in live else None for r in range(self.world_size)]
 
     # ---- host control
     def barrier(self):
@@ -281,16 +281,16 @@ class DistTransport:
     def all_gather_object(self, obj):
         if self.degraded:
             return self._store_gather(obj)
-        out = [None] * self.world_size
-        dist.all_gather_object(out, obj, group=self.ctrl)
-        return out
+        from . import objwire  # JSON, never pickle (objwire.py)
+
+        return objwire.all_gather(obj, self.ctrl, self.world_size)
 
     def broadcast_object(self, obj):
         if self.degraded:
             return self._store_gather(obj if self.rank == 0 else None)[0]
-        lst = [obj]
-        dist.broadcast_object_list(lst, src=0, group=self.ctrl)
-        return lst[0]
+        from . import objwire
+
+        return objwire.broadcast(obj, self.ctrl, src=0, rank=self.rank)
 
     def close(self):
         if dist.is_initialized():

@@ -89,6 +89,8 @@ def test_lost_error_classification():
     assert elastic.lost_error(NativeSyncError(-60))
     for rc in (-50, -61, -62, -63, -64):  # apply kernel, core, checkpoint, ...: the job fails
         assert not elastic.lost_error(NativeSyncError(rc))
+    for rc in (-50, -61):  # after this server's abort(), the loop's first error is often a HIP one
+        assert elastic.lost_error(NativeSyncError(rc, aborted=True))
     assert not elastic.lost_error(RuntimeError("native sync server failed (-65)"))  # only the typed error
     assert not elastic.lost_error(ValueError("x"))
 

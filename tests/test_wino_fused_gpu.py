@@ -133,12 +133,12 @@ def _bn_in(c, part_scale=1.0, seed=0):
     return t
 
 
-def test_wino_fused_bn_in_fold():
+@pytest.mark.parametrize("nb,h,c,k", [(8, 16, 128, 128)])
+def test_wino_fused_bn_in_fold(nb, h, c, k):
     """The previous layer's training BN finalize + BN + ReLU folded into the input transform: the
     fused launch == the three-launch path with the same fold (output, statistics, the published
     affine / saved / running / shift statistics)."""
     torch.manual_seed(3)
-    nb, h, c, k = 8, 16, 128, 128
     z = torch.randn(nb, h, h, c, device=DEV) * 2 + 0.5  # pre-BN output of the previous conv
     cnt = nb * h * h
     sl = torch.zeros(K.STAT_SLOTS, 2, c, device=DEV)
@@ -313,3 +313,36 @@ def test_engine_bwd_fold_matches_unfolded(monkeypatch):
     print("bwd fold vs apply: median %.2e, worst %s" % (errs[len(errs) // 2][0], errs[-3:]))
     assert errs[-1][0] < 1e-2, errs[-3:]
     assert errs[len(errs) // 2][0] < 1e-3, errs
+
+
+@pytest.mark.parametrize("bad", [float("inf"), float("nan"), 1e30])
+def test_deterministic_poison(bad):
+    """Deterministic mode: a non-finite or out-of-range partial (|v| >= 2^38, past the fixed-point
+    pairs' exact range) poisons its slot entry (bnfin.hpp kFixPoison) instead of adding an undefined
+    integer: the decoded sums and the finalized mean / variance read NaN, as the float-atomic mode
+    lets an Inf / NaN through; finite inputs leave every entry clean."""
+    torch.manual_seed(4)
+    nb, h, c, k = 16, 16, 64, 64
+    w = torch.randn(k, c, 3, 3, device=DEV) * (2.0 / (9 * c)) ** 0.5
+    uf, _ = _uf(w, k, c)
+    try:
+        K.set_deterministic(True)
+        for poisoned in (False, True):
+            x = torch.relu(torch.randn(nb, h, h, c, device=DEV))
+            if poisoned:
+                x[3, 5, 7, :] = bad  # every output channel sees it
+            y = torch.empty(nb, h, h, k, device=DEV)
+            stats = torch.zeros(K.STAT_SLOTS * K.det_slot_scale(), 2, k, device=DEV)
+            K.wino_fused(x, uf, y, None, stats, None, nb, h, h, c, k)
+            t = _bn_in(k, seed=2)
+            K.bn_finalize(stats, K.STAT_SLOTS, k, nb * h * h, t["gamma"], t["beta"], 1e-5, 0.1, t["rm"], t["rv"],
+                          t["affine"], t["saved"])
+            torch.cuda.synchronize()
+            vals = K.det_slot_values(stats, (K.STAT_SLOTS, 2, k)).sum(0)
+            if poisoned:
+                assert torch.isnan(vals).all()
+                assert torch.isnan(t["saved"][0]).all() and torch.isnan(t["affine"]).all()
+            else:
+                assert torch.isfinite(vals).all() and torch.isfinite(t["saved"]).all()
+    finally:
+        K.set_deterministic(None)

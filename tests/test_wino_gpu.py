@@ -64,13 +64,13 @@ def _nhwc(t):
                                           (2, 16, 64, 64, False), (4, 4, 512, 512, False), (8, 32, 64, 64, True),
                                           # partial edge tiles (ResNet-50's 14x14 / 7x7 stages, odd sizes)
                                           (2, 14, 256, 256, True), (3, 7, 512, 512, False), (2, 5, 64, 128, True),
-                                          (2, 10, 128, 64, False)])
-@pytest.mark.parametrize("s2", [1, 4])
-def test_wino_fwd(nb, h, c, k, res, s2, monkeypatch):
-    """The input transform, the 36 batched GEMMs (s2: the reduction split, partial slabs summed
-    by the output transform) and the output transform (+ residual, + BN slot sums of y) against
-    float64."""
-    monkeypatch.setenv("PSX_TUNE", f"wino_s2={s2}")
+                                          (2, 10, 128, 64, False),
+                                          # >= 768 GEMM workgroups: the unsplit reduction (s2 = 1)
+                                          (32, 32, 64, 64, True)])
+def test_wino_fwd(nb, h, c, k, res):
+    """The input transform, the 36 batched GEMMs (their reduction split s2 is a function of the
+    shape: 2 for the small cases, partial slabs summed by the output transform, 1 for the last) and
+    the output transform (+ residual, + BN slot sums of y) against float64."""
     torch.manual_seed(nb * h + c)
     x = torch.relu(torch.randn(nb, c, h, h, device=DEV, dtype=torch.float64))
     w = torch.randn(k, c, 3, 3, device=DEV, dtype=torch.float64) * (2.0 / (9 * c)) ** 0.5

@@ -168,12 +168,20 @@ class Run:
     def measure(self, steps, warmup):
         """Untimed warmup, then exactly ``steps`` timed steps; returns (max seconds over ranks,
         host issue times of this rank)."""
+        self.server_round_us = None
         if self.native is not None:  # the native server rank runs its rounds in one call each
             self.native.run(warmup, watchdog=self.watchdog)
             self.barrier_sync()
+            p0 = self.native.phase_totals()  # the warmup rounds are retired (run() drains)
             t0 = time.perf_counter()
             self.native.run(steps, watchdog=self.watchdog)
+            p1 = self.native.phase_totals()
             host = None  # no per-step host issue: every round was issued by one native call
+            nr = p1[0] - p0[0]
+            if nr > 0:  # rank 0's device time per timed round, per phase (sync_loop.cpp psx_sync_phase_us)
+                self.server_round_us = {k: round((p1[i] - p0[i]) / nr, 1)
+                                        for i, k in ((1, "gather_incl_worker_wait"), (2, "apply"), (3, "broadcast"))}
+                self.server_round_us["rounds"] = nr
         else:
             for i in range(warmup):
                 self.step(i)
@@ -380,10 +388,14 @@ def main():
                 "deterministic": (cfg.deterministic if cfg.deterministic is not None
                                   else os.environ.get("PSX_DETERMINISTIC", "1") == "1"),
             },
+            "value_per_worker": round(value / W, 2),
             "global_steps": run.server.core.global_step,
             "last_loss": round(loss, 4) if loss is not None else None,
             "baseline_img_s": BASELINE_SYNC_IMG_S if r18 else None,
         }
+    if rank == 0 and run.server_round_us is not None:
+        # dedicated server: device time per round per phase (bucket phases overlap with --overlap)
+        rec["server_round_us"] = run.server_round_us
     if a.host_timing and host:
         wait = getattr(run.wk.compute, "host_wait_s", 0.0) if run.wk is not None else 0.0
         print(json.dumps({"rank": rank, "host_issue_ms_per_step": round(1e3 * sum(host) / len(host), 4),

@@ -131,6 +131,11 @@ struct PsxSyncSlot {
   hipEvent_t done = nullptr;
   std::vector<hipEvent_t> t0, t1;  // [max(1, nbuckets)]
   int nt = 0;                      // ranges timed this round
+  // per-phase device ranges of the round (psx_sync_phase_us): gather g0/g1 (receive posted ->
+  // every worker's wire landed, so it includes waiting for the workers' step) and broadcast
+  // c0/c1, one pair per bucket (+1: the first round's whole-wire broadcast); the apply is t0/t1
+  std::vector<hipEvent_t> g0, g1, c0, c1;
+  int ng = 0, nc = 0;
 };
 
 struct PsxSync {
@@ -152,6 +157,9 @@ struct PsxSync {
   std::atomic<int> aborting{0};
   long long good = -1;
   int mom_first0 = 0;  // mom_first at creation (a rollback to round 0 restores it)
+  // retired rounds' device time per phase, us: [gather, apply, broadcast] (under mu)
+  double ph_us[3] = {0, 0, 0};
+  long long ph_rounds = 0;
 };
 
 namespace {
@@ -199,7 +207,20 @@ void retire_slot(PsxSync* S, int k) {
     sec += 1e-3 * (double)ms;
   }
   if (sl.nt) S->rt.ps_record_update_time(S->c.core, sec);
-  sl.nt = 0;
+  auto span_us = [&](const std::vector<hipEvent_t>& a, const std::vector<hipEvent_t>& b, int n) {
+    double us = 0;
+    for (int i = 0; i < n; ++i) {
+      float ms = 0.f;
+      PSX_SHIP(S, hipEventElapsedTime(&ms, a[i], b[i]));
+      us += 1e3 * (double)ms;
+    }
+    return us;
+  };
+  S->ph_us[0] += span_us(sl.g0, sl.g1, sl.ng);
+  S->ph_us[1] += 1e6 * sec;
+  S->ph_us[2] += span_us(sl.c0, sl.c1, sl.nc);
+  S->ph_rounds++;
+  sl.nt = sl.ng = sl.nc = 0;
   S->done.fetch_add(1);
 }
 
@@ -221,10 +242,23 @@ void retire(PsxSync* S, size_t keep) {
 void gather(PsxSync* S, long lo, long n, hipStream_t st) {
   const int dt = S->c.grad_fp16 ? PSX_F16 : PSX_F32;
   const size_t es = S->c.grad_fp16 ? 2 : 4;
+  PsxSyncSlot& sl = S->slot[S->cur];
+  const bool timed = sl.ng < (int)sl.g0.size();
+  if (timed) PSX_SHIP(S, hipEventRecord(sl.g0[sl.ng], st));
   PSX_SCOMM(S, psx_comm_group_start());
   for (int r = 1; r <= S->c.nworkers; ++r)
     PSX_SCOMM(S, psx_comm_recv(S->c.comm, (char*)S->c.gbufs[r - 1] + lo * es, n, dt, r, st));
   PSX_SCOMM(S, psx_comm_group_end());
+  if (timed) PSX_SHIP(S, hipEventRecord(sl.g1[sl.ng++], st));
+}
+
+// a broadcast of the round, device-timed (phase 2)
+void bcast(PsxSync* S, void* buf, long n, int dt, hipStream_t st) {
+  PsxSyncSlot& sl = S->slot[S->cur];
+  const bool timed = sl.nc < (int)sl.c0.size();
+  if (timed) PSX_SHIP(S, hipEventRecord(sl.c0[sl.nc], st));
+  PSX_SCOMM(S, psx_comm_broadcast(S->c.comm, buf, n, dt, 0, st));
+  if (timed) PSX_SHIP(S, hipEventRecord(sl.c1[sl.nc++], st));
 }
 
 // p[lo:hi] -= lr * sum_k g_k[lo:hi] / W (+ momentum / wd), image (nullable) of the range
@@ -292,9 +326,9 @@ void serial_round(PsxSync* S) {
     (void)hipGetLastError();
     if (S->c.small_n && S->rt.gather_f32(S->c.arena, S->c.small_idx, S->c.small_n, S->c.wire_small, st) && !S->err)
       S->err = -64;
-    PSX_SCOMM(S, psx_comm_broadcast(S->c.comm, S->c.wire_buf, S->c.wire_bytes, PSX_U8, 0, st));
+    bcast(S, S->c.wire_buf, S->c.wire_bytes, PSX_U8, st);
   } else {
-    PSX_SCOMM(S, psx_comm_broadcast(S->c.comm, S->c.arena, S->c.arena_numel, PSX_F32, 0, st));
+    bcast(S, S->c.arena, S->c.arena_numel, PSX_F32, st);
   }
   gather(S, 0, S->c.n_params, st);
   if (S->err) return;  // a failed gather is never applied
@@ -308,7 +342,7 @@ void overlap_round(PsxSync* S) {
   fetch_bookkeeping(S);
   if (!S->c.primed) {  // first round: the whole wire (every segment + the BN buffers), packed by the host
     after(S, cs, us);
-    PSX_SCOMM(S, psx_comm_broadcast(S->c.comm, S->c.full_wire, S->c.full_wire_bytes, PSX_U8, 0, cs));
+    bcast(S, S->c.full_wire, S->c.full_wire_bytes, PSX_U8, cs);
     S->c.primed = 1;
   }
   std::vector<hipEvent_t>& got = S->got;
@@ -327,11 +361,11 @@ void overlap_round(PsxSync* S) {
       (void)hipGetLastError();
       if (b.nsmall && S->rt.gather_f32(S->c.arena, b.small, b.nsmall, b.seg_small, us) && !S->err) S->err = -64;
       after(S, cs, us);
-      PSX_SCOMM(S, psx_comm_broadcast(S->c.comm, b.seg, b.seg_bytes, PSX_U8, 0, cs));
+      bcast(S, b.seg, b.seg_bytes, PSX_U8, cs);
     } else {  // fp32 segment = the arena slice itself, broadcast in place
       apply_range(S, b.lo, b.hi, nullptr, us);
       after(S, cs, us);
-      PSX_SCOMM(S, psx_comm_broadcast(S->c.comm, S->c.arena + b.lo, b.seg_bytes, PSX_U8, 0, cs));
+      bcast(S, S->c.arena + b.lo, b.seg_bytes, PSX_U8, cs);
     }
   };
   for (int k = 0; k < S->c.nbuckets; ++k) {
@@ -388,10 +422,10 @@ void* psx_sync_create(const PsxSyncCfg* cfg, const char* runtime_path, const cha
   const int nt = std::max(1, cfg->nbuckets);
   for (PsxSyncSlot& sl : S->slot) {
     ev_ok = ev_ok && hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
-    sl.t0.assign(nt, nullptr);
-    sl.t1.assign(nt, nullptr);
-    for (int i = 0; i < nt; ++i)
-      ev_ok = ev_ok && hipEventCreate(&sl.t0[i]) == hipSuccess && hipEventCreate(&sl.t1[i]) == hipSuccess;
+    for (auto* v : {&sl.t0, &sl.t1, &sl.g0, &sl.g1, &sl.c0, &sl.c1}) {
+      v->assign(v == &sl.c0 || v == &sl.c1 ? nt + 1 : nt, nullptr);
+      for (auto& e : *v) ev_ok = ev_ok && hipEventCreate(&e) == hipSuccess;
+    }
   }
   if (!ev_ok) {
     fprintf(stderr, "psx_sync_create: hipEventCreate failed\n");
@@ -415,7 +449,8 @@ int psx_sync_run(void* h, long long rounds) {
       S->err = -65;
       break;
     }
-    S->slot[S->cur].nt = 0;
+    PsxSyncSlot& sl = S->slot[S->cur];
+    sl.nt = sl.ng = sl.nc = 0;
     if (S->c.nbuckets > 0)
       overlap_round(S);
     else
@@ -446,6 +481,16 @@ void psx_sync_progress(void* h, long long* out) {
 }
 
 int psx_sync_mom_first(void* h) { return ((PsxSync*)h)->c.mom_first; }
+
+// Device time of the retired rounds per phase: out = [rounds, gather us, apply us, broadcast us]
+// (sums; the gather range runs from the receives' post to the last worker's wire landing, so it
+// holds the workers' step; with bucketed overlap the phases of different buckets overlap).
+void psx_sync_phase_us(void* h, double* out) {
+  PsxSync* S = (PsxSync*)h;
+  std::lock_guard<std::mutex> lk(S->mu);
+  out[0] = (double)S->ph_rounds;
+  for (int i = 0; i < 3; ++i) out[1 + i] = S->ph_us[i];
+}
 
 // Liveness watchdog (another thread): freezes the count of rounds known good, stops the loop from
 // issuing more and aborts the communicator (the blocked loop thread then runs out). Returns the
@@ -497,10 +542,9 @@ void psx_sync_destroy(void* h) {
     if (ev) hipEventDestroy(ev);
   for (PsxSyncSlot& sl : S->slot) {
     if (sl.done) hipEventDestroy(sl.done);
-    for (hipEvent_t ev : sl.t0)
-      if (ev) hipEventDestroy(ev);
-    for (hipEvent_t ev : sl.t1)
-      if (ev) hipEventDestroy(ev);
+    for (auto* v : {&sl.t0, &sl.t1, &sl.g0, &sl.g1, &sl.c0, &sl.c1})
+      for (hipEvent_t ev : *v)
+        if (ev) hipEventDestroy(ev);
   }
   delete S;
 }

@@ -18,6 +18,11 @@
 //                group of mutual sends and receives cannot deadlock.
 // Every wait has a deadline (PSX_FAKECOMM_TIMEOUT_S, default 120 s): a stalled peer turns into
 // ncclRemoteError and a sticky async error instead of a hang.
+// Streams: every copy and reduction kernel runs on a private non-blocking stream of the calling
+// thread, waited for with hipStreamSynchronize — never the legacy null stream (hipMemcpy,
+// hipDeviceSynchronize): a null-stream call from the server's comm thread invalidates a graph
+// capture that the co-located worker's thread has open, in every capture mode
+// (scripts/dev/capture_probe.py, profiles/r6_capture_probe.jsonl).
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -121,6 +126,19 @@ bool wait_for(Comm* c, P pred) {
   return true;
 }
 
+// the calling thread's private non-blocking stream (see the header)
+hipStream_t priv() {
+  thread_local hipStream_t s = nullptr;
+  if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+  return s;
+}
+
+bool copy_d2d(void* dst, const void* src, size_t bytes) {
+  hipStream_t s = priv();
+  return s && hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s) == hipSuccess &&
+         hipStreamSynchronize(s) == hipSuccess;
+}
+
 ncclResult_t fail(Comm* c, ncclResult_t e) {
   c->async_err = e;
   return e;
@@ -206,19 +224,21 @@ bool sum_into(const std::vector<const void*>& srcs, void* dst, size_t n, ncclDat
   Srcs s{};
   s.n = (int)srcs.size();
   for (int k = 0; k < s.n; ++k) s.p[k] = srcs[k];
+  hipStream_t ps = priv();
+  if (!ps) return false;
   size_t g = (n + 255) / 256;
   if (g > 4096) g = 4096;
   if (g < 1) g = 1;
   switch (t) {
-    case ncclFloat32: hipLaunchKernelGGL(sum_kernel<float>, dim3(g), dim3(256), 0, 0, s, (float*)dst, n); break;
-    case ncclFloat16: hipLaunchKernelGGL(sum_kernel<__half>, dim3(g), dim3(256), 0, 0, s, (__half*)dst, n); break;
+    case ncclFloat32: hipLaunchKernelGGL(sum_kernel<float>, dim3(g), dim3(256), 0, ps, s, (float*)dst, n); break;
+    case ncclFloat16: hipLaunchKernelGGL(sum_kernel<__half>, dim3(g), dim3(256), 0, ps, s, (__half*)dst, n); break;
     case ncclBfloat16:
-      hipLaunchKernelGGL(sum_kernel<unsigned short>, dim3(g), dim3(256), 0, 0, s, (unsigned short*)dst, n);
+      hipLaunchKernelGGL(sum_kernel<unsigned short>, dim3(g), dim3(256), 0, ps, s, (unsigned short*)dst, n);
       break;
-    case ncclInt32: hipLaunchKernelGGL(sum_i32_kernel, dim3(g), dim3(256), 0, 0, s, (int*)dst, n); break;
+    case ncclInt32: hipLaunchKernelGGL(sum_i32_kernel, dim3(g), dim3(256), 0, ps, s, (int*)dst, n); break;
     default: return false;
   }
-  return hipDeviceSynchronize() == hipSuccess;
+  return hipStreamSynchronize(ps) == hipSuccess;
 }
 
 // one collective step: publish `mine`, barrier, body(peer mappings), device sync, barrier
@@ -238,8 +258,8 @@ ncclResult_t collective(Comm* c, const void* mine, hipStream_t st, B body) {
       if (!peer[r]) return fail(c, ncclUnhandledCudaError);
     }
   }
-  const bool ok = body(peer);
-  if (hipDeviceSynchronize() != hipSuccess || !ok) return fail(c, ncclUnhandledCudaError);
+  const bool ok = body(peer);  // its copies / kernels completed on priv() before it returned
+  if (!ok) return fail(c, ncclUnhandledCudaError);
   if (!barrier(c)) return fail(c, ncclRemoteError);
   return ncclSuccess;
 }
@@ -270,7 +290,7 @@ ncclResult_t do_recv(Comm* c, void* buf, size_t bytes, int peer) {
   if (sl.bytes != bytes) return fail(c, ncclInvalidUsage);
   void* src = open_ptr(c, sl.buf);
   if (!src) return fail(c, ncclUnhandledCudaError);
-  if (hipMemcpy(buf, src, bytes, hipMemcpyDeviceToDevice) != hipSuccess) return fail(c, ncclUnhandledCudaError);
+  if (!copy_d2d(buf, src, bytes)) return fail(c, ncclUnhandledCudaError);
   s->done[peer][c->rank].store(k + 1);
   return ncclSuccess;
 }
@@ -385,7 +405,7 @@ ncclResult_t ncclAllReduce(const void* send, void* recv, size_t count, ncclDataT
     std::vector<const void*> srcs(peer.begin(), peer.end());
     return sum_into(srcs, tmp, count, t);
   });
-  if (r == ncclSuccess && hipMemcpy(recv, tmp, count * dsize(t), hipMemcpyDeviceToDevice) != hipSuccess)
+  if (r == ncclSuccess && !copy_d2d(recv, tmp, count * dsize(t)))
     r = ncclUnhandledCudaError;
   hipFree(tmp);
   return r;
@@ -403,7 +423,7 @@ ncclResult_t ncclReduceScatter(const void* send, void* recv, size_t count, ncclD
     for (void* p : peer) srcs.push_back((const char*)p + (size_t)c->rank * count * es);
     return sum_into(srcs, tmp, count, t);
   });
-  if (r == ncclSuccess && hipMemcpy(recv, tmp, count * es, hipMemcpyDeviceToDevice) != hipSuccess)
+  if (r == ncclSuccess && !copy_d2d(recv, tmp, count * es))
     r = ncclUnhandledCudaError;
   hipFree(tmp);
   return r;
@@ -419,11 +439,11 @@ ncclResult_t ncclAllGather(const void* send, void* recv, size_t count, ncclDataT
   if (hipMalloc(&tmp, count * es * c->nranks) != hipSuccess) return ncclUnhandledCudaError;
   ncclResult_t r = collective(c, send, st, [&](std::vector<void*>& peer) {
     for (int p = 0; p < c->nranks; ++p)
-      if (hipMemcpy((char*)tmp + (size_t)p * count * es, peer[p], count * es, hipMemcpyDeviceToDevice) != hipSuccess)
+      if (!copy_d2d((char*)tmp + (size_t)p * count * es, peer[p], count * es))
         return false;
     return true;
   });
-  if (r == ncclSuccess && hipMemcpy(recv, tmp, count * es * c->nranks, hipMemcpyDeviceToDevice) != hipSuccess)
+  if (r == ncclSuccess && !copy_d2d(recv, tmp, count * es * c->nranks))
     r = ncclUnhandledCudaError;
   hipFree(tmp);
   return r;
@@ -436,9 +456,9 @@ ncclResult_t ncclBroadcast(const void* send, void* recv, size_t count, ncclDataT
   if (!es) return ncclInvalidArgument;
   return collective(c, c->rank == root ? send : nullptr, st, [&](std::vector<void*>& peer) {
     if (c->rank == root) {
-      return send == recv || hipMemcpy(recv, send, count * es, hipMemcpyDeviceToDevice) == hipSuccess;
+      return send == recv || copy_d2d(recv, send, count * es);
     }
-    return hipMemcpy(recv, peer[root], count * es, hipMemcpyDeviceToDevice) == hipSuccess;
+    return copy_d2d(recv, peer[root], count * es);
   });
 }
 

@@ -1141,7 +1141,11 @@ class HipResNetEngine:
         graphs = []
         for fn in self._segment_fns(arena, images_u8, labels_all, unpack):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=graphs[0].pool() if graphs else None):
+            # thread-local capture: in torch's default (global) mode any other thread's stream
+            # synchronize, allocation or copy invalidates the capture (hipErrorStreamCaptureInvalidated,
+            # profiles/r6_capture_probe.jsonl) — the co-located async server's comm thread does all
+            # three while this worker thread captures its first step (docs/ARCHITECTURE.md)
+            with torch.cuda.graph(g, pool=graphs[0].pool() if graphs else None, capture_error_mode="thread_local"):
                 fn()
             graphs.append(g)
         self.graphs = graphs

@@ -53,6 +53,7 @@ _SIGS = {
     "psx_sync_run": (i32, [vp, C.c_longlong]),
     "psx_sync_drain": (i32, [vp]),
     "psx_sync_progress": (None, [vp, C.POINTER(C.c_longlong)]),
+    "psx_sync_phase_us": (None, [vp, C.POINTER(C.c_double)]),
     "psx_sync_mom_first": (i32, [vp]),
     "psx_sync_primed": (i32, [vp]),
     "psx_sync_abort": (C.c_longlong, [vp]),
@@ -197,6 +198,14 @@ class NativeSyncServer:
         out = (C.c_longlong * 2)()
         _lib().psx_sync_progress(self.h, out)
         return int(out[0]), int(out[1])
+
+    def phase_totals(self) -> tuple[int, float, float, float]:
+        """(rounds retired, gather us, apply us, broadcast us): device time summed over the loop's
+        retired rounds (csrc/server/sync_loop.cpp psx_sync_phase_us). The gather range spans the
+        receives' post to the last worker's wire landing, so it holds the workers' step."""
+        out = (C.c_double * 4)()
+        _lib().psx_sync_phase_us(self.h, out)
+        return int(out[0]), float(out[1]), float(out[2]), float(out[3])
 
     def run(self, rounds: int, watchdog=None):
         """All ``rounds`` rounds of the job; returns when their device work is done."""

@@ -143,6 +143,14 @@ def test_bench_multirank(world, topology):
     assert abs(rec["value"] - 3 * 128 * W / (rec["ms_per_step"] * 3e-3)) <= 1e-3 * rec["value"] + 0.02, rec
     assert 0.5 < rec["ms_per_step"] < 5000, rec
     assert rec["last_loss"] is None or 0.0 < rec["last_loss"] < 20.0
+    assert abs(rec["value_per_worker"] * W - rec["value"]) <= 0.05, rec
+    if want == "dedicated":
+        # rank 0's (native server) device time per timed round, per phase
+        sr = rec["server_round_us"]
+        assert sr["rounds"] == 3, sr
+        assert all(sr[k] > 0 for k in ("gather_incl_worker_wait", "apply", "broadcast")), sr
+        # the gather waits for the workers' step; the apply is one fused kernel (R18 fp32 ~20 us)
+        assert sr["apply"] < sr["gather_incl_worker_wait"], sr
 
 
 def test_bench_stalled_worker_exits():
@@ -237,7 +245,7 @@ import psx
 from psx.parallel.runner import run_distributed
 from psx.utils.config import PSConfig
 cfg = PSConfig(model="resnet18", batch_size=64, epochs=1, train_samples=1024, eval_every=0, verbose=0, lr=0.05,
-               max_steps=4, mode="async", topology={topo!r}, heartbeat_timeout=0, use_graph=False).validate()
+               max_steps=4, mode="async", topology={topo!r}, heartbeat_timeout=0, use_graph=True).validate()
 res = run_distributed(cfg, log=lambda *a, **k: None)
 if "server" in res:
     s = res["server"]
@@ -257,11 +265,12 @@ def test_async_remote_workers(world, topology, native_loop, tmp_path):
     W = world - 1 if topology == "dedicated" else world
     script = tmp_path / "arun.py"
     script.write_text(_ARUN.format(root=ROOT, topo=topology))
-    # the stand-in's point-to-point is host-synchronous and three processes share one GPU: a
-    # rank whose first steps capture graphs can leave a peer's send unmatched for tens of
-    # seconds (one 60 s timeout seen in ~10 runs; in round 5 one full-suite run stalled > 180 s),
-    # so this test runs the workers without HIP graphs (the graph path: the sync tests) and gets
-    # a longer deadline
+    # Workers capture HIP graphs (use_graph=True) while the co-located server's comm thread runs
+    # point-to-point: round 5 turned graphs off here after a stall; the cause was a capture
+    # invalidated from another thread — torch's default global capture mode lets any other
+    # thread's stream sync / allocation / copy break it, and the stand-in's null-stream copies
+    # break it in every mode (profiles/r6_capture_probe.jsonl). The engine now captures
+    # thread-locally and the stand-in never touches the null stream.
     out = _torchrun(world, [str(script)], extra={"PSX_NATIVE_LOOP": native_loop, "PSX_FAKECOMM_TIMEOUT_S": "240"})
     recs = [r for r in _json_lines(out, "RESULT ") if r]
     assert len(recs) == 1, out[-3000:]

@@ -55,6 +55,7 @@ from psx.parallel.worker import Worker  # noqa: E402
 from psx.utils.config import PSConfig  # noqa: E402
 
 BASELINE_SYNC_IMG_S = 82.7  # sync PS, 4 workers, measured (experiment_results/sync_4workers.json)
+BASELINE_ASYNC_IMG_S = 168.6  # async PS, 8 workers, measured (experiment_results/async_8workers.json)
 FALLBACK_HINT = ("; fallbacks to try: PSX_PAIR_COMMS=0 (async point-to-point on the job communicator), "
                  "PSX_SYNC_AGG=reduce (ncclReduce instead of the send/recv gather), --overlap off (serial "
                  "rounds), PSX_NATIVE_SYNC=0 (Python server rounds), PSX_TRANSPORT=torch (torch.distributed)")
@@ -259,6 +260,37 @@ def rccl_choices(path, limit=24):
     return out
 
 
+def async_threads(a, W: int) -> dict:
+    """BASELINE config 4's async PS with W = 7 workers on ONE GPU: W worker threads, each with its
+    own HIP stream, engine and graph, pushing into the native event loop in real arrival order
+    (parallel/runner.py run_local_threads). img/s counts ACCEPTED pushes only; the staleness
+    histogram is the distribution those arrivals produced (bound --staleness-bound)."""
+    from psx.parallel.runner import run_local_threads
+
+    try:
+        steps = max(5, min(a.steps, 20))
+        cfg = PSConfig(mode="async", staleness_bound=a.staleness_bound, model=a.model, batch_size=a.batch,
+                       train_samples=a.train_samples or 50000, lr=0.1, sync_steps=1, epochs=1, eval_every=0,
+                       verbose=0, codec="fp16", use_graph=not a.no_graph, fetch_codec="fp32", workers=W,
+                       dtype=a.dtype).validate()
+        res = run_local_threads(cfg, steps, log=lambda *x, **k: None, emit=False)
+        sm, tm = res["server"], res["timed"]
+        hist = sm.get("staleness_histogram") or []
+        return {"value": tm["images_per_second"], "unit": "images/s (accepted pushes only)",
+                "ms_per_round": round(1e3 * tm["timed_seconds"] / steps, 4), "dtype": a.dtype, "workers": W,
+                "topology": "threads (W worker threads + native event loop on 1 GPU)", "steps_per_worker": steps,
+                "timed_pushes": tm["timed_pushes"], "timed_accepted_pushes": tm["timed_accepted_pushes"],
+                "images_per_second_all_pushes": tm["images_per_second_all_pushes"],
+                "vs_baseline_async_8w": round(tm["images_per_second"] / BASELINE_ASYNC_IMG_S, 2),
+                "async_staleness": {k: sm.get(k) for k in ("average_gradient_staleness", "max_staleness_observed",
+                                                           "mean_staleness_all", "async_updates", "rejected_pushes",
+                                                           "staleness_histogram", "staleness_bound")},
+                "max_staleness_accepted": max((i for i, n in enumerate(hist[: a.staleness_bound + 1]) if n),
+                                              default=0)}
+    except Exception as e:  # noqa: BLE001 - a secondary number never costs the headline
+        return {"error": f"{type(e).__name__}: {e}"[:300]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -451,6 +483,8 @@ def main():
                 r2.close()
             except Exception as e:  # noqa: BLE001 - a secondary number never costs the headline
                 secondary[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        if world == 1:
+            secondary["async_w7"] = async_threads(a, 7)
     if rank == 0:
         if secondary:
             rec["secondary"] = secondary

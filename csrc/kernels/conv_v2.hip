@@ -84,6 +84,10 @@ struct Conv2Args {
   const void* in2;
   const void* w2;
   int Kg2;
+  // LDS ring depth of the generic mainloop: 3 (default, 0) or 2 — a 2-deep ring halves nothing
+  // per k-step but fits 5 instead of 3 fp32 64x64 workgroups per CU (32 vs 48 KB), the batched
+  // Winograd GEMMs' 1152-workgroup grids then run in one round (launch2 / psx_bgemm_f32_split)
+  int nstg;
 };
 
 // Winograd F(4x4,3x3) output transform A^T (wino.hip has the matrices): y = A^T P A
@@ -489,8 +493,10 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
     for (int n = 0; n < NT; ++n)
       fb[n] = *reinterpret_cast<const u32x4*>(B + kmaj2(wn * (BN / WGN) + n * 16 + frow, kk * 4 + fch));
   };
-  if (nk > 0) issue(0, 0);
-  if (nk > 1) issue(1, 1);
+  if (a.nstg != 2) {
+    if (nk > 0) issue(0, 0);
+    if (nk > 1) issue(1, 1);
+  }
   if constexpr (sizeof(T) == 4 && (PSX_CONV_PF & 2)) {
     // fp32: the fragments of the next half k-step are read before the MFMAs of the current one
     // (register double buffer, as in the tap-reuse loop); the stage boundary — DMA of k-step
@@ -527,6 +533,23 @@ __global__ __launch_bounds__(256) void conv2_kernel(Conv2Args a) {
       __builtin_amdgcn_sched_barrier(0);
       mma_tiles<MT, NT, T>(acc, fa1, fb1);
       stage = nxt;
+    }
+  } else if (a.nstg == 2) {
+    // 2-deep ring: k-step ks + 1 is issued into the other stage once every wave has passed the
+    // barrier, i.e. finished reading it (k-step ks - 1); its DMA overlaps k-step ks's MFMAs
+    for (int ks = 0; ks < nk; ++ks) {
+      const int stage = ks & 1;
+      if (ks == 0) issue(0, 0);  // (the shared prologue above issued nothing: nstg == 2 skips it)
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (ks + 1 < nk) issue(ks + 1, stage ^ 1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        u32x4 fa[MT], fb[NT];
+        load_frags(stage, kk, fa, fb);
+        mma_tiles<MT, NT, T>(acc, fa, fb);
+      }
     }
   } else {
     int stage = 0;
@@ -881,7 +904,7 @@ int launch2(const Conv2Args& a, hipStream_t st) {
   // overlap another's loads (a 128x128 bf16 tile: 96 -> 67.6 KB, 1 -> 2 per CU; measured neutral on
   // the ResNet-50 step, r5_call13, kept as the tighter bound)
   const int nk_max = SPLIT ? a.kps : (MODE == 3 ? 3 : a.Kg / kKS<T>);
-  const int stages = nk_max < 3 ? (nk_max < 1 ? 1 : nk_max) : 3;
+  const int stages = nk_max < 3 ? (nk_max < 1 ? 1 : nk_max) : (a.nstg == 2 ? 2 : 3);
   const size_t ring = (size_t)stages * (BM + BN) * 128, epi = (size_t)BN * (BM + 4) * 4;
   const size_t red = (size_t)(256 / (BM / 8)) * 3 * BM * 4;  // the epilogue's statistic reduction
   const size_t epr = epi > red ? epi : red;
@@ -1173,6 +1196,12 @@ int psx_conv_dgrad2_sc(const void* dy, const void* wd, void* dx, const void* res
 // 1x4 waves, 3: 64x128 / 1x4 waves; N rows x M pixels).
 // s2 > 1: each batch's Kd-long reduction as s2 ranges (whole k-steps) writing s2 partial slabs
 // P[b s2 + j][M][N] (the Winograd output transform sums them, wino.hip psx_wino_conv)
+// LDS ring depth of the batched GEMMs (Conv2Args::nstg): 2 (5 fp32 64x64 workgroups per CU
+// instead of 3). Same box, wino_conv forward us 3-deep / 2-deep (bench/wino_gemm_ab.py,
+// profiles/r6_wino_gemm_stages_ab.jsonl): 8x8x256 51.0 / 49.9, 4x4x512 45.9 / 44.8, 14x14x256
+// 144.8 / 139.8, 7x7x512 120.9 / 120.1
+static int bgemm_stages() { return 2; }
+
 int psx_bgemm_f32_split(const float* A, const float* B, float* P, const void* zero, int M, int N, int Kd, int nb,
                         int s2, int cfg, hipStream_t st) {
   if (N % 64 || Kd < kKS<float> || (Kd & (Kd - 1)) || M < 1 || nb < 1 || s2 < 1 || (Kd / kKS<float>) % s2) return -2;
@@ -1197,6 +1226,7 @@ int psx_bgemm_f32_split(const float* A, const float* B, float* P, const void* ze
   a.n_pix_tiles = (M + p.BN - 1) / p.BN;
   a.splits = nb * s2;
   a.kps = Kd / kKS<float> / s2;
+  a.nstg = bgemm_stages();
   return nb * s2 > 1 ? dispatch2<float, 0, false>(p, a, st) : -2;
 }
 

@@ -125,6 +125,96 @@ def run_local(cfg, log=print, depart=None) -> dict:
     return {"server": sm, "workers": [getattr(w, "final_metrics", None) for w in workers]}
 
 
+def run_local_threads(cfg, steps: int, log=print, emit: bool = True) -> dict:
+    """Async PS on ONE device with W worker THREADS in real arrival order.
+
+    The loopback (run_local) interleaves its W workers' pushes round-robin, so every push there
+    has staleness exactly W - 1. Here each worker is a host thread with its own HIP stream, engine
+    and step graph and its own data shard; all of them fetch from and push into the native event
+    loop (csrc/server/event_loop.cpp, psx_loop_local_fetch / _push) as their steps complete, the
+    way the reference's 20-thread gRPC pool receives concurrent workers (server.py:171-186,
+    290-304): the staleness of a push is whatever number of other workers' updates landed since
+    its fetch. The workers share the GPU, so this measures the server's staleness behaviour and
+    its throughput over accepted pushes, not multi-GPU scaling.
+
+    Each worker's first step (its HIP graph capture) runs on the main thread, one worker after the
+    other (a capture must not overlap another thread's device-wide synchronize); then ``steps``
+    more per worker on the threads, timed. Returns the server metrics plus the timed region's
+    processed / accepted pushes and images per second counted over ACCEPTED pushes only."""
+    assert cfg.mode == "async"
+    cfg.resolve_overlap(1)
+    device = _device_for(0)
+    W = cfg.workers
+    model, layout, arena, counters = build_state(cfg)
+    server = ParameterServer(cfg, layout, arena, counters, device=device, total_workers=W, log=log)
+    train, test = make_datasets(cfg, device, model.fc.out_features)
+    mbox = CP.ShmMailbox(f"/psx_thr_{uuid.uuid4().hex[:12]}", nreply=1, owner=True)
+    loop = NativeServerLoop(server, None, mbox, {}, W, update_stream=None)
+    workers = []
+    try:
+        for w in range(W):
+            st = torch.cuda.Stream(device)
+            with torch.cuda.stream(st):
+                m = model if w == 0 else build_model(cfg.model, cfg.num_classes, seed=cfg.seed)
+                comp = make_compute(m, layout, cfg.batch_size, device, cfg.model, _wire_dtype(cfg), seed=cfg.seed + w,
+                                    use_graph=cfg.use_graph, dtype=cfg.dtype, deterministic=cfg.deterministic)
+                wk = Worker(cfg, comp, NativeLocalChannel(server, loop), train, test,
+                            worker_name=f"{cfg.worker_name}-{w}", rank=0, log=log, requested_id=w,
+                            steps_per_epoch=_common_steps(cfg, W, len(train)))
+                wk.connect_to_server()
+                wk.setup_data()
+                batches = wk.sampler.epoch_indices(0)
+                wk.fetch_parameters()  # first step: the graph capture, one worker at a time
+                wk.train_local_batch(batches[0])
+                wk.push_gradients()
+            workers.append((wk, st, batches))
+        torch.cuda.synchronize()
+        m0 = server.core.metrics()
+        go, errs = threading.Barrier(W + 1), []
+
+        def body(wk, st, batches):
+            try:
+                with torch.cuda.device(device), torch.cuda.stream(st):
+                    go.wait()
+                    wk.training_start_time = time.time()
+                    for i in range(1, steps + 1):
+                        wk.fetch_parameters()
+                        wk.train_local_batch(batches[i % len(batches)])
+                        wk.push_gradients()
+                    st.synchronize()
+            except Exception as e:  # noqa: BLE001 - reported after the join
+                errs.append(e)
+
+        ths = [threading.Thread(target=body, args=x, daemon=True) for x in workers]
+        for th in ths:
+            th.start()
+        go.wait()
+        t0 = time.perf_counter()
+        for th in ths:
+            th.join()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if errs:
+            raise errs[0]
+        m1 = server.core.metrics()
+        for wk, _, _ in workers:
+            wk.epoch_times.append(dt)
+            if emit:
+                wk.print_worker_statistics()  # WORKER_FINAL_METRICS (utils/results.py aggregates them)
+    finally:
+        for wk, _, _ in workers:
+            wk.channel.finished(wk.worker_id)
+        loop.join()
+        mbox.close()
+    done = int(m1.get("gradients_processed", 0)) - int(m0.get("gradients_processed", 0))
+    acc = int(m1.get("async_updates", 0)) - int(m0.get("async_updates", 0))
+    extra = {"images_per_second": round(acc * cfg.batch_size / dt, 2), "gpus": 1, "topology": "threads",
+             "timed_pushes": done, "timed_accepted_pushes": acc, "timed_seconds": round(dt, 4),
+             "images_per_second_all_pushes": round(done * cfg.batch_size / dt, 2)}
+    sm = server.final_metrics(emit=emit, extra=extra)
+    return {"server": sm, "workers": [getattr(w, "final_metrics", None) for w, _, _ in workers], "timed": extra}
+
+
 def _interleave(cfg, workers, server, log, depart=None):
     """W simulated workers on one device. Sync: every worker fetches the same version, the last
     push of a round triggers the averaged update. Async: pipelined round-robin (each worker

@@ -52,6 +52,14 @@ def main():
         r["fwd_v2_us"] = t_us(lambda: K.conv_fwd2(xh, wf, y, stats, ws, B, hw, hw, cp, cout, k, s, p, kg))
         if cin != 3:
             r["dgrad_v2_us"] = t_us(lambda: K.conv_dgrad2(dy, wd, dx, None, ws, B, hw, hw, cp, cout, k, s, p, kgd))
+            # as the step runs it: the consumer BN's backward sums in the epilogue + the masked store
+            o = torch.randn(B, hw, hw, cp, device="cuda").to(torch.bfloat16)
+            y1 = torch.randn(B, hw, hw, cp, device="cuda").to(torch.bfloat16)
+            saved = torch.stack([torch.randn(cp, device="cuda"), torch.rand(cp, device="cuda") + 0.5]).contiguous()
+            part = torch.zeros(K.STAT_SLOTS, 2, cp, device="cuda")
+            bst = K.bwd_stats_desc(part, o, y1, saved, mask_store=True)
+            r["dgrad_bst_v2_us"] = t_us(lambda: K.conv_dgrad2(dy, wd, dx, None, ws, B, hw, hw, cp, cout, k, s, p, kgd,
+                                                             bst=bst))
         out16 = torch.empty(cout * cin * k * k, dtype=torch.float16, device="cuda")
         spl2 = K.conv_wgrad2_splits(B, hw, hw, cp, cout, k, s, p, kg)
         part2 = torch.empty(spl2 * cout * kg, device="cuda")

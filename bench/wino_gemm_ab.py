@@ -1,9 +1,9 @@
 """Same-process A/B of the three-launch fp32 Winograd conv (wino.hip: input transform + 36 batched
 GEMMs on the conv_v2 mainloop + output transform) on ResNet-18's 8x8x256 / 4x4x512 layers and
-ResNet-50's 14x14x256 / 7x7x512 (batch 128), per PSX_TUNE setting given on the command line
-(e.g. "wino_s2=1" ""): forward and data gradient with BN sums, microseconds, and the
-batched GEMM alone (psx_bgemm_f32_split through wino_conv's shapes). One JSON line per layer and
-setting; the settings alternate per layer (same box, interleaved).
+ResNet-50's 14x14x256 / 7x7x512 (batch 128), forward with BN sums in microseconds, per PSX_TUNE
+setting given on the command line ("" = defaults; round 6 measured the batched GEMMs' LDS ring
+depth this way, profiles/r6_wino_gemm_stages_ab.jsonl). One JSON line per layer and setting; the
+settings alternate per layer (same box, interleaved).
 
   python bench/wino_gemm_ab.py "" "some_key=1"
 """

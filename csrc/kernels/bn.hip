@@ -403,13 +403,7 @@ DetRed det_for(const float* part) {
 using namespace psx;
 
 // workgroup cap of the folded-finalize apply launches (each workgroup recomputes the affine)
-static int fin_grid_cap() {
-  static int cap = [] {
-    const char* e = tune("fin_grid");
-    return e ? atoi(e) : 1024;  // 1024 vs 2048: 1.852 vs 1.867-1.875 ms/step (bench.py A/B)
-  }();
-  return cap;
-}
+static int fin_grid_cap() { return 1024; }  // 1024 vs 2048: 1.852 vs 1.867-1.875 ms/step (bench.py A/B)
 
 static int ew_grid(size_t nvec) {
   size_t g = (nvec + 255) / 256;

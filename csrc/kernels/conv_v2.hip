@@ -976,6 +976,9 @@ int tapr_bn(int R, int S, int stride, int pad, int H, int W, int IC, int OC, int
   return BN;
 }
 
+// (Round 6 measured split-K over the tap-reuse macro steps, partials through conv_splitk_epilogue,
+// at every tile width x 2-8 splits on ResNet-18's four 3x3 layers, bench/conv_layers.py: slower on
+// every one — the 4x4x512 layer's best 23.6 vs 21.2 us unsplit — profiles/r6_tapr_split_sweep.txt.)
 template <typename T, int MODE, bool RES>
 int dispatch_tapr(int bn, Conv2Args& a, hipStream_t st) {
   a.n_oc_tiles = a.OC / 64;
@@ -1059,7 +1062,7 @@ int conv_dgrad2_t(Conv2Args& a, float* ws, hipStream_t st) {
   a.n_pix_tiles = (a.npix + p.BN - 1) / p.BN;
   a.splits = p.splits;
   a.kps = (Kg / KS + p.splits - 1) / p.splits;
-  const bool parity = a.stride == 2 && a.log2_icc >= 3 && !tune("dgrad_s2_gather");
+  const bool parity = a.stride == 2 && a.log2_icc >= 3;
   if (p.splits > 1 && !ws && !parity) return -9;  // the parity-class path never splits K
   int e;
   if (a.stride == 1)
@@ -1070,10 +1073,6 @@ int conv_dgrad2_t(Conv2Args& a, float* ws, hipStream_t st) {
     // parity classes: each class GEMM covers dx pixels (2i+py, 2j+px), ~1/4 of them
     Plan q = plan_for(IC_fwd, (a.npix + 3) / 4, Kg / KS, sizeof(T) == 4);
     q.splits = 1;
-    // tile sweep overrides (PSX_TUNE dgrad_s2_bn / _WGM / _BM): the classes are short-K GEMMs
-    if (const char* e = tune("dgrad_s2_bn")) q.BN = atoi(e);
-    if (const char* e = tune("dgrad_s2_wgm")) q.WGM = atoi(e);
-    if (const char* e = tune("dgrad_s2_bm")) q.BM = atoi(e);
     if (IC_fwd % q.BM) q.BM = 64;
     a.n_oc_tiles = IC_fwd / q.BM;
     a.n_pix_tiles = (Nb * ((H + 1) / 2) * ((W + 1) / 2) + q.BN - 1) / q.BN;
@@ -1157,7 +1156,6 @@ int psx_conv_dgrad2_sc(const void* dy, const void* wd, void* dx, const void* res
   Conv2Args a{};
   if (dy_sc) {
     if (R != 3 || S != 3 || stride != 2 || pad != 1 || res || Kg_sc != OC_fwd || !wd_sc) return -11;
-    if (tune("dgrad_s2_gather")) return -11;
     a.in2 = dy_sc;
     a.w2 = wd_sc;
     a.Kg2 = Kg_sc;

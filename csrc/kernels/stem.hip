@@ -435,8 +435,6 @@ extern "C" {
 // weights [64][Kg], k = tap * cp + c. -11: not this shape (the caller runs psx_conv_fwd2 instead).
 int psx_stem_conv(const void* x, const void* wf, void* y, float* stats, const float* sshift, int Nb, int H, int W,
                   int cin, int cp, int OC, int Kg, int f32, hipStream_t st) {
-  if (const char* e = tune("stem_direct"))
-    if (e[0] == '0') return -11;
   if (cin != 3 || OC != 64 || cp != (f32 ? 4 : 8) || Kg < 9 * cp || W % 4) return -11;
   const long npix = (long)Nb * H * W;
   if (npix <= 0 || npix > (1L << 30)) return -2;
@@ -460,8 +458,6 @@ int psx_stem_conv(const void* x, const void* wf, void* y, float* stats, const fl
 // The output is 112 x 112 (IH = IW = 224). -11: not this shape (the caller runs psx_conv_fwd2).
 int psx_stem7_conv(const void* x, const void* wf, void* y, float* stats, const float* sshift, int Nb, int IH,
                    int IW, int cin, int cp, int OC, int Kg, int f32, hipStream_t st) {
-  if (const char* e = tune("stem_direct"))
-    if (e[0] == '0') return -11;
   if (cin != 3 || cp != (f32 ? 4 : 8) || OC != 64 || Kg < 49 * cp || IH != 224 || IW != 224 || Nb < 1) return -11;
   const unsigned grid = (unsigned)Nb * (kS7W / kS7Rows);
   const DetRed det = stats ? det_for(stats) : DetRed{};
@@ -481,8 +477,6 @@ int psx_stem7_conv(const void* x, const void* wf, void* y, float* stats, const f
 // psx_conv_wgrad2 query). -11: not this shape.
 int psx_stem7_wgrad(const float* x, const float* dy, float* part, int Nb, int IH, int IW, int cin, int cp, int OC,
                     int Kg, hipStream_t st) {
-  if (const char* e = tune("stem_direct"))
-    if (e[0] == '0') return -11;
   if (cin != 3 || cp != 4 || OC != 64 || Kg < 196 || IH != 224 || IW != 224 || Nb < 1) return -11;
   if (!part) return kS7WGrid;
   const int ntiles = Nb * (kS7W / kS7WRows);

@@ -244,7 +244,7 @@ int psx_wgrad_reduce_batch(int n, const float* const* part, void* const* out, co
 
 int psx_wgrad_reduce(const float* part, int splits, int OC, int Kg, int Cin, int IC, int R, int S, float scale,
                      void* out, int out_fp16, hipStream_t st) {
-  if (R * S <= 49 && IC % 16 == 0 && !tune("wgrad_reduce_v1")) {
+  if (R * S <= 49 && IC % 16 == 0) {
     const int CW = reduce2_cw(OC, IC);
     const dim3 grid(OC, IC / CW);
     if (out_fp16)
@@ -258,7 +258,7 @@ int psx_wgrad_reduce(const float* part, int splits, int OC, int Kg, int Cin, int
   if (((long)OC * Kg) % 256) return -2;
   const int grid = (int)(((long)OC * Kg) / 256);
   int sstride = 1;
-  if (grid < 128 && splits > 2 * kPre && !tune("wgrad_no_presum")) {
+  if (grid < 128 && splits > 2 * kPre) {
     // few columns, many slabs: spread the slab sum over grid x splits/kPre workgroups first
     const int groups = (splits + kPre - 1) / kPre;
     hipLaunchKernelGGL(wgrad_presum_kernel, dim3(grid, groups), dim3(256), 0, st, const_cast<float*>(part), splits,

@@ -666,17 +666,8 @@ struct WPlan {
   int BR, BC, NS, splits, sps;
 };
 
-// Share of the chip the weight gradient plans for (PSX_TUNE wg_share, default 1): below 1 when it runs
-// on a side stream next to the dgrad -> BN-backward chain (models/engine.py wg_stream).
-int wg_slots(int occ) {
-  static const double share = [] {
-    const char* e = tune("wg_share");
-    const double v = e ? atof(e) : 1.0;
-    return v > 0.05 && v <= 1.0 ? v : 1.0;
-  }();
-  const int s = (int)(256 * occ * share);
-  return s > 0 ? s : 1;
-}
+// Workgroup slots of the chip the weight gradient plans for (256 CUs x occupancy).
+int wg_slots(int occ) { return 256 * occ; }
 
 // LDS bytes per workgroup of an NS-stage BR x BC tile (64 pixels per stage).
 constexpr int wlds(int BR, int BC, int NS) { return NS * 64 * (BR + BC) * 2; }
@@ -926,18 +917,11 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
     const int e = psx_stem7_wgrad((const float*)x, (const float*)dy, part, Nb, H, W, 3, 4, OC, Kg, st);
     if (e != -11) return e;
   }
-  const char* w3env = tune("wg3");
-  const bool w3ok = R == 3 && S == 3 && stride == 1 && pad == 1 && IC % 64 == 0 && !(w3env && w3env[0] == '0');
+  const bool w3ok = R == 3 && S == 3 && stride == 1 && pad == 1 && IC % 64 == 0;
   if (f32 && w3ok && (W & (W - 1)) == 0 && (H & (H - 1)) == 0 && W <= 32 && W >= 2 && a.npix % 32 == 0 &&
       Kg == 9 * IC) {
-    // 3x3 stride-1 layers: fp32 tap-reuse kernel (PSX_TUNE wg3=0 disables)
+    // 3x3 stride-1 layers: fp32 tap-reuse kernel
     WPlan p = wplan3f(OC, IC, Kg, a.npix);
-    if (const char* e = tune("wg_bc")) p.BC = atoi(e);
-    if (const char* e = tune("wgf_splits"); e && atoi(e) > 0) {
-      const int steps = a.npix / 32;
-      p.sps = (steps + atoi(e) - 1) / atoi(e);
-      p.splits = (steps + p.sps - 1) / p.sps;
-    }
     if (OC % p.BC) return -2;
     if (!part) return p.splits;
     Wgrad3Args b{};
@@ -952,13 +936,6 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
     a.log2_icc = ilog2w(IC / 4);
     if (IC % 4 || (IC & (IC - 1))) return -2;
     WPlan p = wplanf(OC, Kg, a.npix);
-    if (const char* e = tune("wgf_br")) p.BR = atoi(e);
-    if (const char* e = tune("wgf_bc")) p.BC = atoi(e);
-    if (const char* e = tune("wgf_splits"); e && atoi(e) > 0) {  // sweeps
-      const int steps = (a.npix + 31) / 32;
-      p.sps = (steps + atoi(e) - 1) / atoi(e);
-      p.splits = (steps + p.sps - 1) / p.sps;
-    }
     if (Kg % p.BR || OC % p.BC) return -2;
     a.n_k_tiles = Kg / p.BR;
     a.n_oc_tiles = OC / p.BC;
@@ -972,20 +949,13 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
     else e = launch_w2f<64, 64>(a, st);
     return e ? -e : p.splits;
   }
-  // 3x3 stride-1 layers, tap-reuse kernel (PSX_TUNE wg3=0 disables): power-of-two rows (64-pixel
+  // 3x3 stride-1 layers, tap-reuse kernel: power-of-two rows (64-pixel
   // steps), or widths dividing 56 (ResNet-50: 56-pixel steps of whole rows, G)
   const bool pow2 = (W & (W - 1)) == 0 && (H & (H - 1)) == 0 && W <= 64 && W >= 2 && a.npix % 64 == 0;
   const bool gen = !pow2 && W >= 2 && 56 % W == 0 && a.npix % 56 == 0;
   if (w3ok && (pow2 || gen)) {
     const int pix = pow2 ? 64 : 56;
     WPlan p = wplan3(OC, IC, Kg, a.npix, pix);
-    if (const char* e = tune("wg_bc")) p.BC = atoi(e);
-    if (const char* e = tune("wg_ns")) p.NS = atoi(e) >= 6 ? 6 : 3;
-    if (const char* e = tune("wg_splits")) {
-      const int steps = a.npix / pix;
-      p.sps = (steps + atoi(e) - 1) / atoi(e);
-      p.splits = (steps + p.sps - 1) / p.sps;
-    }
     if (OC % p.BC) return -2;
     if (!part) return p.splits;
     Wgrad3Args b{};
@@ -1007,21 +977,9 @@ int psx_conv_wgrad2(const void* x, const void* dy, float* part, const void* zero
   // Tile: the round-5 sweep (bench/r50_wgrad_tiles.py, profiles/r5_r50_wgrad_tiles.jsonl, ResNet-50's
   // 1x1 layers): 64 (k) x 128 (oc) wins by 10-20 % on every layer up to 28x28 with OC % 128 == 0
   // (128x512x28 42.0 -> 34.7 us, 1024x2048x14/s2 64.3 -> 55.4), 64x64 on the 56x56 ones (the
-  // model's choice there); PSX_TUNE wg_plan=model: the cost model alone (round 4).
-  static const bool model_only = [] {
-    const char* e = tune("wg_plan");
-    return e && !strcmp(e, "model");
-  }();
-  const bool t128 = !model_only && OC % 128 == 0 && Kg % 64 == 0 && a.npix <= 128 * 28 * 28;
+  // model's choice there).
+  const bool t128 = OC % 128 == 0 && Kg % 64 == 0 && a.npix <= 128 * 28 * 28;
   WPlan p = t128 ? wplan(OC, Kg, a.npix, 64, 128) : wplan(OC, Kg, a.npix);
-  // experiment overrides (tile sweep): PSX_TUNE wg_br / PSX_TUNE wg_bc / PSX_TUNE wg_splits
-  if (const char* e = tune("wg_br")) p.BR = atoi(e);
-  if (const char* e = tune("wg_bc")) p.BC = atoi(e);
-  if (const char* e = tune("wg_splits")) {
-    const int steps = (a.npix + 63) / 64;
-    p.sps = (steps + atoi(e) - 1) / atoi(e);
-    p.splits = (steps + p.sps - 1) / p.sps;
-  }
   if (Kg % p.BR || OC % p.BC) return -2;
   a.n_k_tiles = Kg / p.BR;
   a.n_oc_tiles = OC / p.BC;

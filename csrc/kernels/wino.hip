@@ -631,15 +631,12 @@ int psx_wino_conv(const float* x, const float* U, float* y, const float* res, fl
   return (int)hipGetLastError();
 }
 
-// Weight-gradient GEMM tile (BR = BC): 64 (3 workgroups per CU) unless PSX_TUNE wino_wbr=128.
-static int wino_wtile(int C, int K) {
-  if (const char* e = tune("wino_wbr"); e && atoi(e) == 128 && C % 128 == 0 && K % 128 == 0) return 128;
-  return 64;
-}
+// Weight-gradient GEMM tile (BR = BC): 64 (3 workgroups per CU).
+static int wino_wtile(int, int) { return 64; }
 
 // Tile-range splits q of the weight-gradient GEMM: 36 * q * (C/BR) * (K/BC) workgroups, each
 // over T / q tiles (a multiple of 32): the smallest q reaching 1024 workgroups while a split keeps
-// >= 256 tiles, at most 8 (PSX_TUNE wino_wq_max). Same-box sweep with the split output transform (B=128,
+// >= 256 tiles, at most 8. Same-box sweep with the split output transform (B=128,
 // us incl. dy transform, q = 1 / 2 / 4 / 8 / 16): 32x32x64 244 / 134 / 79 / 69 / 83, 16x16x128
 // 72 / 62 / 51 / 48 / 69, 8x8x256 51 / 46 / 47 / 55 / 81, 4x4x512 47 / 54 / 75 (bench/wino_fused_ab.py).
 // 0 = not applicable.
@@ -648,13 +645,7 @@ int psx_wino_wgrad_q(int N, int H, int W, int C, int K) {
   if (!psx_wino_ok(H, W, C, K) || T % 32) return 0;
   const int bt = wino_wtile(C, K);
   int q = 1;
-  static const int qmax = [] {
-    const char* e = tune("wino_wq_max");
-    return e && atoi(e) > 0 ? atoi(e) : 8;
-  }();
-  if (const char* e = tune("wino_wq"); e && atoi(e) > 0) q = atoi(e);
-  else
-    while (36L * q * (C / bt) * (K / bt) < 1024 && q < qmax && T % (32 * 2 * q) == 0 && T / (2 * q) >= 256) q *= 2;
+  while (36L * q * (C / bt) * (K / bt) < 1024 && q < 8 && T % (32 * 2 * q) == 0 && T / (2 * q) >= 256) q *= 2;
   return T % (32 * q) ? 0 : q;
 }
 

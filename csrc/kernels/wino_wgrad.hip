@@ -255,18 +255,14 @@ using namespace psx;
 extern "C" {
 
 // Tile ranges q of the fused weight gradient (0: not applicable): ~512 workgroups, ranges of
-// whole groups of 16 tiles (four per wave) and >= 64 tiles. PSX_TUNE wino_wgf_q overrides.
+// whole groups of 16 tiles (four per wave) and >= 64 tiles.
 int psx_wino_wgrad_fused_q(int N, int H, int W, int C, int K) {
   if (H % 4 || W % 4 || C % 16 || K % 16 || C < 16 || K < 16) return 0;
   const int T = N * (H / 4) * (W / 4);
   if (T % 16) return 0;
   const long nblk = (long)(K / 16) * (C / 16);
   int q = 1;
-  if (const char* e = tune("wino_wgf_q"); e && atoi(e) > 0) {
-    q = atoi(e);
-  } else {
-    while (nblk * q * 2 <= 512 && T % (16 * q * 2) == 0 && T / (q * 2) >= 64) q *= 2;
-  }
+  while (nblk * q * 2 <= 512 && T % (16 * q * 2) == 0 && T / (q * 2) >= 64) q *= 2;
   return (T % (16 * q) == 0 && nblk * q < (1L << 30)) ? q : 0;
 }
 

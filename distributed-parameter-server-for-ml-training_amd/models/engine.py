@@ -31,7 +31,7 @@ import numpy as np
 import torch
 
 from ..ops import kernels as K
-from ..utils.tune import tune, tune_flag, tune_int
+from ..utils.tune import tune, tune_flag
 from .layout import ParamLayout
 from .resnet import Bottleneck, BasicBlock
 
@@ -188,24 +188,25 @@ class HipResNetEngine:
         self.graph = None
         self.graphs = None
         self.segments = None  # backward split points (set_segments), None = one segment
-        # BN finalize inside the producing launch (csrc/kernels/bnfin.hpp); 0 = separate kernels
-        self.fuse_fin = tune_flag("fuse_bnfin", False)
+        # BN finalize inside the producing launch (csrc/kernels/bnfin.hpp): off (tests switch the
+        # attribute: tests/test_engine_gpu.py)
+        self.fuse_fin = False
         # BN-backward sums from the dgrad epilogue (skips the separate bn_bwd_reduce pass where a
         # dgrad produces the BN's input gradient): neutral with 32 stat slots + separate finalize
         # (2.215 vs 2.217 ms/step), a small win with 8 slots + folded finalize (1.996/2.000 vs
-        # 2.010/2.006 ms/step, two same-box A/B pairs), so on by default (PSX_TUNE fuse_bnbwd=0: off)
+        # 2.010/2.006 ms/step, two same-box A/B pairs), so on (the attribute is a test switch)
         # BN finalize folded into the consuming apply launches (bnfin.hpp bn_fin_lds): every apply
         # workgroup re-derives the affine/coefficients from the stat slots, removing 40 finalize
         # launches per step. With 32 slot rows it measured slower (2.18 vs 2.10 ms/step); with 8
-        # rows (csrc/kernels/common.hpp) it wins: 1.999 vs 2.019 ms/step. PSX_TUNE bnfin_apply=0: off
-        self.fin_apply = not self.fuse_fin and tune_flag("bnfin_apply", True)
-        self.fuse_bnbwd = tune_flag("fuse_bnbwd", True)
+        # rows (csrc/kernels/common.hpp) it wins: 1.999 vs 2.019 ms/step.
+        self.fin_apply = not self.fuse_fin
+        self.fuse_bnbwd = True
         self._prereduced = set()
         # with the fused sums the dgrad epilogue already reads the ReLU mask operand o: it stores
         # dz = g*[o > 0] instead of g (bwd_stats_desc mask_store), the BN-backward apply then runs
         # without o (one activation read less per BN layer) and dz doubles as the identity
-        # shortcut's gradient (no dzout copy). PSX_TUNE mask_store=0: off
-        self.mask_store = self.fuse_bnbwd and tune_flag("mask_store", True)
+        # shortcut's gradient (no dzout copy)
+        self.mask_store = self.fuse_bnbwd
         # BN-backward applies folded into the fused Winograd data gradient + dy transform (_bn_bwd_to)
         self.bwd_fold = self.mask_store and tune_flag("wino_bwdfold", True)
         self._bwd_fold = {}
@@ -221,13 +222,12 @@ class HipResNetEngine:
         if ws == "auto":
             ws = "0" if (self.f32 and max(self.spec.in_hw) <= 64) else "1"
         self.wg_stream = torch.cuda.Stream(device=self.dev) if ws == "1" else None
-        self.fold_sc = tune_flag("dgrad_fold_sc", True)
+        # the stride-2 block's 1x1 shortcut data gradient folded into the 3x3 one's launch
+        self.fold_sc = True
         # the CIFAR stem on the direct vector-ALU kernel (csrc/kernels/stem.hip): fp32 27.4 -> 19.5 us
-        # in isolation (bench/stem_probe.py); step A/B within noise, bf16 unmeasured in isolation, so
-        # "auto" = fp32 only
-        sd = tune("stem_direct", "auto")
-        # the direct stems: fp32 (CIFAR 3x3 and ImageNet 7x7) and the bf16 ImageNet 7x7 (stem.hip)
-        self.stem_direct = sd == "1" or (sd == "auto" and (self.f32 or self.spec.stem_conv.k == 7))
+        # in isolation (bench/stem_probe.py); step A/B within noise, bf16 unmeasured in isolation.
+        # The direct stems: fp32 (CIFAR 3x3 and ImageNet 7x7) and the bf16 ImageNet 7x7 (stem.hip)
+        self.stem_direct = self.f32 or self.spec.stem_conv.k == 7
         # the later stages' Winograd weight transforms overlap the first stage's forward on the
         # side stream; without one they stay on the compute stream (a stream of their own measured
         # 3.36 vs 3.28 ms/step — a forked branch at the step start costs more than the overlap
@@ -235,8 +235,6 @@ class HipResNetEngine:
         self.wt_stream = self.wg_stream
         self._wg_batch = None
         self._fins = {}
-        # conv-operand unpack: "tiles" (flat grid, fp32 arena or bf16 image source) or "tap"
-        self.unpack_impl = tune("unpack_impl", "tiles")
         self.wsrc = None        # bf16 weight image to unpack from (set_weight_source), None = arena
         self.pre_unpack = None
         self._build()
@@ -408,9 +406,9 @@ class HipResNetEngine:
 
     def _plan_wino(self):
         """fp32 Winograd F(4x4,3x3) (csrc/kernels/wino.hip) for the 3x3 / stride-1 layers: forward
-        and data gradient on images up to PSX_TUNE wino_maxhw (default 64: every 3x3 stride-1 layer of
+        and data gradient on images up to 64x64 (every 3x3 stride-1 layer of
         ResNet-18 CIFAR and ResNet-50's 56x56 / 28x28 ones; R50 fp32 top-k 3,060 -> 3,188 img/s),
-        weight gradient (PSX_TUNE wino_wgrad=1, default) up to PSX_TUNE wino_wgrad_maxhw
+        weight gradient up to 64x64
         (default 16: on 32x32 the direct tap-reuse kernel is faster, 101 vs 129 us). Same-box
         per-layer A/B in profiles/r2s4_wino_*.jsonl. Per layer: the transformed forward weights
         U [cout][36][cin] and data-gradient weights U' [cin][36][cout] (rebuilt by unpack() every
@@ -419,7 +417,7 @@ class HipResNetEngine:
         like every other producer (wino_out_kernel + bnfin.hpp DetRed). Not for bf16. PSX_TUNE wino=0:
         direct kernels everywhere. Layers with 64 / 128 input channels (ResNet-18's 32x32 and 16x16
         stages) run forward and data gradient as ONE fused launch each (wino_fused.hip: the
-        transforms inside the GEMM, V / P never in HBM; PSX_TUNE wino_fuse=0: the three-launch path;
+        transforms inside the GEMM, V / P never in HBM; the other layers take the three-launch path;
         bench/wino_fused_ab.py: 32x32x64 fwd / dgrad 80 / 95 -> 58 / 63 us, 16x16x128 59 / 62 -> 50 / 51).
         The fused forward still writes V where the Winograd weight gradient reads it."""
         self.wino_layers = {}
@@ -430,21 +428,20 @@ class HipResNetEngine:
         self._xfold = {}        # conv -> (pre-BN y, BN affine): its input is relu(BN(y)), never written
         if not self.f32 or not tune_flag("wino", True):
             return
-        fuse = tune_flag("wino_fuse", True)
-        # fused weight gradient (wino_wgrad.hip) on images of at least PSX_TUNE wino_wgf_minhw: same box,
+        fuse = True  # the fused single-launch kernel (wino_fused.hip) wherever it applies
+        # fused weight gradient (wino_wgrad.hip) on images of at least 16x16: same box,
         # B = 128, us incl. output transform, fused vs three-launch (bench/wino_wgrad_ab.py,
         # profiles/r4_wino_wgrad_ab.jsonl): 32x32x64 58.4 vs 71.2, 16x16x128 55.3 vs 46.9 (+ the
         # forward's V store the three-launch path needs, ~7), 8x8x256 53.7 vs 43.2, 4x4x512 61.7 vs
         # 44.1. In the step (side stream; the forward's V store is on the critical path) same box:
         # off 3.568, >= 32 3.412, >= 16 3.363-3.372 ms/step (profiles/r4_numbers.jsonl)
-        wgf = tune_flag("wino_wgf", True)
-        wgf_minhw = tune_int("wino_wgf_minhw", 16)
-        maxhw = tune_int("wino_maxhw", 64)
-        wg = tune_flag("wino_wgrad", True)
+        wgf, wgf_minhw = True, 16
+        maxhw = 64
+        wg = True
         # Winograd weight gradient up to 64x64 images: ResNet-50's 56x56 3x3 layers take the fused
         # one (their direct alternative is wgrad2f: the tap-reuse kernel needs power-of-two rows):
         # same box 36.8 -> 36.4 ms/step (profiles/r5_numbers.jsonl r5_call6)
-        wg_maxhw = tune_int("wino_wgrad_maxhw", 64)
+        wg_maxhw = 64
         B = self.B
         s_main = s_d = s_part = 0
         for cs in all_convs(self.spec):
@@ -461,7 +458,7 @@ class HipResNetEngine:
             self.wino_fused[cs.name] = (ff, fd)
             uf = self._f32((40 if ff else 36) * cs.cout * cs.cp)
             ud = self._f32((40 if fd else 36) * cs.cout * cs.cp) if cs.need_dgrad else None
-            # fused weight gradient (wino_wgrad.hip, PSX_TUNE wino_wgf=1): transforms x and dy itself, so
+            # fused weight gradient (wino_wgrad.hip): transforms x and dy itself, so
             # the forward keeps no V and no D is formed
             qf = (K.wino_wgrad_fused_q(B, cs.h, cs.w, cs.cp, cs.cout)
                   if q > 0 and wgf and min(cs.h, cs.w) >= wgf_minhw else 0)
@@ -496,7 +493,7 @@ class HipResNetEngine:
         self.wino_wpart = self._f32(max(1, s_part))
         # the first block's first conv's weight gradient runs on the compute stream, concurrently
         # with the side stream's (_bwd_stem): its own scratch
-        self.tail_split = (self.wg_stream is not None and tune_flag("tail_split", True)
+        self.tail_split = (self.wg_stream is not None
                            and bool(self.spec.blocks) and self.spec.blocks[0].convs[0].name in self.wino_wgrad)
         self.wino_wd2 = self._f32(max(1, s_d)) if self.tail_split else None
         self.wino_wpart2 = self._f32(max(1, s_part)) if self.tail_split else None
@@ -511,7 +508,7 @@ class HipResNetEngine:
         if getattr(self, "_wino_wb_key", None) != key:
             convs = [cs for cs in all_convs(self.spec) if cs.name in self.wino_layers]
             hw0 = max((cs.h for cs in convs), default=0)
-            split = self.wt_stream is not None and tune_flag("wino_wsplit", True)
+            split = self.wt_stream is not None
             early, late = [], []
             self._wino_late = set()
             for cs in convs:
@@ -735,7 +732,7 @@ class HipResNetEngine:
 
     def _dgrad(self, cs: ConvSpec, dy, dx, res=None, bn_next=None, sc=None):
         """bn_next = (BNSpec, o, y, two|None): the BN whose backward consumes dx; with conv v2 its
-        reduction (sum dz, sum dz*xhat) is produced by the dgrad epilogue (PSX_TUNE fuse_bnbwd).
+        reduction (sum dz, sum dz*xhat) is produced by the dgrad epilogue (fuse_bnbwd).
         sc = (shortcut ConvSpec, its output gradient): fold the block's 1x1 / stride-2 shortcut
         data gradient into this 3x3 / stride-2 launch; returns False (nothing launched) when the
         layer cannot fold."""
@@ -861,9 +858,6 @@ class HipResNetEngine:
         """OIHW master weights -> bf16 implicit-GEMM operands. The source is the fp32 arena, or
         the bf16 weight image ``self.wsrc`` when the fetch delivers one (parallel/codec.py
         WeightWire: the server's apply wrote those bits; identical operands either way)."""
-        if self.unpack_impl == "tap" and not self.f32:  # the original per-tap kernel (A/B: PSX_TUNE unpack_impl=tap)
-            K.param_unpack(arena, self.descs, self.ndesc, self.wbuf)
-            return
         src = self.wsrc if self.wsrc is not None else arena
         K.param_unpack_tiles(src, self.descs, self.ndesc, self.ntiles, self.wbuf, scatter=self.small_scatter)
         if self.wino_layers:
@@ -882,7 +876,6 @@ class HipResNetEngine:
         if img is not None:
             assert not self.f32, "the fp32 engine unpacks its operands from the fp32 arena (fetch codec fp32)"
             assert img.dtype == torch.bfloat16 and img.numel() >= self.layout.param_numel
-            assert self.unpack_impl != "tap", "the per-tap unpack kernel reads fp32 only"
         assert scatter is None or (img is not None and pre_unpack is None)
         self.wsrc = img
         self.pre_unpack = pre_unpack

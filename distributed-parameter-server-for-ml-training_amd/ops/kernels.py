@@ -14,7 +14,7 @@ import ctypes as C
 
 import torch
 
-from ..utils.tune import tune, tune_int
+from ..utils.tune import tune
 from ._lib import check, kernels, ptr, stream_ptr
 
 def conv_out_hw(h: int, w: int, k: int, stride: int, pad: int):
@@ -227,9 +227,6 @@ def wino_wgrad_q(nb, h, w, c, k) -> int:
     return int(kernels().psx_wino_wgrad_q(nb, h, w, c, k))
 
 
-WINO_CFG = tune_int("wino_cfg", 0)
-
-
 def wino_weights(w_oihw, u, k, c, flip=False):
     """Winograd F(4x4,3x3) weight transform (csrc/kernels/wino.hip): forward U[k][36][c] from the
     fp32 OIHW weights, or (flip) the data-gradient operand U[c][36][k] of rot180(w)^T."""
@@ -305,7 +302,7 @@ def wino_conv(x, u, y, res, stats, v, p, nb, h, w, c, k, cfg=None, bst: "BwdStat
     assert v.numel() >= wino_v_floats(nb, h, w, c) and p.numel() >= wino_p_floats(nb, h, w, c, k)
     assert res is None or res.numel() == y.numel()
     check(kernels().psx_wino_conv(ptr(x), ptr(u), ptr(y), ptr(res), ptr(stats), ptr(v), ptr(p), ptr(zero_page(x.device)),
-                                  nb, h, w, c, k, WINO_CFG if cfg is None else cfg,
+                                  nb, h, w, c, k, 0 if cfg is None else cfg,
                                   C.byref(bst) if bst is not None else None,
                                   ptr(bn_in[0]) if bn_in is not None else None,
                                   C.byref(bn_in[1]) if bn_in is not None else None, ptr(sshift), stream_ptr()),
@@ -385,7 +382,7 @@ WRBATCH_MAX = 4
 
 def wgrad_reduce_batchable(ic, k) -> bool:
     """The v2 reduce handles the layer (what wgrad_reduce_batch requires)."""
-    return k * k <= 49 and ic % 16 == 0 and tune("wgrad_reduce_v1") is None
+    return k * k <= 49 and ic % 16 == 0
 
 
 def wgrad_reduce_batch(items, scale, out_fp16: bool):

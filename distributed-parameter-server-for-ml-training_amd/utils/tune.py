@@ -1,16 +1,19 @@
-"""Developer tuning overrides: the engine's A/B switches and the kernel planners' tile sweeps in
-ONE environment variable, ``PSX_TUNE="key=value[,key=value...]"`` (a bare key means "1"), read
-by this module and by the native planners (csrc/kernels/common.hpp ``tune``). Production runs
-set nothing; every default is the measured-best path. Keys (lower case):
+"""Developer overrides in ONE environment variable, ``PSX_TUNE="key=value[,key=value...]"`` (a
+bare key means "1"), read by this module and by the native planners (csrc/kernels/common.hpp
+``tune``). Production runs set nothing; every default is the measured-best path. Round 6 cut the
+set from ~50 keys to the 12 below, each exercised by a test (the A/B switches whose other side
+was measured slower, and the tile-sweep overrides of the retired sweep scripts, are gone):
 
-  engine (models/engine.py): wino (0: direct kernels), wino_fuse, wino_wgf, wino_wgf_minhw,
-    wino_maxhw, wino_wgrad, wino_wgrad_maxhw, wino_bnfold, wino_bwdfold, wino_wsplit,
-    wgrad_stream (0/1/auto), wgrad_rbatch, tail_split, dgrad_fold_sc, stem_direct (0/1/auto),
-    fuse_bnfin, bnfin_apply, fuse_bnbwd, mask_store, unpack_impl (tiles/tap), wino_cfg
-  native planners: cv_bm, cv_bn, cv_wgm, cv_splits, cv_f32_128, cv_tapr, cv_tapr_halo,
-    cv_tapr_bn, dgrad_s2_bm, dgrad_s2_bn, dgrad_s2_wgm, dgrad_s2_gather, wg_br, wg_bc, wg_ns,
-    wg_splits, wg3, wg_share, wgf_br, wgf_bc, wgf_splits, wino_wbr, wino_wq, wino_wq_max,
-    wino_wgf_q, wgrad_reduce_v1, wgrad_no_presum, fin_grid
+  engine (models/engine.py):
+    wino=0            direct kernels instead of Winograd (tests/test_wino_gpu.py, test_fp32_gpu.py)
+    wino_bnfold=0     BN + ReLU not folded into the next Winograd conv (tests/test_wino_gpu.py)
+    wino_bwdfold=0    BN-backward applies not folded (tests/test_wino_fused_gpu.py)
+    wgrad_stream=0|1  weight gradients on / off the side stream (default auto;
+                      tests/test_deterministic_gpu.py)
+    wgrad_rbatch=0    per-layer weight-gradient reductions (tests/test_wgrad_batch_gpu.py)
+  conv tile plan (csrc/kernels/conv_v2.hip; tests/test_conv_v2_gpu.py, tests/test_fp32_gpu.py run
+  every tile instantiation through them):
+    cv_bm, cv_bn, cv_wgm, cv_splits, cv_tapr=0, cv_tapr_bn, cv_tapr_halo=1
 """
 from __future__ import annotations
 

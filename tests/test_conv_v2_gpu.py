@@ -127,19 +127,20 @@ def test_conv2_tap_reuse(shape, bn, monkeypatch):
     start mid-row, any width: the ResNet-50 56/28/14/7 layers; forced on the power-of-two shapes
     too): fwd (+ BN statistics) and dgrad (+ residual, + fused BN-backward sums) against torch fp32."""
     n, cin, cout, hw, k, s, p = shape
+    extra = ""
     if bn == "halo":
-        monkeypatch.setenv("PSX_TUNE", "cv_tapr_halo=1")
+        monkeypatch.setenv("PSX_TUNE", "cv_tapr_halo=1" + extra)
     elif (n * hw * hw) % bn or bn % hw:
         pytest.skip("tile does not hold whole image rows")
     else:
-        monkeypatch.setenv("PSX_TUNE", f"cv_tapr_bn={bn}")
+        monkeypatch.setenv("PSX_TUNE", f"cv_tapr_bn={bn}" + extra)
     torch.manual_seed(4)
     x = torch.randn(n, cin, hw, hw, device=DEV).to(torch.bfloat16).float()
     w = (torch.randn(cout, cin, k, k, device=DEV) / (cin * k * k) ** 0.5).to(torch.bfloat16).float()
     wf, wd, cp, kg, kgd = make_operands(w)
     y = torch.empty(n, hw, hw, cout, dtype=torch.bfloat16, device=DEV)
     stats = torch.zeros(K.STAT_SLOTS, 2, cout, device=DEV)
-    K.conv_fwd2(to_nhwc(x, cp), wf, y, stats, None, n, hw, hw, cp, cout, k, s, p, kg)
+    K.conv_fwd2(to_nhwc(x, cp), wf, y, stats, _ws(n, hw, hw, cout, kg), n, hw, hw, cp, cout, k, s, p, kg)
     ref = F.conv2d(x, w, stride=s, padding=p).permute(0, 2, 3, 1)
     assert _rel(y, ref) < 1e-2, (shape, bn)
     yq = y.float().reshape(-1, cout)
@@ -154,7 +155,7 @@ def test_conv2_tap_reuse(shape, bn, monkeypatch):
     saved = torch.stack([0.1 * torch.randn(cp, device=DEV), 1.0 + torch.rand(cp, device=DEV)])
     part = torch.zeros(K.STAT_SLOTS, 2, cp, device=DEV)
     bst = K.bwd_stats_desc(part, o, y1, saved)
-    K.conv_dgrad2(to_nhwc(dy, cout), wd, dx, res, None, n, hw, hw, cp, cout, k, s, p, kgd, bst=bst)
+    K.conv_dgrad2(to_nhwc(dy, cout), wd, dx, res, _ws(n, hw, hw, cp, kgd), n, hw, hw, cp, cout, k, s, p, kgd, bst=bst)
     assert _rel(dx[..., :cin], dref + res[..., :cin].float()) < 1e-2, (shape, bn)
     dz = (dx.float() * (o.float() > 0)).reshape(-1, cp)
     xhat = ((y1.float().reshape(-1, cp) - saved[0]) * saved[1])

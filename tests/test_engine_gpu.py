@@ -118,7 +118,7 @@ def test_graph_replay_matches_eager(setup):
 def test_fused_bn_finalize_matches_separate_kernels(setup, mode):
     """Folded BN finalize gives exactly what the separate finalize kernels compute from the same
     slot sums (every BN layer, two consecutive steps). conv_epilogue: last workgroup of the
-    producing launch (PSX_TUNE fuse_bnfin); apply (default): every workgroup of the consuming apply
+    producing launch (engine.fuse_fin); apply (default): every workgroup of the consuming apply
     launch (bnfin.hpp bn_fin_lds), with the backward sums from bn_bwd_reduce or from the dgrad
     epilogue (apply_bnbwd). Also: running statistics updated exactly once per step, and the
     block-internal apply outputs equal bn_apply with the recomputed affine.
@@ -183,7 +183,7 @@ def test_fused_bn_finalize_matches_separate_kernels(setup, mode):
 
 
 def test_dgrad_fused_bn_backward_sums_match_reduce_kernel(setup):
-    """PSX_TUNE fuse_bnbwd: the BN-backward slot sums produced in the dgrad epilogue equal what the
+    """engine.fuse_bnbwd: the BN-backward slot sums produced in the dgrad epilogue equal what the
     separate bn_bwd_reduce pass computes from the stored dgrad output."""
     model, layout, arena, eng, x, y = setup
     n = 256

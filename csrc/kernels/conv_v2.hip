@@ -26,15 +26,11 @@
 #ifndef PSX_CONV_PF
 #define PSX_CONV_PF 1
 #endif
-// bf16: the same double buffer in the tap-reuse loop, and 256-pixel tiles (64x64 wave tiles)
-// where they keep >= 256 workgroups. Same-box A/B (bf16 layers, us fwd/dgrad): 32x32 30.9/23.0
-// -> 25.5/22.0, 16x16 22.9/19.4 -> 18.9/17.3, 4x4 23.5/22.0 -> 21.1/19.7; bench --dtype bf16
-// 1.858 -> 1.81-1.83 ms/step (the tiles alone: 1.838)
+// bf16: the same double buffer in the tap-reuse loop. Same-box A/B (bf16 layers, us fwd/dgrad):
+// 32x32 30.9/23.0 -> 25.5/22.0, 16x16 22.9/19.4 -> 18.9/17.3, 4x4 23.5/22.0 -> 21.1/19.7 (the
+// bf16 tile widths: tapr_bn)
 #ifndef PSX_CONV_PF_BF16
 #define PSX_CONV_PF_BF16 1
-#endif
-#ifndef PSX_TAPR_BF16_256
-#define PSX_TAPR_BF16_256 1
 #endif
 // epilogue rows whose global loads are issued together (A/B builds: -D PSX_EPI_U=1)
 #ifndef PSX_EPI_U
@@ -964,8 +960,13 @@ int tapr_bn(int R, int S, int stride, int pad, int H, int W, int IC, int OC, int
   // vs 94/92 — and lose below (8x8x256: 148 vs 89); the f32 MFMA work per stage then hides the
   // DMA wait at one workgroup per CU
   int BN = force ? force : 64;
-  if (!force && (f32 || PSX_TAPR_BF16_256) && npix % 256 == 0 && 256 % W == 0 && (long)(npix / 256) * (OC / 64) >= 256)
-    BN = 256;
+  if (!force && f32 && npix % 256 == 0 && 256 % W == 0 && (long)(npix / 256) * (OC / 64) >= 256) BN = 256;
+  // bf16: 128-pixel tiles (two workgroups per CU: one's epilogue — the BN statistics or the BN-backward
+  // sums — runs under the other's mainloop) where they fill two rounds of the chip, 64 below. Round 6,
+  // same box (bench/conv_layers.py, profiles/r6_tapr_split_sweep.txt, us fwd / dgrad + BN-backward sums):
+  // 32x32x64 24.3 / 31.8 (256-pixel tiles, the round-5 choice) -> 21.5 / 26.9, 16x16x128 18.3 / 20.1 ->
+  // 17.2 / 20.6; the bf16 step 1.660 -> 1.605 ms (3 interleaved pairs, profiles/r6_numbers.jsonl)
+  if (!force && !f32 && npix % 128 == 0 && 128 % W == 0 && (long)(npix / 128) * (OC / 64) >= 512) BN = 128;
 #if PSX_TAPR_F32_128
   // fp32 with the register double buffer: 128-pixel tiles (two workgroups per CU, one's epilogue
   // under the other's mainloop) where they fill two full rounds of the chip. Same-box A/B: 32x32x64

@@ -330,13 +330,19 @@ class Worker:
         self.global_step_cache = self.channel.fetch(self.worker_id, self.compute.local_arena)
         return self.global_step_cache
 
-    # sync shrink + top-k: the error-feedback residual as it was before each of the last RSNAP
-    # rounds' encodes (a rollback to round R restores the residual of round R; the host runs at
-    # most the compute's staging ring — 4 steps — ahead of the device, so 8 slots cover every
-    # rollback target)
-    RSNAP = 8
+    # sync shrink + top-k: the error-feedback residual as it was before each of the last few
+    # rounds' encodes (a rollback to round R restores the residual of round R). A rollback target
+    # is at most (host run-ahead) + (rounds the server keeps in flight) rounds back: the host runs
+    # at most len(compute._meta_ring) steps ahead of the device (HipCompute._set_batch blocks on
+    # the ring) and the server keeps at most RSERVER rounds in flight (sync_loop.cpp NSLOT = 3,
+    # parallel/runner.py _PyRollback), so _rsnap_depth() slots cover every target.
+    RSERVER = 3
     _rsnap = None
     _pushes = 0
+
+    def _rsnap_depth(self) -> int:
+        ring = len(getattr(self.compute, "_meta_ring", ())) or 4
+        return ring + self.RSERVER + 1
 
     def push_gradients(self):
         bufs = None
@@ -356,9 +362,10 @@ class Worker:
     def _snapshot_resid(self):
         r = self.topk.resid
         if self._rsnap is None:
-            self._rsnap = ([torch.empty_like(r) for _ in range(self.RSNAP)], [-1] * self.RSNAP)
+            d = self._rsnap_depth()
+            self._rsnap = ([torch.empty_like(r) for _ in range(d)], [-1] * d)
         bufs, rounds = self._rsnap
-        k = self._pushes % self.RSNAP
+        k = self._pushes % len(bufs)
         bufs[k].copy_(r)
         rounds[k] = self._pushes
 
@@ -368,7 +375,7 @@ class Worker:
             self._pushes = rounds_kept
             return
         bufs, rounds = self._rsnap
-        k = rounds_kept % self.RSNAP
+        k = rounds_kept % len(bufs)
         if rounds[k] == rounds_kept:
             self.topk.resid.copy_(bufs[k])
         elif rounds_kept != self._pushes:

@@ -20,8 +20,10 @@ def main():
     ap.add_argument("--n", type=int, default=11_220_132)
     ap.add_argument("--ratio", type=float, default=0.01)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--dtype", choices=["both", "fp32", "fp16"], default="both")
     a = ap.parse_args()
-    for dt in (torch.float32, torch.float16):
+    dts = {"both": (torch.float32, torch.float16), "fp32": (torch.float32,), "fp16": (torch.float16,)}[a.dtype]
+    for dt in dts:
         g = (torch.randn(a.n, device="cuda") * 1e-3).to(dt)
         c = T.TopKCodec(a.n, a.ratio, "cuda")
         for _ in range(3):
@@ -38,8 +40,9 @@ def main():
             T.decode_add(c.payload, dst, 1.0, c.kcap)
         torch.cuda.synchronize()
         dec = (time.perf_counter() - t0) / a.iters * 1e6
+        nc = int(c.ws[3])  # candidates of the last encode (topk.hip state word TK_NC)
         print(f"{str(dt):14s} n={a.n} k={c.k}: encode {enc:8.1f} us  decode {dec:6.1f} us  "
-              f"payload {c.nbytes / 1e6:.2f} MB", flush=True)
+              f"payload {c.nbytes / 1e6:.2f} MB  candidates {nc}", flush=True)
 
 
 if __name__ == "__main__":

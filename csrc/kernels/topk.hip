@@ -9,16 +9,18 @@
 //
 // Two passes over the gradient, five launches, no host round trip (stream-ordered,
 // graph-capturable):
-//   A  (1024 workgroups, one contiguous chunk each) acc = resid + g in place and a 4096-bin LDS
-//      histogram of the top 12 magnitude bits (exponent + 4 mantissa bits); flushed to a global
-//      histogram with sparse atomics, and kept per workgroup as suffix sums;
-//   S  (one workgroup) the bin b0 holding the k-th largest; every chunk's count of elements above
-//      b0 ("sure") and inside it ("candidates") is two lookups in its suffix row: exclusive scans
-//      give each chunk its write bases;
-//   B  (1024 workgroups, same chunks) writes the sure entries to the payload in index order
-//      (workgroup-scan ranks; resid -= fp16 value), compacts the candidates (index, acc) in index
-//      order and histograms their remaining 19 bits: 1024 coarse bins (bits 18..9, LDS) and the
-//      full 2^19 fine bins (global atomics);
+//   A  (1024 chunks, four per 1024-thread workgroup — one workgroup per CU, one 256-thread group
+//      per chunk) acc = resid + g in place and a 4096-bin LDS histogram per chunk of the top 12
+//      magnitude bits (exponent + 4 mantissa bits), kept as the chunk's suffix sums and flushed
+//      to 16 global copies (chunk-group & 15: 256 same-address atomics per bin serialise at the
+//      memory side) with sparse atomics;
+//   S  (one workgroup) the bin b0 holding the k-th largest;
+//   B  (1024 workgroups of 256 threads, the same chunks) sums its chunk's bases from the rows
+//      (counts above b0 — "sure" — and inside it — "candidates" — of the preceding chunks), writes
+//      the sure entries to the payload in index order (ranks from wave ballots plus one
+//      cross-wave prefix per tile; resid -= fp16 value), compacts the candidates (index, acc) in
+//      index order and histograms their remaining 19 bits: 1024 coarse bins (bits 18..9, LDS,
+//      flushed to 8 copies) and the full 2^19 fine bins (global atomics);
 //   Rc (256 workgroups over the candidates) every workgroup finds the exact threshold T from the
 //      two histograms (coarse bin, then its 512 fine bins) and counts its range's candidates
 //      above T and equal to T;
@@ -28,11 +30,15 @@
 // With error feedback the unsent mass piles up just below the threshold (10x the candidates of a
 // Gaussian), so the candidate stage is grid-parallel. Deterministic: positions come from ordered
 // scans, never from same-address atomics. The previous encoder made three full histogram passes
-// + count / scan / write (5 passes, 11 launches).
+// + count / scan / write (5 passes, 11 launches). Round 6 (ResNet-18 step, 11.2 M values: 91 ->
+// ~75 us): pipelined loads without exec-masked fallbacks (full vmcnt waits before), histogram
+// copies, bases summed in B instead of S; profiles/r6_topk_*.
 //
 // Payload (int32 words): [count, kcap, n, 0 | idx[kcap] | fp16 val[kcap] (packed)]
 // Server side: dst[idx] += scale * val (decode into a dense fp32 buffer, or straight into the
 // fp32 master parameters with scale = -lr * weight when there is no optimizer state).
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace psx {
@@ -41,8 +47,13 @@ enum { TK_KREM = 0, TK_B0 = 1, TK_CNTGT = 2, TK_NC = 3, TK_T = 4, TK_NEED = 5, T
 constexpr int TK_RB = 256;                 // workgroups of the candidate stage
 constexpr int TK_FINE = 1 << 19;           // fine bins: magnitude bits 18..0
 constexpr int TK_NB0 = 4096, TK_SH0 = 19;  // first-level bins: magnitude bits 30..19
-constexpr int TK_BLOCKS = 1024;            // chunks of passes A / B
+constexpr int TK_MAXBLK = 1024;            // chunks of passes A / B
 constexpr int TK_ROW = TK_NB0 + 1;         // per-chunk suffix row (entry 4096 = 0)
+// The global histograms are spread over copies (chunk & (copies - 1)): every chunk finishes at
+// about the same time, and 256 same-address atomics per bin serialise at the memory side (pass A
+// 37 -> 22.5 us without them at ResNet-18 size); the consumers sum the copies.
+constexpr int TK_HCOPY = 16;               // copies of the 4096-bin histogram (pass A -> S)
+constexpr int TK_CCOPY = 8;                // copies of the candidates' 1024-bin histogram (B -> Rc)
 
 PSX_DEV uint32_t mag_key(float a) { return __float_as_uint(a) & 0x7fffffffu; }
 
@@ -80,115 +91,20 @@ PSX_DEV float tk_load_g(const GT* g, long i) {
   else return (float)g[i];
 }
 
-// Pass A: acc = resid + g (g may be null), 4096-bin histogram -> global + per-chunk suffix row.
-template <typename GT>
-__global__ __launch_bounds__(256) void tk_pass_a(const GT* __restrict__ g, float* __restrict__ resid, long n,
-                                                 long chunk, uint32_t* __restrict__ ghist,
-                                                 uint32_t* __restrict__ rows) {
-  __shared__ uint32_t lh2[2 * TK_NB0];  // two copies (waves 0-1 / 2-3): half the same-bin contention
-  __shared__ uint32_t wsum[4];
-  const int t = threadIdx.x;
-  for (int i = t; i < 2 * TK_NB0; i += 256) lh2[i] = 0;
-  __syncthreads();
-  uint32_t* const lh = lh2 + (t >> 7) * TK_NB0;
-  const long lo = (long)blockIdx.x * chunk;
-  const long hi = lo + chunk < n ? lo + chunk : n;
-  // 4 tiles of 1024 per iteration: their loads are all in flight before the first add / atomic
-  constexpr int U = 4;
-  long i = lo + 4 * t;
-  for (; i + (U - 1) * 1024 + 3 < hi; i += U * 1024) {
-    f32x4 r[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) r[u] = *reinterpret_cast<const f32x4*>(resid + i + u * 1024);
-    if (g != nullptr) {
-      if constexpr (sizeof(GT) == 2) {
-        u32x2 hv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) hv[u] = *reinterpret_cast<const u32x2*>(g + i + u * 1024);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const _Float16* hp = reinterpret_cast<const _Float16*>(&hv[u]);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) r[u][e] += (float)hp[e];
-        }
-      } else {
-        f32x4 gv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) gv[u] = *reinterpret_cast<const f32x4*>(g + i + u * 1024);
-#pragma unroll
-        for (int u = 0; u < U; ++u) r[u] += gv[u];
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) *reinterpret_cast<f32x4*>(resid + i + u * 1024) = r[u];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) atomicAdd(&lh[mag_key(r[u][e]) >> TK_SH0], 1u);
-  }
-  for (; i < hi; i += 1024) {
-    if (i + 3 < hi) {
-      f32x4 r = *reinterpret_cast<const f32x4*>(resid + i);
-      if (g != nullptr) {
-        if constexpr (sizeof(GT) == 2) {
-          const u32x2 h = *reinterpret_cast<const u32x2*>(g + i);
-          const _Float16* hp = reinterpret_cast<const _Float16*>(&h);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) r[e] += (float)hp[e];
-        } else {
-          r += *reinterpret_cast<const f32x4*>(g + i);
-        }
-        *reinterpret_cast<f32x4*>(resid + i) = r;
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) atomicAdd(&lh[mag_key(r[e]) >> TK_SH0], 1u);
-    } else {
-      for (long j = i; j < hi; ++j) {
-        float a = resid[j];
-        if (g != nullptr) {
-          a += tk_load_g(g, j);
-          resid[j] = a;
-        }
-        atomicAdd(&lh[mag_key(a) >> TK_SH0], 1u);
-      }
-    }
-  }
-  __syncthreads();
-  for (int i = t; i < TK_NB0; i += 256) lh2[i] += lh2[TK_NB0 + i];
-  __syncthreads();
-  // suffix sums in descending bin order: thread t owns bins 4095 - 16 t - j (j < 16)
-  uint32_t c[16], local = 0;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    c[j] = lh2[TK_NB0 - 1 - (16 * t + j)];
-    local += c[j];
-  }
-  uint32_t tot;
-  uint32_t above = tk_excl_scan<256>(local, wsum, &tot);
-  uint32_t* row = rows + (size_t)blockIdx.x * TK_ROW;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    above += c[j];
-    row[TK_NB0 - 1 - (16 * t + j)] = above;  // # elements of this chunk in bins >= bin
-  }
-  if (t == 0) row[TK_NB0] = 0;
-  for (int i = t; i < TK_NB0; i += 256)
-    if (lh2[i]) atomicAdd(&ghist[i], lh2[i]);
-}
-
-// S: one workgroup of 1024 threads. The bin b0 holding the k-th largest; per-chunk bases of the
-// sure entries and of the candidates; clears the global histogram for the next encode.
-__global__ __launch_bounds__(1024) void tk_select0(uint32_t* __restrict__ ghist, const uint32_t* __restrict__ rows,
-                                                   uint32_t* __restrict__ state, uint32_t* __restrict__ bases, int k) {
+// S: one workgroup of 1024 threads. The bin b0 holding the k-th largest, summing the histogram
+// copies; clears them for the next encode. (Each pass-B workgroup sums its chunk's bases from the
+// rows itself: done here, the 1024 dependent row reads and scans made this launch 10 us. Run by
+// pass A's last-arriving workgroup instead, A measured 47 us vs 30 + 7 here.)
+__global__ __launch_bounds__(1024) void tk_select0(uint32_t* __restrict__ ghist, uint32_t* __restrict__ state, int k) {
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t sb[2];
   const int t = threadIdx.x;
-  uint32_t c[4], local = 0;
+  // thread t owns bins 4095 - 4 t - j (j < 4): the 16-byte word at bin 4092 - 4 t of every copy
+  u32x4 cv = {0u, 0u, 0u, 0u};
+  u32x4* const hv = reinterpret_cast<u32x4*>(ghist) + (TK_NB0 / 4 - 1 - t);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    c[j] = ghist[TK_NB0 - 1 - (4 * t + j)];
-    local += c[j];
-  }
+  for (int h = 0; h < TK_HCOPY; ++h) cv += hv[h * (TK_NB0 / 4)];
+  uint32_t c[4] = {cv[3], cv[2], cv[1], cv[0]}, local = c[0] + c[1] + c[2] + c[3];
   if (t == 0) sb[0] = sb[1] = 0;
   uint32_t tot;
   uint32_t above = tk_excl_scan<1024>(local, wsum, &tot);
@@ -207,105 +123,281 @@ __global__ __launch_bounds__(1024) void tk_select0(uint32_t* __restrict__ ghist,
   __syncthreads();
   const uint32_t b0 = sb[0], cnt_gt = sb[1];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) ghist[4 * t + j] = 0;
-  // chunk t: sure = bins > b0, candidates = bin b0
-  const uint32_t* row = rows + (size_t)t * TK_ROW;
-  const uint32_t sure = row[b0 + 1], cand = row[b0] - sure;
-  uint32_t ts, tc;
-  const uint32_t bs = tk_excl_scan<1024>(sure, wsum, &ts);
-  const uint32_t bc = tk_excl_scan<1024>(cand, wsum, &tc);
-  bases[2 * t] = bs;
-  bases[2 * t + 1] = bc;
+  for (int h = 0; h < TK_HCOPY; ++h) hv[h * (TK_NB0 / 4)] = u32x4{0u, 0u, 0u, 0u};
   if (t == 0) {
     state[TK_KREM] = kk - cnt_gt;
     state[TK_B0] = b0;
     state[TK_CNTGT] = cnt_gt;
-    state[TK_NC] = tc;
   }
 }
 
+// Pass A: acc = resid + g (g may be null), 4096-bin histogram -> global + per-chunk suffix rows.
+// One workgroup of 1024 threads per CU runs four chunks, one per 256-thread group (LDS histogram
+// copy = group): pass B runs the same chunks as 256-thread workgroups (its per-tile rank barrier
+// is cheaper over 4 waves than over 16), while 256-thread workgroups here measured 2.5x slower
+// (65 vs 26 us at ResNet-18 size: four times the workgroup epilogues and LDS clears per CU).
+template <typename GT, bool HASG>
+__global__ __launch_bounds__(1024) void tk_pass_a(const GT* __restrict__ g, float* __restrict__ resid, long n,
+                                                  long chunk, uint32_t* __restrict__ ghist,
+                                                  uint32_t* __restrict__ rows) {
+  constexpr int NT = 256, TILE = 4 * NT;  // per group; a tile = 4 consecutive elements per thread
+  __shared__ uint32_t lh4[4 * TK_NB0];
+  __shared__ uint32_t wsum[16];
+  for (int i = threadIdx.x; i < 4 * TK_NB0; i += 1024) lh4[i] = 0;
+  __syncthreads();
+  const int gq = threadIdx.x >> 8, t = threadIdx.x & (NT - 1);
+  const int vb = 4 * blockIdx.x + gq;  // this group's chunk
+  uint32_t* const lh = lh4 + gq * TK_NB0;
+  const long lo = (long)vb * chunk;
+  const long hi = lo + chunk < n ? lo + chunk : n;
+  // Full tiles (no bounds checks, so no exec-masked fallback loads that force a full vmcnt wait),
+  // PF of them in flight: the loop is unrolled by PF and tile u's registers are refilled (tile
+  // u + PF) right after they are consumed, so the loads stay queued behind the atomics; the
+  // chunk's partial last tile (the last chunk only) after the loop.
+  constexpr int PF = 3;
+  constexpr bool hasg = HASG;  // compile-time: a runtime flag leaves register merges (copies of
+                               // tiles still in flight) in the loop
+  const long nfull = hi > lo ? (hi - lo) / TILE : 0;
+  using GV = std::conditional_t<sizeof(GT) == 2, u32x2, f32x4>;  // raw g in the ring (fp16: converted
+                                                                 // when consumed, not when loaded)
+  auto load = [&](long i, f32x4& r, GV& gv) {
+    r = *reinterpret_cast<const f32x4*>(resid + i);
+    if constexpr (hasg) gv = *reinterpret_cast<const GV*>(g + i);
+  };
+  auto consume = [&](const f32x4& rv, const GV& gv, long i) {
+    f32x4 r = rv;
+    if constexpr (hasg) {
+      if constexpr (sizeof(GT) == 2) {
+        const _Float16* hp = reinterpret_cast<const _Float16*>(&gv);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r[e] += (float)hp[e];
+      } else {
+        r += gv;
+      }
+      *reinterpret_cast<f32x4*>(resid + i) = r;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) atomicAdd(&lh[mag_key(r[e]) >> TK_SH0], 1u);
+  };
+  // groups of PF tiles with straight-line bodies (the last group's refills re-load its own tiles,
+  // unused): a skipped refill would leave the wait counter's bookkeeping with a full wait
+  const long ng = nfull / PF;
+  f32x4 br[PF];
+  GV bg[PF];
+  if (ng > 0) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) load(lo + (long)u * TILE + 4 * t, br[u], bg[u]);
+  }
+  for (long gi = 0; gi < ng; ++gi) {
+    const long nxt = gi + 1 < ng ? PF * TILE : 0;
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const long i = lo + (gi * PF + u) * TILE + 4 * t;
+      const f32x4 r = br[u];
+      const GV gv = bg[u];
+      load(i + nxt, br[u], bg[u]);
+      consume(r, gv, i);
+      // keep the refill here: hoisted to the top of the body, the scheduler would have to wait
+      // for every tile in flight before overwriting their registers
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  for (long tt = ng * PF; tt < nfull; ++tt) {  // leftover full tiles
+    f32x4 r;
+    GV gv;
+    const long i = lo + tt * TILE + 4 * t;
+    load(i, r, gv);
+    consume(r, gv, i);
+  }
+  for (long i = lo + nfull * TILE + t; i < hi; i += NT) {  // partial tile
+    float a = resid[i];
+    if (hasg) {
+      a += tk_load_g(g, i);
+      resid[i] = a;
+    }
+    atomicAdd(&lh[mag_key(a) >> TK_SH0], 1u);
+  }
+  __syncthreads();
+  // the group's suffix row, descending bins: thread t owns bins 4095 - 16 t - j (j < 16); the
+  // exclusive scan runs over the group's 4 waves
+  constexpr int BT = TK_NB0 / NT;
+  uint32_t c[BT], local = 0;
+#pragma unroll
+  for (int j = 0; j < BT; ++j) {
+    c[j] = lh[TK_NB0 - 1 - (BT * t + j)];
+    local += c[j];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t incl = local;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t x = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += x;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t above = incl - local;
+  for (int i = gq * 4; i < w; ++i) above += wsum[i];
+  uint32_t* row = rows + (size_t)vb * TK_ROW;
+#pragma unroll
+  for (int j = 0; j < BT; ++j) {
+    above += c[j];
+    row[TK_NB0 - 1 - (BT * t + j)] = above;  // # elements of this chunk in bins >= bin
+  }
+  if (t == 0) row[TK_NB0] = 0;
+  // the global histogram: the four groups' counts summed, one atomic per non-empty bin
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int b = 4 * (int)threadIdx.x + j;
+    const uint32_t v = lh4[b] + lh4[TK_NB0 + b] + lh4[2 * TK_NB0 + b] + lh4[3 * TK_NB0 + b];
+    if (v) atomicAdd(&ghist[(blockIdx.x & (TK_HCOPY - 1)) * TK_NB0 + b], v);
+  }
+}
+
+
 // B: sure entries -> payload (index order), candidates -> (cidx, cval) (index order) + their
-// coarse / fine histograms. Tiles of 1024 elements, 4 consecutive ones per thread (one 16-byte
-// load), ranks by a workgroup scan.
+// coarse / fine histograms. Tiles of 4096 elements, 4 consecutive ones per thread (one 16-byte
+// load, three tiles in flight ahead); an element's rank = the preceding waves' counts (one
+// cross-wave prefix per tile, double-buffered so one barrier suffices) + the wave's ballots below
+// it + its own earlier flags.
 __global__ __launch_bounds__(256) void tk_pass_b(float* __restrict__ resid, long n, long chunk,
-                                                 const uint32_t* __restrict__ state,
-                                                 const uint32_t* __restrict__ bases, int* __restrict__ payload,
-                                                 int kcap, int* __restrict__ cidx, float* __restrict__ cval,
-                                                 uint32_t* __restrict__ coarse, uint32_t* __restrict__ fine) {
-  __shared__ uint32_t wsum[4];
+                                                   uint32_t* __restrict__ state,
+                                                   const uint32_t* __restrict__ rows, int* __restrict__ payload,
+                                                   int kcap, int* __restrict__ cidx, float* __restrict__ cval,
+                                                   uint32_t* __restrict__ coarse, uint32_t* __restrict__ fine) {
+  constexpr int TK_NT = 256, NW = TK_NT / 64, TK_TILE = 4 * TK_NT;
+  __shared__ uint32_t wsum[2][NW];
   __shared__ uint32_t lh[1024];
-  for (int i = threadIdx.x; i < 1024; i += 256) lh[i] = 0;
+  for (int i = threadIdx.x; i < 1024; i += TK_NT) lh[i] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long below = (1ull << lane) - 1ull;
   const uint32_t b0 = state[TK_B0];
   int* idx = payload + 4;
   uint16_t* val = reinterpret_cast<uint16_t*>(payload + 4 + kcap);
   const long lo = (long)blockIdx.x * chunk;
   const long hi = lo + chunk < n ? lo + chunk : n;
-  uint32_t rs = bases[2 * blockIdx.x], rc = bases[2 * blockIdx.x + 1];
-  auto load4 = [&](long i0, float (&a)[4]) {
-    if (i0 + 3 < hi) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(resid + i0);
+  // this chunk's payload / candidate bases: the preceding chunks' counts above b0 and in b0 (their
+  // suffix rows at b0 + 1 and b0); the last chunk also publishes the candidate total
+  uint32_t rs = 0, rc = 0;
+  {
+    const int vb = blockIdx.x;
+    const bool last = vb == (int)gridDim.x - 1;
+    uint32_t s1 = 0, s0 = 0;
+    for (int c = threadIdx.x; c < vb || (last && c == vb); c += TK_NT) {
+      const uint32_t* row = rows + (size_t)c * TK_ROW;
+      s1 += row[b0 + 1];
+      s0 += row[b0];
+    }
+    // (each count < 2^31: the chunk sums of s1 and of s0 - s1 fit; reduce both packed as 64-bit)
+    unsigned long long v = ((unsigned long long)(s0 - s1) << 32) | s1;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) a[e] = v[e];
-    } else {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __shared__ unsigned long long bred[NW];
+    if (lane == 0) bred[w] = v;
+    __syncthreads();
+    v = 0;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) a[e] = i0 + e < hi ? resid[i0 + e] : 0.f;
+    for (int j = 0; j < NW; ++j) v += bred[j];
+    if (last) {  // v includes this chunk: the candidate total
+      if (threadIdx.x == 0) state[TK_NC] = (uint32_t)(v >> 32);
+      const uint32_t* row = rows + (size_t)vb * TK_ROW;
+      v -= ((unsigned long long)(row[b0] - row[b0 + 1]) << 32) | row[b0 + 1];
+    }
+    rs = (uint32_t)v;
+    rc = (uint32_t)(v >> 32);
+  }
+  int it = 0;
+  // one tile: a = this thread's 4 elements at i0 (in = the first nin of them exist)
+  auto tile = [&](const f32x4& a, long i0, int nin) {
+    uint32_t fs = 0, fc = 0;  // per-element flags (bit e): sure / candidate
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool in = e < nin;
+      const uint32_t bin = mag_key(a[e]) >> TK_SH0;
+      fs |= (uint32_t)(in && bin > b0) << e;
+      fc |= (uint32_t)(in && bin == b0) << e;
+    }
+    uint32_t ws = 0, wc = 0, ts = 0, tc = 0;  // this lane's rank in the wave, the wave's totals
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const unsigned long long bs = __ballot((fs >> e) & 1u), bc = __ballot((fc >> e) & 1u);
+      ws += __popcll(bs & below);
+      wc += __popcll(bc & below);
+      ts += __popcll(bs);
+      tc += __popcll(bc);
+    }
+    if (lane == 0) wsum[it][w] = ts | (tc << 16);
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      const uint32_t x = wsum[it][j];
+      pre += j < w ? x : 0u;
+      tot += x;
+    }
+    it ^= 1;
+    uint32_t ps = rs + (pre & 0xffffu) + ws, pc = rc + (pre >> 16) + wc;
+    rs += tot & 0xffffu;
+    rc += tot >> 16;
+    if (fs | fc) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long i = i0 + e;
+        if ((fs >> e) & 1u) {
+          if (ps < (uint32_t)kcap) {
+            const uint16_t h = tk_half(a[e]);
+            idx[ps] = (int)i;
+            val[ps] = h;
+            resid[i] = a[e] - (float)__builtin_bit_cast(_Float16, h);
+          }
+          ++ps;
+        } else if ((fc >> e) & 1u) {
+          const uint32_t key = mag_key(a[e]);
+          cidx[pc] = (int)i;
+          cval[pc] = a[e];
+          ++pc;
+          atomicAdd(&lh[(key >> 9) & 1023u], 1u);
+          atomicAdd(&fine[key & (TK_FINE - 1)], 1u);
+        }
+      }
     }
   };
-  float nx1[4], nx2[4];  // tiles t + 1 and t + 2 are in flight while tile t is ranked and written
-  load4(lo + 4 * threadIdx.x, nx1);
-  load4(lo + 1024 + 4 * threadIdx.x, nx2);
-  for (long base = lo; base < hi; base += 1024) {
-    const long i0 = base + 4 * threadIdx.x;
-    float a[4];
+  // full tiles, PF in flight (unrolled ring without bounds checks, as in pass A), then the partial one
+  constexpr int PF = 3;
+  const long nfull = hi > lo ? (hi - lo) / TK_TILE : 0;
+  const long ng = nfull / PF;
+  f32x4 nx[PF];
+  if (ng > 0) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      a[e] = nx1[e];
-      nx1[e] = nx2[e];
-    }
-    if (base + 2048 < hi) load4(i0 + 2048, nx2);
-    uint32_t ns = 0, ncnd = 0, fs = 0, fc = 0;  // counts and per-element flags (bit e)
+    for (int u = 0; u < PF; ++u) nx[u] = *reinterpret_cast<const f32x4*>(resid + lo + (long)u * TK_TILE + 4 * threadIdx.x);
+  }
+  for (long gi = 0; gi < ng; ++gi) {
+    const long nxt = gi + 1 < ng ? PF * TK_TILE : 0;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const bool in = i0 + e < hi;
-      const uint32_t bin = mag_key(a[e]) >> TK_SH0;
-      if (in && bin > b0) {
-        fs |= 1u << e;
-        ++ns;
-      } else if (in && bin == b0) {
-        fc |= 1u << e;
-        ++ncnd;
-      }
+    for (int u = 0; u < PF; ++u) {
+      const long i0 = lo + (gi * PF + u) * TK_TILE + 4 * threadIdx.x;
+      const f32x4 a = nx[u];
+      nx[u] = *reinterpret_cast<const f32x4*>(resid + i0 + nxt);
+      tile(a, i0, 4);
+      __builtin_amdgcn_sched_barrier(0);  // (see pass A)
     }
-    uint32_t tp;  // one scan of both counts packed (each <= 1024 per tile)
-    const uint32_t ex = tk_excl_scan<256>(ns | (ncnd << 16), wsum, &tp);
-    const uint32_t ts = tp & 0xffffu, tc = tp >> 16;
-    uint32_t ps = rs + (ex & 0xffffu), pc = rc + (ex >> 16);
+  }
+  for (long tt = ng * PF; tt < nfull; ++tt) {  // leftover full tiles
+    const long i0 = lo + tt * TK_TILE + 4 * threadIdx.x;
+    tile(*reinterpret_cast<const f32x4*>(resid + i0), i0, 4);
+  }
+  if (lo + nfull * TK_TILE < hi) {
+    const long i0 = lo + nfull * TK_TILE + 4 * threadIdx.x;
+    f32x4 a;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const long i = i0 + e;
-      if (fs >> e & 1u) {
-        if (ps < (uint32_t)kcap) {
-          const uint16_t h = tk_half(a[e]);
-          idx[ps] = (int)i;
-          val[ps] = h;
-          resid[i] = a[e] - (float)__builtin_bit_cast(_Float16, h);
-        }
-        ++ps;
-      } else if (fc >> e & 1u) {
-        const uint32_t key = mag_key(a[e]);
-        cidx[pc] = (int)i;
-        cval[pc] = a[e];
-        ++pc;
-        atomicAdd(&lh[(key >> 9) & 1023u], 1u);
-        atomicAdd(&fine[key & (TK_FINE - 1)], 1u);
-      }
-    }
-    rs += ts;
-    rc += tc;
+    for (int e = 0; e < 4; ++e) a[e] = i0 + e < hi ? resid[i0 + e] : 0.f;
+    const long left = hi - i0;
+    tile(a, i0, left <= 0 ? 0 : left >= 4 ? 4 : (int)left);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 1024; i += 256)
-    if (lh[i]) atomicAdd(&coarse[i], lh[i]);
+  for (int i = threadIdx.x; i < 1024; i += TK_NT)
+    if (lh[i]) atomicAdd(&coarse[(blockIdx.x & (TK_CCOPY - 1)) * 1024 + i], lh[i]);
 }
 
 PSX_DEV void tk_crange(uint32_t nc, uint32_t& lo, uint32_t& hi) {
@@ -330,7 +422,9 @@ __global__ __launch_bounds__(256) void tk_refine_count(const float* __restrict__
   uint32_t c[4], local = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    c[j] = coarse[1023 - (4 * t + j)];
+    c[j] = 0;
+#pragma unroll
+    for (int h = 0; h < TK_CCOPY; ++h) c[j] += coarse[h * 1024 + 1023 - (4 * t + j)];
     local += c[j];
   }
   uint32_t tot;
@@ -434,7 +528,7 @@ __global__ __launch_bounds__(256) void tk_refine_write(float* __restrict__ resid
     run_tie += teq;
   }
   if (blockIdx.x == 0) {
-    for (int i = t; i < 1024; i += 256) coarse[i] = 0;
+    for (int i = t; i < TK_CCOPY * 1024; i += 256) coarse[i] = 0;
     if (t == 0) {
       payload[0] = k < kcap ? k : kcap;
       payload[1] = kcap;
@@ -458,16 +552,16 @@ __global__ __launch_bounds__(256) void topk_decode_add_kernel(const int* __restr
 
 using namespace psx;
 
-static long tk_chunk(long n) { return ((n + TK_BLOCKS - 1) / TK_BLOCKS + 1023) / 1024 * 1024; }
+static long tk_chunk(long n, int nblk, int tile) { return ((n + nblk - 1) / nblk + tile - 1) / tile * tile; }
 
 extern "C" {
 
-// int32 words of workspace for gradients of n elements (histogram, state, chunk bases, per-chunk
+// int32 words of workspace for gradients of n elements (state, histogram copies, per-chunk
 // suffix rows, candidate buffers of n entries — never overflow, whatever the distribution —,
 // the candidates' coarse / fine histograms and the candidate stage's range counts).
 long psx_topk_workspace_words(long n) {
-  return (long)TK_NB0 + TK_STATE_WORDS + 2L * TK_BLOCKS + (long)TK_BLOCKS * TK_ROW + 2L * (((n > 0 ? n : 1) + 3) / 4 * 4) +
-         1024 + TK_FINE + 2L * TK_RB;
+  return (long)TK_STATE_WORDS + (long)TK_HCOPY * TK_NB0 + (long)TK_MAXBLK * TK_ROW +
+         2L * (((n > 0 ? n : 1) + 3) / 4 * 4) + (long)TK_CCOPY * 1024 + TK_FINE + 2L * TK_RB;
 }
 
 int psx_topk_payload_words(int kcap) { return 4 + kcap + (kcap + 1) / 2; }
@@ -481,25 +575,27 @@ int psx_topk_encode(const void* g, int g_fp16, float* resid, long n, int k, int 
   if ((long)k > n) k = (int)n;
   if (k < 1 || n < 1) return (int)hipErrorInvalidValue;
   if (((uintptr_t)resid & 15) || (g && ((uintptr_t)g & (g_fp16 ? 7 : 15)))) return (int)hipErrorInvalidValue;
-  uint32_t* hist = ws;
-  uint32_t* state = hist + TK_NB0;
-  uint32_t* bases = state + TK_STATE_WORDS;
-  uint32_t* rows = bases + 2 * TK_BLOCKS;
-  int* cidx = (int*)(rows + (size_t)TK_BLOCKS * TK_ROW);
+  uint32_t* state = ws;  // (bench/topk_bench.py reads the candidate count, word TK_NC)
+  uint32_t* hist = state + TK_STATE_WORDS;
+  uint32_t* rows = hist + TK_HCOPY * TK_NB0;
+  int* cidx = (int*)(rows + (size_t)TK_MAXBLK * TK_ROW);
   float* cval = (float*)(cidx + (n + 3) / 4 * 4);
   uint32_t* coarse = (uint32_t*)(cval + (n + 3) / 4 * 4);
-  uint32_t* fine = coarse + 1024;
+  uint32_t* fine = coarse + TK_CCOPY * 1024;
   uint32_t* rcounts = fine + TK_FINE;
-  const long chunk = tk_chunk(n);
-  if (g_fp16)
-    hipLaunchKernelGGL((tk_pass_a<uint16_t>), dim3(TK_BLOCKS), dim3(256), 0, st, (const uint16_t*)g, resid, n, chunk,
-                       hist, rows);
+  const long chunk = tk_chunk(n, TK_MAXBLK, 1024);  // pass A: 4 chunks per workgroup
+  if (!g)
+    hipLaunchKernelGGL((tk_pass_a<float, false>), dim3(TK_MAXBLK / 4), dim3(1024), 0, st, (const float*)nullptr, resid,
+                       n, chunk, hist, rows);
+  else if (g_fp16)
+    hipLaunchKernelGGL((tk_pass_a<uint16_t, true>), dim3(TK_MAXBLK / 4), dim3(1024), 0, st, (const uint16_t*)g, resid,
+                       n, chunk, hist, rows);
   else
-    hipLaunchKernelGGL((tk_pass_a<float>), dim3(TK_BLOCKS), dim3(256), 0, st, (const float*)g, resid, n, chunk, hist,
-                       rows);
-  hipLaunchKernelGGL(tk_select0, dim3(1), dim3(1024), 0, st, hist, rows, state, bases, k);
-  hipLaunchKernelGGL(tk_pass_b, dim3(TK_BLOCKS), dim3(256), 0, st, resid, n, chunk, state, bases, payload, kcap,
-                     cidx, cval, coarse, fine);
+    hipLaunchKernelGGL((tk_pass_a<float, true>), dim3(TK_MAXBLK / 4), dim3(1024), 0, st, (const float*)g, resid, n,
+                       chunk, hist, rows);
+  hipLaunchKernelGGL(tk_select0, dim3(1), dim3(1024), 0, st, hist, state, k);
+  hipLaunchKernelGGL(tk_pass_b, dim3(TK_MAXBLK), dim3(256), 0, st, resid, n, chunk, state, rows, payload, kcap, cidx,
+                     cval, coarse, fine);
   hipLaunchKernelGGL(tk_refine_count, dim3(TK_RB), dim3(256), 0, st, cval, state, coarse, fine, rcounts);
   hipLaunchKernelGGL(tk_refine_write, dim3(TK_RB), dim3(256), 0, st, resid, cidx, cval, state, rcounts, payload, kcap,
                      n, k, coarse, fine);

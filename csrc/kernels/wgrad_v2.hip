@@ -462,8 +462,11 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(Wgrad3Args a) {
 #pragma unroll
   for (int i = 0; i < NS - 1; ++i)
     if (i < nsteps) issue(i, i);
-  int stage = 0;
-  for (int st = 0; st < nsteps; ++st) {
+  // The step loop is unrolled by NS so that every step's stage is a compile-time constant: the
+  // fragment reads then address LDS as per-lane offsets hoisted out of the loop + an immediate
+  // (a runtime stage base cost one v_add per read, ~2 of wgrad3's 5.3 VALU per MFMA).
+  auto step = [&](const int st, auto sc) {
+    constexpr int stage = decltype(sc)::value;
     wait_ahead<2 + LD, NS - 2>(min(NS - 2, nsteps - 1 - st));
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -495,8 +498,12 @@ __global__ __launch_bounds__(256) void wgrad3_kernel(Wgrad3Args a) {
         for (int n = 0; n < NT; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
     }
-    stage = stage == NS - 1 ? 0 : stage + 1;
-  }
+  };
+  for (int st0 = 0; st0 < nsteps; st0 += NS)
+    static_for<0, NS>([&](auto sc) {
+      const int st = st0 + decltype(sc)::value;
+      if (st < nsteps) step(st, sc);
+    });
 
   float* part = a.part + (size_t)split * a.OC * a.Kg;
 #pragma unroll

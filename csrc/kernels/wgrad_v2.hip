@@ -91,6 +91,9 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(Wgrad2Args a) {
   const uint16_t* const xg = (const uint16_t*)a.x;
   const uint16_t* const dyg = (const uint16_t*)a.dy;
   const uint16_t* const zero = (const uint16_t*)a.zero;
+  // 1x1 / stride 1 / pad 0 (most of ResNet-50's weight gradients): output pixel == input pixel,
+  // no (n, oh, ow) decomposition per staged row
+  const bool ident = a.R == 1 && a.S == 1 && a.stride == 1 && a.pad == 0;
   auto issue = [&](int st, int stage) {
     unsigned char* base = smem + stage * STAGE;
     const int p0 = pbeg + st * 64;
@@ -98,7 +101,9 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(Wgrad2Args a) {
     for (int i = 0; i < LX; ++i) {
       const int pix = p0 + xrow[i];
       const uint16_t* src = zero;
-      if (pix < a.npix && xtap_ok[i]) {
+      if (ident) {
+        if (pix < a.npix && xtap_ok[i]) src = xg + (size_t)pix * a.IC + xc0[i];
+      } else if (pix < a.npix && xtap_ok[i]) {
         const int n = fdiv(pix, a.div_ohw);
         const int rem = pix - n * a.div_ohw.d;
         const int oh = fdiv(rem, a.div_ow);
@@ -128,8 +133,9 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(Wgrad2Args a) {
   for (int i = 0; i < NS - 1; ++i)
     if (i < nsteps) issue(i, i);
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  int stage = 0;
-  for (int st = 0; st < nsteps; ++st) {
+  // unrolled by NS: compile-time stage offsets (see wgrad3_kernel)
+  auto step = [&](const int st, auto sc) {
+    constexpr int stage = decltype(sc)::value;
     const int ahead = min(NS - 2, nsteps - 1 - st);  // groups issued after step st's
     if (ahead >= NS - 2)
       wait_vmcnt<(NS - 2) * (LX + LD)>();
@@ -166,8 +172,12 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(Wgrad2Args a) {
         for (int n = 0; n < NT; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
     }
-    stage = stage == NS - 1 ? 0 : stage + 1;
-  }
+  };
+  for (int st0 = 0; st0 < nsteps; st0 += NS)
+    static_for<0, NS>([&](auto sc) {
+      const int st = st0 + decltype(sc)::value;
+      if (st < nsteps) step(st, sc);
+    });
 
   float* part = a.part + (size_t)split * a.OC * a.Kg;
 #pragma unroll
@@ -238,6 +248,7 @@ __global__ __launch_bounds__(256) void wgrad2f_kernel(Wgrad2Args a) {
     dchunk[i] = (lane % DCPR) ^ ((row & 1) << 2);
   }
   const int OW = a.div_ow.d;
+  const bool ident = a.R == 1 && a.S == 1 && a.stride == 1 && a.pad == 0;  // (see wgrad2_kernel)
 
   auto issue = [&](int st, int stage) {
     unsigned char* base = smem + stage * STAGE;
@@ -246,7 +257,9 @@ __global__ __launch_bounds__(256) void wgrad2f_kernel(Wgrad2Args a) {
     for (int i = 0; i < LX; ++i) {
       const int pix = p0 + xrow[i];
       const float* src = zero;
-      if (pix < a.npix && xtap_ok[i]) {
+      if (ident) {
+        if (pix < a.npix && xtap_ok[i]) src = xg + (size_t)pix * a.IC + xc0[i];
+      } else if (pix < a.npix && xtap_ok[i]) {
         const int n = fdiv(pix, a.div_ohw);
         const int rem = pix - n * a.div_ohw.d;
         const int oh = fdiv(rem, a.div_ow);
@@ -288,8 +301,9 @@ __global__ __launch_bounds__(256) void wgrad2f_kernel(Wgrad2Args a) {
 #pragma unroll
   for (int i = 0; i < NS - 1; ++i)
     if (i < nsteps) issue(i, i);
-  int stage = 0;
-  for (int st = 0; st < nsteps; ++st) {
+  // unrolled by NS: compile-time stage offsets (see wgrad3_kernel)
+  auto step = [&](const int st, auto sc) {
+    constexpr int stage = decltype(sc)::value;
     const int ahead = min(NS - 2, nsteps - 1 - st);
     if (ahead >= NS - 2)
       wait_vmcnt<(NS - 2) * (LX + LD)>();
@@ -316,8 +330,12 @@ __global__ __launch_bounds__(256) void wgrad2f_kernel(Wgrad2Args a) {
         for (int n = 0; n < NT; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[m], fb[n], acc[m][n], 0, 0, 0);
     }
-    stage = stage == NS - 1 ? 0 : stage + 1;
-  }
+  };
+  for (int st0 = 0; st0 < nsteps; st0 += NS)
+    static_for<0, NS>([&](auto sc) {
+      const int st = st0 + decltype(sc)::value;
+      if (st < nsteps) step(st, sc);
+    });
 
   float* part = a.part + (size_t)split * a.OC * a.Kg;
 #pragma unroll

@@ -99,3 +99,22 @@ def test_encode_speed_resnet18():
     us = (time.perf_counter() - t0) / 20 * 1e6
     print(f"topk encode n={n} k={c.k}: {us:.1f} us")
     assert us < 2000
+
+
+def test_encode_without_gradient_selects_from_resid():
+    """g = NULL (tk_pass_a<float, false>): selection straight from the residual equals the encode of
+    the same values pushed as a gradient onto a zero residual, including an n that leaves a
+    partial last tile and empty chunks."""
+    from psx.ops import kernels as K
+
+    torch.manual_seed(1)
+    for n in (1_000_003, 5000):
+        g = torch.randn(n, device=DEV)
+        a = T.TopKCodec(n, 0.01, DEV)
+        pa = a.encode(g).clone()
+        b = T.TopKCodec(n, 0.01, DEV)
+        b.resid.copy_(g)
+        K.topk_encode(None, b.resid, b.k, b.kcap, b.payload, b.ws)
+        torch.cuda.synchronize()
+        assert torch.equal(b.payload, pa)
+        assert torch.equal(b.resid, a.resid)

@@ -721,7 +721,9 @@ WPlan wplan(int OC, int Kg, int npix, int fbr = 0, int fbc = 0) {
       const long tiles = (long)(Kg / BR) * (OC / BC);
       const double step_us = 0.55 + 0.15 * (double)(BR * BC) / 4096.0;
       int smax = steps / 8 > 0 ? steps / 8 : 1;
-      for (int sp = 1; sp <= smax && sp <= 64; ++sp) {
+      // (cap 64 until round 6: ResNet-50's 56x56 1x1 layers sat at it with ~98 steps per
+      // workgroup; 256 measured -2 % on its bf16 step, profiles/r6_wgrad_split_cap_ab.jsonl)
+      for (int sp = 1; sp <= smax && sp <= 256; ++sp) {
         const int sps = (steps + sp - 1) / sp;
         const int spl = (steps + sps - 1) / sps;
         const long wgs = tiles * spl;

@@ -770,14 +770,30 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
     }
   }
   const int pbeg = blockIdx.x * pix_per_block, pend = min(npix, pbeg + pix_per_block);
-  for (int p = pbeg + pr; p < pend; p += tpp) {
-    const size_t off = (size_t)p * OC + cg * 8;
-    f32x4 x0 = *reinterpret_cast<const f32x4*>(part + off);
-    f32x4 x1 = *reinterpret_cast<const f32x4*>(part + off + 4);
-    for (int s = 1; s < splits; ++s) {
-      x0 += *reinterpret_cast<const f32x4*>(part + s * slab + off);
-      x1 += *reinterpret_cast<const f32x4*>(part + s * slab + off + 4);
+  // PP pixel rows per thread at a time: their split slabs are loaded together (one round trip
+  // per split instead of one per row and split)
+  constexpr int PP = 4;
+  for (int pg = pbeg + pr; pg < pend; pg += PP * tpp) {
+    f32x4 xs0[PP], xs1[PP];
+    size_t offs[PP];
+#pragma unroll
+    for (int u = 0; u < PP; ++u) {
+      const int pu = pg + u * tpp;
+      offs[u] = (size_t)(pu < pend ? pu : pg) * OC + cg * 8;
+      xs0[u] = *reinterpret_cast<const f32x4*>(part + offs[u]);
+      xs1[u] = *reinterpret_cast<const f32x4*>(part + offs[u] + 4);
     }
+    for (int s = 1; s < splits; ++s)
+#pragma unroll
+      for (int u = 0; u < PP; ++u) {
+        xs0[u] += *reinterpret_cast<const f32x4*>(part + s * slab + offs[u]);
+        xs1[u] += *reinterpret_cast<const f32x4*>(part + s * slab + offs[u] + 4);
+      }
+#pragma unroll
+  for (int u = 0; u < PP; ++u) {
+    if (pg + u * tpp >= pend) break;
+    const size_t off = offs[u];
+    const f32x4 x0 = xs0[u], x1 = xs1[u];
     float v[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
     if (HAS_RES) {
       float r[8];
@@ -816,6 +832,7 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue(const float* __restr
       else
         st8(out + off, v);
     }
+  }
   }
   if (!stats && !bwd) return;
   float* mine = sred + threadIdx.x * 24;
@@ -999,8 +1016,12 @@ template <typename T>
 int finish_split(const Conv2Args& a, hipStream_t st) {
   const int cvec = a.OC / 8;
   if (256 % cvec) return -8;
-  int ppb = (a.npix + 511) / 512;
-  if (ppb < 8) ppb = 8;
+  // 32 pixels per workgroup (was >= 8, ~512 workgroups): every workgroup adds one set of
+  // per-channel BN partials with same-address atomics, and fewer, longer workgroups halve that
+  // traffic; their slab loads are batched 4 rows at a time. ResNet-18's one split-K layer
+  // (4x4x512, 2048 pixels -> 64 workgroups): step fp32 3.268 -> 3.258 ms, bf16 1.580 -> 1.569
+  // (profiles/r6_splitk_epilogue_ab.jsonl)
+  const int ppb = 32;
   const int grid = (a.npix + ppb - 1) / ppb;
   const size_t lds = 256 * 24 * sizeof(float);
   DetRed det{};

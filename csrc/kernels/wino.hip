@@ -170,9 +170,12 @@ __global__ __launch_bounds__(64) void wino_w_multi_kernel(WinoWBatch bt) {
 // next tile's row prefetched behind the current tile's transform.
 constexpr int kXfWaves = 6;
 
-// grid.y of the split kernels: ~8 workgroups per CU over the channel blocks, at most a tile each
+// grid.y of the split kernels: ~4 workgroups per CU over the channel blocks, at most a tile each
+// (8 per CU until round 6: each workgroup also adds one set of BN partial sums, and 1024 vs 2048
+// workgroups measured ResNet-18 fp32 3.277 -> 3.257 ms, ResNet-50 35.50 -> 35.47; 512 the same
+// as 1024, 256 +2 %, 4096 neutral: profiles/r6_wino_xf_grid_ab.jsonl)
 int wino_xf_grid(int T, int cblocks) {
-  int gy = 2048 / cblocks;
+  int gy = 1024 / cblocks;
   if (gy < 1) gy = 1;
   return gy > T ? T : gy;
 }

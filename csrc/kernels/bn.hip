@@ -405,7 +405,7 @@ using namespace psx;
 // workgroup cap of the folded-finalize apply launches (each workgroup recomputes the affine)
 // (1024 vs 2048: 1.852 vs 1.867-1.875 ms/step, round 4; round 6, same box: 512 vs 1024 fp32
 // 3.262 -> 3.254, bf16 1.605 -> 1.581; 256 worse in bf16: profiles/r6_bn_fin_grid_ab.jsonl)
-static int fin_grid_cap() { return 512; }  // 1024 vs 2048: 1.852 vs 1.867-1.875 ms/step (bench.py A/B)
+static int fin_grid_cap() { return 512; }
 
 static int ew_grid(size_t nvec) {
   size_t g = (nvec + 255) / 256;

@@ -763,7 +763,9 @@ WPlan wplan3(int OC, int IC, int Kg, int npix, int pix = 64) {
     const long tiles = 3L * (IC / 64) * (OC / BC);
     const double step_us = (BC == 64 ? 0.9 : 1.3) * (NS == 6 ? 0.8 : 1.0);
     const int smax = steps / 4 > 0 ? steps / 4 : 1;
-    for (int sp = 1; sp <= smax && sp <= 256; ++sp) {
+    // split cap 128 (256 until round 6): fewer partial slabs to write and reduce; ResNet-18 bf16
+    // -9.5 us twice, ResNet-50 bf16 -24 us, 64 +30 us (profiles/r6_wgrad3_split_cap_ab.jsonl)
+    for (int sp = 1; sp <= smax && sp <= 128; ++sp) {
       const int sps = (steps + sp - 1) / sp;
       const int spl = (steps + sps - 1) / sps;
       const long wgs = tiles * spl;
